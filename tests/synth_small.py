@@ -1,0 +1,126 @@
+"""Small seeded anchor-pair generator for CPU-side parity tests.
+
+Follows SURVEY.md §8(d)'s recipe at toy scale: junctions planted at GT..AG /
+CT..AC sites half of the time, uniform otherwise; backsplice reads are
+``G[end-kA:end] + G[start:start+L-kA]``, linear reads ``G[d-kA:d] + G[a:a+L-kA]``;
+per-base substitutions; optional read ends clipped (emulating bwa local
+alignment), N bases and lower-case bytes in reads; some pairs placed at the
+chromosome ends so the genome windows get N-padded (find_circ.py:194-211).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List
+
+import numpy as np
+
+from bwa_emul import read_fasta
+
+
+@dataclass
+class SmallSpan:
+    chrom: str
+    chrom_idx: int
+    a_pos: int
+    a_aend: int
+    b_pos: int
+    b_aend: int
+    read_part: bytes
+    primary_reverse: bool
+
+    @property
+    def is_backsplice(self):
+        return self.b_pos - self.a_aend < 0
+
+
+def _find_site(g: str, p: int, motif: str, step: int, limit: int = 400):
+    for k in range(limit):
+        q = p + k * step
+        if 0 <= q and q + 2 <= len(g) and g[q:q + 2].upper() == motif:
+            return q
+    return None
+
+
+def make_spans(genome: Dict[str, str], n: int, seed: int, L=(60, 160), asize=15, mut=0.01,
+               p_planted=0.5, p_backsplice=0.6, p_edge=0.05, p_readN=0.05, p_lower=0.05,
+               p_clip=0.2, p_short=0.02) -> List[SmallSpan]:
+    rng = np.random.default_rng(seed)
+    names = list(genome)
+    out: List[SmallSpan] = []
+    while len(out) < n:
+        ci = int(rng.integers(len(names)))
+        chrom = names[ci]
+        g = genome[chrom]
+        G = len(g)
+        Lr = int(rng.integers(L[0], L[1] + 1))
+        if rng.random() < p_short:
+            Lr = int(rng.integers(2 * asize - 6, 2 * asize + 3))
+        kA = int(rng.integers(asize, max(asize + 1, Lr - asize + 1)))
+        kB = Lr - kA
+        bs = rng.random() < p_backsplice
+        planted = rng.random() < p_planted
+        minus = rng.random() < 0.3
+        if bs:
+            # exon [start, end): A = G[end-kA:end], B = G[start:start+kB]
+            span = int(rng.integers(max(kA, kB) + 1, max(max(kA, kB) + 2, min(G, 1500))))
+            end = int(rng.integers(kA, G + 1))
+            if planted:
+                q = _find_site(g, end, "CT" if minus else "GT", 1)
+                if q is not None:
+                    end = q
+            start = end - span
+            if planted and start >= 2:
+                q = _find_site(g, start - 2, "AC" if minus else "AG", -1)
+                if q is not None:
+                    start = q + 2
+            if rng.random() < p_edge:   # touch a chromosome end -> N padded windows
+                if rng.random() < 0.5:
+                    start = int(rng.integers(0, 6))
+                else:
+                    end = G - int(rng.integers(0, 6))
+                    start = min(start, end - max(kA, kB) - 1)
+            if start < 0 or end - kA < 0 or start + kB > G or end > G or start >= end:
+                continue
+            read = g[end - kA:end] + g[start:start + kB]
+            a_pos, a_aend, b_pos, b_aend = end - kA, end, start, start + kB
+        else:
+            # intron [d, a): A = G[d-kA:d], B = G[a:a+kB]
+            d = int(rng.integers(kA, G))
+            if planted:
+                q = _find_site(g, d, "CT" if minus else "GT", 1)
+                if q is not None:
+                    d = q
+            a = d + int(rng.integers(30, 1200))
+            if planted:
+                q = _find_site(g, a - 2, "AC" if minus else "AG", 1)
+                if q is not None:
+                    a = q + 2
+            if d - kA < 0 or a + kB > G:
+                continue
+            read = g[d - kA:d] + g[a:a + kB]
+            a_pos, a_aend, b_pos, b_aend = d - kA, d, a, a + kB
+        r = np.frombuffer(read.upper().encode(), dtype=np.uint8).copy()
+        # substitutions
+        m = rng.random(len(r)) < mut
+        if m.any():
+            alph = np.frombuffer(b"ACGT", dtype=np.uint8)
+            r[m] = alph[rng.integers(0, 4, m.sum())]
+        if rng.random() < p_readN:
+            k = int(rng.integers(1, 4))
+            r[rng.integers(0, len(r), k)] = ord('N')
+        if rng.random() < p_lower:
+            lo = rng.random(len(r)) < 0.3
+            r[lo] = r[lo] + 32
+        c0 = c1 = 0
+        if rng.random() < p_clip:
+            c0, c1 = int(rng.integers(0, 4)), int(rng.integers(0, 4))
+            if kA - c0 < 2 or kB - c1 < 2:
+                c0 = c1 = 0
+        read_b = bytes(r[c0:len(r) - c1])
+        out.append(SmallSpan(chrom, ci, a_pos + c0, a_aend, b_pos, b_aend - c1, read_b,
+                             bool(rng.random() < 0.5)))
+    return out
+
+
+def load_genome(path: str) -> Dict[str, str]:
+    return read_fasta(path)
