@@ -1,0 +1,16 @@
+"""find_circ2_amd -- MI355X-native breakpoint search for find_circ2.
+
+One hot path of find_circ2 (find_circ.py 1.99), ``JunctionSpan.find_breakpoints``
+plus its genome window fetch, as hand-written HIP kernels for gfx950 behind a
+C ABI (include/fc2_bp.h, libfc2.so).  See DESIGN.md.
+"""
+from . import _native
+from .genome import Genome, sq_table, synthetic_n_intervals
+from .hotpath import (BreakpointEngine, BreakpointError, JunctionSpan, Options, PairBatch, ScanOutput, Splice,
+                      SynthConfig, decode_splices, first_tie_arrays, gtag_str, scan)
+
+__version__ = "0.1.0"
+
+__all__ = ["Genome", "Options", "PairBatch", "ScanOutput", "Splice", "SynthConfig", "JunctionSpan",
+           "BreakpointEngine", "BreakpointError", "scan", "decode_splices", "first_tie_arrays", "gtag_str",
+           "sq_table", "synthetic_n_intervals"]

@@ -1,0 +1,163 @@
+"""ctypes binding of libfc2.so (C ABI in include/fc2_bp.h).
+
+The library is built in-tree (``find_circ2_amd/libfc2.so``) by
+``__graft_entry__.build()`` / ``make -C find_circ2_amd/csrc``.  There is no
+fallback: if the library is missing, importing a GPU entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libfc2.so")
+
+FC2_OK = 0
+FC2_E_PARAM = -1
+FC2_E_HIP = -2
+FC2_E_FORMAT = -3
+FC2_E_RANGE = -4
+FC2_E_IO = -5
+FC2_E_KEY = -6
+
+PAIR_BACKSPLICE = 0x01
+PAIR_PRIMARY_REV = 0x02
+PAIR_READ_N = 0x04
+PAIR_BYTEPATH = 0x08
+PAIR_SKIP = 0x10
+
+RES_MINUS = 0x0001
+RES_GTAG_SHIFT = 1
+RES_GTAG_MASK = 0x1FFE
+RES_ERR_KEY = 0x2000
+RES_ERR_WIN = 0x4000
+RES_DONE = 0x8000
+
+PAIR_DTYPE = np.dtype([("a_pos", "<i4"), ("b_aend", "<i4"), ("chrom", "<u4"), ("read_len", "<u2"),
+                       ("flags", "u1"), ("_pad", "u1")])
+RESULT_DTYPE = np.dtype([("best_x", "<i2"), ("dist", "u1"), ("ov", "u1"), ("n_ties", "<u2"), ("info", "<u2")])
+assert PAIR_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 8
+
+
+class Fc2Error(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__("libfc2 error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Params(ctypes.Structure):
+    """``fc2_params``: the options find_breakpoints reads (find_circ.py:393-404)."""
+    _fields_ = [("asize", ctypes.c_int32), ("margin", ctypes.c_int32), ("maxdist", ctypes.c_int32),
+                ("noncanonical", ctypes.c_uint8), ("strandpref", ctypes.c_uint8),
+                ("allhits", ctypes.c_uint8), ("_pad", ctypes.c_uint8)]
+
+
+class GenomeView(ctypes.Structure):
+    _fields_ = [("units", ctypes.c_void_p), ("nplane", ctypes.c_void_p), ("ncoarse", ctypes.c_void_p),
+                ("chrom_start", ctypes.c_void_p), ("chrom_size", ctypes.c_void_p),
+                ("n_units", ctypes.c_uint64), ("n_chrom", ctypes.c_uint32), ("dummy", ctypes.c_uint32)]
+
+
+class BatchView(ctypes.Structure):
+    _fields_ = [("pairs", ctypes.c_void_p), ("read_words", ctypes.c_void_p), ("read_nwords", ctypes.c_void_p),
+                ("n", ctypes.c_uint64), ("stride", ctypes.c_uint64), ("rw", ctypes.c_uint32),
+                ("nw", ctypes.c_uint32), ("max_l", ctypes.c_int32), ("_pad", ctypes.c_uint32)]
+
+
+class BytesView(ctypes.Structure):
+    _fields_ = [("index", ctypes.c_void_p), ("pairs", ctypes.c_void_p), ("arena", ctypes.c_void_p),
+                ("off", ctypes.c_void_p), ("m", ctypes.c_uint64)]
+
+
+class SynthCfg(ctypes.Structure):
+    _fields_ = [("seed", ctypes.c_uint64), ("len_min", ctypes.c_int32), ("len_max", ctypes.c_int32),
+                ("p_planted", ctypes.c_float), ("p_minus_site", ctypes.c_float),
+                ("p_backsplice", ctypes.c_float), ("mut_rate", ctypes.c_float), ("n_rate", ctypes.c_float),
+                ("p_clip", ctypes.c_float), ("span_min", ctypes.c_int32), ("span_max", ctypes.c_int32)]
+
+
+# every symbol include/fc2_bp.h declares (checked by tests/test_abi.py)
+EXPORTED = [
+    "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_max_fast_l", "fc2_batch_geometry",
+    "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch",
+    "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
+    "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
+    "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill",
+    "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_synth_pairs_launch",
+]
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    srcdir = os.path.join(_HERE, "csrc")
+    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_host.cpp", "fc2_common.h", "Makefile")]
+    srcs.append(os.path.join(os.path.dirname(_HERE), "include", "fc2_bp.h"))
+    newest = max(os.path.getmtime(s) for s in srcs)
+    if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
+        subprocess.check_call(["make", "-s", "-C", srcdir])
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libfc2.so is not built (%s); run __graft_entry__.build() -- there is no CPU fallback"
+                          % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i32, i64 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int32, ctypes.c_int64
+    P = ctypes.POINTER
+    sig = {
+        "fc2_abi_version": (ctypes.c_int, []),
+        "fc2_last_error": (ctypes.c_char_p, []),
+        "fc2_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
+        "fc2_max_fast_l": (ctypes.c_int, []),
+        "fc2_batch_geometry": (ctypes.c_int, [P(Params), i32, P(u32), P(u32), P(u32)]),
+        "fc2_bp_scan_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp, u32, vp]),
+        "fc2_bp_scan_bytes_launch": (ctypes.c_int, [P(Params), P(BytesView), vp, vp, u32, u64, vp]),
+        "fc2_fasta_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(vp)]),
+        "fc2_fasta_close": (None, [vp]),
+        "fc2_fasta_n_chrom": (ctypes.c_int, [vp]),
+        "fc2_fasta_chrom": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(i64), P(i64), P(i64),
+                                           P(i64), P(ctypes.c_int)]),
+        "fc2_fasta_find": (ctypes.c_int, [vp, ctypes.c_char_p]),
+        "fc2_fasta_get_upper": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, vp, i64, P(i64)]),
+        "fc2_fasta_layout": (ctypes.c_int, [vp, P(u64), P(u64), vp]),
+        "fc2_fasta_pack": (ctypes.c_int, [vp, vp, vp, vp, P(u64), ctypes.c_int]),
+        "fc2_pack_pairs": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, vp, u32, vp, u32, u64, P(u64),
+                                          ctypes.c_int]),
+        "fc2_bytepath_size": (ctypes.c_int, [P(Params), u64, vp, P(u64), P(u64)]),
+        "fc2_bytepath_fill": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, vp, vp, vp, vp]),
+        "fc2_synth_genome_launch": (ctypes.c_int, [u64, vp, vp, vp, u64, vp, vp, u32, vp]),
+        "fc2_coarse_launch": (ctypes.c_int, [vp, vp, u64, vp]),
+        "fc2_synth_pairs_launch": (ctypes.c_int, [P(Params), P(SynthCfg), P(GenomeView), vp, u64, vp, vp, u32,
+                                                  vp, u32, u64, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.fc2_abi_version() != 1:
+        raise ImportError("libfc2.so ABI mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int) -> None:
+    if rc != FC2_OK:
+        msg = lib().fc2_last_error()
+        raise Fc2Error(rc, msg.decode("utf-8", "replace") if msg else "")
+
+
+def ptr(a) -> int:
+    """Address of a numpy array or torch tensor (None -> NULL)."""
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()

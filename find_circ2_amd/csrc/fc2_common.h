@@ -1,0 +1,23 @@
+// Internal helpers shared by the HIP and host translation units of libfc2.so.
+#pragma once
+#include <stdint.h>
+#include <string>
+
+#include "../../include/fc2_bp.h"
+
+namespace fc2 {
+
+// Thread-local message behind fc2_last_error().
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+
+// Largest internal length l handled by the register kernel (NW = 8 words of
+// 64 positions hold l + 2 <= 512 window bases).
+constexpr int kMaxFastL = 510;
+
+// Validate the options the hot path reads; returns FC2_OK or FC2_E_PARAM.
+int validate_params(const fc2_params *p);
+
+inline int eff_anchor(const fc2_params *p) { return p->asize - p->margin; }  // find_circ.py:882
+
+}  // namespace fc2

@@ -1,0 +1,720 @@
+// fc2_host.cpp -- host side of libfc2.so: FASTA access with the reference's
+// indexed_fasta semantics, genome/pair packing into the device layout, and the
+// byte-exact arena for rare pairs.  No GPU calls here.
+//
+// Reference: find_circ.py:103-215 (indexed_fasta), 821-852 (JunctionSpan),
+// 854-974 (find_breakpoints).
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <functional>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "fc2_common.h"
+
+namespace fc2 {
+
+static thread_local std::string g_err;
+
+void set_error(const std::string &msg) { g_err = msg; }
+int fail(int code, const std::string &msg) {
+    g_err = msg;
+    return code;
+}
+
+int validate_params(const fc2_params *p) {
+    if (!p) return fail(FC2_E_PARAM, "null fc2_params");
+    if (p->asize - p->margin <= 0)
+        return fail(FC2_E_PARAM,
+                    "asize - margin <= 0: the reference's read[eff_a:-eff_a] (find_circ.py:895) "
+                    "is empty/garbled and find_breakpoints fails; unsupported");
+    if (p->margin > 255) return fail(FC2_E_RANGE, "margin > 255 is not supported (ov is stored in 8 bits)");
+    return FC2_OK;
+}
+
+static int n_workers(int n_threads) {
+    if (n_threads > 0) return n_threads;
+    unsigned h = std::thread::hardware_concurrency();
+    const char *env = getenv("OMP_NUM_THREADS");
+    if (env && atoi(env) > 0) h = (unsigned)atoi(env);
+    if (h == 0) h = 1;
+    if (h > 64) h = 64;
+    return (int)h;
+}
+
+// Run body(begin, end) over [0, n) split into contiguous chunks on `threads` threads.
+static void parallel_for(uint64_t n, int threads, const std::function<void(uint64_t, uint64_t)> &body) {
+    if (n == 0) return;
+    if (threads <= 1 || n < 4096) {
+        body(0, n);
+        return;
+    }
+    uint64_t t = (uint64_t)threads;
+    if (t > n) t = n;
+    std::vector<std::thread> pool;
+    pool.reserve(t);
+    for (uint64_t k = 0; k < t; ++k) {
+        const uint64_t b = n * k / t, e = n * (k + 1) / t;
+        pool.emplace_back([&body, b, e] { body(b, e); });
+    }
+    for (auto &th : pool) th.join();
+}
+
+static inline uint8_t upc(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
+
+// base class of an (uppercased) byte: 0..3 = ACGT, 4 = N, 5 = other
+static inline int bclass(uint8_t c) {
+    switch (upc(c)) {
+        case 'A': return 0;
+        case 'C': return 1;
+        case 'G': return 2;
+        case 'T': return 3;
+        case 'N': return 4;
+        default: return 5;
+    }
+}
+
+static inline bool py_isspace(uint8_t c) {
+    return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
+}
+
+}  // namespace fc2
+
+using namespace fc2;
+
+struct fc2_chrom_rec {
+    std::string name;
+    int64_t ofs = 0, ldata = 0, skip = 0, size = 0;
+    std::string skipchar;
+    int nfields = 4;   // the reference's chrom_stats list length (5 when complete)
+    int regular = -1;  // -1 unknown until packed
+    uint64_t gstart = 0;
+};
+
+struct fc2_fasta {
+    std::string path;
+    int fd = -1;
+    const uint8_t *data = nullptr;
+    size_t n = 0;
+    std::vector<fc2_chrom_rec> chroms;
+    std::unordered_map<std::string, int> by_name;
+    std::vector<uint64_t> exotic;  // sorted global positions of non-ACGTN bases
+    bool packed = false;
+};
+
+// ---------------------------------------------------------------------------
+// index (find_circ.py:120-155) and .byo_index (157-187)
+// ---------------------------------------------------------------------------
+static int build_index(fc2_fasta *f) {
+    std::unordered_map<std::string, int> &idx = f->by_name;
+    std::vector<fc2_chrom_rec> &cs = f->chroms;
+    int64_t ofs = 0, chrom_ofs = 0, size = 0;
+    std::string chrom = "undef";
+    const uint8_t *d = f->data;
+    const size_t n = f->n;
+    size_t i = 0;
+    while (i < n) {
+        const uint8_t *nl = (const uint8_t *)memchr(d + i, '\n', n - i);
+        const size_t j = nl ? (size_t)(nl - d) + 1 : n;
+        const uint8_t *line = d + i;
+        const int64_t len = (int64_t)(j - i);
+        ofs += len;
+        if (line[0] == '>') {
+            if (size) {  // self.chrom_stats[chrom].append(size)
+                auto it = idx.find(chrom);
+                if (it == idx.end())
+                    return fail(FC2_E_FORMAT, "FASTA header without sequence before '" + chrom +
+                                                  "': reference indexed_fasta.index raises KeyError");
+                cs[it->second].size = size;
+                cs[it->second].nfields += 1;
+            }
+            int64_t s = 1;
+            while (s < len && py_isspace(line[s])) ++s;
+            int64_t e = s;
+            while (e < len && !py_isspace(line[e])) ++e;
+            if (e == s) return fail(FC2_E_FORMAT, "empty FASTA header: reference raises IndexError");
+            chrom.assign((const char *)line + s, (size_t)(e - s));
+            chrom_ofs = ofs;
+        } else {
+            int64_t a = 0, b = len;
+            while (a < b && py_isspace(line[a])) ++a;
+            while (b > a && py_isspace(line[b - 1])) --b;
+            const int64_t stripped = b - a;
+            if (idx.find(chrom) == idx.end()) {
+                size = 0;
+                fc2_chrom_rec r;
+                r.name = chrom;
+                r.ofs = chrom_ofs;
+                r.ldata = stripped;
+                r.skip = len - stripped;
+                r.skipchar.assign((const char *)line + stripped, (size_t)(len - stripped));
+                idx[chrom] = (int)cs.size();
+                cs.push_back(r);
+            }
+            size += stripped;
+        }
+        i = j;
+    }
+    if (size) {
+        auto it = idx.find(chrom);
+        if (it != idx.end()) {
+            cs[it->second].size = size;
+            cs[it->second].nfields += 1;
+        }
+    }
+    for (auto &c : cs)
+        if (c.nfields != 5)
+            return fail(FC2_E_FORMAT, "chromosome '" + c.name +
+                                          "' has an inconsistent index entry (empty or duplicated sequence); "
+                                          "the reference's store_index/get_data fail on it");
+    return FC2_OK;
+}
+
+static std::string py2_repr(const std::string &s) {
+    std::string o = "'";
+    for (unsigned char c : s) {
+        if (c == '\n') o += "\\n";
+        else if (c == '\r') o += "\\r";
+        else if (c == '\t') o += "\\t";
+        else if (c == '\'') o += "\\'";
+        else if (c == '\\') o += "\\\\";
+        else if (c >= 32 && c < 127) o += (char)c;
+        else {
+            char buf[8];
+            snprintf(buf, sizeof buf, "\\x%02x", c);
+            o += buf;
+        }
+    }
+    return o + "'";
+}
+
+static bool py2_unescape(const std::string &in, std::string &out) {  // 'string_escape' for repr output
+    out.clear();
+    for (size_t i = 0; i < in.size(); ++i) {
+        char c = in[i];
+        if (c != '\\') { out += c; continue; }
+        if (++i >= in.size()) return false;
+        switch (in[i]) {
+            case 'n': out += '\n'; break;
+            case 'r': out += '\r'; break;
+            case 't': out += '\t'; break;
+            case '\\': out += '\\'; break;
+            case '\'': out += '\''; break;
+            case '"': out += '"'; break;
+            case 'x': {
+                if (i + 2 >= in.size()) return false;
+                out += (char)strtol(in.substr(i + 1, 2).c_str(), nullptr, 16);
+                i += 2;
+                break;
+            }
+            default: out += '\\'; out += in[i];
+        }
+    }
+    return true;
+}
+
+static int load_index_file(fc2_fasta *f, const std::string &ipath) {
+    FILE *fp = fopen(ipath.c_str(), "r");
+    if (!fp) return fail(FC2_E_IO, "cannot read " + ipath);
+    char *line = nullptr;
+    size_t cap = 0;
+    ssize_t len;
+    int rc = FC2_OK;
+    while ((len = getline(&line, &cap, fp)) > 0) {
+        std::string s(line, (size_t)len);
+        while (!s.empty() && py_isspace((uint8_t)s.back())) s.pop_back();  // rstrip()
+        std::vector<std::string> parts;
+        size_t st = 0;
+        for (;;) {
+            size_t t = s.find('\t', st);
+            parts.push_back(s.substr(st, t == std::string::npos ? std::string::npos : t - st));
+            if (t == std::string::npos) break;
+            st = t + 1;
+        }
+        if (parts.size() != 6 || parts[4].size() < 2) { rc = fail(FC2_E_FORMAT, "malformed .byo_index line: " + s); break; }
+        fc2_chrom_rec r;
+        r.name = parts[0];
+        r.ofs = atoll(parts[1].c_str());
+        r.ldata = atoll(parts[2].c_str());
+        r.skip = atoll(parts[3].c_str());
+        if (!py2_unescape(parts[4].substr(1, parts[4].size() - 2), r.skipchar)) { rc = fail(FC2_E_FORMAT, "bad skipchar in .byo_index"); break; }
+        r.size = atoll(parts[5].c_str());
+        r.nfields = 5;
+        f->by_name[r.name] = (int)f->chroms.size();
+        f->chroms.push_back(r);
+    }
+    free(line);
+    fclose(fp);
+    return rc;
+}
+
+static void store_index_file(const fc2_fasta *f, const std::string &ipath) {
+    // find_circ.py:157-179: temp file in the same directory, fsync, chmod 0444, rename
+    std::vector<const fc2_chrom_rec *> v;
+    for (auto &c : f->chroms) v.push_back(&c);
+    std::sort(v.begin(), v.end(), [](const fc2_chrom_rec *a, const fc2_chrom_rec *b) { return a->name < b->name; });
+    std::string dir = ipath.substr(0, ipath.find_last_of('/') == std::string::npos ? 0 : ipath.find_last_of('/') + 1);
+    std::string tmpl = (dir.empty() ? std::string("./") : dir) + "tmpXXXXXX";
+    std::vector<char> buf(tmpl.begin(), tmpl.end());
+    buf.push_back(0);
+    int fd = mkstemp(buf.data());
+    if (fd < 0) return;  // like the reference, a failure here is not fatal for reading
+    std::string body;
+    for (auto *c : v) {
+        char num[128];
+        body += c->name;
+        snprintf(num, sizeof num, "\t%lld\t%lld\t%lld\t", (long long)c->ofs, (long long)c->ldata, (long long)c->skip);
+        body += num;
+        body += py2_repr(c->skipchar);
+        snprintf(num, sizeof num, "\t%lld\n", (long long)c->size);
+        body += num;
+    }
+    ssize_t w = write(fd, body.data(), body.size());
+    (void)w;
+    fsync(fd);
+    close(fd);
+    chmod(buf.data(), S_IRUSR | S_IRGRP | S_IROTH);
+    if (rename(buf.data(), ipath.c_str()) != 0) unlink(buf.data());
+}
+
+// ---------------------------------------------------------------------------
+// get_data(...).upper()  (find_circ.py:189-215, 901-902), Python slice semantics
+// ---------------------------------------------------------------------------
+static inline int64_t floordiv(int64_t a, int64_t b) {
+    int64_t q = a / b;
+    if ((a % b != 0) && ((a < 0) != (b < 0))) --q;
+    return q;
+}
+static inline int64_t pyclip(int64_t i, int64_t n) {
+    if (i < 0) { i += n; if (i < 0) i = 0; }
+    return i > n ? n : i;
+}
+
+static int get_upper_impl(const fc2_fasta *f, int ci, int64_t start, int64_t end, std::string &out) {
+    out.clear();
+    if (!f) {  // GenomeAccessor.get_dummy (find_circ.py:370-371)
+        if (end > start) out.assign((size_t)(end - start), 'N');
+        return FC2_OK;
+    }
+    if (ci < 0 || ci >= (int)f->chroms.size()) return fail(FC2_E_KEY, "unknown chromosome index");
+    const fc2_chrom_rec &c = f->chroms[ci];
+    if (c.ldata == 0) return fail(FC2_E_FORMAT, "chromosome '" + c.name + "' has ldata 0: reference raises ZeroDivisionError");
+    int64_t pad_start = 0, pad_end = 0;
+    if (start < 0) { pad_start = -start; start = 0; }
+    if (end > c.size) { pad_end = end - c.size; end = c.size; }
+    const int64_t os = pyclip(floordiv(start, c.ldata) * c.skip + start + c.ofs, (int64_t)f->n);
+    const int64_t oe = pyclip(floordiv(end, c.ldata) * c.skip + end + c.ofs, (int64_t)f->n);
+    out.reserve((size_t)(pad_start + pad_end + (oe > os ? oe - os : 0)));
+    out.append((size_t)pad_start, 'N');
+    const size_t sl = c.skipchar.size();
+    for (int64_t p = os; p < oe;) {
+        if (sl && p + (int64_t)sl <= oe && !memcmp(f->data + p, c.skipchar.data(), sl)) { p += (int64_t)sl; continue; }
+        out.push_back((char)upc(f->data[p]));
+        ++p;
+    }
+    out.append((size_t)pad_end, 'N');
+    return FC2_OK;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI: library info
+// ---------------------------------------------------------------------------
+extern "C" int fc2_abi_version(void) { return FC2_ABI_VERSION; }
+extern "C" const char *fc2_last_error(void) { return g_err.c_str(); }
+extern "C" int fc2_max_fast_l(void) { return kMaxFastL; }
+
+extern "C" int fc2_batch_geometry(const fc2_params *p, int32_t max_read_len, uint32_t *rw, uint32_t *nw, uint32_t *tw) {
+    int rc = validate_params(p);
+    if (rc) return rc;
+    int lmax = max_read_len - 2 * eff_anchor(p);
+    if (lmax < 0) lmax = 0;
+    const int lfast = lmax > kMaxFastL ? kMaxFastL : lmax;
+    if (rw) *rw = (uint32_t)std::max(1, (2 * lfast + 63) / 64);
+    if (nw) *nw = (uint32_t)std::max(1, (lfast + 63) / 64);
+    if (tw) *tw = (uint32_t)(2 * std::max(1, (lmax + 1 + 63) / 64));
+    return FC2_OK;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI: FASTA
+// ---------------------------------------------------------------------------
+extern "C" int fc2_fasta_open(const char *path, int write_index, fc2_fasta **out) {
+    if (!path || !out) return fail(FC2_E_PARAM, "fc2_fasta_open: null argument");
+    *out = nullptr;
+    int fd = open(path, O_RDONLY);
+    if (fd < 0) return fail(FC2_E_IO, std::string("cannot open FASTA '") + path + "': " + strerror(errno));
+    struct stat st;
+    if (fstat(fd, &st) != 0) { close(fd); return fail(FC2_E_IO, "fstat failed"); }
+    fc2_fasta *f = new fc2_fasta();
+    f->path = path;
+    f->fd = fd;
+    f->n = (size_t)st.st_size;
+    if (f->n) {
+        void *m = mmap(nullptr, f->n, PROT_READ, MAP_SHARED, fd, 0);
+        if (m == MAP_FAILED) { close(fd); delete f; return fail(FC2_E_IO, "mmap failed"); }
+        f->data = (const uint8_t *)m;
+        madvise(m, f->n, MADV_WILLNEED);
+    }
+    const std::string ipath = std::string(path) + ".byo_index";
+    int rc;
+    if (access(ipath.c_str(), R_OK) == 0) {       // find_circ.py:110-112
+        rc = load_index_file(f, ipath);
+    } else {
+        rc = build_index(f);                       // find_circ.py:114-115
+        if (rc == FC2_OK && write_index) store_index_file(f, ipath);
+    }
+    if (rc != FC2_OK) { fc2_fasta_close(f); return rc; }
+    *out = f;
+    return FC2_OK;
+}
+
+extern "C" void fc2_fasta_close(fc2_fasta *f) {
+    if (!f) return;
+    if (f->data) munmap((void *)f->data, f->n);
+    if (f->fd >= 0) close(f->fd);
+    delete f;
+}
+
+extern "C" int fc2_fasta_n_chrom(const fc2_fasta *f) { return f ? (int)f->chroms.size() : 0; }
+
+extern "C" int fc2_fasta_chrom(const fc2_fasta *f, int i, const char **name, int64_t *size, int64_t *ofs, int64_t *ldata,
+                               int64_t *skip, int *regular) {
+    if (!f || i < 0 || i >= (int)f->chroms.size()) return fail(FC2_E_PARAM, "fc2_fasta_chrom: bad index");
+    const fc2_chrom_rec &c = f->chroms[i];
+    if (name) *name = c.name.c_str();
+    if (size) *size = c.size;
+    if (ofs) *ofs = c.ofs;
+    if (ldata) *ldata = c.ldata;
+    if (skip) *skip = c.skip;
+    if (regular) *regular = c.regular;
+    return FC2_OK;
+}
+
+extern "C" int fc2_fasta_find(const fc2_fasta *f, const char *name) {
+    if (!f || !name) return -1;
+    auto it = f->by_name.find(name);
+    return it == f->by_name.end() ? -1 : it->second;
+}
+
+extern "C" int fc2_fasta_get_upper(const fc2_fasta *f, int chrom, int64_t start, int64_t end, uint8_t *out, int64_t cap,
+                                   int64_t *len) {
+    std::string s;
+    int rc = get_upper_impl(f, chrom, start, end, s);
+    if (rc) return rc;
+    if (len) *len = (int64_t)s.size();
+    if (out && cap > 0) memcpy(out, s.data(), (size_t)std::min<int64_t>(cap, (int64_t)s.size()));
+    return FC2_OK;
+}
+
+static void compute_layout(fc2_fasta *f, uint64_t *n_units) {
+    uint64_t g = 0;
+    for (auto &c : f->chroms) {
+        c.gstart = g;
+        g += ((uint64_t)std::max<int64_t>(c.size, 0) + 63) & ~63ull;
+    }
+    *n_units = std::max<uint64_t>(1, g / 64);
+}
+
+extern "C" int fc2_fasta_layout(const fc2_fasta *cf, uint64_t *n_units, uint64_t *n_coarse_words, uint64_t *chrom_start) {
+    if (!cf) return fail(FC2_E_PARAM, "fc2_fasta_layout: null");
+    fc2_fasta *f = const_cast<fc2_fasta *>(cf);
+    uint64_t nu;
+    compute_layout(f, &nu);
+    if (n_units) *n_units = nu;
+    if (n_coarse_words) *n_coarse_words = (((nu + 15) >> 4) + 31) >> 5;
+    if (chrom_start)
+        for (size_t i = 0; i < f->chroms.size(); ++i) chrom_start[i] = f->chroms[i].gstart;
+    return FC2_OK;
+}
+
+// Is the chromosome laid out exactly as the index arithmetic assumes?  Then
+// get_data's slice-and-strip yields base p at file offset ofs + (p//ldata)*skip + p.
+static bool chrom_regular(const fc2_fasta *f, const fc2_chrom_rec &c) {
+    if (c.size <= 0) return true;
+    if (c.ldata <= 0) return false;
+    if ((int64_t)c.skipchar.size() != c.skip) return false;
+    for (char ch : c.skipchar)
+        if (!py_isspace((uint8_t)ch)) return false;
+    const int64_t nfull = c.size / c.ldata, rem = c.size % c.ldata;
+    const int64_t stride = c.ldata + c.skip;
+    for (int64_t k = 0; k < nfull; ++k) {
+        const int64_t st = c.ofs + k * stride;
+        if (st + c.ldata > (int64_t)f->n) return false;
+        if (memchr(f->data + st, '\n', (size_t)c.ldata)) return false;
+        const int64_t te = st + c.ldata;
+        const bool last = (k == nfull - 1) && rem == 0;
+        if (te + c.skip <= (int64_t)f->n) {
+            if (memcmp(f->data + te, c.skipchar.data(), (size_t)c.skip) != 0) {
+                if (!(last && te == (int64_t)f->n)) return false;
+            }
+        } else if (!(last && te == (int64_t)f->n)) {
+            return false;
+        }
+    }
+    if (rem) {
+        const int64_t st = c.ofs + nfull * stride;
+        if (st + rem > (int64_t)f->n) return false;
+        if (memchr(f->data + st, '\n', (size_t)rem)) return false;
+    }
+    return true;
+}
+
+extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,
+                              uint64_t *n_exotic, int n_threads) {
+    if (!cf || !units || !nplane || !ncoarse) return fail(FC2_E_PARAM, "fc2_fasta_pack: null argument");
+    fc2_fasta *f = const_cast<fc2_fasta *>(cf);
+    uint64_t nu;
+    compute_layout(f, &nu);
+    const int T = n_workers(n_threads);
+    // regularity per chromosome
+    {
+        std::atomic<size_t> next{0};
+        std::vector<std::thread> pool;
+        for (int t = 0; t < std::min<int>(T, (int)f->chroms.size()); ++t)
+            pool.emplace_back([&] {
+                for (size_t k; (k = next.fetch_add(1)) < f->chroms.size();)
+                    f->chroms[k].regular = chrom_regular(f, f->chroms[k]) ? 1 : 0;
+            });
+        for (auto &th : pool) th.join();
+    }
+    // work items: (chrom, unit range) of <= 2^14 units
+    struct Item { int c; uint64_t u0, u1; };
+    std::vector<Item> items;
+    for (int c = 0; c < (int)f->chroms.size(); ++c) {
+        const fc2_chrom_rec &r = f->chroms[c];
+        const uint64_t cu = ((uint64_t)std::max<int64_t>(r.size, 0) + 63) / 64;
+        for (uint64_t u = 0; u < cu; u += 16384) items.push_back({c, u, std::min(cu, u + 16384)});
+    }
+    // padding units (between chromosomes / tail) stay all-N
+    parallel_for(nu, T, [&](uint64_t b, uint64_t e) {
+        for (uint64_t u = b; u < e; ++u) { units[2 * u] = 0; units[2 * u + 1] = 0; nplane[u] = ~0ull; }
+    });
+    std::vector<std::vector<uint64_t>> exo(items.size());
+    std::atomic<size_t> next{0};
+    std::vector<std::thread> pool;
+    for (int t = 0; t < std::max(1, std::min<int>(T, (int)items.size())); ++t)
+        pool.emplace_back([&] {
+            for (size_t k; (k = next.fetch_add(1)) < items.size();) {
+                const Item it = items[k];
+                const fc2_chrom_rec &r = f->chroms[it.c];
+                const uint64_t gu0 = r.gstart / 64;
+                if (r.regular != 1) continue;  // stays N; pairs on it take the byte path
+                for (uint64_t u = it.u0; u < it.u1; ++u) {
+                    uint64_t lo = 0, hi = 0, nn = 0;
+                    const int64_t p0 = (int64_t)u * 64;
+                    const int64_t p1 = std::min<int64_t>(p0 + 64, r.size);
+                    int64_t line = p0 / r.ldata, col = p0 % r.ldata;
+                    int64_t off = r.ofs + line * (r.ldata + r.skip) + col;
+                    for (int64_t p = p0; p < p1; ++p) {
+                        const int b = (int)(p - p0);
+                        const int cl = bclass(f->data[off]);
+                        if (cl < 4) {
+                            lo |= (uint64_t)(cl & 1) << b;
+                            hi |= (uint64_t)((cl >> 1) & 1) << b;
+                        } else {
+                            nn |= 1ull << b;
+                            if (cl == 5) exo[k].push_back(r.gstart + (uint64_t)p);
+                        }
+                        ++off;
+                        if (++col == r.ldata) { col = 0; off += r.skip; }
+                    }
+                    for (int b = (int)(p1 - p0); b < 64; ++b) nn |= 1ull << b;
+                    units[2 * (gu0 + u)] = lo;
+                    units[2 * (gu0 + u) + 1] = hi;
+                    nplane[gu0 + u] = nn;
+                }
+            }
+        });
+    for (auto &th : pool) th.join();
+    f->exotic.clear();
+    for (auto &v : exo) f->exotic.insert(f->exotic.end(), v.begin(), v.end());
+    // irregular chromosomes: every base is "exotic" for routing purposes (handled by chrom flag)
+    const uint64_t n_blocks = (nu + 15) >> 4, n_words = (n_blocks + 31) >> 5;
+    parallel_for(n_words, T, [&](uint64_t b, uint64_t e) {
+        for (uint64_t w = b; w < e; ++w) {
+            uint32_t bits = 0;
+            for (int k = 0; k < 32; ++k) {
+                const uint64_t blk = w * 32 + k;
+                if (blk >= n_blocks) break;
+                uint64_t acc = 0;
+                for (int j = 0; j < 16; ++j) {
+                    const uint64_t u = blk * 16 + j;
+                    if (u < nu) acc |= nplane[u];
+                }
+                if (acc) bits |= 1u << k;
+            }
+            ncoarse[w] = bits;
+        }
+    });
+    if (n_exotic) *n_exotic = f->exotic.size();
+    f->packed = true;
+    return FC2_OK;
+}
+
+// ---------------------------------------------------------------------------
+// C ABI: pair packing
+// ---------------------------------------------------------------------------
+static bool touches_exotic(const fc2_fasta *f, uint64_t g0, uint64_t g1) {
+    if (f->exotic.empty() || g1 <= g0) return false;
+    auto it = std::lower_bound(f->exotic.begin(), f->exotic.end(), g0);
+    return it != f->exotic.end() && *it < g1;
+}
+
+extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t n, const uint8_t *reads,
+                              const uint64_t *read_off, fc2_pair *pairs, uint64_t *read_words, uint32_t rw,
+                              uint64_t *read_nwords, uint32_t nw, uint64_t stride, uint64_t *n_bytepath,
+                              int n_threads) {
+    int rc = validate_params(p);
+    if (rc) return rc;
+    if (n && (!reads || !read_off || !pairs || !read_words || !read_nwords)) return fail(FC2_E_PARAM, "fc2_pack_pairs: null argument");
+    if (stride < n) return fail(FC2_E_PARAM, "fc2_pack_pairs: stride < n");
+    if (f && !f->packed) return fail(FC2_E_PARAM, "fc2_pack_pairs: genome must be packed first (fc2_fasta_pack)");
+    const int e = eff_anchor(p);
+    const int T = n_workers(n_threads);
+    std::atomic<uint64_t> nbp{0};
+    std::atomic<int64_t> bad_chrom{-1}, bad_rows{-1}, bad_dist{-1};
+    const int nch = f ? (int)f->chroms.size() : 0;
+    parallel_for(n, T, [&](uint64_t b, uint64_t en) {
+        uint64_t local_bp = 0;
+        for (uint64_t i = b; i < en; ++i) {
+            fc2_pair &pr = pairs[i];
+            pr.flags &= (uint8_t)(FC2_PAIR_BACKSPLICE | FC2_PAIR_PRIMARY_REV | FC2_PAIR_SKIP);
+            pr._pad = 0;
+            for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = 0;
+            for (uint32_t j = 0; j < nw; ++j) read_nwords[(uint64_t)j * stride + i] = 0;
+            if (pr.flags & FC2_PAIR_SKIP) continue;
+            if (f && (int)pr.chrom >= nch) { int64_t x = -1; bad_chrom.compare_exchange_strong(x, (int64_t)i); continue; }
+            const int L = pr.read_len;
+            const int l = L - 2 * e;
+            if (l < 0) continue;  // range(l+1) is empty: no hit, no window use
+            if (p->maxdist > 255 && l > 255) { int64_t x = -1; bad_dist.compare_exchange_strong(x, (int64_t)i); }
+            const uint8_t *I = reads + read_off[i] + e;
+            bool bytepath = l > kMaxFastL, anyN = false;
+            if (!bytepath) {
+                if ((uint64_t)2 * l > (uint64_t)rw * 64 || (uint64_t)l > (uint64_t)nw * 64) {
+                    int64_t x = -1; bad_rows.compare_exchange_strong(x, (int64_t)i); continue;
+                }
+                // tight bit-sliced row: low bits at [0, l), high bits at [l, 2l)
+                for (int j = 0; j < l; ++j) {
+                    const int cl = bclass(I[j]);
+                    if (cl == 5) { bytepath = true; break; }
+                    if (cl == 4) {
+                        anyN = true;
+                        read_nwords[(uint64_t)(j >> 6) * stride + i] |= 1ull << (j & 63);
+                        continue;
+                    }
+                    if (cl & 1) read_words[(uint64_t)(j >> 6) * stride + i] |= 1ull << (j & 63);
+                    if (cl & 2) {
+                        const int t = l + j;
+                        read_words[(uint64_t)(t >> 6) * stride + i] |= 1ull << (t & 63);
+                    }
+                }
+            }
+            if (!bytepath && f) {
+                const fc2_chrom_rec &c = f->chroms[pr.chrom];
+                const int64_t W = l + 2;
+                const int64_t wsA = (int64_t)pr.a_pos + e, wsB = (int64_t)pr.b_aend - e - W;
+                if (c.regular != 1) bytepath = true;
+                else if (wsA > c.size || wsA + W < 0 || wsB > c.size || wsB + W < 0) bytepath = true;
+                else {
+                    auto clampg = [&](int64_t s) { return (uint64_t)std::min<int64_t>(std::max<int64_t>(s, 0), c.size) + c.gstart; };
+                    if (touches_exotic(f, clampg(wsA), clampg(wsA + W)) || touches_exotic(f, clampg(wsB), clampg(wsB + W)))
+                        bytepath = true;
+                }
+            }
+            if (bytepath) {
+                pr.flags |= FC2_PAIR_BYTEPATH;
+                for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = 0;
+                for (uint32_t j = 0; j < nw; ++j) read_nwords[(uint64_t)j * stride + i] = 0;
+                ++local_bp;
+            } else if (anyN) {
+                pr.flags |= FC2_PAIR_READ_N;
+            }
+        }
+        nbp += local_bp;
+    });
+    if (bad_chrom.load() >= 0)
+        return fail(FC2_E_KEY, "pair " + std::to_string(bad_chrom.load()) +
+                                   ": chromosome not in the genome index (reference KeyError, find_circ.py:193)");
+    if (bad_rows.load() >= 0) return fail(FC2_E_PARAM, "pair " + std::to_string(bad_rows.load()) + ": read rows too narrow");
+    if (bad_dist.load() >= 0) return fail(FC2_E_RANGE, "maxdist > 255 with reads whose l > 255 is not supported");
+    if (n_bytepath) *n_bytepath = nbp.load();
+    return FC2_OK;
+}
+
+static inline uint64_t block_bytes(int l) {  // header + I + A + B (windows up to l+3)
+    const uint64_t lc = (uint64_t)std::max(0, l);
+    return (12 + lc + 2 * (lc + 3) + 3) & ~3ull;
+}
+
+extern "C" int fc2_bytepath_size(const fc2_params *p, uint64_t n, const fc2_pair *pairs, uint64_t *m, uint64_t *arena_bytes) {
+    int rc = validate_params(p);
+    if (rc) return rc;
+    const int e = eff_anchor(p);
+    uint64_t mm = 0, bytes = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        if (!(pairs[i].flags & FC2_PAIR_BYTEPATH)) continue;
+        bytes += block_bytes((int)pairs[i].read_len - 2 * e);
+        ++mm;
+    }
+    if (m) *m = mm;
+    if (arena_bytes) *arena_bytes = bytes;
+    return FC2_OK;
+}
+
+extern "C" int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64_t n, const uint8_t *reads,
+                                 const uint64_t *read_off, const fc2_pair *pairs, uint64_t *index, fc2_pair *bpairs,
+                                 uint64_t *off, uint8_t *arena) {
+    int rc = validate_params(p);
+    if (rc) return rc;
+    const int e = eff_anchor(p);
+    uint64_t k = 0, pos = 0;
+    std::string A, B;
+    for (uint64_t i = 0; i < n; ++i) {
+        const fc2_pair &pr = pairs[i];
+        if (!(pr.flags & FC2_PAIR_BYTEPATH)) continue;
+        const int L = pr.read_len;
+        const int l = L - 2 * e;
+        int32_t lenI = std::max(0, l);
+        A.clear(); B.clear();
+        if (l >= 0) {
+            const int64_t flank = l + 2;
+            rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + flank, A);
+            if (rc) return rc;
+            rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - flank, (int64_t)pr.b_aend - e, B);
+            if (rc) return rc;
+        }
+        // a window of unexpected length (outside get_data's defined range) is kept at
+        // l+3 bytes so the kernel sees the length mismatch and reports ERR_WIN
+        const int lc = std::max(0, l);
+        const int32_t lenA = (int32_t)std::min<size_t>(A.size(), (size_t)lc + 3);
+        const int32_t lenB = (int32_t)std::min<size_t>(B.size(), (size_t)lc + 3);
+        index[k] = i;
+        bpairs[k] = pr;
+        off[k] = pos;
+        uint8_t *blk = arena + pos;
+        memcpy(blk, &lenI, 4);
+        memcpy(blk + 4, &lenA, 4);
+        memcpy(blk + 8, &lenB, 4);
+        uint8_t *q = blk + 12;
+        for (int j = 0; j < lenI; ++j) q[j] = upc(reads[read_off[i] + e + j]);
+        q += lenI;
+        memcpy(q, A.data(), (size_t)std::min<int32_t>(lenA, (int32_t)A.size()));
+        q += lenA;
+        memcpy(q, B.data(), (size_t)std::min<int32_t>(lenB, (int32_t)B.size()));
+        pos += block_bytes(l);
+        ++k;
+    }
+    return FC2_OK;
+}

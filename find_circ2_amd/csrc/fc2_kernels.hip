@@ -1,0 +1,776 @@
+// fc2_kernels.hip -- CDNA4 (gfx950) kernels for find_circ2's breakpoint search.
+//
+// Hot path: JunctionSpan.find_breakpoints (find_circ.py:854-974) with its
+// genome window fetch (indexed_fasta.get_data, find_circ.py:189-215) for a
+// whole batch of anchor pairs, one pair per lane.
+//
+// Per pair the reference tries every breakpoint x in [0, l] and counts
+//     dist(x) = #{i < x : A[i] != I[i]} + #{x <= i < l : B[i+2] != I[i]}
+// (A/B = upper-cased genome windows of l+2 bases, I = internal read part),
+// keeps x with dist <= maxdist whose dinucleotides A[x:x+2]+B[x:x+2] are GTAG
+// ('+') or CTAC ('-') (every x with --non-canonical), scores them
+// 20*canonical - 10*dist - ov (+100 strand match with --strand-pref) and
+// returns the best-score ties in (x ascending, '+' before '-') order.
+//
+// Here every sequence is held bit-sliced (one bit per base per plane: low code
+// bit, high code bit, N), so one 64-bit VALU op compares 64 bases:
+//   mismatch(i) = (loA^loI | hiA^hiI | nA^nI)(i)        ('N'=='N' is a match)
+//   dist(x)     = popc(mA & below(x)) + popc(mB) - popc(mB & below(x))
+//   GTAG mask   = G_A & T_A>>1 & A_B & G_B>>1  (bitwise, all x at once)
+// so the O(l^2) byte loop of find_circ.py:906-908 becomes ~NW word ops plus
+// a popcount per signal candidate.  The work is integer and HBM-bound (no
+// MFMA); see DESIGN.md for the roofline.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fc2_common.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint64_t lowbits(int n) {  // n in any range; bits [0, n)
+    return n >= 64 ? ~0ull : (n <= 0 ? 0ull : ((1ull << n) - 1ull));
+}
+
+// bits [s, s+64) of the 128-bit value hi:lo, s in [0, 63]
+__device__ __forceinline__ uint64_t fsh(uint64_t lo, uint64_t hi, unsigned s) {
+    return s ? ((lo >> s) | (hi << (64u - s))) : lo;
+}
+
+// positions [a, b) restricted to word k (positions 64k .. 64k+63)
+__device__ __forceinline__ uint64_t rmask(int a, int b, int k) {
+    const int lo = a - 64 * k, hi = b - 64 * k;
+    if (hi <= 0 || lo >= 64 || hi <= lo) return 0ull;
+    return lowbits(hi) & ~lowbits(lo);
+}
+
+template <int NW>
+struct Planes {
+    uint64_t lo[NW + 1], hi[NW + 1], n[NW + 1];
+};
+
+// One genome window of W bases starting at chromosome position ws, as three
+// bit planes.  Positions outside [0, csize) read as 'N' (get_data's padding,
+// find_circ.py:194-211).
+template <int NW>
+__device__ __forceinline__ void load_window(const fc2_genome_view &g, uint64_t cstart, int64_t csize,
+                                            int64_t ws, int W, Planes<NW> &P) {
+    if (g.dummy) {
+#pragma unroll
+        for (int k = 0; k <= NW; ++k) { P.lo[k] = 0; P.hi[k] = 0; P.n[k] = ~0ull; }
+        return;
+    }
+    const int64_t g0 = (int64_t)cstart + ws;
+    const int64_t u0 = g0 >> 6;  // floor division
+    const unsigned sh = (unsigned)(g0 & 63);
+    const ulonglong2 *U = reinterpret_cast<const ulonglong2 *>(g.units);
+    uint64_t ul[NW + 2], uh[NW + 2];
+#pragma unroll
+    for (int j = 0; j <= NW; ++j) {
+        const int64_t u = u0 + j;
+        const bool need = (j < NW) || (sh != 0);
+        if (need && u >= 0 && (uint64_t)u < g.n_units) {
+            const ulonglong2 v = U[u];
+            ul[j] = v.x; uh[j] = v.y;
+        } else {
+            ul[j] = 0; uh[j] = 0;
+        }
+    }
+    ul[NW + 1] = 0; uh[NW + 1] = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        P.lo[k] = fsh(ul[k], ul[k + 1], sh);
+        P.hi[k] = fsh(uh[k], uh[k + 1], sh);
+    }
+    P.lo[NW] = 0; P.hi[NW] = 0;
+
+    // N plane: only touched when the coarse map says a 1024-base block has an N.
+    bool anyN = false;
+    {
+        const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
+        const int64_t b0 = u0 >> 4, b1 = (u0 + NW) >> 4;
+        if (b0 >= 0 && b0 < nb) anyN |= (g.ncoarse[b0 >> 5] >> (b0 & 31)) & 1u;
+        if (b1 != b0 && b1 >= 0 && b1 < nb) anyN |= (g.ncoarse[b1 >> 5] >> (b1 & 31)) & 1u;
+    }
+    if (anyN) {
+        uint64_t un[NW + 2];
+#pragma unroll
+        for (int j = 0; j <= NW; ++j) {
+            const int64_t u = u0 + j;
+            un[j] = (u >= 0 && (uint64_t)u < g.n_units) ? g.nplane[u] : 0ull;
+        }
+        un[NW + 1] = 0;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) P.n[k] = fsh(un[k], un[k + 1], sh);
+    } else {
+#pragma unroll
+        for (int k = 0; k < NW; ++k) P.n[k] = 0;
+    }
+    P.n[NW] = 0;
+
+    // chromosome bounds -> 'N'
+    int64_t vlo = -ws, vhi = csize - ws;
+    vlo = vlo < 0 ? 0 : (vlo > W ? W : vlo);
+    vhi = vhi < 0 ? 0 : (vhi > W ? W : vhi);
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const uint64_t v = rmask((int)vlo, (int)vhi, k);
+        P.lo[k] &= v; P.hi[k] &= v; P.n[k] = (P.n[k] & v) | ~v;
+    }
+}
+
+// base code (A0 C1 G2 T3 N4) at runtime position pos < 64*NW
+template <int NW>
+__device__ __forceinline__ unsigned code_at(const Planes<NW> &P, int pos) {
+    const int k = pos >> 6, b = pos & 63;
+    unsigned c = 0;
+#pragma unroll
+    for (int kk = 0; kk < NW; ++kk) {
+        if (kk == k) {
+            c = ((P.n[kk] >> b) & 1ull) ? 4u
+                                        : (unsigned)(((P.lo[kk] >> b) & 1ull) | (((P.hi[kk] >> b) & 1ull) << 1));
+        }
+    }
+    return c;
+}
+
+struct Best {
+    int n_hits = 0;        // number of Splices appended (find_circ.py:947-954)
+    int best_score = 0;
+    int best_x = -1;
+    int best_minus = 0;
+    int best_dist = 0;
+    int best_ov = 0;
+    int n_ties = 0;
+};
+
+__device__ __forceinline__ int ov_of(int x, int l, int margin) {  // find_circ.py:917-922
+    int ov = 0;
+    if (margin) {
+        if (x < margin) ov = margin - x;
+        if (l - x < margin) ov = margin - (l - x);
+    }
+    return ov;
+}
+
+__device__ __forceinline__ void add_hit(Best &B, int x, int minus, int dist, int ov, int score) {
+    if (B.n_hits == 0 || score > B.best_score) {
+        B.best_score = score; B.best_x = x; B.best_minus = minus; B.best_dist = dist; B.best_ov = ov;
+        B.n_ties = 1;
+    } else if (score == B.best_score) {
+        B.n_ties += 1;
+    }
+    B.n_hits += 1;
+}
+
+__device__ __forceinline__ uint64_t pack_result(const Best &B, unsigned gtag12, unsigned err) {
+    uint64_t r;
+    if (B.n_hits == 0) {
+        r = (uint64_t)(uint16_t)(int16_t)-1;
+        r |= (uint64_t)(FC2_RES_DONE | err) << 48;
+        return r;
+    }
+    const unsigned nt = B.n_hits >= 2 ? (unsigned)B.n_ties : 1u;   // find_circ.py:961-972
+    const unsigned dist = B.best_dist > 255 ? 255u : (unsigned)B.best_dist;
+    const unsigned info = FC2_RES_DONE | err | (B.best_minus ? FC2_RES_MINUS : 0u) |
+                          ((gtag12 << FC2_RES_GTAG_SHIFT) & FC2_RES_GTAG_MASK);
+    r = (uint64_t)(uint16_t)(int16_t)B.best_x;
+    r |= (uint64_t)(dist & 0xFF) << 16;
+    r |= (uint64_t)(B.best_ov & 0xFF) << 24;
+    r |= (uint64_t)(nt > 0xFFFF ? 0xFFFFu : nt) << 32;
+    r |= (uint64_t)info << 48;
+    return r;
+}
+
+__device__ __forceinline__ uint64_t nohit_result(unsigned err) {
+    Best B;
+    return pack_result(B, 0, err);
+}
+
+// ---------------------------------------------------------------------------
+// register kernel: one pair per lane, NW 64-bit words per bit plane
+// ---------------------------------------------------------------------------
+template <int NW>
+__global__ __launch_bounds__(kBlock) void bp_scan_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+                                                         uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
+                                                         uint32_t tw) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= bv.n) return;
+    const fc2_pair pr = bv.pairs[i];
+    if (pr.flags & FC2_PAIR_BYTEPATH) return;  // left for the byte-exact kernel
+
+    const int e = p.asize - p.margin;
+    const int L = (int)pr.read_len;
+    const int l = L - 2 * e;
+    const bool want_ties = p.allhits != 0;
+
+    if ((pr.flags & FC2_PAIR_SKIP) || l < 0 || l > 64 * NW - 2 || pr.chrom >= g.n_chrom) {
+        unsigned err = 0;
+        if (!(pr.flags & FC2_PAIR_SKIP) && l >= 0 && (l > 64 * NW - 2 || pr.chrom >= g.n_chrom)) err = FC2_RES_ERR_WIN;
+        out[i] = nohit_result(err);
+        if (want_ties)
+            for (uint32_t k = 0; k < tw; ++k) tiemask[(uint64_t)k * bv.stride + i] = 0;
+        return;
+    }
+    const int W = l + 2;  // flank, find_circ.py:900
+
+    // --- internal read part I[0..l): three bit planes --------------------------
+    uint64_t Ilo[NW], Ihi[NW], In[NW];
+    {
+        uint64_t r[2 * NW + 1];
+#pragma unroll
+        for (int j = 0; j < 2 * NW; ++j)
+            r[j] = ((uint32_t)j < bv.rw) ? bv.read_words[(uint64_t)j * bv.stride + i] : 0ull;
+        r[2 * NW] = 0;
+        const int base = l >> 6;
+        const unsigned s = (unsigned)(l & 63);
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            const uint64_t m = rmask(0, l, k);
+            Ilo[k] = r[k] & m;
+            uint64_t v = 0;
+#pragma unroll
+            for (int bb = 0; bb < NW; ++bb)
+                if (bb == base) v = fsh(r[bb + k], r[bb + k + 1], s);
+            Ihi[k] = v & m;
+        }
+        if (pr.flags & FC2_PAIR_READ_N) {
+#pragma unroll
+            for (int k = 0; k < NW; ++k)
+                In[k] = ((uint32_t)k < bv.nw ? bv.read_nwords[(uint64_t)k * bv.stride + i] : 0ull) & rmask(0, l, k);
+        } else {
+#pragma unroll
+            for (int k = 0; k < NW; ++k) In[k] = 0;
+        }
+    }
+
+    // --- the two genome windows (find_circ.py:900-902) -------------------------
+    const uint64_t cstart = g.dummy ? 0ull : g.chrom_start[pr.chrom];
+    const int64_t csize = g.dummy ? (int64_t)1 << 62 : g.chrom_size[pr.chrom];
+    const int64_t wsA = (int64_t)pr.a_pos + e;
+    const int64_t wsB = (int64_t)pr.b_aend - e - W;
+    // get_data is only length-preserving for start <= size and end >= 0; the host
+    // routes anything else to the byte kernel -- flag defensively here.
+    if (wsA > csize || wsA + W < 0 || wsB > csize || wsB + W < 0) {
+        out[i] = nohit_result(FC2_RES_ERR_WIN);
+        if (want_ties)
+            for (uint32_t k = 0; k < tw; ++k) tiemask[(uint64_t)k * bv.stride + i] = 0;
+        return;
+    }
+    Planes<NW> A, B;
+    load_window<NW>(g, cstart, csize, wsA, W, A);
+    load_window<NW>(g, cstart, csize, wsB, W, B);
+
+    // --- mismatch planes ------------------------------------------------------
+    uint64_t mA[NW], mB[NW];
+    int cA[NW], cB[NW];
+    int totB = 0, accA = 0;
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const uint64_t m = rmask(0, l, k);
+        mA[k] = ((A.lo[k] ^ Ilo[k]) | (A.hi[k] ^ Ihi[k]) | (A.n[k] ^ In[k])) & m;
+        const uint64_t blo = fsh(B.lo[k], B.lo[k + 1], 2), bhi = fsh(B.hi[k], B.hi[k + 1], 2),
+                       bn = fsh(B.n[k], B.n[k + 1], 2);
+        mB[k] = ((blo ^ Ilo[k]) | (bhi ^ Ihi[k]) | (bn ^ In[k])) & m;
+        cA[k] = accA; cB[k] = totB;
+        accA += __popcll(mA[k]);
+        totB += __popcll(mB[k]);
+    }
+
+    // --- splice-signal masks: GTAG -> '+', CTAC -> '-' (find_circ.py:924-954) --
+    uint64_t plus[NW], minus[NW];
+#pragma unroll
+    for (int k = 0; k < NW; ++k) {
+        const uint64_t xm = rmask(0, l + 1, k);
+        const uint64_t aLo1 = fsh(A.lo[k], A.lo[k + 1], 1), aHi1 = fsh(A.hi[k], A.hi[k + 1], 1);
+        const uint64_t bLo1 = fsh(B.lo[k], B.lo[k + 1], 1), bHi1 = fsh(B.hi[k], B.hi[k + 1], 1);
+        const uint64_t A_T1 = aHi1 & aLo1;                             // A[x+1] == 'T'
+        const uint64_t B_A0 = ~(B.lo[k] | B.hi[k] | B.n[k]);           // B[x]   == 'A'
+        const uint64_t A_G0 = A.hi[k] & ~A.lo[k];                      // A[x]   == 'G'
+        const uint64_t A_C0 = A.lo[k] & ~A.hi[k];                      // A[x]   == 'C'
+        const uint64_t B_G1 = bHi1 & ~bLo1;                            // B[x+1] == 'G'
+        const uint64_t B_C1 = bLo1 & ~bHi1;                            // B[x+1] == 'C'
+        plus[k] = A_G0 & A_T1 & B_A0 & B_G1 & xm;
+        minus[k] = A_C0 & A_T1 & B_A0 & B_C1 & xm;
+    }
+
+    const int prim_minus = (pr.flags & FC2_PAIR_PRIMARY_REV) ? 1 : 0;
+    const int sp_plus = p.strandpref ? (prim_minus ? 0 : 100) : 0;   // find_circ.py:796-797
+    const int sp_minus = p.strandpref ? (prim_minus ? 100 : 0) : 0;
+    Best Bst;
+
+    if (!p.noncanonical) {
+        // only signal positions can produce hits: iterate their set bits in x order
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            uint64_t w = plus[k] | minus[k];
+            while (w) {
+                const int b = __ffsll((long long)w) - 1;
+                w &= w - 1;
+                const int x = 64 * k + b;
+                const uint64_t below = lowbits(b);
+                const int dist = cA[k] + __popcll(mA[k] & below) + totB - (cB[k] + __popcll(mB[k] & below));
+                if (dist <= p.maxdist) {
+                    const int ov = ov_of(x, l, p.margin);
+                    const int isminus = (int)((minus[k] >> b) & 1ull);
+                    const int score = 20 - 10 * dist - ov + (isminus ? sp_minus : sp_plus);
+                    add_hit(Bst, x, isminus, dist, ov, score);
+                }
+            }
+        }
+    } else {
+        // every x with dist <= maxdist yields a '+' and a '-' Splice (find_circ.py:947-949)
+        int d = totB;
+#pragma unroll
+        for (int k = 0; k < NW; ++k) {
+            for (int b = 0; b < 64; ++b) {
+                const int x = 64 * k + b;
+                if (x > l) break;
+                if (d <= p.maxdist) {
+                    const int ov = ov_of(x, l, p.margin);
+                    const int cp = (int)((plus[k] >> b) & 1ull), cm = (int)((minus[k] >> b) & 1ull);
+                    add_hit(Bst, x, 0, d, ov, 20 * cp - 10 * d - ov + sp_plus);
+                    add_hit(Bst, x, 1, d, ov, 20 * cm - 10 * d - ov + sp_minus);
+                }
+                d += (int)((mA[k] >> b) & 1ull) - (int)((mB[k] >> b) & 1ull);
+            }
+        }
+    }
+
+    unsigned gtag12 = 0;
+    if (Bst.n_hits) {
+        const int x = Bst.best_x;
+        gtag12 = code_at<NW>(A, x) | (code_at<NW>(A, x + 1) << 3) | (code_at<NW>(B, x) << 6) |
+                 (code_at<NW>(B, x + 1) << 9);
+    }
+    out[i] = pack_result(Bst, gtag12, 0);
+
+    if (want_ties) {
+        // --all-hits: mark every tie (find_circ.py:966-974), second pass over the same hits
+        uint64_t tp[NW], tm[NW];
+#pragma unroll
+        for (int k = 0; k < NW; ++k) { tp[k] = 0; tm[k] = 0; }
+        if (Bst.n_hits) {
+            const int best = Bst.best_score;
+            if (!p.noncanonical) {
+#pragma unroll
+                for (int k = 0; k < NW; ++k) {
+                    uint64_t w = plus[k] | minus[k];
+                    while (w) {
+                        const int b = __ffsll((long long)w) - 1;
+                        w &= w - 1;
+                        const int x = 64 * k + b;
+                        const uint64_t below = lowbits(b);
+                        const int dist = cA[k] + __popcll(mA[k] & below) + totB - (cB[k] + __popcll(mB[k] & below));
+                        if (dist <= p.maxdist) {
+                            const int isminus = (int)((minus[k] >> b) & 1ull);
+                            const int score = 20 - 10 * dist - ov_of(x, l, p.margin) + (isminus ? sp_minus : sp_plus);
+                            if (score == best) {
+                                if (isminus) tm[k] |= 1ull << b; else tp[k] |= 1ull << b;
+                            }
+                        }
+                    }
+                }
+            } else {
+                int d = totB;
+#pragma unroll
+                for (int k = 0; k < NW; ++k) {
+                    for (int b = 0; b < 64; ++b) {
+                        const int x = 64 * k + b;
+                        if (x > l) break;
+                        if (d <= p.maxdist) {
+                            const int ov = ov_of(x, l, p.margin);
+                            const int cp = (int)((plus[k] >> b) & 1ull), cm = (int)((minus[k] >> b) & 1ull);
+                            if (20 * cp - 10 * d - ov + sp_plus == best) tp[k] |= 1ull << b;
+                            if (20 * cm - 10 * d - ov + sp_minus == best) tm[k] |= 1ull << b;
+                        }
+                        d += (int)((mA[k] >> b) & 1ull) - (int)((mB[k] >> b) & 1ull);
+                    }
+                }
+            }
+        }
+        const uint32_t half = tw / 2;
+        for (uint32_t k = 0; k < half; ++k) {
+            uint64_t vp = 0, vm = 0;
+#pragma unroll
+            for (int kk = 0; kk < NW; ++kk)
+                if ((uint32_t)kk == k) { vp = tp[kk]; vm = tm[kk]; }
+            tiemask[(uint64_t)k * bv.stride + i] = vp;
+            tiemask[(uint64_t)(half + k) * bv.stride + i] = vm;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// byte-exact kernel: any bytes, any read length (rare pairs)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool is_acgtn(uint8_t c) {
+    return c == 'A' || c == 'C' || c == 'G' || c == 'T' || c == 'N';
+}
+__device__ __forceinline__ unsigned code_of(uint8_t c) {
+    return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
+}
+
+__global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_bytes_view v, uint64_t *__restrict__ out,
+                                                          uint64_t *__restrict__ tiemask, uint32_t tw, uint64_t stride) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= v.m) return;
+    const uint64_t i = v.index[k];
+    const fc2_pair pr = v.pairs[k];
+    const uint8_t *blk = v.arena + v.off[k];
+    const int lenI = ((const int32_t *)blk)[0], lenA = ((const int32_t *)blk)[1], lenB = ((const int32_t *)blk)[2];
+    const uint8_t *I = blk + 12;
+    const uint8_t *Af = I + lenI;
+    const uint8_t *Bf = Af + lenA;
+    const int e = p.asize - p.margin;
+    const int l = (int)pr.read_len - 2 * e;
+    const bool want_ties = p.allhits != 0;
+    const uint32_t half = tw / 2;
+    if (want_ties)
+        for (uint32_t w = 0; w < tw; ++w) tiemask[(uint64_t)w * stride + i] = 0;
+    if ((pr.flags & FC2_PAIR_SKIP) || l < 0) { out[i] = nohit_result(0); return; }
+    if (lenI != l || lenA != l + 2 || lenB != l + 2) { out[i] = nohit_result(FC2_RES_ERR_WIN); return; }
+
+    int totB = 0;
+    for (int j = 0; j < l; ++j) totB += Bf[j + 2] != I[j];
+    const int prim_minus = (pr.flags & FC2_PAIR_PRIMARY_REV) ? 1 : 0;
+    const int sp_plus = p.strandpref ? (prim_minus ? 0 : 100) : 0;
+    const int sp_minus = p.strandpref ? (prim_minus ? 100 : 0) : 0;
+    Best Bst;
+    unsigned err = 0;
+    for (int pass = 0; pass < (want_ties ? 2 : 1); ++pass) {
+        int d = totB;
+        for (int x = 0; x <= l; ++x) {
+            if (x > 0) d += (int)(Af[x - 1] != I[x - 1]) - (int)(Bf[x + 1] != I[x - 1]);
+            if (d > p.maxdist) continue;
+            const uint8_t g0 = Af[x], g1 = Af[x + 1], g2 = Bf[x], g3 = Bf[x + 1];
+            if (!(is_acgtn(g0) && is_acgtn(g1) && is_acgtn(g2) && is_acgtn(g3))) { err = FC2_RES_ERR_KEY; break; }
+            const int cp = (g0 == 'G' && g1 == 'T' && g2 == 'A' && g3 == 'G');
+            const int cm = (g0 == 'C' && g1 == 'T' && g2 == 'A' && g3 == 'C');
+            const int ov = ov_of(x, l, p.margin);
+            if (p.noncanonical) {
+                const int s1 = 20 * cp - 10 * d - ov + sp_plus, s2 = 20 * cm - 10 * d - ov + sp_minus;
+                if (pass == 0) { add_hit(Bst, x, 0, d, ov, s1); add_hit(Bst, x, 1, d, ov, s2); }
+                else {
+                    if (s1 == Bst.best_score) tiemask[(uint64_t)(x >> 6) * stride + i] |= 1ull << (x & 63);
+                    if (s2 == Bst.best_score) tiemask[(uint64_t)(half + (x >> 6)) * stride + i] |= 1ull << (x & 63);
+                }
+            } else if (cp || cm) {
+                const int s = 20 - 10 * d - ov + (cm ? sp_minus : sp_plus);
+                if (pass == 0) add_hit(Bst, x, cm, d, ov, s);
+                else if (s == Bst.best_score)
+                    tiemask[(uint64_t)((cm ? half : 0) + (x >> 6)) * stride + i] |= 1ull << (x & 63);
+            }
+        }
+        if (err || !Bst.n_hits) break;
+    }
+    if (err) { out[i] = nohit_result(err); return; }
+    unsigned gtag12 = 0;
+    if (Bst.n_hits) {
+        const int x = Bst.best_x;
+        gtag12 = code_of(Af[x]) | (code_of(Af[x + 1]) << 3) | (code_of(Bf[x]) << 6) | (code_of(Bf[x + 1]) << 9);
+    }
+    out[i] = pack_result(Bst, gtag12, 0);
+}
+
+// ---------------------------------------------------------------------------
+// synthetic workloads (bench / tests): counter-based RNG, fully reproducible
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t smix(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+__global__ void synth_genome_kernel(uint64_t seed, uint64_t *units, uint64_t *nplane, uint64_t n_units,
+                                    const int64_t *n_lo, const int64_t *n_hi, uint32_t n_iv) {
+    const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n_units) return;
+    uint64_t lo = smix(seed * 0x2545F4914F6CDD1Dull ^ (2 * u));
+    uint64_t hi = smix(seed * 0x2545F4914F6CDD1Dull ^ (2 * u + 1));
+    const int64_t b0 = (int64_t)u * 64, b1 = b0 + 64;
+    // first interval with n_hi > b0
+    uint32_t a = 0, z = n_iv;
+    while (a < z) {
+        const uint32_t m = (a + z) >> 1;
+        if (n_hi[m] <= b0) a = m + 1; else z = m;
+    }
+    uint64_t nm = 0;
+    for (uint32_t k = a; k < n_iv && n_lo[k] < b1; ++k) {
+        const int64_t s = n_lo[k] > b0 ? n_lo[k] - b0 : 0;
+        const int64_t t = n_hi[k] < b1 ? n_hi[k] - b0 : 64;
+        nm |= lowbits((int)t) & ~lowbits((int)s);
+    }
+    units[2 * u] = lo & ~nm;
+    units[2 * u + 1] = hi & ~nm;
+    nplane[u] = nm;
+}
+
+__global__ void coarse_kernel(const uint64_t *nplane, uint32_t *ncoarse, uint64_t n_units) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n_blocks = (n_units + 15) >> 4;
+    const uint64_t n_words = (n_blocks + 31) >> 5;
+    if (w >= n_words) return;
+    uint32_t bits = 0;
+    for (int b = 0; b < 32; ++b) {
+        const uint64_t blk = w * 32 + b;
+        if (blk >= n_blocks) break;
+        uint64_t acc = 0;
+        for (int j = 0; j < 16; ++j) {
+            const uint64_t u = blk * 16 + j;
+            if (u < n_units) acc |= nplane[u];
+        }
+        if (acc) bits |= 1u << b;
+    }
+    ncoarse[w] = bits;
+}
+
+struct Rng {
+    uint64_t s;
+    __device__ uint64_t next() { s += 0x9E3779B97F4A7C15ull; return smix(s); }
+    __device__ float uni() { return (float)(next() >> 40) * (1.0f / 16777216.0f); }
+    __device__ int64_t below(int64_t n) { return n <= 0 ? 0 : (int64_t)(next() % (uint64_t)n); }
+};
+
+__device__ __forceinline__ unsigned gbase(const fc2_genome_view &g, uint64_t cstart, int64_t csize, int64_t p) {
+    if (g.dummy || p < 0 || p >= csize) return 4u;
+    const uint64_t q = cstart + (uint64_t)p;
+    const uint64_t u = q >> 6;
+    const unsigned b = (unsigned)(q & 63);
+    if ((g.nplane[u] >> b) & 1ull) return 4u;
+    return (unsigned)(((g.units[2 * u] >> b) & 1ull) | (((g.units[2 * u + 1] >> b) & 1ull) << 1));
+}
+
+__device__ __forceinline__ bool dinuc(const fc2_genome_view &g, uint64_t cs, int64_t sz, int64_t q, unsigned c0, unsigned c1) {
+    return gbase(g, cs, sz, q) == c0 && gbase(g, cs, sz, q + 1) == c1;
+}
+
+constexpr unsigned cA = 0, cC = 1, cG = 2, cT = 3;
+
+__global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_view g, const int64_t *chrom_cum,
+                                   uint64_t n, fc2_pair *pairs, uint64_t *read_words, uint32_t rw,
+                                   uint64_t *read_nwords, uint32_t nw, uint64_t stride, int32_t *truth) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    Rng R{smix(cfg.seed ^ smix(i + 0x51ED2701ull))};
+    const int e = p.asize - p.margin;
+    const int amin = p.asize;
+    int L = cfg.len_min + (int)R.below(cfg.len_max - cfg.len_min + 1);
+    if (L < 2 * amin) L = 2 * amin;
+    const int kA = amin + (int)R.below(L - 2 * amin + 1);
+    const int kB = L - kA;
+    const bool bs = R.uni() < cfg.p_backsplice;
+    const bool planted = R.uni() < cfg.p_planted;
+    const bool msite = R.uni() < cfg.p_minus_site;
+    const int64_t total = chrom_cum[g.n_chrom];
+
+    uint32_t chrom = 0;
+    uint64_t cs = 0;
+    int64_t sz = 0, A0 = 0, B0 = 0, t0 = 0, t1 = 0;
+    bool ok = false;
+    for (int attempt = 0; attempt < 16 && !ok; ++attempt) {
+        const int64_t gp = R.below(total);
+        uint32_t a = 0, z = g.n_chrom;  // chrom_cum[c] <= gp < chrom_cum[c+1]
+        while (z - a > 1) {
+            const uint32_t m = (a + z) >> 1;
+            if (chrom_cum[m] <= gp) a = m; else z = m;
+        }
+        chrom = a;
+        cs = g.chrom_start[chrom];
+        sz = g.chrom_size[chrom];
+        const int64_t off = gp - chrom_cum[chrom];
+        const int64_t span = cfg.span_min + R.below(cfg.span_max - cfg.span_min + 1);
+        if (bs) {
+            // exon [start, end): read = G[end-kA:end] + G[start:start+kB]
+            int64_t end = off;
+            if (planted) {
+                for (int q = 0; q < 512; ++q)
+                    if (dinuc(g, cs, sz, off + q, msite ? cC : cG, cT)) { end = off + q; break; }
+            }
+            int64_t start = end - (span > (int64_t)(kA > kB ? kA : kB) ? span : (int64_t)(kA > kB ? kA : kB) + 1);
+            if (planted) {
+                for (int q = 0; q < 512; ++q)
+                    if (dinuc(g, cs, sz, start - 2 - q, cA, msite ? cC : cG)) { start = start - q; break; }
+            }
+            if (start >= 0 && end <= sz && end - kA >= 0 && start + kB <= end && kA <= end - start) {
+                A0 = end - kA; B0 = start; t0 = start; t1 = end; ok = true;
+            }
+        } else {
+            // intron [d, a): read = G[d-kA:d] + G[a:a+kB]
+            int64_t d = off;
+            if (planted) {
+                for (int q = 0; q < 512; ++q)
+                    if (dinuc(g, cs, sz, off + q, msite ? cC : cG, cT)) { d = off + q; break; }
+            }
+            int64_t a = d + span;
+            if (planted) {
+                for (int q = 0; q < 512; ++q)
+                    if (dinuc(g, cs, sz, a - 2 + q, cA, msite ? cC : cG)) { a = a + q; break; }
+            }
+            if (d - kA >= 0 && a + kB <= sz && a > d) { A0 = d - kA; B0 = a; t0 = d; t1 = a; ok = true; }
+        }
+    }
+    int c0 = 0, c1 = 0;
+    if (R.uni() < cfg.p_clip) { c0 = (int)R.below(4); c1 = (int)R.below(4); }
+    const int Lp = L - c0 - c1;
+    const int l = Lp - 2 * e;
+    fc2_pair pr;
+    pr.a_pos = (int32_t)(A0 + c0);
+    pr.b_aend = (int32_t)(B0 + kB - c1);
+    pr.chrom = chrom;
+    pr.read_len = (uint16_t)Lp;
+    pr.flags = (uint8_t)((bs ? FC2_PAIR_BACKSPLICE : 0u) | ((R.next() & 1ull) ? FC2_PAIR_PRIMARY_REV : 0u) |
+                         (ok ? 0u : FC2_PAIR_SKIP));
+    pr._pad = 0;
+    if (truth) { truth[2 * i] = ok ? (int32_t)t0 : -1; truth[2 * i + 1] = ok ? (int32_t)t1 : -1; }
+
+    // internal bases I[j] = read[c0 + e + j], j < l ; read[t] = t < kA ? G[A0+t] : G[B0+t-kA]
+    uint64_t wlo = 0, whi_first = 0;
+    (void)whi_first;
+    bool anyN = false;
+    // pass 1: low plane bits [0,l) and N words; pass 2: high plane bits [l,2l)
+    uint32_t wi = 0;   // next read word to store
+    uint64_t acc = 0;
+    int accn = 0;
+    uint64_t nacc = 0;
+    uint32_t ni = 0;
+    const int lim = l > 0 ? l : 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        Rng R2{smix(cfg.seed ^ smix(i * 0x9E37ull + 0xABCDEFull))};   // same mutation stream both passes
+        for (int j = 0; j < lim; ++j) {
+            const int t = c0 + e + j;
+            unsigned c = t < kA ? gbase(g, cs, sz, A0 + t) : gbase(g, cs, sz, B0 + t - kA);
+            if (R2.uni() < cfg.mut_rate) c = (c >= 4u) ? (unsigned)R2.below(4) : ((c + 1u + (unsigned)R2.below(3)) & 3u);
+            else (void)R2.next();
+            if (R2.uni() < cfg.n_rate) c = 4u;
+            const uint64_t bit = pass == 0 ? (c == 4u ? 0ull : (c & 1ull)) : (c == 4u ? 0ull : ((c >> 1) & 1ull));
+            acc |= bit << accn;
+            if (++accn == 64) {
+                if (wi < rw) read_words[(uint64_t)wi * stride + i] = acc;
+                ++wi; acc = 0; accn = 0;
+            }
+            if (pass == 0) {
+                if (c == 4u) { anyN = true; nacc |= 1ull << (j & 63); }
+                if ((j & 63) == 63 || j == lim - 1) {
+                    if (ni < nw && read_nwords) read_nwords[(uint64_t)ni * stride + i] = nacc;
+                    ++ni; nacc = 0;
+                }
+            }
+        }
+    }
+    if (accn) { if (wi < rw) read_words[(uint64_t)wi * stride + i] = acc; ++wi; }
+    for (; wi < rw; ++wi) read_words[(uint64_t)wi * stride + i] = 0;
+    if (read_nwords)
+        for (; ni < nw; ++ni) read_nwords[(uint64_t)ni * stride + i] = 0;
+    (void)wlo;
+    if (anyN) pr.flags |= FC2_PAIR_READ_N;
+    pairs[i] = pr;
+}
+
+inline int hip_check(hipError_t e, const char *what) {
+    if (e != hipSuccess) return fc2::fail(FC2_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    return FC2_OK;
+}
+
+inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
+
+}  // namespace
+
+// ===========================================================================
+// C ABI: launches
+// ===========================================================================
+extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                                  fc2_result *results, uint64_t *tiemask, uint32_t tw, void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (!g || !b || !results) return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: null argument");
+    if (b->n == 0) return FC2_OK;
+    if (!b->pairs || !b->read_words || b->stride < b->n || b->rw == 0)
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: bad batch view");
+    if (!g->dummy && (!g->units || !g->nplane || !g->ncoarse || !g->chrom_start || !g->chrom_size))
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: bad genome view");
+    if (p->allhits && (!tiemask || tw < 2))
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: --all-hits needs a tie mask");
+    const int ml = b->max_l < 0 ? 0 : b->max_l;
+    if (ml > fc2::kMaxFastL) return fc2::fail(FC2_E_RANGE, "fc2_bp_scan_launch: max_l exceeds the register kernel");
+    const int nwords = (ml + 2 + 63) / 64;
+    if (p->allhits && tw / 2 < (uint32_t)nwords)
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: tie mask too narrow");
+    if ((uint64_t)b->rw * 32 < (uint64_t)ml || (b->read_nwords && (uint64_t)b->nw * 64 < (uint64_t)ml))
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: read rows too narrow for max_l");
+    hipStream_t s = (hipStream_t)stream;
+    const unsigned grid = grid_for(b->n, kBlock);
+    uint64_t *out = reinterpret_cast<uint64_t *>(results);
+    if (nwords <= 2)
+        hipLaunchKernelGGL(bp_scan_kernel<2>, dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw);
+    else if (nwords <= 4)
+        hipLaunchKernelGGL(bp_scan_kernel<4>, dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw);
+    else
+        hipLaunchKernelGGL(bp_scan_kernel<8>, dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw);
+    return hip_check(hipGetLastError(), "bp_scan_kernel launch");
+}
+
+extern "C" int fc2_bp_scan_bytes_launch(const fc2_params *p, const fc2_bytes_view *v, fc2_result *results,
+                                        uint64_t *tiemask, uint32_t tw, uint64_t stride, void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (!v || !results) return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_bytes_launch: null argument");
+    if (v->m == 0) return FC2_OK;
+    if (!v->index || !v->pairs || !v->arena || !v->off)
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_bytes_launch: bad view");
+    if (p->allhits && (!tiemask || tw < 2))
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_bytes_launch: --all-hits needs a tie mask");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(bp_bytes_kernel, dim3(grid_for(v->m, kBlock)), dim3(kBlock), 0, s, *p, *v,
+                       reinterpret_cast<uint64_t *>(results), tiemask, tw, stride);
+    return hip_check(hipGetLastError(), "bp_bytes_kernel launch");
+}
+
+extern "C" int fc2_synth_genome_launch(uint64_t seed, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,
+                                       uint64_t n_units, const int64_t *n_lo, const int64_t *n_hi,
+                                       uint32_t n_intervals, void *stream) {
+    if (!units || !nplane || !ncoarse || n_units == 0) return fc2::fail(FC2_E_PARAM, "fc2_synth_genome_launch: bad args");
+    if (n_intervals && (!n_lo || !n_hi)) return fc2::fail(FC2_E_PARAM, "fc2_synth_genome_launch: intervals");
+    hipStream_t s = (hipStream_t)stream;
+    hipLaunchKernelGGL(synth_genome_kernel, dim3(grid_for(n_units, 256)), dim3(256), 0, s, seed, units, nplane,
+                       n_units, n_lo, n_hi, n_intervals);
+    int rc = hip_check(hipGetLastError(), "synth_genome_kernel launch");
+    if (rc) return rc;
+    return fc2_coarse_launch(nplane, ncoarse, n_units, stream);
+}
+
+extern "C" int fc2_coarse_launch(const uint64_t *nplane, uint32_t *ncoarse, uint64_t n_units, void *stream) {
+    if (!nplane || !ncoarse) return fc2::fail(FC2_E_PARAM, "fc2_coarse_launch: bad args");
+    const uint64_t n_words = (((n_units + 15) >> 4) + 31) >> 5;
+    hipLaunchKernelGGL(coarse_kernel, dim3(grid_for(n_words, 256)), dim3(256), 0, (hipStream_t)stream, nplane, ncoarse,
+                       n_units);
+    return hip_check(hipGetLastError(), "coarse_kernel launch");
+}
+
+extern "C" int fc2_synth_pairs_launch(const fc2_params *p, const fc2_synth_cfg *cfg, const fc2_genome_view *g,
+                                      const int64_t *chrom_cum, uint64_t n, fc2_pair *pairs, uint64_t *read_words,
+                                      uint32_t rw, uint64_t *read_nwords, uint32_t nw, uint64_t stride, int32_t *truth,
+                                      void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (!cfg || !g || !chrom_cum || !pairs || !read_words || stride < n)
+        return fc2::fail(FC2_E_PARAM, "fc2_synth_pairs_launch: bad args");
+    if (cfg->len_min < 2 * p->asize || cfg->len_max < cfg->len_min || cfg->len_max > 65535)
+        return fc2::fail(FC2_E_PARAM, "fc2_synth_pairs_launch: read length range");
+    const int lmax = cfg->len_max - 2 * fc2::eff_anchor(p);
+    if ((int64_t)rw * 32 < lmax || (read_nwords && (int64_t)nw * 64 < lmax))
+        return fc2::fail(FC2_E_PARAM, "fc2_synth_pairs_launch: rows too narrow");
+    if (n == 0) return FC2_OK;
+    hipLaunchKernelGGL(synth_pairs_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, *p, *cfg, *g,
+                       chrom_cum, n, pairs, read_words, rw, read_nwords, nw, stride, truth);
+    return hip_check(hipGetLastError(), "synth_pairs_kernel launch");
+}
+
+extern "C" int fc2_device_count(int *count) {
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (count) *count = (e == hipSuccess) ? c : 0;
+    return FC2_OK;
+}

@@ -1,0 +1,532 @@
+"""The hot path: ``JunctionSpan.find_breakpoints`` for batches of anchor pairs on MI355X.
+
+Reference interface (find_circ.py 1.99, Python 2):
+
+* ``Splice``                         find_circ.py:766-806
+* ``JunctionSpan.__init__``          find_circ.py:821-844
+* ``JunctionSpan.find_breakpoints``  find_circ.py:854-974 (called from
+  ``record_hits`` at :1303 / :1355, one pair at a time)
+
+Here the same function is evaluated for a whole ``PairBatch`` by one HIP
+launch (``fc2_bp_scan_launch``; rare pairs with exotic bytes / irregular FASTA
+layout / very long reads by ``fc2_bp_scan_bytes_launch``), and the per-pair
+results decode to exactly the ``Splice`` lists the reference returns.
+``JunctionSpan.find_breakpoints()`` is kept as a drop-in (one-pair batch) so
+code written against the reference keeps working; real callers batch.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Iterable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _native as N
+from .genome import Genome, _require_gpu, _torch
+
+_CODE = "ACGTN"
+_COMP = {"A": "T", "C": "G", "G": "C", "T": "A", "N": "N"}
+
+
+def rev_comp4(s: str) -> str:
+    return "".join(_COMP[c] for c in reversed(s))
+
+
+# ---------------------------------------------------------------------------
+# options (find_circ.py:393-404)
+# ---------------------------------------------------------------------------
+@dataclass
+class Options:
+    asize: int = 15            # -a/--anchor
+    margin: int = 2            # -m/--margin
+    maxdist: int = 2           # -d/--max-mismatch
+    noncanonical: bool = False # --non-canonical
+    strandpref: bool = False   # --strand-pref
+    allhits: bool = False      # --all-hits
+
+    def params(self) -> N.Params:
+        return N.Params(int(self.asize), int(self.margin), int(self.maxdist), int(bool(self.noncanonical)),
+                        int(bool(self.strandpref)), int(bool(self.allhits)), 0)
+
+    @property
+    def eff_a(self) -> int:   # find_circ.py:882
+        return self.asize - self.margin
+
+
+@dataclass
+class SynthConfig:
+    """Synthetic anchor-pair workload."""
+    seed: int = 1337
+    len_min: int = 100
+    len_max: int = 100
+    p_planted: float = 0.5
+    p_minus_site: float = 0.2
+    p_backsplice: float = 1.0
+    mut_rate: float = 0.005
+    n_rate: float = 0.0005
+    p_clip: float = 0.2
+    span_min: int = 150
+    span_max: int = 5000
+
+    def cfg(self) -> N.SynthCfg:
+        return N.SynthCfg(int(self.seed), int(self.len_min), int(self.len_max), float(self.p_planted),
+                          float(self.p_minus_site), float(self.p_backsplice), float(self.mut_rate),
+                          float(self.n_rate), float(self.p_clip), int(self.span_min), int(self.span_max))
+
+
+# ---------------------------------------------------------------------------
+# batches
+# ---------------------------------------------------------------------------
+class PairBatch:
+    """A batch of anchor pairs resident in device memory (layout: include/fc2_bp.h)."""
+
+    def __init__(self):
+        self.n = 0
+        self.stride = 0
+        self.rw = self.nw = self.tw = 1
+        self.max_l = 0
+        self.device = None
+        self.pairs = None          # torch uint8 [n*16]
+        self.read_words = None     # torch int64 [rw*stride]
+        self.read_nwords = None    # torch int64 [nw*stride]
+        self.host_pairs: Optional[np.ndarray] = None   # PAIR_DTYPE [n]
+        self.truth = None          # synthetic only: torch int32 [2n]
+        self.m_bytepath = 0
+        self.bp_index = self.bp_pairs = self.bp_arena = self.bp_off = None
+        self.options: Optional[Options] = None
+
+    # -------------------------------------------------------------- from reads
+    @classmethod
+    def pack(cls, options: Options, genome: Genome, reads, a_pos, b_aend, chrom, flags,
+             device=None, n_threads: int = 0) -> "PairBatch":
+        """Pack anchor pairs (``read_part`` bytes + JunctionSpan fields) and upload them.
+
+        ``reads``: list of ``bytes`` (``JunctionSpan.read_part``, find_circ.py:844) or a
+        ``(buffer uint8, offsets uint64, lengths)`` triple.  ``flags``: PAIR_* bits
+        (BACKSPLICE, PRIMARY_REV, SKIP).
+        """
+        torch = _torch()
+        dev = torch.device(device) if device is not None else genome.device
+        p = options.params()
+        if isinstance(reads, tuple):
+            buf, off, lens = reads
+            buf = np.ascontiguousarray(buf, np.uint8)
+            off = np.ascontiguousarray(off, np.uint64)
+            lens = np.ascontiguousarray(lens, np.int64)
+        else:
+            lens = np.fromiter((len(r) for r in reads), np.int64, len(reads))
+            off = np.zeros(len(reads), np.uint64)
+            if len(reads):
+                off[1:] = np.cumsum(lens[:-1]).astype(np.uint64)
+            buf = np.frombuffer(b"".join(reads) + b"\0" * 16, np.uint8)
+        n = len(lens)
+        if n and lens.max() > 65535:
+            raise ValueError("read_part longer than 65535 bases")
+        hp = np.zeros(n, N.PAIR_DTYPE)
+        hp["a_pos"] = np.asarray(a_pos, np.int64)
+        hp["b_aend"] = np.asarray(b_aend, np.int64)
+        hp["chrom"] = np.asarray(chrom, np.int64).astype(np.uint32)
+        hp["read_len"] = lens
+        hp["flags"] = np.asarray(flags, np.uint8)
+        max_len = int(lens.max()) if n else 0
+        rw, nw, tw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(N.lib().fc2_batch_geometry(ctypes.byref(p), max_len, ctypes.byref(rw), ctypes.byref(nw),
+                                           ctypes.byref(tw)))
+        b = cls()
+        b.options = options
+        b.n, b.stride = n, max(n, 1)
+        b.rw, b.nw, b.tw = rw.value, nw.value, tw.value
+        words = np.zeros(b.rw * b.stride, np.uint64)
+        nwords = np.zeros(b.nw * b.stride, np.uint64)
+        nbp = ctypes.c_uint64()
+        N.check(N.lib().fc2_pack_pairs(ctypes.byref(p), genome.fasta if not genome.dummy else None, n,
+                                       buf.ctypes.data, off.ctypes.data, hp.ctypes.data, words.ctypes.data, b.rw,
+                                       nwords.ctypes.data, b.nw, b.stride, ctypes.byref(nbp), int(n_threads)))
+        fast = (hp["flags"] & (N.PAIR_BYTEPATH | N.PAIR_SKIP)) == 0
+        ls = hp["read_len"].astype(np.int64) - 2 * options.eff_a
+        b.max_l = int(max(0, ls[fast].max())) if fast.any() else 0
+        b.host_pairs = hp
+        b.device = dev
+        b.pairs = torch.from_numpy(hp.view(np.uint8)).to(dev)
+        b.read_words = torch.from_numpy(words.view(np.int64)).to(dev)
+        b.read_nwords = torch.from_numpy(nwords.view(np.int64)).to(dev)
+        b.m_bytepath = int(nbp.value)
+        if b.m_bytepath and genome.fasta is None and not genome.dummy:
+            raise RuntimeError("%d pairs need byte-exact windows, which come from a FASTA-backed genome"
+                               % b.m_bytepath)
+        if b.m_bytepath:
+            b._pack_bytepath(p, genome, buf, off)
+        return b
+
+    def _pack_bytepath(self, p, genome, buf, off):
+        torch = _torch()
+        m, nbytes = ctypes.c_uint64(), ctypes.c_uint64()
+        hp = self.host_pairs
+        N.check(N.lib().fc2_bytepath_size(ctypes.byref(p), self.n, hp.ctypes.data, ctypes.byref(m),
+                                          ctypes.byref(nbytes)))
+        m = int(m.value)
+        idx = np.zeros(m, np.uint64)
+        bpairs = np.zeros(m, N.PAIR_DTYPE)
+        offs = np.zeros(m, np.uint64)
+        arena = np.zeros(max(16, int(nbytes.value)), np.uint8)
+        N.check(N.lib().fc2_bytepath_fill(ctypes.byref(p), genome.fasta if not genome.dummy else None, self.n,
+                                          buf.ctypes.data, off.ctypes.data, hp.ctypes.data, idx.ctypes.data,
+                                          bpairs.ctypes.data, offs.ctypes.data, arena.ctypes.data))
+        dev = self.device
+        self.bp_index = torch.from_numpy(idx.view(np.int64)).to(dev)
+        self.bp_pairs = torch.from_numpy(bpairs.view(np.uint8)).to(dev)
+        self.bp_off = torch.from_numpy(offs.view(np.int64)).to(dev)
+        self.bp_arena = torch.from_numpy(arena).to(dev)
+
+    # -------------------------------------------------------------- synthetic
+    @classmethod
+    def synthetic(cls, options: Options, genome: Genome, n: int, cfg: SynthConfig = None,
+                  with_truth: bool = False) -> "PairBatch":
+        """Generate ``n`` pairs on the device from ``genome`` (see fc2_synth_pairs_launch)."""
+        torch = _torch()
+        cfg = cfg or SynthConfig()
+        p = options.params()
+        rw, nw, tw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(N.lib().fc2_batch_geometry(ctypes.byref(p), int(cfg.len_max), ctypes.byref(rw), ctypes.byref(nw),
+                                           ctypes.byref(tw)))
+        if cfg.len_max - 2 * options.eff_a > N.lib().fc2_max_fast_l():
+            raise ValueError("synthetic reads longer than the register kernel supports")
+        b = cls()
+        b.options = options
+        b.n, b.stride = n, max(n, 1)
+        b.rw, b.nw, b.tw = rw.value, nw.value, tw.value
+        b.max_l = max(0, cfg.len_max - 2 * options.eff_a)
+        dev = genome.device
+        b.device = dev
+        b.pairs = torch.empty(16 * b.stride, dtype=torch.uint8, device=dev)
+        b.read_words = torch.empty(b.rw * b.stride, dtype=torch.int64, device=dev)
+        b.read_nwords = torch.empty(b.nw * b.stride, dtype=torch.int64, device=dev)
+        if with_truth:
+            b.truth = torch.empty(2 * b.stride, dtype=torch.int32, device=dev)
+        cum = np.zeros(len(genome.names) + 1, np.int64)
+        cum[1:] = np.cumsum(genome.sizes)
+        d_cum = torch.from_numpy(cum).to(dev)
+        gv = genome.view()
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        N.check(N.lib().fc2_synth_pairs_launch(ctypes.byref(p), ctypes.byref(cfg.cfg()), ctypes.byref(gv),
+                                               d_cum.data_ptr(), n, b.pairs.data_ptr(), b.read_words.data_ptr(),
+                                               b.rw, b.read_nwords.data_ptr(), b.nw, b.stride,
+                                               b.truth.data_ptr() if with_truth else None, stream))
+        torch.cuda.synchronize(dev)
+        b.host_pairs = None   # fetched lazily
+        return b
+
+    def fetch_host_pairs(self) -> np.ndarray:
+        if self.host_pairs is None:
+            self.host_pairs = self.pairs[:16 * self.n].cpu().numpy().view(N.PAIR_DTYPE).copy()
+        return self.host_pairs
+
+    def view(self) -> N.BatchView:
+        return N.BatchView(self.pairs.data_ptr(), self.read_words.data_ptr(), self.read_nwords.data_ptr(),
+                           self.n, self.stride, self.rw, self.nw, self.max_l, 0)
+
+    def bytes_view(self) -> N.BytesView:
+        return N.BytesView(self.bp_index.data_ptr(), self.bp_pairs.data_ptr(), self.bp_arena.data_ptr(),
+                           self.bp_off.data_ptr(), self.m_bytepath)
+
+
+# ---------------------------------------------------------------------------
+# scan
+# ---------------------------------------------------------------------------
+class ScanOutput:
+    def __init__(self, results, tiemask, tw, stride):
+        self.results = results      # torch int64 [stride] (fc2_result)
+        self.tiemask = tiemask      # torch int64 [tw*stride] or None
+        self.tw = tw
+        self.stride = stride
+
+    def host(self, n: int) -> np.ndarray:
+        return self.results[:n].cpu().numpy().view(N.RESULT_DTYPE).copy()
+
+
+def scan(options: Options, genome: Genome, batch: PairBatch, out: ScanOutput = None, stream=None) -> ScanOutput:
+    """Run find_breakpoints for every pair of ``batch`` (asynchronous on ``stream``)."""
+    torch = _torch()
+    dev = batch.device
+    p = options.params()
+    if out is None:
+        res = torch.empty(batch.stride, dtype=torch.int64, device=dev)
+        tm = torch.zeros(batch.tw * batch.stride, dtype=torch.int64, device=dev) if options.allhits else None
+        out = ScanOutput(res, tm, batch.tw, batch.stride)
+    s = stream if stream is not None else torch.cuda.current_stream(dev).cuda_stream
+    gv = genome.view()
+    bv = batch.view()
+    tptr = out.tiemask.data_ptr() if out.tiemask is not None else None
+    N.check(N.lib().fc2_bp_scan_launch(ctypes.byref(p), ctypes.byref(gv), ctypes.byref(bv), out.results.data_ptr(),
+                                       tptr, out.tw, s))
+    if batch.m_bytepath:
+        v = batch.bytes_view()
+        N.check(N.lib().fc2_bp_scan_bytes_launch(ctypes.byref(p), ctypes.byref(v), out.results.data_ptr(), tptr,
+                                                 out.tw, batch.stride, s))
+    return out
+
+
+# ---------------------------------------------------------------------------
+# decoding to the reference's Splice objects
+# ---------------------------------------------------------------------------
+class Splice:
+    """Mirror of ``Splice`` (find_circ.py:766-806)."""
+
+    __slots__ = ("junc_span", "chrom", "start", "end", "strand", "dist", "ov", "gtag", "n_hits", "_score")
+
+    def __init__(self, junc_span, chrom, start, end, strand, dist, ov, gtag):
+        self.junc_span = junc_span
+        self.chrom = chrom
+        self.start = start
+        self.end = end
+        self.strand = strand
+        self.dist = dist
+        self.ov = ov
+        self.gtag = gtag
+        self.n_hits = 1
+        self._score = None
+
+    @property
+    def is_canonical(self):          # find_circ.py:778-780
+        return self.gtag == 'GTAG'
+
+    @property
+    def is_backsplice(self):         # find_circ.py:782-785
+        return self.junc_span.is_backsplice
+
+    @property
+    def score(self):                 # find_circ.py:791-799 (value computed with the options of the scan)
+        return self._score
+
+    @property
+    def coord(self):                 # find_circ.py:801-806
+        if self.start < self.end:
+            return (self.chrom, self.start, self.end, self.strand)
+        return (self.chrom, self.end, self.start, self.strand)
+
+    def __repr__(self):
+        return "Splice(%s:%d-%d:%s edits=%s ov=%d gtag=%s n_hits=%d)" % (
+            self.chrom, self.start, self.end, self.strand, self.dist, self.ov, self.gtag, self.n_hits)
+
+
+class BreakpointError(RuntimeError):
+    pass
+
+
+def first_tie_arrays(options: Options, host_pairs: np.ndarray, res: np.ndarray):
+    """Vectorised decode of ties[0] for every pair -> dict of numpy arrays.
+
+    start/end follow find_circ.py:929-945; ``gtag`` is the Splice's signal
+    (rev_comp for '-' hits, find_circ.py:949/954).
+    """
+    e = options.eff_a
+    L = host_pairs["read_len"].astype(np.int64)
+    l = L - 2 * e
+    x = res["best_x"].astype(np.int64)
+    s0 = host_pairs["b_aend"].astype(np.int64) - e - l + x
+    e0 = host_pairs["a_pos"].astype(np.int64) + e + x + 1
+    start = np.minimum(s0, e0)
+    end = np.maximum(s0, e0)
+    bs = (host_pairs["flags"] & N.PAIR_BACKSPLICE) != 0
+    end = np.where(bs, end - 1, end)
+    start = np.where(bs, start, start - 1)
+    info = res["info"].astype(np.int64)
+    return dict(hit=x >= 0, x=x, start=start, end=end, minus=(info & N.RES_MINUS) != 0,
+                dist=res["dist"].astype(np.int64), ov=res["ov"].astype(np.int64),
+                n_ties=res["n_ties"].astype(np.int64), gtag12=(info & N.RES_GTAG_MASK) >> N.RES_GTAG_SHIFT,
+                err_key=(info & N.RES_ERR_KEY) != 0, err_win=(info & N.RES_ERR_WIN) != 0,
+                done=(info & N.RES_DONE) != 0)
+
+
+def gtag_str(gtag12: int) -> str:
+    return "".join(_CODE[(gtag12 >> (3 * k)) & 7] for k in range(4))
+
+
+def raise_reference_errors(options: Options, host_pairs: np.ndarray, res: np.ndarray, evaluated=None):
+    """Re-raise what the reference would raise for the first failing evaluated pair."""
+    info = res["info"]
+    bad = (info & (N.RES_ERR_KEY | N.RES_ERR_WIN)) != 0
+    if evaluated is not None:
+        bad &= evaluated
+    if not bad.any():
+        return
+    i = int(np.nonzero(bad)[0][0])
+    if info[i] & N.RES_ERR_KEY:
+        raise KeyError("pair %d: splice signal with a byte outside ACGTN (reference KeyError in fast_4mer_RC, "
+                       "find_circ.py:927)" % i)
+    raise BreakpointError("pair %d: genome window outside the range where indexed_fasta.get_data is defined "
+                          "(find_circ.py:194-211)" % i)
+
+
+def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: ScanOutput,
+                   spans: Sequence = None) -> List[List[Splice]]:
+    """Per pair, the list ``find_breakpoints`` returns (ties, find_circ.py:961-974)."""
+    hp = batch.fetch_host_pairs()
+    res = out.host(batch.n)
+    evaluated = (hp["flags"] & N.PAIR_SKIP) == 0
+    raise_reference_errors(options, hp, res, evaluated)
+    a = first_tie_arrays(options, hp, res)
+    e = options.eff_a
+    tm = None
+    if options.allhits:
+        tm = out.tiemask[:batch.tw * batch.stride].cpu().numpy().view(np.uint64).reshape(batch.tw, batch.stride)
+    result: List[List[Splice]] = []
+    for i in range(batch.n):
+        span = spans[i] if spans is not None else None
+        if not a["hit"][i] or not evaluated[i]:
+            result.append([])
+            continue
+        chrom = genome.names[hp["chrom"][i]] if not genome.dummy else (span.chrom if span is not None else "")
+        g = gtag_str(int(a["gtag12"][i]))
+        strand = '-' if a["minus"][i] else '+'
+        sig = rev_comp4(g) if strand == '-' else g
+        dist = int(a["dist"][i])
+        dist_v = False if options.maxdist == 0 else dist     # simple_match returns a bool (find_circ.py:865-871)
+        s = Splice(span, chrom, int(a["start"][i]), int(a["end"][i]), strand, dist_v, int(a["ov"][i]), sig)
+        nt = int(a["n_ties"][i])
+        s.n_hits = nt
+        s._score = _score(options, sig, dist, s.ov, strand, hp["flags"][i])
+        ties = [s]
+        if options.allhits and nt > 1:
+            ties = _expand_ties(options, genome, hp, i, tm, s, span, chrom)
+        result.append(ties)
+    return result
+
+
+def _score(options, sig, dist, ov, strand, flags):
+    sc = (sig == 'GTAG') * 20 - dist * 10 - ov
+    if options.strandpref:
+        prim = '-' if flags & N.PAIR_PRIMARY_REV else '+'
+        sc += 100 * (strand == prim)
+    return sc
+
+
+def _expand_ties(options, genome, hp, i, tm, best: Splice, span, chrom):
+    """All ties of pair i in (x asc, '+' before '-') order from the tie mask."""
+    e = options.eff_a
+    L = int(hp["read_len"][i])
+    l = L - 2 * e
+    half = tm.shape[0] // 2
+    out = []
+    for x in range(l + 1):
+        k, b = x >> 6, x & 63
+        for strand, row in (('+', k), ('-', half + k)):
+            if not (int(tm[row, i]) >> b) & 1:
+                continue
+            s0 = int(hp["b_aend"][i]) - e - l + x
+            e0 = int(hp["a_pos"][i]) + e + x + 1
+            st, en = min(s0, e0), max(s0, e0)
+            if hp["flags"][i] & N.PAIR_BACKSPLICE:
+                en -= 1
+            else:
+                st -= 1
+            ov = 0
+            if options.margin:
+                if x < options.margin:
+                    ov = options.margin - x
+                if l - x < options.margin:
+                    ov = options.margin - (l - x)
+            if options.noncanonical:
+                g = _window_gtag(genome, hp, i, x, e, l)
+                sig = g if strand == '+' else rev_comp4(g)
+            else:
+                sig = 'GTAG'
+            canon = 20 * (sig == 'GTAG')
+            sp = 0
+            if options.strandpref:
+                prim = '-' if hp["flags"][i] & N.PAIR_PRIMARY_REV else '+'
+                sp = 100 * (strand == prim)
+            dist = (canon - ov + sp - best.score) // 10
+            s = Splice(span, chrom, st, en, strand, False if options.maxdist == 0 else dist, ov, sig)
+            s.n_hits = best.n_hits
+            s._score = best.score
+            out.append(s)
+    return out
+
+
+def _window_gtag(genome: Genome, hp, i, x, e, l) -> str:
+    c = int(hp["chrom"][i])
+    a0 = int(hp["a_pos"][i]) + e + x
+    b0 = int(hp["b_aend"][i]) - e - (l + 2) + x
+    if genome.dummy:
+        return "NNNN"
+    A = genome.get_upper(c, a0, a0 + 2)
+    B = genome.get_upper(c, b0, b0 + 2)
+    return (A + B).decode("latin-1")
+
+
+# ---------------------------------------------------------------------------
+# drop-in mirror of the reference objects
+# ---------------------------------------------------------------------------
+def uniqness(align) -> int:
+    """AS - XS (find_circ.py:809-819)."""
+    u = align.get_tag('AS')
+    if align.has_tag('XS'):
+        u -= align.get_tag('XS')
+    return u
+
+
+class JunctionSpan:
+    """Mirror of ``JunctionSpan`` (find_circ.py:821-852).
+
+    ``align_A``/``align_B``/``primary`` are pysam-like records (``.pos``,
+    ``.aend``, ``.seq``, ``.is_reverse``, ``get_tag``/``has_tag``); ``chrom`` is
+    the reference name of ``align_A`` (``fast_chrom_lookup``, find_circ.py:471-477).
+    """
+
+    engine = None   # set by BreakpointEngine.install() (the reference uses globals)
+
+    def __init__(self, align_A, align_B, primary, q_start, q_end, weight, chrom=None):
+        self.primary = primary
+        self.align_A = align_A
+        self.align_B = align_B
+        self.q_start = q_start
+        self.q_end = q_end
+        self.weight = weight
+        self.uniq_A = uniqness(align_A)
+        self.uniq_B = uniqness(align_B)
+        self.uniq = min(self.uniq_A, self.uniq_B)
+        self.strand = '-' if primary.is_reverse else '+'
+        self.dist = align_B.pos - align_A.aend
+        self.read_part = primary.seq[q_start:q_end]
+        self.chrom = chrom
+
+    def is_uniq_for(self, min_uniq_qual: int) -> bool:        # find_circ.py:846-848
+        return self.uniq >= min_uniq_qual
+
+    @property
+    def is_backsplice(self):                                  # find_circ.py:850-852
+        return self.dist < 0
+
+    def find_breakpoints(self):                               # find_circ.py:854
+        if JunctionSpan.engine is None:
+            raise RuntimeError("no BreakpointEngine installed (BreakpointEngine(...).install())")
+        return JunctionSpan.engine.find_breakpoints_batch([self])[0]
+
+
+class BreakpointEngine:
+    """Genome + options + device: evaluates lists of JunctionSpans in one launch."""
+
+    def __init__(self, genome: Genome, options: Options):
+        self.genome = genome
+        self.options = options
+
+    def install(self):
+        JunctionSpan.engine = self
+        return self
+
+    def find_breakpoints_batch(self, spans: Sequence[JunctionSpan]) -> List[List[Splice]]:
+        if not spans:
+            return []
+        reads = []
+        for s in spans:
+            r = s.read_part
+            reads.append(r if isinstance(r, bytes) else r.encode("latin-1"))
+        chrom = [self.genome.chrom_index_or_missing(s.chrom) for s in spans]
+        flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.strand == '-' else 0)
+                 for s in spans]
+        b = PairBatch.pack(self.options, self.genome, reads, [s.align_A.pos for s in spans],
+                           [s.align_B.aend for s in spans], chrom, flags)
+        out = scan(self.options, self.genome, b)
+        return decode_splices(self.options, self.genome, b, out, spans)

@@ -1,0 +1,267 @@
+/*
+ * fc2_bp.h -- C ABI of the MI355X breakpoint-search library (libfc2.so).
+ *
+ * Drop-in boundary for ONE hot path of find_circ2 (find_circ.py 1.99):
+ *
+ *   JunctionSpan.find_breakpoints(self) -> [Splice]   find_circ.py:854-974
+ *     + its genome window fetch  Track.get -> GenomeAccessor.get_data ->
+ *       indexed_fasta.get_data                         find_circ.py:310-312, 362-368, 189-215
+ *
+ * The reference has no FFI: the path is a Python method called from
+ * record_hits (find_circ.py:1303 circ spans, 1355 linear spans).  This header
+ * is what a ctypes binding of that method binds; the
+ * Python host layer find_circ2_amd/hotpath.py mirrors the method itself.
+ *
+ * Conventions
+ *  - plain C types, no torch types; every function returns an int status
+ *    (FC2_OK = 0, negative = error class) and never throws;
+ *    fc2_last_error() gives the message of the last failure on this thread.
+ *  - device pointers are HIP device pointers owned by the caller (the Python
+ *    layer allocates them as torch tensors); `stream` is a hipStream_t.
+ *    fc2_*_launch functions are asynchronous on that stream.
+ *  - host pointers are ordinary host memory owned by the caller.
+ *  - reference errors that are fatal in find_circ.py (KeyError at :927 and
+ *    :193, undefined windows at :194-211) are reported per pair in
+ *    fc2_result.info, never silently dropped.
+ */
+#ifndef FC2_BP_H
+#define FC2_BP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FC2_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define FC2_OK        0
+#define FC2_E_PARAM  -1   /* invalid argument / unsupported option value          */
+#define FC2_E_HIP    -2   /* HIP runtime error (message via fc2_last_error)       */
+#define FC2_E_FORMAT -3   /* malformed FASTA / index                               */
+#define FC2_E_RANGE  -4   /* value outside the supported range                     */
+#define FC2_E_IO     -5   /* file could not be opened / mapped                     */
+#define FC2_E_KEY    -6   /* unknown chromosome (reference KeyError, find_circ.py:193) */
+
+/* ---- options the hot path reads (find_circ.py:393-404) ----------------- */
+typedef struct fc2_params {
+    int32_t asize;        /* -a/--anchor      (default 15)  find_circ.py:394 */
+    int32_t margin;       /* -m/--margin      (default 2)   find_circ.py:395 */
+    int32_t maxdist;      /* -d/--max-mismatch(default 2)   find_circ.py:396 */
+    uint8_t noncanonical; /* --non-canonical                find_circ.py:401 */
+    uint8_t strandpref;   /* --strand-pref                  find_circ.py:404 */
+    uint8_t allhits;      /* --all-hits                     find_circ.py:402 */
+    uint8_t _pad;
+} fc2_params;
+
+/* ---- one anchor pair (a JunctionSpan, find_circ.py:821-852), 16 bytes ---- */
+#define FC2_PAIR_BACKSPLICE  0x01u  /* align_B.pos - align_A.aend < 0   (:842, :851) */
+#define FC2_PAIR_PRIMARY_REV 0x02u  /* primary.is_reverse -> span strand '-' (:834) */
+#define FC2_PAIR_READ_N      0x04u  /* internal read part has 'N' bytes: N plane present */
+#define FC2_PAIR_BYTEPATH    0x08u  /* evaluated by the byte-exact kernel (exotic bytes,
+                                       irregular FASTA line layout, very long reads) */
+#define FC2_PAIR_SKIP        0x10u  /* not evaluated (e.g. not is_uniq, :1299): no hit */
+
+typedef struct fc2_pair {
+    int32_t  a_pos;     /* align_A.pos  (0-based)                                    */
+    int32_t  b_aend;    /* align_B.aend (exclusive)                                  */
+    uint32_t chrom;     /* index into the genome's chromosome table                  */
+    uint16_t read_len;  /* L = len(read_part)                                        */
+    uint8_t  flags;     /* FC2_PAIR_*                                                */
+    uint8_t  _pad;
+} fc2_pair;
+
+/* ---- per-pair result, 8 bytes ------------------------------------------- */
+/* best_x = breakpoint index x of ties[0] (the Splice record_hits keeps,
+ * find_circ.py:1312-1317), -1 if find_breakpoints returned [].
+ * n_ties = Splice.n_hits of the returned ties (1 if a single hit).
+ * Coordinates follow from x (find_circ.py:929-945):
+ *   s0 = b_aend - e - l + x,  e0 = a_pos + e + x + 1,  e = asize - margin,  l = L - 2e
+ *   (start, end) = (min, max); backsplice: end -= 1, else start -= 1.          */
+#define FC2_RES_MINUS       0x0001u  /* strand of ties[0] is '-'                        */
+#define FC2_RES_GTAG_SHIFT  1        /* 4 x 3-bit base codes of gtag = A[x]A[x+1]B[x]B[x+1]
+                                        (A0 C1 G2 T3 N4), first base in the lowest bits;
+                                        a '-' Splice's signal is rev_comp(gtag)           */
+#define FC2_RES_GTAG_MASK   0x1FFEu
+#define FC2_RES_ERR_KEY     0x2000u  /* reference raises KeyError (find_circ.py:927)    */
+#define FC2_RES_ERR_WIN     0x4000u  /* window outside the range where get_data is defined
+                                        (find_circ.py:194-211); reference output undefined */
+#define FC2_RES_DONE        0x8000u  /* written by a kernel                               */
+
+typedef struct fc2_result {
+    int16_t  best_x;
+    uint8_t  dist;      /* mismatches of ties[0]  (Splice.dist)  */
+    uint8_t  ov;        /* anchor overlap of ties[0] (Splice.ov) */
+    uint16_t n_ties;
+    uint16_t info;      /* FC2_RES_*                              */
+} fc2_result;
+
+/* ---- device-resident genome (2-bit bit-sliced + N plane) ---------------- */
+/* Bases of all chromosomes are concatenated, each chromosome starting at a
+ * multiple of 64.  Unit u covers global bases [64u, 64u+64):
+ *   units[2u]   : low  code bit of each base (bit b = base 64u+b)
+ *   units[2u+1] : high code bit            (A=00 C=01 G=10 T=11, N=00)
+ *   nplane[u]   : 1 where the (uppercased) base is 'N'
+ *   ncoarse     : bit k set iff any of units [16k, 16k+16) contains an N
+ * Positions outside [0, chrom_size) read as 'N' (get_data's N padding). */
+typedef struct fc2_genome_view {
+    const uint64_t *units;       /* device [2*n_units] */
+    const uint64_t *nplane;      /* device [n_units]   */
+    const uint32_t *ncoarse;     /* device [ceil(n_units/16/32)] */
+    const uint64_t *chrom_start; /* device [n_chrom] */
+    const int64_t  *chrom_size;  /* device [n_chrom] */
+    uint64_t n_units;
+    uint32_t n_chrom;
+    uint32_t dummy;              /* 1: every window is all 'N' (GenomeAccessor dummy mode, :340-345) */
+} fc2_genome_view;
+
+/* ---- a batch of anchor pairs in device memory (SoA) --------------------- */
+/* Internal read part I = upper(read_part[e:L-e]) (find_circ.py:895), l = L-2e
+ * bases, packed per pair in rw 64-bit words stored column-major
+ * (word j of pair i at read_words[j*stride + i]): low code bits at bit
+ * positions [0,l), high code bits at [l,2l).  read_nwords holds the N bits
+ * ([nw][stride], only read for FC2_PAIR_READ_N pairs). */
+typedef struct fc2_batch_view {
+    const fc2_pair *pairs;       /* device [n] */
+    const uint64_t *read_words;  /* device [rw][stride] */
+    const uint64_t *read_nwords; /* device [nw][stride] (may be NULL if no pair has READ_N) */
+    uint64_t n;
+    uint64_t stride;
+    uint32_t rw;
+    uint32_t nw;
+    int32_t  max_l;              /* largest l = L - 2e of a non-BYTEPATH pair (selects the kernel width) */
+    uint32_t _pad;
+} fc2_batch_view;
+
+/* ---- pairs that need byte-exact evaluation ------------------------------ */
+/* Block for pair k at arena[off[k]]: int32 lenI, lenA, lenB, then
+ * I (lenI bytes, uppercased internal read), A window (lenA), B window (lenB),
+ * exactly as get_data(...).upper() returns them (find_circ.py:895, 901-902). */
+typedef struct fc2_bytes_view {
+    const uint64_t *index;       /* device [m] : pair index into results/tiemask */
+    const fc2_pair *pairs;       /* device [m] */
+    const uint8_t  *arena;       /* device */
+    const uint64_t *off;         /* device [m] */
+    uint64_t m;
+} fc2_bytes_view;
+
+/* ======================================================================== */
+/* library info                                                              */
+/* ======================================================================== */
+int         fc2_abi_version(void);
+const char *fc2_last_error(void);
+/* Returns FC2_OK and the device count (0 on a host without GPUs is not an error). */
+int         fc2_device_count(int *count);
+
+/* Largest l the register kernel handles (longer reads go to the byte kernel). */
+int         fc2_max_fast_l(void);
+/* Words per pair for the chosen max l: rw (read planes), nw (read N plane),
+ * tw (all-hits tie mask: tw/2 words of '+' ties then tw/2 words of '-' ties). */
+int         fc2_batch_geometry(const fc2_params *p, int32_t max_read_len,
+                               uint32_t *rw, uint32_t *nw, uint32_t *tw);
+
+/* ======================================================================== */
+/* device kernels (asynchronous on `stream`)                                 */
+/* ======================================================================== */
+/* The hot path: JunctionSpan.find_breakpoints for every pair of the batch
+ * (pairs flagged FC2_PAIR_BYTEPATH are left for fc2_bp_scan_bytes_launch).
+ * tiemask: device [tw][stride] (required iff p->allhits). */
+int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                       fc2_result *results, uint64_t *tiemask, uint32_t tw, void *stream);
+
+/* Byte-exact evaluation of the pairs listed in v (any read length, any bytes). */
+int fc2_bp_scan_bytes_launch(const fc2_params *p, const fc2_bytes_view *v, fc2_result *results,
+                             uint64_t *tiemask, uint32_t tw, uint64_t stride, void *stream);
+
+/* ======================================================================== */
+/* host side: FASTA (indexed_fasta semantics, find_circ.py:103-215)         */
+/* ======================================================================== */
+typedef struct fc2_fasta fc2_fasta;
+
+/* Open + mmap a (multi-)FASTA.  If <path>.byo_index is readable it is used
+ * (find_circ.py:110-112); otherwise the file is indexed (:120-155) and, when
+ * write_index != 0, the index is stored atomically next to it (:157-179). */
+int  fc2_fasta_open(const char *path, int write_index, fc2_fasta **out);
+void fc2_fasta_close(fc2_fasta *f);
+int  fc2_fasta_n_chrom(const fc2_fasta *f);
+/* chrom table in index order; name buffer owned by f. */
+int  fc2_fasta_chrom(const fc2_fasta *f, int i, const char **name, int64_t *size,
+                     int64_t *ofs, int64_t *ldata, int64_t *skip, int *regular);
+int  fc2_fasta_find(const fc2_fasta *f, const char *name);   /* -1 if absent */
+/* Reference get_data(chrom, start, end, '+').upper() into out (cap bytes);
+ * *len = produced length (= end-start inside the defined range). */
+int  fc2_fasta_get_upper(const fc2_fasta *f, int chrom, int64_t start, int64_t end,
+                         uint8_t *out, int64_t cap, int64_t *len);
+/* Device genome layout for this FASTA. */
+int  fc2_fasta_layout(const fc2_fasta *f, uint64_t *n_units, uint64_t *n_coarse_words,
+                      uint64_t *chrom_start /* [n_chrom] or NULL */);
+/* Pack into host buffers sized by fc2_fasta_layout (units [2*n_units],
+ * nplane [n_units], ncoarse [n_coarse_words]); *n_exotic = number of bases
+ * that are neither ACGT nor N after uppercasing (they are stored as N and
+ * pairs touching them take the byte path).  n_threads <= 0: all cores. */
+int  fc2_fasta_pack(const fc2_fasta *f, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,
+                    uint64_t *n_exotic, int n_threads);
+
+/* ======================================================================== */
+/* host side: pair packing                                                   */
+/* ======================================================================== */
+/* Pack n anchor pairs into the device SoA layout (host buffers).
+ * reads/read_off/read_len: the read_part strings (find_circ.py:844).
+ * pairs_io: in = a_pos, b_aend, chrom, read_len, flags (BACKSPLICE,
+ * PRIMARY_REV, SKIP); out = READ_N / BYTEPATH set as needed.
+ * f (may be NULL = dummy genome) is used to route pairs whose windows touch
+ * exotic genome bytes or irregular FASTA layout, or fall outside the defined
+ * window range, to the byte path.  *n_bytepath = number of such pairs. */
+int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t n,
+                   const uint8_t *reads, const uint64_t *read_off,
+                   fc2_pair *pairs_io, uint64_t *read_words, uint32_t rw,
+                   uint64_t *read_nwords, uint32_t nw, uint64_t stride,
+                   uint64_t *n_bytepath, int n_threads);
+
+/* Size (bytes) of the byte-path arena for the pairs flagged BYTEPATH. */
+int fc2_bytepath_size(const fc2_params *p, uint64_t n, const fc2_pair *pairs, uint64_t *m,
+                      uint64_t *arena_bytes);
+/* Fill index/pairs/off/arena (host) for the BYTEPATH pairs; windows come
+ * from f with the reference's get_data semantics (dummy genome if f == NULL). */
+int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64_t n,
+                      const uint8_t *reads, const uint64_t *read_off, const fc2_pair *pairs,
+                      uint64_t *index, fc2_pair *bpairs, uint64_t *off, uint8_t *arena);
+
+/* ======================================================================== */
+/* synthetic workloads (cf. simulate_reads.py)              */
+/* ======================================================================== */
+typedef struct fc2_synth_cfg {
+    uint64_t seed;
+    int32_t  len_min, len_max;     /* read length L range                   */
+    float    p_planted;            /* junction at a GT..AG / CT..AC site     */
+    float    p_minus_site;         /* of planted: CT..AC instead of GT..AG   */
+    float    p_backsplice;         /* backsplice vs linear                   */
+    float    mut_rate;             /* per-base substitution rate             */
+    float    n_rate;               /* per-base N rate in reads               */
+    float    p_clip;               /* clip 0..3 bases off each read end      */
+    int32_t  span_min, span_max;   /* exon (circ) / intron (linear) span     */
+} fc2_synth_cfg;
+
+/* Fill a synthetic genome on the device: random bases from a counter-based
+ * hash of (seed, unit), 'N' over the given sorted, non-overlapping global
+ * base intervals [n_lo[k], n_hi[k]) (device arrays), coarse map rebuilt. */
+int fc2_synth_genome_launch(uint64_t seed, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,
+                            uint64_t n_units, const int64_t *n_lo, const int64_t *n_hi,
+                            uint32_t n_intervals, void *stream);
+/* Rebuild the coarse N map from nplane (device). */
+int fc2_coarse_launch(const uint64_t *nplane, uint32_t *ncoarse, uint64_t n_units, void *stream);
+
+/* Generate n anchor pairs from the device genome, packed for fc2_bp_scan_launch.
+ * chrom_cum: device [n_chrom+1] cumulative chrom sizes used to draw loci.
+ * truth (optional, device [2n] int32): planted junction (start, end). */
+int fc2_synth_pairs_launch(const fc2_params *p, const fc2_synth_cfg *cfg, const fc2_genome_view *g,
+                           const int64_t *chrom_cum, uint64_t n, fc2_pair *pairs,
+                           uint64_t *read_words, uint32_t rw, uint64_t *read_nwords, uint32_t nw,
+                           uint64_t stride, int32_t *truth, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FC2_BP_H */

@@ -105,7 +105,10 @@ class OracleFasta:
         cap = max(0, end - start) + 64
         out = np.zeros(cap, dtype=np.uint8)
         k = lib().orc_get_upper(self.h, chrom, start, end, out.ctypes.data, cap)
-        return bytes(out[:min(k, cap)])
+        if k > cap:   # outside get_data's defined range the slice can wrap (Python slice semantics)
+            out = np.zeros(k, dtype=np.uint8)
+            k = lib().orc_get_upper(self.h, chrom, start, end, out.ctypes.data, k)
+        return bytes(out[:k])
 
 
 def _ptr(a):

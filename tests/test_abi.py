@@ -1,0 +1,301 @@
+"""CPU tests of the C ABI library (no GPU needed): load, exports, host-side FASTA
+semantics vs the oracle, genome/pair packing round trips, byte-path arena."""
+import ctypes
+import os
+import re
+import shutil
+
+import numpy as np
+import pytest
+
+import oracle
+from conftest import GOLDEN, ROOT
+from find_circ2_amd import _native as N
+from oracle.bp_oracle import RefIndexedFasta
+from planes import decode_genome, decode_read
+from synth_small import load_genome, make_spans
+
+
+@pytest.fixture(scope="module")
+def L():
+    N.build()
+    return N.lib()
+
+
+def test_exports_every_declared_symbol(L):
+    hdr = open(os.path.join(ROOT, "include", "fc2_bp.h")).read()
+    declared = set(re.findall(r"\b(fc2_[a-z0-9_]+)\s*\(", hdr))
+    assert declared, "no declarations parsed"
+    assert declared == set(N.EXPORTED), declared ^ set(N.EXPORTED)
+    for name in declared:
+        assert hasattr(L, name), name
+
+
+def test_info_calls(L):
+    assert L.fc2_abi_version() == 1
+    c = ctypes.c_int(-1)
+    assert L.fc2_device_count(ctypes.byref(c)) == 0 and c.value >= 0
+    assert L.fc2_max_fast_l() == 510
+    p = N.Params(15, 2, 2, 0, 0, 0, 0)
+    rw, nw, tw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    assert L.fc2_batch_geometry(ctypes.byref(p), 100, ctypes.byref(rw), ctypes.byref(nw), ctypes.byref(tw)) == 0
+    assert (rw.value, nw.value, tw.value) == (3, 2, 4)      # l=74: 148 bits, 74 bits, 75 x-bits
+    assert L.fc2_batch_geometry(ctypes.byref(p), 150, ctypes.byref(rw), ctypes.byref(nw), ctypes.byref(tw)) == 0
+    assert (rw.value, nw.value, tw.value) == (4, 2, 4)      # l=124
+    bad = N.Params(2, 2, 2, 0, 0, 0, 0)
+    assert L.fc2_batch_geometry(ctypes.byref(bad), 100, None, None, None) == N.FC2_E_PARAM
+    assert b"asize - margin" in L.fc2_last_error()
+
+
+def _open(path, write_index=0):
+    h = ctypes.c_void_p()
+    rc = N.lib().fc2_fasta_open(path.encode(), write_index, ctypes.byref(h))
+    return rc, h
+
+
+def _chroms(h):
+    L = N.lib()
+    out = []
+    for i in range(L.fc2_fasta_n_chrom(h)):
+        nm, sz, of, ld, sk, rg = (ctypes.c_char_p(), ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64(),
+                                  ctypes.c_int64(), ctypes.c_int())
+        assert L.fc2_fasta_chrom(h, i, ctypes.byref(nm), ctypes.byref(sz), ctypes.byref(of), ctypes.byref(ld),
+                                 ctypes.byref(sk), ctypes.byref(rg)) == 0
+        out.append((nm.value.decode(), of.value, ld.value, sk.value, sz.value, rg.value))
+    return out
+
+
+def _pack(h):
+    L = N.lib()
+    nu, ncw = ctypes.c_uint64(), ctypes.c_uint64()
+    n = L.fc2_fasta_n_chrom(h)
+    cs = np.zeros(max(1, n), np.uint64)
+    assert L.fc2_fasta_layout(h, ctypes.byref(nu), ctypes.byref(ncw), cs.ctypes.data) == 0
+    units = np.zeros(2 * nu.value, np.uint64)
+    npl = np.zeros(nu.value, np.uint64)
+    nco = np.zeros(max(1, ncw.value), np.uint32)
+    ne = ctypes.c_uint64()
+    assert L.fc2_fasta_pack(h, units.ctypes.data, npl.ctypes.data, nco.ctypes.data, ctypes.byref(ne), 2) == 0
+    return units, npl, nco, cs, ne.value
+
+
+WEIRD_FASTA = (b">c1 some description\n"
+               b"ACGTNacgtn\nRYKMacgtAC\nGT\n"
+               b">c2\n"
+               b"AAAAACCCCC\r\nGGGGGTTTTT\r\nNNNNNACGTA\r\nAC\r\n"
+               b">c3\n"
+               b"ACGTACGTAC\nACG\nTACGTAC\n"          # irregular: short middle line
+               b">c4\n"
+               b"acgtacgtacgtacgtacgtacgtacgtacgtacgtacgtacgtacgtacgtacgtacgtacgtacgtacgt")  # no newline
+
+
+@pytest.mark.parametrize("fa", ["CDR1as_locus.fa", "test_ref.fa", "weird"])
+def test_fasta_index_and_get_match_oracle(L, fa, tmp_path):
+    if fa == "weird":
+        path = str(tmp_path / "weird.fa")
+        open(path, "wb").write(WEIRD_FASTA)
+    else:
+        path = str(tmp_path / fa)
+        shutil.copy(os.path.join(GOLDEN, fa), path)
+    rc, h = _open(path)
+    assert rc == 0, L.fc2_last_error()
+    ref = RefIndexedFasta(path)
+    of = oracle.OracleFasta(path)
+    got = _chroms(h)
+    assert [g[0] for g in got] == of.names
+    for name, ofs, ldata, skip, size, _ in got:
+        r = ref.chrom_stats[name]
+        assert (ofs, ldata, skip, size) == (r[0], r[1], r[2], r[4]), name
+    rng = np.random.default_rng(7)
+    buf = np.zeros(400, np.uint8)
+    ln = ctypes.c_int64()
+    for ci, (name, _, _, _, size, _) in enumerate(got):
+        for _ in range(200):
+            s = int(rng.integers(-30, size + 30))
+            e = s + int(rng.integers(0, 90))
+            assert L.fc2_fasta_get_upper(h, ci, s, e, buf.ctypes.data, 400, ctypes.byref(ln)) == 0
+            mine = bytes(buf[:ln.value])
+            assert mine == ref.get_data(name, s, e).upper(), (name, s, e)
+            assert mine == of.get_upper(ci, s, e)
+    L.fc2_fasta_close(h)
+
+
+def test_index_file_roundtrip(L, tmp_path):
+    path = str(tmp_path / "t.fa")
+    open(path, "wb").write(WEIRD_FASTA)
+    rc, h = _open(path, write_index=1)
+    assert rc == 0
+    L.fc2_fasta_close(h)
+    written = open(path + ".byo_index").read()
+    assert written == RefIndexedFasta(path).index_text()
+    # a present index is used as is (find_circ.py:110-112)
+    rc, h2 = _open(path)
+    assert rc == 0
+    ref = RefIndexedFasta(path)
+    for name, ofs, ldata, skip, size, _ in _chroms(h2):
+        r = ref.chrom_stats[name]
+        assert (ofs, ldata, skip, size) == (r[0], r[1], r[2], r[4])
+    L.fc2_fasta_close(h2)
+
+
+def test_malformed_fasta_errors(L, tmp_path):
+    p = str(tmp_path / "dup.fa")
+    open(p, "wb").write(b">a\nACGT\n>a\nACGT\n")
+    rc, h = _open(p)
+    assert rc == N.FC2_E_FORMAT
+    p = str(tmp_path / "empty.fa")
+    open(p, "wb").write(b">a\n>b\nACGT\n")
+    rc, h = _open(p)
+    assert rc == 0          # header without sequence before a header with none pending is fine
+    rc, h = _open(str(tmp_path / "missing.fa"))
+    assert rc == N.FC2_E_IO
+
+
+@pytest.mark.parametrize("fa", ["CDR1as_locus.fa", "test_ref.fa", "weird"])
+def test_genome_pack_roundtrip(L, fa, tmp_path):
+    if fa == "weird":
+        path = str(tmp_path / "weird.fa")
+        open(path, "wb").write(WEIRD_FASTA)
+    else:
+        path = os.path.join(GOLDEN, fa)
+    rc, h = _open(path)
+    assert rc == 0
+    units, npl, nco, cs, n_exo = _pack(h)
+    ref = RefIndexedFasta(path)
+    chroms = _chroms(h)
+    exo_expected = 0
+    for ci, (name, _, _, _, size, regular) in enumerate(chroms):
+        want = ref.get_data(name, 0, size).upper()
+        if regular == 1:
+            got = decode_genome(units, npl, int(cs[ci]), size)
+            exp = bytes(c if c in b"ACGTN" else ord('N') for c in want)
+            assert got == exp, name
+            exo_expected += sum(c not in b"ACGTN" for c in want)
+        else:
+            assert name == "c3"
+            assert decode_genome(units, npl, int(cs[ci]), size) == b"N" * size
+    assert n_exo == exo_expected
+    # coarse map consistent with the N plane
+    for blk in range((len(npl) + 15) // 16):
+        anyn = bool(np.bitwise_or.reduce(npl[blk * 16:blk * 16 + 16]))
+        assert bool((nco[blk >> 5] >> (blk & 31)) & 1) == anyn
+    L.fc2_fasta_close(h)
+
+
+def _pack_pairs(L, p, h, spans, chrom_idx):
+    reads = [s.read_part for s in spans]
+    lens = np.array([len(r) for r in reads], np.int64)
+    off = np.zeros(len(reads), np.uint64)
+    off[1:] = np.cumsum(lens[:-1])
+    buf = np.frombuffer(b"".join(reads) + b"\0" * 16, np.uint8)
+    hp = np.zeros(len(spans), N.PAIR_DTYPE)
+    hp["a_pos"] = [s.a_pos for s in spans]
+    hp["b_aend"] = [s.b_aend for s in spans]
+    hp["chrom"] = chrom_idx
+    hp["read_len"] = lens
+    hp["flags"] = [(1 if s.is_backsplice else 0) | (2 if s.primary_reverse else 0) for s in spans]
+    rw, nw, tw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+    assert L.fc2_batch_geometry(ctypes.byref(p), int(lens.max()), ctypes.byref(rw), ctypes.byref(nw),
+                                ctypes.byref(tw)) == 0
+    stride = len(spans) + 3
+    words = np.zeros(rw.value * stride, np.uint64)
+    nwords = np.zeros(nw.value * stride, np.uint64)
+    nbp = ctypes.c_uint64()
+    rc = L.fc2_pack_pairs(ctypes.byref(p), h, len(spans), buf.ctypes.data, off.ctypes.data, hp.ctypes.data,
+                          words.ctypes.data, rw.value, nwords.ctypes.data, nw.value, stride, ctypes.byref(nbp), 3)
+    return rc, hp, words, nwords, stride, nbp.value, buf, off
+
+
+def test_pair_pack_roundtrip(L):
+    path = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    rc, h = _open(path)
+    _pack(h)
+    genome = load_genome(path)
+    spans = make_spans(genome, 300, seed=5, p_readN=0.3, p_lower=0.3)
+    # exotic bytes in a few reads
+    for k in (3, 17, 101):
+        s = spans[k]
+        rp = bytearray(s.read_part)
+        rp[len(rp) // 2] = ord('R')
+        s.read_part = bytes(rp)
+    p = N.Params(15, 2, 2, 0, 0, 0, 0)
+    rc, hp, words, nwords, stride, nbp, _, _ = _pack_pairs(L, p, h, spans, [0] * len(spans))
+    assert rc == 0, L.fc2_last_error()
+    e = 13
+    n_bp = 0
+    for i, s in enumerate(spans):
+        l = len(s.read_part) - 2 * e
+        internal = s.read_part[e:len(s.read_part) - e].upper()
+        flags = int(hp["flags"][i])
+        if l < 0:
+            assert flags & N.PAIR_BYTEPATH == 0
+            continue
+        exotic = any(c not in b"ACGTN" for c in internal)
+        assert bool(flags & N.PAIR_BYTEPATH) == exotic, i
+        if exotic:
+            n_bp += 1
+            continue
+        assert bool(flags & N.PAIR_READ_N) == (b"N" in internal), i
+        assert decode_read(words, nwords, stride, i, l, bool(flags & N.PAIR_READ_N)) == internal, i
+    assert n_bp == nbp == 3
+    L.fc2_fasta_close(h)
+
+
+def test_pack_unknown_chrom_is_key_error(L):
+    path = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    rc, h = _open(path)
+    _pack(h)
+    spans = make_spans(load_genome(path), 5, seed=9)
+    p = N.Params(15, 2, 2, 0, 0, 0, 0)
+    rc, *_ = _pack_pairs(L, p, h, spans, [0, 0, 7, 0, 0])
+    assert rc == N.FC2_E_KEY and b"KeyError" in L.fc2_last_error()
+    L.fc2_fasta_close(h)
+
+
+def test_bytepath_arena_matches_reference_windows(L, tmp_path):
+    path = str(tmp_path / "weird.fa")
+    open(path, "wb").write(WEIRD_FASTA * 1)
+    rc, h = _open(path)
+    _pack(h)
+    ref = RefIndexedFasta(path)
+    chroms = _chroms(h)
+    # pairs on every chrom, short reads (asize 5, margin 1 -> e 4)
+    p = N.Params(5, 1, 2, 0, 0, 0, 0)
+    from synth_small import SmallSpan
+    spans, cidx = [], []
+    rng = np.random.default_rng(3)
+    for ci, (name, _, _, _, size, regular) in enumerate(chroms):
+        for _ in range(6):
+            L_ = int(rng.integers(8, 20))
+            a = int(rng.integers(-2, size))
+            b = int(rng.integers(0, size + 3))
+            spans.append(SmallSpan(name, ci, a, a + 5, b - 5, b, bytes(rng.choice(list(b"ACGTNR"), L_)), False))
+            cidx.append(ci)
+    rc, hp, words, nwords, stride, nbp, buf, off = _pack_pairs(L, p, h, spans, cidx)
+    assert rc == 0, L.fc2_last_error()
+    m, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    assert L.fc2_bytepath_size(ctypes.byref(p), len(spans), hp.ctypes.data, ctypes.byref(m), ctypes.byref(nb)) == 0
+    assert m.value == nbp > 0
+    idx = np.zeros(m.value, np.uint64)
+    bp = np.zeros(m.value, N.PAIR_DTYPE)
+    offs = np.zeros(m.value, np.uint64)
+    arena = np.zeros(nb.value, np.uint8)
+    assert L.fc2_bytepath_fill(ctypes.byref(p), h, len(spans), buf.ctypes.data, off.ctypes.data, hp.ctypes.data,
+                               idx.ctypes.data, bp.ctypes.data, offs.ctypes.data, arena.ctypes.data) == 0
+    e = 4
+    for k in range(m.value):
+        i = int(idx[k])
+        s = spans[i]
+        o = int(offs[k])
+        lenI, lenA, lenB = np.frombuffer(arena[o:o + 12].tobytes(), np.int32)
+        l = len(s.read_part) - 2 * e
+        assert lenI == max(0, l)
+        I = arena[o + 12:o + 12 + lenI].tobytes()
+        assert I == s.read_part[e:len(s.read_part) - e].upper()
+        if l >= 0:
+            A = arena[o + 12 + lenI:o + 12 + lenI + lenA].tobytes()
+            B = arena[o + 12 + lenI + lenA:o + 12 + lenI + lenA + lenB].tobytes()
+            ra = ref.get_data(s.chrom, s.a_pos + e, s.a_pos + e + l + 2).upper()
+            rb = ref.get_data(s.chrom, s.b_aend - e - l - 2, s.b_aend - e).upper()
+            assert A == ra[:l + 3] and B == rb[:l + 3]
+    L.fc2_fasta_close(h)
