@@ -430,10 +430,16 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
     if (want_ties)
         for (uint32_t w = 0; w < tw; ++w) tiemask[(uint64_t)w * stride + i] = 0;
     if ((pr.flags & FC2_PAIR_SKIP) || l < 0) { out[i] = nohit_result(0); return; }
-    if (lenI != l || lenA != l + 2 || lenB != l + 2) { out[i] = nohit_result(FC2_RES_ERR_WIN); return; }
 
+    // Windows normally have l+2 bytes.  Outside get_data's defined range they can
+    // come back shorter or longer (find_circ.py:194-211); then the literal
+    // string form of find_circ.py:907-908 is followed byte by byte, including
+    // the reference's failure when the spliced string's length differs from the
+    // internal part (numpy comparison, :863) -> ERR_WIN.
+    const bool regular = (lenI == l && lenA == l + 2 && lenB == l + 2);
     int totB = 0;
-    for (int j = 0; j < l; ++j) totB += Bf[j + 2] != I[j];
+    if (regular)
+        for (int j = 0; j < l; ++j) totB += Bf[j + 2] != I[j];
     const int prim_minus = (pr.flags & FC2_PAIR_PRIMARY_REV) ? 1 : 0;
     const int sp_plus = p.strandpref ? (prim_minus ? 0 : 100) : 0;
     const int sp_minus = p.strandpref ? (prim_minus ? 100 : 0) : 0;
@@ -442,10 +448,24 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
     for (int pass = 0; pass < (want_ties ? 2 : 1); ++pass) {
         int d = totB;
         for (int x = 0; x <= l; ++x) {
-            if (x > 0) d += (int)(Af[x - 1] != I[x - 1]) - (int)(Bf[x + 1] != I[x - 1]);
+            if (regular) {
+                if (x > 0) d += (int)(Af[x - 1] != I[x - 1]) - (int)(Bf[x + 1] != I[x - 1]);
+            } else {
+                const int n1 = x < lenA ? x : lenA;
+                const int n2 = lenB - (x + 2) > 0 ? lenB - (x + 2) : 0;
+                if (n1 + n2 != lenI) {
+                    if (p.maxdist != 0) { err = FC2_RES_ERR_WIN; break; }
+                    continue;  // simple_match: unequal strings never qualify (find_circ.py:865-866)
+                }
+                d = 0;
+                for (int j = 0; j < n1; ++j) d += Af[j] != I[j];
+                for (int j = 0; j < n2; ++j) d += Bf[x + 2 + j] != I[n1 + j];
+            }
             if (d > p.maxdist) continue;
-            const uint8_t g0 = Af[x], g1 = Af[x + 1], g2 = Bf[x], g3 = Bf[x + 1];
-            if (!(is_acgtn(g0) && is_acgtn(g1) && is_acgtn(g2) && is_acgtn(g3))) { err = FC2_RES_ERR_KEY; break; }
+            const bool have4 = (x + 1 < lenA) && (x + 1 < lenB);
+            const uint8_t g0 = x < lenA ? Af[x] : 0, g1 = have4 ? Af[x + 1] : 0;
+            const uint8_t g2 = x < lenB ? Bf[x] : 0, g3 = have4 ? Bf[x + 1] : 0;
+            if (!(have4 && is_acgtn(g0) && is_acgtn(g1) && is_acgtn(g2) && is_acgtn(g3))) { err = FC2_RES_ERR_KEY; break; }
             const int cp = (g0 == 'G' && g1 == 'T' && g2 == 'A' && g3 == 'G');
             const int cm = (g0 == 'C' && g1 == 'T' && g2 == 'A' && g3 == 'C');
             const int ov = ov_of(x, l, p.margin);

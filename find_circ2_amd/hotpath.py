@@ -115,6 +115,7 @@ class PairBatch:
             off = np.ascontiguousarray(off, np.uint64)
             lens = np.ascontiguousarray(lens, np.int64)
         else:
+            reads = [r.encode("latin-1") if isinstance(r, str) else r for r in reads]
             lens = np.fromiter((len(r) for r in reads), np.int64, len(reads))
             off = np.zeros(len(reads), np.uint64)
             if len(reads):
@@ -446,14 +447,15 @@ def _expand_ties(options, genome, hp, i, tm, best: Splice, span, chrom):
 
 
 def _window_gtag(genome: Genome, hp, i, x, e, l) -> str:
-    c = int(hp["chrom"][i])
-    a0 = int(hp["a_pos"][i]) + e + x
-    b0 = int(hp["b_aend"][i]) - e - (l + 2) + x
+    # gt = A_flank[x:x+2], ag = B_flank[x:x+2] of the full windows (find_circ.py:901-902, 924-926)
     if genome.dummy:
         return "NNNN"
-    A = genome.get_upper(c, a0, a0 + 2)
-    B = genome.get_upper(c, b0, b0 + 2)
-    return (A + B).decode("latin-1")
+    c = int(hp["chrom"][i])
+    a0 = int(hp["a_pos"][i]) + e
+    b1 = int(hp["b_aend"][i]) - e
+    A = genome.get_upper(c, a0, a0 + l + 2)
+    B = genome.get_upper(c, b1 - l - 2, b1)
+    return (A[x:x + 2] + B[x:x + 2]).decode("latin-1")
 
 
 # ---------------------------------------------------------------------------

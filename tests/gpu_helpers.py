@@ -41,7 +41,9 @@ def assert_same(gpu, orc, mask=None, label=""):
     m = np.ones(n, bool) if mask is None else mask
     keyerr = orc["err_key"] & m
     assert np.array_equal(gpu["err_key"][m], orc["err_key"][m]), label + " KeyError flags differ"
-    ok = m & ~keyerr
+    shape = orc.get("err_shape", np.zeros(n, bool)) & m
+    assert np.array_equal(gpu["err_win"][m], shape[m]), label + " window/shape error flags differ"
+    ok = m & ~keyerr & ~shape
     assert np.array_equal(gpu["n_ties"][ok], orc["n_ties"][ok]), _first_diff(gpu, orc, ok, "n_ties", label)
     hit = ok & (orc["n_ties"] > 0)
     for k in ("x", "start", "end", "dist", "ov"):
