@@ -1,0 +1,359 @@
+#!/usr/bin/env python
+"""Benchmark: anchor-pairs/s of the breakpoint search (find_circ.py:854-974) on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W`` prints ONE
+JSON line.  For N > 1 it runs under torch.distributed.run, one rank per GPU.
+
+Workload (BASELINE.json configs[2] at N=1, configs[3] per GPU for N>1):
+an hg19-shaped synthetic genome (the 93 @SQ contigs of test_data/test_norm.sam,
+3.137 Gbp, ~7 % N runs) resident in HBM on every GPU, and per GPU a batch of
+50M synthetic 100 bp backsplice anchor pairs (seeded).  A
+"step" is one pass of the hot path over the GPU's batch: one find_breakpoints
+evaluation per pair, genome window gather included.  Pairs are independent, so
+ranks process their own shards with no collective on the data path (weak
+scaling); the only collectives are the timing barrier and the max-over-ranks.
+
+Also reported (``extra``): configs[1] (1M pairs on CDR1as_locus.fa), and the
+CPU baselines (literal Python restatement, C naive O(l^2), C O(l) on all cores).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+METRIC = "anchor-pairs/sec (backsplice calls) at 100 bp reads, 1/2/4/8 MI355X"
+
+
+def algo_bytes_per_pair(L: int, asize: int = 15, margin: int = 2) -> int:
+    """B(L) = ceil(l/4) + 2*ceil((l+2)/4) + 16 + 8 (2-bit read, two 2-bit windows,
+    16 B record, 8 B result); 81 B at L = 100."""
+    l = L - 2 * (asize - margin)
+    return -(-l // 4) + 2 * (-(-(l + 2) // 4)) + 16 + 8
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=["hg19", "cdr1as"], default="hg19")
+    ap.add_argument("--pairs", type=int, default=0, help="pairs per GPU (default 50M hg19 / 1M cdr1as)")
+    ap.add_argument("--read-len", type=int, default=100)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    return ap.parse_args()
+
+
+def setup_dist(args):
+    import torch
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def max_over_ranks(x: float, ws: int, dev) -> float:
+    if ws == 1:
+        return x
+    import torch
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def build_workload(args, rank, dev):
+    from find_circ2_amd import Genome, Options, PairBatch, SynthConfig, sq_table
+    opt = Options()
+    if args.workload == "hg19":
+        names, sizes = sq_table(os.path.join(GOLDEN, "test_norm.sam"))
+        g = Genome.synthetic(names, sizes, seed=4711, device=dev)
+        n = args.pairs or 50_000_000
+        span = (150, 20000)
+    else:
+        g = Genome.from_fasta(os.path.join(GOLDEN, "CDR1as_locus.fa"), device=dev)
+        n = args.pairs or 1_000_000
+        span = (150, 2500)
+    cfg = SynthConfig(seed=1337 + 7919 * rank, len_min=args.read_len, len_max=args.read_len, p_backsplice=1.0,
+                      p_planted=0.5, mut_rate=0.005, n_rate=0.0005, span_min=span[0], span_max=span[1])
+    b = PairBatch.synthetic(opt, g, n, cfg)
+    return opt, g, b
+
+
+def timed_scans(opt, g, b, steps, warmup, ws, dev):
+    """Warmup, then exactly `steps` scans bracketed by barrier + synchronize; per-launch HIP events."""
+    import torch
+    from find_circ2_amd import scan
+    out = scan(opt, g, b)
+    for _ in range(max(0, warmup - 1)):
+        scan(opt, g, b, out=out)
+    torch.cuda.synchronize(dev)
+    stream = torch.cuda.current_stream(dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    barrier(ws)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        ev[k][0].record(stream)
+        scan(opt, g, b, out=out, stream=stream.cuda_stream)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    t1 = time.perf_counter()
+    kms = [s.elapsed_time(e) for s, e in ev]
+    return t1 - t0, float(np.mean(kms)), out
+
+
+# ---------------------------------------------------------------------------
+# CPU baseline (oracle = test infrastructure, used ONLY as the reported baseline)
+# ---------------------------------------------------------------------------
+def _decode_sample(opt, g, b, idx):
+    """Bytes of sampled pairs (internal read part padded with dummy anchors, both windows)."""
+    import torch
+    from find_circ2_amd import _native as N
+    hp = b.fetch_host_pairs()[idx]
+    e = opt.eff_a
+    m = len(idx)
+    W = b.read_words.view(b.rw, b.stride)[:, torch.as_tensor(idx, device=b.device)].cpu().numpy()
+    bits = np.unpackbits(np.ascontiguousarray(W.T).view(np.uint8).reshape(m, -1), axis=1, bitorder="little")
+    NWm = b.read_nwords.view(b.nw, b.stride)[:, torch.as_tensor(idx, device=b.device)].cpu().numpy()
+    nbits = np.unpackbits(np.ascontiguousarray(NWm.T).view(np.uint8).reshape(m, -1), axis=1, bitorder="little")
+    code = np.frombuffer(b"ACGTN", np.uint8)
+    ls = hp["read_len"].astype(np.int64) - 2 * e
+    lmax = int(ls.max())
+    j = np.arange(lmax)[None, :]
+    lo = np.take_along_axis(bits, np.minimum(j, bits.shape[1] - 1).repeat(m, 0), 1)
+    hi = np.take_along_axis(bits, np.minimum(ls[:, None] + j, bits.shape[1] - 1), 1)
+    I = code[(lo | (hi << 1)).astype(np.int64)]
+    nmask = nbits[:, :lmax].astype(bool) & ((hp["flags"] & N.PAIR_READ_N) != 0)[:, None]
+    I[nmask] = ord("N")
+    U = g.units.cpu().numpy().view(np.uint64)
+    NP = g.nplane.cpu().numpy().view(np.uint64)
+
+    def windows(starts, lens):
+        pos = starts[:, None] + np.arange(lens)[None, :]
+        c = hp["chrom"].astype(np.int64)
+        cs = g.chrom_start[c].astype(np.int64)[:, None]
+        sz = g.sizes[c][:, None]
+        inside = (pos >= 0) & (pos < sz)
+        gp = np.where(inside, pos + cs, 0).astype(np.uint64)
+        u = (gp >> np.uint64(6)).astype(np.int64)
+        bb = gp & np.uint64(63)
+        lo_ = (U[2 * u] >> bb) & np.uint64(1)
+        hi_ = (U[2 * u + 1] >> bb) & np.uint64(1)
+        nn = ((NP[u] >> bb) & np.uint64(1)).astype(bool) | ~inside
+        w = code[(lo_ | (hi_ << np.uint64(1))).astype(np.int64)]
+        w[nn] = ord("N")
+        return w
+
+    Lw = lmax + 2
+    A = windows(hp["a_pos"].astype(np.int64) + e, Lw)
+    B = windows(hp["b_aend"].astype(np.int64) - e - (ls + 2), Lw)
+    reads, parts, woff = [], [], np.zeros(m, np.int64)
+    pos = 0
+    for k in range(m):
+        lk = int(ls[k])
+        reads.append(b"A" * e + I[k, :lk].tobytes() + b"A" * e)
+        woff[k] = pos
+        parts.append(A[k, :lk + 2].tobytes() + B[k, :lk + 2].tobytes())
+        pos += 2 * (lk + 2)
+    wins = np.frombuffer(b"".join(parts) + b"\0", np.uint8)
+    return hp, reads, wins, woff, ls
+
+
+def cpu_baselines(opt, g, b, budget_s):
+    import oracle
+    from oracle.bp_oracle import Options as ROpt, find_breakpoints as py_find, Span
+
+    rng = np.random.default_rng(99)
+    n_sample = min(b.n, 200_000)
+    idx = np.sort(rng.choice(b.n, n_sample, replace=False))
+    hp, reads, wins, woff, ls = _decode_sample(opt, g, b, idx)
+    e = opt.eff_a
+    bs = (hp["flags"] & 1) != 0
+    rev = (hp["flags"] & 2) != 0
+    skip = (hp["flags"] & 0x10) != 0
+
+    # (1) literal Python restatement (the reference's own idiom: string concat + numpy compare per x)
+    class _Win:
+        def __init__(self):
+            self.k = 0
+
+        def get_data(self, chrom, start, end, sense="+"):
+            # hand out the pre-decoded windows in call order: A then B (find_circ.py:901-902)
+            k = self.k
+            self.k += 1
+            pair, which = divmod(k, 2)
+            lw = int(ls[pair]) + 2
+            o = int(woff[pair]) + which * lw
+            return wins[o:o + lw].tobytes()
+
+    wg = _Win()
+    ro = ROpt()
+    t0 = time.perf_counter()
+    done = 0
+    for k in range(len(reads)):
+        if skip[k]:
+            wg.k += 2
+            continue
+        # is_backsplice = B.pos - A.aend < 0 (find_circ.py:842): encode the flag through these two
+        a_aend, b_pos = (1, 0) if bs[k] else (0, 1)
+        sp = Span("c", int(hp["a_pos"][k]), a_aend, b_pos, int(hp["b_aend"][k]), reads[k], bool(rev[k]))
+        py_find(sp, wg, ro)
+        done += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    py_rate = done / (time.perf_counter() - t0)
+    py_sample = done
+
+    # (2) C, literal O(l^2), one core;  (3) C, O(l), all host cores (ctypes releases the GIL)
+    p = oracle.params()
+
+    def run_c(use_fast, lo, hi):
+        return oracle.scan_windows(p, reads[lo:hi], wins, woff[lo:hi], hp["a_pos"][lo:hi], hp["b_aend"][lo:hi],
+                                   bs[lo:hi], rev[lo:hi], use_fast=use_fast)
+
+    t0 = time.perf_counter()
+    k = 0
+    chunk = 2000
+    while k < len(reads) and time.perf_counter() - t0 < budget_s:
+        run_c(False, k, min(len(reads), k + chunk))
+        k += chunk
+    naive_rate = min(k, len(reads)) / (time.perf_counter() - t0)
+    cores = len(os.sched_getaffinity(0))
+    cores = min(cores, 16)         # the GPU box's CPU share for one GPU
+    t0 = time.perf_counter()
+    done_fast = 0
+    rounds = 0
+    while time.perf_counter() - t0 < budget_s / 2 or rounds == 0:
+        ths = []
+        per = (len(reads) + cores - 1) // cores
+        for c in range(cores):
+            th = threading.Thread(target=run_c, args=(True, c * per, min(len(reads), (c + 1) * per)))
+            th.start()
+            ths.append(th)
+        for th in ths:
+            th.join()
+        done_fast += len(reads)
+        rounds += 1
+    fast_rate = done_fast / (time.perf_counter() - t0)
+    try:
+        model = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
+    except Exception:
+        model = "unknown"
+    return dict(
+        main={"value": round(py_rate, 1), "unit": "anchor-pairs/s", "cores": 1, "kind": "port",
+              "sample": "%d pairs of this batch, literal Python restatement of find_circ.py:854-974 "
+                        "(per-x string concat + numpy byte compare, oracle/bp_oracle.py), windows pre-decoded"
+                        % py_sample},
+        c_naive={"value": round(naive_rate, 1), "unit": "anchor-pairs/s", "cores": 1, "kind": "port",
+                 "sample": "C literal O(l^2) restatement (oracle/bp_oracle.c) on the same sample"},
+        c_fast={"value": round(fast_rate, 1), "unit": "anchor-pairs/s", "cores": cores, "kind": "port",
+                "sample": "C O(l) prefix-sum restatement, %d threads, %d pairs x %d rounds" % (
+                    cores, len(reads), rounds)},
+        cpu_model=model)
+
+
+def main():
+    args = parse()
+    import torch
+    ws, rank, local = setup_dist(args)
+    if args.gpus != ws and ws > 1:
+        print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, ws), file=sys.stderr)
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    opt, g, b = build_workload(args, rank, dev)
+    elapsed, kernel_ms, out = timed_scans(opt, g, b, args.steps, args.warmup, ws, dev)
+    elapsed = max_over_ranks(elapsed, ws, dev)
+    kernel_ms = max_over_ranks(kernel_ms, ws, dev)
+    total_pairs = b.n * args.steps * ws
+    value = total_pairs / elapsed
+    bpp = algo_bytes_per_pair(args.read_len, opt.asize, opt.margin)
+    achieved = bpp * b.n / (kernel_ms * 1e-3) / 1e9
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            w = tj.get(args.workload)
+            if w and int(w.get("pairs_per_launch", -1)) == b.n:
+                traffic = w.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    res = out.host(b.n)
+    hits = int((res["best_x"] >= 0).sum())
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "anchor-pairs/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (seeded; genome and anchor pairs generated on device, SURVEY.md 8(d))",
+        "config": {
+            "workload": ("configs[2]/[3]: hg19-shaped synthetic genome (93 @SQ contigs of test_norm.sam, 3.137 Gbp, "
+                         "~7%% N) x %dM synthetic %d bp backsplice anchor pairs per GPU" % (b.n // 10**6, args.read_len))
+            if args.workload == "hg19" else
+            ("configs[1]: CDR1as_locus.fa x %d synthetic %d bp backsplice anchor pairs per GPU" % (b.n, args.read_len)),
+            "pairs_per_gpu": b.n, "read_len": args.read_len, "asize": opt.asize, "margin": opt.margin,
+            "maxdist": opt.maxdist, "parallelism": "dp%d (independent pair shards, no collective)" % ws,
+            "pairs_with_hit": hits,
+        },
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel_ms": round(kernel_ms, 4), "algo_bytes_per_pair": bpp,
+                     "kernel": "bp_scan_kernel<2> (one anchor pair per lane)"},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:
+        cb = cpu_baselines(opt, g, b, args.cpu_seconds)
+        line["cpu_baseline"] = cb["main"]
+        line["cpu_baseline_extra"] = {"c_naive_1core": cb["c_naive"], "c_fast_allcores": cb["c_fast"],
+                                      "cpu_model": cb["cpu_model"]}
+    if rank == 0 and ws == 1 and not args.no_extra and args.workload == "hg19":
+        del b, out
+        torch.cuda.empty_cache()
+        a2 = argparse.Namespace(**vars(args))
+        a2.workload, a2.pairs = "cdr1as", 1_000_000
+        o2, g2, b2 = build_workload(a2, rank, dev)
+        el2, km2, _ = timed_scans(o2, g2, b2, max(args.steps, 20), args.warmup, 1, dev)
+        line["extra"] = {"configs[1]_cdr1as_1M": {
+            "value": round(b2.n * max(args.steps, 20) / el2, 1), "unit": "anchor-pairs/s",
+            "kernel_ms": round(km2, 4),
+            "achieved_algo_GBs": round(bpp * b2.n / (km2 * 1e-3) / 1e9, 1)}}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if ws > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
