@@ -81,7 +81,8 @@ class SynthCfg(ctypes.Structure):
 
 # every symbol include/fc2_bp.h declares (checked by tests/test_abi.py)
 EXPORTED = [
-    "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_max_fast_l", "fc2_batch_geometry",
+    "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_set_tuning", "fc2_max_fast_l",
+    "fc2_batch_geometry",
     "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch",
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
@@ -94,7 +95,8 @@ _lib = None
 
 def build(force: bool = False) -> str:
     srcdir = os.path.join(_HERE, "csrc")
-    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_host.cpp", "fc2_common.h", "Makefile")]
+    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_scan32.h", "fc2_host.cpp",
+                                              "fc2_common.h", "Makefile")]
     srcs.append(os.path.join(os.path.dirname(_HERE), "include", "fc2_bp.h"))
     newest = max(os.path.getmtime(s) for s in srcs)
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
@@ -117,6 +119,7 @@ def lib() -> ctypes.CDLL:
         "fc2_last_error": (ctypes.c_char_p, []),
         "fc2_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
         "fc2_max_fast_l": (ctypes.c_int, []),
+        "fc2_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
         "fc2_batch_geometry": (ctypes.c_int, [P(Params), i32, P(u32), P(u32), P(u32)]),
         "fc2_bp_scan_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp, u32, vp]),
         "fc2_bp_scan_bytes_launch": (ctypes.c_int, [P(Params), P(BytesView), vp, vp, u32, u64, vp]),

@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include "fc2_common.h"
+#include "fc2_scan32.h"
 
 namespace {
 
@@ -50,6 +51,29 @@ struct Planes {
     uint64_t lo[NW + 1], hi[NW + 1], n[NW + 1];
 };
 
+// Streaming (read-once) traffic: optionally non-temporal so it does not evict
+// genome lines from L2 / the Infinity Cache.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ uint64_t ld_stream(const uint64_t *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st_stream(uint64_t *p, uint64_t v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <bool NT>
+__device__ __forceinline__ fc2_pair ld_pair(const fc2_pair *p) {
+    u64x2 v;
+    if constexpr (NT) v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
+    else v = *reinterpret_cast<const u64x2 *>(p);
+    fc2_pair r;
+    __builtin_memcpy(&r, &v, sizeof r);
+    return r;
+}
+
 // One genome window of W bases starting at chromosome position ws, as three
 // bit planes.  Positions outside [0, csize) read as 'N' (get_data's padding,
 // find_circ.py:194-211).
@@ -69,7 +93,7 @@ __device__ __forceinline__ void load_window(const fc2_genome_view &g, uint64_t c
 #pragma unroll
     for (int j = 0; j <= NW; ++j) {
         const int64_t u = u0 + j;
-        const bool need = (j < NW) || (sh != 0);
+        const bool need = j <= (((int)sh + W - 1) >> 6);   // units the W window actually spans
         if (need && u >= 0 && (uint64_t)u < g.n_units) {
             const ulonglong2 v = U[u];
             ul[j] = v.x; uh[j] = v.y;
@@ -191,13 +215,13 @@ __device__ __forceinline__ uint64_t nohit_result(unsigned err) {
 // ---------------------------------------------------------------------------
 // register kernel: one pair per lane, NW 64-bit words per bit plane
 // ---------------------------------------------------------------------------
-template <int NW>
+template <int NW, bool NT>
 __global__ __launch_bounds__(kBlock) void bp_scan_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
                                                          uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
                                                          uint32_t tw) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
     if (i >= bv.n) return;
-    const fc2_pair pr = bv.pairs[i];
+    const fc2_pair pr = ld_pair<NT>(bv.pairs + i);
     if (pr.flags & FC2_PAIR_BYTEPATH) return;  // left for the byte-exact kernel
 
     const int e = p.asize - p.margin;
@@ -208,7 +232,7 @@ __global__ __launch_bounds__(kBlock) void bp_scan_kernel(fc2_params p, fc2_genom
     if ((pr.flags & FC2_PAIR_SKIP) || l < 0 || l > 64 * NW - 2 || pr.chrom >= g.n_chrom) {
         unsigned err = 0;
         if (!(pr.flags & FC2_PAIR_SKIP) && l >= 0 && (l > 64 * NW - 2 || pr.chrom >= g.n_chrom)) err = FC2_RES_ERR_WIN;
-        out[i] = nohit_result(err);
+        st_stream<NT>(out + i, nohit_result(err));
         if (want_ties)
             for (uint32_t k = 0; k < tw; ++k) tiemask[(uint64_t)k * bv.stride + i] = 0;
         return;
@@ -221,7 +245,7 @@ __global__ __launch_bounds__(kBlock) void bp_scan_kernel(fc2_params p, fc2_genom
         uint64_t r[2 * NW + 1];
 #pragma unroll
         for (int j = 0; j < 2 * NW; ++j)
-            r[j] = ((uint32_t)j < bv.rw) ? bv.read_words[(uint64_t)j * bv.stride + i] : 0ull;
+            r[j] = ((uint32_t)j < bv.rw) ? ld_stream<NT>(bv.read_words + (uint64_t)j * bv.stride + i) : 0ull;
         r[2 * NW] = 0;
         const int base = l >> 6;
         const unsigned s = (unsigned)(l & 63);
@@ -238,7 +262,7 @@ __global__ __launch_bounds__(kBlock) void bp_scan_kernel(fc2_params p, fc2_genom
         if (pr.flags & FC2_PAIR_READ_N) {
 #pragma unroll
             for (int k = 0; k < NW; ++k)
-                In[k] = ((uint32_t)k < bv.nw ? bv.read_nwords[(uint64_t)k * bv.stride + i] : 0ull) & rmask(0, l, k);
+                In[k] = ((uint32_t)k < bv.nw ? ld_stream<NT>(bv.read_nwords + (uint64_t)k * bv.stride + i) : 0ull) & rmask(0, l, k);
         } else {
 #pragma unroll
             for (int k = 0; k < NW; ++k) In[k] = 0;
@@ -253,7 +277,7 @@ __global__ __launch_bounds__(kBlock) void bp_scan_kernel(fc2_params p, fc2_genom
     // get_data is only length-preserving for start <= size and end >= 0; the host
     // routes anything else to the byte kernel -- flag defensively here.
     if (wsA > csize || wsA + W < 0 || wsB > csize || wsB + W < 0) {
-        out[i] = nohit_result(FC2_RES_ERR_WIN);
+        st_stream<NT>(out + i, nohit_result(FC2_RES_ERR_WIN));
         if (want_ties)
             for (uint32_t k = 0; k < tw; ++k) tiemask[(uint64_t)k * bv.stride + i] = 0;
         return;
@@ -344,7 +368,7 @@ __global__ __launch_bounds__(kBlock) void bp_scan_kernel(fc2_params p, fc2_genom
         gtag12 = code_at<NW>(A, x) | (code_at<NW>(A, x + 1) << 3) | (code_at<NW>(B, x) << 6) |
                  (code_at<NW>(B, x + 1) << 9);
     }
-    out[i] = pack_result(Bst, gtag12, 0);
+    st_stream<NT>(out + i, pack_result(Bst, gtag12, 0));
 
     if (want_ties) {
         // --all-hits: mark every tie (find_circ.py:966-974), second pass over the same hits
@@ -614,7 +638,9 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
                 for (int q = 0; q < 512; ++q)
                     if (dinuc(g, cs, sz, start - 2 - q, cA, msite ? cC : cG)) { start = start - q; break; }
             }
-            if (start >= 0 && end <= sz && end - kA >= 0 && start + kB <= end && kA <= end - start) {
+            // real alignments never sit on 'N': redraw loci whose junction bases are N
+            if (start >= 0 && end <= sz && end - kA >= 0 && start + kB <= end && kA <= end - start &&
+                gbase(g, cs, sz, end - 1) < 4u && gbase(g, cs, sz, start) < 4u) {
                 A0 = end - kA; B0 = start; t0 = start; t1 = end; ok = true;
             }
         } else {
@@ -629,7 +655,9 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
                 for (int q = 0; q < 512; ++q)
                     if (dinuc(g, cs, sz, a - 2 + q, cA, msite ? cC : cG)) { a = a + q; break; }
             }
-            if (d - kA >= 0 && a + kB <= sz && a > d) { A0 = d - kA; B0 = a; t0 = d; t1 = a; ok = true; }
+            if (d - kA >= 0 && a + kB <= sz && a > d && gbase(g, cs, sz, d - 1) < 4u && gbase(g, cs, sz, a) < 4u) {
+                A0 = d - kA; B0 = a; t0 = d; t1 = a; ok = true;
+            }
         }
     }
     int c0 = 0, c1 = 0;
@@ -696,6 +724,12 @@ inline int hip_check(hipError_t e, const char *what) {
 
 inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
+// Tuning knobs (fc2_set_tuning): non-temporal streaming of the per-pair
+// inputs/outputs, default on.
+int g_stream_nt = 1;
+int g_kernel32 = 1;   // 1: bp_scan32_kernel (32-bit plane words), 0: bp_scan_kernel (64-bit)
+inline bool stream_nt() { return g_stream_nt != 0; }
+
 }  // namespace
 
 // ===========================================================================
@@ -723,12 +757,17 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     hipStream_t s = (hipStream_t)stream;
     const unsigned grid = grid_for(b->n, kBlock);
     uint64_t *out = reinterpret_cast<uint64_t *>(results);
-    if (nwords <= 2)
-        hipLaunchKernelGGL(bp_scan_kernel<2>, dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw);
-    else if (nwords <= 4)
-        hipLaunchKernelGGL(bp_scan_kernel<4>, dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw);
-    else
-        hipLaunchKernelGGL(bp_scan_kernel<8>, dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw);
+    const bool nt = stream_nt();
+    if (g_kernel32) {
+        fc2::launch_scan32((ml + 2 + 31) / 32, nt, grid, s, *p, *g, *b, out, tiemask, tw);
+        return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
+    }
+#define FC2_LAUNCH(NWV, NTV) \
+    hipLaunchKernelGGL((bp_scan_kernel<NWV, NTV>), dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw)
+    if (nwords <= 2) { if (nt) FC2_LAUNCH(2, true); else FC2_LAUNCH(2, false); }
+    else if (nwords <= 4) { if (nt) FC2_LAUNCH(4, true); else FC2_LAUNCH(4, false); }
+    else { if (nt) FC2_LAUNCH(8, true); else FC2_LAUNCH(8, false); }
+#undef FC2_LAUNCH
     return hip_check(hipGetLastError(), "bp_scan_kernel launch");
 }
 
@@ -786,6 +825,14 @@ extern "C" int fc2_synth_pairs_launch(const fc2_params *p, const fc2_synth_cfg *
     hipLaunchKernelGGL(synth_pairs_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, *p, *cfg, *g,
                        chrom_cum, n, pairs, read_words, rw, read_nwords, nw, stride, truth);
     return hip_check(hipGetLastError(), "synth_pairs_kernel launch");
+}
+
+extern "C" int fc2_set_tuning(int key, int value) {
+    switch (key) {
+        case FC2_TUNE_STREAM_NT: g_stream_nt = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_KERNEL32: g_kernel32 = value ? 1 : 0; return FC2_OK;
+        default: return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: unknown key");
+    }
 }
 
 extern "C" int fc2_device_count(int *count) {

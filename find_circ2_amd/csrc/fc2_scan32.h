@@ -1,0 +1,12 @@
+// Launcher of the 32-bit-word breakpoint-search kernel (fc2_scan32.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/fc2_bp.h"
+
+namespace fc2 {
+// nq: 32-bit words per plane needed by the batch (rounded up to 4/8/16 inside).
+void launch_scan32(int nq, bool nt, unsigned grid, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+                   const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw);
+}  // namespace fc2

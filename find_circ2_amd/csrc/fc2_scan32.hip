@@ -1,0 +1,393 @@
+// fc2_scan32.hip -- the breakpoint-search kernel on 32-bit bit-plane words.
+//
+// Same algorithm and results as bp_scan_kernel (fc2_kernels.hip; reference
+// find_circ.py:854-974), re-cut for the gfx950 VALU: every plane is held as
+// 32-bit words so that each funnel shift (window alignment, B[x+2], the
+// dinucleotide shift) is ONE v_alignbit_b32 and each popcount ONE v_bcnt_u32,
+// instead of the 64-bit shift/or/select sequences.  NQ = 32-bit words per
+// plane: 4 / 8 / 16 <-> l + 2 <= 128 / 256 / 512.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "fc2_common.h"
+#include "fc2_scan32.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ uint32_t lowbits32(int n) {  // bits [0, n), any n
+    return n >= 32 ? ~0u : (n <= 0 ? 0u : ((1u << n) - 1u));
+}
+// bits [s, s+32) of the 64-bit value hi:lo, s in [0, 31]
+__device__ __forceinline__ uint32_t alignr(uint32_t hi, uint32_t lo, unsigned s) {
+    return __builtin_amdgcn_alignbit(hi, lo, s);
+}
+__device__ __forceinline__ uint32_t rmask32(int a, int b, int k) {  // positions [a, b) in word k
+    return lowbits32(b - 32 * k) & ~lowbits32(a - 32 * k);
+}
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+template <bool NT>
+__device__ __forceinline__ uint64_t ld_stream(const uint64_t *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st_stream(uint64_t *p, uint64_t v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+template <bool NT>
+__device__ __forceinline__ fc2_pair ld_pair(const fc2_pair *p) {
+    u64x2 v;
+    if constexpr (NT) v = __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
+    else v = *reinterpret_cast<const u64x2 *>(p);
+    fc2_pair r;
+    __builtin_memcpy(&r, &v, sizeof r);
+    return r;
+}
+
+template <int NQ>
+struct P32 {
+    uint32_t lo[NQ + 1], hi[NQ + 1], n[NQ + 1];
+};
+
+// shift the word array left by `sel` words (sel in [0, 2^levels)), selects only
+template <int M>
+__device__ __forceinline__ void word_shift(uint32_t (&a)[M], int sel, int levels) {
+#pragma unroll
+    for (int lv = 0; lv < 5; ++lv) {
+        if (lv >= levels) break;
+        const int d = 1 << lv;
+        const bool on = (sel >> lv) & 1;
+#pragma unroll
+        for (int k = 0; k < M; ++k) a[k] = on ? (k + d < M ? a[k + d] : 0u) : a[k];
+    }
+}
+
+// Genome window [ws, ws+W) of a chromosome starting at global base cstart.
+template <int NQ>
+__device__ __forceinline__ void load_window32(const fc2_genome_view &g, uint64_t cstart, int64_t csize, int64_t ws,
+                                              int W, P32<NQ> &P) {
+    if (g.dummy) {
+#pragma unroll
+        for (int k = 0; k <= NQ; ++k) { P.lo[k] = 0; P.hi[k] = 0; P.n[k] = ~0u; }
+        return;
+    }
+    constexpr int NU = NQ / 2 + 1;           // 64-bit units covering NQ+1 32-bit words at any parity
+    const int64_t g0 = (int64_t)cstart + ws;
+    const int64_t q0 = g0 >> 5;              // first 32-bit word (floor)
+    const unsigned sh = (unsigned)(g0 & 31);
+    const int64_t u0 = q0 >> 1;
+    const int odd = (int)(q0 & 1);
+    const int qlast = odd + (((int)sh + W - 1) >> 5);   // last word needed, relative to 2*u0
+    const ulonglong2 *U = reinterpret_cast<const ulonglong2 *>(g.units);
+    uint32_t xl[2 * NU], xh[2 * NU];
+    const bool interior = u0 >= 0 && (uint64_t)(u0 + NU) <= g.n_units;
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+        const int64_t u = u0 + j;
+        const bool need = 2 * j <= qlast;
+        ulonglong2 v = {0ull, 0ull};
+        if (need && (interior || (u >= 0 && (uint64_t)u < g.n_units))) v = U[u];
+        xl[2 * j] = (uint32_t)v.x; xl[2 * j + 1] = (uint32_t)(v.x >> 32);
+        xh[2 * j] = (uint32_t)v.y; xh[2 * j + 1] = (uint32_t)(v.y >> 32);
+    }
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        const uint32_t l0 = odd ? xl[k + 1] : xl[k], l1 = odd ? xl[k + 2] : xl[k + 1];
+        const uint32_t h0 = odd ? xh[k + 1] : xh[k], h1 = odd ? xh[k + 2] : xh[k + 1];
+        P.lo[k] = alignr(l1, l0, sh);
+        P.hi[k] = alignr(h1, h0, sh);
+    }
+    P.lo[NQ] = 0; P.hi[NQ] = 0;
+
+    bool anyN = false;
+    {
+        const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
+        const int64_t b0 = u0 >> 4, b1 = (u0 + NU - 1) >> 4;
+        if (b0 >= 0 && b0 < nb) anyN |= (g.ncoarse[b0 >> 5] >> (b0 & 31)) & 1u;
+        if (b1 != b0 && b1 >= 0 && b1 < nb) anyN |= (g.ncoarse[b1 >> 5] >> (b1 & 31)) & 1u;
+    }
+    if (anyN) {
+        uint32_t xn[2 * NU];
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            const int64_t u = u0 + j;
+            const uint64_t v = (u >= 0 && (uint64_t)u < g.n_units) ? g.nplane[u] : 0ull;
+            xn[2 * j] = (uint32_t)v; xn[2 * j + 1] = (uint32_t)(v >> 32);
+        }
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            const uint32_t n0 = odd ? xn[k + 1] : xn[k], n1 = odd ? xn[k + 2] : xn[k + 1];
+            P.n[k] = alignr(n1, n0, sh);
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) P.n[k] = 0;
+    }
+    P.n[NQ] = 0;
+
+    // positions outside [0, csize) of the chromosome read as 'N'
+    int64_t vlo = -ws, vhi = csize - ws;
+    vlo = vlo < 0 ? 0 : (vlo > W ? W : vlo);
+    vhi = vhi < 0 ? 0 : (vhi > W ? W : vhi);
+    if (vlo != 0 || vhi != W) {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            const uint32_t v = rmask32((int)vlo, (int)vhi, k);
+            P.lo[k] &= v; P.hi[k] &= v; P.n[k] = (P.n[k] & v) | ~v;
+        }
+    }
+}
+
+template <int NQ>
+__device__ __forceinline__ unsigned code_at32(const P32<NQ> &P, int pos) {
+    const int k = pos >> 5, b = pos & 31;
+    uint32_t lo = 0, hi = 0, nn = 0;
+#pragma unroll
+    for (int kk = 0; kk < NQ; ++kk)
+        if (kk == k) { lo = P.lo[kk]; hi = P.hi[kk]; nn = P.n[kk]; }
+    return ((nn >> b) & 1u) ? 4u : (((lo >> b) & 1u) | (((hi >> b) & 1u) << 1));
+}
+
+struct Best32 {
+    int n_hits = 0, best_score = 0, best_x = -1, best_minus = 0, best_dist = 0, best_ov = 0, n_ties = 0;
+};
+
+__device__ __forceinline__ int ov_of(int x, int l, int margin) {  // find_circ.py:917-922
+    int ov = 0;
+    if (margin) {
+        if (x < margin) ov = margin - x;
+        if (l - x < margin) ov = margin - (l - x);
+    }
+    return ov;
+}
+
+__device__ __forceinline__ void add_hit(Best32 &B, int x, int minus, int dist, int ov, int score) {
+    if (B.n_hits == 0 || score > B.best_score) {
+        B.best_score = score; B.best_x = x; B.best_minus = minus; B.best_dist = dist; B.best_ov = ov; B.n_ties = 1;
+    } else if (score == B.best_score) {
+        B.n_ties += 1;
+    }
+    B.n_hits += 1;
+}
+
+__device__ __forceinline__ uint64_t pack_result(const Best32 &B, unsigned gtag12, unsigned err) {
+    if (B.n_hits == 0) return (uint64_t)(uint16_t)(int16_t)-1 | ((uint64_t)(FC2_RES_DONE | err) << 48);
+    const unsigned nt = B.n_hits >= 2 ? (unsigned)B.n_ties : 1u;   // find_circ.py:961-972
+    const unsigned dist = B.best_dist > 255 ? 255u : (unsigned)B.best_dist;
+    const unsigned info = FC2_RES_DONE | err | (B.best_minus ? FC2_RES_MINUS : 0u) |
+                          ((gtag12 << FC2_RES_GTAG_SHIFT) & FC2_RES_GTAG_MASK);
+    return (uint64_t)(uint16_t)(int16_t)B.best_x | ((uint64_t)(dist & 0xFF) << 16) |
+           ((uint64_t)(B.best_ov & 0xFF) << 24) | ((uint64_t)(nt > 0xFFFF ? 0xFFFFu : nt) << 32) |
+           ((uint64_t)info << 48);
+}
+
+template <int NQ, bool NT>
+__global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+                                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
+                                                           uint32_t tw) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= bv.n) return;
+    const fc2_pair pr = ld_pair<NT>(bv.pairs + i);
+    if (pr.flags & FC2_PAIR_BYTEPATH) return;  // left for the byte-exact kernel
+
+    const int e = p.asize - p.margin;
+    const int l = (int)pr.read_len - 2 * e;
+    const bool want_ties = p.allhits != 0;
+    const int W = l + 2;                       // flank, find_circ.py:900
+    const uint64_t cstart = (g.dummy || pr.chrom >= g.n_chrom) ? 0ull : g.chrom_start[pr.chrom];
+    const int64_t csize = g.dummy ? (int64_t)1 << 62 : (pr.chrom >= g.n_chrom ? 0 : g.chrom_size[pr.chrom]);
+    const int64_t wsA = (int64_t)pr.a_pos + e;
+    const int64_t wsB = (int64_t)pr.b_aend - e - W;
+    if ((pr.flags & FC2_PAIR_SKIP) || l < 0 || l > 32 * NQ - 2 || pr.chrom >= g.n_chrom || wsA > csize ||
+        wsA + W < 0 || wsB > csize || wsB + W < 0) {
+        // skipped / empty x-range: no hit; anything else is routed to the byte path by the host
+        const bool err = !(pr.flags & FC2_PAIR_SKIP) && l >= 0;
+        Best32 none;
+        st_stream<NT>(out + i, pack_result(none, 0, err ? FC2_RES_ERR_WIN : 0u));
+        if (want_ties)
+            for (uint32_t k = 0; k < tw; ++k) tiemask[(uint64_t)k * bv.stride + i] = 0;
+        return;
+    }
+
+    // --- internal read part: 32-bit plane words ---------------------------------
+    uint32_t Ilo[NQ], Ihi[NQ], In[NQ];
+    {
+        constexpr int R = NQ + 1;              // 64-bit row words the largest row can use (2l <= 64R)
+        uint32_t r[2 * R + 1];
+#pragma unroll
+        for (int j = 0; j < R; ++j) {
+            const uint64_t v = ((uint32_t)j < bv.rw) ? ld_stream<NT>(bv.read_words + (uint64_t)j * bv.stride + i) : 0ull;
+            r[2 * j] = (uint32_t)v; r[2 * j + 1] = (uint32_t)(v >> 32);
+        }
+        r[2 * R] = 0;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) Ilo[k] = r[k] & rmask32(0, l, k);
+        // high plane starts at bit l: shift by l>>5 words (selects), then by l&31 bits (alignbit)
+        uint32_t h[2 * R + 1];
+#pragma unroll
+        for (int k = 0; k < 2 * R + 1; ++k) h[k] = r[k];
+        constexpr int LV = NQ <= 4 ? 2 : (NQ <= 8 ? 3 : 4);
+        word_shift(h, l >> 5, LV);
+        const unsigned s = (unsigned)(l & 31);
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) Ihi[k] = alignr(h[k + 1], h[k], s) & rmask32(0, l, k);
+        if (pr.flags & FC2_PAIR_READ_N) {
+#pragma unroll
+            for (int j = 0; j < (NQ + 1) / 2; ++j) {
+                const uint64_t v =
+                    ((uint32_t)j < bv.nw) ? ld_stream<NT>(bv.read_nwords + (uint64_t)j * bv.stride + i) : 0ull;
+                In[2 * j] = (uint32_t)v & rmask32(0, l, 2 * j);
+                if (2 * j + 1 < NQ) In[2 * j + 1] = (uint32_t)(v >> 32) & rmask32(0, l, 2 * j + 1);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) In[k] = 0;
+        }
+    }
+
+    // --- genome windows (find_circ.py:900-902) ----------------------------------
+    P32<NQ> A, B;
+    load_window32<NQ>(g, cstart, csize, wsA, W, A);
+    load_window32<NQ>(g, cstart, csize, wsB, W, B);
+
+    // --- mismatch planes and prefix counts ---------------------------------------
+    uint32_t mA[NQ], mB[NQ];
+    int cA[NQ], cB[NQ];
+    int totB = 0, accA = 0;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        const uint32_t m = rmask32(0, l, k);
+        mA[k] = ((A.lo[k] ^ Ilo[k]) | (A.hi[k] ^ Ihi[k]) | (A.n[k] ^ In[k])) & m;
+        const uint32_t blo = alignr(B.lo[k + 1], B.lo[k], 2), bhi = alignr(B.hi[k + 1], B.hi[k], 2),
+                       bn = alignr(B.n[k + 1], B.n[k], 2);
+        mB[k] = ((blo ^ Ilo[k]) | (bhi ^ Ihi[k]) | (bn ^ In[k])) & m;
+        cA[k] = accA; cB[k] = totB;
+        accA += __popc(mA[k]);
+        totB += __popc(mB[k]);
+    }
+
+    // --- GTAG ('+') / CTAC ('-') masks for every x at once (find_circ.py:924-954) --
+    uint32_t plus[NQ], minus[NQ];
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        const uint32_t xm = rmask32(0, l + 1, k);
+        const uint32_t aLo1 = alignr(A.lo[k + 1], A.lo[k], 1), aHi1 = alignr(A.hi[k + 1], A.hi[k], 1);
+        const uint32_t bLo1 = alignr(B.lo[k + 1], B.lo[k], 1), bHi1 = alignr(B.hi[k + 1], B.hi[k], 1);
+        const uint32_t A_T1 = aHi1 & aLo1;
+        const uint32_t B_A0 = ~(B.lo[k] | B.hi[k] | B.n[k]);
+        const uint32_t common = A_T1 & B_A0 & xm;
+        plus[k] = (A.hi[k] & ~A.lo[k]) & (bHi1 & ~bLo1) & common;
+        minus[k] = (A.lo[k] & ~A.hi[k]) & (bLo1 & ~bHi1) & common;
+    }
+
+    const int prim_minus = (pr.flags & FC2_PAIR_PRIMARY_REV) ? 1 : 0;
+    const int sp_plus = p.strandpref ? (prim_minus ? 0 : 100) : 0;     // find_circ.py:796-797
+    const int sp_minus = p.strandpref ? (prim_minus ? 100 : 0) : 0;
+    Best32 Bst;
+    if (!p.noncanonical) {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            uint32_t w = plus[k] | minus[k];
+            while (w) {
+                const int b = __ffs(w) - 1;
+                w &= w - 1;
+                const uint32_t below = (1u << b) - 1u;
+                const int dist = cA[k] + __popc(mA[k] & below) + totB - cB[k] - __popc(mB[k] & below);
+                if (dist <= p.maxdist) {
+                    const int x = 32 * k + b;
+                    const int isminus = (int)((minus[k] >> b) & 1u);
+                    add_hit(Bst, x, isminus, dist, ov_of(x, l, p.margin),
+                            20 - 10 * dist - ov_of(x, l, p.margin) + (isminus ? sp_minus : sp_plus));
+                }
+            }
+        }
+    } else {
+        int d = totB;
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            for (int b = 0; b < 32; ++b) {
+                const int x = 32 * k + b;
+                if (x > l) break;
+                if (d <= p.maxdist) {
+                    const int ov = ov_of(x, l, p.margin);
+                    const int cp = (int)((plus[k] >> b) & 1u), cm = (int)((minus[k] >> b) & 1u);
+                    add_hit(Bst, x, 0, d, ov, 20 * cp - 10 * d - ov + sp_plus);
+                    add_hit(Bst, x, 1, d, ov, 20 * cm - 10 * d - ov + sp_minus);
+                }
+                d += (int)((mA[k] >> b) & 1u) - (int)((mB[k] >> b) & 1u);
+            }
+        }
+    }
+
+    unsigned gtag12 = 0;
+    if (Bst.n_hits) {
+        const int x = Bst.best_x;
+        gtag12 = code_at32<NQ>(A, x) | (code_at32<NQ>(A, x + 1) << 3) | (code_at32<NQ>(B, x) << 6) |
+                 (code_at32<NQ>(B, x + 1) << 9);
+    }
+    st_stream<NT>(out + i, pack_result(Bst, gtag12, 0));
+
+    if (want_ties) {
+        // --all-hits: every tie (find_circ.py:966-974); tie words are 64-bit, x-major
+        uint32_t tp[NQ], tm[NQ];
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) { tp[k] = 0; tm[k] = 0; }
+        if (Bst.n_hits) {
+            const int best = Bst.best_score;
+            int d = totB;
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                for (int b = 0; b < 32; ++b) {
+                    const int x = 32 * k + b;
+                    if (x > l) break;
+                    if (d <= p.maxdist) {
+                        const int ov = ov_of(x, l, p.margin);
+                        const int cp = (int)((plus[k] >> b) & 1u), cm = (int)((minus[k] >> b) & 1u);
+                        if (p.noncanonical) {
+                            if (20 * cp - 10 * d - ov + sp_plus == best) tp[k] |= 1u << b;
+                            if (20 * cm - 10 * d - ov + sp_minus == best) tm[k] |= 1u << b;
+                        } else if (cp || cm) {
+                            if (20 - 10 * d - ov + (cm ? sp_minus : sp_plus) == best) {
+                                if (cm) tm[k] |= 1u << b; else tp[k] |= 1u << b;
+                            }
+                        }
+                    }
+                    d += (int)((mA[k] >> b) & 1u) - (int)((mB[k] >> b) & 1u);
+                }
+            }
+        }
+        const uint32_t half = tw / 2;
+        for (uint32_t k = 0; k < half; ++k) {
+            uint64_t vp = 0, vm = 0;
+#pragma unroll
+            for (int kk = 0; kk < NQ / 2; ++kk)
+                if ((uint32_t)kk == k) {
+                    vp = (uint64_t)tp[2 * kk] | ((uint64_t)tp[2 * kk + 1] << 32);
+                    vm = (uint64_t)tm[2 * kk] | ((uint64_t)tm[2 * kk + 1] << 32);
+                }
+            tiemask[(uint64_t)k * bv.stride + i] = vp;
+            tiemask[(uint64_t)(half + k) * bv.stride + i] = vm;
+        }
+    }
+}
+
+}  // namespace
+
+namespace fc2 {
+
+void launch_scan32(int nq, bool nt, unsigned grid, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+                   const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
+#define FC2_L32(NQV, NTV) \
+    hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV>), dim3(grid), dim3(kBlock), 0, s, p, g, b, out, tiemask, tw)
+    if (nq <= 4) { if (nt) FC2_L32(4, true); else FC2_L32(4, false); }
+    else if (nq <= 8) { if (nt) FC2_L32(8, true); else FC2_L32(8, false); }
+    else { if (nt) FC2_L32(16, true); else FC2_L32(16, false); }
+#undef FC2_L32
+}
+
+}  // namespace fc2

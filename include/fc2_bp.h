@@ -155,6 +155,11 @@ const char *fc2_last_error(void);
 /* Returns FC2_OK and the device count (0 on a host without GPUs is not an error). */
 int         fc2_device_count(int *count);
 
+/* Performance knobs (results never depend on them); used for A/B measurements. */
+#define FC2_TUNE_STREAM_NT 1   /* 1 (default): per-pair inputs/results use non-temporal loads/stores */
+#define FC2_TUNE_KERNEL32  2   /* 1 (default): 32-bit-word scan kernel; 0: 64-bit-word scan kernel */
+int         fc2_set_tuning(int key, int value);
+
 /* Largest l the register kernel handles (longer reads go to the byte kernel). */
 int         fc2_max_fast_l(void);
 /* Words per pair for the chosen max l: rw (read planes), nw (read N plane),

@@ -1,0 +1,64 @@
+#!/usr/bin/env python
+"""Interleaved A/B timing of bp_scan_kernel tuning knobs in ONE process (guide §5.4 rule 24).
+
+usage: python scripts/ab_kernel.py [--workload hg19|cdr1as] [--pairs N] [--rounds R] [--reps K]
+Prints one JSON line per variant: median / min kernel ms over rounds, pairs/s.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workload", default="hg19")
+    ap.add_argument("--pairs", type=int, default=50_000_000)
+    ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--variants", default="k32nt1,k64nt1",
+                    help="comma list of k32|k64 + nt1|nt0 (FC2_TUNE_KERNEL32 / FC2_TUNE_STREAM_NT)")
+    a = ap.parse_args()
+    import torch
+    import bench
+    from find_circ2_amd import scan, _native as N
+    dev = torch.device("cuda", 0)
+    args = argparse.Namespace(workload=a.workload, pairs=a.pairs, read_len=100)
+    opt, g, b = bench.build_workload(args, 0, dev)
+    out = scan(opt, g, b)
+    torch.cuda.synchronize()
+    ref = out.results[:b.n].clone()
+    variants = a.variants.split(",")
+
+    def apply(v):
+        N.lib().fc2_set_tuning(1, 0 if "nt0" in v else 1)
+        N.lib().fc2_set_tuning(2, 0 if "k64" in v else 1)
+
+    times = {v: [] for v in variants}
+    stream = torch.cuda.current_stream(dev)
+    for r in range(a.rounds):
+        for v in variants:
+            apply(v)
+            scan(opt, g, b, out=out)
+            torch.cuda.synchronize()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record(stream)
+            for _ in range(a.reps):
+                scan(opt, g, b, out=out)
+            e.record(stream)
+            torch.cuda.synchronize()
+            times[v].append(s.elapsed_time(e) / a.reps)
+            assert torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
+    for v in variants:
+        t = np.array(times[v])
+        print(json.dumps({"variant": v, "workload": a.workload, "pairs": b.n, "median_ms": round(float(np.median(t)), 4),
+                          "min_ms": round(float(t.min()), 4), "pairs_per_s": round(b.n / (np.median(t) * 1e-3), 1)}))
+
+
+if __name__ == "__main__":
+    main()
