@@ -76,13 +76,8 @@ def barrier(ws):
 
 
 def max_over_ranks(x: float, ws: int, dev) -> float:
-    if ws == 1:
-        return x
-    import torch
-    import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    from find_circ2_amd.shard import max_over_ranks as _mor   # gloo-tested helper (tests/test_shard_gloo.py)
+    return x if ws == 1 else _mor(x, device=dev)
 
 
 def build_workload(args, rank, dev):

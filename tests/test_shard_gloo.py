@@ -1,0 +1,78 @@
+"""world_size-2 gloo tests (CPU) of the multi-GPU sharding logic (find_circ2_amd/shard.py).
+
+Each rank "scans" its round-robin batches with a deterministic stand-in for the
+kernel (per-pair results are a pure function of the pair, as find_breakpoints
+is), results are gathered to rank 0 and merged in input order; the merged array
+must equal a sequential single-process scan.  The timing max-over-ranks used by
+bench.py is checked on gloo too.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from find_circ2_amd import shard
+
+
+def fake_scan(pairs: np.ndarray) -> np.ndarray:
+    # any pure per-pair function stands in for the kernel (8-byte records)
+    x = pairs.astype(np.uint64)
+    return (x * np.uint64(0x9E3779B97F4A7C15)) ^ (x >> np.uint64(7))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, n, batch, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pairs = np.arange(n, dtype=np.int64) * 31 + 7
+    mine = shard.my_batches(n, batch, rank, world)
+    local = [(k, fake_scan(pairs[s:e])) for k, s, e in mine]
+    merged = shard.gather_ordered(local, len(shard.batch_bounds(n, batch)))
+    t = shard.max_over_ranks(float(rank + 1))
+    if rank == 0:
+        q.put((merged, t))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n,batch", [(1000, 64), (10, 100), (999, 1), (0, 8)])
+def test_gloo_two_ranks_ordered_merge(n, batch):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    merged, t = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    expect = fake_scan(np.arange(n, dtype=np.int64) * 31 + 7)
+    assert np.array_equal(merged, expect)
+    assert t == 2.0
+
+
+def test_batches_cover_and_partition():
+    for n, batch, world in [(1000, 64, 8), (7, 3, 2), (0, 5, 4)]:
+        seen = []
+        for r in range(world):
+            seen += [(s, e) for _, s, e in shard.my_batches(n, batch, r, world)]
+        seen.sort()
+        assert sum(e - s for s, e in seen) == n
+        assert all(seen[i][1] == seen[i + 1][0] for i in range(len(seen) - 1))
+    with pytest.raises(ValueError):
+        shard.ordered_merge([[(0, np.zeros(1))], [(0, np.zeros(1))]], 1)
+    with pytest.raises(ValueError):
+        shard.ordered_merge([[(0, np.zeros(1))]], 2)
