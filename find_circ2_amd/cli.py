@@ -1,0 +1,207 @@
+"""find_circ.py 1.99-compatible command line with the MI355X breakpoint search.
+
+    bwa mem -t<threads> [-p] -A2 -B10 -k 15 -T 1 $GENOME_INDEX reads.fastq.gz | \\
+        python -m find_circ2_amd.cli -G genome.fa -n sample -o outdir
+    python -m find_circ2_amd.cli [options] <bwa_mem_genome_alignments.bam|.sam>
+
+Same options (find_circ.py:383-413), output directory layout and file formats
+(circ_splice_sites.bed, lin_splice_sites.bed, spliced_reads.fastq.gz,
+multi_events.tsv, test_results.tsv, run.log; find_circ.py:420-458).
+Unsupported: ``-S/--system`` (needs the absent ``byo`` library) and ``-B/--bam``
+(needs a BAM writer; spliced alignments are not written).  ``--stranded`` fails
+exactly like the reference (AttributeError in Hit.add, find_circ.py:532-533).
+"""
+from __future__ import annotations
+
+import gzip
+import io
+import logging
+import optparse
+import os
+import sys
+import traceback
+
+__version__ = "1.99"
+
+USAGE = """
+   bwa mem -t<threads> [-p] -A2 -B10 -k 15 -T 1 $GENOME_INDEX reads.fastq.gz | %prog [options]
+
+   OR:
+
+   %prog [options] <bwa_mem_genome_alignments.bam>
+"""
+
+
+def build_parser() -> optparse.OptionParser:
+    p = optparse.OptionParser(usage=USAGE)
+    a = p.add_option
+    a("-v", "--version", dest="version", action="store_true", default=False, help="get version information")
+    a("-S", "--system", dest="system", type=str, default="", help="model system database (needs byo; unsupported)")
+    a("-G", "--genome", dest="genome", type=str, default="", help="path to genome (one multichromosome FASTA file)")
+    a("", "--known-circ", dest="known_circ", type=str, default="", help="file with known circRNA junctions (BED6)")
+    a("", "--known-lin", dest="known_lin", type=str, default="", help="file with known linear splice junctions (BED6)")
+    a("-o", "--output", dest="output", default="find_circ_run", help="where to store output")
+    a("-q", "--silent", dest="silent", default=False, action="store_true", help="suppress normal output to stdout")
+    a("", "--stdout", dest="stdout", default=None, choices=['circs', 'lins', 'reads', 'multi', 'test'],
+      help="direct chosen type of output (circs, lins, reads, multi) to stdout instead of file")
+    a("-n", "--name", dest="name", default="unknown", help="tissue/sample name to use (default='unknown')")
+    a("", "--min-uniq-qual", dest="min_uniq_qual", type=int, default=2, help="minimal uniqness for anchor alignments")
+    a("-a", "--anchor", dest="asize", type=int, default=15, help="anchor size (default=15)")
+    a("-m", "--margin", dest="margin", type=int, default=2, help="maximum nts the BP may reside within a segment")
+    a("-d", "--max-mismatch", dest="maxdist", type=int, default=2, help="maximum mismatches in segment extensions")
+    a("", "--short-threshold", dest="short_threshold", type=int, default=100, help="span below which a circ is SHORT")
+    a("", "--huge-threshold", dest="huge_threshold", type=int, default=100000, help="span above which it is HUGE")
+    a("", "--debug", dest="debug", default=False, action="store_true", help="debug output (not implemented)")
+    a("", "--profile", dest="profile", default=False, action="store_true", help="run under cProfile")
+    a("", "--non-canonical", dest="noncanonical", default=False, action="store_true", help="relax GU/AG")
+    a("", "--all-hits", dest="allhits", default=False, action="store_true", help="report each tied hit")
+    a("", "--stranded", dest="stranded", default=False, action="store_true", help="reads are stranded")
+    a("", "--strand-pref", dest="strandpref", default=False, action="store_true", help="prefer matching strand")
+    a("", "--half-unique", dest="halfunique", default=False, action="store_true", help="one unique anchor suffices")
+    a("", "--report-nobridges", dest="report_nobridges", default=False, action="store_true",
+      help="also report junctions lacking a uniquely bridged read")
+    a("-B", "--bam", dest="bam", default=False, action="store_true", help="store anchor alignments (unsupported)")
+    a("-t", "--throughput", dest="throughput", default=False, action="store_true", help="print throughput to stderr")
+    a("", "--chunk-size", dest="chunksize", type=int, default=100000, help="reads per chunk (default=100000)")
+    a("", "--noop", dest="noop", default=False, action="store_true", help="only process the alignment stream")
+    a("", "--test", dest="test", default=False, action="store_true", help="compare to splicing encoded in read names")
+    a("", "--no-linear", dest="nolinear", default=False, action="store_true", help="skip linear junctions")
+    a("", "--no-multi", dest="multi_events", default=True, action="store_false", help="do not record multi-events")
+    a("", "--device", dest="device", default="cuda:0", help="HIP device (find_circ2_amd extension)")
+    return p
+
+
+def gpu_evaluator(genome, hp_options):
+    """evaluate(spans): one batched GPU scan; per-span results or the reference's exception."""
+    from . import _native as N
+    from .hotpath import PairBatch, decode_splices, scan
+    missing = 0xFFFFFFFF
+
+    def evaluate(spans):
+        idx = [genome.chrom_index_or_missing(s.chrom) for s in spans]
+        flags = [((N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.strand == '-' else 0) |
+                  (N.PAIR_SKIP if c == missing else 0)) for s, c in zip(spans, idx)]
+        b = PairBatch.pack(hp_options, genome, [s.read_part for s in spans], [s.align_A.pos for s in spans],
+                           [s.align_B.aend for s in spans], [0 if c == missing else c for c in idx], flags)
+        out = scan(hp_options, genome, b)
+        res = decode_splices(hp_options, genome, b, out, spans, raise_errors=False)
+        for s, r, c in zip(spans, res, idx):
+            s.result = KeyError(s.chrom) if c == missing else r   # indexed_fasta.get_data, find_circ.py:193
+    return evaluate
+
+
+def main(argv=None, evaluator_factory=None) -> int:
+    parser = build_parser()
+    options, args = parser.parse_args(argv)
+    if options.version:
+        print("find_circ.py version {0}\n\n(c) Marvin Jens 2012-2016.\nCheck http://www.circbase.org for more "
+              "information.\n(MI355X breakpoint search: find_circ2_amd)".format(__version__))
+        return 0
+    if not os.path.isdir(options.output):
+        os.makedirs(options.output)
+    log_h = logging.FileHandler(os.path.join(options.output, "run.log"), mode="w")
+    log_h.setFormatter(logging.Formatter('%(asctime)-20s\t%(levelname)s\t%(name)s\t%(message)s'))
+    root = logging.getLogger()
+    root.handlers = [log_h]
+    root.setLevel(logging.INFO)
+    logger = logging.getLogger('find_circ')
+    logger.info("find_circ {0} invoked as '{1}'".format(__version__, " ".join(sys.argv)))
+    if options.system:
+        sys.stderr.write("-S/--system needs the byo library, which is not available\n")
+        return 1
+    if not options.genome:
+        print("need to specify either model system database (-S) or genome FASTA file (-G).")
+        return 1
+
+    from .caller import Caller, CallerOptions
+    from .hotpath import Options as HPOptions
+    from .samio import AlignmentFile
+
+    out = {"circs": open(os.path.join(options.output, "circ_splice_sites.bed"), "w"),
+           "lins": open(os.path.join(options.output, "lin_splice_sites.bed"), "w"),
+           "reads": gzip.open(os.path.join(options.output, "spliced_reads.fastq.gz"), "wt"),
+           "multi": open(os.path.join(options.output, "multi_events.tsv"), "w"),
+           "test": open(os.path.join(options.output, "test_results.tsv"), "w") if options.test else None}
+    if options.stdout:
+        out[options.stdout].write('# redirected to stdout\n')
+        logger.info('redirected {0} to stdout'.format(options.stdout))
+        out[options.stdout] = sys.stdout
+
+    hp = HPOptions(asize=options.asize, margin=options.margin, maxdist=options.maxdist,
+                   noncanonical=options.noncanonical, strandpref=options.strandpref, allhits=options.allhits)
+    if evaluator_factory is None:
+        from .genome import Genome
+        try:
+            genome = Genome.from_fasta(options.genome, device=options.device, write_index=True)
+        except Exception as ex:        # GenomeAccessor dummy mode (find_circ.py:340-345)
+            if "cannot open" not in str(ex):
+                raise
+            logging.getLogger("GenomeAccessor").warning(
+                "Could not access '%s'. Switching to dummy mode (only Ns)" % options.genome)
+            genome = Genome.dummy_genome(device=options.device)
+        evaluate = gpu_evaluator(genome, hp)
+    else:
+        evaluate = evaluator_factory(options, hp)
+
+    if args:
+        logger.info('reading from {0}'.format(args[0]))
+        sam = AlignmentFile(args[0], "r" if args[0].endswith("sam") else "rb")
+    else:
+        logger.info('reading from stdin')
+        sam = AlignmentFile("-", "r")
+
+    cache = {}
+
+    def chrom_of(a):                  # fast_chrom_lookup (find_circ.py:471-477)
+        t = a.tid
+        if t not in cache:
+            if t < 0:
+                raise ValueError("reference id %d out of range" % t)
+            cache[t] = sam.getrname(t)
+        return cache[t]
+
+    copts = CallerOptions(**{k: getattr(options, k) for k in (
+        "name", "min_uniq_qual", "asize", "margin", "maxdist", "short_threshold", "huge_threshold", "noncanonical",
+        "allhits", "stranded", "strandpref", "halfunique", "report_nobridges", "throughput", "chunksize", "noop",
+        "test", "nolinear", "multi_events", "debug")})
+    caller = Caller(copts, evaluate, chrom_of, out, options.known_circ, options.known_lin)
+    try:
+        if options.profile:
+            import cProfile
+            prof = cProfile.Profile()
+            seconds = prof.runcall(caller.run, sam)
+            prof.print_stats()
+        else:
+            seconds = caller.run(sam)
+    except KeyboardInterrupt:
+        logging.warning("KeyboardInterrupt by user while processing input")
+        seconds = 0.0
+    except Exception:
+        logging.error("Unhandled exception raised while processing input")
+        exc = traceback.format_exc()
+        logging.error(exc)
+        sys.stderr.write(exc)
+        return 1
+    M = caller.n_reads / 1e6
+    krps = caller.n_reads / seconds / 1000. if seconds > 0 else 0.0
+    txt = "processed {0:.2f}M (paired or single end) reads in {1:.1f} minutes (overall {2:.2f}k reads/second on " \
+          "average)".format(M, seconds / 60., krps)
+    logger.info(txt)
+    if not options.silent and not options.stdout:
+        print("#", txt)
+        print("# results stored in '{0}'".format(options.output))
+    logger.info('run finished')
+    for key in sorted(caller.N):
+        logger.info('{0}={1}'.format(key, caller.N[key]))
+    logger.info('breakpoint search: {0} spans, {1:.3f} s incl. pack/transfer/decode'.format(
+        caller.n_spans_evaluated, caller.gpu_seconds))
+    caller.circ_splices.store(out["circs"])
+    caller.linear_splices.store(out["lins"])
+    for k, fh in out.items():
+        if fh is not None and fh is not sys.stdout:
+            fh.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

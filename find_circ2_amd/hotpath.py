@@ -361,12 +361,18 @@ def raise_reference_errors(options: Options, host_pairs: np.ndarray, res: np.nda
 
 
 def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: ScanOutput,
-                   spans: Sequence = None) -> List[List[Splice]]:
-    """Per pair, the list ``find_breakpoints`` returns (ties, find_circ.py:961-974)."""
+                   spans: Sequence = None, raise_errors: bool = True) -> List[List[Splice]]:
+    """Per pair, the list ``find_breakpoints`` returns (ties, find_circ.py:961-974).
+
+    With ``raise_errors=False`` a pair the reference would fail on gets the
+    exception instance instead of a list, so a caller that evaluated pairs
+    speculatively can raise it exactly where the reference calls the method.
+    """
     hp = batch.fetch_host_pairs()
     res = out.host(batch.n)
     evaluated = (hp["flags"] & N.PAIR_SKIP) == 0
-    raise_reference_errors(options, hp, res, evaluated)
+    if raise_errors:
+        raise_reference_errors(options, hp, res, evaluated)
     a = first_tie_arrays(options, hp, res)
     e = options.eff_a
     tm = None
@@ -375,6 +381,11 @@ def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: Scan
     result: List[List[Splice]] = []
     for i in range(batch.n):
         span = spans[i] if spans is not None else None
+        if evaluated[i] and (a["err_key"][i] or a["err_win"][i]):
+            result.append(KeyError("splice signal with a byte outside ACGTN (find_circ.py:927)") if a["err_key"][i]
+                          else BreakpointError("genome window outside get_data's defined range "
+                                               "(find_circ.py:194-211)"))
+            continue
         if not a["hit"][i] or not evaluated[i]:
             result.append([])
             continue

@@ -1,0 +1,277 @@
+"""SAM / BAM input for the caller (pysam is not available in this image).
+
+Provides the subset of ``pysam.AlignedSegment`` / ``pysam.Samfile`` that
+find_circ.py reads (find_circ.py:461-477, 809-852, 976-1140, 1442-1486):
+``qname, flag, is_* flags, tid, pos, aend, cigar, seq, query, qual, tags,
+get_tag, has_tag`` and ``getrname``.  Semantics follow the SAM spec as pysam
+exposes it:
+
+* ``pos`` 0-based; ``aend`` = pos + reference span (M/D/N/=/X), None if unmapped
+* ``cigar`` = list of (op, length), op codes M0 I1 D2 N3 S4 H5 P6 =7 X8
+* ``seq`` = SAM SEQ (None for '*'); ``query`` = SEQ without soft clips
+* ``qual`` = SAM QUAL string (None for '*')
+"""
+from __future__ import annotations
+
+import gzip
+import io
+import re
+import struct
+import sys
+from typing import Dict, Iterator, List, Optional, Tuple
+
+_CIGAR_RE = re.compile(r"(\d+)([MIDNSHP=X])")
+_CIGAR_OPS = {"M": 0, "I": 1, "D": 2, "N": 3, "S": 4, "H": 5, "P": 6, "=": 7, "X": 8}
+_REF_OPS = (0, 2, 3, 7, 8)
+
+
+class AlignedSegment:
+    __slots__ = ("qname", "flag", "tid", "pos", "mapq", "cigar", "seq", "qual", "tags", "_aend")
+
+    def __init__(self, qname, flag, tid, pos, mapq, cigar, seq, qual, tags):
+        self.qname = qname
+        self.flag = flag
+        self.tid = tid
+        self.pos = pos
+        self.mapq = mapq
+        self.cigar = cigar
+        self.seq = seq
+        self.qual = qual
+        self.tags = tags
+        self._aend = -1
+
+    # flags (SAM spec §1.4)
+    is_paired = property(lambda self: bool(self.flag & 0x1))
+    is_proper_pair = property(lambda self: bool(self.flag & 0x2))
+    is_unmapped = property(lambda self: bool(self.flag & 0x4))
+    mate_is_unmapped = property(lambda self: bool(self.flag & 0x8))
+    is_reverse = property(lambda self: bool(self.flag & 0x10))
+    mate_is_reverse = property(lambda self: bool(self.flag & 0x20))
+    is_read1 = property(lambda self: bool(self.flag & 0x40))
+    is_read2 = property(lambda self: bool(self.flag & 0x80))
+    is_secondary = property(lambda self: bool(self.flag & 0x100))
+    is_qcfail = property(lambda self: bool(self.flag & 0x200))
+    is_duplicate = property(lambda self: bool(self.flag & 0x400))
+    is_supplementary = property(lambda self: bool(self.flag & 0x800))
+
+    @property
+    def aend(self):
+        if self._aend == -1:
+            if self.is_unmapped or not self.cigar:
+                self._aend = None
+            else:
+                self._aend = self.pos + sum(n for op, n in self.cigar if op in _REF_OPS)
+        return self._aend
+
+    @property
+    def query(self):
+        """Aligned part of SEQ (soft clips removed), pysam's query_alignment_sequence."""
+        if self.seq is None:
+            return None
+        s = 0
+        for op, n in self.cigar:
+            if op == 4:
+                s += n
+            elif op != 5:
+                break
+        e = len(self.seq)
+        for op, n in reversed(self.cigar):
+            if op == 4:
+                e -= n
+            elif op != 5:
+                break
+        return self.seq[s:e]
+
+    def get_tag(self, tag):
+        for t, v in self.tags:
+            if t == tag:
+                return v
+        raise KeyError("tag '%s' not present" % tag)
+
+    def has_tag(self, tag):
+        return any(t == tag for t, _ in self.tags)
+
+    def __repr__(self):
+        return "AlignedSegment(%s flag=%d tid=%d pos=%d cigar=%s)" % (self.qname, self.flag, self.tid, self.pos,
+                                                                      self.cigar)
+
+
+def parse_cigar(s: str) -> List[Tuple[int, int]]:
+    if s == "*":
+        return []
+    return [(_CIGAR_OPS[op], int(n)) for n, op in _CIGAR_RE.findall(s)]
+
+
+def _tag_value(typ: str, val: str):
+    if typ == "i":
+        return int(val)
+    if typ == "f":
+        return float(val)
+    if typ == "B":
+        parts = val.split(",")
+        conv = float if parts[0] == "f" else int
+        return [conv(x) for x in parts[1:]]
+    return val            # Z, A, H
+
+
+class AlignmentFile:
+    """Sequential reader of SAM text (path or '-' for stdin) or BAM (BGZF)."""
+
+    def __init__(self, path: str, mode: str = "r"):
+        self.path = path
+        self.references: List[str] = []
+        self.lengths: List[int] = []
+        self.header_lines: List[str] = []
+        self._tid: Dict[str, int] = {}
+        self._bam = "b" in mode
+        if path == "-":
+            raw = sys.stdin.buffer
+        else:
+            raw = open(path, "rb")
+        self._raw = raw
+        if self._bam:
+            self._fh = gzip.GzipFile(fileobj=raw, mode="rb")
+            self._read_bam_header()
+        else:
+            self._fh = io.TextIOWrapper(raw, encoding="latin-1", newline="\n")
+            self._pending = None
+            self._read_sam_header()
+
+    # ------------------------------------------------------------------ SAM
+    def _read_sam_header(self):
+        for line in self._fh:
+            if not line.startswith("@"):
+                self._pending = line
+                break
+            self.header_lines.append(line.rstrip("\n"))
+            if line.startswith("@SQ"):
+                d = dict(kv.split(":", 1) for kv in line.rstrip("\r\n").split("\t")[1:] if ":" in kv)
+                self._tid[d["SN"]] = len(self.references)
+                self.references.append(d["SN"])
+                self.lengths.append(int(d.get("LN", 0)))
+
+    def _parse_sam(self, line: str) -> AlignedSegment:
+        f = line.rstrip("\r\n").split("\t")
+        if len(f) < 11:
+            raise ValueError("malformed SAM line: %r" % line[:80])
+        rname = f[2]
+        tid = -1 if rname == "*" else self._tid.get(rname, -1)
+        tags = []
+        for t in f[11:]:
+            tg, typ, val = t.split(":", 2)
+            tags.append((tg, _tag_value(typ, val)))
+        return AlignedSegment(f[0], int(f[1]), tid, int(f[3]) - 1, int(f[4]), parse_cigar(f[5]),
+                              None if f[9] == "*" else f[9], None if f[10] == "*" else f[10], tags)
+
+    # ------------------------------------------------------------------ BAM
+    def _read(self, n):
+        b = self._fh.read(n)
+        if len(b) != n:
+            raise EOFError
+        return b
+
+    def _read_bam_header(self):
+        if self._read(4) != b"BAM\1":
+            raise ValueError("not a BAM file")
+        l_text, = struct.unpack("<i", self._read(4))
+        text = self._read(l_text).decode("latin-1")
+        self.header_lines = [l for l in text.split("\n") if l]
+        n_ref, = struct.unpack("<i", self._read(4))
+        for _ in range(n_ref):
+            l_name, = struct.unpack("<i", self._read(4))
+            name = self._read(l_name)[:-1].decode("latin-1")
+            l_ref, = struct.unpack("<i", self._read(4))
+            self._tid[name] = len(self.references)
+            self.references.append(name)
+            self.lengths.append(l_ref)
+
+    _SEQ = "=ACMGRSVTWYHKDBN"
+
+    def _parse_bam(self, buf: bytes) -> AlignedSegment:
+        (ref_id, pos, l_name, mapq, _bin, n_cig, flag, l_seq, _nref, _npos, _tlen) = struct.unpack_from(
+            "<iiBBHHHiiii", buf, 0)
+        o = 32
+        qname = buf[o:o + l_name - 1].decode("latin-1")
+        o += l_name
+        cig = struct.unpack_from("<%dI" % n_cig, buf, o)
+        o += 4 * n_cig
+        cigar = [(c & 0xF, c >> 4) for c in cig]
+        nb = (l_seq + 1) // 2
+        sb = buf[o:o + nb]
+        o += nb
+        seq = "".join(self._SEQ[b >> 4] + self._SEQ[b & 0xF] for b in sb)[:l_seq] if l_seq else None
+        qb = buf[o:o + l_seq]
+        o += l_seq
+        qual = None if (l_seq == 0 or qb[0] == 0xFF) else "".join(chr(q + 33) for q in qb)
+        tags = []
+        while o < len(buf):
+            tg = buf[o:o + 2].decode("latin-1")
+            typ = chr(buf[o + 2])
+            o += 3
+            if typ in "cCsSiI":
+                fmt = {"c": "<b", "C": "<B", "s": "<h", "S": "<H", "i": "<i", "I": "<I"}[typ]
+                v, = struct.unpack_from(fmt, buf, o)
+                o += struct.calcsize(fmt)
+            elif typ == "f":
+                v, = struct.unpack_from("<f", buf, o)
+                o += 4
+            elif typ == "A":
+                v = chr(buf[o])
+                o += 1
+            elif typ in "ZH":
+                e = buf.index(b"\0", o)
+                v = buf[o:e].decode("latin-1")
+                o = e + 1
+            elif typ == "B":
+                sub = chr(buf[o])
+                cnt, = struct.unpack_from("<i", buf, o + 1)
+                fmt = {"c": "b", "C": "B", "s": "h", "S": "H", "i": "i", "I": "I", "f": "f"}[sub]
+                v = list(struct.unpack_from("<%d%s" % (cnt, fmt), buf, o + 5))
+                o += 5 + cnt * struct.calcsize(fmt)
+            else:
+                raise ValueError("bad BAM tag type %r" % typ)
+            tags.append((tg, v))
+        return AlignedSegment(qname, flag, ref_id, pos, mapq, cigar, seq, qual, tags)
+
+    # ------------------------------------------------------------------ api
+    def __iter__(self) -> Iterator[AlignedSegment]:
+        if self._bam:
+            while True:
+                try:
+                    n, = struct.unpack("<i", self._read(4))
+                except EOFError:
+                    return
+                yield self._parse_bam(self._read(n))
+        else:
+            if self._pending is not None:
+                line, self._pending = self._pending, None
+                if line.strip():
+                    yield self._parse_sam(line)
+            for line in self._fh:
+                if line.strip():
+                    yield self._parse_sam(line)
+
+    def getrname(self, tid: int) -> str:
+        return self.references[tid]
+
+    def close(self):
+        try:
+            self._fh.close()
+        finally:
+            if self._raw is not sys.stdin.buffer:
+                self._raw.close()
+
+
+def sam_line(rec: AlignedSegment, references: List[str]) -> str:
+    """Format a record back to SAM text (used by tests and the -B writer)."""
+    cig = "".join("%d%s" % (n, "MIDNSHP=X"[op]) for op, n in rec.cigar) or "*"
+    tags = []
+    for t, v in rec.tags:
+        if isinstance(v, int):
+            tags.append("%s:i:%d" % (t, v))
+        elif isinstance(v, float):
+            tags.append("%s:f:%g" % (t, v))
+        else:
+            tags.append("%s:Z:%s" % (t, v))
+    return "\t".join([rec.qname, str(rec.flag), references[rec.tid] if rec.tid >= 0 else "*", str(rec.pos + 1),
+                      str(rec.mapq), cig, "*", "0", "0", rec.seq or "*", rec.qual or "*"] + tags)
