@@ -58,15 +58,25 @@ def parse():
 
 
 def setup_dist(args):
+    """One process per GPU.  The hot path exchanges nothing between ranks, so the only
+    collectives (timing barrier, max over ranks) run on a host gloo group by default;
+    FC2_DIST_BACKEND=nccl selects RCCL instead.  With fewer GPUs than ranks (rehearsal
+    on a 1-GPU box) ranks share devices round-robin."""
     import torch
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ndev = max(1, torch.cuda.device_count())
+    dev_index = local % ndev
     if ws > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return ws, rank, local
+        torch.cuda.set_device(dev_index)
+        backend = os.environ.get("FC2_DIST_BACKEND", "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group("gloo")
+    return ws, rank, dev_index
 
 
 def barrier(ws):

@@ -127,3 +127,19 @@ def test_cli_stranded_fails_like_reference(tmp_path):
     fa = os.path.join(GOLDEN, "test_ref.fa")
     rc, out = run_cli(tmp_path, fa, _reads(os.path.join(GOLDEN, "test_reads.fa")), extra=["--stranded"])
     assert rc == 1     # AttributeError in Hit.add (find_circ.py:532-533) -> sys.exit(1)
+
+
+def test_cmp_bed_semantics(tmp_path, capsys):
+    from find_circ2_amd import cmp_bed
+    fa = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    rc, out = run_cli(tmp_path, fa, _reads(os.path.join(GOLDEN, "cdr1as_reads.fa")))
+    mine = os.path.join(out, "circ_splice_sites.bed")
+    ref = os.path.join(GOLDEN, "cdr1as_reference.bed")
+    assert cmp_bed.main([ref, mine]) == 0
+    cap = capsys.readouterr()
+    assert "files contain identical splice sites!" in cap.err and "overlap\t1" in cap.err
+    other = tmp_path / "other.bed"
+    other.write_text("#h\nCDR1as_locus\t728\t2214\tx\t1\t+\n")
+    assert not cmp_bed.compare(ref, str(other))
+    cap = capsys.readouterr()
+    assert cap.out.startswith("MISSING\tCDR1as_locus\t728\t2213") and "input2_not_in_input1\t1" in cap.err
