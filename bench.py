@@ -72,10 +72,22 @@ def setup_dist(args):
         import torch.distributed as dist
         torch.cuda.set_device(dev_index)
         backend = os.environ.get("FC2_DIST_BACKEND", "gloo")
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
-        else:
-            dist.init_process_group("gloo")
+        # the process-group libraries log connection chatter on fd 1; keep stdout for the JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+            else:
+                dist.init_process_group("gloo")
+            dist.barrier()
+        finally:
+            import ctypes
+            ctypes.CDLL(None).fflush(None)   # C stdio buffers of the C++ libraries too
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     return ws, rank, dev_index
 
 
