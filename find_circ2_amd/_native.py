@@ -88,7 +88,21 @@ EXPORTED = [
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill",
     "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_synth_pairs_launch",
+    # include/fc2_ingest.h
+    "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
+    "fc2_ingest_next",
 ]
+
+
+class IngestParams(ctypes.Structure):
+    _fields_ = [("asize", ctypes.c_int32), ("nolinear", ctypes.c_uint8), ("noop", ctypes.c_uint8),
+                ("_pad", ctypes.c_uint8 * 2)]
+
+
+class IngestCounts(ctypes.Structure):
+    _fields_ = [("n_reads", ctypes.c_uint64), ("total_mates", ctypes.c_uint64), ("unmapped_reads", ctypes.c_uint64),
+                ("unspliced_mates", ctypes.c_uint64), ("seg_too_short_skip", ctypes.c_uint64),
+                ("records", ctypes.c_uint64), ("handed_back", ctypes.c_uint64)]
 
 _lib = None
 
@@ -96,8 +110,8 @@ _lib = None
 def build(force: bool = False) -> str:
     srcdir = os.path.join(_HERE, "csrc")
     srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_scan32.h", "fc2_host.cpp",
-                                              "fc2_common.h", "Makefile")]
-    srcs.append(os.path.join(os.path.dirname(_HERE), "include", "fc2_bp.h"))
+                                              "fc2_ingest.cpp", "fc2_common.h", "Makefile")]
+    srcs += [os.path.join(os.path.dirname(_HERE), "include", h) for h in ("fc2_bp.h", "fc2_ingest.h")]
     newest = max(os.path.getmtime(s) for s in srcs)
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
         subprocess.check_call(["make", "-s", "-C", srcdir])
@@ -140,6 +154,13 @@ def lib() -> ctypes.CDLL:
         "fc2_coarse_launch": (ctypes.c_int, [vp, vp, u64, vp]),
         "fc2_synth_pairs_launch": (ctypes.c_int, [P(Params), P(SynthCfg), P(GenomeView), vp, u64, vp, vp, u32,
                                                   vp, u32, u64, vp, vp]),
+        "fc2_ingest_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(vp)]),
+        "fc2_ingest_close": (None, [vp]),
+        "fc2_ingest_n_refs": (ctypes.c_int, [vp]),
+        "fc2_ingest_ref_name": (ctypes.c_char_p, [vp, ctypes.c_int]),
+        "fc2_ingest_header": (ctypes.c_char_p, [vp]),
+        "fc2_ingest_next": (ctypes.c_int, [vp, P(IngestParams), u64, P(IngestCounts), P(ctypes.c_void_p), P(u64),
+                                           P(u64), P(ctypes.c_int)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

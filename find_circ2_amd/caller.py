@@ -664,3 +664,44 @@ class Caller:
         if o.throughput:
             stderr.write('\n')
         return time.time() - t0
+
+    def run_native(self, ingest, stderr=sys.stderr):
+        """Same loop with the native ingest (include/fc2_ingest.h): only fragments carrying
+        anchor pairs come back as records; the grouping counters of the others come from C++."""
+        o = self.o
+        t0 = time.time()
+        t_last = t0
+        scratch = defaultdict(float)      # grouping counters of handed-back fragments are counted natively
+        pending: List[Fragment] = []
+        last_reads = 0
+        while not ingest.eof:
+            for recs in ingest.next_chunk(o.asize, o.nolinear, o.noop, o.chunksize):
+                for _, mate1, mate2 in group_alignments(recs, scratch):
+                    frag = Fragment(mate2.primary.qname, mate1, mate2)
+                    if mate1:
+                        self._process_mate(mate1, frag)
+                    if mate2:
+                        self._process_mate(mate2, frag)
+                    if not frag.circ and o.nolinear:
+                        continue
+                    if frag.circ or frag.lin:
+                        pending.append(frag)
+                if len(pending) >= o.chunksize:
+                    self._flush(pending)
+            self.n_reads = int(ingest.counts.n_reads)
+            if o.throughput and self.n_reads // o.chunksize > last_reads // o.chunksize:
+                t1 = time.time()
+                stderr.write("\rprocessed {0:.1f}M (paired-end) reads in {1:.1f} minutes ({2:.2f}k reads/second)"
+                             "       \r".format(self.n_reads / 1e6, (t1 - t0) / 60.,
+                                                (self.n_reads - last_reads) / max(t1 - t_last, 1e-9) / 1000.))
+                t_last, last_reads = t1, self.n_reads
+        self._flush(pending)
+        c = ingest.counts
+        for key, v in (("total_mates", c.total_mates), ("unmapped_reads", c.unmapped_reads),
+                       ("unspliced_mates", c.unspliced_mates), ("seg_too_short_skip", c.seg_too_short_skip)):
+            if v:
+                self.N[key] += float(v)
+        self.n_reads = int(c.n_reads)
+        if o.throughput:
+            stderr.write('\n')
+        return time.time() - t0

@@ -68,6 +68,8 @@ def build_parser() -> optparse.OptionParser:
     a("", "--no-linear", dest="nolinear", default=False, action="store_true", help="skip linear junctions")
     a("", "--no-multi", dest="multi_events", default=True, action="store_false", help="do not record multi-events")
     a("", "--device", dest="device", default="cuda:0", help="HIP device (find_circ2_amd extension)")
+    a("", "--python-ingest", dest="python_ingest", default=False, action="store_true",
+      help="parse and group alignments in Python instead of the native ingest (find_circ2_amd extension)")
     return p
 
 
@@ -143,12 +145,16 @@ def main(argv=None, evaluator_factory=None) -> int:
     else:
         evaluate = evaluator_factory(options, hp)
 
-    if args:
-        logger.info('reading from {0}'.format(args[0]))
-        sam = AlignmentFile(args[0], "r" if args[0].endswith("sam") else "rb")
+    path = args[0] if args else "-"
+    is_bam = bool(args) and not args[0].endswith("sam")          # find_circ.py:461-469
+    logger.info('reading from {0}'.format(args[0]) if args else 'reading from stdin')
+    if options.python_ingest:
+        sam = AlignmentFile(path, "rb" if is_bam else "r")
+        run = lambda: caller.run(sam)                              # noqa: E731
     else:
-        logger.info('reading from stdin')
-        sam = AlignmentFile("-", "r")
+        from .ingest import NativeIngest
+        sam = NativeIngest(path, is_bam)
+        run = lambda: caller.run_native(sam)                       # noqa: E731
 
     cache = {}
 
@@ -169,10 +175,10 @@ def main(argv=None, evaluator_factory=None) -> int:
         if options.profile:
             import cProfile
             prof = cProfile.Profile()
-            seconds = prof.runcall(caller.run, sam)
+            seconds = prof.runcall(run)
             prof.print_stats()
         else:
-            seconds = caller.run(sam)
+            seconds = run()
     except KeyboardInterrupt:
         logging.warning("KeyboardInterrupt by user while processing input")
         seconds = 0.0

@@ -1,0 +1,575 @@
+// fc2_ingest.cpp -- native SAM/BAM ingest: parse, group into fragments, form
+// anchor pairs; hand back only the fragments that carry pairs (include/fc2_ingest.h).
+//
+// Grouping follows collected_bwa_mem_segments (find_circ.py:1450-1486): the
+// first record always opens a mate; later unmapped records are counted and
+// skipped; a record continues the current mate if it has the same qname and
+// read1 flag, opens the other mate if the read1 flag differs, and otherwise
+// closes the fragment.  Pairing follows MateSegments.add_segment /
+// adjacent_segment_pairs / process_mate (:1039-1140, 1492-1527).
+#include <ctype.h>
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <string.h>
+#include <unistd.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/fc2_ingest.h"
+#include "fc2_common.h"
+
+namespace {
+
+struct Rec {
+    std::string text;      // SAM line (no newline)
+    std::string qname;
+    uint32_t flag = 0;
+    int32_t tid = -1;
+    int64_t pos = -1;
+    int64_t aend = -1;     // -1: None (unmapped / no cigar)
+    int32_t astart = 0;    // aligned_start_from_cigar (:1086-1097)
+    int32_t qlen = -1;     // len(query); -1: query is None (SEQ '*')
+    bool has_seq = false;
+    bool unmapped() const { return flag & 0x4; }
+    bool read1() const { return flag & 0x40; }
+    bool reverse() const { return flag & 0x10; }
+};
+
+struct Mate {
+    std::vector<Rec> recs;       // primary first, then every added segment (for hand-back)
+    std::vector<int> proper;     // indices into recs
+    bool valid = false;
+};
+
+// CIGAR helpers ------------------------------------------------------------
+struct CigarInfo {
+    int64_t ref_span = 0;
+    int32_t astart = 0, lead_s = 0, trail_s = 0;
+    bool any = false;
+};
+
+CigarInfo cigar_info(const std::vector<std::pair<int, int>> &ops) {
+    CigarInfo c;
+    c.any = !ops.empty();
+    bool stop = false;
+    for (auto &o : ops) {
+        if (o.first == 0 || o.first == 2 || o.first == 3 || o.first == 7 || o.first == 8) c.ref_span += o.second;
+        if (!stop) {
+            if (o.first == 4 || o.first == 5) c.astart += o.second;
+            else if (o.first == 0) stop = true;
+        }
+    }
+    for (auto &o : ops) {              // leading soft clips (hard clips skipped)
+        if (o.first == 4) c.lead_s += o.second;
+        else if (o.first != 5) break;
+    }
+    for (auto it = ops.rbegin(); it != ops.rend(); ++it) {
+        if (it->first == 4) c.trail_s += it->second;
+        else if (it->first != 5) break;
+    }
+    return c;
+}
+
+int cig_code(char c) {
+    switch (c) {
+        case 'M': return 0; case 'I': return 1; case 'D': return 2; case 'N': return 3; case 'S': return 4;
+        case 'H': return 5; case 'P': return 6; case '=': return 7; case 'X': return 8; default: return -1;
+    }
+}
+
+void finish_rec(Rec &r, const std::vector<std::pair<int, int>> &ops, int64_t seqlen) {
+    CigarInfo c = cigar_info(ops);
+    r.astart = c.astart;
+    r.aend = (r.unmapped() || !c.any) ? -1 : r.pos + c.ref_span;
+    r.qlen = r.has_seq ? (int32_t)(seqlen - c.lead_s - c.trail_s) : -1;
+}
+
+}  // namespace
+
+struct fc2_ingest {
+    int fd = -1;
+    bool bam = false;
+    bool eof_in = false;
+    // raw input buffer (SAM text or inflated BAM)
+    std::vector<char> buf;
+    size_t beg = 0, end = 0;
+    // zlib
+    z_stream zs{};
+    bool z_init = false;
+    std::vector<char> zin;
+    bool z_done = false;
+    // header
+    std::string header;
+    std::vector<std::string> refs;
+    std::unordered_map<std::string, int> tid_of;
+    // grouping state
+    bool started = false;
+    Mate current, other;
+    bool have_other = false;
+    uint64_t n_records = 0;
+    std::string out;
+    fc2_ingest_counts counts{};
+    bool finished = false;
+};
+
+namespace {
+
+// ---- input plumbing --------------------------------------------------------
+bool fill_raw(fc2_ingest *h, std::vector<char> &dst, size_t want) {
+    // append up to `want` bytes of raw file data to dst; false at EOF
+    size_t old = dst.size();
+    dst.resize(old + want);
+    ssize_t k;
+    do { k = read(h->fd, dst.data() + old, want); } while (k < 0 && errno == EINTR);
+    if (k <= 0) { dst.resize(old); return false; }
+    dst.resize(old + (size_t)k);
+    return true;
+}
+
+// make at least n bytes available in buf[beg..end); false if the input ends first
+bool ensure(fc2_ingest *h, size_t n) {
+    while (h->end - h->beg < n) {
+        if (h->beg > 0) {  // compact
+            memmove(h->buf.data(), h->buf.data() + h->beg, h->end - h->beg);
+            h->end -= h->beg;
+            h->beg = 0;
+        }
+        if (h->buf.size() < h->end + (1 << 22)) h->buf.resize(h->end + (1 << 22));
+        if (!h->bam) {
+            if (h->eof_in) return false;
+            ssize_t k;
+            do { k = read(h->fd, h->buf.data() + h->end, h->buf.size() - h->end); } while (k < 0 && errno == EINTR);
+            if (k <= 0) { h->eof_in = true; return false; }
+            h->end += (size_t)k;
+        } else {
+            if (h->z_done) return false;
+            // inflate more
+            if (h->zs.avail_in == 0) {
+                h->zin.clear();
+                if (!fill_raw(h, h->zin, 1 << 20)) { h->z_done = true; return false; }
+                h->zs.next_in = (Bytef *)h->zin.data();
+                h->zs.avail_in = (uInt)h->zin.size();
+            }
+            h->zs.next_out = (Bytef *)(h->buf.data() + h->end);
+            h->zs.avail_out = (uInt)(h->buf.size() - h->end);
+            int rc = inflate(&h->zs, Z_NO_FLUSH);
+            h->end = h->buf.size() - h->zs.avail_out;
+            if (rc == Z_STREAM_END) {
+                // concatenated gzip members (BGZF blocks): restart on the remaining input
+                if (inflateReset(&h->zs) != Z_OK) return false;
+            } else if (rc != Z_OK && rc != Z_BUF_ERROR) {
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
+// SAM: next line into `line` (without newline); false at EOF
+bool next_line(fc2_ingest *h, std::string &line) {
+    for (;;) {
+        const char *s = h->buf.data() + h->beg;
+        const char *nl = (const char *)memchr(s, '\n', h->end - h->beg);
+        if (nl) {
+            line.assign(s, nl);
+            h->beg = (size_t)(nl - h->buf.data()) + 1;
+            if (!line.empty() && line.back() == '\r') line.pop_back();
+            return true;
+        }
+        size_t have = h->end - h->beg;
+        if (!ensure(h, have + 1)) {
+            if (h->end > h->beg) {
+                line.assign(h->buf.data() + h->beg, h->end - h->beg);
+                h->beg = h->end;
+                if (!line.empty() && line.back() == '\r') line.pop_back();
+                return true;
+            }
+            return false;
+        }
+    }
+}
+
+int parse_sam_record(fc2_ingest *h, const std::string &line, Rec &r) {
+    // fields 1-11
+    size_t f[12];
+    int nf = 0;
+    f[nf++] = 0;
+    for (size_t i = 0; i < line.size() && nf < 12; ++i)
+        if (line[i] == '\t') f[nf++] = i + 1;
+    if (nf < 11) return fc2::fail(FC2_E_FORMAT, "malformed SAM line: " + line.substr(0, 80));
+    auto field = [&](int k) {
+        size_t b = f[k];
+        size_t e = (k + 1 < nf) ? f[k + 1] - 1 : line.size();
+        if (k + 1 >= nf) {
+            size_t t = line.find('\t', b);
+            if (t != std::string::npos) e = t;
+        }
+        return std::string(line, b, e - b);
+    };
+    r.text = line;
+    r.qname = field(0);
+    r.flag = (uint32_t)strtoul(field(1).c_str(), nullptr, 10);
+    std::string rn = field(2);
+    if (rn == "*") r.tid = -1;
+    else {
+        auto it = h->tid_of.find(rn);
+        r.tid = it == h->tid_of.end() ? -1 : it->second;
+    }
+    r.pos = strtoll(field(3).c_str(), nullptr, 10) - 1;
+    std::string cig = field(5);
+    std::vector<std::pair<int, int>> ops;
+    if (cig != "*") {
+        long n = 0;
+        for (char c : cig) {
+            if (c >= '0' && c <= '9') n = n * 10 + (c - '0');
+            else {
+                int code = cig_code(c);
+                if (code < 0) return fc2::fail(FC2_E_FORMAT, "bad CIGAR: " + cig);
+                ops.emplace_back(code, (int)n);
+                n = 0;
+            }
+        }
+    }
+    std::string seq = field(9);
+    r.has_seq = seq != "*";
+    finish_rec(r, ops, r.has_seq ? (int64_t)seq.size() : 0);
+    return FC2_OK;
+}
+
+void append_bam_tags(std::string &t, const uint8_t *p, const uint8_t *end) {
+    char tmp[64];
+    while (p + 3 <= end) {
+        t += '\t';
+        t.append((const char *)p, 2);
+        const char ty = (char)p[2];
+        p += 3;
+        auto ival = [&](long long v) { snprintf(tmp, sizeof tmp, ":i:%lld", v); t += tmp; };
+        switch (ty) {
+            case 'c': ival(*(const int8_t *)p); p += 1; break;
+            case 'C': ival(*(const uint8_t *)p); p += 1; break;
+            case 's': { int16_t v; memcpy(&v, p, 2); ival(v); p += 2; break; }
+            case 'S': { uint16_t v; memcpy(&v, p, 2); ival(v); p += 2; break; }
+            case 'i': { int32_t v; memcpy(&v, p, 4); ival(v); p += 4; break; }
+            case 'I': { uint32_t v; memcpy(&v, p, 4); ival(v); p += 4; break; }
+            case 'f': { float v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, ":f:%g", v); t += tmp; p += 4; break; }
+            case 'A': t += ":A:"; t += (char)*p; p += 1; break;
+            case 'Z': case 'H': {
+                const uint8_t *z = (const uint8_t *)memchr(p, 0, (size_t)(end - p));
+                if (!z) z = end;
+                t += ':'; t += ty; t += ':';
+                t.append((const char *)p, (size_t)(z - p));
+                p = z + 1;
+                break;
+            }
+            case 'B': {
+                const char sub = (char)p[0];
+                int32_t cnt; memcpy(&cnt, p + 1, 4);
+                p += 5;
+                t += ":B:"; t += sub;
+                for (int32_t k = 0; k < cnt; ++k) {
+                    t += ',';
+                    switch (sub) {
+                        case 'c': snprintf(tmp, sizeof tmp, "%d", *(const int8_t *)p); p += 1; break;
+                        case 'C': snprintf(tmp, sizeof tmp, "%u", *(const uint8_t *)p); p += 1; break;
+                        case 's': { int16_t v; memcpy(&v, p, 2); snprintf(tmp, sizeof tmp, "%d", v); p += 2; break; }
+                        case 'S': { uint16_t v; memcpy(&v, p, 2); snprintf(tmp, sizeof tmp, "%u", v); p += 2; break; }
+                        case 'i': { int32_t v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, "%d", v); p += 4; break; }
+                        case 'I': { uint32_t v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, "%u", v); p += 4; break; }
+                        default: { float v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, "%g", v); p += 4; break; }
+                    }
+                    t += tmp;
+                }
+                break;
+            }
+            default: return;
+        }
+    }
+}
+
+int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
+    got = false;
+    if (!ensure(h, 4)) return FC2_OK;
+    int32_t bs;
+    memcpy(&bs, h->buf.data() + h->beg, 4);
+    if (bs < 32 || !ensure(h, 4 + (size_t)bs)) return fc2::fail(FC2_E_FORMAT, "truncated BAM record");
+    const uint8_t *b = (const uint8_t *)h->buf.data() + h->beg + 4;
+    const uint8_t *e = b + bs;
+    int32_t ref_id, pos, l_seq, nref, npos, tlen;
+    uint8_t l_name, mapq;
+    uint16_t bin, n_cig, flag;
+    memcpy(&ref_id, b, 4); memcpy(&pos, b + 4, 4); l_name = b[8]; mapq = b[9]; memcpy(&bin, b + 10, 2);
+    memcpy(&n_cig, b + 12, 2); memcpy(&flag, b + 14, 2); memcpy(&l_seq, b + 16, 4); memcpy(&nref, b + 20, 4);
+    memcpy(&npos, b + 24, 4); memcpy(&tlen, b + 28, 4);
+    const uint8_t *p = b + 32;
+    r.qname.assign((const char *)p, l_name ? l_name - 1 : 0);
+    p += l_name;
+    std::vector<std::pair<int, int>> ops(n_cig);
+    std::string cig;
+    char tmp[32];
+    for (int k = 0; k < n_cig; ++k) {
+        uint32_t c; memcpy(&c, p + 4 * k, 4);
+        ops[k] = {(int)(c & 0xF), (int)(c >> 4)};
+        snprintf(tmp, sizeof tmp, "%u%c", c >> 4, "MIDNSHP=X"[(c & 0xF) < 9 ? (c & 0xF) : 0]);
+        cig += tmp;
+    }
+    p += 4 * n_cig;
+    static const char *SEQ = "=ACMGRSVTWYHKDBN";
+    std::string seq;
+    seq.reserve((size_t)l_seq);
+    for (int k = 0; k < l_seq; ++k) seq += SEQ[(p[k >> 1] >> ((k & 1) ? 0 : 4)) & 0xF];
+    p += (l_seq + 1) / 2;
+    std::string qual;
+    if (l_seq == 0 || p[0] == 0xFF) qual = "*";
+    else { qual.resize((size_t)l_seq); for (int k = 0; k < l_seq; ++k) qual[k] = (char)(p[k] + 33); }
+    p += l_seq;
+    r.flag = flag;
+    r.tid = ref_id;
+    r.pos = pos;
+    r.has_seq = l_seq > 0;
+    finish_rec(r, ops, l_seq);
+    // SAM text (only needed for hand-back, but cheap relative to inflate)
+    std::string &t = r.text;
+    t = r.qname;
+    snprintf(tmp, sizeof tmp, "\t%u\t", flag); t += tmp;
+    t += (ref_id >= 0 && ref_id < (int)h->refs.size()) ? h->refs[ref_id] : std::string("*");
+    snprintf(tmp, sizeof tmp, "\t%d\t%u\t", pos + 1, mapq); t += tmp;
+    t += cig.empty() ? std::string("*") : cig;
+    t += "\t*\t0\t0\t";
+    t += l_seq ? seq : std::string("*");
+    t += '\t';
+    t += qual;
+    append_bam_tags(t, p, e);
+    h->beg += 4 + (size_t)bs;
+    got = true;
+    return FC2_OK;
+}
+
+int read_header(fc2_ingest *h) {
+    if (!h->bam) {
+        std::string line;
+        for (;;) {
+            // peek: header lines start with '@'
+            if (!ensure(h, 1)) return FC2_OK;
+            if (h->buf[h->beg] != '@') return FC2_OK;
+            if (!next_line(h, line)) return FC2_OK;
+            h->header += line;
+            h->header += '\n';
+            if (line.compare(0, 3, "@SQ") == 0) {
+                size_t p = line.find("\tSN:");
+                if (p != std::string::npos) {
+                    size_t e = line.find('\t', p + 4);
+                    std::string name = line.substr(p + 4, e == std::string::npos ? std::string::npos : e - p - 4);
+                    h->tid_of[name] = (int)h->refs.size();
+                    h->refs.push_back(name);
+                }
+            }
+        }
+    }
+    if (!ensure(h, 12)) return fc2::fail(FC2_E_FORMAT, "truncated BAM header");
+    if (memcmp(h->buf.data() + h->beg, "BAM\1", 4) != 0) return fc2::fail(FC2_E_FORMAT, "not a BAM file");
+    int32_t lt;
+    memcpy(&lt, h->buf.data() + h->beg + 4, 4);
+    if (!ensure(h, 8 + (size_t)lt + 4)) return fc2::fail(FC2_E_FORMAT, "truncated BAM header");
+    h->header.assign(h->buf.data() + h->beg + 8, (size_t)lt);
+    while (!h->header.empty() && h->header.back() == '\0') h->header.pop_back();
+    h->beg += 8 + (size_t)lt;
+    int32_t nref;
+    memcpy(&nref, h->buf.data() + h->beg, 4);
+    h->beg += 4;
+    for (int k = 0; k < nref; ++k) {
+        if (!ensure(h, 4)) return fc2::fail(FC2_E_FORMAT, "truncated BAM refs");
+        int32_t ln;
+        memcpy(&ln, h->buf.data() + h->beg, 4);
+        if (!ensure(h, 4 + (size_t)ln + 4)) return fc2::fail(FC2_E_FORMAT, "truncated BAM refs");
+        std::string name(h->buf.data() + h->beg + 4, ln > 0 ? (size_t)ln - 1 : 0);
+        h->beg += 4 + (size_t)ln + 4;
+        h->tid_of[name] = (int)h->refs.size();
+        h->refs.push_back(name);
+    }
+    return FC2_OK;
+}
+
+bool next_record(fc2_ingest *h, Rec &r, int &rc) {
+    rc = FC2_OK;
+    if (h->bam) {
+        bool got;
+        rc = parse_bam_record(h, r, got);
+        return rc == FC2_OK && got;
+    }
+    std::string line;
+    for (;;) {
+        if (!next_line(h, line)) return false;
+        bool blank = true;
+        for (char c : line) if (!isspace((unsigned char)c)) { blank = false; break; }
+        if (blank) continue;
+        rc = parse_sam_record(h, line, r);
+        return rc == FC2_OK;
+    }
+}
+
+// ---- fragment logic ----------------------------------------------------------
+void open_mate(fc2_ingest *h, Mate &m, Rec &&r) {
+    h->counts.total_mates++;
+    m.recs.clear();
+    m.proper.clear();
+    m.recs.push_back(std::move(r));
+    m.proper.push_back(0);
+    m.valid = true;
+}
+
+void add_segment(Mate &m, Rec &&r) {
+    const Rec &p = m.recs[0];
+    const bool proper = r.tid == p.tid && r.reverse() == p.reverse();
+    m.recs.push_back(std::move(r));
+    if (proper) m.proper.push_back((int)m.recs.size() - 1);
+}
+
+struct MateEval {
+    int n_circ = 0, n_lin = 0, too_short = 0;
+    bool unspliced = false;
+    bool python_must_see = false;   // the reference would fail or compute on it: let the caller do it
+};
+
+MateEval eval_mate(const Mate &m, int asize) {
+    MateEval ev;
+    if (m.proper.size() < 2) { ev.unspliced = true; return ev; }
+    const Rec &prim = m.recs[0];
+    if (!prim.has_seq) { ev.python_must_see = true; return ev; }   // len(None) in the reference
+    std::vector<int> segs = m.proper;
+    for (int k : segs) {
+        const Rec &s = m.recs[k];
+        if (s.qlen < 0 || s.aend < 0) { ev.python_must_see = true; return ev; }
+    }
+    std::stable_sort(segs.begin(), segs.end(), [&](int a, int b) { return m.recs[a].astart < m.recs[b].astart; });
+    for (size_t k = 0; k + 1 < segs.size(); ++k) {
+        const Rec &a = m.recs[segs[k]], &b = m.recs[segs[k + 1]];
+        if (a.qlen < asize || b.qlen < asize) { ev.too_short++; continue; }
+        if (b.pos - a.aend < 0) ev.n_circ++; else ev.n_lin++;
+    }
+    return ev;
+}
+
+void emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed) {
+    h->counts.n_reads++;
+    if (p->noop) return;
+    const Mate *mates[2] = {h->have_other ? &h->other : nullptr, &h->current};
+    MateEval ev[2];
+    int circ = 0, lin = 0;
+    bool must = false;
+    for (int k = 0; k < 2; ++k) {
+        if (!mates[k]) continue;
+        ev[k] = eval_mate(*mates[k], p->asize);
+        circ += ev[k].n_circ;
+        lin += ev[k].n_lin;
+        must |= ev[k].python_must_see;
+    }
+    bool hand = must || ((circ || lin) && !(circ == 0 && p->nolinear));
+    if (!hand) {
+        for (int k = 0; k < 2; ++k) {
+            if (!mates[k]) continue;
+            if (ev[k].unspliced) h->counts.unspliced_mates++;
+            h->counts.seg_too_short_skip += (uint64_t)ev[k].too_short;
+        }
+        return;
+    }
+    for (int k = 0; k < 2; ++k) {
+        if (!mates[k]) continue;
+        for (const Rec &r : mates[k]->recs) { h->out += r.text; h->out += '\n'; }
+    }
+    h->out += '\n';
+    ++n_handed;
+    h->counts.handed_back++;
+}
+
+}  // namespace
+
+extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
+    if (!path || !out) return fc2::fail(FC2_E_PARAM, "fc2_ingest_open: null argument");
+    *out = nullptr;
+    int fd = strcmp(path, "-") == 0 ? dup(0) : open(path, O_RDONLY);
+    if (fd < 0) return fc2::fail(FC2_E_IO, std::string("cannot open '") + path + "': " + strerror(errno));
+    fc2_ingest *h = new fc2_ingest();
+    h->fd = fd;
+    h->bam = is_bam != 0;
+    h->buf.resize(1 << 22);
+    if (h->bam) {
+        if (inflateInit2(&h->zs, 15 + 32) != Z_OK) { close(fd); delete h; return fc2::fail(FC2_E_IO, "zlib init"); }
+        h->z_init = true;
+    }
+    int rc = read_header(h);
+    if (rc) { fc2_ingest_close(h); return rc; }
+    *out = h;
+    return FC2_OK;
+}
+
+extern "C" void fc2_ingest_close(fc2_ingest *h) {
+    if (!h) return;
+    if (h->z_init) inflateEnd(&h->zs);
+    if (h->fd >= 0) close(h->fd);
+    delete h;
+}
+
+extern "C" int fc2_ingest_n_refs(const fc2_ingest *h) { return h ? (int)h->refs.size() : 0; }
+extern "C" const char *fc2_ingest_ref_name(const fc2_ingest *h, int tid) {
+    return (h && tid >= 0 && tid < (int)h->refs.size()) ? h->refs[tid].c_str() : nullptr;
+}
+extern "C" const char *fc2_ingest_header(const fc2_ingest *h) { return h ? h->header.c_str() : ""; }
+
+extern "C" int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags,
+                               fc2_ingest_counts *counts, const char **text, uint64_t *text_len, uint64_t *n_handed,
+                               int *eof) {
+    if (!h || !p) return fc2::fail(FC2_E_PARAM, "fc2_ingest_next: null argument");
+    h->out.clear();
+    uint64_t handed = 0, frags = 0;
+    int rc = FC2_OK;
+    bool done = h->finished;
+    while (!done && frags < max_frags) {
+        Rec r;
+        if (!next_record(h, r, rc)) {
+            if (rc) return rc;
+            // end of input: the final yield (:1486)
+            if (h->started) {
+                if (h->n_records == 1)
+                    return fc2::fail(FC2_E_FORMAT, "UnboundLocalError: local variable 'line_num' referenced before "
+                                                   "assignment (single-record input, find_circ.py:1486)");
+                emit_or_count(h, p, handed);
+                ++frags;
+            }
+            h->finished = done = true;
+            break;
+        }
+        h->n_records++;
+        h->counts.records++;
+        if (!h->started) {           // first record always opens a mate (:1462-1463)
+            open_mate(h, h->current, std::move(r));
+            h->started = true;
+            continue;
+        }
+        if (r.unmapped()) { h->counts.unmapped_reads++; continue; }
+        const Rec &prim = h->current.recs[0];
+        if (r.read1() == prim.read1() && r.qname == prim.qname) {
+            add_segment(h->current, std::move(r));
+        } else if (r.read1() != prim.read1() && r.qname == prim.qname) {
+            std::swap(h->other, h->current);
+            h->have_other = true;
+            open_mate(h, h->current, std::move(r));
+        } else {
+            emit_or_count(h, p, handed);
+            ++frags;
+            h->have_other = false;
+            h->other = Mate();
+            open_mate(h, h->current, std::move(r));
+        }
+    }
+    if (counts) *counts = h->counts;
+    if (text) *text = h->out.c_str();
+    if (text_len) *text_len = h->out.size();
+    if (n_handed) *n_handed = handed;
+    if (eof) *eof = done ? 1 : 0;
+    return FC2_OK;
+}

@@ -1,0 +1,54 @@
+"""Python handle of the native SAM/BAM ingest (include/fc2_ingest.h)."""
+from __future__ import annotations
+
+import ctypes
+from typing import Dict, List, Tuple
+
+from . import _native as N
+from .samio import AlignedSegment, parse_sam_line
+
+
+class NativeIngest:
+    """Streams fragments that carry anchor pairs; counts the rest natively."""
+
+    def __init__(self, path: str, is_bam: bool):
+        self.h = ctypes.c_void_p()
+        N.check(N.lib().fc2_ingest_open(path.encode(), int(is_bam), ctypes.byref(self.h)))
+        L = N.lib()
+        self.references = [L.fc2_ingest_ref_name(self.h, i).decode("latin-1")
+                           for i in range(L.fc2_ingest_n_refs(self.h))]
+        self.tid_of: Dict[str, int] = {n: i for i, n in enumerate(self.references)}
+        self.counts = N.IngestCounts()
+        self.eof = False
+
+    def getrname(self, tid: int) -> str:
+        return self.references[tid]
+
+    def next_chunk(self, asize: int, nolinear: bool, noop: bool, max_frags: int) -> List[List[AlignedSegment]]:
+        """Records of the next handed-back fragments (up to max_frags fragments read)."""
+        p = N.IngestParams(int(asize), int(bool(nolinear)), int(bool(noop)))
+        text = ctypes.c_void_p()
+        ln, nh = ctypes.c_uint64(), ctypes.c_uint64()
+        eof = ctypes.c_int()
+        N.check(N.lib().fc2_ingest_next(self.h, ctypes.byref(p), max_frags, ctypes.byref(self.counts),
+                                        ctypes.byref(text), ctypes.byref(ln), ctypes.byref(nh), ctypes.byref(eof)))
+        self.eof = bool(eof.value)
+        if not ln.value:
+            return []
+        raw = ctypes.string_at(text, ln.value).decode("latin-1")
+        frags = []
+        for block in raw.split("\n\n"):
+            if block:
+                frags.append([parse_sam_line(l, self.tid_of) for l in block.split("\n") if l])
+        return frags
+
+    def close(self):
+        if self.h:
+            N.lib().fc2_ingest_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -102,6 +102,21 @@ def parse_cigar(s: str) -> List[Tuple[int, int]]:
     return [(_CIGAR_OPS[op], int(n)) for n, op in _CIGAR_RE.findall(s)]
 
 
+def parse_sam_line(line: str, tid_of: Dict[str, int]) -> AlignedSegment:
+    """One SAM text line -> AlignedSegment (reference names resolved through tid_of)."""
+    f = line.rstrip("\r\n").split("\t")
+    if len(f) < 11:
+        raise ValueError("malformed SAM line: %r" % line[:80])
+    rname = f[2]
+    tid = -1 if rname == "*" else tid_of.get(rname, -1)
+    tags = []
+    for t in f[11:]:
+        tg, typ, val = t.split(":", 2)
+        tags.append((tg, _tag_value(typ, val)))
+    return AlignedSegment(f[0], int(f[1]), tid, int(f[3]) - 1, int(f[4]), parse_cigar(f[5]),
+                          None if f[9] == "*" else f[9], None if f[10] == "*" else f[10], tags)
+
+
 def _tag_value(typ: str, val: str):
     if typ == "i":
         return int(val)
@@ -151,17 +166,7 @@ class AlignmentFile:
                 self.lengths.append(int(d.get("LN", 0)))
 
     def _parse_sam(self, line: str) -> AlignedSegment:
-        f = line.rstrip("\r\n").split("\t")
-        if len(f) < 11:
-            raise ValueError("malformed SAM line: %r" % line[:80])
-        rname = f[2]
-        tid = -1 if rname == "*" else self._tid.get(rname, -1)
-        tags = []
-        for t in f[11:]:
-            tg, typ, val = t.split(":", 2)
-            tags.append((tg, _tag_value(typ, val)))
-        return AlignedSegment(f[0], int(f[1]), tid, int(f[3]) - 1, int(f[4]), parse_cigar(f[5]),
-                              None if f[9] == "*" else f[9], None if f[10] == "*" else f[10], tags)
+        return parse_sam_line(line, self._tid)
 
     # ------------------------------------------------------------------ BAM
     def _read(self, n):

@@ -1,0 +1,63 @@
+/*
+ * fc2_ingest.h -- native SAM/BAM ingest for the find_circ2 caller (libfc2.so).
+ *
+ * Replaces the per-record Python work of find_circ.py's read loop
+ * (pysam iteration find_circ.py:461-469, collected_bwa_mem_segments
+ * :1450-1486, MateSegments :976-1140, process_mate :1492-1527) for the records
+ * that never reach the breakpoint search: every record is parsed and grouped
+ * into fragments (mate pairs / single reads) here, adjacent segment pairs are
+ * formed with the reference's rules, and only fragments that carry at least
+ * one anchor pair are handed back (as SAM text) for the per-fragment logic.
+ * Counters the reference keeps for the others are accumulated here.
+ *
+ * Reads SAM text (path or "-" for stdin) and BAM (BGZF, via zlib).
+ */
+#ifndef FC2_INGEST_H
+#define FC2_INGEST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fc2_ingest fc2_ingest;
+
+typedef struct fc2_ingest_params {
+    int32_t asize;      /* -a: minimal segment length of an anchor (find_circ.py:1125) */
+    uint8_t nolinear;   /* --no-linear: fragments without backsplice spans are skipped (:1568-1569) */
+    uint8_t noop;       /* --noop: count reads only (:1554-1558) */
+    uint8_t _pad[2];
+} fc2_ingest_params;
+
+typedef struct fc2_ingest_counts {  /* cumulative since open (the reference's N[...] keys) */
+    uint64_t n_reads;               /* fragments yielded (n_reads, :1536) */
+    uint64_t total_mates;           /* N['total_mates'] (:978) */
+    uint64_t unmapped_reads;        /* N['unmapped_reads'] (:1467) */
+    uint64_t unspliced_mates;       /* N['unspliced_mates'] of skipped fragments (:1494) */
+    uint64_t seg_too_short_skip;    /* N['seg_too_short_skip'] of skipped fragments (:1127) */
+    uint64_t records;               /* alignment records read */
+    uint64_t handed_back;           /* fragments returned to the caller */
+} fc2_ingest_counts;
+
+/* is_bam: 0 = SAM text, 1 = BAM; path "-" reads stdin. */
+int  fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out);
+void fc2_ingest_close(fc2_ingest *h);
+int  fc2_ingest_n_refs(const fc2_ingest *h);
+const char *fc2_ingest_ref_name(const fc2_ingest *h, int tid);
+/* SAM header text (one line per @ record). */
+const char *fc2_ingest_header(const fc2_ingest *h);
+
+/* Process up to max_frags fragments.  *text / *text_len: SAM lines of the
+ * returned fragments, each fragment's records consecutive and followed by an
+ * empty line; valid until the next call.  *n_handed: fragments in *text.
+ * *eof = 1 when the input is exhausted.  Returns FC2_OK or a negative status
+ * (FC2_E_FORMAT for malformed input; the reference's UnboundLocalError on
+ * single-record input is FC2_E_FORMAT with that message). */
+int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, fc2_ingest_counts *counts,
+                    const char **text, uint64_t *text_len, uint64_t *n_handed, int *eof);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FC2_INGEST_H */
