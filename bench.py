@@ -346,7 +346,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_ms": round(kernel_ms, 4), "algo_bytes_per_pair": bpp,
-                     "kernel": "bp_scan_kernel<2> (one anchor pair per lane)"},
+                     "kernel": "bp_scan32_kernel<4,NT> (one anchor pair per lane)"},
         "cpu_baseline": None,
     }
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
