@@ -84,7 +84,8 @@ def gpu_evaluator(genome, hp_options):
         flags = [((N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.strand == '-' else 0) |
                   (N.PAIR_SKIP if c == missing else 0)) for s, c in zip(spans, idx)]
         b = PairBatch.pack(hp_options, genome, [s.read_part for s in spans], [s.align_A.pos for s in spans],
-                           [s.align_B.aend for s in spans], [0 if c == missing else c for c in idx], flags)
+                           [s.align_B.aend for s in spans], [0 if c == missing else c for c in idx], flags,
+                           locus_order=True)
         out = scan(hp_options, genome, b)
         res = decode_splices(hp_options, genome, b, out, spans, raise_errors=False)
         for s, r, c in zip(spans, res, idx):

@@ -615,7 +615,14 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
     int64_t sz = 0, A0 = 0, B0 = 0, t0 = 0, t1 = 0;
     bool ok = false;
     for (int attempt = 0; attempt < 16 && !ok; ++attempt) {
-        const int64_t gp = R.below(total);
+        int64_t gp;
+        if (cfg.locus_ordered) {   // i-th of n strata (redraws stay in the stratum's neighbourhood)
+            const double s = ((double)i + (double)R.uni()) / (double)n;
+            gp = (int64_t)(s * (double)total) + (attempt ? R.below(4096) : 0);
+            if (gp >= total) gp = total - 1;
+        } else {
+            gp = R.below(total);
+        }
         uint32_t a = 0, z = g.n_chrom;  // chrom_cum[c] <= gp < chrom_cum[c+1]
         while (z - a > 1) {
             const uint32_t m = (a + z) >> 1;
@@ -728,6 +735,7 @@ inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + bl
 // inputs/outputs, default on.
 int g_stream_nt = 1;
 int g_kernel32 = 1;   // 1: bp_scan32_kernel (32-bit plane words), 0: bp_scan_kernel (64-bit)
+int g_xcd_swizzle = 0; // 1: XCD-contiguous block order in bp_scan32_kernel (measured: no gain, r01)
 inline bool stream_nt() { return g_stream_nt != 0; }
 
 }  // namespace
@@ -759,7 +767,7 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     uint64_t *out = reinterpret_cast<uint64_t *>(results);
     const bool nt = stream_nt();
     if (g_kernel32) {
-        fc2::launch_scan32((ml + 2 + 31) / 32, nt, grid, s, *p, *g, *b, out, tiemask, tw);
+        fc2::launch_scan32((ml + 2 + 31) / 32, nt, g_xcd_swizzle, grid, s, *p, *g, *b, out, tiemask, tw);
         return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
     }
 #define FC2_LAUNCH(NWV, NTV) \
@@ -831,6 +839,7 @@ extern "C" int fc2_set_tuning(int key, int value) {
     switch (key) {
         case FC2_TUNE_STREAM_NT: g_stream_nt = value ? 1 : 0; return FC2_OK;
         case FC2_TUNE_KERNEL32: g_kernel32 = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_XCD_SWIZZLE: g_xcd_swizzle = value ? 1 : 0; return FC2_OK;
         default: return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: unknown key");
     }
 }

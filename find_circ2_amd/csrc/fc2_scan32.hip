@@ -186,11 +186,21 @@ __device__ __forceinline__ uint64_t pack_result(const Best32 &B, unsigned gtag12
            ((uint64_t)info << 48);
 }
 
+// XCD-aware block order (guide §5.5 T1): the dispatcher deals blocks round-robin
+// over the 8 XCDs, so block b runs on XCD b % 8; remap so that XCD x processes a
+// contiguous range of the batch (bijective for any grid size).  Only a
+// performance hint: correctness never depends on placement.
+__device__ __forceinline__ uint64_t xcd_block(uint32_t b, uint32_t nwg) {
+    const uint32_t x = b & 7u, j = b >> 3, q = nwg >> 3, r = nwg & 7u;
+    return (uint64_t)x * q + (x < r ? x : r) + j;
+}
+
 template <int NQ, bool NT>
 __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
                                                            uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
-                                                           uint32_t tw) {
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+                                                           uint32_t tw, int swizzle) {
+    const uint64_t blk = swizzle ? xcd_block(blockIdx.x, gridDim.x) : (uint64_t)blockIdx.x;
+    const uint64_t i = blk * kBlock + threadIdx.x;
     if (i >= bv.n) return;
     const fc2_pair pr = ld_pair<NT>(bv.pairs + i);
     if (pr.flags & FC2_PAIR_BYTEPATH) return;  // left for the byte-exact kernel
@@ -380,10 +390,11 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
 
 namespace fc2 {
 
-void launch_scan32(int nq, bool nt, unsigned grid, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
-                   const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
+void launch_scan32(int nq, bool nt, int swizzle, unsigned grid, hipStream_t s, const fc2_params &p,
+                   const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
 #define FC2_L32(NQV, NTV) \
-    hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV>), dim3(grid), dim3(kBlock), 0, s, p, g, b, out, tiemask, tw)
+    hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV>), dim3(grid), dim3(kBlock), 0, s, p, g, b, out, tiemask, tw, \
+                       swizzle)
     if (nq <= 4) { if (nt) FC2_L32(4, true); else FC2_L32(4, false); }
     else if (nq <= 8) { if (nt) FC2_L32(8, true); else FC2_L32(8, false); }
     else { if (nt) FC2_L32(16, true); else FC2_L32(16, false); }

@@ -68,11 +68,13 @@ class SynthConfig:
     p_clip: float = 0.2
     span_min: int = 150
     span_max: int = 5000
+    locus_ordered: bool = False
 
     def cfg(self) -> N.SynthCfg:
         return N.SynthCfg(int(self.seed), int(self.len_min), int(self.len_max), float(self.p_planted),
                           float(self.p_minus_site), float(self.p_backsplice), float(self.mut_rate),
-                          float(self.n_rate), float(self.p_clip), int(self.span_min), int(self.span_max))
+                          float(self.n_rate), float(self.p_clip), int(self.span_min), int(self.span_max),
+                          int(bool(self.locus_ordered)), 0)
 
 
 # ---------------------------------------------------------------------------
@@ -95,16 +97,19 @@ class PairBatch:
         self.m_bytepath = 0
         self.bp_index = self.bp_pairs = self.bp_arena = self.bp_off = None
         self.options: Optional[Options] = None
+        self.perm: Optional[np.ndarray] = None   # packed slot k holds input pair perm[k] (locus order)
 
     # -------------------------------------------------------------- from reads
     @classmethod
     def pack(cls, options: Options, genome: Genome, reads, a_pos, b_aend, chrom, flags,
-             device=None, n_threads: int = 0) -> "PairBatch":
+             device=None, n_threads: int = 0, locus_order: bool = False) -> "PairBatch":
         """Pack anchor pairs (``read_part`` bytes + JunctionSpan fields) and upload them.
 
         ``reads``: list of ``bytes`` (``JunctionSpan.read_part``, find_circ.py:844) or a
         ``(buffer uint8, offsets uint64, lengths)`` triple.  ``flags``: PAIR_* bits
-        (BACKSPLICE, PRIMARY_REV, SKIP).
+        (BACKSPLICE, PRIMARY_REV, SKIP).  ``locus_order``: lay the batch out in genome
+        order of the A window (the windows of a wave then share L2 lines); results are
+        returned in input order all the same.
         """
         torch = _torch()
         dev = torch.device(device) if device is not None else genome.device
@@ -130,6 +135,14 @@ class PairBatch:
         hp["chrom"] = np.asarray(chrom, np.int64).astype(np.uint32)
         hp["read_len"] = lens
         hp["flags"] = np.asarray(flags, np.uint8)
+        perm = None
+        if locus_order and n > 1 and not genome.dummy and len(genome.chrom_start):
+            cs = genome.chrom_start.astype(np.int64)
+            c = np.minimum(hp["chrom"].astype(np.int64), len(cs) - 1)
+            perm = np.argsort(cs[c] + hp["a_pos"].astype(np.int64), kind="stable")
+            hp = hp[perm]
+            off = off[perm]
+            lens = lens[perm]
         max_len = int(lens.max()) if n else 0
         rw, nw, tw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
         N.check(N.lib().fc2_batch_geometry(ctypes.byref(p), max_len, ctypes.byref(rw), ctypes.byref(nw),
@@ -148,6 +161,7 @@ class PairBatch:
         ls = hp["read_len"].astype(np.int64) - 2 * options.eff_a
         b.max_l = int(max(0, ls[fast].max())) if fast.any() else 0
         b.host_pairs = hp
+        b.perm = perm
         b.device = dev
         b.pairs = torch.from_numpy(hp.view(np.uint8)).to(dev)
         b.read_words = torch.from_numpy(words.view(np.int64)).to(dev)
@@ -370,6 +384,11 @@ def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: Scan
     """
     hp = batch.fetch_host_pairs()
     res = out.host(batch.n)
+    slot = np.arange(batch.n)
+    if batch.perm is not None:           # locus-ordered layout: back to input order
+        slot = np.empty_like(batch.perm)
+        slot[batch.perm] = np.arange(batch.n)
+        hp, res = hp[slot], res[slot]
     evaluated = (hp["flags"] & N.PAIR_SKIP) == 0
     if raise_errors:
         raise_reference_errors(options, hp, res, evaluated)
@@ -401,7 +420,7 @@ def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: Scan
         s._score = _score(options, sig, dist, s.ov, strand, hp["flags"][i])
         ties = [s]
         if options.allhits and nt > 1:
-            ties = _expand_ties(options, genome, hp, i, tm, s, span, chrom)
+            ties = _expand_ties(options, genome, hp, i, tm[:, int(slot[i])], s, span, chrom)
         result.append(ties)
     return result
 
@@ -424,7 +443,7 @@ def _expand_ties(options, genome, hp, i, tm, best: Splice, span, chrom):
     for x in range(l + 1):
         k, b = x >> 6, x & 63
         for strand, row in (('+', k), ('-', half + k)):
-            if not (int(tm[row, i]) >> b) & 1:
+            if not (int(tm[row]) >> b) & 1:
                 continue
             s0 = int(hp["b_aend"][i]) - e - l + x
             e0 = int(hp["a_pos"][i]) + e + x + 1

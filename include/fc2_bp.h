@@ -158,6 +158,7 @@ int         fc2_device_count(int *count);
 /* Performance knobs (results never depend on them); used for A/B measurements. */
 #define FC2_TUNE_STREAM_NT 1   /* 1 (default): per-pair inputs/results use non-temporal loads/stores */
 #define FC2_TUNE_KERNEL32  2   /* 1 (default): 32-bit-word scan kernel; 0: 64-bit-word scan kernel */
+#define FC2_TUNE_XCD_SWIZZLE 3 /* 1: each XCD scans a contiguous range of the batch (default 0) */
 int         fc2_set_tuning(int key, int value);
 
 /* Largest l the register kernel handles (longer reads go to the byte kernel). */
@@ -247,6 +248,9 @@ typedef struct fc2_synth_cfg {
     float    n_rate;               /* per-base N rate in reads               */
     float    p_clip;               /* clip 0..3 bases off each read end      */
     int32_t  span_min, span_max;   /* exon (circ) / intron (linear) span     */
+    int32_t  locus_ordered;        /* 1: pair i's locus is drawn from the i-th of n equal genome
+                                      strata (a batch ordered by position); 0: uniform (read order) */
+    int32_t  _pad;
 } fc2_synth_cfg;
 
 /* Fill a synthetic genome on the device: random bases from a counter-based

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--workload", default="hg19")
     ap.add_argument("--pairs", type=int, default=50_000_000)
     ap.add_argument("--rounds", type=int, default=7)
+    ap.add_argument("--ordered", action="store_true", help="locus-ordered synthetic batch")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="k32nt1,k64nt1",
                     help="comma list of k32|k64 + nt1|nt0 (FC2_TUNE_KERNEL32 / FC2_TUNE_STREAM_NT)")
@@ -28,7 +29,7 @@ def main():
     import bench
     from find_circ2_amd import scan, _native as N
     dev = torch.device("cuda", 0)
-    args = argparse.Namespace(workload=a.workload, pairs=a.pairs, read_len=100)
+    args = argparse.Namespace(workload=a.workload, pairs=a.pairs, read_len=100, locus_ordered=a.ordered)
     opt, g, b = bench.build_workload(args, 0, dev)
     out = scan(opt, g, b)
     torch.cuda.synchronize()
@@ -38,6 +39,7 @@ def main():
     def apply(v):
         N.lib().fc2_set_tuning(1, 0 if "nt0" in v else 1)
         N.lib().fc2_set_tuning(2, 0 if "k64" in v else 1)
+        N.lib().fc2_set_tuning(3, 0 if "sw0" in v else 1)
 
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream(dev)
@@ -56,7 +58,7 @@ def main():
             assert torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
     for v in variants:
         t = np.array(times[v])
-        print(json.dumps({"variant": v, "workload": a.workload, "pairs": b.n, "median_ms": round(float(np.median(t)), 4),
+        print(json.dumps({"variant": v, "workload": a.workload + ("-ordered" if a.ordered else ""), "pairs": b.n, "median_ms": round(float(np.median(t)), 4),
                           "min_ms": round(float(t.min()), 4), "pairs_per_s": round(b.n / (np.median(t) * 1e-3), 1)}))
 
 

@@ -92,6 +92,29 @@ def test_spans_vs_oracle(fa, oi):
                   int(e["ov"]), int(e["n_hits"])) for e in exp], i
 
 
+@pytest.mark.parametrize("o", [dict(), dict(allhits=True, noncanonical=True, strandpref=True)])
+def test_locus_ordered_layout_same_results(o):
+    """PairBatch.pack(locus_order=True) lays the batch out in genome order; decoded
+    results (all ties) must be those of the input-order layout, pair by pair."""
+    opt = Options(**o)
+    path = os.path.join(GOLDEN, "test_ref.fa")
+    g = genome(path)
+    spans = make_spans(load_genome(path), 4000, seed=27, L=(40, 200), p_readN=0.05)
+    args = ([s.read_part for s in spans], [s.a_pos for s in spans], [s.b_aend for s in spans],
+            [g.chrom_index(s.chrom) for s in spans],
+            [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.primary_reverse else 0)
+             for s in spans])
+    b0 = PairBatch.pack(opt, g, *args)
+    b1 = PairBatch.pack(opt, g, *args, locus_order=True)
+    assert b1.perm is not None and not np.array_equal(b1.perm, np.arange(len(spans)))
+    r0 = decode_splices(opt, g, b0, scan(opt, g, b0), raise_errors=False)
+    r1 = decode_splices(opt, g, b1, scan(opt, g, b1), raise_errors=False)
+    key = lambda t: [(s.start, s.end, s.strand, s.gtag, s.dist, s.ov, s.n_hits) for s in t] \
+        if isinstance(t, list) else repr(t)
+    assert [key(t) for t in r0] == [key(t) for t in r1]
+    assert sum(1 for t in r0 if isinstance(t, list) and t) > 500
+
+
 def test_known_answers_through_gpu():
     from bwa_emul import emulate_pairs, read_fasta, truth_from_name
     from find_circ2_amd import BreakpointEngine, JunctionSpan
