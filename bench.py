@@ -50,6 +50,8 @@ def parse():
     ap.add_argument("--workload", choices=["hg19", "cdr1as"], default="hg19")
     ap.add_argument("--pairs", type=int, default=0, help="pairs per GPU (default 50M hg19 / 1M cdr1as)")
     ap.add_argument("--read-len", type=int, default=100)
+    ap.add_argument("--locus-ordered", dest="locus_ordered", action="store_true",
+                    help="lay the batch out by A-window locus (PairBatch.pack(locus_order=True)); default read order")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
@@ -315,7 +317,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            w = tj.get(args.workload)
+            w = tj.get(args.workload + ("_locus_ordered" if args.locus_ordered else ""))
             if w and int(w.get("pairs_per_launch", -1)) == b.n:
                 traffic = w.get("hbm_bytes_per_launch")
         except Exception:

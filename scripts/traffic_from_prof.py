@@ -1,9 +1,10 @@
 #!/usr/bin/env python
-"""Build profiles/traffic_<round>.json from the rocprofv3 PMC passes of scripts/profile_r01.sh.
+"""Build profiles/traffic_<round>.json from the rocprofv3 passes of scripts/profile_r01.sh.
 
-HBM bytes per launch of bp_scan_kernel = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024
-(gfx950: FETCH_SIZE tallies 128-B requests at 64 B, MI355X_MICROARCH.md §HBM; the factor is
-checked on the cdr1as run, whose reads are pure streaming because the genome is L2-resident).
+HBM bytes per launch of the scan kernel = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024
+(gfx950 tallies 128-B line fills at 64 B, MI355X_MICROARCH.md §HBM; confirmed for this
+kernel by the cdr1as run, whose reads are pure streaming because the genome is
+L2-resident, and by scripts/gather_probe.hip for random 16-B gathers).
 """
 import collections
 import csv
@@ -13,20 +14,27 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KERN = "bp_scan"
+N_PAIRS = 50_000_000
 
 
-def agg(prof, name, kern="bp_scan"):
-    rows = list(csv.DictReader(open(os.path.join(prof, name, "pmc_counter_collection.csv"))))
+def agg(prof, name):
+    p = os.path.join(prof, name, "pmc_counter_collection.csv")
+    if not os.path.exists(p):
+        return {}
     a = collections.defaultdict(list)
-    for r in rows:
-        if kern in r["Kernel_Name"]:
+    for r in csv.DictReader(open(p)):
+        if KERN in r["Kernel_Name"]:
             a[r["Counter_Name"]].append(float(r["Counter_Value"]))
     return {k: sum(v) / len(v) for k, v in a.items()}
 
 
-def kstats(prof, name, kern="bp_scan"):
-    for r in csv.DictReader(open(os.path.join(prof, name, "kt_kernel_stats.csv"))):
-        if kern in r["Name"]:
+def kstats(prof, name):
+    p = os.path.join(prof, name, "kt_kernel_stats.csv")
+    if not os.path.exists(p):
+        return None, 0
+    for r in csv.DictReader(open(p)):
+        if KERN in r["Name"]:
             return float(r["AverageNs"]), int(r["Calls"])
     return None, 0
 
@@ -34,33 +42,30 @@ def kstats(prof, name, kern="bp_scan"):
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
     prof = os.path.join(ROOT, "gpurun_out", "prof")
-    f, w, h, fc = agg(prof, "fetch_hg19"), agg(prof, "write_hg19"), agg(prof, "hit_hg19"), agg(prof, "fetch_cdr1as")
-    ns, calls = kstats(prof, "kt_hg19")
-    nsc, _ = kstats(prof, "kt_cdr1as")
-    n = 50_000_000
-    hbm = 2 * f["FETCH_SIZE"] * 1024 + w["WRITE_SIZE"] * 1024
-    out = {
-        "hg19": {"pairs_per_launch": n, "kernel": "bp_scan_kernel<2,NT>", "avg_kernel_ns_rocprof": ns,
-                 "FETCH_SIZE_kB_raw": f["FETCH_SIZE"], "WRITE_SIZE_kB": w["WRITE_SIZE"],
-                 "TCC_HIT_sum": h.get("TCC_HIT_sum"), "TCC_MISS_sum": h.get("TCC_MISS_sum"),
-                 "hbm_bytes_per_launch": round(hbm), "hbm_bytes_per_pair": round(hbm / n, 1),
-                 "moved_TBps": round(hbm / (ns * 1e-9) / 1e12, 3) if ns else None,
-                 "correction": "reads = 2 x FETCH_SIZE x 1024 (gfx950), writes = WRITE_SIZE x 1024 (exact: 8 B x pairs)"},
-        "cdr1as_50M_calibration": {"pairs_per_launch": n, "avg_kernel_ns_rocprof": nsc,
-                                   "FETCH_SIZE_kB_raw": fc["FETCH_SIZE"],
-                                   "reads_x2_bytes": round(2 * fc["FETCH_SIZE"] * 1024),
-                                   "streamed_bytes_expected": n * 40,
-                                   "note": "genome L2-resident: reads are the 16 B record + 24 B read row per pair "
-                                           "plus N rows of READ_N pairs"},
-        "source": "rocprofv3 --pmc passes (scripts/profile_r01.sh): bench.py --steps 10 --warmup 2; averages over "
-                  "the bp_scan_kernel dispatches",
-    }
+    out = {}
+    for w, key in (("hg19", "hg19"), ("hg19o", "hg19_locus_ordered"), ("cdr1as", "cdr1as_50M_calibration")):
+        f, wr, h = agg(prof, "fetch_" + w), agg(prof, "write_" + w), agg(prof, "hit_" + w)
+        ns, calls = kstats(prof, "kt_" + w)
+        if not f:
+            continue
+        hbm = 2 * f["FETCH_SIZE"] * 1024 + wr.get("WRITE_SIZE", 0) * 1024
+        out[key] = {"pairs_per_launch": N_PAIRS, "kernel": "bp_scan32_kernel<4,NT>", "avg_kernel_ns_rocprof": ns,
+                    "FETCH_SIZE_kB_raw": f["FETCH_SIZE"], "WRITE_SIZE_kB": wr.get("WRITE_SIZE"),
+                    "TCC_HIT_sum": h.get("TCC_HIT_sum"), "TCC_MISS_sum": h.get("TCC_MISS_sum"),
+                    "hbm_bytes_per_launch": round(hbm), "hbm_bytes_per_pair": round(hbm / N_PAIRS, 1),
+                    "moved_TBps": round(hbm / (ns * 1e-9) / 1e12, 3) if ns else None}
+    out["correction"] = ("reads = 2 x FETCH_SIZE x 1024 (gfx950 128-B fills tallied at 64 B), writes = WRITE_SIZE x "
+                         "1024 (exact: 8 B x pairs)")
+    out["source"] = ("rocprofv3 --kernel-trace --stats and separate --pmc passes (scripts/profile_r01.sh): bench.py "
+                     "--steps 10 --warmup 2; averages over the scan-kernel dispatches")
     path = os.path.join(ROOT, "profiles", "traffic_%s.json" % rnd)
     json.dump(out, open(path, "w"), indent=1)
     dst = os.path.join(ROOT, "profiles", rnd)
     os.makedirs(dst, exist_ok=True)
-    for d in ("kt_hg19", "kt_cdr1as"):
-        shutil.copy(os.path.join(prof, d, "kt_kernel_stats.csv"), os.path.join(dst, d + "_kernel_stats.csv"))
+    for w in ("hg19", "hg19o", "cdr1as"):
+        src = os.path.join(prof, "kt_" + w, "kt_kernel_stats.csv")
+        if os.path.exists(src):
+            shutil.copy(src, os.path.join(dst, "kt_%s_kernel_stats.csv" % w))
     print(json.dumps(out, indent=1))
 
 
