@@ -58,13 +58,23 @@ class Params(ctypes.Structure):
 class GenomeView(ctypes.Structure):
     _fields_ = [("units", ctypes.c_void_p), ("nplane", ctypes.c_void_p), ("ncoarse", ctypes.c_void_p),
                 ("chrom_start", ctypes.c_void_p), ("chrom_size", ctypes.c_void_p),
-                ("n_units", ctypes.c_uint64), ("n_chrom", ctypes.c_uint32), ("dummy", ctypes.c_uint32)]
+                ("n_units", ctypes.c_uint64), ("n_chrom", ctypes.c_uint32), ("dummy", ctypes.c_uint32),
+                ("units_twin", ctypes.c_void_p)]
 
 
 class BatchView(ctypes.Structure):
     _fields_ = [("pairs", ctypes.c_void_p), ("read_words", ctypes.c_void_p), ("read_nwords", ctypes.c_void_p),
                 ("n", ctypes.c_uint64), ("stride", ctypes.c_uint64), ("rw", ctypes.c_uint32),
-                ("nw", ctypes.c_uint32), ("max_l", ctypes.c_int32), ("_pad", ctypes.c_uint32)]
+                ("nw", ctypes.c_uint32), ("max_l", ctypes.c_int32), ("layout", ctypes.c_uint32)]
+
+
+BATCH_LOCUS_ORDERED = 0x1
+
+
+class ReorderInfo(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("workspace_bytes", ctypes.c_uint64), ("shift", ctypes.c_uint32),
+                ("n_buckets", ctypes.c_uint32), ("bucket_bits", ctypes.c_uint32), ("n_chunks", ctypes.c_uint32),
+                ("n_groups", ctypes.c_uint32), ("chunk", ctypes.c_uint32)]
 
 
 class BytesView(ctypes.Structure):
@@ -88,7 +98,8 @@ EXPORTED = [
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill",
-    "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_synth_pairs_launch",
+    "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_twin_launch", "fc2_synth_pairs_launch",
+    "fc2_reorder_plan", "fc2_reorder_launch",
     # include/fc2_ingest.h
     "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
     "fc2_ingest_next",
@@ -110,7 +121,7 @@ _lib = None
 
 def build(force: bool = False) -> str:
     srcdir = os.path.join(_HERE, "csrc")
-    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_scan32.h", "fc2_host.cpp",
+    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_reorder.hip", "fc2_scan32.h", "fc2_host.cpp",
                                               "fc2_ingest.cpp", "fc2_common.h", "Makefile")]
     srcs += [os.path.join(os.path.dirname(_HERE), "include", h) for h in ("fc2_bp.h", "fc2_ingest.h")]
     newest = max(os.path.getmtime(s) for s in srcs)
@@ -153,8 +164,11 @@ def lib() -> ctypes.CDLL:
         "fc2_bytepath_fill": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, vp, vp, vp, vp]),
         "fc2_synth_genome_launch": (ctypes.c_int, [u64, vp, vp, vp, u64, vp, vp, u32, vp]),
         "fc2_coarse_launch": (ctypes.c_int, [vp, vp, u64, vp]),
+        "fc2_twin_launch": (ctypes.c_int, [vp, u64, vp, vp]),
         "fc2_synth_pairs_launch": (ctypes.c_int, [P(Params), P(SynthCfg), P(GenomeView), vp, u64, vp, vp, u32,
                                                   vp, u32, u64, vp, vp]),
+        "fc2_reorder_plan": (ctypes.c_int, [P(GenomeView), u64, P(ReorderInfo)]),
+        "fc2_reorder_launch": (ctypes.c_int, [P(ReorderInfo), P(GenomeView), P(BatchView), vp, vp, vp, vp, vp, vp]),
         "fc2_ingest_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(vp)]),
         "fc2_ingest_close": (None, [vp]),
         "fc2_ingest_n_refs": (ctypes.c_int, [vp]),

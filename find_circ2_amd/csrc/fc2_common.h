@@ -18,6 +18,10 @@ constexpr int kMaxFastL = 510;
 // Validate the options the hot path reads; returns FC2_OK or FC2_E_PARAM.
 int validate_params(const fc2_params *p);
 
+// fc2_reorder.hip tuning (fc2_set_tuning)
+extern int g_reorder_rounds;
+extern int g_reorder_nt;
+
 inline int eff_anchor(const fc2_params *p) { return p->asize - p->margin; }  // find_circ.py:882
 
 }  // namespace fc2

@@ -729,13 +729,21 @@ inline int hip_check(hipError_t e, const char *what) {
     return FC2_OK;
 }
 
+// units_twin[w] = units[w - 8] (4 units = 8 words later), zero outside the genome
+__global__ void twin_kernel(const uint64_t *__restrict__ units, uint64_t n_units, uint64_t *__restrict__ twin) {
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= 2 * (n_units + 8)) return;
+    twin[w] = (w >= 8 && w - 8 < 2 * n_units) ? units[w - 8] : 0ull;
+}
+
 inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
 // Tuning knobs (fc2_set_tuning): non-temporal streaming of the per-pair
 // inputs/outputs, default on.
 int g_stream_nt = 1;
 int g_kernel32 = 1;   // 1: bp_scan32_kernel (32-bit plane words), 0: bp_scan_kernel (64-bit)
-int g_xcd_swizzle = 0; // 1: XCD-contiguous block order in bp_scan32_kernel (measured: no gain, r01)
+int g_xcd_swizzle = 2; // XCD-contiguous block order in bp_scan32_kernel: 0 never, 1 always, 2 for locus-ordered batches
+int g_twin = 2;        // units_twin: 0 never, 1 always, 2 for batches not flagged locus-ordered
 inline bool stream_nt() { return g_stream_nt != 0; }
 
 }  // namespace
@@ -767,7 +775,12 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     uint64_t *out = reinterpret_cast<uint64_t *>(results);
     const bool nt = stream_nt();
     if (g_kernel32) {
-        fc2::launch_scan32((ml + 2 + 31) / 32, nt, g_xcd_swizzle, grid, s, *p, *g, *b, out, tiemask, tw);
+        const int sw = g_xcd_swizzle == 2 ? ((b->layout & FC2_BATCH_LOCUS_ORDERED) ? 1 : 0) : g_xcd_swizzle;
+        fc2_genome_view gv = *g;
+        // locus-ordered batches re-read their lines from L2: the twin only doubles the footprint there
+        const bool ordered = (b->layout & FC2_BATCH_LOCUS_ORDERED) != 0;
+        if (g_twin == 0 || (g_twin == 2 && ordered)) gv.units_twin = nullptr;
+        fc2::launch_scan32((ml + 2 + 31) / 32, nt, sw, grid, s, *p, gv, *b, out, tiemask, tw);
         return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
     }
 #define FC2_LAUNCH(NWV, NTV) \
@@ -808,6 +821,14 @@ extern "C" int fc2_synth_genome_launch(uint64_t seed, uint64_t *units, uint64_t 
     return fc2_coarse_launch(nplane, ncoarse, n_units, stream);
 }
 
+extern "C" int fc2_twin_launch(const uint64_t *units, uint64_t n_units, uint64_t *units_twin, void *stream) {
+    if (!units || !units_twin || n_units == 0) return fc2::fail(FC2_E_PARAM, "fc2_twin_launch: bad args");
+    const uint64_t n_words = 2 * (n_units + 8);
+    hipLaunchKernelGGL(twin_kernel, dim3(grid_for(n_words, 256)), dim3(256), 0, (hipStream_t)stream, units, n_units,
+                       units_twin);
+    return hip_check(hipGetLastError(), "twin_kernel launch");
+}
+
 extern "C" int fc2_coarse_launch(const uint64_t *nplane, uint32_t *ncoarse, uint64_t n_units, void *stream) {
     if (!nplane || !ncoarse) return fc2::fail(FC2_E_PARAM, "fc2_coarse_launch: bad args");
     const uint64_t n_words = (((n_units + 15) >> 4) + 31) >> 5;
@@ -839,7 +860,16 @@ extern "C" int fc2_set_tuning(int key, int value) {
     switch (key) {
         case FC2_TUNE_STREAM_NT: g_stream_nt = value ? 1 : 0; return FC2_OK;
         case FC2_TUNE_KERNEL32: g_kernel32 = value ? 1 : 0; return FC2_OK;
-        case FC2_TUNE_XCD_SWIZZLE: g_xcd_swizzle = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_REORDER_ROUNDS:
+            if (value < 1 || value > 32) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: reorder rounds 1..32");
+            fc2::g_reorder_rounds = value; return FC2_OK;
+        case FC2_TUNE_REORDER_NT: fc2::g_reorder_nt = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_TWIN:
+            if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: twin is 0, 1 or 2");
+            g_twin = value; return FC2_OK;
+        case FC2_TUNE_XCD_SWIZZLE:
+            if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: swizzle is 0, 1 or 2");
+            g_xcd_swizzle = value; return FC2_OK;
         default: return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: unknown key");
     }
 }

@@ -67,34 +67,66 @@ __device__ __forceinline__ void word_shift(uint32_t (&a)[M], int sel, int levels
     }
 }
 
-// Genome window [ws, ws+W) of a chromosome starting at global base cstart.
+// Genome window [ws, ws+W) of a chromosome starting at global base cstart, in two
+// phases so that a lane's loads for BOTH windows (units + coarse N words) are in
+// flight together: window_issue only issues loads (straight-line, clamped
+// addresses, no branches), window_finish consumes them.  Only the N plane of a
+// window whose 1024-base blocks contain an N costs a further round trip.
 template <int NQ>
-__device__ __forceinline__ void load_window32(const fc2_genome_view &g, uint64_t cstart, int64_t csize, int64_t ws,
-                                              int W, P32<NQ> &P) {
-    if (g.dummy) {
-#pragma unroll
-        for (int k = 0; k <= NQ; ++k) { P.lo[k] = 0; P.hi[k] = 0; P.n[k] = ~0u; }
-        return;
-    }
-    constexpr int NU = NQ / 2 + 1;           // 64-bit units covering NQ+1 32-bit words at any parity
+struct WinRaw {
+    static constexpr int NU = NQ / 2 + 1;    // 64-bit units covering NQ+1 32-bit words at any parity
+    ulonglong2 v[NU];
+    uint32_t cw0, cw1;                       // coarse N words of the first / last block
+    int64_t u0;
+    unsigned sh;
+    int odd, jl;                             // word parity; last needed unit (relative to u0)
+    bool ok[NU];
+};
+
+template <int NQ>
+__device__ __forceinline__ void window_issue(const fc2_genome_view &g, uint64_t cstart, int64_t ws, int W,
+                                             WinRaw<NQ> &R) {
+    constexpr int NU = WinRaw<NQ>::NU;
     const int64_t g0 = (int64_t)cstart + ws;
     const int64_t q0 = g0 >> 5;              // first 32-bit word (floor)
-    const unsigned sh = (unsigned)(g0 & 31);
-    const int64_t u0 = q0 >> 1;
-    const int odd = (int)(q0 & 1);
-    const int qlast = odd + (((int)sh + W - 1) >> 5);   // last word needed, relative to 2*u0
-    const ulonglong2 *U = reinterpret_cast<const ulonglong2 *>(g.units);
-    uint32_t xl[2 * NU], xh[2 * NU];
-    const bool interior = u0 >= 0 && (uint64_t)(u0 + NU) <= g.n_units;
+    R.sh = (unsigned)(g0 & 31);
+    R.u0 = q0 >> 1;
+    R.odd = (int)(q0 & 1);
+    const int qlast = R.odd + (((int)R.sh + W - 1) >> 5);   // last word needed, relative to 2*u0
+    R.jl = qlast >> 1;
+    // A window straddling a 128-B line (8 units) of `units` sits inside one line of the twin
+    // copy (shifted by 4 units): one line fill per window instead of two.
+    const bool straddle = (int)(R.u0 & 7) + R.jl >= 8;
+    const ulonglong2 *U = (straddle && g.units_twin) ? reinterpret_cast<const ulonglong2 *>(g.units_twin) + 4
+                                                     : reinterpret_cast<const ulonglong2 *>(g.units);
+    const int64_t last = (int64_t)g.n_units - 1;
 #pragma unroll
     for (int j = 0; j < NU; ++j) {
-        const int64_t u = u0 + j;
-        const bool need = 2 * j <= qlast;
-        ulonglong2 v = {0ull, 0ull};
-        if (need && (interior || (u >= 0 && (uint64_t)u < g.n_units))) v = U[u];
+        const int64_t u = R.u0 + (j < R.jl ? j : R.jl);     // unneeded units re-read the last needed one
+        R.ok[j] = j <= R.jl && u >= 0 && u <= last;
+        R.v[j] = U[u < 0 ? 0 : (u > last ? last : u)];
+    }
+    const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
+    int64_t b0 = R.u0 >> 4, b1 = (R.u0 + NU - 1) >> 4;
+    b0 = b0 < 0 ? 0 : (b0 >= nb ? nb - 1 : b0);
+    b1 = b1 < 0 ? 0 : (b1 >= nb ? nb - 1 : b1);
+    R.cw0 = g.ncoarse[b0 >> 5];               // raw words: consumed (shifted) only in window_finish
+    R.cw1 = g.ncoarse[b1 >> 5];
+}
+
+template <int NQ>
+__device__ __forceinline__ void window_finish(const fc2_genome_view &g, const WinRaw<NQ> &R, int64_t csize,
+                                              int64_t ws, int W, P32<NQ> &P) {
+    constexpr int NU = WinRaw<NQ>::NU;
+    uint32_t xl[2 * NU], xh[2 * NU];
+#pragma unroll
+    for (int j = 0; j < NU; ++j) {
+        const ulonglong2 v = R.ok[j] ? R.v[j] : ulonglong2{0ull, 0ull};
         xl[2 * j] = (uint32_t)v.x; xl[2 * j + 1] = (uint32_t)(v.x >> 32);
         xh[2 * j] = (uint32_t)v.y; xh[2 * j + 1] = (uint32_t)(v.y >> 32);
     }
+    const int odd = R.odd;
+    const unsigned sh = R.sh;
 #pragma unroll
     for (int k = 0; k < NQ; ++k) {
         const uint32_t l0 = odd ? xl[k + 1] : xl[k], l1 = odd ? xl[k + 2] : xl[k + 1];
@@ -104,18 +136,16 @@ __device__ __forceinline__ void load_window32(const fc2_genome_view &g, uint64_t
     }
     P.lo[NQ] = 0; P.hi[NQ] = 0;
 
-    bool anyN = false;
-    {
-        const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
-        const int64_t b0 = u0 >> 4, b1 = (u0 + NU - 1) >> 4;
-        if (b0 >= 0 && b0 < nb) anyN |= (g.ncoarse[b0 >> 5] >> (b0 & 31)) & 1u;
-        if (b1 != b0 && b1 >= 0 && b1 < nb) anyN |= (g.ncoarse[b1 >> 5] >> (b1 & 31)) & 1u;
-    }
+    // blocks outside the genome hold no N; the clamped coarse words then belong to another block
+    const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
+    const int64_t b0 = R.u0 >> 4, b1 = (R.u0 + NU - 1) >> 4;
+    const bool anyN = ((b0 >= 0 && b0 < nb) && ((R.cw0 >> (b0 & 31)) & 1u)) ||
+                      ((b1 != b0 && b1 >= 0 && b1 < nb) && ((R.cw1 >> (b1 & 31)) & 1u));
     if (anyN) {
         uint32_t xn[2 * NU];
 #pragma unroll
         for (int j = 0; j < NU; ++j) {
-            const int64_t u = u0 + j;
+            const int64_t u = R.u0 + j;
             const uint64_t v = (u >= 0 && (uint64_t)u < g.n_units) ? g.nplane[u] : 0ull;
             xn[2 * j] = (uint32_t)v; xn[2 * j + 1] = (uint32_t)(v >> 32);
         }
@@ -141,6 +171,12 @@ __device__ __forceinline__ void load_window32(const fc2_genome_view &g, uint64_t
             P.lo[k] &= v; P.hi[k] &= v; P.n[k] = (P.n[k] & v) | ~v;
         }
     }
+}
+
+template <int NQ>
+__device__ __forceinline__ void window_dummy(P32<NQ> &P) {
+#pragma unroll
+    for (int k = 0; k <= NQ; ++k) { P.lo[k] = 0; P.hi[k] = 0; P.n[k] = ~0u; }
 }
 
 template <int NQ>
@@ -202,15 +238,30 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
     const uint64_t blk = swizzle ? xcd_block(blockIdx.x, gridDim.x) : (uint64_t)blockIdx.x;
     const uint64_t i = blk * kBlock + threadIdx.x;
     if (i >= bv.n) return;
+    // round trip 1: the pair record and its read rows (both indexed by i only)
     const fc2_pair pr = ld_pair<NT>(bv.pairs + i);
+    constexpr int R = NQ + 1;                  // 64-bit row words the largest row can use (2l <= 64R)
+    uint64_t rv[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j)
+        rv[j] = ((uint32_t)j < bv.rw) ? ld_stream<NT>(bv.read_words + (uint64_t)j * bv.stride + i) : 0ull;
     if (pr.flags & FC2_PAIR_BYTEPATH) return;  // left for the byte-exact kernel
 
     const int e = p.asize - p.margin;
     const int l = (int)pr.read_len - 2 * e;
     const bool want_ties = p.allhits != 0;
     const int W = l + 2;                       // flank, find_circ.py:900
-    const uint64_t cstart = (g.dummy || pr.chrom >= g.n_chrom) ? 0ull : g.chrom_start[pr.chrom];
-    const int64_t csize = g.dummy ? (int64_t)1 << 62 : (pr.chrom >= g.n_chrom ? 0 : g.chrom_size[pr.chrom]);
+    // round trip 2: the chromosome table (L2-resident)
+    uint64_t cstart = 0;
+    int64_t csize = (int64_t)1 << 62;          // dummy genome: every window is all 'N'
+    if (!g.dummy) {
+        const bool known = pr.chrom < g.n_chrom;
+        const uint32_t c = known ? pr.chrom : 0u;
+        cstart = g.chrom_start[c];
+        csize = g.chrom_size[c];
+        __builtin_amdgcn_sched_barrier(0);     // both loads issued before either is waited on
+        if (!known) { cstart = 0; csize = 0; }
+    }
     const int64_t wsA = (int64_t)pr.a_pos + e;
     const int64_t wsB = (int64_t)pr.b_aend - e - W;
     if ((pr.flags & FC2_PAIR_SKIP) || l < 0 || l > 32 * NQ - 2 || pr.chrom >= g.n_chrom || wsA > csize ||
@@ -224,16 +275,20 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
         return;
     }
 
-    // --- internal read part: 32-bit plane words ---------------------------------
+    // round trip 3: both genome windows (find_circ.py:900-902) and their coarse N words
+    WinRaw<NQ> rA, rB;
+    if (!g.dummy) {
+        window_issue<NQ>(g, cstart, wsA, W, rA);
+        window_issue<NQ>(g, cstart, wsB, W, rB);
+    }
+    __builtin_amdgcn_sched_barrier(0);         // every window load in flight before the first wait
+
+    // --- internal read part: 32-bit plane words (while the windows are in flight) ---
     uint32_t Ilo[NQ], Ihi[NQ], In[NQ];
     {
-        constexpr int R = NQ + 1;              // 64-bit row words the largest row can use (2l <= 64R)
         uint32_t r[2 * R + 1];
 #pragma unroll
-        for (int j = 0; j < R; ++j) {
-            const uint64_t v = ((uint32_t)j < bv.rw) ? ld_stream<NT>(bv.read_words + (uint64_t)j * bv.stride + i) : 0ull;
-            r[2 * j] = (uint32_t)v; r[2 * j + 1] = (uint32_t)(v >> 32);
-        }
+        for (int j = 0; j < R; ++j) { r[2 * j] = (uint32_t)rv[j]; r[2 * j + 1] = (uint32_t)(rv[j] >> 32); }
         r[2 * R] = 0;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) Ilo[k] = r[k] & rmask32(0, l, k);
@@ -260,10 +315,14 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
         }
     }
 
-    // --- genome windows (find_circ.py:900-902) ----------------------------------
     P32<NQ> A, B;
-    load_window32<NQ>(g, cstart, csize, wsA, W, A);
-    load_window32<NQ>(g, cstart, csize, wsB, W, B);
+    if (!g.dummy) {
+        window_finish<NQ>(g, rA, csize, wsA, W, A);
+        window_finish<NQ>(g, rB, csize, wsB, W, B);
+    } else {
+        window_dummy<NQ>(A);
+        window_dummy<NQ>(B);
+    }
 
     // --- mismatch planes and prefix counts ---------------------------------------
     uint32_t mA[NQ], mB[NQ];

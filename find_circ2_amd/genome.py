@@ -46,6 +46,7 @@ class Genome:
         self.chrom_start: np.ndarray = np.zeros(0, np.uint64)
         self.n_units = 0
         self.units = self.nplane = self.ncoarse = None      # torch device tensors
+        self.units_twin = None                              # units shifted by half a line (fc2_twin_launch)
         self.d_chrom_start = self.d_chrom_size = None
         self.dummy = False
         self.fasta = None                                   # ctypes handle (host FASTA) or None
@@ -153,14 +154,18 @@ class Genome:
         sz = self.sizes.astype(np.int64) if len(self.sizes) else np.zeros(1, np.int64)
         self.d_chrom_start = torch.from_numpy(cs.copy()).to(self.device)
         self.d_chrom_size = torch.from_numpy(sz.copy()).to(self.device)
+        if self.n_units:
+            self.units_twin = torch.empty(2 * (self.n_units + 8), dtype=torch.int64, device=self.device)
+            N.check(N.lib().fc2_twin_launch(self.units.data_ptr(), self.n_units, self.units_twin.data_ptr(),
+                                            torch.cuda.current_stream(self.device).cuda_stream))
 
     # ------------------------------------------------------------------ access
     def view(self) -> N.GenomeView:
         if self.dummy:
-            return N.GenomeView(None, None, None, None, None, 0, 0xFFFFFFFF, 1)
+            return N.GenomeView(None, None, None, None, None, 0, 0xFFFFFFFF, 1, None)
         return N.GenomeView(self.units.data_ptr(), self.nplane.data_ptr(), self.ncoarse.data_ptr(),
                             self.d_chrom_start.data_ptr(), self.d_chrom_size.data_ptr(), self.n_units,
-                            len(self.names), 0)
+                            len(self.names), 0, self.units_twin.data_ptr() if self.units_twin is not None else None)
 
     def chrom_index(self, name: str) -> int:
         """Chromosome -> table index; KeyError like indexed_fasta.get_data (find_circ.py:193)."""

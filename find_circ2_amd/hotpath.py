@@ -98,6 +98,10 @@ class PairBatch:
         self.bp_index = self.bp_pairs = self.bp_arena = self.bp_off = None
         self.options: Optional[Options] = None
         self.perm: Optional[np.ndarray] = None   # packed slot k holds input pair perm[k] (locus order)
+        self.layout = 0            # FC2_BATCH_* hints for the scan
+        self.slot = None           # reorder() output: torch int32 [n], device twin of perm
+        self.reorder_info = None
+        self.workspace = None
 
     # -------------------------------------------------------------- from reads
     @classmethod
@@ -162,6 +166,7 @@ class PairBatch:
         b.max_l = int(max(0, ls[fast].max())) if fast.any() else 0
         b.host_pairs = hp
         b.perm = perm
+        b.layout = N.BATCH_LOCUS_ORDERED if perm is not None else 0
         b.device = dev
         b.pairs = torch.from_numpy(hp.view(np.uint8)).to(dev)
         b.read_words = torch.from_numpy(words.view(np.int64)).to(dev)
@@ -212,6 +217,7 @@ class PairBatch:
         b.n, b.stride = n, max(n, 1)
         b.rw, b.nw, b.tw = rw.value, nw.value, tw.value
         b.max_l = max(0, cfg.len_max - 2 * options.eff_a)
+        b.layout = N.BATCH_LOCUS_ORDERED if cfg.locus_ordered else 0
         dev = genome.device
         b.device = dev
         b.pairs = torch.empty(16 * b.stride, dtype=torch.uint8, device=dev)
@@ -237,9 +243,15 @@ class PairBatch:
             self.host_pairs = self.pairs[:16 * self.n].cpu().numpy().view(N.PAIR_DTYPE).copy()
         return self.host_pairs
 
+    def fetch_perm(self) -> Optional[np.ndarray]:
+        """perm (packed slot k holds input pair perm[k]) or None for input order."""
+        if self.perm is None and self.slot is not None:
+            self.perm = self.slot[:self.n].cpu().numpy().astype(np.int64)
+        return self.perm
+
     def view(self) -> N.BatchView:
         return N.BatchView(self.pairs.data_ptr(), self.read_words.data_ptr(), self.read_nwords.data_ptr(),
-                           self.n, self.stride, self.rw, self.nw, self.max_l, 0)
+                           self.n, self.stride, self.rw, self.nw, self.max_l, self.layout)
 
     def bytes_view(self) -> N.BytesView:
         return N.BytesView(self.bp_index.data_ptr(), self.bp_pairs.data_ptr(), self.bp_arena.data_ptr(),
@@ -280,6 +292,52 @@ def scan(options: Options, genome: Genome, batch: PairBatch, out: ScanOutput = N
         N.check(N.lib().fc2_bp_scan_bytes_launch(ctypes.byref(p), ctypes.byref(v), out.results.data_ptr(), tptr,
                                                  out.tw, batch.stride, s))
     return out
+
+
+def reorder(genome: Genome, batch: PairBatch, into: PairBatch = None) -> PairBatch:
+    """Device locality reorder (``fc2_reorder_launch``) of a batch in input order.
+
+    Returns a batch holding the same pairs stably sorted by genome bucket of the
+    A window, flagged locus-ordered, whose ``slot`` (device) / ``fetch_perm()``
+    (host) map each position back to the input pair; ``decode_splices`` of a scan
+    over it returns results in input order.  ``into``: a previous result for a
+    batch of the same shape whose buffers are reused.  Runs on torch's current
+    stream.
+    """
+    torch = _torch()
+    if batch.slot is not None or batch.perm is not None:
+        raise ValueError("batch is already locus-ordered")
+    dev = batch.device
+    gv = genome.view()
+    r = into
+    info = N.ReorderInfo()
+    N.check(N.lib().fc2_reorder_plan(ctypes.byref(gv), batch.n, ctypes.byref(info)))
+    if r is None or r.n != batch.n or r.rw != batch.rw or r.nw != batch.nw or \
+            r.reorder_info.chunk != info.chunk or r.workspace.numel() < info.workspace_bytes:
+        r = PairBatch()
+        r.options = batch.options
+        r.n, r.stride, r.rw, r.nw, r.tw, r.max_l = batch.n, batch.stride, batch.rw, batch.nw, batch.tw, batch.max_l
+        r.device = dev
+        r.pairs = torch.empty_like(batch.pairs)
+        r.read_words = torch.empty_like(batch.read_words)
+        r.read_nwords = torch.empty_like(batch.read_nwords)
+        r.slot = torch.empty(max(batch.n, 1), dtype=torch.int32, device=dev)
+        r.workspace = torch.empty(max(1, int(info.workspace_bytes)), dtype=torch.uint8, device=dev)
+        r.reorder_info = info
+        r.layout = N.BATCH_LOCUS_ORDERED
+    r.host_pairs = None
+    r.perm = None
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    N.check(N.lib().fc2_reorder_launch(ctypes.byref(r.reorder_info), ctypes.byref(gv), ctypes.byref(batch.view()),
+                                       r.pairs.data_ptr(), r.read_words.data_ptr(), r.read_nwords.data_ptr(),
+                                       r.slot.data_ptr(), r.workspace.data_ptr(), stream))
+    r.m_bytepath = batch.m_bytepath
+    if batch.m_bytepath:             # byte-path results go to the pair's reordered position
+        inv = torch.empty(batch.n, dtype=torch.int64, device=dev)
+        inv[r.slot[:batch.n].long()] = torch.arange(batch.n, dtype=torch.int64, device=dev)
+        r.bp_index = inv[batch.bp_index]
+        r.bp_pairs, r.bp_arena, r.bp_off = batch.bp_pairs, batch.bp_arena, batch.bp_off
+    return r
 
 
 # ---------------------------------------------------------------------------
@@ -385,9 +443,10 @@ def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: Scan
     hp = batch.fetch_host_pairs()
     res = out.host(batch.n)
     slot = np.arange(batch.n)
-    if batch.perm is not None:           # locus-ordered layout: back to input order
-        slot = np.empty_like(batch.perm)
-        slot[batch.perm] = np.arange(batch.n)
+    perm = batch.fetch_perm()
+    if perm is not None:                 # locus-ordered layout: back to input order
+        slot = np.empty_like(perm)
+        slot[perm] = np.arange(batch.n)
         hp, res = hp[slot], res[slot]
     evaluated = (hp["flags"] & N.PAIR_SKIP) == 0
     if raise_errors:

@@ -115,6 +115,11 @@ typedef struct fc2_genome_view {
     uint64_t n_units;
     uint32_t n_chrom;
     uint32_t dummy;              /* 1: every window is all 'N' (GenomeAccessor dummy mode, :340-345) */
+    const uint64_t *units_twin;  /* device [2*(n_units+8)] or NULL: units shifted by half a 128-B line,
+                                    units_twin[2t..2t+1] = units of unit t-4 (zero outside the genome);
+                                    a window that straddles a line of `units` lies inside one line of
+                                    the twin, so a random window costs one line fill instead of ~1.15
+                                    (fc2_twin_launch builds it) */
 } fc2_genome_view;
 
 /* ---- a batch of anchor pairs in device memory (SoA) --------------------- */
@@ -132,8 +137,10 @@ typedef struct fc2_batch_view {
     uint32_t rw;
     uint32_t nw;
     int32_t  max_l;              /* largest l = L - 2e of a non-BYTEPATH pair (selects the kernel width) */
-    uint32_t _pad;
+    uint32_t layout;             /* FC2_BATCH_* hints (results never depend on them) */
 } fc2_batch_view;
+#define FC2_BATCH_LOCUS_ORDERED 0x1u  /* pairs are sorted by genome locus (fc2_reorder_launch output or a
+                                         host-sorted batch): the scan deals each XCD a contiguous range */
 
 /* ---- pairs that need byte-exact evaluation ------------------------------ */
 /* Block for pair k at arena[off[k]]: int32 lenI, lenA, lenB, then
@@ -158,7 +165,13 @@ int         fc2_device_count(int *count);
 /* Performance knobs (results never depend on them); used for A/B measurements. */
 #define FC2_TUNE_STREAM_NT 1   /* 1 (default): per-pair inputs/results use non-temporal loads/stores */
 #define FC2_TUNE_KERNEL32  2   /* 1 (default): 32-bit-word scan kernel; 0: 64-bit-word scan kernel */
-#define FC2_TUNE_XCD_SWIZZLE 3 /* 1: each XCD scans a contiguous range of the batch (default 0) */
+#define FC2_TUNE_XCD_SWIZZLE 3 /* each XCD scans a contiguous range of the batch: 0 never, 1 always,
+                                  2 (default) iff the batch view has FC2_BATCH_LOCUS_ORDERED */
+#define FC2_TUNE_REORDER_ROUNDS 4 /* fc2_reorder: pairs per thread per 256-thread chunk (1..32), read by
+                                     fc2_reorder_plan */
+#define FC2_TUNE_REORDER_NT 5  /* fc2_reorder: 1 = non-temporal scatter stores (default 0) */
+#define FC2_TUNE_TWIN 6        /* windows that straddle a line read the genome view's twin: 0 never,
+                                  1 always, 2 (default) unless the batch is FC2_BATCH_LOCUS_ORDERED */
 int         fc2_set_tuning(int key, int value);
 
 /* Largest l the register kernel handles (longer reads go to the byte kernel). */
@@ -181,6 +194,31 @@ int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_
 int fc2_bp_scan_bytes_launch(const fc2_params *p, const fc2_bytes_view *v, fc2_result *results,
                              uint64_t *tiemask, uint32_t tw, uint64_t stride, void *stream);
 
+/* ---- locality reorder ---------------------------------------------------- */
+/* A batch in read order sends the lanes of a wave to unrelated genome loci, so
+ * every window costs a full HBM line fill.  fc2_reorder_launch writes a copy of
+ * the batch stably sorted by genome bucket of the A window
+ * (bucket = (chrom_start + a_pos) >> shift, <= 1024 buckets); a scan of the copy
+ * (view flagged FC2_BATCH_LOCUS_ORDERED) reads each genome line about once per
+ * XCD.  Results of that scan are in reordered order: result i belongs to input
+ * pair slot[i].  BYTEPATH / SKIP pairs are moved like any other pair. */
+typedef struct fc2_reorder_info {
+    uint64_t n;                  /* batch size the plan is for */
+    uint64_t workspace_bytes;    /* device scratch fc2_reorder_launch needs */
+    uint32_t shift;              /* log2 bases per bucket */
+    uint32_t n_buckets;
+    uint32_t bucket_bits;        /* ceil(log2(n_buckets)) */
+    uint32_t n_chunks;           /* chunks of `chunk` pairs (one workgroup each) */
+    uint32_t n_groups;           /* groups of chunks for the offset prefix (<= 128) */
+    uint32_t chunk;
+} fc2_reorder_info;
+int fc2_reorder_plan(const fc2_genome_view *g, uint64_t n, fc2_reorder_info *info);
+/* out arrays have the input's shapes: pairs_out [n], read_words_out [rw][stride],
+ * read_nwords_out [nw][stride] (only READ_N pairs' rows are written; may be NULL
+ * iff in->read_nwords is NULL), slot_out [n]; n < 2^32. */
+int fc2_reorder_launch(const fc2_reorder_info *info, const fc2_genome_view *g, const fc2_batch_view *in,
+                       fc2_pair *pairs_out, uint64_t *read_words_out, uint64_t *read_nwords_out,
+                       uint32_t *slot_out, void *workspace, void *stream);
 /* ======================================================================== */
 /* host side: FASTA (indexed_fasta semantics, find_circ.py:103-215)         */
 /* ======================================================================== */
@@ -259,6 +297,8 @@ typedef struct fc2_synth_cfg {
 int fc2_synth_genome_launch(uint64_t seed, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,
                             uint64_t n_units, const int64_t *n_lo, const int64_t *n_hi,
                             uint32_t n_intervals, void *stream);
+/* Build units_twin (device [2*(n_units+8)]) from units (device [2*n_units]). */
+int fc2_twin_launch(const uint64_t *units, uint64_t n_units, uint64_t *units_twin, void *stream);
 /* Rebuild the coarse N map from nplane (device). */
 int fc2_coarse_launch(const uint64_t *nplane, uint32_t *ncoarse, uint64_t n_units, void *stream);
 

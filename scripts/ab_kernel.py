@@ -23,7 +23,8 @@ def main():
     ap.add_argument("--ordered", action="store_true", help="locus-ordered synthetic batch")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--variants", default="k32nt1,k64nt1",
-                    help="comma list of k32|k64 + nt1|nt0 (FC2_TUNE_KERNEL32 / FC2_TUNE_STREAM_NT)")
+                    help="comma list of k32|k64 + nt1|nt0 + sw0|sw1 + tw0|tw1 (FC2_TUNE_KERNEL32 / STREAM_NT / "
+                         "XCD_SWIZZLE (default auto) / TWIN)")
     a = ap.parse_args()
     import torch
     import bench
@@ -39,7 +40,8 @@ def main():
     def apply(v):
         N.lib().fc2_set_tuning(1, 0 if "nt0" in v else 1)
         N.lib().fc2_set_tuning(2, 0 if "k64" in v else 1)
-        N.lib().fc2_set_tuning(3, 0 if "sw0" in v else 1)
+        N.lib().fc2_set_tuning(3, 0 if "sw0" in v else (1 if "sw1" in v else 2))
+        N.lib().fc2_set_tuning(6, 0 if "tw0" in v else (1 if "tw1" in v else 2))
 
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream(dev)
