@@ -59,7 +59,8 @@ class GenomeView(ctypes.Structure):
     _fields_ = [("units", ctypes.c_void_p), ("nplane", ctypes.c_void_p), ("ncoarse", ctypes.c_void_p),
                 ("chrom_start", ctypes.c_void_p), ("chrom_size", ctypes.c_void_p),
                 ("n_units", ctypes.c_uint64), ("n_chrom", ctypes.c_uint32), ("dummy", ctypes.c_uint32),
-                ("units_twin", ctypes.c_void_p)]
+                ("units_twin", ctypes.c_void_p), ("nsuper", ctypes.c_void_p), ("nsuper_shift", ctypes.c_uint32),
+                ("nsuper_words", ctypes.c_uint32)]
 
 
 class BatchView(ctypes.Structure):
@@ -98,7 +99,8 @@ EXPORTED = [
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill",
-    "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_twin_launch", "fc2_synth_pairs_launch",
+    "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_twin_launch",
+    "fc2_nsuper_geometry", "fc2_nsuper_launch", "fc2_synth_pairs_launch",
     "fc2_reorder_plan", "fc2_reorder_launch",
     # include/fc2_ingest.h
     "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
@@ -165,6 +167,8 @@ def lib() -> ctypes.CDLL:
         "fc2_synth_genome_launch": (ctypes.c_int, [u64, vp, vp, vp, u64, vp, vp, u32, vp]),
         "fc2_coarse_launch": (ctypes.c_int, [vp, vp, u64, vp]),
         "fc2_twin_launch": (ctypes.c_int, [vp, u64, vp, vp]),
+        "fc2_nsuper_geometry": (ctypes.c_int, [u64, P(u32), P(u32)]),
+        "fc2_nsuper_launch": (ctypes.c_int, [vp, u64, vp, vp]),
         "fc2_synth_pairs_launch": (ctypes.c_int, [P(Params), P(SynthCfg), P(GenomeView), vp, u64, vp, vp, u32,
                                                   vp, u32, u64, vp, vp]),
         "fc2_reorder_plan": (ctypes.c_int, [P(GenomeView), u64, P(ReorderInfo)]),

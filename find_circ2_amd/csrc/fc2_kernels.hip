@@ -736,6 +736,23 @@ __global__ void twin_kernel(const uint64_t *__restrict__ units, uint64_t n_units
     twin[w] = (w >= 8 && w - 8 < 2 * n_units) ? units[w - 8] : 0ull;
 }
 
+// nsuper word w: bit b = OR of the coarse bits of blocks [(32w+b) << (shift-10), +1 << (shift-10))
+__global__ void nsuper_kernel(const uint32_t *__restrict__ ncoarse, uint64_t n_units, uint32_t shift, uint32_t words,
+                              uint32_t *__restrict__ nsuper) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= words) return;
+    const uint64_t nb = (n_units + 15) >> 4;               // coarse blocks
+    const uint64_t per = 1ull << (shift - 10);             // coarse blocks per super bit
+    uint32_t out = 0;
+    for (uint32_t b = 0; b < 32; ++b) {
+        const uint64_t c0 = ((uint64_t)w * 32 + b) * per;
+        bool any = false;
+        for (uint64_t c = c0; c < c0 + per && c < nb && !any; ++c) any = (ncoarse[c >> 5] >> (c & 31)) & 1u;
+        out |= (uint32_t)any << b;
+    }
+    nsuper[w] = out;
+}
+
 inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
 // Tuning knobs (fc2_set_tuning): non-temporal streaming of the per-pair
@@ -743,6 +760,7 @@ inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + bl
 int g_stream_nt = 1;
 int g_kernel32 = 1;   // 1: bp_scan32_kernel (32-bit plane words), 0: bp_scan_kernel (64-bit)
 int g_xcd_swizzle = 2; // XCD-contiguous block order in bp_scan32_kernel: 0 never, 1 always, 2 for locus-ordered batches
+int g_stage = 2;       // bp_scan32 LDS staging: 0 never, 1 always, 2 read-order batch over a large genome
 int g_twin = 2;        // units_twin: 0 never, 1 always, 2 for batches not flagged locus-ordered
 inline bool stream_nt() { return g_stream_nt != 0; }
 
@@ -780,7 +798,11 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         // locus-ordered batches re-read their lines from L2: the twin only doubles the footprint there
         const bool ordered = (b->layout & FC2_BATCH_LOCUS_ORDERED) != 0;
         if (g_twin == 0 || (g_twin == 2 && ordered)) gv.units_twin = nullptr;
-        fc2::launch_scan32((ml + 2 + 31) / 32, nt, sw, grid, s, *p, gv, *b, out, tiemask, tw);
+        // LDS staging pays where every L2 request counts: read-order batch over a genome far larger
+        // than the caches (profiles/r01/ab_stage.jsonl)
+        const bool big = !g->dummy && g->n_units * 16 >= (64ull << 20);
+        const bool stage = g_stage == 2 ? (big && !ordered) : g_stage != 0;
+        fc2::launch_scan32((ml + 2 + 31) / 32, nt, sw, stage, grid, s, *p, gv, *b, out, tiemask, tw);
         return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
     }
 #define FC2_LAUNCH(NWV, NTV) \
@@ -829,6 +851,25 @@ extern "C" int fc2_twin_launch(const uint64_t *units, uint64_t n_units, uint64_t
     return hip_check(hipGetLastError(), "twin_kernel launch");
 }
 
+extern "C" int fc2_nsuper_geometry(uint64_t n_units, uint32_t *shift, uint32_t *words) {
+    if (!shift || !words) return fc2::fail(FC2_E_PARAM, "fc2_nsuper_geometry: null argument");
+    const uint64_t bases = (n_units ? n_units : 1) * 64;
+    uint32_t s = 10;                               // >= one coarse block (1024 bases)
+    while (((bases + (1ull << s) - 1) >> s) > 2048ull * 32) ++s;
+    *shift = s;
+    *words = (uint32_t)((((bases + (1ull << s) - 1) >> s) + 31) >> 5);
+    return FC2_OK;
+}
+
+extern "C" int fc2_nsuper_launch(const uint32_t *ncoarse, uint64_t n_units, uint32_t *nsuper, void *stream) {
+    if (!ncoarse || !nsuper || n_units == 0) return fc2::fail(FC2_E_PARAM, "fc2_nsuper_launch: bad args");
+    uint32_t shift, words;
+    fc2_nsuper_geometry(n_units, &shift, &words);
+    hipLaunchKernelGGL(nsuper_kernel, dim3(grid_for(words, 256)), dim3(256), 0, (hipStream_t)stream, ncoarse, n_units,
+                       shift, words, nsuper);
+    return hip_check(hipGetLastError(), "nsuper_kernel launch");
+}
+
 extern "C" int fc2_coarse_launch(const uint64_t *nplane, uint32_t *ncoarse, uint64_t n_units, void *stream) {
     if (!nplane || !ncoarse) return fc2::fail(FC2_E_PARAM, "fc2_coarse_launch: bad args");
     const uint64_t n_words = (((n_units + 15) >> 4) + 31) >> 5;
@@ -864,6 +905,9 @@ extern "C" int fc2_set_tuning(int key, int value) {
             if (value < 1 || value > 32) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: reorder rounds 1..32");
             fc2::g_reorder_rounds = value; return FC2_OK;
         case FC2_TUNE_REORDER_NT: fc2::g_reorder_nt = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_STAGE:
+            if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: stage is 0, 1 or 2");
+            g_stage = value; return FC2_OK;
         case FC2_TUNE_TWIN:
             if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: twin is 0, 1 or 2");
             g_twin = value; return FC2_OK;

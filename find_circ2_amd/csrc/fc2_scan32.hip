@@ -15,6 +15,8 @@
 namespace {
 
 constexpr int kBlock = 256;
+constexpr int kChromLds = 512;   // chromosome-table entries a block stages in LDS (8 KB)
+constexpr int kSuperLds = 2048;  // nsuper words a block stages in LDS (8 KB)
 
 __device__ __forceinline__ uint32_t lowbits32(int n) {  // bits [0, n), any n
     return n >= 32 ? ~0u : (n <= 0 ? 0u : ((1u << n) - 1u));
@@ -38,6 +40,11 @@ template <bool NT>
 __device__ __forceinline__ void st_stream(uint64_t *p, uint64_t v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
+}
+template <bool NT>
+__device__ __forceinline__ u64x2 ld_pair_raw(const fc2_pair *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
+    else return *reinterpret_cast<const u64x2 *>(p);
 }
 template <bool NT>
 __device__ __forceinline__ fc2_pair ld_pair(const fc2_pair *p) {
@@ -75,17 +82,43 @@ __device__ __forceinline__ void word_shift(uint32_t (&a)[M], int sel, int levels
 template <int NQ>
 struct WinRaw {
     static constexpr int NU = NQ / 2 + 1;    // 64-bit units covering NQ+1 32-bit words at any parity
-    ulonglong2 v[NU];
-    uint32_t cw0, cw1;                       // coarse N words of the first / last block
+    ulonglong2 v[NU];                        // code planes (lo, hi) of units u0 .. u0+jl
+    uint64_t nv[NU];                         // N plane of the same units (super-map path, flagged windows)
+    uint64_t cw;                             // coarse path: N bits of 1024-base blocks [32*w, 32*w + 64),
+                                             // w = coarse_word(u0) (recomputed, not carried)
     int64_t u0;
     unsigned sh;
     int odd, jl;                             // word parity; last needed unit (relative to u0)
     bool ok[NU];
 };
 
+// Does any base of [g0, g0 + W) (clipped to the genome) lie in a super block holding an N?
+__device__ __forceinline__ bool super_flag(const uint32_t *s_nsuper, uint32_t shift, int64_t g0, int W,
+                                           uint64_t n_units) {
+    int64_t lo = g0, hi = g0 + W - 1;
+    const int64_t top = (int64_t)(n_units * 64) - 1;
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > top ? top : hi;
+    if (lo > hi) return false;
+    const uint64_t k0 = (uint64_t)lo >> shift, k1 = (uint64_t)hi >> shift;   // k1 <= k0 + 1 (W <= 2^shift)
+    return ((s_nsuper[k0 >> 5] >> (k0 & 31)) & 1u) || ((s_nsuper[k1 >> 5] >> (k1 & 31)) & 1u);
+}
+
+// First of the two coarse-map words loaded for a window whose first unit is u0.
+__device__ __forceinline__ int64_t coarse_word(const fc2_genome_view &g, int64_t u0) {
+    const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
+    const int64_t nw = (nb + 31) >> 5;
+    int64_t b0 = u0 >> 4;
+    b0 = b0 < 0 ? 0 : (b0 >= nb ? nb - 1 : b0);
+    const int64_t w = b0 >> 5;
+    return nw >= 2 ? (w > nw - 2 ? nw - 2 : w) : 0;
+}
+
+// s_nsuper: the LDS copy of g.nsuper, or nullptr (then the coarse map decides in window_finish,
+// one round trip later).
 template <int NQ>
-__device__ __forceinline__ void window_issue(const fc2_genome_view &g, uint64_t cstart, int64_t ws, int W,
-                                             WinRaw<NQ> &R) {
+__device__ __forceinline__ void window_issue(const fc2_genome_view &g, const uint32_t *s_nsuper, uint64_t cstart,
+                                             int64_t ws, int W, WinRaw<NQ> &R) {
     constexpr int NU = WinRaw<NQ>::NU;
     const int64_t g0 = (int64_t)cstart + ws;
     const int64_t q0 = g0 >> 5;              // first 32-bit word (floor)
@@ -100,30 +133,43 @@ __device__ __forceinline__ void window_issue(const fc2_genome_view &g, uint64_t 
     const ulonglong2 *U = (straddle && g.units_twin) ? reinterpret_cast<const ulonglong2 *>(g.units_twin) + 4
                                                      : reinterpret_cast<const ulonglong2 *>(g.units);
     const int64_t last = (int64_t)g.n_units - 1;
+    const bool nflag = s_nsuper && super_flag(s_nsuper, g.nsuper_shift, g0, W, g.n_units);
 #pragma unroll
     for (int j = 0; j < NU; ++j) {
-        const int64_t u = R.u0 + (j < R.jl ? j : R.jl);     // unneeded units re-read the last needed one
+        const int64_t u = R.u0 + j;
+        const int64_t uc = u < 0 ? 0 : (u > last ? last : u);
         R.ok[j] = j <= R.jl && u >= 0 && u <= last;
-        R.v[j] = U[u < 0 ? 0 : (u > last ? last : u)];
+        // every request is an L2 transaction even when it hits (profiles/r01: ~0.29 ms per extra
+        // request per pair at 50M pairs), so units past the window are not loaded at all
+        R.v[j] = ulonglong2{0ull, 0ull};
+        R.nv[j] = 0;
+        if (j < 2 || j <= R.jl) R.v[j] = U[uc];
+        if (nflag && j <= R.jl) R.nv[j] = g.nplane[uc];
     }
-    const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
-    int64_t b0 = R.u0 >> 4, b1 = (R.u0 + NU - 1) >> 4;
-    b0 = b0 < 0 ? 0 : (b0 >= nb ? nb - 1 : b0);
-    b1 = b1 < 0 ? 0 : (b1 >= nb ? nb - 1 : b1);
-    R.cw0 = g.ncoarse[b0 >> 5];               // raw words: consumed (shifted) only in window_finish
-    R.cw1 = g.ncoarse[b1 >> 5];
+    R.cw = 0;
+    if (!s_nsuper) {
+        // coarse N bits of the window's first and last 1024-base block (b1 <= b0 + 1) with ONE
+        // dword-aligned 8-byte load covering words w, w+1; consumed only in window_finish
+        const int64_t w = coarse_word(g, R.u0);
+        if ((((g.n_units + 15) >> 4) + 31) >> 5 >= 2)
+            R.cw = *reinterpret_cast<const uint64_t *>(g.ncoarse + w);   // 4-B aligned: a dwordx2 needs no more
+        else
+            R.cw = g.ncoarse[0];
+    }
 }
 
 template <int NQ>
-__device__ __forceinline__ void window_finish(const fc2_genome_view &g, const WinRaw<NQ> &R, int64_t csize,
-                                              int64_t ws, int W, P32<NQ> &P) {
+__device__ __forceinline__ void window_finish(const fc2_genome_view &g, const uint32_t *s_nsuper, const WinRaw<NQ> &R,
+                                              int64_t csize, int64_t ws, int W, P32<NQ> &P) {
     constexpr int NU = WinRaw<NQ>::NU;
-    uint32_t xl[2 * NU], xh[2 * NU];
+    uint32_t xl[2 * NU], xh[2 * NU], xn[2 * NU];
 #pragma unroll
     for (int j = 0; j < NU; ++j) {
         const ulonglong2 v = R.ok[j] ? R.v[j] : ulonglong2{0ull, 0ull};
+        const uint64_t n = R.ok[j] ? R.nv[j] : 0ull;
         xl[2 * j] = (uint32_t)v.x; xl[2 * j + 1] = (uint32_t)(v.x >> 32);
         xh[2 * j] = (uint32_t)v.y; xh[2 * j + 1] = (uint32_t)(v.y >> 32);
+        xn[2 * j] = (uint32_t)n; xn[2 * j + 1] = (uint32_t)(n >> 32);
     }
     const int odd = R.odd;
     const unsigned sh = R.sh;
@@ -136,27 +182,38 @@ __device__ __forceinline__ void window_finish(const fc2_genome_view &g, const Wi
     }
     P.lo[NQ] = 0; P.hi[NQ] = 0;
 
-    // blocks outside the genome hold no N; the clamped coarse words then belong to another block
-    const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
-    const int64_t b0 = R.u0 >> 4, b1 = (R.u0 + NU - 1) >> 4;
-    const bool anyN = ((b0 >= 0 && b0 < nb) && ((R.cw0 >> (b0 & 31)) & 1u)) ||
-                      ((b1 != b0 && b1 >= 0 && b1 < nb) && ((R.cw1 >> (b1 & 31)) & 1u));
-    if (anyN) {
-        uint32_t xn[2 * NU];
-#pragma unroll
-        for (int j = 0; j < NU; ++j) {
-            const int64_t u = R.u0 + j;
-            const uint64_t v = (u >= 0 && (uint64_t)u < g.n_units) ? g.nplane[u] : 0ull;
-            xn[2 * j] = (uint32_t)v; xn[2 * j + 1] = (uint32_t)(v >> 32);
-        }
+    if (s_nsuper) {                          // N plane already loaded for flagged windows (else zero)
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
             const uint32_t n0 = odd ? xn[k + 1] : xn[k], n1 = odd ? xn[k + 2] : xn[k + 1];
             P.n[k] = alignr(n1, n0, sh);
         }
     } else {
+        // blocks outside the genome hold no N; the clamped coarse words then belong to another block
+        const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
+        const int64_t b0 = R.u0 >> 4, b1 = (R.u0 + NU - 1) >> 4;
+        const int64_t cwi = coarse_word(g, R.u0);
+        auto nbit = [&](int64_t b) -> bool {
+            const int64_t k = b - 32 * cwi;
+            return b >= 0 && b < nb && k >= 0 && k < 64 && ((R.cw >> k) & 1ull);
+        };
+        const bool anyN = nbit(b0) || (b1 != b0 && nbit(b1));
+        if (anyN) {
 #pragma unroll
-        for (int k = 0; k < NQ; ++k) P.n[k] = 0;
+            for (int j = 0; j < NU; ++j) {
+                const int64_t u = R.u0 + j;
+                const uint64_t v = (u >= 0 && (uint64_t)u < g.n_units) ? g.nplane[u] : 0ull;
+                xn[2 * j] = (uint32_t)v; xn[2 * j + 1] = (uint32_t)(v >> 32);
+            }
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) {
+                const uint32_t n0 = odd ? xn[k + 1] : xn[k], n1 = odd ? xn[k + 2] : xn[k + 1];
+                P.n[k] = alignr(n1, n0, sh);
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) P.n[k] = 0;
+        }
     }
     P.n[NQ] = 0;
 
@@ -231,35 +288,43 @@ __device__ __forceinline__ uint64_t xcd_block(uint32_t b, uint32_t nwg) {
     return (uint64_t)x * q + (x < r ? x : r) + j;
 }
 
+// One pair per lane of tile t: the hot path.  s_cstart/s_csize: LDS chromosome table (if lds_tab);
+// s_nsuper: LDS super-coarse N map or nullptr.
 template <int NQ, bool NT>
-__global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
-                                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
-                                                           uint32_t tw, int swizzle) {
-    const uint64_t blk = swizzle ? xcd_block(blockIdx.x, gridDim.x) : (uint64_t)blockIdx.x;
-    const uint64_t i = blk * kBlock + threadIdx.x;
+__device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &bv,
+                                          uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask, uint32_t tw,
+                                          uint64_t i, const uint64_t *s_cstart, const int64_t *s_csize, bool lds_tab,
+                                          const uint32_t *s_nsuper) {
     if (i >= bv.n) return;
     // round trip 1: the pair record and its read rows (both indexed by i only)
-    const fc2_pair pr = ld_pair<NT>(bv.pairs + i);
+    const u64x2 prv = ld_pair_raw<NT>(bv.pairs + i);
     constexpr int R = NQ + 1;                  // 64-bit row words the largest row can use (2l <= 64R)
     uint64_t rv[R];
 #pragma unroll
     for (int j = 0; j < R; ++j)
         rv[j] = ((uint32_t)j < bv.rw) ? ld_stream<NT>(bv.read_words + (uint64_t)j * bv.stride + i) : 0ull;
+    fc2_pair pr;
+    __builtin_memcpy(&pr, &prv, sizeof pr);
     if (pr.flags & FC2_PAIR_BYTEPATH) return;  // left for the byte-exact kernel
 
     const int e = p.asize - p.margin;
     const int l = (int)pr.read_len - 2 * e;
     const bool want_ties = p.allhits != 0;
     const int W = l + 2;                       // flank, find_circ.py:900
-    // round trip 2: the chromosome table (L2-resident)
+    // chromosome of the pair: LDS, or (very many contigs) one more round trip to L2
     uint64_t cstart = 0;
     int64_t csize = (int64_t)1 << 62;          // dummy genome: every window is all 'N'
     if (!g.dummy) {
         const bool known = pr.chrom < g.n_chrom;
         const uint32_t c = known ? pr.chrom : 0u;
-        cstart = g.chrom_start[c];
-        csize = g.chrom_size[c];
-        __builtin_amdgcn_sched_barrier(0);     // both loads issued before either is waited on
+        if (lds_tab) {
+            cstart = s_cstart[c];
+            csize = s_csize[c];
+        } else {
+            cstart = g.chrom_start[c];
+            csize = g.chrom_size[c];
+            __builtin_amdgcn_sched_barrier(0); // both loads issued before either is waited on
+        }
         if (!known) { cstart = 0; csize = 0; }
     }
     const int64_t wsA = (int64_t)pr.a_pos + e;
@@ -278,8 +343,8 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
     // round trip 3: both genome windows (find_circ.py:900-902) and their coarse N words
     WinRaw<NQ> rA, rB;
     if (!g.dummy) {
-        window_issue<NQ>(g, cstart, wsA, W, rA);
-        window_issue<NQ>(g, cstart, wsB, W, rB);
+        window_issue<NQ>(g, s_nsuper, cstart, wsA, W, rA);
+        window_issue<NQ>(g, s_nsuper, cstart, wsB, W, rB);
     }
     __builtin_amdgcn_sched_barrier(0);         // every window load in flight before the first wait
 
@@ -317,8 +382,8 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
 
     P32<NQ> A, B;
     if (!g.dummy) {
-        window_finish<NQ>(g, rA, csize, wsA, W, A);
-        window_finish<NQ>(g, rB, csize, wsB, W, B);
+        window_finish<NQ>(g, s_nsuper, rA, csize, wsA, W, A);
+        window_finish<NQ>(g, s_nsuper, rB, csize, wsB, W, B);
     } else {
         window_dummy<NQ>(A);
         window_dummy<NQ>(B);
@@ -445,18 +510,68 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
     }
 }
 
+
+// STAGE: the block stages the chromosome table and the super-coarse N map in LDS (8 + 8 KB)
+// behind one barrier, so a window's N test and its chromosome cost no memory request (read-order
+// batches over a large genome: every L2 request counts there).  Without STAGE both come from L2,
+// which is cheaper when the batch is locus-ordered or the genome is cache-resident (the kernel is
+// then VALU-bound and the staging's registers and barrier cost more than they save).
+template <int NQ, bool NT, bool STAGE>
+__global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+                                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
+                                                           uint32_t tw, int swizzle) {
+    const uint64_t blk = swizzle ? xcd_block(blockIdx.x, gridDim.x) : (uint64_t)blockIdx.x;
+    const uint64_t i = blk * kBlock + threadIdx.x;
+    if constexpr (STAGE) {
+        __shared__ uint64_t s_cstart[kChromLds];
+        __shared__ int64_t s_csize[kChromLds];
+        __shared__ __attribute__((aligned(16))) uint32_t s_nsuper_buf[kSuperLds];
+        const bool lds_tab = !g.dummy && g.n_chrom <= (uint32_t)kChromLds;
+        const bool lds_super = !g.dummy && g.nsuper && g.nsuper_words <= (uint32_t)kSuperLds;
+        if (lds_super) {                       // 4 words per thread per pass, two passes (8 KB)
+            uint4 q[2];
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const uint32_t w = c * (kSuperLds / 2) + 4 * threadIdx.x;
+                q[c] = uint4{0u, 0u, 0u, 0u}; // allocation is a multiple of 4 words (fc2_bp.h)
+                if (w < g.nsuper_words) q[c] = *reinterpret_cast<const uint4 *>(g.nsuper + w);
+            }
+#pragma unroll
+            for (int c = 0; c < 2; ++c)
+                *reinterpret_cast<uint4 *>(s_nsuper_buf + c * (kSuperLds / 2) + 4 * threadIdx.x) = q[c];
+        }
+        if (lds_tab) {
+            static_assert(kChromLds == 2 * kBlock, "two table entries per thread");
+            const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kBlock;
+            uint64_t a0 = 0, a1 = 0;
+            int64_t z0 = 0, z1 = 0;
+            if (k0 < g.n_chrom) { a0 = g.chrom_start[k0]; z0 = g.chrom_size[k0]; }
+            if (k1 < g.n_chrom) { a1 = g.chrom_start[k1]; z1 = g.chrom_size[k1]; }
+            s_cstart[k0] = a0; s_csize[k0] = z0;
+            s_cstart[k1] = a1; s_csize[k1] = z1;
+        }
+        if (lds_tab || lds_super) __syncthreads();
+        scan_pair<NQ, NT>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, lds_tab,
+                          lds_super ? s_nsuper_buf : nullptr);
+    } else {
+        scan_pair<NQ, NT>(p, g, bv, out, tiemask, tw, i, nullptr, nullptr, false, nullptr);
+    }
+}
+
 }  // namespace
 
 namespace fc2 {
 
-void launch_scan32(int nq, bool nt, int swizzle, unsigned grid, hipStream_t s, const fc2_params &p,
+void launch_scan32(int nq, bool nt, int swizzle, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
                    const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
-#define FC2_L32(NQV, NTV) \
-    hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV>), dim3(grid), dim3(kBlock), 0, s, p, g, b, out, tiemask, tw, \
-                       swizzle)
-    if (nq <= 4) { if (nt) FC2_L32(4, true); else FC2_L32(4, false); }
-    else if (nq <= 8) { if (nt) FC2_L32(8, true); else FC2_L32(8, false); }
-    else { if (nt) FC2_L32(16, true); else FC2_L32(16, false); }
+#define FC2_L32(NQV, NTV, STV)                                                                                   \
+    hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV, STV>), dim3(grid), dim3(kBlock), 0, s, p, g, b, out, tiemask, \
+                       tw, swizzle)
+#define FC2_L32S(NQV, NTV) do { if (stage) FC2_L32(NQV, NTV, true); else FC2_L32(NQV, NTV, false); } while (0)
+    if (nq <= 4) { if (nt) FC2_L32S(4, true); else FC2_L32S(4, false); }
+    else if (nq <= 8) { if (nt) FC2_L32S(8, true); else FC2_L32S(8, false); }
+    else { if (nt) FC2_L32S(16, true); else FC2_L32S(16, false); }
+#undef FC2_L32S
 #undef FC2_L32
 }
 

@@ -47,6 +47,8 @@ class Genome:
         self.n_units = 0
         self.units = self.nplane = self.ncoarse = None      # torch device tensors
         self.units_twin = None                              # units shifted by half a line (fc2_twin_launch)
+        self.nsuper = None                                  # LDS-sized N map (fc2_nsuper_launch)
+        self.nsuper_shift = self.nsuper_words = 0
         self.d_chrom_start = self.d_chrom_size = None
         self.dummy = False
         self.fasta = None                                   # ctypes handle (host FASTA) or None
@@ -158,14 +160,22 @@ class Genome:
             self.units_twin = torch.empty(2 * (self.n_units + 8), dtype=torch.int64, device=self.device)
             N.check(N.lib().fc2_twin_launch(self.units.data_ptr(), self.n_units, self.units_twin.data_ptr(),
                                             torch.cuda.current_stream(self.device).cuda_stream))
+            sh, nw = ctypes.c_uint32(), ctypes.c_uint32()
+            N.check(N.lib().fc2_nsuper_geometry(self.n_units, ctypes.byref(sh), ctypes.byref(nw)))
+            self.nsuper_shift, self.nsuper_words = sh.value, nw.value
+            self.nsuper = torch.empty((nw.value + 3) // 4 * 4, dtype=torch.int32, device=self.device)
+            N.check(N.lib().fc2_nsuper_launch(self.ncoarse.data_ptr(), self.n_units, self.nsuper.data_ptr(),
+                                              torch.cuda.current_stream(self.device).cuda_stream))
 
     # ------------------------------------------------------------------ access
     def view(self) -> N.GenomeView:
         if self.dummy:
-            return N.GenomeView(None, None, None, None, None, 0, 0xFFFFFFFF, 1, None)
+            return N.GenomeView(None, None, None, None, None, 0, 0xFFFFFFFF, 1, None, None, 0, 0)
         return N.GenomeView(self.units.data_ptr(), self.nplane.data_ptr(), self.ncoarse.data_ptr(),
                             self.d_chrom_start.data_ptr(), self.d_chrom_size.data_ptr(), self.n_units,
-                            len(self.names), 0, self.units_twin.data_ptr() if self.units_twin is not None else None)
+                            len(self.names), 0, self.units_twin.data_ptr() if self.units_twin is not None else None,
+                            self.nsuper.data_ptr() if self.nsuper is not None else None, self.nsuper_shift,
+                            self.nsuper_words)
 
     def chrom_index(self, name: str) -> int:
         """Chromosome -> table index; KeyError like indexed_fasta.get_data (find_circ.py:193)."""

@@ -120,6 +120,13 @@ typedef struct fc2_genome_view {
                                     a window that straddles a line of `units` lies inside one line of
                                     the twin, so a random window costs one line fill instead of ~1.15
                                     (fc2_twin_launch builds it) */
+    const uint32_t *nsuper;      /* device [nsuper_words rounded up to a multiple of 4] or NULL: bit k
+                                    set iff global bases
+                                    [k << nsuper_shift, (k+1) << nsuper_shift) contain an N; small
+                                    enough (<= 2048 words) to live in LDS, so a window's N test costs
+                                    no memory request (fc2_nsuper_geometry / fc2_nsuper_launch) */
+    uint32_t nsuper_shift;
+    uint32_t nsuper_words;
 } fc2_genome_view;
 
 /* ---- a batch of anchor pairs in device memory (SoA) --------------------- */
@@ -172,6 +179,9 @@ int         fc2_device_count(int *count);
 #define FC2_TUNE_REORDER_NT 5  /* fc2_reorder: 1 = non-temporal scatter stores (default 0) */
 #define FC2_TUNE_TWIN 6        /* windows that straddle a line read the genome view's twin: 0 never,
                                   1 always, 2 (default) unless the batch is FC2_BATCH_LOCUS_ORDERED */
+#define FC2_TUNE_STAGE 7       /* scan kernel stages the chromosome table and nsuper in LDS: 0 never,
+                                  1 always, 2 (default) for batches not locus-ordered over a genome of
+                                  >= 64 MiB of code planes */
 int         fc2_set_tuning(int key, int value);
 
 /* Largest l the register kernel handles (longer reads go to the byte kernel). */
@@ -299,6 +309,10 @@ int fc2_synth_genome_launch(uint64_t seed, uint64_t *units, uint64_t *nplane, ui
                             uint32_t n_intervals, void *stream);
 /* Build units_twin (device [2*(n_units+8)]) from units (device [2*n_units]). */
 int fc2_twin_launch(const uint64_t *units, uint64_t n_units, uint64_t *units_twin, void *stream);
+/* Super-coarse N map for n_units: *shift (>= 10) and *words (<= 2048). */
+int fc2_nsuper_geometry(uint64_t n_units, uint32_t *shift, uint32_t *words);
+/* Build nsuper (device [words]) from the coarse N map ncoarse (device). */
+int fc2_nsuper_launch(const uint32_t *ncoarse, uint64_t n_units, uint32_t *nsuper, void *stream);
 /* Rebuild the coarse N map from nplane (device). */
 int fc2_coarse_launch(const uint64_t *nplane, uint32_t *ncoarse, uint64_t n_units, void *stream);
 

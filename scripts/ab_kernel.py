@@ -42,6 +42,7 @@ def main():
         N.lib().fc2_set_tuning(2, 0 if "k64" in v else 1)
         N.lib().fc2_set_tuning(3, 0 if "sw0" in v else (1 if "sw1" in v else 2))
         N.lib().fc2_set_tuning(6, 0 if "tw0" in v else (1 if "tw1" in v else 2))
+        N.lib().fc2_set_tuning(7, 0 if "st0" in v else (1 if "st1" in v else 2))
 
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream(dev)

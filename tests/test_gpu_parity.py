@@ -23,6 +23,15 @@ from find_circ2_amd import _native as N  # noqa: E402
 from oracle.bp_oracle import Options as ROptions, RefIndexedFasta, Span, find_breakpoints  # noqa: E402
 
 
+@pytest.fixture(params=[1, 0], ids=["stage", "nostage"], autouse=True)
+def scan_variant(request):
+    """Every parity case runs through both bp_scan32 forms: LDS-staged (chromosome table +
+    super-coarse N map) and unstaged (coarse map from L2); the default picks per batch."""
+    N.lib().fc2_set_tuning(7, request.param)
+    yield request.param
+    N.lib().fc2_set_tuning(7, 2)
+
+
 def _dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
