@@ -158,6 +158,107 @@ __device__ __forceinline__ void window_issue(const fc2_genome_view &g, const uin
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Cooperative unit loads (read-order batches, NQ == 4).  Every 16-B load instruction is one L2
+// request per distinct line it touches, and a lane's two unit loads of one window sit in two
+// instructions: two requests for one line.  Here lanes 2m and 2m+1 load units 0 and 1 of the
+// window of pair 32c + m in instruction c, so one request serves both (profiles/r01:
+// pattern_probe paired vs unpaired); the units travel back to their owner lane through LDS.
+// The owner still loads a window's rare third unit and its N-plane units itself.
+// Packed window for the loading lanes: (u0 + 8) in bits 0..30, bit 31 = read the twin.
+template <int NQ>
+__device__ __forceinline__ uint32_t window_geom(const fc2_genome_view &g, uint64_t cstart, int64_t ws, int W,
+                                                WinRaw<NQ> &R) {
+    constexpr int NU = WinRaw<NQ>::NU;
+    const int64_t g0 = (int64_t)cstart + ws;
+    const int64_t q0 = g0 >> 5;
+    R.sh = (unsigned)(g0 & 31);
+    R.u0 = q0 >> 1;
+    R.odd = (int)(q0 & 1);
+    R.jl = (R.odd + (((int)R.sh + W - 1) >> 5)) >> 1;
+    const int64_t last = (int64_t)g.n_units - 1;
+#pragma unroll
+    for (int j = 0; j < NU; ++j) R.ok[j] = j <= R.jl && R.u0 + j >= 0 && R.u0 + j <= last;
+    const bool twin = g.units_twin && (int)(R.u0 & 7) + R.jl >= 8;
+    return (uint32_t)(R.u0 + 8) | ((uint32_t)twin << 31);
+}
+
+__device__ __forceinline__ const ulonglong2 *unit_base(const fc2_genome_view &g, uint32_t packed) {
+    return (packed >> 31) ? reinterpret_cast<const ulonglong2 *>(g.units_twin) + 4
+                          : reinterpret_cast<const ulonglong2 *>(g.units);
+}
+
+__device__ __forceinline__ ulonglong2 unit_load(const fc2_genome_view &g, uint32_t packed, int j) {
+    const int64_t last = (int64_t)g.n_units - 1;
+    int64_t u = (int64_t)(packed & 0x7FFFFFFFu) - 8 + j;
+    u = u < 0 ? 0 : (u > last ? last : u);   // out-of-genome units are zeroed by the owner's ok[]
+    return unit_base(g, packed)[u];
+}
+
+// Issue phase for BOTH windows of the lane's pair; all 64 lanes must execute it (inactive lanes
+// pass a harmless geometry).  cl[X][c]: the unit this lane loaded for window X in instruction c.
+template <int NQ>
+__device__ __forceinline__ void windows_issue_coop(const fc2_genome_view &g, const uint32_t *s_nsuper,
+                                                   uint64_t cstart, int64_t wsA, int64_t wsB, int W, bool active,
+                                                   WinRaw<NQ> &rA, WinRaw<NQ> &rB, ulonglong2 (&cl)[2][2]) {
+    constexpr int NU = WinRaw<NQ>::NU;
+    static_assert(NU == 3, "cooperative loads cover units 0 and 1; the owner loads unit 2");
+    const uint32_t pk[2] = {window_geom<NQ>(g, cstart, wsA, W, rA), window_geom<NQ>(g, cstart, wsB, W, rB)};
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint32_t src = (uint32_t)__builtin_amdgcn_ds_bpermute((32 * c + (lane >> 1)) << 2, (int)pk[x]);
+            cl[x][c] = unit_load(g, src, lane & 1);
+        }
+    }
+    WinRaw<NQ> *R[2] = {&rA, &rB};
+    const int64_t wsx[2] = {wsA, wsB};
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        WinRaw<NQ> &Q = *R[x];
+        Q.v[0] = Q.v[1] = Q.v[2] = ulonglong2{0ull, 0ull};
+        if (active && Q.jl >= 2) Q.v[2] = unit_load(g, pk[x], 2);
+        const int64_t g0 = (int64_t)cstart + wsx[x];
+        const bool nflag = active && s_nsuper && super_flag(s_nsuper, g.nsuper_shift, g0, W, g.n_units);
+        const int64_t last = (int64_t)g.n_units - 1;
+#pragma unroll
+        for (int j = 0; j < NU; ++j) {
+            const int64_t u = Q.u0 + j;
+            Q.nv[j] = 0;
+            if (nflag && j <= Q.jl) Q.nv[j] = g.nplane[u < 0 ? 0 : (u > last ? last : u)];
+        }
+        Q.cw = 0;
+        if (!s_nsuper && active) {
+            const int64_t w = coarse_word(g, Q.u0);
+            if ((((g.n_units + 15) >> 4) + 31) >> 5 >= 2)
+                Q.cw = *reinterpret_cast<const uint64_t *>(g.ncoarse + w);
+            else
+                Q.cw = g.ncoarse[0];
+        }
+    }
+}
+
+// Exchange: every lane parks what it loaded in its wave's LDS slots, then takes its own units.
+template <int NQ>
+__device__ __forceinline__ void windows_exchange_coop(ulonglong2 *xchg, const ulonglong2 (&cl)[2][2],
+                                                      WinRaw<NQ> &rA, WinRaw<NQ> &rB) {
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) xchg[(2 * x + c) * 64 + lane] = cl[x][c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int c = lane >> 5, m = lane & 31;
+    rA.v[0] = xchg[(0 + c) * 64 + 2 * m];
+    rA.v[1] = xchg[(0 + c) * 64 + 2 * m + 1];
+    rB.v[0] = xchg[(2 + c) * 64 + 2 * m];
+    rB.v[1] = xchg[(2 + c) * 64 + 2 * m + 1];
+}
+
 template <int NQ>
 __device__ __forceinline__ void window_finish(const fc2_genome_view &g, const uint32_t *s_nsuper, const WinRaw<NQ> &R,
                                               int64_t csize, int64_t ws, int W, P32<NQ> &P) {
@@ -290,27 +391,36 @@ __device__ __forceinline__ uint64_t xcd_block(uint32_t b, uint32_t nwg) {
 
 // One pair per lane of tile t: the hot path.  s_cstart/s_csize: LDS chromosome table (if lds_tab);
 // s_nsuper: LDS super-coarse N map or nullptr.
-template <int NQ, bool NT>
+// COOP: cooperative window loads (windows_issue_coop); then no lane may leave before the
+// exchange, so exits are deferred through `active`.  xchg: this wave's 4 x 64 LDS slots.
+template <int NQ, bool NT, bool COOP>
 __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &bv,
                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask, uint32_t tw,
                                           uint64_t i, const uint64_t *s_cstart, const int64_t *s_csize, bool lds_tab,
-                                          const uint32_t *s_nsuper) {
-    if (i >= bv.n) return;
+                                          const uint32_t *s_nsuper, ulonglong2 *xchg) {
+    const bool live = i < bv.n;
+    if (!COOP && !live) return;
     // round trip 1: the pair record and its read rows (both indexed by i only)
-    const u64x2 prv = ld_pair_raw<NT>(bv.pairs + i);
     constexpr int R = NQ + 1;                  // 64-bit row words the largest row can use (2l <= 64R)
+    u64x2 prv = {0ull, 0ull};
     uint64_t rv[R];
 #pragma unroll
-    for (int j = 0; j < R; ++j)
-        rv[j] = ((uint32_t)j < bv.rw) ? ld_stream<NT>(bv.read_words + (uint64_t)j * bv.stride + i) : 0ull;
+    for (int j = 0; j < R; ++j) rv[j] = 0;
+    if (live) {
+        prv = ld_pair_raw<NT>(bv.pairs + i);
+#pragma unroll
+        for (int j = 0; j < R; ++j)
+            rv[j] = ((uint32_t)j < bv.rw) ? ld_stream<NT>(bv.read_words + (uint64_t)j * bv.stride + i) : 0ull;
+    }
     fc2_pair pr;
     __builtin_memcpy(&pr, &prv, sizeof pr);
-    if (pr.flags & FC2_PAIR_BYTEPATH) return;  // left for the byte-exact kernel
+    bool active = live && !(pr.flags & FC2_PAIR_BYTEPATH);   // BYTEPATH: left for the byte-exact kernel
+    if (!COOP && !active) return;
 
     const int e = p.asize - p.margin;
     const int l = (int)pr.read_len - 2 * e;
     const bool want_ties = p.allhits != 0;
-    const int W = l + 2;                       // flank, find_circ.py:900
+    int W = l + 2;                             // flank, find_circ.py:900
     // chromosome of the pair: LDS, or (very many contigs) one more round trip to L2
     uint64_t cstart = 0;
     int64_t csize = (int64_t)1 << 62;          // dummy genome: every window is all 'N'
@@ -329,20 +439,26 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     }
     const int64_t wsA = (int64_t)pr.a_pos + e;
     const int64_t wsB = (int64_t)pr.b_aend - e - W;
-    if ((pr.flags & FC2_PAIR_SKIP) || l < 0 || l > 32 * NQ - 2 || pr.chrom >= g.n_chrom || wsA > csize ||
-        wsA + W < 0 || wsB > csize || wsB + W < 0) {
+    if (active && ((pr.flags & FC2_PAIR_SKIP) || l < 0 || l > 32 * NQ - 2 || pr.chrom >= g.n_chrom ||
+                   wsA > csize || wsA + W < 0 || wsB > csize || wsB + W < 0)) {
         // skipped / empty x-range: no hit; anything else is routed to the byte path by the host
         const bool err = !(pr.flags & FC2_PAIR_SKIP) && l >= 0;
         Best32 none;
         st_stream<NT>(out + i, pack_result(none, 0, err ? FC2_RES_ERR_WIN : 0u));
         if (want_ties)
             for (uint32_t k = 0; k < tw; ++k) tiemask[(uint64_t)k * bv.stride + i] = 0;
-        return;
+        if (!COOP) return;
+        active = false;
     }
 
     // round trip 3: both genome windows (find_circ.py:900-902) and their coarse N words
     WinRaw<NQ> rA, rB;
-    if (!g.dummy) {
+    ulonglong2 cl[2][2];
+    if constexpr (COOP) {
+        if (!active) W = 2;                    // a harmless window for a lane that only loads for others
+        windows_issue_coop<NQ>(g, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active,
+                               rA, rB, cl);
+    } else if (!g.dummy) {
         window_issue<NQ>(g, s_nsuper, cstart, wsA, W, rA);
         window_issue<NQ>(g, s_nsuper, cstart, wsB, W, rB);
     }
@@ -366,7 +482,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         const unsigned s = (unsigned)(l & 31);
 #pragma unroll
         for (int k = 0; k < NQ; ++k) Ihi[k] = alignr(h[k + 1], h[k], s) & rmask32(0, l, k);
-        if (pr.flags & FC2_PAIR_READ_N) {
+        if (active && (pr.flags & FC2_PAIR_READ_N)) {
 #pragma unroll
             for (int j = 0; j < (NQ + 1) / 2; ++j) {
                 const uint64_t v =
@@ -380,6 +496,10 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         }
     }
 
+    if constexpr (COOP) {
+        windows_exchange_coop<NQ>(xchg, cl, rA, rB);
+        if (!active) return;
+    }
     P32<NQ> A, B;
     if (!g.dummy) {
         window_finish<NQ>(g, s_nsuper, rA, csize, wsA, W, A);
@@ -551,10 +671,20 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
             s_cstart[k1] = a1; s_csize[k1] = z1;
         }
         if (lds_tab || lds_super) __syncthreads();
-        scan_pair<NQ, NT>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, lds_tab,
-                          lds_super ? s_nsuper_buf : nullptr);
+        if constexpr (NQ == 4) {
+            // cooperative unit loads need every window inside the genome arrays' reach: the dummy
+            // genome has none (uniform branch)
+            __shared__ ulonglong2 s_xchg[kBlock / 64][4 * 64];
+            if (!g.dummy) {
+                scan_pair<NQ, NT, true>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, lds_tab,
+                                        lds_super ? s_nsuper_buf : nullptr, s_xchg[threadIdx.x >> 6]);
+                return;
+            }
+        }
+        scan_pair<NQ, NT, false>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, lds_tab,
+                                 lds_super ? s_nsuper_buf : nullptr, nullptr);
     } else {
-        scan_pair<NQ, NT>(p, g, bv, out, tiemask, tw, i, nullptr, nullptr, false, nullptr);
+        scan_pair<NQ, NT, false>(p, g, bv, out, tiemask, tw, i, nullptr, nullptr, false, nullptr, nullptr);
     }
 }
 

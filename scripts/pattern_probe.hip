@@ -20,7 +20,7 @@ __device__ __forceinline__ uint64_t mix(uint64_t x) {
     return x ^ (x >> 31);
 }
 
-template <int G, bool STREAM>
+template <int G, bool STREAM, bool PAIRED = false>
 __global__ __launch_bounds__(256) void pattern(const ulonglong2 *__restrict__ pairs, const uint64_t *__restrict__ words,
                                                int rw, const ulonglong2 *__restrict__ table, uint64_t n_units,
                                                uint64_t n, uint64_t *__restrict__ out) {
@@ -36,7 +36,11 @@ __global__ __launch_bounds__(256) void pattern(const ulonglong2 *__restrict__ pa
     }
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-        const uint64_t u = mix(i * 0x9E37ull + k + (seed & 1)) % n_units;
+        // PAIRED: lanes 2m, 2m+1 read the two adjacent 16-B units of ONE random 32-B span
+        // (one line), i.e. per lane one 16-B load but half the distinct lines
+        const uint64_t key = PAIRED ? (i >> 1) : i;
+        uint64_t u = mix(key * 0x9E37ull + k + (seed & 1)) % n_units;
+        if (PAIRED) u = (u & ~1ull) + (i & 1);
         const ulonglong2 v = table[u];
         acc ^= v.x + v.y;
     }
@@ -44,17 +48,17 @@ __global__ __launch_bounds__(256) void pattern(const ulonglong2 *__restrict__ pa
     else if (acc == 0x123456789ull) out[i] = acc;     // keeps the gathers live without a store stream
 }
 
-template <int G, bool S>
+template <int G, bool S, bool PR = false>
 float run(const ulonglong2 *pairs, const uint64_t *words, int rw, const ulonglong2 *t, uint64_t nu, uint64_t n,
           uint64_t *out) {
     hipEvent_t a, b;
     (void)hipEventCreate(&a);
     (void)hipEventCreate(&b);
     const unsigned grid = (unsigned)((n + 255) / 256);
-    pattern<G, S><<<grid, 256>>>(pairs, words, rw, t, nu, n, out);
+    pattern<G, S, PR><<<grid, 256>>>(pairs, words, rw, t, nu, n, out);
     (void)hipDeviceSynchronize();
     (void)hipEventRecord(a);
-    for (int r = 0; r < 10; ++r) pattern<G, S><<<grid, 256>>>(pairs, words, rw, t, nu, n, out);
+    for (int r = 0; r < 10; ++r) pattern<G, S, PR><<<grid, 256>>>(pairs, words, rw, t, nu, n, out);
     (void)hipEventRecord(b);
     (void)hipEventSynchronize(b);
     float ms;
@@ -82,9 +86,11 @@ int main() {
     const float b1 = run<1, true>(pairs, words, rw, t, nu, n, out);
     const float b2 = run<2, true>(pairs, words, rw, t, nu, n, out);
     const float b3 = run<3, true>(pairs, words, rw, t, nu, n, out);
+    const float p4 = run<4, true, true>(pairs, words, rw, t, nu, n, out);
+    const float b4 = run<4, true>(pairs, words, rw, t, nu, n, out);
     printf("{\"pairs\": %llu, \"stream_only_ms\": %.4f, \"gather1_only_ms\": %.4f, \"gather2_only_ms\": %.4f, "
            "\"stream_gather1_ms\": %.4f, \"stream_gather2_ms\": %.4f, \"stream_gather3_ms\": %.4f, "
-           "\"gathers_per_s_2only\": %.4g}\n",
-           (unsigned long long)n, s0, g1, g2, b1, b2, b3, 2.0 * n / (g2 * 1e-3));
+           "\"gathers_per_s_2only\": %.4g, \"stream_gather4_ms\": %.4f, \"stream_gather4_paired_ms\": %.4f}\n",
+           (unsigned long long)n, s0, g1, g2, b1, b2, b3, 2.0 * n / (g2 * 1e-3), b4, p4);
     return 0;
 }
