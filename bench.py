@@ -297,6 +297,26 @@ def cpu_baselines(opt, g, b, budget_s):
         cpu_model=model)
 
 
+def kernel_label(g, ordered: bool) -> str:
+    """The bp_scan32 form fc2_bp_scan_launch picks for this batch (FC2_TUNE_STAGE auto rule)."""
+    staged = (not ordered) and (not g.dummy) and g.n_units * 16 >= (64 << 20)
+    if staged:
+        return ("bp_scan32_kernel<4,NT,STAGE> (one anchor pair per lane; chromosome table + super-coarse N map in "
+                "LDS, lane pairs load each window line with one L2 request)")
+    return "bp_scan32_kernel<4,NT> (one anchor pair per lane)"
+
+
+def pattern_ceiling():
+    """Speed of light of the read-order access pattern on this GPU (scripts/pattern_probe.hip)."""
+    p = os.path.join(ROOT, "profiles", "r01", "pattern_probe.json")
+    try:
+        j = json.load(open(p))
+        return {"ms_per_50M_pairs": j["stream_gather2_ms"], "source": "profiles/r01/pattern_probe.json "
+                "(stream 48 B/pair + 2 random 16-B window gathers, no compute)"}
+    except Exception:
+        return None
+
+
 def main():
     args = parse()
     import torch
@@ -349,9 +369,11 @@ def main():
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel_ms": round(kernel_ms, 4), "algo_bytes_per_pair": bpp,
-                     "kernel": "bp_scan32_kernel<4,NT> (one anchor pair per lane)"},
+                     "kernel": kernel_label(g, args.locus_ordered)},
         "cpu_baseline": None,
     }
+    if args.workload == "hg19" and not args.locus_ordered and b.n == 50_000_000:
+        line["roofline"]["access_pattern_ceiling"] = pattern_ceiling()
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cb = cpu_baselines(opt, g, b, args.cpu_seconds)
         line["cpu_baseline"] = cb["main"]

@@ -49,7 +49,9 @@ def main():
         if not f:
             continue
         hbm = 2 * f["FETCH_SIZE"] * 1024 + wr.get("WRITE_SIZE", 0) * 1024
-        out[key] = {"pairs_per_launch": N_PAIRS, "kernel": "bp_scan32_kernel<4,NT>", "avg_kernel_ns_rocprof": ns,
+        out[key] = {"pairs_per_launch": N_PAIRS, "kernel": ("bp_scan32_kernel<4,NT,STAGE>" if w == "hg19"
+                                                             else "bp_scan32_kernel<4,NT>"),
+                    "avg_kernel_ns_rocprof": ns,
                     "FETCH_SIZE_kB_raw": f["FETCH_SIZE"], "WRITE_SIZE_kB": wr.get("WRITE_SIZE"),
                     "TCC_HIT_sum": h.get("TCC_HIT_sum"), "TCC_MISS_sum": h.get("TCC_MISS_sum"),
                     "hbm_bytes_per_launch": round(hbm), "hbm_bytes_per_pair": round(hbm / N_PAIRS, 1),
