@@ -802,7 +802,8 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         // than the caches (profiles/r01/ab_stage.jsonl)
         const bool big = !g->dummy && g->n_units * 16 >= (64ull << 20);
         const bool stage = g_stage == 2 ? (big && !ordered) : g_stage != 0;
-        fc2::launch_scan32((ml + 2 + 31) / 32, nt, sw, stage, grid, s, *p, gv, *b, out, tiemask, tw);
+        const int opts = sw ? fc2::kOptSwizzle : 0;
+        fc2::launch_scan32((ml + 2 + 31) / 32, nt, opts, stage, grid, s, *p, gv, *b, out, tiemask, tw);
         return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
     }
 #define FC2_LAUNCH(NWV, NTV) \

@@ -7,7 +7,9 @@
 
 namespace fc2 {
 // nq: 32-bit words per plane needed by the batch (rounded up to 4/8/16 inside); grid: one
-// 256-pair tile per block; stage: the LDS-staging kernel variant (see bp_scan32_kernel).
-void launch_scan32(int nq, bool nt, int swizzle, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
+// 256-pair tile per block; stage: the LDS-staging kernel variant (see bp_scan32_kernel);
+// opts: kOptSwizzle.
+constexpr int kOptSwizzle = 1;     // XCD-contiguous block order
+void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
                    const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw);
 }  // namespace fc2

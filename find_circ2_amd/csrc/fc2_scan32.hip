@@ -580,9 +580,17 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
 
     unsigned gtag12 = 0;
     if (Bst.n_hits) {
-        const int x = Bst.best_x;
-        gtag12 = code_at32<NQ>(A, x) | (code_at32<NQ>(A, x + 1) << 3) | (code_at32<NQ>(B, x) << 6) |
-                 (code_at32<NQ>(B, x + 1) << 9);
+        if (!p.noncanonical) {
+            // a canonical hit sits where the GTAG / CTAC mask is set: A[x]A[x+1]B[x]B[x+1] is
+            // "GTAG" or "CTAC" by construction (codes A0 C1 G2 T3), no base lookup needed
+            constexpr unsigned kGTAG = 2u | (3u << 3) | (0u << 6) | (2u << 9);
+            constexpr unsigned kCTAC = 1u | (3u << 3) | (0u << 6) | (1u << 9);
+            gtag12 = Bst.best_minus ? kCTAC : kGTAG;
+        } else {
+            const int x = Bst.best_x;
+            gtag12 = code_at32<NQ>(A, x) | (code_at32<NQ>(A, x + 1) << 3) | (code_at32<NQ>(B, x) << 6) |
+                     (code_at32<NQ>(B, x + 1) << 9);
+        }
     }
     st_stream<NT>(out + i, pack_result(Bst, gtag12, 0));
 
@@ -639,7 +647,8 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
 template <int NQ, bool NT, bool STAGE>
 __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
                                                            uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
-                                                           uint32_t tw, int swizzle) {
+                                                           uint32_t tw, int opts) {
+    const bool swizzle = opts & fc2::kOptSwizzle;
     const uint64_t blk = swizzle ? xcd_block(blockIdx.x, gridDim.x) : (uint64_t)blockIdx.x;
     const uint64_t i = blk * kBlock + threadIdx.x;
     if constexpr (STAGE) {
@@ -692,11 +701,11 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
 
 namespace fc2 {
 
-void launch_scan32(int nq, bool nt, int swizzle, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
+void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
                    const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
 #define FC2_L32(NQV, NTV, STV)                                                                                   \
     hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV, STV>), dim3(grid), dim3(kBlock), 0, s, p, g, b, out, tiemask, \
-                       tw, swizzle)
+                       tw, opts)
 #define FC2_L32S(NQV, NTV) do { if (stage) FC2_L32(NQV, NTV, true); else FC2_L32(NQV, NTV, false); } while (0)
     if (nq <= 4) { if (nt) FC2_L32S(4, true); else FC2_L32S(4, false); }
     else if (nq <= 8) { if (nt) FC2_L32S(8, true); else FC2_L32S(8, false); }
