@@ -89,7 +89,6 @@ struct WinRaw {
     int64_t u0;
     unsigned sh;
     int odd, jl;                             // word parity; last needed unit (relative to u0)
-    bool ok[NU];
 };
 
 // Does any base of [g0, g0 + W) (clipped to the genome) lie in a super block holding an N?
@@ -138,7 +137,6 @@ __device__ __forceinline__ void window_issue(const fc2_genome_view &g, const uin
     for (int j = 0; j < NU; ++j) {
         const int64_t u = R.u0 + j;
         const int64_t uc = u < 0 ? 0 : (u > last ? last : u);
-        R.ok[j] = j <= R.jl && u >= 0 && u <= last;
         // every request is an L2 transaction even when it hits (profiles/r01: ~0.29 ms per extra
         // request per pair at 50M pairs), so units past the window are not loaded at all
         R.v[j] = ulonglong2{0ull, 0ull};
@@ -176,9 +174,6 @@ __device__ __forceinline__ uint32_t window_geom(const fc2_genome_view &g, uint64
     R.u0 = q0 >> 1;
     R.odd = (int)(q0 & 1);
     R.jl = (R.odd + (((int)R.sh + W - 1) >> 5)) >> 1;
-    const int64_t last = (int64_t)g.n_units - 1;
-#pragma unroll
-    for (int j = 0; j < NU; ++j) R.ok[j] = j <= R.jl && R.u0 + j >= 0 && R.u0 + j <= last;
     const bool twin = g.units_twin && (int)(R.u0 & 7) + R.jl >= 8;
     return (uint32_t)(R.u0 + 8) | ((uint32_t)twin << 31);
 }
@@ -191,7 +186,7 @@ __device__ __forceinline__ const ulonglong2 *unit_base(const fc2_genome_view &g,
 __device__ __forceinline__ ulonglong2 unit_load(const fc2_genome_view &g, uint32_t packed, int j) {
     const int64_t last = (int64_t)g.n_units - 1;
     int64_t u = (int64_t)(packed & 0x7FFFFFFFu) - 8 + j;
-    u = u < 0 ? 0 : (u > last ? last : u);   // out-of-genome units are zeroed by the owner's ok[]
+    u = u < 0 ? 0 : (u > last ? last : u);   // out-of-genome positions are masked to 'N' in window_finish
     return unit_base(g, packed)[u];
 }
 
@@ -266,8 +261,10 @@ __device__ __forceinline__ void window_finish(const fc2_genome_view &g, const ui
     uint32_t xl[2 * NU], xh[2 * NU], xn[2 * NU];
 #pragma unroll
     for (int j = 0; j < NU; ++j) {
-        const ulonglong2 v = R.ok[j] ? R.v[j] : ulonglong2{0ull, 0ull};
-        const uint64_t n = R.ok[j] ? R.nv[j] : 0ull;
+        // units outside the genome were loaded from a clamped index: their positions lie outside
+        // the chromosome, which the [vlo, vhi) mask below turns into 'N' whatever was loaded
+        const ulonglong2 v = R.v[j];
+        const uint64_t n = R.nv[j];
         xl[2 * j] = (uint32_t)v.x; xl[2 * j + 1] = (uint32_t)(v.x >> 32);
         xh[2 * j] = (uint32_t)v.y; xh[2 * j + 1] = (uint32_t)(v.y >> 32);
         xn[2 * j] = (uint32_t)n; xn[2 * j + 1] = (uint32_t)(n >> 32);
