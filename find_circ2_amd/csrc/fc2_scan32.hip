@@ -167,7 +167,6 @@ __device__ __forceinline__ void window_issue(const fc2_genome_view &g, const uin
 template <int NQ>
 __device__ __forceinline__ uint32_t window_geom(const fc2_genome_view &g, uint64_t cstart, int64_t ws, int W,
                                                 WinRaw<NQ> &R) {
-    constexpr int NU = WinRaw<NQ>::NU;
     const int64_t g0 = (int64_t)cstart + ws;
     const int64_t q0 = g0 >> 5;
     R.sh = (unsigned)(g0 & 31);
