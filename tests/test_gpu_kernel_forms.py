@@ -1,0 +1,101 @@
+"""GPU: every form of the scan kernel agrees bit for bit at the bench's full size.
+
+bp_scan32 has an LDS-staged form with cooperative window loads (read-order
+batches over a large genome) and a plain form (locus-ordered batches, small
+genomes); bp_scan is the 64-bit-word variant; the genome twin is optional.  They
+share no window-loading code path, so identical raw results on all 50M pairs of
+the BASELINE configs[2] workload (read order and locus order) are a
+size-independent parity property on top of the oracle comparisons of
+test_gpu_parity.py, which run at sizes the oracle finishes in seconds.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+from find_circ2_amd import Genome, Options, PairBatch, SynthConfig, scan, sq_table  # noqa: E402
+from find_circ2_amd import _native as N  # noqa: E402
+
+# (FC2_TUNE_KERNEL32, FC2_TUNE_STAGE, FC2_TUNE_TWIN)
+FORMS = {"scan32_staged_coop_twin": (1, 1, 1), "scan32_plain_no_twin": (1, 0, 0),
+         "scan32_plain_twin": (1, 0, 1), "scan64": (0, 0, 0)}
+
+
+def _set(form):
+    k32, st, tw = FORMS[form]
+    L = N.lib()
+    N.check(L.fc2_set_tuning(2, k32))
+    N.check(L.fc2_set_tuning(7, st))
+    N.check(L.fc2_set_tuning(6, tw))
+
+
+def _reset():
+    L = N.lib()
+    L.fc2_set_tuning(2, 1)
+    L.fc2_set_tuning(7, 2)
+    L.fc2_set_tuning(6, 2)
+
+
+@pytest.fixture(scope="module")
+def hg19():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    names, sizes = sq_table(os.path.join(GOLDEN, "test_norm.sam"))
+    return Genome.synthetic(names, sizes, seed=4711, device="cuda:0")
+
+
+@pytest.mark.parametrize("ordered", [False, True], ids=["read_order", "locus_order"])
+def test_forms_agree_full_size(hg19, ordered):
+    opt = Options()
+    n = 50_000_000
+    b = PairBatch.synthetic(opt, hg19, n, SynthConfig(seed=1337, span_max=20000, locus_ordered=ordered))
+    ref = None
+    try:
+        for form in FORMS:
+            _set(form)
+            out = scan(opt, hg19, b)
+            torch.cuda.synchronize()
+            res = out.results[:n].clone()
+            del out
+            if ref is None:
+                ref = res
+                info = (ref >> 48) & 0xFFFF
+                assert bool(((info & N.RES_DONE) != 0).all())
+                hit = ((ref & 0xFFFF) != 0xFFFF)
+                assert float(hit.float().mean()) > 0.4          # ~half of the pairs are planted junctions
+            else:
+                neq = int((res != ref).sum())
+                assert neq == 0, "%s differs from %s on %d of %d pairs" % (form, next(iter(FORMS)), neq, n)
+            del res
+    finally:
+        _reset()
+        del b, ref
+        torch.cuda.empty_cache()
+
+
+def test_forms_agree_all_hits_ties(hg19):
+    """--all-hits --non-canonical --strand-pref: results and tie masks of every form agree."""
+    opt = Options(allhits=True, noncanonical=True, strandpref=True)
+    n = 4_000_000
+    b = PairBatch.synthetic(opt, hg19, n, SynthConfig(seed=99, span_max=20000, p_backsplice=0.5))
+    ref = None
+    try:
+        for form in FORMS:
+            _set(form)
+            out = scan(opt, hg19, b)
+            torch.cuda.synchronize()
+            cur = (out.results[:n].clone(), out.tiemask.view(out.tw, out.stride)[:, :n].clone())
+            if ref is None:
+                ref = cur
+                assert int((ref[1] != 0).any(dim=0).sum()) > n // 10
+            else:
+                assert torch.equal(cur[0], ref[0]), form
+                assert torch.equal(cur[1], ref[1]), form
+    finally:
+        _reset()
+        torch.cuda.empty_cache()
