@@ -760,6 +760,7 @@ inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + bl
 int g_stream_nt = 1;
 int g_kernel32 = 1;   // 1: bp_scan32_kernel (32-bit plane words), 0: bp_scan_kernel (64-bit)
 int g_xcd_swizzle = 2; // XCD-contiguous block order in bp_scan32_kernel: 0 never, 1 always, 2 for locus-ordered batches
+int g_extra_lds = 0;   // bytes of unused dynamic LDS per scan block (occupancy experiments)
 int g_stage = 2;       // bp_scan32 LDS staging: 0 never, 1 always, 2 read-order batch over a large genome
 int g_twin = 2;        // units_twin: 0 never, 1 always, 2 for batches not flagged locus-ordered
 inline bool stream_nt() { return g_stream_nt != 0; }
@@ -803,7 +804,8 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         const bool big = !g->dummy && g->n_units * 16 >= (64ull << 20);
         const bool stage = g_stage == 2 ? (big && !ordered) : g_stage != 0;
         const int opts = sw ? fc2::kOptSwizzle : 0;
-        fc2::launch_scan32((ml + 2 + 31) / 32, nt, opts, stage, grid, s, *p, gv, *b, out, tiemask, tw);
+        fc2::launch_scan32((ml + 2 + 31) / 32, nt, opts, stage, grid, s, *p, gv, *b, out, tiemask, tw,
+                           (unsigned)g_extra_lds);
         return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
     }
 #define FC2_LAUNCH(NWV, NTV) \
@@ -906,6 +908,9 @@ extern "C" int fc2_set_tuning(int key, int value) {
             if (value < 1 || value > 32) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: reorder rounds 1..32");
             fc2::g_reorder_rounds = value; return FC2_OK;
         case FC2_TUNE_REORDER_NT: fc2::g_reorder_nt = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_EXTRA_LDS:
+            if (value < 0 || value > 65536) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: extra LDS 0..65536");
+            g_extra_lds = value; return FC2_OK;
         case FC2_TUNE_STAGE:
             if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: stage is 0, 1 or 2");
             g_stage = value; return FC2_OK;

@@ -11,5 +11,6 @@ namespace fc2 {
 // opts: kOptSwizzle.
 constexpr int kOptSwizzle = 1;     // XCD-contiguous block order
 void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
-                   const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw);
+                   const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
+                   unsigned extra_lds = 0);   // occupancy experiments only (FC2_TUNE_EXTRA_LDS)
 }  // namespace fc2

@@ -698,9 +698,10 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
 namespace fc2 {
 
 void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
-                   const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
+                   const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
+                   unsigned extra_lds) {
 #define FC2_L32(NQV, NTV, STV)                                                                                   \
-    hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV, STV>), dim3(grid), dim3(kBlock), 0, s, p, g, b, out, tiemask, \
+    hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV, STV>), dim3(grid), dim3(kBlock), extra_lds, s, p, g, b, out, tiemask, \
                        tw, opts)
 #define FC2_L32S(NQV, NTV) do { if (stage) FC2_L32(NQV, NTV, true); else FC2_L32(NQV, NTV, false); } while (0)
     if (nq <= 4) { if (nt) FC2_L32S(4, true); else FC2_L32S(4, false); }

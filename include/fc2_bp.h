@@ -182,6 +182,7 @@ int         fc2_device_count(int *count);
 #define FC2_TUNE_STAGE 7       /* scan kernel stages the chromosome table and nsuper in LDS: 0 never,
                                   1 always, 2 (default) for batches not locus-ordered over a genome of
                                   >= 64 MiB of code planes */
+#define FC2_TUNE_EXTRA_LDS 9   /* bytes of unused LDS added to each scan block (occupancy experiments; 0) */
 int         fc2_set_tuning(int key, int value);
 
 /* Largest l the register kernel handles (longer reads go to the byte kernel). */

@@ -43,6 +43,7 @@ def main():
         N.lib().fc2_set_tuning(3, 0 if "sw0" in v else (1 if "sw1" in v else 2))
         N.lib().fc2_set_tuning(6, 0 if "tw0" in v else (1 if "tw1" in v else 2))
         N.lib().fc2_set_tuning(7, 0 if "st0" in v else (1 if "st1" in v else 2))
+        N.lib().fc2_set_tuning(9, 8192 if "lds8k" in v else (65536 if "lds64k" in v else 0))
 
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream(dev)
