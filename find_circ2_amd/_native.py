@@ -107,7 +107,10 @@ EXPORTED = [
     "fc2_reorder_plan", "fc2_reorder_launch",
     # include/fc2_ingest.h
     "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
-    "fc2_ingest_next",
+    "fc2_ingest_next", "fc2_ingest_counts_get",
+    # include/fc2_caller.h
+    "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
+    "fc2_caller_submit", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
 ]
 
 
@@ -121,14 +124,31 @@ class IngestCounts(ctypes.Structure):
                 ("unspliced_mates", ctypes.c_uint64), ("seg_too_short_skip", ctypes.c_uint64),
                 ("records", ctypes.c_uint64), ("handed_back", ctypes.c_uint64)]
 
+class CallerOpts(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("known_circ", ctypes.c_char_p), ("known_lin", ctypes.c_char_p),
+                ("min_uniq_qual", ctypes.c_int32), ("asize", ctypes.c_int32), ("margin", ctypes.c_int32),
+                ("maxdist", ctypes.c_int32), ("short_threshold", ctypes.c_int32), ("huge_threshold", ctypes.c_int32),
+                ("noncanonical", ctypes.c_uint8), ("allhits", ctypes.c_uint8), ("stranded", ctypes.c_uint8),
+                ("strandpref", ctypes.c_uint8), ("halfunique", ctypes.c_uint8), ("report_nobridges", ctypes.c_uint8),
+                ("test", ctypes.c_uint8), ("nolinear", ctypes.c_uint8), ("multi_events", ctypes.c_uint8),
+                ("noop", ctypes.c_uint8), ("write_reads", ctypes.c_uint8), ("write_multi", ctypes.c_uint8),
+                ("_pad", ctypes.c_uint32), ("chunksize", ctypes.c_uint64)]
+
+
+class CallerBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("reads", ctypes.c_void_p), ("read_off", ctypes.c_void_p),
+                ("pairs", ctypes.c_void_p)]
+
+
 _lib = None
 
 
 def build(force: bool = False) -> str:
     srcdir = os.path.join(_HERE, "csrc")
-    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_reorder.hip", "fc2_scan32.h", "fc2_host.cpp",
-                                              "fc2_ingest.cpp", "fc2_common.h", "Makefile")]
-    srcs += [os.path.join(os.path.dirname(_HERE), "include", h) for h in ("fc2_bp.h", "fc2_ingest.h")]
+    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_reorder.hip", "fc2_scan32.h",
+                                              "fc2_host.cpp", "fc2_ingest.cpp", "fc2_ingest_impl.h", "fc2_caller.cpp",
+                                              "fc2_common.h", "Makefile")]
+    srcs += [os.path.join(os.path.dirname(_HERE), "include", h) for h in ("fc2_bp.h", "fc2_ingest.h", "fc2_caller.h")]
     newest = max(os.path.getmtime(s) for s in srcs)
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
         subprocess.check_call(["make", "-s", "-C", srcdir])
@@ -183,6 +203,17 @@ def lib() -> ctypes.CDLL:
         "fc2_ingest_header": (ctypes.c_char_p, [vp]),
         "fc2_ingest_next": (ctypes.c_int, [vp, P(IngestParams), u64, P(IngestCounts), P(ctypes.c_void_p), P(u64),
                                            P(u64), P(ctypes.c_int)]),
+        "fc2_ingest_counts_get": (ctypes.c_int, [vp, P(IngestCounts)]),
+        "fc2_caller_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(CallerOpts), P(vp)]),
+        "fc2_caller_set_genome": (ctypes.c_int, [vp, vp, i32, vp, P(u64), P(u64)]),
+        "fc2_caller_ingest": (vp, [vp]),
+        "fc2_caller_close": (None, [vp]),
+        "fc2_caller_next": (ctypes.c_int, [vp, P(CallerBatch), P(ctypes.c_int)]),
+        "fc2_caller_submit": (ctypes.c_int, [vp, vp, vp, u32, u64]),
+        "fc2_caller_take": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
+        "fc2_caller_rows": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
+        "fc2_caller_counter": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(ctypes.c_double)]),
+        "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(L, name)

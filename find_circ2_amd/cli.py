@@ -69,7 +69,9 @@ def build_parser() -> optparse.OptionParser:
     a("", "--no-multi", dest="multi_events", default=True, action="store_false", help="do not record multi-events")
     a("", "--device", dest="device", default="cuda:0", help="HIP device (find_circ2_amd extension)")
     a("", "--python-ingest", dest="python_ingest", default=False, action="store_true",
-      help="parse and group alignments in Python instead of the native ingest (find_circ2_amd extension)")
+      help="parse and group alignments in Python instead of the native ingest (implies --python-caller)")
+    a("", "--python-caller", dest="python_caller", default=False, action="store_true",
+      help="run record_hits and the junction tables in Python (find_circ2_amd.caller) instead of the native caller")
     return p
 
 
@@ -132,6 +134,7 @@ def main(argv=None, evaluator_factory=None) -> int:
 
     hp = HPOptions(asize=options.asize, margin=options.margin, maxdist=options.maxdist,
                    noncanonical=options.noncanonical, strandpref=options.strandpref, allhits=options.allhits)
+    genome = None
     if evaluator_factory is None:
         from .genome import Genome
         try:
@@ -143,12 +146,14 @@ def main(argv=None, evaluator_factory=None) -> int:
                 "Could not access '%s'. Switching to dummy mode (only Ns)" % options.genome)
             genome = Genome.dummy_genome(device=options.device)
         evaluate = gpu_evaluator(genome, hp)
-    else:
+    elif options.python_ingest or options.python_caller:
         evaluate = evaluator_factory(options, hp)
 
     path = args[0] if args else "-"
     is_bam = bool(args) and not args[0].endswith("sam")          # find_circ.py:461-469
     logger.info('reading from {0}'.format(args[0]) if args else 'reading from stdin')
+    if not (options.python_ingest or options.python_caller):
+        return _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome)
     if options.python_ingest:
         sam = AlignmentFile(path, "rb" if is_bam else "r")
         run = lambda: caller.run(sam)                              # noqa: E731
@@ -189,8 +194,18 @@ def main(argv=None, evaluator_factory=None) -> int:
         logging.error(exc)
         sys.stderr.write(exc)
         return 1
-    M = caller.n_reads / 1e6
-    krps = caller.n_reads / seconds / 1000. if seconds > 0 else 0.0
+    _finish(options, seconds, caller.n_reads, logger, caller.N, caller.n_spans_evaluated, caller.gpu_seconds)
+    caller.circ_splices.store(out["circs"])
+    caller.linear_splices.store(out["lins"])
+    for k, fh in out.items():
+        if fh is not None and fh is not sys.stdout:
+            fh.close()
+    return 0
+
+
+def _finish(options, seconds, n_reads, logger, counters, n_spans, eval_seconds):
+    M = n_reads / 1e6
+    krps = n_reads / seconds / 1000. if seconds > 0 else 0.0
     txt = "processed {0:.2f}M (paired or single end) reads in {1:.1f} minutes (overall {2:.2f}k reads/second on " \
           "average)".format(M, seconds / 60., krps)
     logger.info(txt)
@@ -198,15 +213,60 @@ def main(argv=None, evaluator_factory=None) -> int:
         print("#", txt)
         print("# results stored in '{0}'".format(options.output))
     logger.info('run finished')
-    for key in sorted(caller.N):
-        logger.info('{0}={1}'.format(key, caller.N[key]))
-    logger.info('breakpoint search: {0} spans, {1:.3f} s incl. pack/transfer/decode'.format(
-        caller.n_spans_evaluated, caller.gpu_seconds))
-    caller.circ_splices.store(out["circs"])
-    caller.linear_splices.store(out["lins"])
-    for k, fh in out.items():
-        if fh is not None and fh is not sys.stdout:
-            fh.close()
+    for key in sorted(counters):
+        logger.info('{0}={1}'.format(key, counters[key]))
+    logger.info('breakpoint search: {0} spans, {1:.3f} s incl. pack/transfer/decode'.format(n_spans, eval_seconds))
+
+
+def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome) -> int:
+    """The read loop in C++ (include/fc2_caller.h); only the breakpoint search is called from here."""
+    from .caller import BED_HEADER, MULTI_HEADER
+    from .native_caller import NativeCaller, gpu_batch_evaluator
+    if evaluator_factory is None:
+        evaluate, names, fasta, dummy = gpu_batch_evaluator(genome, hp), genome.names, genome.fasta, genome.dummy
+    else:
+        engine = getattr(evaluator_factory, "batch", None)
+        if engine is None:
+            raise ValueError("evaluator_factory has no batch form for the native caller (use --python-caller)")
+        evaluate, names, fasta, dummy = engine(options, hp)
+    nc = NativeCaller(path, is_bam, options, names, fasta, write_reads=out.get("reads") is not None,
+                      write_multi=out.get("multi") is not None, genome_dummy=dummy,
+                      known_circ=options.known_circ, known_lin=options.known_lin)
+    try:
+        n_kc, n_kl = nc.open()
+        for n, p in ((n_kc, options.known_circ), (n_kl, options.known_lin)):
+            if p:
+                logger.info("loaded {0} known splice sites from '{1}'".format(n, p))
+        if out.get("multi") is not None:
+            out["multi"].write(MULTI_HEADER)
+        try:
+            if options.profile:
+                import cProfile
+                prof = cProfile.Profile()
+                seconds, n_reads, n_pairs, eval_s = prof.runcall(nc.run, evaluate, out, sys.stderr,
+                                                                 options.throughput, options.chunksize)
+                prof.print_stats()
+            else:
+                seconds, n_reads, n_pairs, eval_s = nc.run(evaluate, out, sys.stderr, options.throughput,
+                                                           options.chunksize)
+        except KeyboardInterrupt:
+            logging.warning("KeyboardInterrupt by user while processing input")
+            (n_reads, n_pairs), seconds, eval_s = nc.stats(), 0.0, 0.0
+        except Exception:
+            logging.error("Unhandled exception raised while processing input")
+            exc = traceback.format_exc()
+            logging.error(exc)
+            sys.stderr.write(exc)
+            return 1
+        _finish(options, seconds, n_reads, logger, nc.counters(), n_pairs, eval_s)
+        for kind, key in ((0, "circs"), (1, "lins")):
+            out[key].write(BED_HEADER)
+            out[key].write(nc.rows(kind))
+    finally:
+        nc.close()
+        for k, fh in out.items():
+            if fh is not None and fh is not sys.stdout:
+                fh.close()
     return 0
 
 

@@ -22,29 +22,12 @@
 
 #include "../../include/fc2_ingest.h"
 #include "fc2_common.h"
+#include "fc2_ingest_impl.h"
+
+using fc2::ing::Mate;
+using fc2::ing::Rec;
 
 namespace {
-
-struct Rec {
-    std::string text;      // SAM line (no newline)
-    std::string qname;
-    uint32_t flag = 0;
-    int32_t tid = -1;
-    int64_t pos = -1;
-    int64_t aend = -1;     // -1: None (unmapped / no cigar)
-    int32_t astart = 0;    // aligned_start_from_cigar (:1086-1097)
-    int32_t qlen = -1;     // len(query); -1: query is None (SEQ '*')
-    bool has_seq = false;
-    bool unmapped() const { return flag & 0x4; }
-    bool read1() const { return flag & 0x40; }
-    bool reverse() const { return flag & 0x10; }
-};
-
-struct Mate {
-    std::vector<Rec> recs;       // primary first, then every added segment (for hand-back)
-    std::vector<int> proper;     // indices into recs
-    bool valid = false;
-};
 
 // CIGAR helpers ------------------------------------------------------------
 struct CigarInfo {
@@ -115,6 +98,7 @@ struct fc2_ingest {
     std::string out;
     fc2_ingest_counts counts{};
     bool finished = false;
+    bool need_text = true;       // false once a native caller pulls structured fragments
 };
 
 namespace {
@@ -194,6 +178,27 @@ bool next_line(fc2_ingest *h, std::string &line) {
     }
 }
 
+// AS / XS of one tag in SAM text form "TG:T:value" (first occurrence wins, like get_tag)
+void note_tag(Rec &r, const char *t, const char *e) {
+    if (e - t < 5 || t[2] != ':' || t[4] != ':') return;
+    const bool as = t[0] == 'A' && t[1] == 'S', xs = t[0] == 'X' && t[1] == 'S';
+    if (!as && !xs) return;
+    if ((as && r.has_as) || (xs && r.has_xs)) return;
+    const bool isint = t[3] == 'i';
+    const int64_t v = isint ? strtoll(std::string(t + 5, e).c_str(), nullptr, 10) : 0;
+    if (as) { r.has_as = true; r.as_int = isint; r.as = v; }
+    else { r.has_xs = true; r.xs_int = isint; r.xs = v; }
+}
+
+void scan_sam_tags(Rec &r, const char *p, const char *end) {
+    while (p < end) {
+        const char *t = (const char *)memchr(p, '\t', (size_t)(end - p));
+        const char *e = t ? t : end;
+        note_tag(r, p, e);
+        p = e + 1;
+    }
+}
+
 int parse_sam_record(fc2_ingest *h, const std::string &line, Rec &r) {
     // fields 1-11
     size_t f[12];
@@ -211,7 +216,7 @@ int parse_sam_record(fc2_ingest *h, const std::string &line, Rec &r) {
         }
         return std::string(line, b, e - b);
     };
-    r.text = line;
+    if (h->need_text) r.text = line;
     r.qname = field(0);
     r.flag = (uint32_t)strtoul(field(1).c_str(), nullptr, 10);
     std::string rn = field(2);
@@ -235,9 +240,12 @@ int parse_sam_record(fc2_ingest *h, const std::string &line, Rec &r) {
             }
         }
     }
-    std::string seq = field(9);
-    r.has_seq = seq != "*";
-    finish_rec(r, ops, r.has_seq ? (int64_t)seq.size() : 0);
+    r.seq = field(9);
+    r.has_seq = r.seq != "*";
+    r.qual = field(10);
+    r.has_qual = r.qual != "*";
+    finish_rec(r, ops, r.has_seq ? (int64_t)r.seq.size() : 0);
+    if (nf == 12) scan_sam_tags(r, line.c_str() + f[11], line.c_str() + line.size());
     return FC2_OK;
 }
 
@@ -291,6 +299,46 @@ void append_bam_tags(std::string &t, const uint8_t *p, const uint8_t *end) {
     }
 }
 
+// AS / XS from binary BAM tags (integer types as ints, anything else marked non-int)
+void scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
+    while (p + 3 <= end) {
+        const char t0 = (char)p[0], t1 = (char)p[1], ty = (char)p[2];
+        p += 3;
+        int64_t v = 0;
+        bool isint = true;
+        size_t adv = 0;
+        switch (ty) {
+            case 'c': v = *(const int8_t *)p; adv = 1; break;
+            case 'C': v = *(const uint8_t *)p; adv = 1; break;
+            case 's': { int16_t x; memcpy(&x, p, 2); v = x; adv = 2; break; }
+            case 'S': { uint16_t x; memcpy(&x, p, 2); v = x; adv = 2; break; }
+            case 'i': { int32_t x; memcpy(&x, p, 4); v = x; adv = 4; break; }
+            case 'I': { uint32_t x; memcpy(&x, p, 4); v = x; adv = 4; break; }
+            case 'f': isint = false; adv = 4; break;
+            case 'A': isint = false; adv = 1; break;
+            case 'Z': case 'H': {
+                const uint8_t *z = (const uint8_t *)memchr(p, 0, (size_t)(end - p));
+                isint = false;
+                adv = (size_t)((z ? z : end) - p) + 1;
+                break;
+            }
+            case 'B': {
+                const char sub = (char)p[0];
+                int32_t cnt; memcpy(&cnt, p + 1, 4);
+                const size_t w = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
+                isint = false;
+                adv = 5 + w * (size_t)(cnt < 0 ? 0 : cnt);
+                break;
+            }
+            default: return;
+        }
+        const bool as = t0 == 'A' && t1 == 'S', xs = t0 == 'X' && t1 == 'S';
+        if (as && !r.has_as) { r.has_as = true; r.as_int = isint; r.as = v; }
+        if (xs && !r.has_xs) { r.has_xs = true; r.xs_int = isint; r.xs = v; }
+        p += adv;
+    }
+}
+
 int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     got = false;
     if (!ensure(h, 4)) return FC2_OK;
@@ -332,7 +380,18 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     r.pos = pos;
     r.has_seq = l_seq > 0;
     finish_rec(r, ops, l_seq);
-    // SAM text (only needed for hand-back, but cheap relative to inflate)
+    scan_bam_tags(r, p, e);
+    r.has_qual = qual != "*";
+    if (!h->need_text) {
+        r.seq = std::move(seq);
+        r.qual = std::move(qual);
+        h->beg += 4 + (size_t)bs;
+        got = true;
+        return FC2_OK;
+    }
+    r.seq = seq;
+    r.qual = qual;
+    // SAM text (hand-back to the Python caller)
     std::string &t = r.text;
     t = r.qname;
     snprintf(tmp, sizeof tmp, "\t%u\t", flag); t += tmp;
@@ -454,9 +513,10 @@ MateEval eval_mate(const Mate &m, int asize) {
     return ev;
 }
 
-void emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed) {
+int emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed,
+                  const fc2::ing::FragSink *sink) {
     h->counts.n_reads++;
-    if (p->noop) return;
+    if (p->noop) return FC2_OK;
     const Mate *mates[2] = {h->have_other ? &h->other : nullptr, &h->current};
     MateEval ev[2];
     int circ = 0, lin = 0;
@@ -475,15 +535,17 @@ void emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed
             if (ev[k].unspliced) h->counts.unspliced_mates++;
             h->counts.seg_too_short_skip += (uint64_t)ev[k].too_short;
         }
-        return;
+        return FC2_OK;
     }
+    ++n_handed;
+    h->counts.handed_back++;
+    if (sink) return (*sink)(mates[0], mates[1], must);
     for (int k = 0; k < 2; ++k) {
         if (!mates[k]) continue;
         for (const Rec &r : mates[k]->recs) { h->out += r.text; h->out += '\n'; }
     }
     h->out += '\n';
-    ++n_handed;
-    h->counts.handed_back++;
+    return FC2_OK;
 }
 
 }  // namespace
@@ -520,11 +582,9 @@ extern "C" const char *fc2_ingest_ref_name(const fc2_ingest *h, int tid) {
 }
 extern "C" const char *fc2_ingest_header(const fc2_ingest *h) { return h ? h->header.c_str() : ""; }
 
-extern "C" int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags,
-                               fc2_ingest_counts *counts, const char **text, uint64_t *text_len, uint64_t *n_handed,
-                               int *eof) {
-    if (!h || !p) return fc2::fail(FC2_E_PARAM, "fc2_ingest_next: null argument");
-    h->out.clear();
+namespace {
+int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const fc2::ing::FragSink *sink,
+             uint64_t *n_handed, int *eof) {
     uint64_t handed = 0, frags = 0;
     int rc = FC2_OK;
     bool done = h->finished;
@@ -537,10 +597,11 @@ extern "C" int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64
                 if (h->n_records == 1)
                     return fc2::fail(FC2_E_FORMAT, "UnboundLocalError: local variable 'line_num' referenced before "
                                                    "assignment (single-record input, find_circ.py:1486)");
-                emit_or_count(h, p, handed);
+                rc = emit_or_count(h, p, handed, sink);
                 ++frags;
             }
             h->finished = done = true;
+            if (rc) return rc;
             break;
         }
         h->n_records++;
@@ -559,17 +620,41 @@ extern "C" int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64
             h->have_other = true;
             open_mate(h, h->current, std::move(r));
         } else {
-            emit_or_count(h, p, handed);
+            rc = emit_or_count(h, p, handed, sink);
             ++frags;
             h->have_other = false;
             h->other = Mate();
             open_mate(h, h->current, std::move(r));
+            if (rc) return rc;
         }
     }
+    if (n_handed) *n_handed = handed;
+    if (eof) *eof = done ? 1 : 0;
+    return FC2_OK;
+}
+}  // namespace
+
+int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof) {
+    if (!h || !p) return fc2::fail(FC2_E_PARAM, "ingest pull: null argument");
+    h->need_text = false;
+    return run_loop(h, p, max_frags, &sink, nullptr, eof);
+}
+
+extern "C" int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags,
+                               fc2_ingest_counts *counts, const char **text, uint64_t *text_len, uint64_t *n_handed,
+                               int *eof) {
+    if (!h || !p) return fc2::fail(FC2_E_PARAM, "fc2_ingest_next: null argument");
+    h->out.clear();
+    const int rc = run_loop(h, p, max_frags, nullptr, n_handed, eof);
+    if (rc) return rc;
     if (counts) *counts = h->counts;
     if (text) *text = h->out.c_str();
     if (text_len) *text_len = h->out.size();
-    if (n_handed) *n_handed = handed;
-    if (eof) *eof = done ? 1 : 0;
+    return FC2_OK;
+}
+
+extern "C" int fc2_ingest_counts_get(const fc2_ingest *h, fc2_ingest_counts *counts) {
+    if (!h || !counts) return fc2::fail(FC2_E_PARAM, "fc2_ingest_counts_get: null argument");
+    *counts = h->counts;
     return FC2_OK;
 }

@@ -1,0 +1,51 @@
+// Internal interface of the native ingest (fc2_ingest.cpp) for the native caller
+// (fc2_caller.cpp): parsed records, mates, and a pull loop that hands fragments
+// carrying anchor pairs to a sink instead of formatting them as SAM text.
+#pragma once
+#include <stdint.h>
+
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../include/fc2_ingest.h"
+
+namespace fc2 {
+namespace ing {
+
+struct Rec {
+    std::string text;      // SAM line (no newline)
+    std::string qname;
+    uint32_t flag = 0;
+    int32_t tid = -1;
+    int64_t pos = -1;
+    int64_t aend = -1;     // -1: None (unmapped / no cigar)
+    int32_t astart = 0;    // aligned_start_from_cigar (:1086-1097)
+    int32_t qlen = -1;     // len(query); -1: query is None (SEQ '*')
+    bool has_seq = false;
+    std::string seq, qual;  // SEQ / QUAL ("*" -> has_seq false / has_qual false)
+    bool has_qual = false;
+    // AS / XS tags as pysam's get_tag returns them: present?, integer-typed?, value
+    bool has_as = false, has_xs = false, as_int = true, xs_int = true;
+    int64_t as = 0, xs = 0;
+    bool unmapped() const { return flag & 0x4; }
+    bool read1() const { return flag & 0x40; }
+    bool reverse() const { return flag & 0x10; }
+};
+
+struct Mate {
+    std::vector<Rec> recs;       // primary first, then every added segment (for hand-back)
+    std::vector<int> proper;     // indices into recs
+    bool valid = false;
+};
+
+// Fragments that carry anchor pairs (or that the reference would fail on: must_see) are passed
+// to the sink in input order; m1 = the other mate (may be null), m2 = the current mate.
+using FragSink = std::function<int(const Mate *m1, const Mate *m2, bool must_see)>;
+
+// The loop of fc2_ingest_next with a sink instead of SAM text; a non-zero return of the sink
+// stops the loop and is returned.
+int pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof);
+
+}  // namespace ing
+}  // namespace fc2

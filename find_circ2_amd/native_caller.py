@@ -1,0 +1,212 @@
+"""Driver of the native read loop (include/fc2_caller.h, fc2_caller.cpp).
+
+The C++ side reads the alignments, forms the anchor pairs, and runs
+``record_hits`` / the junction tables / the writers of find_circ.py 1.99 (the
+same logic as :mod:`find_circ2_amd.caller`, which stays as the reference path
+behind ``--python-caller``).  This module moves the pairs of each chunk to the
+breakpoint search and the results back, writes the text the C++ side produced,
+and turns its errors into the exceptions the reference raises.
+
+``evaluate(reads, read_off, pairs) -> (results, tiemask)``: ``pairs`` is a
+``PAIR_DTYPE`` array (chrom = genome index), ``results`` the raw ``fc2_result``
+words (int64 [n]) in the same order, ``tiemask`` uint64 [tw, n] with
+``--all-hits`` (else None).  :func:`gpu_batch_evaluator` is the MI355X one.
+"""
+from __future__ import annotations
+
+import ctypes
+import sys
+import time
+from typing import Callable, Dict, Optional
+
+import numpy as np
+
+from . import _native as N
+from .hotpath import BreakpointError
+
+_EXC = {"KeyError": KeyError, "TypeError": TypeError, "ValueError": ValueError, "AttributeError": AttributeError,
+        "IndexError": IndexError, "IOError": OSError, "BreakpointError": BreakpointError,
+        "UnboundLocalError": UnboundLocalError}
+
+
+def _raise_native(rc: int):
+    msg = N.lib().fc2_last_error()
+    msg = msg.decode("utf-8", "replace") if msg else ""
+    kind, _, rest = msg.partition(": ")
+    exc = _EXC.get(kind)
+    if exc is None:
+        raise N.Fc2Error(rc, msg)
+    if exc is KeyError and rest.startswith("'") and rest.endswith("'"):
+        raise KeyError(rest[1:-1])
+    raise exc(rest)
+
+
+def _check(rc: int):
+    if rc != N.FC2_OK:
+        _raise_native(rc)
+
+
+def gpu_batch_evaluator(genome, hp) -> Callable:
+    """One fc2_bp_scan_launch per chunk, the batch packed in locus order; results in input order."""
+    from .hotpath import PairBatch, scan
+
+    def evaluate(reads, read_off, pairs):
+        n = len(pairs)
+        lens = pairs["read_len"].astype(np.int64)
+        b = PairBatch.pack(hp, genome, (reads, read_off, lens), pairs["a_pos"], pairs["b_aend"], pairs["chrom"],
+                           pairs["flags"], locus_order=True)
+        out = scan(hp, genome, b)
+        res = out.results[:n].cpu().numpy()
+        perm = b.fetch_perm()
+        if perm is not None:
+            r = np.empty_like(res)
+            r[perm] = res
+            res = r
+        tm = None
+        if hp.allhits:
+            t = out.tiemask[:b.tw * b.stride].cpu().numpy().view(np.uint64).reshape(b.tw, b.stride)[:, :n]
+            if perm is not None:
+                t2 = np.empty_like(t)
+                t2[:, perm] = t
+                t = t2
+            tm = np.ascontiguousarray(t)
+        return np.ascontiguousarray(res), tm
+    return evaluate
+
+
+class NativeCaller:
+    """One pass over an alignment file (path or '-') with the native read loop."""
+
+    def __init__(self, path: str, is_bam: bool, copts, genome_names, fasta_handle=None, write_reads=True,
+                 write_multi=True, genome_dummy=False, known_circ: str = "", known_lin: str = ""):
+        o = copts
+        # the strings must outlive the handle's open call (fc2_caller_open copies them)
+        self._keep = [o.name.encode(), known_circ.encode() if known_circ else None,
+                      known_lin.encode() if known_lin else None]
+        self.opts = N.CallerOpts(
+            self._keep[0], self._keep[1], self._keep[2], int(o.min_uniq_qual), int(o.asize), int(o.margin),
+            int(o.maxdist), int(o.short_threshold), int(o.huge_threshold), int(bool(o.noncanonical)),
+            int(bool(o.allhits)), int(bool(o.stranded)), int(bool(o.strandpref)), int(bool(o.halfunique)),
+            int(bool(o.report_nobridges)), int(bool(o.test)), int(bool(o.nolinear)), int(bool(o.multi_events)),
+            int(bool(o.noop)), int(bool(write_reads)), int(bool(write_multi)), 0, int(o.chunksize))
+        self.h = ctypes.c_void_p()
+        self.genome_names = list(genome_names or [])
+        self.genome_dummy = genome_dummy
+        self.fasta_handle = fasta_handle
+        self._path = path
+        self._is_bam = is_bam
+        self.opened = False
+
+    def open(self):
+        """Open the input, map its reference ids to genome indices, load the known sites.
+
+        Returns (#known circ sites, #known linear sites)."""
+        L = N.lib()
+        N.check(L.fc2_caller_open(self._path.encode(), 1 if self._is_bam else 0, ctypes.byref(self.opts),
+                                  ctypes.byref(self.h)))
+        self.opened = True
+        ing = L.fc2_caller_ingest(self.h)
+        n_ref = L.fc2_ingest_n_refs(ing)
+        self.refs = [L.fc2_ingest_ref_name(ing, t).decode("latin-1") for t in range(n_ref)]
+        index = {nm: k for k, nm in enumerate(self.genome_names)}
+        if self.genome_dummy:             # every window is all 'N'; no chromosome is missing
+            t2c = np.zeros(max(1, n_ref), np.int32)
+        else:
+            t2c = np.array([index.get(nm, -1) for nm in self.refs] or [-1], np.int32)
+        self._t2c = t2c
+        nkc, nkl = ctypes.c_uint64(), ctypes.c_uint64()
+        _check(L.fc2_caller_set_genome(self.h, t2c.ctypes.data, n_ref, self.fasta_handle, ctypes.byref(nkc),
+                                       ctypes.byref(nkl)))
+        return int(nkc.value), int(nkl.value)
+
+    def stats(self):
+        nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(N.lib().fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs)))
+        return int(nr.value), int(npairs.value)
+
+    def close(self):
+        if self.opened:
+            N.lib().fc2_caller_close(self.h)
+            self.opened = False
+
+    def _take(self, stream: int) -> str:
+        t, n = ctypes.c_void_p(), ctypes.c_uint64()
+        N.check(N.lib().fc2_caller_take(self.h, stream, ctypes.byref(t), ctypes.byref(n)))
+        return ctypes.string_at(t.value, n.value).decode("latin-1") if n.value else ""
+
+    def _write_outputs(self, outputs: Dict):
+        for k, key in ((0, "reads"), (1, "multi"), (2, "test")):
+            txt = self._take(k)
+            if txt and outputs.get(key) is not None:
+                outputs[key].write(txt)
+
+    def run(self, evaluate: Callable, outputs: Dict, stderr=sys.stderr, throughput=False, chunksize=100000):
+        """Process the whole input; returns (seconds, n_reads, n_pairs, evaluate_seconds)."""
+        L = N.lib()
+        t0 = time.time()
+        t_last, last_reads = t0, 0
+        eval_s = 0.
+        batch = N.CallerBatch()
+        eof = ctypes.c_int(0)
+        while True:
+            rc = L.fc2_caller_next(self.h, ctypes.byref(batch), ctypes.byref(eof))
+            if rc != N.FC2_OK:
+                _raise_native(rc)
+            n = int(batch.n)
+            res_ptr = tm_ptr = None
+            tw = 0
+            if n:
+                pairs = np.ctypeslib.as_array(ctypes.cast(batch.pairs, ctypes.POINTER(ctypes.c_uint8)),
+                                              (16 * n,)).view(N.PAIR_DTYPE).copy()
+                off = np.ctypeslib.as_array(ctypes.cast(batch.read_off, ctypes.POINTER(ctypes.c_uint64)),
+                                            (n,)).copy()
+                total = int((off + pairs["read_len"].astype(np.uint64)).max())
+                reads = np.zeros(total + 16, np.uint8)          # zero tail: the packer reads whole words
+                if total:
+                    reads[:total] = np.ctypeslib.as_array(
+                        ctypes.cast(batch.reads, ctypes.POINTER(ctypes.c_uint8)), (total,))
+                te = time.perf_counter()
+                res, tm = evaluate(reads, off, pairs)
+                eval_s += time.perf_counter() - te
+                res = np.ascontiguousarray(res, dtype=np.int64)
+                res_ptr = res.ctypes.data
+                if tm is not None:
+                    tm = np.ascontiguousarray(tm, dtype=np.uint64)
+                    tw = tm.shape[0]
+                    tm_ptr = tm.ctypes.data
+            rc = L.fc2_caller_submit(self.h, res_ptr, tm_ptr, tw, n)
+            self._write_outputs(outputs)        # what record_hits wrote before any failure
+            if rc != N.FC2_OK:
+                _raise_native(rc)
+            if throughput:
+                nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
+                L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
+                if nr.value // chunksize > last_reads // chunksize:
+                    t1 = time.time()
+                    stderr.write("\rprocessed {0:.1f}M (paired-end) reads in {1:.1f} minutes ({2:.2f}k "
+                                 "reads/second)       \r".format(nr.value / 1e6, (t1 - t0) / 60.,
+                                                               (nr.value - last_reads) / max(t1 - t_last, 1e-9)
+                                                               / 1000.))
+                    t_last, last_reads = t1, nr.value
+            if eof.value:
+                break
+        if throughput:
+            stderr.write('\n')
+        nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
+        L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
+        return time.time() - t0, int(nr.value), int(npairs.value), eval_s
+
+    def counters(self) -> Dict[str, float]:
+        L = N.lib()
+        out = {}
+        k = 0
+        nm, v = ctypes.c_char_p(), ctypes.c_double()
+        while L.fc2_caller_counter(self.h, k, ctypes.byref(nm), ctypes.byref(v)) == N.FC2_OK:
+            out[nm.value.decode()] = float(v.value)
+            k += 1
+        return out
+
+    def rows(self, kind: int) -> str:
+        t, n = ctypes.c_void_p(), ctypes.c_uint64()
+        N.check(N.lib().fc2_caller_rows(self.h, kind, ctypes.byref(t), ctypes.byref(n)))
+        return ctypes.string_at(t.value, n.value).decode("latin-1") if n.value else ""

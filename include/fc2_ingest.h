@@ -57,6 +57,8 @@ const char *fc2_ingest_header(const fc2_ingest *h);
 int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, fc2_ingest_counts *counts,
                     const char **text, uint64_t *text_len, uint64_t *n_handed, int *eof);
 
+/* Counters so far (also returned by fc2_ingest_next). */
+int fc2_ingest_counts_get(const fc2_ingest *h, fc2_ingest_counts *counts);
 #ifdef __cplusplus
 }
 #endif

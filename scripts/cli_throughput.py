@@ -7,6 +7,11 @@ known segment coordinates), then runs ``python -m find_circ2_amd.cli`` on it and
 reports reads/s plus the time spent in the batched breakpoint search.
 
 usage: python scripts/cli_throughput.py [--reads N] [--genome-mb M] [--frac-spliced F] [--out DIR]
+                                       [--mode native|python-caller|python-ingest ...] [--null-eval]
+
+``--mode`` picks the read loop (C++ caller by default; several modes run one after
+the other on the same input).  ``--null-eval`` replaces the breakpoint search by
+"no hit" results, which times the host loop alone (runs without a GPU).
 """
 import argparse
 import json
@@ -80,6 +85,8 @@ def main():
     ap.add_argument("--genome-mb", type=int, default=20)
     ap.add_argument("--frac-spliced", type=float, default=0.3)
     ap.add_argument("--out", default="/tmp/fc2_cli_tp")
+    ap.add_argument("--mode", action="append", choices=["native", "python-caller", "python-ingest"])
+    ap.add_argument("--null-eval", action="store_true")
     a = ap.parse_args()
     os.makedirs(a.out, exist_ok=True)
     rng = np.random.default_rng(27)
@@ -90,15 +97,45 @@ def main():
     write_sam(sam, seqs, a.reads, a.frac_spliced, 100, rng)
     t_gen = time.time() - t0
     from find_circ2_amd import cli
-    t0 = time.time()
-    rc = cli.main(["-G", fa, "-o", os.path.join(a.out, "run"), "-n", "tp", "-q", sam])
-    wall = time.time() - t0
-    log = open(os.path.join(a.out, "run", "run.log")).read()
-    bp = [l for l in log.splitlines() if "breakpoint search:" in l]
-    circ = sum(1 for l in open(os.path.join(a.out, "run", "circ_splice_sites.bed")) if not l.startswith("#"))
-    print(json.dumps({"rc": rc, "reads": a.reads, "frac_spliced": a.frac_spliced, "wall_s": round(wall, 2),
-                      "reads_per_s": round(a.reads / wall, 1), "gen_s": round(t_gen, 1),
-                      "breakpoint_search": bp[-1].split("\t")[-1] if bp else None, "circ_rows": circ}))
+    factory = null_factory if a.null_eval else None
+    for mode in a.mode or ["native"]:
+        flag = [] if mode == "native" else ["--" + mode]
+        run = os.path.join(a.out, "run_" + mode)
+        t0 = time.time()
+        rc = cli.main(["-G", fa, "-o", run, "-n", "tp", "-q"] + flag + [sam], evaluator_factory=factory)
+        wall = time.time() - t0
+        log = open(os.path.join(run, "run.log")).read()
+        bp = [l for l in log.splitlines() if "breakpoint search:" in l]
+        circ = sum(1 for l in open(os.path.join(run, "circ_splice_sites.bed")) if not l.startswith("#"))
+        print(json.dumps({"mode": mode, "null_eval": a.null_eval, "rc": rc, "reads": a.reads,
+                          "frac_spliced": a.frac_spliced, "wall_s": round(wall, 2),
+                          "reads_per_s": round(a.reads / wall, 1), "gen_s": round(t_gen, 1),
+                          "breakpoint_search": bp[-1].split("\t")[-1] if bp else None, "circ_rows": circ}), flush=True)
+
+
+def null_factory(options, hp):
+    """Breakpoint search stub: every span "no hit" (host-loop timing only)."""
+    def evaluate(spans):
+        for s in spans:
+            s.result = []
+    return evaluate
+
+
+def _null_batch(options, hp):
+    from find_circ2_amd import _native as N
+    names = [l[1:].split()[0] for l in open(options.genome) if l.startswith(">")]
+
+    def evaluate(reads, read_off, pairs):
+        res = np.zeros(len(pairs), N.RESULT_DTYPE)
+        res["best_x"] = -1
+        res["info"] = N.RES_DONE
+        tw = 2 * ((int(pairs["read_len"].max()) + 64) // 64) if len(pairs) else 2
+        tm = np.zeros((tw, len(pairs)), np.uint64) if hp.allhits else None
+        return res.view(np.int64), tm
+    return evaluate, names, None, False
+
+
+null_factory.batch = _null_batch
 
 
 if __name__ == "__main__":

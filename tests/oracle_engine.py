@@ -37,3 +37,73 @@ def oracle_evaluator_factory(options, hp):
                     out.append(sp)
                 s.result = out
     return evaluate
+
+
+def oracle_batch_engine(options, hp):
+    """The same oracle behind the native caller's batch hook (find_circ2_amd.native_caller).
+
+    Returns (evaluate, genome names, fc2_fasta handle, dummy): ``evaluate`` turns the
+    oracle's hits back into raw ``fc2_result`` words and the ``--all-hits`` tie mask,
+    the form the HIP scan hands to fc2_caller_submit (include/fc2_bp.h).
+    """
+    import ctypes
+
+    import numpy as np
+
+    from find_circ2_amd import _native as N
+
+    of = oracle.OracleFasta(options.genome)
+    p = oracle.params(hp.asize, hp.margin, hp.maxdist, hp.noncanonical, hp.strandpref, hp.allhits)
+    h = ctypes.c_void_p()
+    N.check(N.lib().fc2_fasta_open(options.genome.encode(), 0, ctypes.byref(h)))
+    code = {c: i for i, c in enumerate("ACGTN")}
+    rc = str.maketrans("ACGTN", "TGCAN")
+    hpp = hp.params()
+
+    def evaluate(reads, read_off, pairs):
+        n = len(pairs)
+        lens = pairs["read_len"].astype(np.int64)
+        rp = [bytes(reads[int(o):int(o) + int(l)]) for o, l in zip(read_off, lens)]
+        skip = (pairs["flags"] & N.PAIR_SKIP) != 0
+        idx = np.where(skip, -1, pairs["chrom"].astype(np.int64))
+        r = oracle.scan_fasta(p, of, rp, idx, pairs["a_pos"], pairs["b_aend"],
+                              (pairs["flags"] & N.PAIR_BACKSPLICE) != 0, (pairs["flags"] & N.PAIR_PRIMARY_REV) != 0,
+                              use_fast=False, all_ties=True)
+        res = np.zeros(n, N.RESULT_DTYPE)
+        res["best_x"] = -1
+        info = np.full(n, N.RES_DONE, np.int64)
+        rw, nw, tw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(N.lib().fc2_batch_geometry(ctypes.byref(hpp), int(lens.max()) if n else 0, ctypes.byref(rw),
+                                           ctypes.byref(nw), ctypes.byref(tw)))
+        tm = np.zeros((tw.value, n), np.uint64) if hp.allhits else None
+        half = tw.value // 2
+        for i in range(n):
+            nt = int(r.n_ties[i])
+            if nt == -oracle.ORC_ERR_KEY:
+                info[i] |= N.RES_ERR_KEY
+            elif nt == -oracle.ORC_ERR_SHAPE:
+                info[i] |= N.RES_ERR_WIN
+            elif nt > 0:
+                f = r.first[i]
+                sig = f["gtag"].decode()
+                minus = f["strand"] == b"-"
+                raw = sig[::-1].translate(rc) if minus else sig     # the kernel keeps the genome-strand 4-mer
+                assert len(raw) == 4, raw
+                res["best_x"][i] = int(f["x"])
+                res["dist"][i] = max(0, int(f["dist"]))
+                res["ov"][i] = int(f["ov"])
+                res["n_ties"][i] = nt
+                g12 = sum(code[c] << (3 * k) for k, c in enumerate(raw))
+                info[i] |= (N.RES_MINUS if minus else 0) | (g12 << N.RES_GTAG_SHIFT)
+                if tm is not None:
+                    for t in r.ties_of(i):
+                        x = int(t["x"])
+                        row = (half if t["strand"] == b"-" else 0) + (x >> 6)
+                        tm[row, i] |= np.uint64(1) << np.uint64(x & 63)
+        res["info"] = info.astype(np.uint16)
+        return res.view(np.int64), tm
+
+    return evaluate, list(of.names), h, False
+
+
+oracle_evaluator_factory.batch = oracle_batch_engine

@@ -56,3 +56,23 @@ def test_gpu_cli_equals_oracle_cli_simulated(tmp_path, fa):
         assert rc1 == rc2
         if rc1 == 0:
             _compare(o1, o2)
+
+
+@pytest.mark.parametrize("extra", [[], ["--all-hits", "--non-canonical", "--strand-pref"], ["-d", "0"]])
+def test_gpu_native_caller_equals_oracle_python_caller(tmp_path, extra):
+    """The shipped configuration (C++ read loop + HIP scan) against the Python read loop
+    with the CPU oracle, on the rich mixed input of test_native_caller.py."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd import cli
+    from oracle_engine import oracle_evaluator_factory
+    from test_ingest import same
+    from test_native_caller import _rich_sam
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 2500, seed=97)
+    o1, o2 = str(tmp_path / "oracle_py"), str(tmp_path / "gpu_native")
+    rc1 = cli.main(["-G", fa, "-o", o1, "-n", "mix", "-q", "--python-caller"] + extra + [sam],
+                   evaluator_factory=oracle_evaluator_factory)
+    rc2 = cli.main(["-G", fa, "-o", o2, "-n", "mix", "-q"] + extra + [sam])
+    assert rc1 == rc2 == 0
+    same(o1, o2)

@@ -1,0 +1,311 @@
+"""Native caller (include/fc2_caller.h) == the Python caller, file for file.
+
+The default CLI runs the whole read loop in C++ (grouping, process_mate,
+record_hits, the junction tables, the writers) and hands only the breakpoint
+search to the batch evaluator.  ``--python-caller`` keeps the loop in Python
+(find_circ2_amd.caller, the line-by-line restatement of find_circ.py:1450-1527
+and :976-1447) on the same native ingest, and ``--python-ingest`` in Python
+end to end.  With the CPU oracle as the breakpoint search behind both hooks,
+every output file and every counter in run.log must agree across the three,
+for SAM and BAM input, every option that changes the host logic, known
+junction files, and the inputs on which the reference raises.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from find_circ2_amd import cli
+from oracle_engine import oracle_evaluator_factory
+from samgen import sam_to_bam
+from test_cli import _reads, run_cli
+from test_ingest import _mixed_sam, counters, same
+
+
+def _three(tmp_path, fa, inp, extra, tag=""):
+    outs, rcs = [], []
+    for t, mode in (("py", ["--python-ingest"]), ("pyc", ["--python-caller"]), ("nat", [])):
+        out = str(tmp_path / (tag + t))
+        rcs.append(cli.main(["-G", fa, "-o", out, "-n", "mix", "-q"] + list(extra) + mode + [inp],
+                            evaluator_factory=oracle_evaluator_factory))
+        outs.append(out)
+    return rcs, outs
+
+
+@pytest.fixture(scope="module")
+def mixed(tmp_path_factory):
+    d = tmp_path_factory.mktemp("mixed")
+    sam = str(d / "mixed.sam")
+    fa = _mixed_sam(sam, 2000, seed=4242)
+    bam = str(d / "mixed.bam")
+    sam_to_bam(open(sam).read(), bam)
+    return fa, sam, bam
+
+
+OPTION_SETS = [[], ["--test"], ["--all-hits", "--non-canonical"], ["--all-hits", "--strand-pref", "-d", "0"],
+               ["-d", "0"], ["--half-unique", "--report-nobridges"], ["--no-linear"], ["--no-multi"], ["--noop"],
+               ["--min-uniq-qual", "0", "-a", "12", "-m", "0"], ["--min-uniq-qual", "9", "-m", "4", "-d", "3"],
+               ["--short-threshold", "1000", "--huge-threshold", "2000"], ["--chunk-size", "13"],
+               ["--stdout", "multi"]]
+
+
+@pytest.mark.parametrize("extra", OPTION_SETS, ids=[" ".join(e) or "default" for e in OPTION_SETS])
+def test_native_caller_equals_python_mixed(tmp_path, mixed, extra, capsys):
+    fa, sam, bam = mixed
+    rcs, outs = _three(tmp_path, fa, sam, extra)
+    assert rcs == [0, 0, 0]
+    if "--stdout" in extra:
+        cap = capsys.readouterr().out
+        third = len(cap) // 3
+        assert cap[:third] == cap[third:2 * third] == cap[2 * third:]
+    same(outs[0], outs[1])
+    same(outs[0], outs[2])
+    if not extra:
+        c = counters(outs[2])
+        assert c["circ_spliced"] > 5 and c["lin_spliced"] + c["lin_no_bp"] > 200
+
+
+def test_native_caller_bam_equals_sam(tmp_path, mixed):
+    fa, sam, bam = mixed
+    rc1 = cli.main(["-G", fa, "-o", str(tmp_path / "s"), "-q", sam], evaluator_factory=oracle_evaluator_factory)
+    rc2 = cli.main(["-G", fa, "-o", str(tmp_path / "b"), "-q", bam], evaluator_factory=oracle_evaluator_factory)
+    assert rc1 == rc2 == 0
+    same(str(tmp_path / "s"), str(tmp_path / "b"))
+
+
+@pytest.mark.parametrize("fa,rf", [("test_ref.fa", "test_reads.fa"), ("CDR1as_locus.fa", "cdr1as_reads.fa")])
+@pytest.mark.parametrize("extra", [["--test"], ["--test", "--all-hits", "--non-canonical"]])
+def test_native_caller_equals_python_golden(tmp_path, fa, rf, extra):
+    fa = os.path.join(GOLDEN, fa)
+    rd = _reads(os.path.join(GOLDEN, rf))
+    _, o1 = run_cli(tmp_path, fa, rd, extra=extra + ["--python-caller"], tag="py")
+    _, o2 = run_cli(tmp_path, fa, rd, extra=extra, tag="native")
+    same(o1, o2)
+
+
+def _known_bed(path, rows, extra_rows):
+    with open(path, "w") as f:
+        f.write("#chrom\tstart\tend\tname\tscore\tstrand\n")
+        for r in rows + extra_rows:
+            f.write("\t".join(str(x) for x in r) + "\n")
+
+
+def test_native_caller_known_sites(tmp_path, mixed):
+    """--known-circ/--known-lin: known names replace novel ones, the table keeps file order
+    and a repeated coordinate keeps its first position; unobserved known sites stay unreported."""
+    fa, sam, _ = mixed
+    rcs, outs = _three(tmp_path, fa, sam, [], tag="pre")
+    circ = [l.split("\t") for l in open(os.path.join(outs[0], "circ_splice_sites.bed")) if l[0] != "#"]
+    lin = [l.split("\t") for l in open(os.path.join(outs[0], "lin_splice_sites.bed")) if l[0] != "#"]
+    assert len(circ) > 4 and len(lin) > 4
+    rng = np.random.default_rng(3)
+    pick = lambda rows: [rows[i] for i in sorted(rng.choice(len(rows), len(rows) // 2, replace=False))]  # noqa
+    kc = [(r[0], r[1], r[2], "KC%d" % i, 0, r[5]) for i, r in enumerate(pick(circ))]
+    kl = [(r[0], r[1], r[2], "KL%d" % i, 0, r[5]) for i, r in enumerate(pick(lin))]
+    c0 = circ[0][0]
+    _known_bed(str(tmp_path / "kc.bed"), kc, [(c0, 5, 900, "never_seen", 0, "+"), kc[0][:3] + ("dup", 0, kc[0][5])])
+    _known_bed(str(tmp_path / "kl.bed"), kl, [(c0, 7, 77, "never_seen_lin", 0, "-")])
+    extra = ["--known-circ", str(tmp_path / "kc.bed"), "--known-lin", str(tmp_path / "kl.bed")]
+    rcs, outs = _three(tmp_path, fa, sam, extra)
+    assert rcs == [0, 0, 0]
+    same(outs[0], outs[1])
+    same(outs[0], outs[2])
+    txt = open(os.path.join(outs[2], "circ_splice_sites.bed")).read()
+    assert "never_seen" not in txt and txt.count("\tKC") > 1
+    log = open(os.path.join(outs[2], "run.log")).read()
+    assert "loaded %d known splice sites" % (len(kc) + 2) in log
+
+
+def test_native_caller_missing_chromosome_fails_like_python(tmp_path, mixed):
+    """A SAM reference absent from the FASTA: KeyError(chrom) in get_data (find_circ.py:193)."""
+    fa, sam, _ = mixed
+    txt = open(sam).read().replace("SN:chr2\t", "SN:chrX\t").replace("\tchr2\t", "\tchrX\t")
+    bad = str(tmp_path / "bad.sam")
+    open(bad, "w").write(txt)
+    rcs, outs = _three(tmp_path, fa, bad, [])
+    assert rcs == [1, 1, 1]
+    for o in outs[1:]:
+        assert "KeyError: 'chrX'" in open(os.path.join(o, "run.log")).read()
+
+
+def test_native_caller_stranded_fails_like_reference(tmp_path):
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    rd = _reads(os.path.join(GOLDEN, "test_reads.fa"))
+    rc1, _ = run_cli(tmp_path, fa, rd, extra=["--stranded", "--python-caller"], tag="py")
+    rc2, o2 = run_cli(tmp_path, fa, rd, extra=["--stranded"], tag="nat")
+    assert rc1 == rc2 == 1
+    assert "AttributeError" in open(os.path.join(o2, "run.log")).read()
+
+
+def test_native_caller_single_record_fails_like_reference(tmp_path):
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    sam = tmp_path / "one.sam"
+    sam.write_text("@SQ\tSN:testbed_plus\tLN:720\nr\t0\ttestbed_plus\t10\t60\t20M\t*\t0\t0\t%s\t*\tAS:i:20\n"
+                   % ("A" * 20))
+    rcs, outs = _three(tmp_path, fa, str(sam), [])
+    assert rcs == [1, 1, 1]
+    assert "UnboundLocalError" in open(os.path.join(outs[2], "run.log")).read()
+
+
+def _rich_sam(path, n_frag, seed, secondary_same_chrom=False):
+    """bwa-mem-like SAM with GT/AG (or CT/AC) planted at every junction: 2- and 3-segment linear
+    and circular reads, paired mates (unspliced inside/outside the circle, on another chromosome,
+    linearly spliced), supplementary/secondary records, uniqueness from AS/XS, N and mismatches."""
+    rng = np.random.default_rng(seed)
+    names = ["chr1", "chr2", "chr3"]
+    size = 90_000
+    g = {c: bytearray(np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, size)].tobytes()) for c in names}
+
+    def plant(c, istart, iend, minus):
+        g[c][istart:istart + 2] = b"CT" if minus else b"GT"
+        g[c][iend - 2:iend] = b"AC" if minus else b"AG"
+
+    frags = []                          # list of mates; a mate = list of (chrom, gpos, qlen)
+    for i in range(n_frag):
+        c = names[int(rng.integers(3))]
+        minus = rng.random() < 0.4
+
+        def unspliced(L=100, lo=1000, hi=size - 1000, chrom=c):
+            p = int(rng.integers(lo, max(lo + 1, hi - L)))
+            return [(chrom, min(max(p, 0), size - L - 1), L)]
+
+        def lin(nseg, L=100):
+            cuts = sorted(rng.choice(np.arange(12, L - 12), nseg - 1, replace=False))
+            lens = np.diff([0] + list(cuts) + [L])
+            p = int(rng.integers(2000, size - 20000))
+            segs = []
+            for k, ln in enumerate(lens):
+                segs.append((c, p, int(ln)))
+                if k < nseg - 1:
+                    nxt = p + int(ln) + int(rng.integers(60, 3000))
+                    plant(c, p + int(ln), nxt, minus)
+                    p = nxt
+            return segs
+
+        def circ(nseg, L=100):
+            kA = int(rng.integers(12, L - 12))
+            span = int(rng.integers(150, 6000))
+            E = int(rng.integers(span + 500, size - 2000))
+            S = E - span
+            plant(c, E, S, minus)
+            if nseg == 2:
+                return [(c, E - kA, kA), (c, S, L - kA)]
+            k1 = int(rng.integers(12, L - kA - 12 + 1)) if L - kA - 24 > 0 else (L - kA) // 2
+            mid = S + k1 + int(rng.integers(40, max(41, span - k1 - kA - 40)))
+            mid = min(mid, E - kA - 20)
+            plant(c, S + k1, mid, minus)
+            return [(c, E - kA, kA), (c, S, k1), (c, mid, L - kA - k1)]
+
+        kind = rng.random()
+        if kind < 0.15:
+            frags.append([unspliced()])
+        elif kind < 0.3:
+            frags.append([lin(2)])
+        elif kind < 0.4:
+            frags.append([lin(3)])
+        elif kind < 0.55:
+            frags.append([circ(2)])
+        elif kind < 0.6:
+            frags.append([circ(3)])
+        else:
+            m1 = circ(2) if rng.random() < 0.75 else lin(2)
+            lo = min(s[1] for s in m1)
+            hi = max(s[1] + s[2] for s in m1)
+            r = rng.random()
+            if r < 0.35:
+                m2 = unspliced(lo=lo, hi=hi + 100)                           # inside the circle
+            elif r < 0.6:
+                m2 = unspliced(lo=hi + 200, hi=hi + 5000)                    # outside
+            elif r < 0.7:
+                m2 = unspliced(chrom=names[(names.index(c) + 1) % 3])        # another chromosome
+            elif r < 0.9:
+                m2 = lin(2)
+            else:
+                m2 = circ(2)
+            frags.append([m1, m2])
+
+    ok = lambda segs: all(ln > 0 and 0 <= p and p + ln <= size for _, p, ln in segs)  # noqa: E731
+    frags = [[m if ok(m) else [(m[0][0], 5000, 100)] for m in mates] for mates in frags]
+    lines = ["@HD\tVN:1.5"] + ["@SQ\tSN:%s\tLN:%d" % (c, size) for c in names]
+    for i, mates in enumerate(frags):
+        qn = "f%05d" % i
+        if rng.random() < 0.03:
+            lines.append("%s\t4\t*\t0\t0\t*\t*\t0\t0\t%s\t*" % (qn, "A" * 100))
+            continue
+        for mi, segs in enumerate(mates):
+            mf = 0 if len(mates) == 1 else (0x41 if mi == 0 else 0x81)
+            if mf and rng.random() < 0.7:
+                mf |= 0x2
+            rev = 16 if rng.random() < 0.3 else 0
+            read = bytearray(b"".join(bytes(g[c][p:p + ln]) for c, p, ln in segs))
+            for _ in range(int(rng.integers(0, 3))):                        # mismatches
+                k = int(rng.integers(len(read)))
+                read[k] = b"ACGT"[(b"ACGT".index(read[k]) + 1) % 4] if read[k] in b"ACGT" else read[k]
+            if rng.random() < 0.05:
+                read[int(rng.integers(len(read)))] = ord("N")
+            seq = read.decode()
+            qual = "*" if rng.random() < 0.1 else "".join(chr(33 + int(q)) for q in rng.integers(2, 40, len(seq)))
+            prim = int(rng.integers(len(segs)))
+            q0 = 0
+            recs = []
+            for k, (c, p, ln) in enumerate(segs):
+                before, after = q0, len(seq) - q0 - ln
+                clip = "S" if k == prim else "H"
+                cig = ("%d%s" % (before, clip) if before else "") + "%dM" % ln + ("%d%s" % (after, clip) if after else "")
+                s_ = seq if k == prim else seq[q0:q0 + ln]
+                qq = qual if (k == prim or qual == "*") else qual[q0:q0 + ln]
+                asv = ln - int(rng.integers(0, 3))
+                tags = "AS:i:%d" % asv
+                if rng.random() < 0.6:
+                    tags += "\tXS:i:%d" % int(rng.integers(0, asv + 2))
+                fl = mf | rev | (0 if k == prim else 2048)
+                recs.append((k != prim, "%s\t%d\t%s\t%d\t%d\t%s\t*\t0\t0\t%s\t%s\t%s" %
+                             (qn, fl, c, p + 1, int(rng.integers(0, 61)), cig, s_, qq, tags)))
+                q0 += ln
+            recs.sort(key=lambda t: t[0])
+            lines += [t[1] for t in recs]
+            if rng.random() < 0.05:
+                c, p, ln = segs[0]
+                if not secondary_same_chrom:
+                    c = names[(names.index(c) + 1) % 3]
+                lines.append("%s\t%d\t%s\t%d\t0\t%dM\t*\t0\t0\t*\t*\tAS:i:%d" % (qn, mf | 256, c, p + 501, ln, ln - 3))
+    with open(path, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    fa = path + ".fa"
+    with open(fa, "w") as f:
+        for c in names:
+            f.write(">%s\n" % c)
+            s = g[c].decode()
+            for k in range(0, size, 70):
+                f.write(s[k:k + 70] + "\n")
+    return fa
+
+
+RICH_SETS = [[], ["--all-hits", "--non-canonical", "--strand-pref"], ["--half-unique", "--report-nobridges"],
+             ["-d", "0", "--min-uniq-qual", "0"], ["--no-linear"], ["--chunk-size", "5", "--all-hits"]]
+
+
+@pytest.mark.parametrize("extra", RICH_SETS, ids=[" ".join(e) or "default" for e in RICH_SETS])
+def test_native_caller_equals_python_rich(tmp_path, extra):
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 2500, seed=97)
+    rcs, outs = _three(tmp_path, fa, sam, extra)
+    assert rcs == [0, 0, 0]
+    same(outs[0], outs[1])
+    same(outs[0], outs[2])
+    if not extra:
+        c = counters(outs[2])
+        assert c["circ_spliced"] > 300 and c["lin_spliced"] > 300
+        multi = open(os.path.join(outs[2], "multi_events.tsv")).read().splitlines()
+        assert len(multi) > 50
+
+
+def test_native_caller_secondary_without_seq_fails_like_python(tmp_path):
+    """A SEQ-less secondary hit next to the primary joins proper_segs; len(None) raises
+    (find_circ.py:1101, pysam query of SEQ "*") in all three read loops."""
+    sam = str(tmp_path / "sec.sam")
+    fa = _rich_sam(sam, 800, seed=5, secondary_same_chrom=True)
+    rcs, outs = _three(tmp_path, fa, sam, [])
+    assert rcs == [1, 1, 1]
+    assert "TypeError: object of type 'NoneType' has no len()" in open(os.path.join(outs[2], "run.log")).read()
