@@ -256,6 +256,12 @@ static int load_index_file(fc2_fasta *f, const std::string &ipath) {
     }
     free(line);
     fclose(fp);
+    // the file lists chromosomes by name; keep FASTA order so that chromosome indices (and
+    // everything laid out by them) do not depend on whether an index file existed
+    std::stable_sort(f->chroms.begin(), f->chroms.end(),
+                     [](const fc2_chrom_rec &a, const fc2_chrom_rec &b) { return a.ofs < b.ofs; });
+    f->by_name.clear();
+    for (size_t i = 0; i < f->chroms.size(); ++i) f->by_name[f->chroms[i].name] = (int)i;
     return rc;
 }
 

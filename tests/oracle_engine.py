@@ -56,6 +56,12 @@ def oracle_batch_engine(options, hp):
     p = oracle.params(hp.asize, hp.margin, hp.maxdist, hp.noncanonical, hp.strandpref, hp.allhits)
     h = ctypes.c_void_p()
     N.check(N.lib().fc2_fasta_open(options.genome.encode(), 0, ctypes.byref(h)))
+    names = []
+    for i in range(N.lib().fc2_fasta_n_chrom(h)):
+        nm = ctypes.c_char_p()
+        N.check(N.lib().fc2_fasta_chrom(h, i, ctypes.byref(nm), None, None, None, None, None))
+        names.append(nm.value.decode())
+    to_oracle = np.array([of.names.index(nm) for nm in names] or [0], np.int64)   # handle index -> oracle index
     code = {c: i for i, c in enumerate("ACGTN")}
     rc = str.maketrans("ACGTN", "TGCAN")
     hpp = hp.params()
@@ -65,7 +71,7 @@ def oracle_batch_engine(options, hp):
         lens = pairs["read_len"].astype(np.int64)
         rp = [bytes(reads[int(o):int(o) + int(l)]) for o, l in zip(read_off, lens)]
         skip = (pairs["flags"] & N.PAIR_SKIP) != 0
-        idx = np.where(skip, -1, pairs["chrom"].astype(np.int64))
+        idx = np.where(skip, -1, to_oracle[np.minimum(pairs["chrom"].astype(np.int64), len(to_oracle) - 1)])
         r = oracle.scan_fasta(p, of, rp, idx, pairs["a_pos"], pairs["b_aend"],
                               (pairs["flags"] & N.PAIR_BACKSPLICE) != 0, (pairs["flags"] & N.PAIR_PRIMARY_REV) != 0,
                               use_fast=False, all_ties=True)
@@ -103,7 +109,7 @@ def oracle_batch_engine(options, hp):
         res["info"] = info.astype(np.uint16)
         return res.view(np.int64), tm
 
-    return evaluate, list(of.names), h, False
+    return evaluate, names, h, False
 
 
 oracle_evaluator_factory.batch = oracle_batch_engine

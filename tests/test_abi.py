@@ -133,10 +133,32 @@ def test_index_file_roundtrip(L, tmp_path):
     rc, h2 = _open(path)
     assert rc == 0
     ref = RefIndexedFasta(path)
-    for name, ofs, ldata, skip, size, _ in _chroms(h2):
+    loaded = _chroms(h2)
+    for name, ofs, ldata, skip, size, _ in loaded:
         r = ref.chrom_stats[name]
         assert (ofs, ldata, skip, size) == (r[0], r[1], r[2], r[4])
+    # chromosome indices keep FASTA order whether or not the index file was there (the file
+    # itself lists them by name)
+    os.rename(path + ".byo_index", path + ".moved")
+    rc, h3 = _open(path)
+    assert rc == 0 and [c[0] for c in _chroms(h3)] == [c[0] for c in loaded]
+    assert [c[1] for c in loaded] == sorted(c[1] for c in loaded)
     L.fc2_fasta_close(h2)
+    L.fc2_fasta_close(h3)
+
+
+def test_index_file_keeps_fasta_order(L, tmp_path):
+    """The .byo_index lists chromosomes by name; indices must still follow the FASTA."""
+    path = str(tmp_path / "u.fa")
+    open(path, "wb").write(b">zeta\nACGTACGT\n>alpha\nGGGG\n>mid\nTTTTTT\n")
+    rc, h = _open(path, write_index=1)
+    built = [c[0] for c in _chroms(h)]
+    L.fc2_fasta_close(h)
+    assert built == ["zeta", "alpha", "mid"]
+    assert [l.split("\t")[0] for l in open(path + ".byo_index")] == ["alpha", "mid", "zeta"]
+    rc, h = _open(path)
+    assert rc == 0 and [c[0] for c in _chroms(h)] == built
+    L.fc2_fasta_close(h)
 
 
 def test_malformed_fasta_errors(L, tmp_path):
