@@ -200,7 +200,8 @@ struct fc2_caller {
         std::unordered_map<std::string, size_t> index;
         int64_t novel = 0;
     } st[2];                                    // 0 circ, 1 lin
-    std::map<std::string, double> N;            // the reference's counters (sorted keys)
+    std::vector<std::pair<const char *, double>> N;   // the reference's counters, keyed by literal
+                                                      // (merged by name into sorted keys on output)
     std::string out[3];                         // reads, multi, test text since the last take
     std::string rows_text;
     std::vector<std::pair<std::string, double>> counters_snapshot;
@@ -209,7 +210,11 @@ struct fc2_caller {
 
 namespace {
 
-void incN(fc2_caller *h, const char *k, double v = 1.) { h->N[k] += v; }
+void incN(fc2_caller *h, const char *k, double v = 1.) {
+    for (auto &kv : h->N)
+        if (kv.first == k) { kv.second += v; return; }
+    h->N.emplace_back(k, v);
+}
 
 // ---- Hit / SpliceSiteStorage ----------------------------------------------------------
 void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
@@ -1076,7 +1081,8 @@ extern "C" int fc2_caller_counter(fc2_caller *h, int i, const char **name, doubl
     if (i == 0) {
         // the caller's own counters plus those the ingest kept for fragments it never handed
         // over (Caller.run_native adds the non-zero ones)
-        std::map<std::string, double> m = h->N;
+        std::map<std::string, double> m;
+        for (const auto &kv : h->N) m[kv.first] += kv.second;
         fc2_ingest_counts c{};
         fc2_ingest_counts_get(h->ing, &c);
         const std::pair<const char *, uint64_t> ing[4] = {{"total_mates", c.total_mates},

@@ -16,7 +16,10 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
+#include <future>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -72,6 +75,122 @@ void finish_rec(Rec &r, const std::vector<std::pair<int, int>> &ops, int64_t seq
     r.qlen = r.has_seq ? (int32_t)(seqlen - c.lead_s - c.trail_s) : -1;
 }
 
+// ---- parallel BGZF ----------------------------------------------------------------------
+// BAM is a series of BGZF blocks (gzip members of <= 64 KiB with the compressed size in a
+// "BC" extra field), so the blocks can be inflated independently.  A batch of blocks is
+// read sequentially and inflated by a few threads while the previous batch is parsed.
+bool read_full(int fd, uint8_t *dst, size_t n, size_t &got) {
+    got = 0;
+    while (got < n) {
+        ssize_t k;
+        do { k = read(fd, dst + got, n - got); } while (k < 0 && errno == EINTR);
+        if (k < 0) return false;
+        if (k == 0) break;
+        got += (size_t)k;
+    }
+    return true;
+}
+
+// BGZF block size from an 18+-byte header, 0 if the header is not BGZF
+size_t bgzf_block_size(const uint8_t *h, size_t avail) {
+    if (avail < 18 || h[0] != 0x1f || h[1] != 0x8b || h[2] != 8 || !(h[3] & 4)) return 0;
+    const size_t xlen = h[10] | (h[11] << 8);
+    if (avail < 12 + xlen) return 0;
+    for (size_t p = 12; p + 4 <= 12 + xlen;) {
+        const size_t slen = h[p + 2] | (h[p + 3] << 8);
+        if (h[p] == 'B' && h[p + 1] == 'C' && slen == 2 && p + 6 <= 12 + xlen) return (size_t)(h[p + 4] | (h[p + 5] << 8)) + 1;
+        p += 4 + slen;
+    }
+    return 0;
+}
+
+struct BgzfBatch {
+    std::vector<char> out;
+    bool eof = false;
+    std::string err;
+};
+
+int bgzf_threads() {
+    const char *e = getenv("FC2_INGEST_THREADS");
+    int n = e ? atoi(e) : (int)std::thread::hardware_concurrency();
+    return std::max(1, std::min(n, 8));
+}
+
+// reads up to `max_blocks` blocks (the first `pre` bytes of the first header are in `pre`)
+BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_threads) {
+    BgzfBatch B;
+    std::vector<uint8_t> raw;
+    std::vector<size_t> boff, bsz;
+    raw.swap(pre);
+    size_t pos = 0;
+    while ((int)boff.size() < max_blocks) {
+        size_t got;
+        if (raw.size() - pos < 18) {           // header
+            const size_t have = raw.size() - pos;
+            raw.resize(pos + 18);
+            if (!read_full(fd, raw.data() + pos + have, 18 - have, got)) { B.err = "read error"; return B; }
+            if (have + got == 0) { raw.resize(pos); B.eof = true; break; }
+            if (have + got < 18) { B.err = "truncated BGZF block header"; return B; }
+        }
+        const size_t xlen = raw[pos + 10] | (raw[pos + 11] << 8);
+        if (raw.size() - pos < 12 + xlen) {
+            const size_t have = raw.size() - pos;
+            raw.resize(pos + 12 + xlen);
+            if (!read_full(fd, raw.data() + pos + have, 12 + xlen - have, got) || got < 12 + xlen - have) {
+                B.err = "truncated BGZF block header";
+                return B;
+            }
+        }
+        const size_t bs = bgzf_block_size(raw.data() + pos, raw.size() - pos);
+        if (bs < 12 + xlen + 8) { B.err = "not a BGZF block"; return B; }
+        const size_t have = raw.size() - pos;
+        raw.resize(pos + bs);
+        if (!read_full(fd, raw.data() + pos + have, bs - have, got) || got < bs - have) {
+            B.err = "truncated BGZF block";
+            return B;
+        }
+        boff.push_back(pos);
+        bsz.push_back(bs);
+        pos += bs;
+    }
+    const size_t nb = boff.size();
+    std::vector<size_t> ooff(nb + 1, 0);
+    for (size_t i = 0; i < nb; ++i) {
+        const uint8_t *t = raw.data() + boff[i] + bsz[i] - 4;
+        ooff[i + 1] = ooff[i] + (size_t)(t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24));
+    }
+    B.out.resize(ooff[nb]);
+    std::atomic<size_t> next{0};
+    std::atomic<bool> bad{false};
+    auto work = [&]() {
+        z_stream zs{};
+        if (inflateInit2(&zs, -15) != Z_OK) { bad = true; return; }
+        for (size_t i; (i = next.fetch_add(1)) < nb && !bad;) {
+            const uint8_t *blk = raw.data() + boff[i];
+            const size_t xl = blk[10] | (blk[11] << 8);
+            inflateReset(&zs);
+            zs.next_in = (Bytef *)(blk + 12 + xl);
+            zs.avail_in = (uInt)(bsz[i] - 12 - xl - 8);
+            zs.next_out = (Bytef *)(B.out.data() + ooff[i]);
+            zs.avail_out = (uInt)(ooff[i + 1] - ooff[i]);
+            const int rc = inflate(&zs, Z_FINISH);
+            const uint8_t *t = blk + bsz[i] - 8;
+            const uint32_t crc = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
+            if (rc != Z_STREAM_END || zs.avail_out != 0 ||
+                crc32(0L, (const Bytef *)(B.out.data() + ooff[i]), (uInt)(ooff[i + 1] - ooff[i])) != crc)
+                bad = true;
+        }
+        inflateEnd(&zs);
+    };
+    const int nt = (int)std::min<size_t>((size_t)n_threads, std::max<size_t>(1, nb));
+    std::vector<std::thread> pool;
+    for (int t = 1; t < nt; ++t) pool.emplace_back(work);
+    work();
+    for (auto &t : pool) t.join();
+    if (bad) B.err = "corrupt BGZF block";
+    return B;
+}
+
 }  // namespace
 
 struct fc2_ingest {
@@ -86,6 +205,11 @@ struct fc2_ingest {
     bool z_init = false;
     std::vector<char> zin;
     bool z_done = false;
+    // BGZF (the BAM case): batches inflated in parallel, one batch ahead of the parser
+    bool bgzf = false;
+    int bgzf_nt = 1;
+    std::future<BgzfBatch> bgzf_next;
+    std::string z_err;
     // header
     std::string header;
     std::vector<std::string> refs;
@@ -99,6 +223,11 @@ struct fc2_ingest {
     fc2_ingest_counts counts{};
     bool finished = false;
     bool need_text = true;       // false once a native caller pulls structured fragments
+    // parse scratch, reused across records (no per-record allocation in steady state)
+    std::vector<std::pair<int, int>> ops;
+    std::vector<Rec> pool;       // recycled records: their strings keep their capacity
+    std::string last_rn;         // RNAME -> tid cache (consecutive records share a chromosome)
+    int last_tid = -1;
 };
 
 namespace {
@@ -130,6 +259,16 @@ bool ensure(fc2_ingest *h, size_t n) {
             do { k = read(h->fd, h->buf.data() + h->end, h->buf.size() - h->end); } while (k < 0 && errno == EINTR);
             if (k <= 0) { h->eof_in = true; return false; }
             h->end += (size_t)k;
+        } else if (h->bgzf) {
+            if (h->z_done) return false;
+            BgzfBatch b = h->bgzf_next.get();
+            if (!b.err.empty()) { h->z_err = b.err; h->z_done = true; return false; }
+            if (b.eof) h->z_done = true;
+            else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), 256,
+                                           h->bgzf_nt);
+            if (h->buf.size() < h->end + b.out.size()) h->buf.resize(h->end + b.out.size());
+            memcpy(h->buf.data() + h->end, b.out.data(), b.out.size());
+            h->end += b.out.size();
         } else {
             if (h->z_done) return false;
             // inflate more
@@ -154,28 +293,52 @@ bool ensure(fc2_ingest *h, size_t n) {
     return true;
 }
 
-// SAM: next line into `line` (without newline); false at EOF
-bool next_line(fc2_ingest *h, std::string &line) {
+// SAM: next line as [*s, *e) inside the input buffer (without newline; valid until the next
+// call); false at EOF
+bool next_line_view(fc2_ingest *h, const char *&ls, const char *&le) {
     for (;;) {
         const char *s = h->buf.data() + h->beg;
         const char *nl = (const char *)memchr(s, '\n', h->end - h->beg);
         if (nl) {
-            line.assign(s, nl);
+            ls = s;
+            le = nl;
             h->beg = (size_t)(nl - h->buf.data()) + 1;
-            if (!line.empty() && line.back() == '\r') line.pop_back();
+            if (le > ls && le[-1] == '\r') --le;
             return true;
         }
         size_t have = h->end - h->beg;
         if (!ensure(h, have + 1)) {
             if (h->end > h->beg) {
-                line.assign(h->buf.data() + h->beg, h->end - h->beg);
+                ls = h->buf.data() + h->beg;
+                le = h->buf.data() + h->end;
                 h->beg = h->end;
-                if (!line.empty() && line.back() == '\r') line.pop_back();
+                if (le > ls && le[-1] == '\r') --le;
                 return true;
             }
             return false;
         }
     }
+}
+
+bool next_line(fc2_ingest *h, std::string &line) {
+    const char *s, *e;
+    if (!next_line_view(h, s, e)) return false;
+    line.assign(s, e);
+    return true;
+}
+
+// strtoll(field, NULL, 10) semantics; digits-only fields (the normal case) without a copy
+int64_t to_i64(const char *b, const char *e) {
+    const char *p = b;
+    bool neg = false;
+    if (p < e && (*p == '-' || *p == '+')) neg = *p++ == '-';
+    if (p < e && p - b <= 1) {
+        int64_t v = 0;
+        const char *q = p;
+        while (q < e && *q >= '0' && *q <= '9' && q - p < 18) v = v * 10 + (*q++ - '0');
+        if (q == e && q > p) return neg ? -v : v;
+    }
+    return strtoll(std::string(b, e).c_str(), nullptr, 10);
 }
 
 // AS / XS of one tag in SAM text form "TG:T:value" (first occurrence wins, like get_tag)
@@ -185,7 +348,7 @@ void note_tag(Rec &r, const char *t, const char *e) {
     if (!as && !xs) return;
     if ((as && r.has_as) || (xs && r.has_xs)) return;
     const bool isint = t[3] == 'i';
-    const int64_t v = isint ? strtoll(std::string(t + 5, e).c_str(), nullptr, 10) : 0;
+    const int64_t v = isint ? to_i64(t + 5, e) : 0;
     if (as) { r.has_as = true; r.as_int = isint; r.as = v; }
     else { r.has_xs = true; r.xs_int = isint; r.xs = v; }
 }
@@ -199,53 +362,61 @@ void scan_sam_tags(Rec &r, const char *p, const char *end) {
     }
 }
 
-int parse_sam_record(fc2_ingest *h, const std::string &line, Rec &r) {
-    // fields 1-11
-    size_t f[12];
+int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r) {
+    // fields 1-11 (and the start of the tags)
+    const char *f[13];
     int nf = 0;
-    f[nf++] = 0;
-    for (size_t i = 0; i < line.size() && nf < 12; ++i)
-        if (line[i] == '\t') f[nf++] = i + 1;
-    if (nf < 11) return fc2::fail(FC2_E_FORMAT, "malformed SAM line: " + line.substr(0, 80));
-    auto field = [&](int k) {
-        size_t b = f[k];
-        size_t e = (k + 1 < nf) ? f[k + 1] - 1 : line.size();
-        if (k + 1 >= nf) {
-            size_t t = line.find('\t', b);
-            if (t != std::string::npos) e = t;
-        }
-        return std::string(line, b, e - b);
-    };
-    if (h->need_text) r.text = line;
-    r.qname = field(0);
-    r.flag = (uint32_t)strtoul(field(1).c_str(), nullptr, 10);
-    std::string rn = field(2);
-    if (rn == "*") r.tid = -1;
-    else {
-        auto it = h->tid_of.find(rn);
-        r.tid = it == h->tid_of.end() ? -1 : it->second;
+    f[nf++] = ls;
+    for (const char *p = ls; nf < 12;) {
+        const char *t = (const char *)memchr(p, '\t', (size_t)(le - p));
+        if (!t) break;
+        f[nf++] = t + 1;
+        p = t + 1;
     }
-    r.pos = strtoll(field(3).c_str(), nullptr, 10) - 1;
-    std::string cig = field(5);
-    std::vector<std::pair<int, int>> ops;
-    if (cig != "*") {
+    if (nf < 11) return fc2::fail(FC2_E_FORMAT, "malformed SAM line: " + std::string(ls, std::min<size_t>(80, le - ls)));
+    auto fb = [&](int k) { return f[k]; };
+    auto fe = [&](int k) {
+        if (k + 1 < nf) return f[k + 1] - 1;
+        const char *t = (const char *)memchr(f[k], '\t', (size_t)(le - f[k]));
+        return t ? t : le;
+    };
+    if (h->need_text) r.text.assign(ls, le);
+    r.qname.assign(fb(0), fe(0));
+    r.flag = (uint32_t)to_i64(fb(1), fe(1));
+    const char *rb = fb(2), *re = fe(2);
+    if (re - rb == 1 && *rb == '*') r.tid = -1;
+    else if ((size_t)(re - rb) == h->last_rn.size() && memcmp(rb, h->last_rn.data(), h->last_rn.size()) == 0) {
+        r.tid = h->last_tid;
+    } else {
+        h->last_rn.assign(rb, re);
+        auto it = h->tid_of.find(h->last_rn);
+        r.tid = h->last_tid = it == h->tid_of.end() ? -1 : it->second;
+    }
+    r.pos = to_i64(fb(3), fe(3)) - 1;
+    std::vector<std::pair<int, int>> &ops = h->ops;
+    ops.clear();
+    const char *cb = fb(5), *ce = fe(5);
+    if (!(ce - cb == 1 && *cb == '*')) {
         long n = 0;
-        for (char c : cig) {
-            if (c >= '0' && c <= '9') n = n * 10 + (c - '0');
+        for (const char *c = cb; c < ce; ++c) {
+            if (*c >= '0' && *c <= '9') n = n * 10 + (*c - '0');
             else {
-                int code = cig_code(c);
-                if (code < 0) return fc2::fail(FC2_E_FORMAT, "bad CIGAR: " + cig);
+                int code = cig_code(*c);
+                if (code < 0) return fc2::fail(FC2_E_FORMAT, "bad CIGAR: " + std::string(cb, ce));
                 ops.emplace_back(code, (int)n);
                 n = 0;
             }
         }
     }
-    r.seq = field(9);
-    r.has_seq = r.seq != "*";
-    r.qual = field(10);
-    r.has_qual = r.qual != "*";
+    r.seq.assign(fb(9), fe(9));
+    r.has_seq = !(r.seq.size() == 1 && r.seq[0] == '*');
+    r.qual.assign(fb(10), fe(10));
+    r.has_qual = !(r.qual.size() == 1 && r.qual[0] == '*');
+    r.has_as = r.has_xs = false;
+    r.as_int = r.xs_int = true;
+    r.as = r.xs = 0;
     finish_rec(r, ops, r.has_seq ? (int64_t)r.seq.size() : 0);
-    if (nf == 12) scan_sam_tags(r, line.c_str() + f[11], line.c_str() + line.size());
+    if (nf == 12) scan_sam_tags(r, f[11], le);
     return FC2_OK;
 }
 
@@ -341,10 +512,11 @@ void scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
 
 int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     got = false;
-    if (!ensure(h, 4)) return FC2_OK;
+    if (!ensure(h, 4)) return h->z_err.empty() ? FC2_OK : fc2::fail(FC2_E_FORMAT, "BAM input: " + h->z_err);
     int32_t bs;
     memcpy(&bs, h->buf.data() + h->beg, 4);
-    if (bs < 32 || !ensure(h, 4 + (size_t)bs)) return fc2::fail(FC2_E_FORMAT, "truncated BAM record");
+    if (bs < 32 || !ensure(h, 4 + (size_t)bs))
+        return fc2::fail(FC2_E_FORMAT, "truncated BAM record" + (h->z_err.empty() ? "" : " (" + h->z_err + ")"));
     const uint8_t *b = (const uint8_t *)h->buf.data() + h->beg + 4;
     const uint8_t *e = b + bs;
     int32_t ref_id, pos, l_seq, nref, npos, tlen;
@@ -356,41 +528,51 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     const uint8_t *p = b + 32;
     r.qname.assign((const char *)p, l_name ? l_name - 1 : 0);
     p += l_name;
-    std::vector<std::pair<int, int>> ops(n_cig);
-    std::string cig;
-    char tmp[32];
+    std::vector<std::pair<int, int>> &ops = h->ops;
+    ops.resize(n_cig);
     for (int k = 0; k < n_cig; ++k) {
         uint32_t c; memcpy(&c, p + 4 * k, 4);
         ops[k] = {(int)(c & 0xF), (int)(c >> 4)};
-        snprintf(tmp, sizeof tmp, "%u%c", c >> 4, "MIDNSHP=X"[(c & 0xF) < 9 ? (c & 0xF) : 0]);
-        cig += tmp;
     }
+    const uint8_t *cigp = p;
     p += 4 * n_cig;
     static const char *SEQ = "=ACMGRSVTWYHKDBN";
-    std::string seq;
-    seq.reserve((size_t)l_seq);
-    for (int k = 0; k < l_seq; ++k) seq += SEQ[(p[k >> 1] >> ((k & 1) ? 0 : 4)) & 0xF];
+    std::string &seq = r.seq;
+    seq.resize((size_t)l_seq);
+    for (int k = 0; k + 1 < l_seq; k += 2) {
+        const uint8_t b2 = p[k >> 1];
+        seq[k] = SEQ[b2 >> 4];
+        seq[k + 1] = SEQ[b2 & 0xF];
+    }
+    if (l_seq & 1) seq[l_seq - 1] = SEQ[p[(l_seq - 1) >> 1] >> 4];
     p += (l_seq + 1) / 2;
-    std::string qual;
-    if (l_seq == 0 || p[0] == 0xFF) qual = "*";
+    std::string &qual = r.qual;
+    if (l_seq == 0 || p[0] == 0xFF) qual.assign(1, '*');
     else { qual.resize((size_t)l_seq); for (int k = 0; k < l_seq; ++k) qual[k] = (char)(p[k] + 33); }
     p += l_seq;
     r.flag = flag;
     r.tid = ref_id;
     r.pos = pos;
     r.has_seq = l_seq > 0;
+    if (!r.has_seq) seq.assign(1, '*');
     finish_rec(r, ops, l_seq);
+    r.has_as = r.has_xs = false;
+    r.as_int = r.xs_int = true;
+    r.as = r.xs = 0;
     scan_bam_tags(r, p, e);
-    r.has_qual = qual != "*";
+    r.has_qual = !(qual.size() == 1 && qual[0] == '*');
     if (!h->need_text) {
-        r.seq = std::move(seq);
-        r.qual = std::move(qual);
         h->beg += 4 + (size_t)bs;
         got = true;
         return FC2_OK;
     }
-    r.seq = seq;
-    r.qual = qual;
+    std::string cig;
+    char tmp[32];
+    for (int k = 0; k < n_cig; ++k) {
+        uint32_t c; memcpy(&c, cigp + 4 * k, 4);
+        snprintf(tmp, sizeof tmp, "%u%c", c >> 4, "MIDNSHP=X"[(c & 0xF) < 9 ? (c & 0xF) : 0]);
+        cig += tmp;
+    }
     // SAM text (hand-back to the Python caller)
     std::string &t = r.text;
     t = r.qname;
@@ -399,7 +581,7 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     snprintf(tmp, sizeof tmp, "\t%d\t%u\t", pos + 1, mapq); t += tmp;
     t += cig.empty() ? std::string("*") : cig;
     t += "\t*\t0\t0\t";
-    t += l_seq ? seq : std::string("*");
+    t += seq;
     t += '\t';
     t += qual;
     append_bam_tags(t, p, e);
@@ -429,11 +611,12 @@ int read_header(fc2_ingest *h) {
             }
         }
     }
-    if (!ensure(h, 12)) return fc2::fail(FC2_E_FORMAT, "truncated BAM header");
+    if (!ensure(h, 12)) return fc2::fail(FC2_E_FORMAT, "truncated BAM header" + (h->z_err.empty() ? "" : " (" + h->z_err + ")"));
     if (memcmp(h->buf.data() + h->beg, "BAM\1", 4) != 0) return fc2::fail(FC2_E_FORMAT, "not a BAM file");
     int32_t lt;
     memcpy(&lt, h->buf.data() + h->beg + 4, 4);
-    if (!ensure(h, 8 + (size_t)lt + 4)) return fc2::fail(FC2_E_FORMAT, "truncated BAM header");
+    if (!ensure(h, 8 + (size_t)lt + 4))
+        return fc2::fail(FC2_E_FORMAT, "truncated BAM header" + (h->z_err.empty() ? "" : " (" + h->z_err + ")"));
     h->header.assign(h->buf.data() + h->beg + 8, (size_t)lt);
     while (!h->header.empty() && h->header.back() == '\0') h->header.pop_back();
     h->beg += 8 + (size_t)lt;
@@ -460,21 +643,29 @@ bool next_record(fc2_ingest *h, Rec &r, int &rc) {
         rc = parse_bam_record(h, r, got);
         return rc == FC2_OK && got;
     }
-    std::string line;
+    const char *ls, *le;
     for (;;) {
-        if (!next_line(h, line)) return false;
+        if (!next_line_view(h, ls, le)) return false;
         bool blank = true;
-        for (char c : line) if (!isspace((unsigned char)c)) { blank = false; break; }
+        for (const char *c = ls; c < le; ++c) if (!isspace((unsigned char)*c)) { blank = false; break; }
         if (blank) continue;
-        rc = parse_sam_record(h, line, r);
+        rc = parse_sam_record(h, ls, le, r);
         return rc == FC2_OK;
     }
 }
 
 // ---- fragment logic ----------------------------------------------------------
+// records go back to the pool instead of being freed: their strings keep their capacity
+void recycle(fc2_ingest *h, Mate &m) {
+    for (Rec &r : m.recs) h->pool.push_back(std::move(r));
+    m.recs.clear();
+    m.proper.clear();
+    m.valid = false;
+}
+
 void open_mate(fc2_ingest *h, Mate &m, Rec &&r) {
     h->counts.total_mates++;
-    m.recs.clear();
+    recycle(h, m);
     m.proper.clear();
     m.recs.push_back(std::move(r));
     m.proper.push_back(0);
@@ -499,13 +690,23 @@ MateEval eval_mate(const Mate &m, int asize) {
     if (m.proper.size() < 2) { ev.unspliced = true; return ev; }
     const Rec &prim = m.recs[0];
     if (!prim.has_seq) { ev.python_must_see = true; return ev; }   // len(None) in the reference
-    std::vector<int> segs = m.proper;
-    for (int k : segs) {
+    for (int k : m.proper) {
         const Rec &s = m.recs[k];
         if (s.qlen < 0 || s.aend < 0) { ev.python_must_see = true; return ev; }
     }
-    std::stable_sort(segs.begin(), segs.end(), [&](int a, int b) { return m.recs[a].astart < m.recs[b].astart; });
-    for (size_t k = 0; k + 1 < segs.size(); ++k) {
+    int small[16];
+    std::vector<int> big;
+    int *segs = small;
+    const size_t n = m.proper.size();
+    if (n > 16) { big.assign(m.proper.begin(), m.proper.end()); segs = big.data(); }
+    else std::copy(m.proper.begin(), m.proper.end(), small);
+    for (size_t i = 1; i < n; ++i) {            // stable insertion sort by query start
+        const int v = segs[i];
+        size_t j = i;
+        while (j > 0 && m.recs[segs[j - 1]].astart > m.recs[v].astart) { segs[j] = segs[j - 1]; --j; }
+        segs[j] = v;
+    }
+    for (size_t k = 0; k + 1 < n; ++k) {
         const Rec &a = m.recs[segs[k]], &b = m.recs[segs[k + 1]];
         if (a.qlen < asize || b.qlen < asize) { ev.too_short++; continue; }
         if (b.pos - a.aend < 0) ev.n_circ++; else ev.n_lin++;
@@ -560,8 +761,22 @@ extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
     h->bam = is_bam != 0;
     h->buf.resize(1 << 22);
     if (h->bam) {
-        if (inflateInit2(&h->zs, 15 + 32) != Z_OK) { close(fd); delete h; return fc2::fail(FC2_E_IO, "zlib init"); }
-        h->z_init = true;
+        // BGZF? (peek the first header; the bytes go to the first batch or to the zlib stream)
+        std::vector<uint8_t> pre(18);
+        size_t got = 0;
+        if (!read_full(fd, pre.data(), 18, got)) { close(fd); delete h; return fc2::fail(FC2_E_IO, "read error"); }
+        pre.resize(got);
+        if (got == 18 && pre[0] == 0x1f && pre[1] == 0x8b && (pre[3] & 4) && pre[12] == 'B' && pre[13] == 'C') {
+            h->bgzf = true;
+            h->bgzf_nt = bgzf_threads();
+            h->bgzf_next = std::async(std::launch::async, bgzf_batch, fd, std::move(pre), 16, h->bgzf_nt);
+        } else {
+            if (inflateInit2(&h->zs, 15 + 32) != Z_OK) { close(fd); delete h; return fc2::fail(FC2_E_IO, "zlib init"); }
+            h->z_init = true;
+            h->zin.assign(pre.begin(), pre.end());
+            h->zs.next_in = (Bytef *)h->zin.data();
+            h->zs.avail_in = (uInt)h->zin.size();
+        }
     }
     int rc = read_header(h);
     if (rc) { fc2_ingest_close(h); return rc; }
@@ -571,6 +786,7 @@ extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
 
 extern "C" void fc2_ingest_close(fc2_ingest *h) {
     if (!h) return;
+    if (h->bgzf_next.valid()) h->bgzf_next.wait();     // the batch reader uses the fd
     if (h->z_init) inflateEnd(&h->zs);
     if (h->fd >= 0) close(h->fd);
     delete h;
@@ -588,8 +804,16 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
     uint64_t handed = 0, frags = 0;
     int rc = FC2_OK;
     bool done = h->finished;
+    Rec r;
+    bool moved = true;               // r was handed to a mate: take a recycled one
     while (!done && frags < max_frags) {
-        Rec r;
+        if (moved) {
+            if (!h->pool.empty()) {
+                r = std::move(h->pool.back());
+                h->pool.pop_back();
+            }
+            moved = false;
+        }
         if (!next_record(h, r, rc)) {
             if (rc) return rc;
             // end of input: the final yield (:1486)
@@ -608,23 +832,27 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
         h->counts.records++;
         if (!h->started) {           // first record always opens a mate (:1462-1463)
             open_mate(h, h->current, std::move(r));
+            moved = true;
             h->started = true;
             continue;
         }
-        if (r.unmapped()) { h->counts.unmapped_reads++; continue; }
+        if (r.unmapped()) { h->counts.unmapped_reads++; continue; }   // r is reused
         const Rec &prim = h->current.recs[0];
         if (r.read1() == prim.read1() && r.qname == prim.qname) {
             add_segment(h->current, std::move(r));
+            moved = true;
         } else if (r.read1() != prim.read1() && r.qname == prim.qname) {
             std::swap(h->other, h->current);
             h->have_other = true;
             open_mate(h, h->current, std::move(r));
+            moved = true;
         } else {
             rc = emit_or_count(h, p, handed, sink);
             ++frags;
             h->have_other = false;
-            h->other = Mate();
+            recycle(h, h->other);
             open_mate(h, h->current, std::move(r));
+            moved = true;
             if (rc) return rc;
         }
     }

@@ -56,8 +56,25 @@ _SEQ_CODE = {c: i for i, c in enumerate("=ACMGRSVTWYHKDBN")}
 _OPS = {c: i for i, c in enumerate("MIDNSHP=X")}
 
 
-def sam_to_bam(sam: str, path: str):
-    """Minimal BAM writer (one BGZF-compatible gzip member; readers use gzip)."""
+def bgzf_compress(data: bytes, block: int = 65280, level: int = 6) -> bytes:
+    """BGZF (SAM/BAM spec 4.1): gzip members of <= 64 KiB, compressed size in a 'BC' extra
+    field, followed by the 28-byte empty EOF block."""
+    import zlib
+    out = bytearray()
+    for k in range(0, len(data), block):
+        chunk = data[k:k + block]
+        co = zlib.compressobj(level, zlib.DEFLATED, -15)
+        cdata = co.compress(chunk) + co.flush()
+        bsize = 18 + len(cdata) + 8
+        out += b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + struct.pack("<H", bsize - 1)
+        out += cdata + struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk))
+    out += bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    return bytes(out)
+
+
+def sam_to_bam(sam: str, path: str, bgzf: bool = True):
+    """Minimal BAM writer: BGZF blocks (as samtools writes them) or, with ``bgzf=False``,
+    one plain gzip member (some tools do; readers must accept both)."""
     import re
     refs, recs = [], []
     for line in sam.splitlines():
@@ -94,5 +111,9 @@ def sam_to_bam(sam: str, path: str):
                            int(f[1]), len(seq), -1, -1, 0)
         body += qn + b"".join(struct.pack("<I", (n << 4) | op) for n, op in cig) + bytes(sb) + qual + bytes(aux)
         out += struct.pack("<i", len(body)) + body
-    with gzip.open(path, "wb") as fh:
-        fh.write(bytes(out))
+    if bgzf:
+        with open(path, "wb") as fh:
+            fh.write(bgzf_compress(bytes(out)))
+    else:
+        with gzip.open(path, "wb") as fh:
+            fh.write(bytes(out))

@@ -309,3 +309,34 @@ def test_native_caller_secondary_without_seq_fails_like_python(tmp_path):
     rcs, outs = _three(tmp_path, fa, sam, [])
     assert rcs == [1, 1, 1]
     assert "TypeError: object of type 'NoneType' has no len()" in open(os.path.join(outs[2], "run.log")).read()
+
+
+@pytest.mark.parametrize("threads", ["1", "3"])
+def test_bam_plain_gzip_and_bgzf_agree(tmp_path, mixed, threads, monkeypatch):
+    """BGZF blocks are inflated in parallel batches (FC2_INGEST_THREADS); a BAM written as one
+    plain gzip member takes the streaming path.  Both give the SAM run's files."""
+    fa, sam, bam = mixed
+    plain = str(tmp_path / "plain.bam")
+    sam_to_bam(open(sam).read(), plain, bgzf=False)
+    monkeypatch.setenv("FC2_INGEST_THREADS", threads)
+    outs = []
+    for tag, inp in (("sam", sam), ("bgzf", bam), ("plain", plain)):
+        out = str(tmp_path / tag)
+        assert cli.main(["-G", fa, "-o", out, "-q", "--all-hits", inp], evaluator_factory=oracle_evaluator_factory) == 0
+        outs.append(out)
+    same(outs[0], outs[1])
+    same(outs[0], outs[2])
+
+
+def test_corrupt_bgzf_block_fails(tmp_path, mixed):
+    fa, sam, bam = mixed
+    data = bytearray(open(bam, "rb").read())
+    data[len(data) // 2] ^= 0xFF                   # inside some block's deflate data
+    bad = str(tmp_path / "bad.bam")
+    open(bad, "wb").write(bytes(data))
+    out = str(tmp_path / "o")
+    # small input: the first batch of blocks holds the BAM header too, so opening fails
+    # (an uncaught exception, as pysam's would be, find_circ.py:461-469)
+    from find_circ2_amd._native import Fc2Error
+    with pytest.raises(Fc2Error, match="corrupt BGZF block"):
+        cli.main(["-G", fa, "-o", out, "-q", bad], evaluator_factory=oracle_evaluator_factory)
