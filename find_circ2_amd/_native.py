@@ -107,7 +107,7 @@ EXPORTED = [
     "fc2_reorder_plan", "fc2_reorder_launch",
     # include/fc2_ingest.h
     "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
-    "fc2_ingest_next", "fc2_ingest_counts_get",
+    "fc2_ingest_next", "fc2_ingest_counts_get", "fc2_ingest_set_bam_out", "fc2_ingest_close_bam_out",
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
     "fc2_caller_submit", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
@@ -147,6 +147,7 @@ def build(force: bool = False) -> str:
     srcdir = os.path.join(_HERE, "csrc")
     srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_reorder.hip", "fc2_scan32.h",
                                               "fc2_host.cpp", "fc2_ingest.cpp", "fc2_ingest_impl.h", "fc2_caller.cpp",
+                                              "fc2_bamout.cpp", "fc2_bamout.h",
                                               "fc2_common.h", "Makefile")]
     srcs += [os.path.join(os.path.dirname(_HERE), "include", h) for h in ("fc2_bp.h", "fc2_ingest.h", "fc2_caller.h")]
     newest = max(os.path.getmtime(s) for s in srcs)
@@ -204,6 +205,8 @@ def lib() -> ctypes.CDLL:
         "fc2_ingest_next": (ctypes.c_int, [vp, P(IngestParams), u64, P(IngestCounts), P(ctypes.c_void_p), P(u64),
                                            P(u64), P(ctypes.c_int)]),
         "fc2_ingest_counts_get": (ctypes.c_int, [vp, P(IngestCounts)]),
+        "fc2_ingest_set_bam_out": (ctypes.c_int, [vp, ctypes.c_char_p]),
+        "fc2_ingest_close_bam_out": (ctypes.c_int, [vp]),
         "fc2_caller_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(CallerOpts), P(vp)]),
         "fc2_caller_set_genome": (ctypes.c_int, [vp, vp, i32, vp, P(u64), P(u64)]),
         "fc2_caller_ingest": (vp, [vp]),

@@ -7,8 +7,8 @@
 Same options (find_circ.py:383-413), output directory layout and file formats
 (circ_splice_sites.bed, lin_splice_sites.bed, spliced_reads.fastq.gz,
 multi_events.tsv, test_results.tsv, run.log; find_circ.py:420-458).
-Unsupported: ``-S/--system`` (needs the absent ``byo`` library) and ``-B/--bam``
-(needs a BAM writer; spliced alignments are not written).  ``--stranded`` fails
+Unsupported: ``-S/--system`` (needs the absent ``byo`` library).  ``-B/--bam``
+writes spliced_alignments.bam through the native ingest (not with ``--python-ingest``).  ``--stranded`` fails
 exactly like the reference (AttributeError in Hit.add, find_circ.py:532-533).
 """
 from __future__ import annotations
@@ -60,7 +60,7 @@ def build_parser() -> optparse.OptionParser:
     a("", "--half-unique", dest="halfunique", default=False, action="store_true", help="one unique anchor suffices")
     a("", "--report-nobridges", dest="report_nobridges", default=False, action="store_true",
       help="also report junctions lacking a uniquely bridged read")
-    a("-B", "--bam", dest="bam", default=False, action="store_true", help="store anchor alignments (unsupported)")
+    a("-B", "--bam", dest="bam", default=False, action="store_true", help="store anchor alignments in spliced_alignments.bam")
     a("-t", "--throughput", dest="throughput", default=False, action="store_true", help="print throughput to stderr")
     a("", "--chunk-size", dest="chunksize", type=int, default=100000, help="reads per chunk (default=100000)")
     a("", "--noop", dest="noop", default=False, action="store_true", help="only process the alignment stream")
@@ -117,6 +117,10 @@ def main(argv=None, evaluator_factory=None) -> int:
     if not options.genome:
         print("need to specify either model system database (-S) or genome FASTA file (-G).")
         return 1
+    if options.bam and options.python_ingest:
+        sys.stderr.write("-B/--bam needs the native ingest (drop --python-ingest)\n")
+        return 1
+    bam_path = os.path.join(options.output, "spliced_alignments.bam") if options.bam else ""
 
     from .caller import Caller, CallerOptions
     from .hotpath import Options as HPOptions
@@ -153,13 +157,15 @@ def main(argv=None, evaluator_factory=None) -> int:
     is_bam = bool(args) and not args[0].endswith("sam")          # find_circ.py:461-469
     logger.info('reading from {0}'.format(args[0]) if args else 'reading from stdin')
     if not (options.python_ingest or options.python_caller):
-        return _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome)
+        return _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path)
     if options.python_ingest:
         sam = AlignmentFile(path, "rb" if is_bam else "r")
         run = lambda: caller.run(sam)                              # noqa: E731
     else:
         from .ingest import NativeIngest
         sam = NativeIngest(path, is_bam)
+        if bam_path:
+            sam.set_bam_out(bam_path)
         run = lambda: caller.run_native(sam)                       # noqa: E731
 
     cache = {}
@@ -194,6 +200,8 @@ def main(argv=None, evaluator_factory=None) -> int:
         logging.error(exc)
         sys.stderr.write(exc)
         return 1
+    if bam_path:
+        sam.close_bam_out()
     _finish(options, seconds, caller.n_reads, logger, caller.N, caller.n_spans_evaluated, caller.gpu_seconds)
     caller.circ_splices.store(out["circs"])
     caller.linear_splices.store(out["lins"])
@@ -218,7 +226,7 @@ def _finish(options, seconds, n_reads, logger, counters, n_spans, eval_seconds):
     logger.info('breakpoint search: {0} spans, {1:.3f} s incl. pack/transfer/decode'.format(n_spans, eval_seconds))
 
 
-def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome) -> int:
+def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path="") -> int:
     """The read loop in C++ (include/fc2_caller.h); only the breakpoint search is called from here."""
     from .caller import BED_HEADER, MULTI_HEADER
     from .native_caller import NativeCaller, gpu_batch_evaluator
@@ -231,7 +239,7 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
         evaluate, names, fasta, dummy = engine(options, hp)
     nc = NativeCaller(path, is_bam, options, names, fasta, write_reads=out.get("reads") is not None,
                       write_multi=out.get("multi") is not None, genome_dummy=dummy,
-                      known_circ=options.known_circ, known_lin=options.known_lin)
+                      known_circ=options.known_circ, known_lin=options.known_lin, bam_out=bam_path)
     try:
         n_kc, n_kl = nc.open()
         for n, p in ((n_kc, options.known_circ), (n_kl, options.known_lin)):
@@ -258,6 +266,7 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             logging.error(exc)
             sys.stderr.write(exc)
             return 1
+        nc.close_bam_out()
         _finish(options, seconds, n_reads, logger, nc.counters(), n_pairs, eval_s)
         for kind, key in ((0, "circs"), (1, "lins")):
             out[key].write(BED_HEADER)

@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/fc2_ingest.h"
+#include "fc2_bamout.h"
 #include "fc2_common.h"
 #include "fc2_ingest_impl.h"
 
@@ -213,7 +214,12 @@ struct fc2_ingest {
     // header
     std::string header;
     std::vector<std::string> refs;
+    std::vector<int64_t> ref_len;
     std::unordered_map<std::string, int> tid_of;
+    // -B/--bam: anchor alignments of every processed mate (find_circ.py:1134-1140)
+    fc2::bam::Writer *bam_out = nullptr;
+    bool bam_stopped = false;    // the reference raised inside process_mate: nothing after it is written
+    std::string bam_err;
     // grouping state
     bool started = false;
     Mate current, other;
@@ -380,7 +386,7 @@ int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r) {
         const char *t = (const char *)memchr(f[k], '\t', (size_t)(le - f[k]));
         return t ? t : le;
     };
-    if (h->need_text) r.text.assign(ls, le);
+    if (h->need_text || h->bam_out) r.text.assign(ls, le);
     r.qname.assign(fb(0), fe(0));
     r.flag = (uint32_t)to_i64(fb(1), fe(1));
     const char *rb = fb(2), *re = fe(2);
@@ -519,6 +525,7 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
         return fc2::fail(FC2_E_FORMAT, "truncated BAM record" + (h->z_err.empty() ? "" : " (" + h->z_err + ")"));
     const uint8_t *b = (const uint8_t *)h->buf.data() + h->beg + 4;
     const uint8_t *e = b + bs;
+    if (h->bam_out) r.raw.assign((const char *)b - 4, 4 + (size_t)bs);
     int32_t ref_id, pos, l_seq, nref, npos, tlen;
     uint8_t l_name, mapq;
     uint16_t bin, n_cig, flag;
@@ -607,6 +614,8 @@ int read_header(fc2_ingest *h) {
                     std::string name = line.substr(p + 4, e == std::string::npos ? std::string::npos : e - p - 4);
                     h->tid_of[name] = (int)h->refs.size();
                     h->refs.push_back(name);
+                    size_t q = line.find("\tLN:");
+                    h->ref_len.push_back(q == std::string::npos ? 0 : strtoll(line.c_str() + q + 4, nullptr, 10));
                 }
             }
         }
@@ -629,6 +638,9 @@ int read_header(fc2_ingest *h) {
         memcpy(&ln, h->buf.data() + h->beg, 4);
         if (!ensure(h, 4 + (size_t)ln + 4)) return fc2::fail(FC2_E_FORMAT, "truncated BAM refs");
         std::string name(h->buf.data() + h->beg + 4, ln > 0 ? (size_t)ln - 1 : 0);
+        int32_t lref;
+        memcpy(&lref, h->buf.data() + h->beg + 4 + ln, 4);
+        h->ref_len.push_back(lref);
         h->beg += 4 + (size_t)ln + 4;
         h->tid_of[name] = (int)h->refs.size();
         h->refs.push_back(name);
@@ -714,10 +726,44 @@ MateEval eval_mate(const Mate &m, int asize) {
     return ev;
 }
 
+// -B: what adjacent_segment_pairs writes while process_mate consumes it (find_circ.py:1134-1140):
+// seg_a of every pair that passes the anchor-length filter, then the last pair's seg_b.  A mate
+// on which the reference raises (len(None) at :1101 / :1497, A.aend None at :851) stops all
+// writing: the run ends there.
+int write_anchors(fc2_ingest *h, const Mate &m, int asize) {
+    if (m.proper.size() < 2) return FC2_OK;
+    const Rec &prim = m.recs[0];
+    if (!prim.has_seq) { h->bam_stopped = true; return FC2_OK; }
+    for (int k : m.proper)
+        if (m.recs[k].qlen < 0) { h->bam_stopped = true; return FC2_OK; }
+    std::vector<int> segs(m.proper.begin(), m.proper.end());
+    std::stable_sort(segs.begin(), segs.end(), [&](int a, int b) { return m.recs[a].astart < m.recs[b].astart; });
+    auto put = [&](const Rec &r) {
+        bool ok;
+        if (h->bam) ok = fc2::bam::write_raw(h->bam_out, (const uint8_t *)r.raw.data(), r.raw.size());
+        else ok = fc2::bam::write_sam(h->bam_out, r.text.data(), r.text.data() + r.text.size(), h->tid_of, h->bam_err);
+        if (!ok) return fc2::fail(FC2_E_IO, h->bam_err.empty() ? "IOError: writing spliced_alignments.bam" : h->bam_err);
+        return (int)FC2_OK;
+    };
+    for (size_t k = 0; k + 1 < segs.size(); ++k) {
+        const Rec &a = m.recs[segs[k]], &b = m.recs[segs[k + 1]];
+        if (a.qlen < asize || b.qlen < asize) continue;
+        if (int rc = put(a)) return rc;
+        if (a.aend < 0) { h->bam_stopped = true; return FC2_OK; }
+    }
+    return put(m.recs[segs.back()]);
+}
+
 int emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed,
                   const fc2::ing::FragSink *sink) {
     h->counts.n_reads++;
     if (p->noop) return FC2_OK;
+    if (h->bam_out) {
+        const Mate *order[2] = {h->have_other ? &h->other : nullptr, &h->current};
+        for (const Mate *m : order)
+            if (m && !h->bam_stopped)
+                if (int rc = write_anchors(h, *m, p->asize)) return rc;
+    }
     const Mate *mates[2] = {h->have_other ? &h->other : nullptr, &h->current};
     MateEval ev[2];
     int circ = 0, lin = 0;
@@ -784,8 +830,28 @@ extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
     return FC2_OK;
 }
 
+extern "C" int fc2_ingest_set_bam_out(fc2_ingest *h, const char *path) {
+    if (!h || !path) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_bam_out: null argument");
+    if (h->bam_out || h->n_records) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_bam_out: call once, before reading");
+    std::string err;
+    h->bam_out = fc2::bam::open_writer(path, h->header, h->refs, h->ref_len, err);
+    return h->bam_out ? FC2_OK : fc2::fail(FC2_E_IO, err);
+}
+
+extern "C" int fc2_ingest_close_bam_out(fc2_ingest *h) {
+    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_ingest_close_bam_out: null argument");
+    std::string err;
+    const bool ok = fc2::bam::close_writer(h->bam_out, err);
+    h->bam_out = nullptr;
+    return ok ? FC2_OK : fc2::fail(FC2_E_IO, err);
+}
+
 extern "C" void fc2_ingest_close(fc2_ingest *h) {
     if (!h) return;
+    if (h->bam_out) {
+        std::string err;
+        fc2::bam::close_writer(h->bam_out, err);
+    }
     if (h->bgzf_next.valid()) h->bgzf_next.wait();     // the batch reader uses the fd
     if (h->z_init) inflateEnd(&h->zs);
     if (h->fd >= 0) close(h->fd);

@@ -14,7 +14,8 @@ namespace fc2 {
 namespace ing {
 
 struct Rec {
-    std::string text;      // SAM line (no newline)
+    std::string text;      // SAM line (no newline): for the Python hand-back and the -B writer
+    std::string raw;       // BAM input with a -B writer: block_size + record bytes
     std::string qname;
     uint32_t flag = 0;
     int32_t tid = -1;

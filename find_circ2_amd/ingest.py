@@ -42,6 +42,13 @@ class NativeIngest:
                 frags.append([parse_sam_line(l, self.tid_of) for l in block.split("\n") if l])
         return frags
 
+    def set_bam_out(self, path: str):
+        """-B/--bam: anchor alignments to ``path`` (include/fc2_ingest.h)."""
+        N.check(N.lib().fc2_ingest_set_bam_out(self.h, path.encode()))
+
+    def close_bam_out(self):
+        N.check(N.lib().fc2_ingest_close_bam_out(self.h))
+
     def close(self):
         if self.h:
             N.lib().fc2_ingest_close(self.h)

@@ -78,7 +78,8 @@ class NativeCaller:
     """One pass over an alignment file (path or '-') with the native read loop."""
 
     def __init__(self, path: str, is_bam: bool, copts, genome_names, fasta_handle=None, write_reads=True,
-                 write_multi=True, genome_dummy=False, known_circ: str = "", known_lin: str = ""):
+                 write_multi=True, genome_dummy=False, known_circ: str = "", known_lin: str = "",
+                 bam_out: str = ""):
         o = copts
         # the strings must outlive the handle's open call (fc2_caller_open copies them)
         self._keep = [o.name.encode(), known_circ.encode() if known_circ else None,
@@ -95,6 +96,7 @@ class NativeCaller:
         self.fasta_handle = fasta_handle
         self._path = path
         self._is_bam = is_bam
+        self.bam_out = bam_out
         self.opened = False
 
     def open(self):
@@ -106,6 +108,8 @@ class NativeCaller:
                                   ctypes.byref(self.h)))
         self.opened = True
         ing = L.fc2_caller_ingest(self.h)
+        if self.bam_out:
+            N.check(L.fc2_ingest_set_bam_out(ing, self.bam_out.encode()))
         n_ref = L.fc2_ingest_n_refs(ing)
         self.refs = [L.fc2_ingest_ref_name(ing, t).decode("latin-1") for t in range(n_ref)]
         index = {nm: k for k, nm in enumerate(self.genome_names)}
@@ -118,6 +122,11 @@ class NativeCaller:
         _check(L.fc2_caller_set_genome(self.h, t2c.ctypes.data, n_ref, self.fasta_handle, ctypes.byref(nkc),
                                        ctypes.byref(nkl)))
         return int(nkc.value), int(nkl.value)
+
+    def close_bam_out(self):
+        """Finish spliced_alignments.bam (EOF block); raises on a write error."""
+        if self.bam_out:
+            N.check(N.lib().fc2_ingest_close_bam_out(N.lib().fc2_caller_ingest(self.h)))
 
     def stats(self):
         nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()

@@ -59,6 +59,15 @@ int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frag
 
 /* Counters so far (also returned by fc2_ingest_next). */
 int fc2_ingest_counts_get(const fc2_ingest *h, fc2_ingest_counts *counts);
+
+/* -B/--bam (replaces pysam.Samfile(spliced_alignments.bam, 'wb', template=sam_input) and
+ * bam_out.write(seg) in adjacent_segment_pairs, find_circ.py:479-483, 1134-1140): every
+ * processed mate's anchor alignments go to a BGZF BAM with the input's header, in the
+ * reference's order.  BAM input records are copied byte for byte; SAM lines are encoded as
+ * htslib's sam_parse1 does.  Call once, before the first fc2_ingest_next; the file is
+ * finished (EOF block) by fc2_ingest_close_bam_out or fc2_ingest_close. */
+int fc2_ingest_set_bam_out(fc2_ingest *h, const char *path);
+int fc2_ingest_close_bam_out(fc2_ingest *h);
 #ifdef __cplusplus
 }
 #endif
