@@ -340,3 +340,23 @@ def test_corrupt_bgzf_block_fails(tmp_path, mixed):
     from find_circ2_amd._native import Fc2Error
     with pytest.raises(Fc2Error, match="corrupt BGZF block"):
         cli.main(["-G", fa, "-o", out, "-q", bad], evaluator_factory=oracle_evaluator_factory)
+
+
+def test_native_caller_reads_stdin(tmp_path, mixed):
+    """No input argument: SAM text from stdin (find_circ.py:461-469), as from `bwa mem | find_circ`."""
+    import subprocess
+    import sys
+    fa, sam, _ = mixed
+    here = os.path.dirname(os.path.abspath(__file__))
+    out1, out2 = str(tmp_path / "file"), str(tmp_path / "stdin")
+    assert cli.main(["-G", fa, "-o", out1, "-q", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "from oracle_engine import oracle_evaluator_factory\n"
+            "from find_circ2_amd import cli\n"
+            "sys.exit(cli.main(['-G', %r, '-o', %r, '-q'], evaluator_factory=oracle_evaluator_factory))"
+            % (here, os.path.dirname(here), fa, out2))
+    with open(sam, "rb") as fh:
+        r = subprocess.run([sys.executable, "-c", code], stdin=fh, capture_output=True, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    same(out1, out2)
+    assert "reading from stdin" in open(os.path.join(out2, "run.log")).read()
