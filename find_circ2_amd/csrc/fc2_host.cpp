@@ -85,6 +85,19 @@ static inline int bclass(uint8_t c) {
     }
 }
 
+// pack code of a byte: bits 0-1 = ACGT code, bit 2 = N plane (N or exotic), bit 3 = exotic
+struct PackTable {
+    uint8_t t[256];
+    PackTable() {
+        for (int c = 0; c < 256; ++c) {
+            const int cl = bclass((uint8_t)c);
+            t[c] = (uint8_t)(cl < 4 ? cl : cl == 4 ? 4 : 4 | 8);
+        }
+    }
+};
+static const PackTable kPackTable;
+static inline uint32_t pack_code(uint8_t c) { return kPackTable.t[c]; }
+
 static inline bool py_isspace(uint8_t c) {
     return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
 }
@@ -520,20 +533,32 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
                     uint64_t lo = 0, hi = 0, nn = 0;
                     const int64_t p0 = (int64_t)u * 64;
                     const int64_t p1 = std::min<int64_t>(p0 + 64, r.size);
-                    int64_t line = p0 / r.ldata, col = p0 % r.ldata;
-                    int64_t off = r.ofs + line * (r.ldata + r.skip) + col;
-                    for (int64_t p = p0; p < p1; ++p) {
-                        const int b = (int)(p - p0);
-                        const int cl = bclass(f->data[off]);
-                        if (cl < 4) {
-                            lo |= (uint64_t)(cl & 1) << b;
-                            hi |= (uint64_t)((cl >> 1) & 1) << b;
-                        } else {
-                            nn |= 1ull << b;
-                            if (cl == 5) exo[k].push_back(r.gstart + (uint64_t)p);
+                    int64_t col = p0 % r.ldata;
+                    const uint8_t *src = f->data + r.ofs + (p0 / r.ldata) * (r.ldata + r.skip) + col;
+                    uint32_t exotic = 0;
+                    // line segments of the unit: table lookups, no branches per base
+                    for (int b = 0; b < (int)(p1 - p0);) {
+                        const int seg = (int)std::min<int64_t>(r.ldata - col, (p1 - p0) - b);
+                        for (int j = 0; j < seg; ++j) {
+                            const uint32_t c = pack_code(src[j]);
+                            lo |= (uint64_t)(c & 1u) << (b + j);
+                            hi |= (uint64_t)((c >> 1) & 1u) << (b + j);
+                            nn |= (uint64_t)((c >> 2) & 1u) << (b + j);
+                            exotic |= c >> 3;
                         }
-                        ++off;
-                        if (++col == r.ldata) { col = 0; off += r.skip; }
+                        b += seg;
+                        src += seg;
+                        col += seg;
+                        if (col == r.ldata) { col = 0; src += r.skip; }
+                    }
+                    if (exotic) {                 // rare: record the exotic positions
+                        int64_t off = r.ofs + (p0 / r.ldata) * (r.ldata + r.skip) + p0 % r.ldata;
+                        int64_t cl2 = p0 % r.ldata;
+                        for (int64_t p = p0; p < p1; ++p) {
+                            if (bclass(f->data[off]) == 5) exo[k].push_back(r.gstart + (uint64_t)p);
+                            ++off;
+                            if (++cl2 == r.ldata) { cl2 = 0; off += r.skip; }
+                        }
                     }
                     for (int b = (int)(p1 - p0); b < 64; ++b) nn |= 1ull << b;
                     units[2 * (gu0 + u)] = lo;
@@ -613,8 +638,9 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
                 }
                 // tight bit-sliced row: low bits at [0, l), high bits at [l, 2l)
                 for (int j = 0; j < l; ++j) {
-                    const int cl = bclass(I[j]);
-                    if (cl == 5) { bytepath = true; break; }
+                    const uint32_t pc = pack_code(I[j]);
+                    if (pc & 8u) { bytepath = true; break; }
+                    const int cl = (pc & 4u) ? 4 : (int)pc;
                     if (cl == 4) {
                         anyN = true;
                         read_nwords[(uint64_t)(j >> 6) * stride + i] |= 1ull << (j & 63);
