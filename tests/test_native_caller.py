@@ -360,3 +360,19 @@ def test_native_caller_reads_stdin(tmp_path, mixed):
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     same(out1, out2)
     assert "reading from stdin" in open(os.path.join(out2, "run.log")).read()
+
+
+@pytest.mark.parametrize("body", ["", "u1\t4\t*\t0\t0\t*\t*\t0\t0\tACGT\t####\nu2\t4\t*\t0\t0\t*\t*\t0\t0\tACGT\t####\n",
+                                  "\n\n"], ids=["header_only", "only_unmapped", "blank_lines"])
+def test_native_caller_degenerate_inputs(tmp_path, body):
+    """Header-only input (the reference's generator ends at the first next(), find_circ.py:1458),
+    unmapped-only input (the first record still opens a mate, :1462-1463) and blank lines."""
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    sam = str(tmp_path / "d.sam")
+    open(sam, "w").write("@SQ\tSN:testbed_plus\tLN:720\n" + body)
+    rcs, outs = _three(tmp_path, fa, sam, [])
+    assert rcs[0] == rcs[1] == rcs[2] == 0
+    same(outs[0], outs[1])
+    same(outs[0], outs[2])
+    rows = [l for l in open(os.path.join(outs[2], "circ_splice_sites.bed")) if not l.startswith("#")]
+    assert rows == []
