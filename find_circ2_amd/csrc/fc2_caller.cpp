@@ -7,7 +7,9 @@
 #include <string.h>
 
 #include <algorithm>
+#include <deque>
 #include <map>
+#include <memory>
 #include <set>
 #include <string>
 #include <tuple>
@@ -75,13 +77,18 @@ char comp(char c) {
     }
 }
 
-std::string rev_comp(const std::string &s) {
-    std::string r(s.size(), ' ');
+void rev_comp_into(const std::string &s, std::string &r) {
+    r.resize(s.size());
     for (size_t k = 0; k < s.size(); ++k) {
         const char c = comp(s[s.size() - 1 - k]);
         if (!c) throw Fatal{FC2_E_KEY, std::string("KeyError: ") + py_repr(std::string(1, s[s.size() - 1 - k]))};
         r[k] = c;
     }
+}
+
+std::string rev_comp(const std::string &s) {
+    std::string r;
+    rev_comp_into(s, r);
     return r;
 }
 
@@ -159,11 +166,30 @@ struct PyMin {
     std::string str() const { return is_bool ? (v ? "True" : "False") : i2s(v); }
 };
 
+// A set of strings of which only the size is read (Hit.readnames / Hit.uniq): a short vector
+// for the usual handful of members, a hash set past 16 (no per-hit hash table otherwise).
+struct StrSet {
+    std::vector<std::string> v;
+    std::unique_ptr<std::unordered_set<std::string>> big;
+    void insert(const std::string &s) {
+        if (big) { big->insert(s); return; }
+        for (const std::string &x : v)
+            if (x == s) return;
+        v.push_back(s);
+        if (v.size() > 16) {
+            big.reset(new std::unordered_set<std::string>(v.begin(), v.end()));
+            v.clear();
+            v.shrink_to_fit();
+        }
+    }
+    size_t size() const { return big ? big->size() : v.size(); }
+};
+
 struct Hit {                                   // Hit (:486-654)
     std::string name;
     Coord coord;
     int64_t n_reads = 0;
-    std::unordered_set<std::string> readnames, uniq;
+    StrSet readnames, uniq;
     bool has_mq = false;
     int64_t mq_a = 0, mq_b = 0;                // max of mapquals_A / _B
     double n_weighted = 0.;
@@ -196,7 +222,7 @@ struct fc2_caller {
     // aggregation
     struct Storage {
         std::string prefix;
-        std::vector<Hit> hits;                  // insertion (= dict) order
+        std::deque<Hit> hits;                   // insertion (= dict) order; never relocated
         std::unordered_map<std::string, size_t> index;
         int64_t novel = 0;
     } st[2];                                    // 0 circ, 1 lin
@@ -239,7 +265,8 @@ void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
 void hit_add_read(fc2_caller *h, Hit &t, const Span &s, const Align &prim) {
     t.readnames.insert(prim.qname);
     const std::string &read = prim.seq;
-    const std::string rc = rev_comp(read);
+    static thread_local std::string rc;
+    rev_comp_into(read, rc);
     t.n_reads += 1;
     (void)h;
     t.has_tissue = true;
@@ -258,18 +285,17 @@ Hit make_hit(fc2_caller *h, const std::string &name, const Splice &sp) {
 
 size_t storage_add(fc2_caller *h, int kind, const Splice &sp, const Align *prim) {
     auto &S = h->st[kind];
-    const std::string key = coord_key(sp.coord());
-    auto it = S.index.find(key);
-    size_t k;
-    if (it == S.index.end()) {
+    auto ins = S.index.try_emplace(coord_key(sp.coord()), S.hits.size());
+    const size_t k = ins.first->second;
+    if (ins.second) {                           // a new junction: named by first appearance (:684-686)
         S.novel += 1;
         char nm[64];
         snprintf(nm, sizeof nm, "_%s_%06lld", S.prefix.c_str(), (long long)S.novel);
-        S.hits.push_back(make_hit(h, h->name + nm, sp));
-        k = S.hits.size() - 1;
-        S.index[key] = k;
+        Hit &t = S.hits.emplace_back();
+        t.name = h->name + nm;
+        t.coord = sp.coord();
+        hit_add(h, t, sp);
     } else {
-        k = it->second;
         hit_add(h, S.hits[k], sp);
     }
     if (sp.span >= 0) hit_add_read(h, S.hits[k], h->spans[sp.span], *prim);
@@ -334,24 +360,39 @@ void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :69
             continue;
         }
         if (t.n_uniq_bridges == 0 && !o.report_nobridges) { incN(h, "no_uniq_bridges"); continue; }
-        std::vector<std::string> tissues, tiss_counts;
-        if (t.has_tissue) { tissues.push_back(h->name); tiss_counts.push_back(py2_float(t.tissue)); }
-        std::vector<std::string> flags, counts;
-        if (!t.flags.empty()) {
-            for (const auto &kv : t.flags) { flags.push_back(kv.first); counts.push_back(i2s(kv.second)); }
-        } else {
-            flags.push_back("N/A");
-            counts.push_back("0");
-        }
+        // the 22 columns of find_circ.py:712-730, appended in place
+        auto col = [&](const std::string &v) { outs += v; outs += '\t'; };
+        col(std::get<0>(t.coord));
+        col(i2s(std::get<1>(t.coord)));
+        col(i2s(std::get<2>(t.coord)));
+        col(t.name);
+        col(i2s((int64_t)t.readnames.size()));
+        col(std::get<3>(t.coord));
+        col(py2_float(t.n_weighted));
+        col(i2s(t.n_spanned));
+        col(i2s((int64_t)(t.uniq.size() / 2)));
+        col(py2_float(t.n_uniq_bridges));
+        col(i2s(qa));
+        col(i2s(qb));
+        col(t.has_tissue ? h->name : std::string());
+        col(t.has_tissue ? py2_float(t.tissue) : std::string());
+        col(t.edits.str());
+        col(t.overlaps.str());
+        col(t.n_hits.str());
+        col(t.signal);
+        col(t.strandmatch);
         std::vector<std::string> cats = categories(h, t);
         std::sort(cats.begin(), cats.end());
-        std::vector<std::string> cols = {
-            std::get<0>(t.coord), i2s(std::get<1>(t.coord)), i2s(std::get<2>(t.coord)), t.name,
-            i2s((int64_t)t.readnames.size()), std::get<3>(t.coord), py2_float(t.n_weighted), i2s(t.n_spanned),
-            i2s((int64_t)(t.uniq.size() / 2)), py2_float(t.n_uniq_bridges), i2s(qa), i2s(qb), join(tissues, ","),
-            join(tiss_counts, ","), t.edits.str(), t.overlaps.str(), t.n_hits.str(), t.signal, t.strandmatch,
-            join(cats, ","), join(flags, ","), join(counts, ",")};
-        outs += join(cols, "\t");
+        col(join(cats, ","));
+        if (!t.flags.empty()) {
+            bool first = true;
+            for (const auto &kv : t.flags) { if (!first) outs += ','; outs += kv.first; first = false; }
+            outs += '\t';
+            first = true;
+            for (const auto &kv : t.flags) { if (!first) outs += ','; outs += i2s(kv.second); first = false; }
+        } else {
+            outs += "N/A\t0";
+        }
         outs += '\n';
     }
 }
