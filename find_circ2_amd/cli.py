@@ -13,7 +13,6 @@ exactly like the reference (AttributeError in Hit.add, find_circ.py:532-533).
 """
 from __future__ import annotations
 
-import gzip
 import io
 import logging
 import optparse
@@ -123,16 +122,18 @@ def main(argv=None, evaluator_factory=None) -> int:
     bam_path = os.path.join(options.output, "spliced_alignments.bam") if options.bam else ""
 
     from .caller import Caller, CallerOptions
+    from .gzout import ParallelGzipWriter
     from .hotpath import Options as HPOptions
     from .samio import AlignmentFile
 
     out = {"circs": open(os.path.join(options.output, "circ_splice_sites.bed"), "w"),
            "lins": open(os.path.join(options.output, "lin_splice_sites.bed"), "w"),
-           "reads": gzip.open(os.path.join(options.output, "spliced_reads.fastq.gz"), "wt"),
+           "reads": ParallelGzipWriter(os.path.join(options.output, "spliced_reads.fastq.gz")),
            "multi": open(os.path.join(options.output, "multi_events.tsv"), "w"),
            "test": open(os.path.join(options.output, "test_results.tsv"), "w") if options.test else None}
     if options.stdout:
         out[options.stdout].write('# redirected to stdout\n')
+        out[options.stdout].close()
         logger.info('redirected {0} to stdout'.format(options.stdout))
         out[options.stdout] = sys.stdout
 

@@ -3,8 +3,8 @@
 Python read loop (--python-caller, same HIP scan) on an hg19-sized synthetic genome.
 
 Writes an hg19-shaped FASTA (93 contigs of tests/golden/test_norm.sam, 50-nt lines, N runs)
-with GT/AG planted at every simulated junction, and a bwa-mem-shaped SAM of single-end
-100-bp reads (unspliced, linear and backspliced, some 3-segment; mismatches; AS/XS), then
+with GT/AG (or CT/AC) planted at every simulated junction, and a bwa-mem-shaped SAM of
+single-end 100-bp reads (unspliced, linear and backspliced; mismatches; AS/XS), then
 runs both loops and requires byte-identical output files and identical run.log counters.
 Prints one JSON line with both wall times.
 
@@ -135,6 +135,9 @@ def main():
         rc = cli.main(["-G", fa, "-o", out, "-n", "scale", "-q"] + extra + [sam])
         res[tag + "_s"] = round(time.time() - t0, 2)
         res[tag + "_rc"] = rc
+        log = open(os.path.join(out, "run.log")).read().splitlines()
+        res[tag + "_log"] = [l.split("\t")[-1] for l in log if "processed" in l or "breakpoint search" in l
+                             or "reading from" in l]
         outs[tag] = out
         print("done", tag, res[tag + "_s"], file=sys.stderr, flush=True)
     same = True
