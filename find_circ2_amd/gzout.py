@@ -47,9 +47,10 @@ class ParallelGzipWriter(io.TextIOBase):
     def _submit(self):
         data = "".join(self._buf).encode(self._enc)
         self._buf, self._n = [], 0
-        self._pending.append(self._pool.submit(_member, data, self._level))
-        while len(self._pending) > self._max_pending:
-            self._f.write(self._pending.popleft().result())
+        for k in range(0, max(1, len(data)), self._piece):      # a large write becomes several members
+            self._pending.append(self._pool.submit(_member, data[k:k + self._piece], self._level))
+            while len(self._pending) > self._max_pending:
+                self._f.write(self._pending.popleft().result())
 
     def flush(self):
         pass            # pieces are written as they complete; close() writes the rest
