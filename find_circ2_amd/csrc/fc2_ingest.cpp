@@ -73,7 +73,18 @@ void finish_rec(Rec &r, const std::vector<std::pair<int, int>> &ops, int64_t seq
     CigarInfo c = cigar_info(ops);
     r.astart = c.astart;
     r.aend = (r.unmapped() || !c.any) ? -1 : r.pos + c.ref_span;
-    r.qlen = r.has_seq ? (int32_t)(seqlen - c.lead_s - c.trail_s) : -1;
+    // len(seq[lead_s : len(seq) - trail_s]) with Python slice semantics (pysam's query when the
+    // clips exceed SEQ: an empty string, or a negative end counted from the back)
+    if (r.has_seq) {
+        const int64_t n = seqlen;
+        int64_t b = c.lead_s, e = n - c.trail_s;
+        if (e < 0) e += n;
+        b = b > n ? n : b;
+        e = e < 0 ? 0 : (e > n ? n : e);
+        r.qlen = (int32_t)(e > b ? e - b : 0);
+    } else {
+        r.qlen = -1;
+    }
 }
 
 // ---- parallel BGZF ----------------------------------------------------------------------
@@ -721,6 +732,13 @@ MateEval eval_mate(const Mate &m, int asize) {
     for (size_t k = 0; k + 1 < n; ++k) {
         const Rec &a = m.recs[segs[k]], &b = m.recs[segs[k + 1]];
         if (a.qlen < asize || b.qlen < asize) { ev.too_short++; continue; }
+        // JunctionSpan.__init__ raises on these whether or not the span is ever evaluated
+        // (uniqness: AS missing or not an integer, :809-819): the caller must see the fragment
+        // even under --no-linear
+        if (!a.has_as || !b.has_as || !a.as_int || !b.as_int || (a.has_xs && !a.xs_int) || (b.has_xs && !b.xs_int)) {
+            ev.python_must_see = true;
+            return ev;
+        }
         if (b.pos - a.aend < 0) ev.n_circ++; else ev.n_lin++;
     }
     return ev;
