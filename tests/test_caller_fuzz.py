@@ -72,8 +72,8 @@ def _mutate(lines, rng, rate):
             f[9] = f[9].lower()
         if rng.random() < rate * 0.05:
             f[9] = "*"
-        if rng.random() < rate * 0.1:
-            f[10] = "*"
+        if rng.random() < rate * 0.1 or f[9] == "*":
+            f[10] = "*"                                                   # SEQ '*' needs QUAL '*' (SAM spec)
         if rng.random() < rate * 0.05:
             f[2] = "chrU"                                                 # in the header, not in the FASTA
         f[1] = str(flag)
@@ -153,3 +153,30 @@ def test_missing_as_raises_under_no_linear(tmp_path):
         "r2\t0\ttestbed_plus\t10\t60\t100M\t*\t0\t0\t%s\t*\tAS:i:100" % seq])
     rc, outs = _agree(tmp_path, fa, sam, ["--no-linear"])
     assert rc == 1 and _exc_type(outs[2]) == "KeyError"
+
+
+@pytest.mark.parametrize("seed", list(range(6)))
+def test_sam_and_bam_inputs_agree_on_mutated_input(tmp_path, seed):
+    """The same mutated records as SAM text, as BGZF / plain-gzip BAM (native reader) and as BAM
+    through the Python reader (reads upper-cased: BAM stores 4-bit bases)."""
+    from samgen import sam_to_bam
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, 300, seed=9000 + seed)
+    lines = open(sam0).read().splitlines()
+    hdr = [l for l in lines if l.startswith("@")] + ["@SQ\tSN:chrU\tLN:5000"]
+    rng = np.random.default_rng(seed)
+    body = _mutate([l for l in lines if not l.startswith("@")], rng, rate=[0.01, 0.05, 0.1][seed % 3])
+    body = ["\t".join(f[:9] + [f[9].upper()] + f[10:]) for f in (l.split("\t") for l in body)]
+    txt = "\n".join(hdr + body) + "\n"
+    sam, bam = str(tmp_path / "m.sam"), str(tmp_path / "m.bam")
+    open(sam, "w").write(txt)
+    sam_to_bam(txt, bam, bgzf=bool(seed % 2))
+    rcs, outs = [], []
+    for tag, inp, mode in (("sam", sam, []), ("bam", bam, []), ("pybam", bam, ["--python-ingest"])):
+        out = str(tmp_path / tag)
+        rcs.append(cli.main(["-G", fa, "-o", out, "-q"] + mode + [inp], evaluator_factory=oracle_evaluator_factory))
+        outs.append(out)
+    assert rcs[0] == rcs[1] == rcs[2], rcs
+    if rcs[0] == 0:
+        same(outs[0], outs[1])
+        same(outs[0], outs[2])
