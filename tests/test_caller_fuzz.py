@@ -40,7 +40,9 @@ def _mutate_cigar(cig, rng):
     return "".join("%d%s" % (n, o) for n, o in ops)
 
 
-def _mutate(lines, rng, rate):
+def _mutate(lines, rng, rate, fatal=True):
+    """fatal=False leaves out the mutations on which the reference raises (AS dropped,
+    SEQ '*', an RNAME outside the FASTA)."""
     out = []
     for l in lines:
         if l.startswith("@"):
@@ -61,7 +63,7 @@ def _mutate(lines, rng, rate):
             as_ = [int(t[5:]) for t in tags if t.startswith("AS:i:")]
             if as_:
                 tags = [t for t in tags if not t.startswith("XS:")] + ["XS:i:%d" % (as_[0] + int(rng.integers(-2, 5)))]
-        if rng.random() < rate * 0.1:
+        if fatal and rng.random() < rate * 0.1:
             tags = [t for t in tags if not t.startswith("AS:")]          # fatal when the segment is used
         if f[9] != "*" and rng.random() < rate:
             s = list(f[9])
@@ -70,11 +72,11 @@ def _mutate(lines, rng, rate):
             f[9] = "".join(s)
         if f[9] != "*" and rng.random() < rate * 0.5:
             f[9] = f[9].lower()
-        if rng.random() < rate * 0.05:
+        if fatal and rng.random() < rate * 0.05:
             f[9] = "*"
         if rng.random() < rate * 0.1 or f[9] == "*":
             f[10] = "*"                                                   # SEQ '*' needs QUAL '*' (SAM spec)
-        if rng.random() < rate * 0.05:
+        if fatal and rng.random() < rate * 0.05:
             f[2] = "chrU"                                                 # in the header, not in the FASTA
         f[1] = str(flag)
         out.append("\t".join(f[:11] + tags))

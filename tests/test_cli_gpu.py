@@ -76,3 +76,31 @@ def test_gpu_native_caller_equals_oracle_python_caller(tmp_path, extra):
     rc2 = cli.main(["-G", fa, "-o", o2, "-n", "mix", "-q"] + extra + [sam])
     assert rc1 == rc2 == 0
     same(o1, o2)
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_gpu_native_caller_on_mutated_input(tmp_path, seed):
+    """Fuzzed records (tests/test_caller_fuzz.py: N / IUPAC / lower-case read bytes, CIGAR
+    variants, flag bits, AS/XS changes) through the shipped CLI vs the Python loop + oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import numpy as np
+    from find_circ2_amd import cli
+    from oracle_engine import oracle_evaluator_factory
+    from test_caller_fuzz import _mutate
+    from test_ingest import same
+    from test_native_caller import _rich_sam
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, 600, seed=700 + seed)
+    lines = open(sam0).read().splitlines()
+    rng = np.random.default_rng(seed)
+    body = _mutate([l for l in lines if not l.startswith("@")], rng, rate=0.03, fatal=False)
+    sam = str(tmp_path / "m.sam")
+    open(sam, "w").write("\n".join([l for l in lines if l.startswith("@")] + body) + "\n")
+    extra = [[], ["--all-hits", "--non-canonical"]][seed % 2]
+    o1, o2 = str(tmp_path / "oracle_py"), str(tmp_path / "gpu_native")
+    rc1 = cli.main(["-G", fa, "-o", o1, "-q", "--python-caller"] + extra + [sam],
+                   evaluator_factory=oracle_evaluator_factory)
+    rc2 = cli.main(["-G", fa, "-o", o2, "-q"] + extra + [sam])
+    assert rc1 == rc2 == 0
+    same(o1, o2)
