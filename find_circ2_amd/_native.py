@@ -63,7 +63,8 @@ class GenomeView(ctypes.Structure):
                 ("chrom_start", ctypes.c_void_p), ("chrom_size", ctypes.c_void_p),
                 ("n_units", ctypes.c_uint64), ("n_chrom", ctypes.c_uint32), ("dummy", ctypes.c_uint32),
                 ("units_twin", ctypes.c_void_p), ("nsuper", ctypes.c_void_p), ("nsuper_shift", ctypes.c_uint32),
-                ("nsuper_words", ctypes.c_uint32)]
+                ("nsuper_words", ctypes.c_uint32), ("wt", ctypes.c_void_p), ("wt_bytes", ctypes.c_uint64),
+                ("wt_twin_off", ctypes.c_uint64)]
 
 
 class BatchView(ctypes.Structure):
@@ -96,13 +97,13 @@ class SynthCfg(ctypes.Structure):
 
 # every symbol include/fc2_bp.h declares (checked by tests/test_abi.py)
 EXPORTED = [
-    "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_set_tuning", "fc2_max_fast_l",
+    "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_set_tuning", "fc2_get_tuning", "fc2_max_fast_l",
     "fc2_batch_geometry",
     "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch",
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill",
-    "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_twin_launch",
+    "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_twin_launch", "fc2_wtab_geometry", "fc2_wtab_launch",
     "fc2_nsuper_geometry", "fc2_nsuper_launch", "fc2_synth_pairs_launch",
     "fc2_reorder_plan", "fc2_reorder_launch",
     # include/fc2_ingest.h
@@ -172,6 +173,7 @@ def lib() -> ctypes.CDLL:
         "fc2_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
         "fc2_max_fast_l": (ctypes.c_int, []),
         "fc2_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
+        "fc2_get_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
         "fc2_batch_geometry": (ctypes.c_int, [P(Params), i32, P(u32), P(u32), P(u32)]),
         "fc2_bp_scan_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp, u32, vp]),
         "fc2_bp_scan_bytes_launch": (ctypes.c_int, [P(Params), P(BytesView), vp, vp, u32, u64, vp]),
@@ -191,6 +193,8 @@ def lib() -> ctypes.CDLL:
         "fc2_synth_genome_launch": (ctypes.c_int, [u64, vp, vp, vp, u64, vp, vp, u32, vp]),
         "fc2_coarse_launch": (ctypes.c_int, [vp, vp, u64, vp]),
         "fc2_twin_launch": (ctypes.c_int, [vp, u64, vp, vp]),
+        "fc2_wtab_geometry": (ctypes.c_int, [u64, P(u64), P(u64)]),
+        "fc2_wtab_launch": (ctypes.c_int, [vp, u64, vp, vp]),
         "fc2_nsuper_geometry": (ctypes.c_int, [u64, P(u32), P(u32)]),
         "fc2_nsuper_launch": (ctypes.c_int, [vp, u64, vp, vp]),
         "fc2_synth_pairs_launch": (ctypes.c_int, [P(Params), P(SynthCfg), P(GenomeView), vp, u64, vp, vp, u32,
@@ -219,6 +223,8 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),
     }
     for name, (res, args) in sig.items():
+        if os.environ.get("FC2_LIB_VARIANT") and not hasattr(L, name):
+            continue              # an A/B build of an older revision may predate a symbol
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
@@ -226,6 +232,13 @@ def lib() -> ctypes.CDLL:
         raise ImportError("libfc2.so ABI mismatch")
     _lib = L
     return L
+
+
+def get_tuning(key: int) -> int:
+    """Current value of an FC2_TUNE_* knob (fc2_get_tuning)."""
+    v = ctypes.c_int(0)
+    check(lib().fc2_get_tuning(key, ctypes.byref(v)))
+    return v.value
 
 
 def check(rc: int) -> None:

@@ -736,6 +736,25 @@ __global__ void twin_kernel(const uint64_t *__restrict__ units, uint64_t n_units
     twin[w] = (w >= 8 && w - 8 < 2 * n_units) ? units[w - 8] : 0ull;
 }
 
+// Word-pair layout (fc2_genome_view.wt): pair q = (low, high) 32-bit code words of bases
+// [32q, 32q + 32), i.e. 32-bit halves of units[2u] / units[2u+1] with u = q >> 1.  The main copy holds
+// pair q at slot q + 16 (16 zero pairs in front, 16 behind), then (at twin_off) the copy with pair q at
+// slot q + 8.  Zero outside the genome.
+__device__ __forceinline__ uint64_t wt_pair(const uint64_t *__restrict__ units, uint64_t n_q, int64_t q) {
+    if (q < 0 || (uint64_t)q >= n_q) return 0ull;
+    const uint64_t u = (uint64_t)q >> 1;
+    const unsigned s = 32u * (unsigned)(q & 1);
+    return ((units[2 * u] >> s) & 0xFFFFFFFFull) | (((units[2 * u + 1] >> s) & 0xFFFFFFFFull) << 32);
+}
+
+__global__ void wtab_kernel(const uint64_t *__restrict__ units, uint64_t n_units, uint64_t *__restrict__ wt,
+                            uint64_t twin_pairs, uint64_t total_pairs) {
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= total_pairs) return;
+    const uint64_t n_q = 2 * n_units;
+    wt[j] = j < twin_pairs ? wt_pair(units, n_q, (int64_t)j - 16) : wt_pair(units, n_q, (int64_t)(j - twin_pairs) - 8);
+}
+
 // nsuper word w: bit b = OR of the coarse bits of blocks [(32w+b) << (shift-10), +1 << (shift-10))
 __global__ void nsuper_kernel(const uint32_t *__restrict__ ncoarse, uint64_t n_units, uint32_t shift, uint32_t words,
                               uint32_t *__restrict__ nsuper) {
@@ -763,6 +782,8 @@ int g_xcd_swizzle = 2; // XCD-contiguous block order in bp_scan32_kernel: 0 neve
 int g_extra_lds = 0;   // bytes of unused dynamic LDS per scan block (occupancy experiments)
 int g_stage = 2;       // bp_scan32 LDS staging: 0 never, 1 always, 2 read-order batch over a large genome
 int g_twin = 2;        // units_twin: 0 never, 1 always, 2 for batches not flagged locus-ordered
+int g_words = 1;       // read-order STAGE scan uses the word-pair layout when the view carries one
+int g_persist = 0;     // persistent STAGE kernel: 0 off, -1 occupancy-sized grid, k > 0 k blocks per CU
 inline bool stream_nt() { return g_stream_nt != 0; }
 
 }  // namespace
@@ -799,11 +820,17 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         // locus-ordered batches re-read their lines from L2: the twin only doubles the footprint there
         const bool ordered = (b->layout & FC2_BATCH_LOCUS_ORDERED) != 0;
         if (g_twin == 0 || (g_twin == 2 && ordered)) gv.units_twin = nullptr;
+        if (!g_words || !gv.wt || gv.wt_bytes == 0 || ml + 2 > 128) gv.wt = nullptr;
         // LDS staging pays where every L2 request counts: read-order batch over a genome far larger
         // than the caches (profiles/r01/ab_stage.jsonl)
         const bool big = !g->dummy && g->n_units * 16 >= (64ull << 20);
         const bool stage = g_stage == 2 ? (big && !ordered) : g_stage != 0;
         const int opts = sw ? fc2::kOptSwizzle : 0;
+        const int nq = (ml + 2 + 31) / 32;
+        if (stage && g_persist != 0 && fc2::persist_ok(nq, gv)) {
+            fc2::launch_scan32_persist(nt, s, *p, gv, *b, out, tiemask, tw, g_persist < 0 ? 0 : g_persist);
+            return hip_check(hipGetLastError(), "bp_scan32_persist_kernel launch");
+        }
         fc2::launch_scan32((ml + 2 + 31) / 32, nt, opts, stage, grid, s, *p, gv, *b, out, tiemask, tw,
                            (unsigned)g_extra_lds);
         return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
@@ -852,6 +879,27 @@ extern "C" int fc2_twin_launch(const uint64_t *units, uint64_t n_units, uint64_t
     hipLaunchKernelGGL(twin_kernel, dim3(grid_for(n_words, 256)), dim3(256), 0, (hipStream_t)stream, units, n_units,
                        units_twin);
     return hip_check(hipGetLastError(), "twin_kernel launch");
+}
+
+extern "C" int fc2_wtab_geometry(uint64_t n_units, uint64_t *bytes, uint64_t *twin_off) {
+    if (!bytes || !twin_off) return fc2::fail(FC2_E_PARAM, "fc2_wtab_geometry: null argument");
+    const uint64_t n_q = 2 * n_units;
+    const uint64_t main_bytes = ((n_q + 32) * 8 + 127) / 128 * 128;
+    const uint64_t total = main_bytes + ((n_q + 24) * 8 + 127) / 128 * 128;
+    if (total > 0xFFFFFF00ull) return fc2::fail(FC2_E_RANGE, "fc2_wtab_geometry: genome too large for 32-bit offsets");
+    *bytes = total;
+    *twin_off = main_bytes;
+    return FC2_OK;
+}
+
+extern "C" int fc2_wtab_launch(const uint64_t *units, uint64_t n_units, uint32_t *wt, void *stream) {
+    if (!units || !wt || n_units == 0) return fc2::fail(FC2_E_PARAM, "fc2_wtab_launch: bad args");
+    uint64_t bytes = 0, twin_off = 0;
+    const int rc = fc2_wtab_geometry(n_units, &bytes, &twin_off);
+    if (rc) return rc;
+    hipLaunchKernelGGL(wtab_kernel, dim3(grid_for(bytes / 8, 256)), dim3(256), 0, (hipStream_t)stream, units, n_units,
+                       reinterpret_cast<uint64_t *>(wt), twin_off / 8, bytes / 8);
+    return hip_check(hipGetLastError(), "wtab_kernel launch");
 }
 
 extern "C" int fc2_nsuper_geometry(uint64_t n_units, uint32_t *shift, uint32_t *words) {
@@ -917,10 +965,31 @@ extern "C" int fc2_set_tuning(int key, int value) {
         case FC2_TUNE_TWIN:
             if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: twin is 0, 1 or 2");
             g_twin = value; return FC2_OK;
+        case FC2_TUNE_WORDS: g_words = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_PERSIST:
+            if (value < -1 || value > 32) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: persist is -1..32");
+            g_persist = value; return FC2_OK;
         case FC2_TUNE_XCD_SWIZZLE:
             if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: swizzle is 0, 1 or 2");
             g_xcd_swizzle = value; return FC2_OK;
         default: return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: unknown key");
+    }
+}
+
+extern "C" int fc2_get_tuning(int key, int *value) {
+    if (!value) return fc2::fail(FC2_E_PARAM, "fc2_get_tuning: null value");
+    switch (key) {
+        case FC2_TUNE_STREAM_NT: *value = g_stream_nt; return FC2_OK;
+        case FC2_TUNE_KERNEL32: *value = g_kernel32; return FC2_OK;
+        case FC2_TUNE_XCD_SWIZZLE: *value = g_xcd_swizzle; return FC2_OK;
+        case FC2_TUNE_REORDER_ROUNDS: *value = fc2::g_reorder_rounds; return FC2_OK;
+        case FC2_TUNE_REORDER_NT: *value = fc2::g_reorder_nt; return FC2_OK;
+        case FC2_TUNE_TWIN: *value = g_twin; return FC2_OK;
+        case FC2_TUNE_STAGE: *value = g_stage; return FC2_OK;
+        case FC2_TUNE_EXTRA_LDS: *value = g_extra_lds; return FC2_OK;
+        case FC2_TUNE_PERSIST: *value = g_persist; return FC2_OK;
+        case FC2_TUNE_WORDS: *value = g_words; return FC2_OK;
+        default: return fc2::fail(FC2_E_PARAM, "fc2_get_tuning: unknown key");
     }
 }
 

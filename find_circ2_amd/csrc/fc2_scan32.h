@@ -13,4 +13,9 @@ constexpr int kOptSwizzle = 1;     // XCD-contiguous block order
 void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
                    const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
                    unsigned extra_lds = 0);   // occupancy experiments only (FC2_TUNE_EXTRA_LDS)
+// Persistent STAGE + cooperative form (grid = CUs x resident blocks); usable when persist_ok().
+bool persist_ok(int nq, const fc2_genome_view &g);
+void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+                           const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
+                           int blocks_per_cu);   // 0: the occupancy limit
 }  // namespace fc2

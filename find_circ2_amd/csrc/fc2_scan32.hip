@@ -14,6 +14,12 @@
 
 namespace {
 
+// Measurement-only ablations (scripts/ablate_build.sh; WRONG results, never in the shipped library):
+// bit 0 skips the owner's third-unit loads, bit 1 skips N-plane loads of flagged windows.
+#ifndef FC2_ABLATE
+#define FC2_ABLATE 0
+#endif
+
 constexpr int kBlock = 256;
 constexpr int kChromLds = 512;   // chromosome-table entries a block stages in LDS (8 KB)
 constexpr int kSuperLds = 2048;  // nsuper words a block stages in LDS (8 KB)
@@ -199,23 +205,49 @@ __device__ __forceinline__ void windows_issue_coop(const fc2_genome_view &g, con
     static_assert(NU == 3, "cooperative loads cover units 0 and 1; the owner loads unit 2");
     const uint32_t pk[2] = {window_geom<NQ>(g, cstart, wsA, W, rA), window_geom<NQ>(g, cstart, wsB, W, rB)};
     const int lane = (int)(threadIdx.x & 63);
+    const int64_t wsx[2] = {wsA, wsB};
+    // All LDS traffic of the issue phase in ONE batch ahead of the first global load: the four
+    // geometry permutes and both windows' two super-map words (read unconditionally, so no
+    // short-circuit branch waits on a first LDS read before issuing the second).
+    uint32_t src[2][2], sw[2][2] = {{0u, 0u}, {0u, 0u}};
+    uint32_t sb[2][2] = {{0u, 0u}, {0u, 0u}};
+    bool sv[2] = {false, false};
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
+    for (int x = 0; x < 2; ++x)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const uint32_t src = (uint32_t)__builtin_amdgcn_ds_bpermute((32 * c + (lane >> 1)) << 2, (int)pk[x]);
-            cl[x][c] = unit_load(g, src, lane & 1);
+        for (int c = 0; c < 2; ++c)
+            src[x][c] = (uint32_t)__builtin_amdgcn_ds_bpermute((32 * c + (lane >> 1)) << 2, (int)pk[x]);
+    if (!(FC2_ABLATE & 2) && s_nsuper) {
+        const int64_t top = (int64_t)(g.n_units * 64) - 1;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            int64_t lo = (int64_t)cstart + wsx[x], hi = lo + W - 1;
+            lo = lo < 0 ? 0 : lo;
+            hi = hi > top ? top : hi;
+            sv[x] = active && lo <= hi;
+            const uint64_t k0 = sv[x] ? (uint64_t)lo >> g.nsuper_shift : 0,
+                           k1 = sv[x] ? (uint64_t)hi >> g.nsuper_shift : 0;   // k1 <= k0 + 1
+            sw[x][0] = s_nsuper[k0 >> 5];
+            sw[x][1] = s_nsuper[k1 >> 5];
+            sb[x][0] = (uint32_t)(k0 & 31);
+            sb[x][1] = (uint32_t)(k1 & 31);
         }
     }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) cl[x][c] = unit_load(g, src[x][c], lane & 1);
     WinRaw<NQ> *R[2] = {&rA, &rB};
-    const int64_t wsx[2] = {wsA, wsB};
 #pragma unroll
     for (int x = 0; x < 2; ++x) {
         WinRaw<NQ> &Q = *R[x];
         Q.v[0] = Q.v[1] = Q.v[2] = ulonglong2{0ull, 0ull};
-        if (active && Q.jl >= 2) Q.v[2] = unit_load(g, pk[x], 2);
-        const int64_t g0 = (int64_t)cstart + wsx[x];
-        const bool nflag = active && s_nsuper && super_flag(s_nsuper, g.nsuper_shift, g0, W, g.n_units);
+        if (!(FC2_ABLATE & 1) && active && Q.jl >= 2) Q.v[2] = unit_load(g, pk[x], 2);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        WinRaw<NQ> &Q = *R[x];
+        const bool nflag = sv[x] && (((sw[x][0] >> sb[x][0]) | (sw[x][1] >> sb[x][1])) & 1u);
         const int64_t last = (int64_t)g.n_units - 1;
 #pragma unroll
         for (int j = 0; j < NU; ++j) {
@@ -327,6 +359,204 @@ __device__ __forceinline__ void window_finish(const fc2_genome_view &g, const ui
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Word-pair layout (g.wt, fc2_wtab_launch): the genome as 8-byte pairs (lo, hi) of 32-base code
+// words, followed in the same allocation by a copy shifted by half a 128-B line (64 B).  A window
+// of W <= 128 bases starting at base g0 needs the nwd = ceil(((g0 & 31) + W) / 32) <= 5 pairs from
+// q0 = g0 >> 5: ONE contiguous 32 B (nwd <= 4: every 100-bp pair) or 40 B run that lies inside one
+// line of either copy.  Both copies carry zero pairs in front (q0 >= -4 for any window the scan
+// evaluates), so no offset is negative.  Lanes 2m, 2m+1 load its two 16-B halves in one instruction (one L2 request,
+// like the cooperative unit loads); the owner adds the fifth pair only when nwd = 5.  Loads are
+// buffer loads with 32-bit offsets: the hardware range check returns 0 past the table, and windows
+// outside the chromosome are masked to 'N' in window_finish_w whatever was read, so no index is
+// clamped.  Compared with the 64-base unit layout there is no word-parity select, no third unit
+// request (17 % of 76-base windows) and no 64-bit address arithmetic.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+
+struct WinW {
+    uint32_t off;       // byte offset of the window's first pair in g.wt (either copy)
+    uint32_t q0;        // first 32-base word (two's complement when the window starts before base 0)
+    unsigned sh;        // g0 & 31
+    int nwd;            // word pairs needed, 1..5
+    u32x4 v0, v1;       // pairs 0-1, 2-3 (lo, hi, lo, hi)
+    u32x2 v4;           // pair 4 (nwd == 5 only)
+    u32x4 n03;          // N-plane words q0 .. q0+3 (flagged windows only)
+    uint32_t n4;        // N-plane word q0+4
+};
+
+__device__ __forceinline__ void window_geom_w(const fc2_genome_view &g, uint64_t cstart, int64_t ws, int W, WinW &R) {
+    const int64_t g0 = (int64_t)cstart + ws;
+    const int32_t q0 = (int32_t)(g0 >> 5);
+    R.q0 = (uint32_t)q0;
+    R.sh = (unsigned)(g0 & 31);
+    R.nwd = ((int)R.sh + W + 31) >> 5;
+    const bool twin = (int)(q0 & 15) + R.nwd > 16;          // would cross a 128-B line of the main copy
+    R.off = twin ? (uint32_t)g.wt_twin_off + (uint32_t)(q0 + 8) * 8u : 128u + (uint32_t)q0 * 8u;   // main copy: 16 zero pairs in front
+}
+
+// Issue phase (all 64 lanes; inactive lanes pass a harmless geometry).  rs/rn: buffer resources of
+// g.wt and of the N plane viewed as 32-bit words.
+__device__ __forceinline__ void windows_issue_w(const fc2_genome_view &g, __amdgpu_buffer_rsrc_t rs,
+                                                __amdgpu_buffer_rsrc_t rn, const uint32_t *s_nsuper, uint64_t cstart,
+                                                int64_t wsA, int64_t wsB, int W, bool active, WinW &rA, WinW &rB,
+                                                u32x4 (&cl)[2][2]) {
+    window_geom_w(g, cstart, wsA, W, rA);
+    window_geom_w(g, cstart, wsB, W, rB);
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t wsx[2] = {wsA, wsB};
+    WinW *R[2] = {&rA, &rB};
+    // all LDS traffic of the issue phase in one batch: four offset permutes + super-map words
+    uint32_t src[2][2], sw[2][2] = {{0u, 0u}, {0u, 0u}}, sb[2][2] = {{0u, 0u}, {0u, 0u}};
+    bool sv[2] = {false, false};
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            src[x][c] = (uint32_t)__builtin_amdgcn_ds_bpermute((32 * c + (lane >> 1)) << 2, (int)R[x]->off);
+    if (!(FC2_ABLATE & 2) && s_nsuper) {
+        const int64_t top = (int64_t)(g.n_units * 64) - 1;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            int64_t lo = (int64_t)cstart + wsx[x], hi = lo + W - 1;
+            lo = lo < 0 ? 0 : lo;
+            hi = hi > top ? top : hi;
+            sv[x] = active && lo <= hi;
+            const uint32_t k0 = sv[x] ? (uint32_t)((uint64_t)lo >> g.nsuper_shift) : 0u,
+                           k1 = sv[x] ? (uint32_t)((uint64_t)hi >> g.nsuper_shift) : 0u;   // k1 <= k0 + 1
+            sw[x][0] = s_nsuper[k0 >> 5];
+            sw[x][1] = s_nsuper[k1 >> 5];
+            sb[x][0] = k0 & 31u;
+            sb[x][1] = k1 & 31u;
+        }
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int c = 0; c < 2; ++c)
+            cl[x][c] = __builtin_amdgcn_raw_buffer_load_b128(rs, src[x][c] + 16u * (uint32_t)(lane & 1), 0, 0);
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        WinW &Q = *R[x];
+        Q.v4 = u32x2{0u, 0u};
+        if (active && Q.nwd > 4) Q.v4 = __builtin_amdgcn_raw_buffer_load_b64(rs, Q.off + 32u, 0, 0);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        WinW &Q = *R[x];
+        const bool nflag = sv[x] && (((sw[x][0] >> sb[x][0]) | (sw[x][1] >> sb[x][1])) & 1u);
+        Q.n03 = u32x4{0u, 0u, 0u, 0u};
+        Q.n4 = 0u;
+        if (nflag) {
+            // one dword per load, each range-checked on its own (a 16-B load past the plane's end would
+            // drop all four); words before base 0 (chromosome 0, window starting at g0 < 0) are not
+            // loaded at all, so no offset ever wraps
+            uint32_t nw[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int32_t w = (int32_t)Q.q0 + j;
+                nw[j] = 0u;
+                if (w >= 0 && j < Q.nwd) nw[j] = __builtin_amdgcn_raw_buffer_load_b32(rn, (uint32_t)w * 4u, 0, 0);
+            }
+            Q.n03 = u32x4{nw[0], nw[1], nw[2], nw[3]};
+            Q.n4 = nw[4];
+        }
+    }
+}
+
+__device__ __forceinline__ void windows_exchange_w(u32x4 *xchg, const u32x4 (&cl)[2][2], WinW &rA, WinW &rB) {
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) xchg[(2 * x + c) * 64 + lane] = cl[x][c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int c = lane >> 5, m = lane & 31;
+    rA.v0 = xchg[(0 + c) * 64 + 2 * m];
+    rA.v1 = xchg[(0 + c) * 64 + 2 * m + 1];
+    rB.v0 = xchg[(2 + c) * 64 + 2 * m];
+    rB.v1 = xchg[(2 + c) * 64 + 2 * m + 1];
+}
+
+// Plain (one lane, one window) form of the word-pair loads, for locus-ordered or cache-resident
+// batches: two 16-B loads (+ the fifth pair), no LDS.  twin_ok = 0 keeps every window in the main
+// copy (an ordered batch re-reads its lines from L2; the shifted copy would only double that
+// footprint).  The N test is the coarse map (one 8-byte word from L2, consumed in
+// window_nwords_plain); flagged windows read their N words one round trip later.
+__device__ __forceinline__ void window_issue_w_plain(const fc2_genome_view &g, __amdgpu_buffer_rsrc_t rs,
+                                                     uint64_t cstart, int64_t ws, int W, bool twin_ok, WinW &R,
+                                                     uint64_t &cw) {
+    const int64_t g0 = (int64_t)cstart + ws;
+    const int32_t q0 = (int32_t)(g0 >> 5);
+    R.q0 = (uint32_t)q0;
+    R.sh = (unsigned)(g0 & 31);
+    R.nwd = ((int)R.sh + W + 31) >> 5;
+    const bool twin = twin_ok && (int)(q0 & 15) + R.nwd > 16;
+    R.off = twin ? (uint32_t)g.wt_twin_off + (uint32_t)(q0 + 8) * 8u : 128u + (uint32_t)q0 * 8u;   // main copy: 16 zero pairs in front
+    R.v0 = __builtin_amdgcn_raw_buffer_load_b128(rs, R.off, 0, 0);
+    R.v1 = __builtin_amdgcn_raw_buffer_load_b128(rs, R.off + 16u, 0, 0);
+    R.v4 = u32x2{0u, 0u};
+    if (R.nwd > 4) R.v4 = __builtin_amdgcn_raw_buffer_load_b64(rs, R.off + 32u, 0, 0);
+    const int64_t w = coarse_word(g, (int64_t)(q0 >> 1));
+    cw = ((((g.n_units + 15) >> 4) + 31) >> 5 >= 2) ? *reinterpret_cast<const uint64_t *>(g.ncoarse + w)
+                                                     : (uint64_t)g.ncoarse[0];
+}
+
+__device__ __forceinline__ void window_nwords_plain(const fc2_genome_view &g, __amdgpu_buffer_rsrc_t rn, uint64_t cw,
+                                                    WinW &R) {
+    const int64_t nb = (int64_t)((g.n_units + 15) >> 4);
+    const int32_t q0 = (int32_t)R.q0;
+    const int64_t g0 = (int64_t)q0 * 32 + R.sh;
+    const int64_t b0 = g0 >> 10, b1 = (g0 + 32 * R.nwd - 1) >> 10;
+    const int64_t cwi = coarse_word(g, (int64_t)(q0 >> 1));
+    auto nbit = [&](int64_t b) -> bool {
+        const int64_t k = b - 32 * cwi;
+        return b >= 0 && b < nb && k >= 0 && k < 64 && ((cw >> k) & 1ull);
+    };
+    R.n03 = u32x4{0u, 0u, 0u, 0u};
+    R.n4 = 0u;
+    if (nbit(b0) || (b1 != b0 && nbit(b1))) {
+        uint32_t nw[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int32_t wj = q0 + j;
+            nw[j] = 0u;
+            if (wj >= 0 && j < R.nwd) nw[j] = __builtin_amdgcn_raw_buffer_load_b32(rn, (uint32_t)wj * 4u, 0, 0);
+        }
+        R.n03 = u32x4{nw[0], nw[1], nw[2], nw[3]};
+        R.n4 = nw[4];
+    }
+}
+
+template <int NQ>
+__device__ __forceinline__ void window_finish_w(const WinW &R, int64_t csize, int64_t ws, int W, P32<NQ> &P) {
+    static_assert(NQ == 4, "word-pair windows cover W <= 128");
+    const uint32_t lo[6] = {R.v0.x, R.v0.z, R.v1.x, R.v1.z, R.v4.x, 0u};
+    const uint32_t hi[6] = {R.v0.y, R.v0.w, R.v1.y, R.v1.w, R.v4.y, 0u};
+    const uint32_t nn[6] = {R.n03.x, R.n03.y, R.n03.z, R.n03.w, R.n4, 0u};
+    const unsigned sh = R.sh;
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) {
+        P.lo[k] = alignr(lo[k + 1], lo[k], sh);
+        P.hi[k] = alignr(hi[k + 1], hi[k], sh);
+        P.n[k] = alignr(nn[k + 1], nn[k], sh);
+    }
+    P.lo[NQ] = 0; P.hi[NQ] = 0; P.n[NQ] = 0;
+    // positions outside [0, csize) of the chromosome read as 'N'
+    int64_t vlo = -ws, vhi = csize - ws;
+    vlo = vlo < 0 ? 0 : (vlo > W ? W : vlo);
+    vhi = vhi < 0 ? 0 : (vhi > W ? W : vhi);
+    if (vlo != 0 || vhi != W) {
+#pragma unroll
+        for (int k = 0; k < NQ; ++k) {
+            const uint32_t v = rmask32((int)vlo, (int)vhi, k);
+            P.lo[k] &= v; P.hi[k] &= v; P.n[k] = (P.n[k] & v) | ~v;
+        }
+    }
+}
+
 template <int NQ>
 __device__ __forceinline__ void window_dummy(P32<NQ> &P) {
 #pragma unroll
@@ -389,7 +619,7 @@ __device__ __forceinline__ uint64_t xcd_block(uint32_t b, uint32_t nwg) {
 // s_nsuper: LDS super-coarse N map or nullptr.
 // COOP: cooperative window loads (windows_issue_coop); then no lane may leave before the
 // exchange, so exits are deferred through `active`.  xchg: this wave's 4 x 64 LDS slots.
-template <int NQ, bool NT, bool COOP>
+template <int NQ, bool NT, bool COOP, bool WL = false>
 __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &bv,
                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask, uint32_t tw,
                                           uint64_t i, const uint64_t *s_cstart, const int64_t *s_csize, bool lds_tab,
@@ -450,7 +680,26 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     // round trip 3: both genome windows (find_circ.py:900-902) and their coarse N words
     WinRaw<NQ> rA, rB;
     ulonglong2 cl[2][2];
-    if constexpr (COOP) {
+    WinW wA, wB;
+    u32x4 wcl[2][2];
+    uint64_t cwA = 0, cwB = 0;
+    __amdgpu_buffer_rsrc_t rs, rn;
+    if constexpr (WL) {
+        rs = __builtin_amdgcn_make_buffer_rsrc((void *)g.wt, 0, (int)(uint32_t)g.wt_bytes, 0x00020000);
+        const uint64_t nb = g.n_units * 8;
+        rn = __builtin_amdgcn_make_buffer_rsrc((void *)g.nplane, 0,
+                                               (int)(uint32_t)(nb > 0xFFFFFFFFull ? 0xFFFFFFFFull : nb), 0x00020000);
+    }
+    if constexpr (COOP && WL) {
+        static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
+        if (!active) W = 2;
+        windows_issue_w(g, rs, rn, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active, wA,
+                        wB, wcl);
+    } else if constexpr (WL) {
+        static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
+        window_issue_w_plain(g, rs, cstart, wsA, W, g.units_twin != nullptr, wA, cwA);
+        window_issue_w_plain(g, rs, cstart, wsB, W, g.units_twin != nullptr, wB, cwB);
+    } else if constexpr (COOP) {
         if (!active) W = 2;                    // a harmless window for a lane that only loads for others
         windows_issue_coop<NQ>(g, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active,
                                rA, rB, cl);
@@ -492,17 +741,29 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         }
     }
 
-    if constexpr (COOP) {
+    P32<NQ> A, B;
+    if constexpr (COOP && WL) {
+        windows_exchange_w(reinterpret_cast<u32x4 *>(xchg), wcl, wA, wB);
+        if (!active) return;
+        window_finish_w<NQ>(wA, csize, wsA, W, A);
+        window_finish_w<NQ>(wB, csize, wsB, W, B);
+    } else if constexpr (WL) {
+        window_nwords_plain(g, rn, cwA, wA);
+        window_nwords_plain(g, rn, cwB, wB);
+        window_finish_w<NQ>(wA, csize, wsA, W, A);
+        window_finish_w<NQ>(wB, csize, wsB, W, B);
+    } else if constexpr (COOP) {
         windows_exchange_coop<NQ>(xchg, cl, rA, rB);
         if (!active) return;
     }
-    P32<NQ> A, B;
-    if (!g.dummy) {
-        window_finish<NQ>(g, s_nsuper, rA, csize, wsA, W, A);
-        window_finish<NQ>(g, s_nsuper, rB, csize, wsB, W, B);
-    } else {
-        window_dummy<NQ>(A);
-        window_dummy<NQ>(B);
+    if constexpr (!WL) {
+        if (!g.dummy) {
+            window_finish<NQ>(g, s_nsuper, rA, csize, wsA, W, A);
+            window_finish<NQ>(g, s_nsuper, rB, csize, wsB, W, B);
+        } else {
+            window_dummy<NQ>(A);
+            window_dummy<NQ>(B);
+        }
     }
 
     // --- mismatch planes and prefix counts ---------------------------------------
@@ -681,21 +942,103 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
             // genome has none (uniform branch)
             __shared__ ulonglong2 s_xchg[kBlock / 64][4 * 64];
             if (!g.dummy) {
-                scan_pair<NQ, NT, true>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, lds_tab,
-                                        lds_super ? s_nsuper_buf : nullptr, s_xchg[threadIdx.x >> 6]);
+                if (g.wt)          // word-pair layout present (fc2_wtab_launch): uniform branch
+                    scan_pair<NQ, NT, true, true>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, lds_tab,
+                                                  lds_super ? s_nsuper_buf : nullptr, s_xchg[threadIdx.x >> 6]);
+                else
+                    scan_pair<NQ, NT, true>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, lds_tab,
+                                            lds_super ? s_nsuper_buf : nullptr, s_xchg[threadIdx.x >> 6]);
                 return;
             }
         }
         scan_pair<NQ, NT, false>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, lds_tab,
                                  lds_super ? s_nsuper_buf : nullptr, nullptr);
     } else {
+        if constexpr (NQ == 4) {
+            if (g.wt && !g.dummy) {   // word-pair layout present (uniform branch)
+                scan_pair<NQ, NT, false, true>(p, g, bv, out, tiemask, tw, i, nullptr, nullptr, false, nullptr,
+                                               nullptr);
+                return;
+            }
+        }
         scan_pair<NQ, NT, false>(p, g, bv, out, tiemask, tw, i, nullptr, nullptr, false, nullptr, nullptr);
     }
+}
+
+// Persistent form of the STAGE + cooperative kernel (read-order batch over a large genome, l + 2
+// <= 128): the grid is sized to the resident capacity of the chip, each block stages the LDS
+// tables ONCE and then walks the batch's 256-pair tiles t = blockIdx.x + k * gridDim.x.  At
+// 50M pairs that removes ~195k block dispatches, each followed by a 7.5 KB LDS fill from L2 and a
+// barrier before the block's first window request.  The loop bound is uniform per block.
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void bp_scan32_persist_kernel(fc2_params p, fc2_genome_view g,
+                                                                   fc2_batch_view bv, uint64_t *__restrict__ out,
+                                                                   uint64_t *__restrict__ tiemask, uint32_t tw,
+                                                                   uint64_t n_tiles) {
+    constexpr int NQ = 4;
+    __shared__ uint64_t s_cstart[kChromLds];
+    __shared__ int64_t s_csize[kChromLds];
+    __shared__ __attribute__((aligned(16))) uint32_t s_nsuper_buf[kSuperLds];
+    __shared__ ulonglong2 s_xchg[kBlock / 64][4 * 64];
+    // the launcher guarantees: genome not dummy, chromosome table and nsuper fit in LDS
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+        const uint32_t w = c * (kSuperLds / 2) + 4 * threadIdx.x;
+        uint4 q = uint4{0u, 0u, 0u, 0u};
+        if (w < g.nsuper_words) q = *reinterpret_cast<const uint4 *>(g.nsuper + w);
+        *reinterpret_cast<uint4 *>(s_nsuper_buf + c * (kSuperLds / 2) + 4 * threadIdx.x) = q;
+    }
+    {
+        const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kBlock;
+        uint64_t a0 = 0, a1 = 0;
+        int64_t z0 = 0, z1 = 0;
+        if (k0 < g.n_chrom) { a0 = g.chrom_start[k0]; z0 = g.chrom_size[k0]; }
+        if (k1 < g.n_chrom) { a1 = g.chrom_start[k1]; z1 = g.chrom_size[k1]; }
+        s_cstart[k0] = a0; s_csize[k0] = z0;
+        s_cstart[k1] = a1; s_csize[k1] = z1;
+    }
+    __syncthreads();
+    for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x)
+        scan_pair<NQ, NT, true, false>(p, g, bv, out, tiemask, tw, t * kBlock + threadIdx.x, s_cstart, s_csize, true,
+                                s_nsuper_buf, s_xchg[threadIdx.x >> 6]);
 }
 
 }  // namespace
 
 namespace fc2 {
+
+bool persist_ok(int nq, const fc2_genome_view &g) {
+    return nq <= 4 && !g.dummy && g.n_chrom <= (uint32_t)kChromLds && g.nsuper &&
+           g.nsuper_words <= (uint32_t)kSuperLds;
+}
+
+void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+                           const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw, int blocks_per_cu) {
+    static int cus = 0, occ[2] = {0, 0};
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[0], bp_scan32_persist_kernel<false>, kBlock, 0) !=
+            hipSuccess)
+            occ[0] = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ[1], bp_scan32_persist_kernel<true>, kBlock, 0) !=
+            hipSuccess)
+            occ[1] = 1;
+    }
+    int per = blocks_per_cu > 0 ? blocks_per_cu : occ[nt ? 1 : 0];
+    if (per <= 0) per = 1;
+    const uint64_t n_tiles = (b.n + kBlock - 1) / kBlock;
+    uint64_t grid = (uint64_t)cus * per;
+    if (grid > n_tiles) grid = n_tiles;
+    if (nt)
+        hipLaunchKernelGGL(bp_scan32_persist_kernel<true>, dim3((unsigned)grid), dim3(kBlock), 0, s, p, g, b, out,
+                           tiemask, tw, n_tiles);
+    else
+        hipLaunchKernelGGL(bp_scan32_persist_kernel<false>, dim3((unsigned)grid), dim3(kBlock), 0, s, p, g, b, out,
+                           tiemask, tw, n_tiles);
+}
 
 void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
                    const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,

@@ -49,6 +49,8 @@ class Genome:
         self.units_twin = None                              # units shifted by half a line (fc2_twin_launch)
         self.nsuper = None                                  # LDS-sized N map (fc2_nsuper_launch)
         self.nsuper_shift = self.nsuper_words = 0
+        self.wt = None                                      # word-pair layout + shifted copy (fc2_wtab_launch)
+        self.wt_bytes = self.wt_twin_off = 0
         self.d_chrom_start = self.d_chrom_size = None
         self.dummy = False
         self.fasta = None                                   # ctypes handle (host FASTA) or None
@@ -166,6 +168,12 @@ class Genome:
             self.nsuper = torch.empty((nw.value + 3) // 4 * 4, dtype=torch.int32, device=self.device)
             N.check(N.lib().fc2_nsuper_launch(self.ncoarse.data_ptr(), self.n_units, self.nsuper.data_ptr(),
                                               torch.cuda.current_stream(self.device).cuda_stream))
+            nb, to = ctypes.c_uint64(), ctypes.c_uint64()
+            if N.lib().fc2_wtab_geometry(self.n_units, ctypes.byref(nb), ctypes.byref(to)) == 0:
+                self.wt_bytes, self.wt_twin_off = nb.value, to.value
+                self.wt = torch.empty(nb.value // 4, dtype=torch.int32, device=self.device)
+                N.check(N.lib().fc2_wtab_launch(self.units.data_ptr(), self.n_units, self.wt.data_ptr(),
+                                                torch.cuda.current_stream(self.device).cuda_stream))
 
     # ------------------------------------------------------------------ access
     def view(self) -> N.GenomeView:
@@ -175,7 +183,8 @@ class Genome:
                             self.d_chrom_start.data_ptr(), self.d_chrom_size.data_ptr(), self.n_units,
                             len(self.names), 0, self.units_twin.data_ptr() if self.units_twin is not None else None,
                             self.nsuper.data_ptr() if self.nsuper is not None else None, self.nsuper_shift,
-                            self.nsuper_words)
+                            self.nsuper_words, self.wt.data_ptr() if self.wt is not None else None,
+                            self.wt_bytes, self.wt_twin_off)
 
     def chrom_index(self, name: str) -> int:
         """Chromosome -> table index; KeyError like indexed_fasta.get_data (find_circ.py:193)."""

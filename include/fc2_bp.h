@@ -127,6 +127,13 @@ typedef struct fc2_genome_view {
                                     no memory request (fc2_nsuper_geometry / fc2_nsuper_launch) */
     uint32_t nsuper_shift;
     uint32_t nsuper_words;
+    const uint32_t *wt;          /* device or NULL: word-pair layout for the read-order scan
+                                    (fc2_wtab_launch): pair q = (low-plane, high-plane) 32-bit code
+                                    words of bases [32q, 32q+32) at byte 128 + 8q, then at byte wt_twin_off
+                                    the same pairs shifted by 64 B (pair q at wt_twin_off + 8(q+8)), so
+                                    that any run of <= 5 pairs lies inside one 128-B line of one copy */
+    uint64_t wt_bytes;           /* size of wt in bytes (< 4 GiB: 32-bit buffer offsets) */
+    uint64_t wt_twin_off;        /* byte offset of the shifted copy inside wt */
 } fc2_genome_view;
 
 /* ---- a batch of anchor pairs in device memory (SoA) --------------------- */
@@ -183,7 +190,12 @@ int         fc2_device_count(int *count);
                                   1 always, 2 (default) for batches not locus-ordered over a genome of
                                   >= 64 MiB of code planes */
 #define FC2_TUNE_EXTRA_LDS 9   /* bytes of unused LDS added to each scan block (occupancy experiments; 0) */
+#define FC2_TUNE_PERSIST 10    /* LDS-staging scan as a persistent grid that stages once per block:
+                                  0 off, -1 grid = CUs x resident blocks, k > 0 = CUs x k blocks */
+#define FC2_TUNE_WORDS 11      /* 1 (default): the LDS-staging scan reads windows from the view's
+                                  word-pair layout (wt) when present; 0: from the unit planes */
 int         fc2_set_tuning(int key, int value);
+int         fc2_get_tuning(int key, int *value);
 
 /* Largest l the register kernel handles (longer reads go to the byte kernel). */
 int         fc2_max_fast_l(void);
@@ -308,6 +320,11 @@ typedef struct fc2_synth_cfg {
 int fc2_synth_genome_launch(uint64_t seed, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,
                             uint64_t n_units, const int64_t *n_lo, const int64_t *n_hi,
                             uint32_t n_intervals, void *stream);
+/* Word-pair layout (fc2_genome_view.wt) for a genome of n_units 64-base units: its size and the
+ * byte offset of the shifted copy (FC2_E_RANGE if it would not fit 32-bit offsets, > ~8 Gbp), and
+ * the kernel that builds it (device [bytes / 4] words) from the unit planes. */
+int fc2_wtab_geometry(uint64_t n_units, uint64_t *bytes, uint64_t *twin_off);
+int fc2_wtab_launch(const uint64_t *units, uint64_t n_units, uint32_t *wt, void *stream);
 /* Build units_twin (device [2*(n_units+8)]) from units (device [2*n_units]). */
 int fc2_twin_launch(const uint64_t *units, uint64_t n_units, uint64_t *units_twin, void *stream);
 /* Super-coarse N map for n_units: *shift (>= 10) and *words (<= 2048). */

@@ -6,6 +6,7 @@ Prints one JSON line per variant: median / min kernel ms over rounds, pairs/s.
 """
 import argparse
 import json
+import re
 import os
 import sys
 
@@ -22,6 +23,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=7)
     ap.add_argument("--ordered", action="store_true", help="locus-ordered synthetic batch")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--read-len", type=int, default=100)
+    ap.add_argument("--no-check", action="store_true", help="measurement-only libraries (ablations) change results")
     ap.add_argument("--variants", default="k32nt1,k64nt1",
                     help="comma list of k32|k64 + nt1|nt0 + sw0|sw1 + tw0|tw1 (FC2_TUNE_KERNEL32 / STREAM_NT / "
                          "XCD_SWIZZLE (default auto) / TWIN)")
@@ -30,7 +33,7 @@ def main():
     import bench
     from find_circ2_amd import scan, _native as N
     dev = torch.device("cuda", 0)
-    args = argparse.Namespace(workload=a.workload, pairs=a.pairs, read_len=100, locus_ordered=a.ordered)
+    args = argparse.Namespace(workload=a.workload, pairs=a.pairs, read_len=a.read_len, locus_ordered=a.ordered)
     opt, g, b = bench.build_workload(args, 0, dev)
     out = scan(opt, g, b)
     torch.cuda.synchronize()
@@ -44,6 +47,10 @@ def main():
         N.lib().fc2_set_tuning(6, 0 if "tw0" in v else (1 if "tw1" in v else 2))
         N.lib().fc2_set_tuning(7, 0 if "st0" in v else (1 if "st1" in v else 2))
         N.lib().fc2_set_tuning(9, 8192 if "lds8k" in v else (65536 if "lds64k" in v else 0))
+        m = re.search(r"pe(A|\d+)", v)   # FC2_TUNE_PERSIST: peA = occupancy-sized grid, peK = K blocks/CU
+        # knobs an older library (FC2_LIB_VARIANT) may not have: set unchecked, default when absent
+        N.lib().fc2_set_tuning(11, 0 if "wo0" in v else 1)                       # FC2_TUNE_WORDS
+        N.lib().fc2_set_tuning(10, 0 if not m else (-1 if m.group(1) == "A" else int(m.group(1))))
 
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream(dev)
@@ -59,7 +66,7 @@ def main():
             e.record(stream)
             torch.cuda.synchronize()
             times[v].append(s.elapsed_time(e) / a.reps)
-            assert torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
+            assert a.no_check or torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
     for v in variants:
         t = np.array(times[v])
         print(json.dumps({"variant": v, "workload": a.workload + ("-ordered" if a.ordered else ""), "pairs": b.n, "median_ms": round(float(np.median(t)), 4),

@@ -59,10 +59,11 @@ def _n_heavy(path, seed=6):
     _write_fasta(path, seqs, width=50)
 
 
-def _run(opt, g, spans, stage, twin):
+def _run(opt, g, spans, stage, twin, words=1):
     L = N.lib()
     N.check(L.fc2_set_tuning(7, stage))
     N.check(L.fc2_set_tuning(6, twin))
+    N.check(L.fc2_set_tuning(11, words))
     try:
         flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.primary_reverse else 0)
                  for s in spans]
@@ -74,6 +75,7 @@ def _run(opt, g, spans, stage, twin):
     finally:
         L.fc2_set_tuning(7, 2)
         L.fc2_set_tuning(6, 2)
+        L.fc2_set_tuning(11, 1)
 
 
 def _oracle(opt, path, spans):
@@ -98,19 +100,19 @@ def genomes(tmp_path_factory):
 
 
 @pytest.mark.parametrize("kind", ["many_contigs", "n_heavy"])
-@pytest.mark.parametrize("stage,twin", [(1, 1), (1, 0), (0, 1), (0, 0)])
+@pytest.mark.parametrize("stage,twin,words", [(1, 1, 1), (1, 1, 0), (1, 0, 0), (0, 1, 1), (0, 0, 1)])
 @pytest.mark.parametrize("o", [dict(), dict(allhits=True, noncanonical=True)])
-def test_genome_shapes_vs_oracle(genomes, kind, stage, twin, o):
+def test_genome_shapes_vs_oracle(genomes, kind, stage, twin, words, o):
     path, g, seqs = genomes[kind]
     opt = Options(**o)
     if kind == "many_contigs":
         assert len(g.names) > 512
     spans = make_spans(seqs, 4000, seed=17, L=(40, 150), p_readN=0.1, p_edge=0.1)
-    b, out = _run(opt, g, spans, stage, twin)
+    b, out = _run(opt, g, spans, stage, twin, words)
     r = _oracle(opt, path, spans)
     ga = gpu_arrays(opt, b.host_pairs, out.host(b.n))
     assert ga["done"].all()
-    hits = assert_same(ga, oracle_arrays(r), label="%s stage=%d twin=%d %s" % (kind, stage, twin, o))
+    hits = assert_same(ga, oracle_arrays(r), label="%s stage=%d twin=%d words=%d %s" % (kind, stage, twin, words, o))
     assert hits > 300
     if kind == "n_heavy":
         # the case under test: windows that overlap N runs (exact, from the FASTA text)

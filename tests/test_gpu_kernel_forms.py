@@ -21,24 +21,26 @@ pytestmark = pytest.mark.gpu
 from find_circ2_amd import Genome, Options, PairBatch, SynthConfig, scan, sq_table  # noqa: E402
 from find_circ2_amd import _native as N  # noqa: E402
 
-# (FC2_TUNE_KERNEL32, FC2_TUNE_STAGE, FC2_TUNE_TWIN)
-FORMS = {"scan32_staged_coop_twin": (1, 1, 1), "scan32_plain_no_twin": (1, 0, 0),
-         "scan32_plain_twin": (1, 0, 1), "scan64": (0, 0, 0)}
+# knob values per form: FC2_TUNE_KERNEL32 (2), STAGE (7), TWIN (6), PERSIST (10), WORDS (11)
+KNOBS = (2, 7, 6, 10, 11)
+FORMS = {"scan32_staged_coop_words": (1, 1, 1, 0, 1), "scan32_staged_coop_units_twin": (1, 1, 1, 0, 0),
+         "scan32_persistent_coop_twin": (1, 1, 1, -1, 0), "scan32_persistent_3_per_cu": (1, 1, 1, 3, 0),
+         "scan32_plain_words_no_twin": (1, 0, 0, 0, 1), "scan32_plain_words_twin": (1, 0, 1, 0, 1),
+         "scan32_plain_units_no_twin": (1, 0, 0, 0, 0), "scan32_plain_units_twin": (1, 0, 1, 0, 0),
+         "scan64": (0, 0, 0, 0, 1)}
+DEFAULTS = {k: N.get_tuning(k) for k in KNOBS}
 
 
 def _set(form):
-    k32, st, tw = FORMS[form]
     L = N.lib()
-    N.check(L.fc2_set_tuning(2, k32))
-    N.check(L.fc2_set_tuning(7, st))
-    N.check(L.fc2_set_tuning(6, tw))
+    for k, v in zip(KNOBS, FORMS[form]):
+        N.check(L.fc2_set_tuning(k, v))
 
 
 def _reset():
     L = N.lib()
-    L.fc2_set_tuning(2, 1)
-    L.fc2_set_tuning(7, 2)
-    L.fc2_set_tuning(6, 2)
+    for k, v in DEFAULTS.items():
+        L.fc2_set_tuning(k, v)
 
 
 @pytest.fixture(scope="module")

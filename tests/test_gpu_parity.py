@@ -101,6 +101,28 @@ def test_spans_vs_oracle(fa, oi):
                   int(e["ov"]), int(e["n_hits"])) for e in exp], i
 
 
+@pytest.mark.parametrize("fa", ["CDR1as_locus.fa", "test_ref.fa"])
+@pytest.mark.parametrize("oi", range(len(OPTS)))
+def test_word_layout_vs_oracle(fa, oi):
+    """Batches with l + 2 <= 128 read their windows from the word-pair layout (both kernel forms via
+    the autouse stage fixture: cooperative and plain loads, the fifth pair for W > 97, the shifted
+    copy, windows hanging over chromosome ends), every option set."""
+    o = OPTS[oi]
+    opt = Options(**o)
+    path = os.path.join(GOLDEN, fa)
+    g = genome(path)
+    e = opt.asize - opt.margin
+    spans = make_spans(load_genome(path), 3000, seed=911 + oi, asize=opt.asize, L=(2 * e, 2 * e + 126),
+                       p_readN=0.1, p_edge=0.2)
+    b, out = run_spans(opt, g, spans)
+    assert b.max_l + 2 <= 128
+    r = oracle_spans(opt, path, spans, g.names)
+    ga = gpu_arrays(opt, b.host_pairs, out.host(b.n))
+    assert ga["done"].all()
+    hits = assert_same(ga, oracle_arrays(r), label=f"word layout {fa} {o}")
+    assert hits > 100
+
+
 @pytest.mark.parametrize("o", [dict(), dict(allhits=True, noncanonical=True, strandpref=True)])
 def test_locus_ordered_layout_same_results(o):
     """PairBatch.pack(locus_order=True) lays the batch out in genome order; decoded
