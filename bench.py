@@ -366,21 +366,47 @@ def cpu_baselines(opt, g, b, budget_s):
 def kernel_label(g, ordered: bool) -> str:
     """The bp_scan32 form fc2_bp_scan_launch picks for this batch (FC2_TUNE_STAGE auto rule)."""
     staged = (not ordered) and (not g.dummy) and g.n_units * 16 >= (64 << 20)
+    words = g.wt is not None
     if staged:
         return ("bp_scan32_kernel<4,NT,STAGE> (one anchor pair per lane; chromosome table + super-coarse N map in "
-                "LDS, lane pairs load each window line with one L2 request)")
-    return "bp_scan32_kernel<4,NT> (one anchor pair per lane)"
+                "LDS; %s)" % ("each window's 32 B of word pairs loaded by a lane pair in one request, from whichever "
+                              "genome copy holds it inside one 128-B line" if words else
+                              "lane pairs load each window line with one L2 request"))
+    return "bp_scan32_kernel<4,NT> (one anchor pair per lane%s)" % ("; word-pair windows" if words else "")
 
 
-def pattern_ceiling():
-    """Speed of light of the read-order access pattern on this GPU (scripts/pattern_probe.hip)."""
-    p = os.path.join(ROOT, "profiles", "r01", "pattern_probe.json")
-    try:
-        j = json.load(open(p))
-        return {"ms_per_50M_pairs": j["stream_gather2_ms"], "source": "profiles/r01/pattern_probe.json "
-                "(stream 48 B/pair + 2 random 16-B window gathers, no compute)"}
-    except Exception:
+def pattern_ceiling(opt, g, b, dev, rounds: int = 5, reps: int = 4):
+    """Speed of light of the read-order access pattern, live on this GPU: fc2_probe_pattern_launch
+    replays the scan's memory traffic for this batch (same records, rows, window offsets and result
+    stores) with none of its arithmetic.  Probe and scan launches are interleaved on one stream."""
+    import ctypes
+    import torch
+    from find_circ2_amd import scan, _native as N
+    if g.wt is None:
         return None
+    stream = torch.cuda.current_stream(dev)
+    junk = torch.empty(b.n, dtype=torch.int64, device=dev)
+    gv, bv, pv = g.view(), b.view(), opt.params()
+    out = scan(opt, g, b)
+    probe, kern = [], []
+    for _ in range(rounds):
+        for which, acc in (("probe", probe), ("scan", kern)):
+            s0, s1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s0.record(stream)
+            for _ in range(reps):
+                if which == "probe":
+                    N.check(N.lib().fc2_probe_pattern_launch(ctypes.byref(pv), ctypes.byref(gv), ctypes.byref(bv),
+                                                             junk.data_ptr(), stream.cuda_stream))
+                else:
+                    scan(opt, g, b, out=out, stream=stream.cuda_stream)
+            s1.record(stream)
+            torch.cuda.synchronize(dev)
+            acc.append(s0.elapsed_time(s1) / reps)
+    pm, km = float(np.median(probe)), float(np.median(kern))
+    return {"probe_ms": round(pm, 4), "scan_ms_same_run": round(km, 4), "scan_frac_of_ceiling": round(pm / km, 4),
+            "source": "live: fc2_probe_pattern_launch replays this batch's memory pattern (NT-streamed records and "
+                      "read rows, both windows' word pairs at the scan's offsets, 8-B result) without the search "
+                      "arithmetic; %d interleaved rounds x %d launches, medians" % (rounds, reps)}
 
 
 def main():
@@ -440,7 +466,7 @@ def main():
         "cpu_baseline": None,
     }
     if args.workload == "hg19" and not args.locus_ordered and b.n == 50_000_000:
-        line["roofline"]["access_pattern_ceiling"] = pattern_ceiling()
+        line["roofline"]["access_pattern_ceiling"] = pattern_ceiling(opt, g, b, dev)
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cb = cpu_baselines(opt, g, b, args.cpu_seconds)
         line["cpu_baseline"] = cb["main"]

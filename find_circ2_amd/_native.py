@@ -99,7 +99,7 @@ class SynthCfg(ctypes.Structure):
 EXPORTED = [
     "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_set_tuning", "fc2_get_tuning", "fc2_max_fast_l",
     "fc2_batch_geometry",
-    "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch",
+    "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch", "fc2_probe_pattern_launch",
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill",
@@ -177,6 +177,7 @@ def lib() -> ctypes.CDLL:
         "fc2_batch_geometry": (ctypes.c_int, [P(Params), i32, P(u32), P(u32), P(u32)]),
         "fc2_bp_scan_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp, u32, vp]),
         "fc2_bp_scan_bytes_launch": (ctypes.c_int, [P(Params), P(BytesView), vp, vp, u32, u64, vp]),
+        "fc2_probe_pattern_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp]),
         "fc2_fasta_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(vp)]),
         "fc2_fasta_close": (None, [vp]),
         "fc2_fasta_n_chrom": (ctypes.c_int, [vp]),

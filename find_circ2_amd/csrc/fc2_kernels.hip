@@ -844,6 +844,18 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     return hip_check(hipGetLastError(), "bp_scan_kernel launch");
 }
 
+extern "C" int fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                                        uint64_t *out, void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (!g || !b || !out || g->dummy || !g->wt || !g->chrom_start || !b->pairs || !b->read_words)
+        return fc2::fail(FC2_E_PARAM, "fc2_probe_pattern_launch: needs a genome with a word-pair table and a batch");
+    if (b->n == 0) return FC2_OK;
+    if (fc2::launch_probe_pattern((hipStream_t)stream, *p, *g, *b, out))
+        return fc2::fail(FC2_E_HIP, "probe_pattern_kernel launch failed");
+    return FC2_OK;
+}
+
 extern "C" int fc2_bp_scan_bytes_launch(const fc2_params *p, const fc2_bytes_view *v, fc2_result *results,
                                         uint64_t *tiemask, uint32_t tw, uint64_t stride, void *stream) {
     int rc = fc2::validate_params(p);

@@ -18,4 +18,7 @@ bool persist_ok(int nq, const fc2_genome_view &g);
 void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                            const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
                            int blocks_per_cu);   // 0: the occupancy limit
+// Measurement kernel: the read-order scan's memory pattern without its arithmetic (needs g.wt).
+int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b,
+                         uint64_t *out);
 }  // namespace fc2

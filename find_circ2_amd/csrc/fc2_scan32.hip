@@ -1003,9 +1003,66 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_persist_kernel(fc2_params p,
                                 s_nsuper_buf, s_xchg[threadIdx.x >> 6]);
 }
 
+// Speed-of-light probe of the read-order scan (measurement only, fc2_probe_pattern_launch): the
+// kernel's exact memory pattern on the same batch and genome -- NT-streamed 16-B records and read
+// rows, chromosome table staged in LDS, both windows' word pairs loaded by lane pairs from the same
+// table offsets (main or shifted copy), 8-B result stored -- with none of the search's arithmetic,
+// no N words and no fifth pair.  Its time bounds what any kernel with this access pattern can reach
+// on this GPU (bench.py: roofline.access_pattern_ceiling).
+__global__ __launch_bounds__(kBlock) void probe_pattern_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+                                                               uint64_t *__restrict__ out) {
+    __shared__ uint64_t s_cstart[kChromLds];
+    const bool lds_tab = g.n_chrom <= (uint32_t)kChromLds;
+    if (lds_tab) {
+        const uint32_t k0 = threadIdx.x, k1 = threadIdx.x + kBlock;
+        s_cstart[k0] = k0 < g.n_chrom ? g.chrom_start[k0] : 0ull;
+        s_cstart[k1] = k1 < g.n_chrom ? g.chrom_start[k1] : 0ull;
+        __syncthreads();
+    }
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const bool live = i < bv.n;
+    u64x2 prv = {0ull, 0ull};
+    uint64_t acc = 0;
+    if (live) {
+        prv = ld_pair_raw<true>(bv.pairs + i);
+        for (uint32_t j = 0; j < bv.rw; ++j) acc += ld_stream<true>(bv.read_words + (uint64_t)j * bv.stride + i);
+    }
+    fc2_pair pr;
+    __builtin_memcpy(&pr, &prv, sizeof pr);
+    const int e = p.asize - p.margin;
+    const int l = (int)pr.read_len - 2 * e;
+    const bool active = live && l >= 0 && l <= 126 && pr.chrom < g.n_chrom;
+    const int W = active ? l + 2 : 2;
+    const uint32_t c = active ? pr.chrom : 0u;
+    const uint64_t cstart = lds_tab ? s_cstart[c] : g.chrom_start[c];
+    WinW wA, wB;
+    window_geom_w(g, active ? cstart : 0, active ? (int64_t)pr.a_pos + e : 0, W, wA);
+    window_geom_w(g, active ? cstart : 0, active ? (int64_t)pr.b_aend - e - W : 0, W, wB);
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)g.wt, 0, (int)(uint32_t)g.wt_bytes,
+                                                                         0x00020000);
+    const int lane = (int)(threadIdx.x & 63);
+    const uint32_t offs[2] = {wA.off, wB.off};
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int cc = 0; cc < 2; ++cc) {
+            const uint32_t src = (uint32_t)__builtin_amdgcn_ds_bpermute((32 * cc + (lane >> 1)) << 2, (int)offs[x]);
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, src + 16u * (uint32_t)(lane & 1), 0, 0);
+            acc ^= (uint64_t)(v.x + v.y) | ((uint64_t)(v.z ^ v.w) << 32);
+        }
+    if (live) st_stream<true>(out + i, acc);
+}
+
 }  // namespace
 
 namespace fc2 {
+
+int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b,
+                         uint64_t *out) {
+    hipLaunchKernelGGL(probe_pattern_kernel, dim3((unsigned)((b.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p, g,
+                       b, out);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
 
 bool persist_ok(int nq, const fc2_genome_view &g) {
     return nq <= 4 && !g.dummy && g.n_chrom <= (uint32_t)kChromLds && g.nsuper &&

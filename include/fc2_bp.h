@@ -176,6 +176,13 @@ const char *fc2_last_error(void);
 /* Returns FC2_OK and the device count (0 on a host without GPUs is not an error). */
 int         fc2_device_count(int *count);
 
+/* Measurement only: the read-order scan's memory pattern (16-B records and read rows streamed, both
+ * windows' word pairs gathered exactly where the scan gathers them, 8-B word per pair stored into
+ * out[n]) with none of its arithmetic; its duration is the access-pattern speed of light that
+ * bench.py reports next to the scan.  Needs g->wt.  out receives meaningless checksums. */
+int         fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                                     uint64_t *out, void *stream);
+
 /* Performance knobs (results never depend on them); used for A/B measurements. */
 #define FC2_TUNE_STREAM_NT 1   /* 1 (default): per-pair inputs/results use non-temporal loads/stores */
 #define FC2_TUNE_KERNEL32  2   /* 1 (default): 32-bit-word scan kernel; 0: 64-bit-word scan kernel */

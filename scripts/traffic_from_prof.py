@@ -1,5 +1,5 @@
 #!/usr/bin/env python
-"""Build profiles/traffic_<round>.json from the rocprofv3 passes of scripts/profile_r01.sh.
+"""Build profiles/traffic_<round>.json from the rocprofv3 passes of scripts/profile_round.sh.
 
 HBM bytes per launch of the scan kernel = 2 x FETCH_SIZE x 1024 + WRITE_SIZE x 1024
 (gfx950 tallies 128-B line fills at 64 B, MI355X_MICROARCH.md §HBM; confirmed for this
@@ -45,6 +45,7 @@ def main():
     out = {}
     for w, key in (("hg19", "hg19"), ("hg19o", "hg19_locus_ordered"), ("cdr1as", "cdr1as_50M_calibration")):
         f, wr, h = agg(prof, "fetch_" + w), agg(prof, "write_" + w), agg(prof, "hit_" + w)
+        rq = agg(prof, "req_" + w)
         ns, calls = kstats(prof, "kt_" + w)
         if not f:
             continue
@@ -54,11 +55,15 @@ def main():
                     "avg_kernel_ns_rocprof": ns,
                     "FETCH_SIZE_kB_raw": f["FETCH_SIZE"], "WRITE_SIZE_kB": wr.get("WRITE_SIZE"),
                     "TCC_HIT_sum": h.get("TCC_HIT_sum"), "TCC_MISS_sum": h.get("TCC_MISS_sum"),
+                    "TCC_EA0_RDREQ_sum": rq.get("TCC_EA0_RDREQ_sum"), "TCC_REQ_sum": rq.get("TCC_REQ_sum"),
+                    "l2_requests_per_pair": round(rq["TCC_REQ_sum"] / N_PAIRS, 3) if rq.get("TCC_REQ_sum") else None,
+                    "hbm_read_requests_per_pair": (round(rq["TCC_EA0_RDREQ_sum"] / N_PAIRS, 3)
+                                                   if rq.get("TCC_EA0_RDREQ_sum") else None),
                     "hbm_bytes_per_launch": round(hbm), "hbm_bytes_per_pair": round(hbm / N_PAIRS, 1),
                     "moved_TBps": round(hbm / (ns * 1e-9) / 1e12, 3) if ns else None}
     out["correction"] = ("reads = 2 x FETCH_SIZE x 1024 (gfx950 128-B fills tallied at 64 B), writes = WRITE_SIZE x "
                          "1024 (exact: 8 B x pairs)")
-    out["source"] = ("rocprofv3 --kernel-trace --stats and separate --pmc passes (scripts/profile_r01.sh): bench.py "
+    out["source"] = ("rocprofv3 --kernel-trace --stats and separate --pmc passes (scripts/profile_round.sh): bench.py "
                      "--steps 10 --warmup 2; averages over the scan-kernel dispatches")
     path = os.path.join(ROOT, "profiles", "traffic_%s.json" % rnd)
     json.dump(out, open(path, "w"), indent=1)
