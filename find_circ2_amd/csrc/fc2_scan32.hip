@@ -801,19 +801,37 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     const int sp_minus = p.strandpref ? (prim_minus ? 100 : 0) : 0;
     Best32 Bst;
     if (!p.noncanonical) {
+        // Every x of word k has dist >= (A mismatches before the word) + (B mismatches after it).
+        // Words whose floor exceeds maxdist hold no hit (random pairs: none survive; planted: one,
+        // rarely two).  The surviving words of a lane are walked in ascending order, one selected
+        // word at a time, so a wave iterates over max(candidates per lane), not over the sum of
+        // per-word maxima; x still ascends, as the stable sort at find_circ.py:966 requires.
+        uint32_t cw[NQ];
+        uint32_t live = 0;
 #pragma unroll
         for (int k = 0; k < NQ; ++k) {
-            uint32_t w = plus[k] | minus[k];
+            const int floor_k = cA[k] + (totB - cB[k] - __popc(mB[k]));
+            cw[k] = floor_k <= p.maxdist ? (plus[k] | minus[k]) : 0u;
+            live |= (cw[k] ? 1u : 0u) << k;
+        }
+        while (live) {
+            const int k = __ffs(live) - 1;
+            live &= live - 1;
+            uint32_t w = 0, a = 0, bm = 0, mi = 0;
+            int base = 0;
+#pragma unroll
+            for (int kk = 0; kk < NQ; ++kk)
+                if (kk == k) { w = cw[kk]; a = mA[kk]; bm = mB[kk]; mi = minus[kk]; base = cA[kk] + totB - cB[kk]; }
             while (w) {
                 const int b = __ffs(w) - 1;
                 w &= w - 1;
                 const uint32_t below = (1u << b) - 1u;
-                const int dist = cA[k] + __popc(mA[k] & below) + totB - cB[k] - __popc(mB[k] & below);
+                const int dist = base + __popc(a & below) - __popc(bm & below);
                 if (dist <= p.maxdist) {
                     const int x = 32 * k + b;
-                    const int isminus = (int)((minus[k] >> b) & 1u);
-                    add_hit(Bst, x, isminus, dist, ov_of(x, l, p.margin),
-                            20 - 10 * dist - ov_of(x, l, p.margin) + (isminus ? sp_minus : sp_plus));
+                    const int isminus = (int)((mi >> b) & 1u);
+                    const int ov = ov_of(x, l, p.margin);
+                    add_hit(Bst, x, isminus, dist, ov, 20 - 10 * dist - ov + (isminus ? sp_minus : sp_plus));
                 }
             }
         }

@@ -52,21 +52,32 @@ def main():
         N.lib().fc2_set_tuning(11, 0 if "wo0" in v else 1)                       # FC2_TUNE_WORDS
         N.lib().fc2_set_tuning(10, 0 if not m else (-1 if m.group(1) == "A" else int(m.group(1))))
 
+    import ctypes
+    junk = torch.empty(b.n, dtype=torch.int64, device=dev)
+
+    def run(v):
+        if v == "probe":          # the scan's access pattern without its arithmetic (fc2_probe_pattern_launch)
+            gv, bv, pv = g.view(), b.view(), opt.params()
+            N.check(N.lib().fc2_probe_pattern_launch(ctypes.byref(pv), ctypes.byref(gv), ctypes.byref(bv),
+                                                     junk.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+        else:
+            scan(opt, g, b, out=out)
+
     times = {v: [] for v in variants}
     stream = torch.cuda.current_stream(dev)
     for r in range(a.rounds):
         for v in variants:
             apply(v)
-            scan(opt, g, b, out=out)
+            run(v)
             torch.cuda.synchronize()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record(stream)
             for _ in range(a.reps):
-                scan(opt, g, b, out=out)
+                run(v)
             e.record(stream)
             torch.cuda.synchronize()
             times[v].append(s.elapsed_time(e) / a.reps)
-            assert a.no_check or torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
+            assert a.no_check or v == "probe" or torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
     for v in variants:
         t = np.array(times[v])
         print(json.dumps({"variant": v, "workload": a.workload + ("-ordered" if a.ordered else ""), "pairs": b.n, "median_ms": round(float(np.median(t)), 4),
