@@ -21,6 +21,7 @@ int validate_params(const fc2_params *p);
 // fc2_reorder.hip tuning (fc2_set_tuning)
 extern int g_reorder_rounds;
 extern int g_reorder_nt;
+extern int g_reorder_shift;
 
 inline int eff_anchor(const fc2_params *p) { return p->asize - p->margin; }  // find_circ.py:882
 

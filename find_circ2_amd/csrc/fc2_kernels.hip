@@ -978,6 +978,10 @@ extern "C" int fc2_set_tuning(int key, int value) {
             if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: twin is 0, 1 or 2");
             g_twin = value; return FC2_OK;
         case FC2_TUNE_WORDS: g_words = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_REORDER_SHIFT:
+            if (value != 0 && (value < 16 || value > 40))
+                return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: reorder shift is 0 or 16..40");
+            fc2::g_reorder_shift = value; return FC2_OK;
         case FC2_TUNE_PERSIST:
             if (value < -1 || value > 32) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: persist is -1..32");
             g_persist = value; return FC2_OK;
@@ -1001,6 +1005,7 @@ extern "C" int fc2_get_tuning(int key, int *value) {
         case FC2_TUNE_EXTRA_LDS: *value = g_extra_lds; return FC2_OK;
         case FC2_TUNE_PERSIST: *value = g_persist; return FC2_OK;
         case FC2_TUNE_WORDS: *value = g_words; return FC2_OK;
+        case FC2_TUNE_REORDER_SHIFT: *value = fc2::g_reorder_shift; return FC2_OK;
         default: return fc2::fail(FC2_E_PARAM, "fc2_get_tuning: unknown key");
     }
 }

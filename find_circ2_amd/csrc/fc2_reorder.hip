@@ -224,6 +224,7 @@ namespace fc2 {
 int g_reorder_rounds = 4;      // pairs per thread per chunk (FC2_TUNE_REORDER_ROUNDS; r01 sweep: 32 -> 4.4 ms,
                                // 8/4 -> 3.3 ms, 2 -> 2.9 ms per 50M pairs)
 int g_reorder_nt = 0;          // non-temporal scatter stores (FC2_TUNE_REORDER_NT)
+int g_reorder_shift = 0;       // bucket = 2^shift bases; 0: ~1024 buckets over the genome (FC2_TUNE_REORDER_SHIFT)
 }  // namespace fc2
 
 extern "C" int fc2_reorder_plan(const fc2_genome_view *g, uint64_t n, fc2_reorder_info *info) {
@@ -233,6 +234,10 @@ extern "C" int fc2_reorder_plan(const fc2_genome_view *g, uint64_t n, fc2_reorde
     unsigned shift = ceil_log2(bases);
     shift = shift > 10 ? shift - 10 : 0;
     if (shift < 16) shift = 16;                    // >= 64 kbp per bucket
+    if (fc2::g_reorder_shift) {                    // FC2_TUNE_REORDER_SHIFT: coarser buckets (fewer fronts)
+        shift = (unsigned)fc2::g_reorder_shift;
+        while (((bases - 1) >> shift) + 1 > (uint64_t)kMaxBuckets) ++shift;
+    }
     const uint64_t nb = ((bases - 1) >> shift) + 1;
     info->n = n;
     info->shift = shift;
