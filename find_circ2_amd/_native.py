@@ -31,6 +31,7 @@ PAIR_PRIMARY_REV = 0x02
 PAIR_READ_N = 0x04
 PAIR_BYTEPATH = 0x08
 PAIR_SKIP = 0x10
+PAIR_WIN_N = 0x20
 
 RES_MINUS = 0x0001
 RES_GTAG_SHIFT = 1
@@ -70,7 +71,9 @@ class GenomeView(ctypes.Structure):
 class BatchView(ctypes.Structure):
     _fields_ = [("pairs", ctypes.c_void_p), ("read_words", ctypes.c_void_p), ("read_nwords", ctypes.c_void_p),
                 ("n", ctypes.c_uint64), ("stride", ctypes.c_uint64), ("rw", ctypes.c_uint32),
-                ("nw", ctypes.c_uint32), ("max_l", ctypes.c_int32), ("layout", ctypes.c_uint32)]
+                ("nw", ctypes.c_uint32), ("max_l", ctypes.c_int32), ("layout", ctypes.c_uint32),
+                ("win_words", ctypes.c_void_p), ("win_nwords", ctypes.c_void_p), ("ww", ctypes.c_uint32),
+                ("wnw", ctypes.c_uint32)]
 
 
 BATCH_LOCUS_ORDERED = 0x1
@@ -102,7 +105,8 @@ EXPORTED = [
     "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch", "fc2_probe_pattern_launch",
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
-    "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill",
+    "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill", "fc2_window_geometry", "fc2_pack_windows",
+    "fc2_gather_windows_launch",
     "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_twin_launch", "fc2_wtab_geometry", "fc2_wtab_launch",
     "fc2_nsuper_geometry", "fc2_nsuper_launch", "fc2_synth_pairs_launch",
     "fc2_reorder_plan", "fc2_reorder_launch",
@@ -190,6 +194,9 @@ def lib() -> ctypes.CDLL:
         "fc2_pack_pairs": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, vp, u32, vp, u32, u64, P(u64),
                                           ctypes.c_int]),
         "fc2_bytepath_size": (ctypes.c_int, [P(Params), u64, vp, P(u64), P(u64)]),
+        "fc2_window_geometry": (ctypes.c_int, [P(Params), ctypes.c_int, P(u32), P(u32), P(u32)]),
+        "fc2_pack_windows": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, u32, u64, ctypes.c_int]),
+        "fc2_gather_windows_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp, vp, u32, vp]),
         "fc2_bytepath_fill": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, vp, vp, vp, vp]),
         "fc2_synth_genome_launch": (ctypes.c_int, [u64, vp, vp, vp, u64, vp, vp, u32, vp]),
         "fc2_coarse_launch": (ctypes.c_int, [vp, vp, u64, vp]),

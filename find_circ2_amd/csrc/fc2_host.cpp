@@ -685,6 +685,75 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
     return FC2_OK;
 }
 
+extern "C" int fc2_window_geometry(const fc2_params *p, int max_read_len, uint32_t *pw, uint32_t *ww,
+                                   uint32_t *wnw) {
+    int rc = validate_params(p);
+    if (rc) return rc;
+    if (!pw || !ww || !wnw) return fail(FC2_E_PARAM, "fc2_window_geometry: null argument");
+    const int l = std::max(0, max_read_len - 2 * eff_anchor(p));
+    if (l + 2 > 128) return fail(FC2_E_RANGE, "fc2_window_geometry: window rows carry l + 2 <= 128 only");
+    *pw = (uint32_t)((l + 2 + 31) / 32);
+    *ww = 2 * *pw;
+    *wnw = *pw;
+    return FC2_OK;
+}
+
+// Af / Bf of each evaluated pair from the FASTA text with get_data's semantics (the same bytes the
+// byte-exact kernel gets), encoded as the rows fc2_batch_view.win_words describes.
+extern "C" int fc2_pack_windows(const fc2_params *p, const fc2_fasta *f, uint64_t n, fc2_pair *pairs,
+                                uint64_t *win_words, uint64_t *win_nwords, uint32_t pw, uint64_t stride,
+                                int n_threads) {
+    int rc = validate_params(p);
+    if (rc) return rc;
+    if (n && (!f || !pairs || !win_words || !win_nwords)) return fail(FC2_E_PARAM, "fc2_pack_windows: null argument");
+    if (pw < 1 || pw > 4) return fail(FC2_E_RANGE, "fc2_pack_windows: pw is 1..4");
+    if (stride < n) return fail(FC2_E_PARAM, "fc2_pack_windows: stride < n");
+    const int e = eff_anchor(p);
+    const int nch = (int)f->chroms.size();
+    std::atomic<int> err{0};
+    parallel_for(n, n_workers(n_threads), [&](uint64_t b, uint64_t en) {
+        std::string A, B;
+        for (uint64_t i = b; i < en; ++i) {
+            fc2_pair &pr = pairs[i];
+            uint32_t w32[16] = {0}, n32[8] = {0};
+            bool anyN = false;
+            const int l = (int)pr.read_len - 2 * e;
+            const int W = l + 2;
+            if (!(pr.flags & (FC2_PAIR_SKIP | FC2_PAIR_BYTEPATH)) && l >= 0 && W <= 32 * (int)pw &&
+                (int)pr.chrom < nch) {
+                const int r1 = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + W, A);
+                const int r2 = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - W, (int64_t)pr.b_aend - e, B);
+                if (r1 || r2) { err = r1 ? r1 : r2; continue; }
+                const std::string *win[2] = {&A, &B};
+                for (int x = 0; x < 2; ++x) {
+                    const std::string &S = *win[x];
+                    // windows of unexpected length lie outside get_data's range: the scan reports them
+                    // (FC2_RES_ERR_WIN) from the coordinates, whatever the rows hold
+                    const int m = std::min<int>(W, (int)S.size());
+                    for (int j = 0; j < m; ++j) {
+                        const uint32_t pc = pack_code((uint8_t)S[j]);
+                        const int k = j >> 5, bit = j & 31;
+                        if (pc & 12u) {                 // 'N' (or an exotic byte: such pairs are BYTEPATH)
+                            n32[x * pw + k] |= 1u << bit;
+                            anyN = true;
+                            continue;
+                        }
+                        if (pc & 1u) w32[(2 * x) * pw + k] |= 1u << bit;
+                        if (pc & 2u) w32[(2 * x + 1) * pw + k] |= 1u << bit;
+                    }
+                }
+            }
+            for (uint32_t j = 0; j < 2 * pw; ++j)
+                win_words[(uint64_t)j * stride + i] = (uint64_t)w32[2 * j] | ((uint64_t)w32[2 * j + 1] << 32);
+            for (uint32_t j = 0; j < pw; ++j)
+                win_nwords[(uint64_t)j * stride + i] = (uint64_t)n32[2 * j] | ((uint64_t)n32[2 * j + 1] << 32);
+            pr.flags = (uint8_t)((pr.flags & ~FC2_PAIR_WIN_N) | (anyN ? FC2_PAIR_WIN_N : 0u));
+        }
+    });
+    if (err.load()) return err.load();
+    return FC2_OK;
+}
+
 static inline uint64_t block_bytes(int l) {  // header + I + A + B (windows up to l+3)
     const uint64_t lc = (uint64_t)std::max(0, l);
     return (12 + lc + 2 * (lc + 3) + 3) & ~3ull;

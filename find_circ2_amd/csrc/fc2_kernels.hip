@@ -799,7 +799,10 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     if (b->n == 0) return FC2_OK;
     if (!b->pairs || !b->read_words || b->stride < b->n || b->rw == 0)
         return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: bad batch view");
-    if (!g->dummy && (!g->units || !g->nplane || !g->ncoarse || !g->chrom_start || !g->chrom_size))
+    const bool carried = b->win_words != nullptr;   // window-carrying batch: no genome gather
+    if (carried && (g->dummy || !g->chrom_size))
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: window rows need the genome's chromosome sizes");
+    if (!carried && !g->dummy && (!g->units || !g->nplane || !g->ncoarse || !g->chrom_start || !g->chrom_size))
         return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: bad genome view");
     if (p->allhits && (!tiemask || tw < 2))
         return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: --all-hits needs a tie mask");
@@ -814,6 +817,14 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     const unsigned grid = grid_for(b->n, kBlock);
     uint64_t *out = reinterpret_cast<uint64_t *>(results);
     const bool nt = stream_nt();
+    if (carried) {
+        const uint32_t pw = (uint32_t)((ml + 2 + 31) / 32);
+        if (ml + 2 > 128) return fc2::fail(FC2_E_RANGE, "fc2_bp_scan_launch: window rows carry l + 2 <= 128 only");
+        if (b->ww < 2 * pw || (b->win_nwords && b->wnw < pw) || !b->win_nwords)
+            return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: window rows too narrow for max_l");
+        fc2::launch_scan32_win((int)pw, nt, s, *p, *g, *b, out, tiemask, tw);
+        return hip_check(hipGetLastError(), "bp_scan32_win_kernel launch");
+    }
     if (g_kernel32) {
         const int sw = g_xcd_swizzle == 2 ? ((b->layout & FC2_BATCH_LOCUS_ORDERED) ? 1 : 0) : g_xcd_swizzle;
         fc2_genome_view gv = *g;
@@ -842,6 +853,20 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     else { if (nt) FC2_LAUNCH(8, true); else FC2_LAUNCH(8, false); }
 #undef FC2_LAUNCH
     return hip_check(hipGetLastError(), "bp_scan_kernel launch");
+}
+
+extern "C" int fc2_gather_windows_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                                         fc2_pair *pairs, uint64_t *win_words, uint64_t *win_nwords, uint32_t pw,
+                                         void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (!g || !b || !pairs || !win_words || !win_nwords || g->dummy || !g->wt || !g->chrom_start || !g->chrom_size)
+        return fc2::fail(FC2_E_PARAM, "fc2_gather_windows_launch: needs a genome with a word-pair table");
+    if (pw < 1 || pw > 4) return fc2::fail(FC2_E_RANGE, "fc2_gather_windows_launch: pw is 1..4");
+    if (b->n == 0) return FC2_OK;
+    if (b->stride < b->n) return fc2::fail(FC2_E_PARAM, "fc2_gather_windows_launch: stride < n");
+    fc2::launch_gather_windows((hipStream_t)stream, *p, *g, b->n, b->stride, pairs, win_words, win_nwords, pw);
+    return hip_check(hipGetLastError(), "gather_windows_kernel launch");
 }
 
 extern "C" int fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,

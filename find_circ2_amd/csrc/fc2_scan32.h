@@ -18,6 +18,11 @@ bool persist_ok(int nq, const fc2_genome_view &g);
 void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                            const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
                            int blocks_per_cu);   // 0: the occupancy limit
+// Window-carrying batches (b.win_words): PW = plane words, 1..4.
+void launch_scan32_win(int pw, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+                       const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw);
+void launch_gather_windows(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, uint64_t n, uint64_t stride,
+                           fc2_pair *pairs, uint64_t *win_words, uint64_t *win_nwords, uint32_t pw);
 // Measurement kernel: the read-order scan's memory pattern without its arithmetic (needs g.wt).
 int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b,
                          uint64_t *out);

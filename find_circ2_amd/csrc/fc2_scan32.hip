@@ -619,7 +619,9 @@ __device__ __forceinline__ uint64_t xcd_block(uint32_t b, uint32_t nwg) {
 // s_nsuper: LDS super-coarse N map or nullptr.
 // COOP: cooperative window loads (windows_issue_coop); then no lane may leave before the
 // exchange, so exits are deferred through `active`.  xchg: this wave's 4 x 64 LDS slots.
-template <int NQ, bool NT, bool COOP, bool WL = false>
+// PW > 0: window-carrying batch (fc2_batch_view.win_words, pw = PW): the windows arrive with the
+// record in round trip 1 and nothing is gathered from the genome (NQ == 4, !COOP, !WL).
+template <int NQ, bool NT, bool COOP, bool WL = false, int PW = 0>
 __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &bv,
                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask, uint32_t tw,
                                           uint64_t i, const uint64_t *s_cstart, const int64_t *s_csize, bool lds_tab,
@@ -632,11 +634,19 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     uint64_t rv[R];
 #pragma unroll
     for (int j = 0; j < R; ++j) rv[j] = 0;
+    static_assert(PW == 0 || (NQ == 4 && !COOP && !WL && PW <= 4), "window rows: plain form, l + 2 <= 128");
+    uint64_t wv[PW > 0 ? 2 * PW : 1];
+#pragma unroll
+    for (int j = 0; j < (PW > 0 ? 2 * PW : 1); ++j) wv[j] = 0;
     if (live) {
         prv = ld_pair_raw<NT>(bv.pairs + i);
 #pragma unroll
         for (int j = 0; j < R; ++j)
             rv[j] = ((uint32_t)j < bv.rw) ? ld_stream<NT>(bv.read_words + (uint64_t)j * bv.stride + i) : 0ull;
+        if constexpr (PW > 0) {
+#pragma unroll
+            for (int j = 0; j < 2 * PW; ++j) wv[j] = ld_stream<NT>(bv.win_words + (uint64_t)j * bv.stride + i);
+        }
     }
     fc2_pair pr;
     __builtin_memcpy(&pr, &prv, sizeof pr);
@@ -653,7 +663,9 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     if (!g.dummy) {
         const bool known = pr.chrom < g.n_chrom;
         const uint32_t c = known ? pr.chrom : 0u;
-        if (lds_tab) {
+        if constexpr (PW > 0) {
+            csize = g.chrom_size[c];           // only the window-range check needs the chromosome
+        } else if (lds_tab) {
             cstart = s_cstart[c];
             csize = s_csize[c];
         } else {
@@ -703,6 +715,8 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         if (!active) W = 2;                    // a harmless window for a lane that only loads for others
         windows_issue_coop<NQ>(g, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active,
                                rA, rB, cl);
+    } else if constexpr (PW > 0) {
+        // windows came with the record
     } else if (!g.dummy) {
         window_issue<NQ>(g, s_nsuper, cstart, wsA, W, rA);
         window_issue<NQ>(g, s_nsuper, cstart, wsB, W, rB);
@@ -742,7 +756,32 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     }
 
     P32<NQ> A, B;
-    if constexpr (COOP && WL) {
+    if constexpr (PW > 0) {
+        // plane p word k = 32-bit word p*PW + k of the row; N rows only for flagged pairs
+        uint32_t w32[8 * PW], n32[2 * PW];
+#pragma unroll
+        for (int j = 0; j < 2 * PW; ++j) { w32[2 * j] = (uint32_t)wv[j]; w32[2 * j + 1] = (uint32_t)(wv[j] >> 32); }
+#pragma unroll
+        for (int j = 0; j < 2 * PW; ++j) n32[j] = 0u;
+        if (active && (pr.flags & FC2_PAIR_WIN_N)) {
+#pragma unroll
+            for (int j = 0; j < PW; ++j) {
+                const uint64_t v = ld_stream<NT>(bv.win_nwords + (uint64_t)j * bv.stride + i);
+                n32[2 * j] = (uint32_t)v;
+                n32[2 * j + 1] = (uint32_t)(v >> 32);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k <= NQ; ++k) {
+            A.lo[k] = k < PW ? w32[0 * PW + (k < PW ? k : 0)] : 0u;
+            A.hi[k] = k < PW ? w32[1 * PW + (k < PW ? k : 0)] : 0u;
+            B.lo[k] = k < PW ? w32[2 * PW + (k < PW ? k : 0)] : 0u;
+            B.hi[k] = k < PW ? w32[3 * PW + (k < PW ? k : 0)] : 0u;
+            A.n[k] = k < PW ? n32[(k < PW ? k : 0)] : 0u;
+            B.n[k] = k < PW ? n32[PW + (k < PW ? k : 0)] : 0u;
+        }
+        if (!active) return;
+    } else if constexpr (COOP && WL) {
         windows_exchange_w(reinterpret_cast<u32x4 *>(xchg), wcl, wA, wB);
         if (!active) return;
         window_finish_w<NQ>(wA, csize, wsA, W, A);
@@ -756,7 +795,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         windows_exchange_coop<NQ>(xchg, cl, rA, rB);
         if (!active) return;
     }
-    if constexpr (!WL) {
+    if constexpr (!WL && PW == 0) {
         if (!g.dummy) {
             window_finish<NQ>(g, s_nsuper, rA, csize, wsA, W, A);
             window_finish<NQ>(g, s_nsuper, rB, csize, wsB, W, B);
@@ -983,6 +1022,81 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
     }
 }
 
+// Window-carrying batches (fc2_batch_view.win_words): one pair per lane, windows streamed with
+// the record -- the design BASELINE.json's north_star sketches (windows gathered on the host
+// from the mmap'd FASTA).  No genome gather, no LDS.
+template <int PW, bool NT>
+__global__ __launch_bounds__(kBlock) void bp_scan32_win_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+                                                               uint64_t *__restrict__ out,
+                                                               uint64_t *__restrict__ tiemask, uint32_t tw) {
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    scan_pair<4, NT, false, false, PW>(p, g, bv, out, tiemask, tw, i, nullptr, nullptr, false, nullptr, nullptr);
+}
+
+// Device gather of the window rows from the resident genome (fc2_gather_windows_launch): the plain
+// word-pair window path of the scan, written out instead of searched.
+template <int PW>
+__global__ __launch_bounds__(kBlock) void gather_windows_kernel(fc2_params p, fc2_genome_view g, uint64_t n,
+                                                                uint64_t stride, fc2_pair *__restrict__ pairs,
+                                                                uint64_t *__restrict__ win_words,
+                                                                uint64_t *__restrict__ win_nwords) {
+    constexpr uint32_t pw = PW;
+    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    fc2_pair pr = pairs[i];
+    uint32_t w32[16], n32[8];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w32[j] = 0u;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) n32[j] = 0u;
+    const int e = p.asize - p.margin;
+    const int l = (int)pr.read_len - 2 * e;
+    const int W = l + 2;
+    bool anyN = false;
+    if (!(pr.flags & (FC2_PAIR_SKIP | FC2_PAIR_BYTEPATH)) && l >= 0 && W <= 32 * (int)pw && pr.chrom < g.n_chrom) {
+        const uint64_t cstart = g.chrom_start[pr.chrom];
+        const int64_t csize = g.chrom_size[pr.chrom];
+        const int64_t wsA = (int64_t)pr.a_pos + e, wsB = (int64_t)pr.b_aend - e - W;
+        if (!(wsA > csize || wsA + W < 0 || wsB > csize || wsB + W < 0)) {
+            const __amdgpu_buffer_rsrc_t rs =
+                __builtin_amdgcn_make_buffer_rsrc((void *)g.wt, 0, (int)(uint32_t)g.wt_bytes, 0x00020000);
+            const uint64_t nb = g.n_units * 8;
+            const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+                (void *)g.nplane, 0, (int)(uint32_t)(nb > 0xFFFFFFFFull ? 0xFFFFFFFFull : nb), 0x00020000);
+            WinW wA, wB;
+            uint64_t cwA = 0, cwB = 0;
+            window_issue_w_plain(g, rs, cstart, wsA, W, g.units_twin != nullptr, wA, cwA);
+            window_issue_w_plain(g, rs, cstart, wsB, W, g.units_twin != nullptr, wB, cwB);
+            window_nwords_plain(g, rn, cwA, wA);
+            window_nwords_plain(g, rn, cwB, wB);
+            P32<4> A, B;
+            window_finish_w<4>(wA, csize, wsA, W, A);
+            window_finish_w<4>(wB, csize, wsB, W, B);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t m = rmask32(0, W, k);
+                if (k < (int)pw) {
+                    w32[0 * pw + k] = A.lo[k] & m;
+                    w32[1 * pw + k] = A.hi[k] & m;
+                    w32[2 * pw + k] = B.lo[k] & m;
+                    w32[3 * pw + k] = B.hi[k] & m;
+                    n32[k] = A.n[k] & m;
+                    n32[pw + k] = B.n[k] & m;
+                    anyN |= (n32[k] | n32[pw + k]) != 0u;
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < 2 * pw; ++j)
+        win_words[(uint64_t)j * stride + i] = (uint64_t)w32[2 * j] | ((uint64_t)w32[2 * j + 1] << 32);
+#pragma unroll
+    for (uint32_t j = 0; j < pw; ++j)
+        win_nwords[(uint64_t)j * stride + i] = (uint64_t)n32[2 * j] | ((uint64_t)n32[2 * j + 1] << 32);
+    const uint8_t f = (uint8_t)((pr.flags & ~FC2_PAIR_WIN_N) | (anyN ? FC2_PAIR_WIN_N : 0u));
+    if (f != pr.flags) pairs[i].flags = f;
+}
+
 // Persistent form of the STAGE + cooperative kernel (read-order batch over a large genome, l + 2
 // <= 128): the grid is sized to the resident capacity of the chip, each block stages the LDS
 // tables ONCE and then walks the batch's 256-pair tiles t = blockIdx.x + k * gridDim.x.  At
@@ -1080,6 +1194,40 @@ int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_vi
     hipLaunchKernelGGL(probe_pattern_kernel, dim3((unsigned)((b.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p, g,
                        b, out);
     return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+void launch_scan32_win(int pw, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+                       const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
+    const unsigned grid = (unsigned)((b.n + kBlock - 1) / kBlock);
+#define FC2_LW(PWV)                                                                                          \
+    do {                                                                                                     \
+        if (nt) hipLaunchKernelGGL((bp_scan32_win_kernel<PWV, true>), dim3(grid), dim3(kBlock), 0, s, p, g, b,  \
+                                   out, tiemask, tw);                                                        \
+        else hipLaunchKernelGGL((bp_scan32_win_kernel<PWV, false>), dim3(grid), dim3(kBlock), 0, s, p, g, b,    \
+                                out, tiemask, tw);                                                           \
+    } while (0)
+    switch (pw) {
+        case 1: FC2_LW(1); break;
+        case 2: FC2_LW(2); break;
+        case 3: FC2_LW(3); break;
+        default: FC2_LW(4); break;
+    }
+#undef FC2_LW
+}
+
+void launch_gather_windows(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, uint64_t n, uint64_t stride,
+                           fc2_pair *pairs, uint64_t *win_words, uint64_t *win_nwords, uint32_t pw) {
+    const dim3 grid((unsigned)((n + kBlock - 1) / kBlock));
+    switch (pw) {
+        case 1: hipLaunchKernelGGL(gather_windows_kernel<1>, grid, dim3(kBlock), 0, s, p, g, n, stride, pairs, win_words,
+                                   win_nwords); break;
+        case 2: hipLaunchKernelGGL(gather_windows_kernel<2>, grid, dim3(kBlock), 0, s, p, g, n, stride, pairs, win_words,
+                                   win_nwords); break;
+        case 3: hipLaunchKernelGGL(gather_windows_kernel<3>, grid, dim3(kBlock), 0, s, p, g, n, stride, pairs, win_words,
+                                   win_nwords); break;
+        default: hipLaunchKernelGGL(gather_windows_kernel<4>, grid, dim3(kBlock), 0, s, p, g, n, stride, pairs,
+                                    win_words, win_nwords); break;
+    }
 }
 
 bool persist_ok(int nq, const fc2_genome_view &g) {

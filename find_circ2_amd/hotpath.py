@@ -102,6 +102,8 @@ class PairBatch:
         self.slot = None           # reorder() output: torch int32 [n], device twin of perm
         self.reorder_info = None
         self.workspace = None
+        self.win_words = self.win_nwords = None   # window-carrying form (fc2_batch_view.win_words)
+        self.pw = 0
 
     # -------------------------------------------------------------- from reads
     @classmethod
@@ -250,8 +252,55 @@ class PairBatch:
         return self.perm
 
     def view(self) -> N.BatchView:
+        carried = self.win_words is not None
         return N.BatchView(self.pairs.data_ptr(), self.read_words.data_ptr(), self.read_nwords.data_ptr(),
-                           self.n, self.stride, self.rw, self.nw, self.max_l, self.layout)
+                           self.n, self.stride, self.rw, self.nw, self.max_l, self.layout,
+                           self.win_words.data_ptr() if carried else None,
+                           self.win_nwords.data_ptr() if carried else None,
+                           2 * self.pw if carried else 0, self.pw if carried else 0)
+
+    # -------------------------------------------------------------- window-carrying form
+    def _alloc_windows(self):
+        torch = _torch()
+        p = self.options.params()
+        pw, ww, wnw = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+        N.check(N.lib().fc2_window_geometry(ctypes.byref(p), self.max_l + 2 * self.options.eff_a, ctypes.byref(pw),
+                                            ctypes.byref(ww), ctypes.byref(wnw)))
+        self.pw = pw.value
+        return torch, p
+
+    def carry_windows_from_fasta(self, genome: Genome, n_threads: int = 0) -> "PairBatch":
+        """North_star's form: Af / Bf of every pair read on the host from the mmap'd FASTA
+        (fc2_pack_windows, get_data semantics find_circ.py:189-215) and uploaded with the
+        batch; the scan then gathers nothing from the genome (only chromosome sizes)."""
+        torch, p = self._alloc_windows()
+        if genome.fasta is None:
+            raise RuntimeError("host window packing needs a FASTA-backed genome")
+        hp = self.fetch_host_pairs().copy()
+        ww = np.zeros(2 * self.pw * self.stride, np.uint64)
+        wn = np.zeros(self.pw * self.stride, np.uint64)
+        N.check(N.lib().fc2_pack_windows(ctypes.byref(p), genome.fasta, self.n, hp.ctypes.data, ww.ctypes.data,
+                                         wn.ctypes.data, self.pw, self.stride, int(n_threads)))
+        self.host_pairs = hp
+        self.pairs = torch.from_numpy(hp.view(np.uint8).copy()).to(self.device)
+        self.win_words = torch.from_numpy(ww.view(np.int64)).to(self.device)
+        self.win_nwords = torch.from_numpy(wn.view(np.int64)).to(self.device)
+        return self
+
+    def carry_windows_from_device(self, genome: Genome) -> "PairBatch":
+        """The same rows gathered on the device from the resident genome
+        (fc2_gather_windows_launch; synthetic workloads, which have no FASTA)."""
+        torch, p = self._alloc_windows()
+        self.win_words = torch.empty(2 * self.pw * self.stride, dtype=torch.int64, device=self.device)
+        self.win_nwords = torch.empty(self.pw * self.stride, dtype=torch.int64, device=self.device)
+        gv, bv = genome.view(), self.view()
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        N.check(N.lib().fc2_gather_windows_launch(ctypes.byref(p), ctypes.byref(gv), ctypes.byref(bv),
+                                                  self.pairs.data_ptr(), self.win_words.data_ptr(),
+                                                  self.win_nwords.data_ptr(), self.pw, stream))
+        torch.cuda.synchronize(self.device)
+        self.host_pairs = None
+        return self
 
     def bytes_view(self) -> N.BytesView:
         return N.BytesView(self.bp_index.data_ptr(), self.bp_pairs.data_ptr(), self.bp_arena.data_ptr(),

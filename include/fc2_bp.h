@@ -63,6 +63,7 @@ typedef struct fc2_params {
 #define FC2_PAIR_BYTEPATH    0x08u  /* evaluated by the byte-exact kernel (exotic bytes,
                                        irregular FASTA line layout, very long reads) */
 #define FC2_PAIR_SKIP        0x10u  /* not evaluated (e.g. not is_uniq, :1299): no hit */
+#define FC2_PAIR_WIN_N       0x20u  /* window-carrying batch: this pair's window N rows are present */
 
 typedef struct fc2_pair {
     int32_t  a_pos;     /* align_A.pos  (0-based)                                    */
@@ -152,6 +153,21 @@ typedef struct fc2_batch_view {
     uint32_t nw;
     int32_t  max_l;              /* largest l = L - 2e of a non-BYTEPATH pair (selects the kernel width) */
     uint32_t layout;             /* FC2_BATCH_* hints (results never depend on them) */
+    /* Optional window-carrying form (north_star's "two genome windows per pair streamed from the
+     * FASTA"; SURVEY.md §8(b) win_2bit): when win_words != NULL the scan reads each pair's windows
+     * Af, Bf (find_circ.py:900-902) from these rows instead of gathering them from the genome view
+     * (which then needs only chrom_size / n_chrom).  pw = ceil((max_l + 2) / 32) <= 4 32-bit words
+     * per plane; pair i's row is ww = 2*pw 64-bit words at win_words[j*stride + i], read as 4*pw
+     * 32-bit words: plane p (0 A-low, 1 A-high, 2 B-low, 3 B-high code bits) word k at 32-bit index
+     * p*pw + k, bit b = window position 32k + b (positions >= l + 2 zero).  'N' (incl. positions
+     * outside the chromosome) = code 00 + a bit in the N row: wnw = pw words at
+     * win_nwords[j*stride + i] (A-N words 0..pw-1, B-N words pw..2pw-1), read only for pairs
+     * flagged FC2_PAIR_WIN_N.  Built by fc2_pack_windows (host, mmap'd FASTA) or
+     * fc2_gather_windows_launch (device, resident genome). */
+    const uint64_t *win_words;
+    const uint64_t *win_nwords;
+    uint32_t ww;
+    uint32_t wnw;
 } fc2_batch_view;
 #define FC2_BATCH_LOCUS_ORDERED 0x1u  /* pairs are sorted by genome locus (fc2_reorder_launch output or a
                                          host-sorted batch): the scan deals each XCD a contiguous range */
@@ -175,6 +191,13 @@ int         fc2_abi_version(void);
 const char *fc2_last_error(void);
 /* Returns FC2_OK and the device count (0 on a host without GPUs is not an error). */
 int         fc2_device_count(int *count);
+
+/* Device side of the window-carrying form: the same rows as fc2_pack_windows, gathered from the
+ * resident genome (needs g->wt); b supplies pairs/n/stride/max_l, pairs (device, = b->pairs) get
+ * FC2_PAIR_WIN_N set or cleared. */
+int         fc2_gather_windows_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                                      fc2_pair *pairs, uint64_t *win_words, uint64_t *win_nwords, uint32_t pw,
+                                      void *stream);
 
 /* Measurement only: the read-order scan's memory pattern (16-B records and read rows streamed, both
  * windows' word pairs gathered exactly where the scan gathers them, 8-B word per pair stored into
@@ -295,6 +318,15 @@ int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t n,
                    fc2_pair *pairs_io, uint64_t *read_words, uint32_t rw,
                    uint64_t *read_nwords, uint32_t nw, uint64_t stride,
                    uint64_t *n_bytepath, int n_threads);
+
+/* Window rows (fc2_batch_view.win_words) for reads up to max_read_len: *pw plane words,
+ * *ww = 2*pw row words, *wnw = pw N-row words; FC2_E_RANGE when l + 2 > 128. */
+int fc2_window_geometry(const fc2_params *p, int max_read_len, uint32_t *pw, uint32_t *ww, uint32_t *wnw);
+/* Host side of the window-carrying form: Af / Bf of every packed, non-SKIP, non-BYTEPATH pair with
+ * l >= 0, read from the mmap'd FASTA with get_data's semantics (find_circ.py:189-215, uppercased as
+ * at :901-902), into rows of pw plane words; sets FC2_PAIR_WIN_N where a window holds an 'N'. */
+int fc2_pack_windows(const fc2_params *p, const fc2_fasta *f, uint64_t n, fc2_pair *pairs_io,
+                     uint64_t *win_words, uint64_t *win_nwords, uint32_t pw, uint64_t stride, int n_threads);
 
 /* Size (bytes) of the byte-path arena for the pairs flagged BYTEPATH. */
 int fc2_bytepath_size(const fc2_params *p, uint64_t n, const fc2_pair *pairs, uint64_t *m,

@@ -1,0 +1,6 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_windows.py -x -v --timeout 300 --timeout-method thread > gpurun_out/win_tests.log 2>&1 && echo WIN_TESTS_OK &&
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 && echo TESTS_OK &&
+timeout -k 10 400 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err && echo BENCH_OK && python -c "
+import json; d=json.load(open('gpurun_out/bench.json')); print(d['value'], d['roofline']); print(json.dumps(d['extra'], indent=1))"
