@@ -38,7 +38,9 @@ def main():
     os.makedirs(a.out, exist_ok=True)
     fa = os.path.join(a.out, "hg19_shaped.fa")
     if not os.path.exists(fa):
+        print("writing", fa, file=sys.stderr, flush=True)
         write_fasta(fa, names, sizes)
+        print("written", file=sys.stderr, flush=True)
     L = N.lib()
     h = ctypes.c_void_p()
     N.check(L.fc2_fasta_open(fa.encode(), 0, ctypes.byref(h)))
@@ -67,7 +69,7 @@ def main():
         out["cpu_model"] = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
     except Exception:
         pass
-    for T in sorted({1, threads}):
+    for T in sorted({1, 4, threads}):
         m = n if T > 1 else max(1, n // 8)
         t0 = time.perf_counter()
         N.check(L.fc2_pack_windows(ctypes.byref(p), h, m, hp.ctypes.data, words.ctypes.data, nwords.ctypes.data,
