@@ -15,7 +15,8 @@
 namespace {
 
 // Measurement-only ablations (scripts/ablate_build.sh; WRONG results, never in the shipped library):
-// bit 0 skips the owner's third-unit loads, bit 1 skips N-plane loads of flagged windows.
+// bit 0 skips the owner's third-unit loads, bit 1 skips N-plane loads of flagged windows, bit 2
+// skips the canonical candidate walk.
 #ifndef FC2_ABLATE
 #define FC2_ABLATE 0
 #endif
@@ -853,6 +854,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
             cw[k] = floor_k <= p.maxdist ? (plus[k] | minus[k]) : 0u;
             live |= (cw[k] ? 1u : 0u) << k;
         }
+        if (FC2_ABLATE & 4) live = 0;     // timing-only: no candidate walk
         while (live) {
             const int k = __ffs(live) - 1;
             live &= live - 1;

@@ -55,7 +55,23 @@ def main():
     import ctypes
     junk = torch.empty(b.n, dtype=torch.int64, device=dev)
 
+    win = {}
+
     def run(v):
+        if v == "carried":        # window-carrying form: rows gathered once (untimed), sizes-only genome view
+            if not win:
+                b.carry_windows_from_device(g)
+                win["gv"] = N.GenomeView(None, None, None, None, g.d_chrom_size.data_ptr(), 0, len(g.names), 0,
+                                         None, None, 0, 0, None, 0, 0)
+                win["bv"] = b.view()
+                win["rows"] = (b.win_words, b.win_nwords)      # keep the rows alive
+                b.win_words = b.win_nwords = None
+                b.pw = 0
+            pv = opt.params()
+            N.check(N.lib().fc2_bp_scan_launch(ctypes.byref(pv), ctypes.byref(win["gv"]), ctypes.byref(win["bv"]),
+                                               out.results.data_ptr(), None, b.tw,
+                                               torch.cuda.current_stream(dev).cuda_stream))
+            return
         if v == "probe":          # the scan's access pattern without its arithmetic (fc2_probe_pattern_launch)
             gv, bv, pv = g.view(), b.view(), opt.params()
             N.check(N.lib().fc2_probe_pattern_launch(ctypes.byref(pv), ctypes.byref(gv), ctypes.byref(bv),
