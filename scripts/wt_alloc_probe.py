@@ -34,6 +34,8 @@ def main():
     hip = ctypes.CDLL("libamdhip64.so")
     nbytes = g.wt_bytes
     tables = {"torch": g.wt}
+    for k in range(int(os.environ.get("WT_EXTRA", "0"))):      # more plain torch allocations
+        tables["torch_%d" % k] = torch.empty(nbytes // 4, dtype=torch.int32, device=dev)
     big = torch.empty(nbytes // 4 + (4 << 20) // 4, dtype=torch.int32, device=dev)
     off = (-big.data_ptr()) % (2 << 20)
     tables["torch_2m"] = big[off // 4: off // 4 + nbytes // 4]
