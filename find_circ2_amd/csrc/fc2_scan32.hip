@@ -1132,9 +1132,15 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_persist_kernel(fc2_params p,
         s_cstart[k1] = a1; s_csize[k1] = z1;
     }
     __syncthreads();
-    for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x)
-        scan_pair<NQ, NT, true, false>(p, g, bv, out, tiemask, tw, t * kBlock + threadIdx.x, s_cstart, s_csize, true,
-                                s_nsuper_buf, s_xchg[threadIdx.x >> 6]);
+    if (g.wt) {                 // word-pair windows (uniform branch)
+        for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x)
+            scan_pair<NQ, NT, true, true>(p, g, bv, out, tiemask, tw, t * kBlock + threadIdx.x, s_cstart, s_csize,
+                                          true, s_nsuper_buf, s_xchg[threadIdx.x >> 6]);
+    } else {
+        for (uint64_t t = blockIdx.x; t < n_tiles; t += gridDim.x)
+            scan_pair<NQ, NT, true, false>(p, g, bv, out, tiemask, tw, t * kBlock + threadIdx.x, s_cstart, s_csize,
+                                           true, s_nsuper_buf, s_xchg[threadIdx.x >> 6]);
+    }
 }
 
 // Speed-of-light probe of the read-order scan (measurement only, fc2_probe_pattern_launch): the
