@@ -368,10 +368,12 @@ def kernel_label(g, ordered: bool) -> str:
     staged = (not ordered) and (not g.dummy) and g.n_units * 16 >= (64 << 20)
     words = g.wt is not None
     if staged:
+        if words:
+            return ("bp_scan32_stage_bt_kernel<512,NT> (one anchor pair per lane, 512-pair blocks; chromosome table "
+                    "+ super-coarse N map in LDS; each window's 32 B of word pairs loaded by a lane pair in one "
+                    "request, from whichever genome copy holds it inside one 128-B line)")
         return ("bp_scan32_kernel<4,NT,STAGE> (one anchor pair per lane; chromosome table + super-coarse N map in "
-                "LDS; %s)" % ("each window's 32 B of word pairs loaded by a lane pair in one request, from whichever "
-                              "genome copy holds it inside one 128-B line" if words else
-                              "lane pairs load each window line with one L2 request"))
+                "LDS; lane pairs load each window line with one L2 request)")
     return "bp_scan32_kernel<4,NT> (one anchor pair per lane%s)" % ("; word-pair windows" if words else "")
 
 

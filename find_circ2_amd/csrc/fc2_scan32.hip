@@ -1099,6 +1099,33 @@ __global__ __launch_bounds__(kBlock) void gather_windows_kernel(fc2_params p, fc
     if (f != pr.flags) pairs[i].flags = f;
 }
 
+// The STAGE + cooperative word-pair form with BT-thread blocks (FC2_TUNE_STAGE_BLOCK): the LDS
+// tables are staged once per BT pairs instead of once per 256 (each staging is ~60 L2 requests).
+template <int BT, bool NT>
+__global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+                                                                uint64_t *__restrict__ out,
+                                                                uint64_t *__restrict__ tiemask, uint32_t tw) {
+    __shared__ uint64_t s_cstart[kChromLds];
+    __shared__ int64_t s_csize[kChromLds];
+    __shared__ __attribute__((aligned(16))) uint32_t s_nsuper_buf[kSuperLds];
+    __shared__ ulonglong2 s_xchg[BT / 64][4 * 64];
+    // the launcher guarantees: genome not dummy, word-pair table, tables fit in LDS
+    for (uint32_t w = 4 * threadIdx.x; w < (uint32_t)kSuperLds; w += 4 * BT) {
+        uint4 q = uint4{0u, 0u, 0u, 0u};
+        if (w < g.nsuper_words) q = *reinterpret_cast<const uint4 *>(g.nsuper + w);
+        *reinterpret_cast<uint4 *>(s_nsuper_buf + w) = q;
+    }
+    for (uint32_t k = threadIdx.x; k < (uint32_t)kChromLds; k += BT) {
+        const bool in = k < g.n_chrom;
+        s_cstart[k] = in ? g.chrom_start[k] : 0ull;
+        s_csize[k] = in ? g.chrom_size[k] : 0ll;
+    }
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * BT + threadIdx.x;
+    scan_pair<4, NT, true, true>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, true, s_nsuper_buf,
+                                 s_xchg[threadIdx.x >> 6]);
+}
+
 // Persistent form of the STAGE + cooperative kernel (read-order batch over a large genome, l + 2
 // <= 128): the grid is sized to the resident capacity of the chip, each block stages the LDS
 // tables ONCE and then walks the batch's 256-pair tiles t = blockIdx.x + k * gridDim.x.  At
@@ -1236,6 +1263,27 @@ void launch_gather_windows(hipStream_t s, const fc2_params &p, const fc2_genome_
         default: hipLaunchKernelGGL(gather_windows_kernel<4>, grid, dim3(kBlock), 0, s, p, g, n, stride, pairs,
                                     win_words, win_nwords); break;
     }
+}
+
+bool stage_bt_ok(int nq, const fc2_genome_view &g) {
+    return nq <= 4 && !g.dummy && g.wt && g.n_chrom <= (uint32_t)kChromLds && g.nsuper &&
+           g.nsuper_words <= (uint32_t)kSuperLds;
+}
+
+void launch_scan32_stage_bt(int bt, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+                            const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
+#define FC2_LBT(BTV)                                                                                          \
+    do {                                                                                                      \
+        const dim3 grid((unsigned)((b.n + BTV - 1) / BTV));                                                   \
+        if (nt) hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<BTV, true>), grid, dim3(BTV), 0, s, p, g, b, out,  \
+                                   tiemask, tw);                                                              \
+        else hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<BTV, false>), grid, dim3(BTV), 0, s, p, g, b, out,    \
+                                tiemask, tw);                                                                 \
+    } while (0)
+    if (bt >= 1024) FC2_LBT(1024);
+    else if (bt >= 512) FC2_LBT(512);
+    else FC2_LBT(256);
+#undef FC2_LBT
 }
 
 bool persist_ok(int nq, const fc2_genome_view &g) {

@@ -50,6 +50,8 @@ def main():
         m = re.search(r"pe(A|\d+)", v)   # FC2_TUNE_PERSIST: peA = occupancy-sized grid, peK = K blocks/CU
         # knobs an older library (FC2_LIB_VARIANT) may not have: set unchecked, default when absent
         N.lib().fc2_set_tuning(11, 0 if "wo0" in v else 1)                       # FC2_TUNE_WORDS
+        mb = re.search(r"bt(\d+)", v)                                            # FC2_TUNE_STAGE_BLOCK
+        N.lib().fc2_set_tuning(13, int(mb.group(1)) if mb else 512)
         N.lib().fc2_set_tuning(10, 0 if not m else (-1 if m.group(1) == "A" else int(m.group(1))))
 
     import ctypes

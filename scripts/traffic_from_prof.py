@@ -14,7 +14,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERN = "bp_scan"
+KERN = "bp_scan"          # bp_scan32_kernel / bp_scan32_stage_bt_kernel / bp_scan_kernel
 N_PAIRS = 50_000_000
 
 

@@ -21,13 +21,16 @@ pytestmark = pytest.mark.gpu
 from find_circ2_amd import Genome, Options, PairBatch, SynthConfig, scan, sq_table  # noqa: E402
 from find_circ2_amd import _native as N  # noqa: E402
 
-# knob values per form: FC2_TUNE_KERNEL32 (2), STAGE (7), TWIN (6), PERSIST (10), WORDS (11)
-KNOBS = (2, 7, 6, 10, 11)
-FORMS = {"scan32_staged_coop_words": (1, 1, 1, 0, 1), "scan32_staged_coop_units_twin": (1, 1, 1, 0, 0),
-         "scan32_persistent_coop_twin": (1, 1, 1, -1, 0), "scan32_persistent_3_per_cu": (1, 1, 1, 3, 0),
-         "scan32_plain_words_no_twin": (1, 0, 0, 0, 1), "scan32_plain_words_twin": (1, 0, 1, 0, 1),
-         "scan32_plain_units_no_twin": (1, 0, 0, 0, 0), "scan32_plain_units_twin": (1, 0, 1, 0, 0),
-         "scan64": (0, 0, 0, 0, 1)}
+# knob values per form: FC2_TUNE_KERNEL32 (2), STAGE (7), TWIN (6), PERSIST (10), WORDS (11), STAGE_BLOCK (13)
+KNOBS = (2, 7, 6, 10, 11, 13)
+FORMS = {"scan32_staged_coop_words": (1, 1, 1, 0, 1, 256), "scan32_staged_coop_words_512": (1, 1, 1, 0, 1, 512),
+         "scan32_staged_coop_words_1024": (1, 1, 1, 0, 1, 1024),
+         "scan32_staged_coop_units_twin": (1, 1, 1, 0, 0, 256),
+         "scan32_persistent_coop_words": (1, 1, 1, -1, 1, 256), "scan32_persistent_coop_twin": (1, 1, 1, -1, 0, 256),
+         "scan32_persistent_3_per_cu": (1, 1, 1, 3, 0, 256),
+         "scan32_plain_words_no_twin": (1, 0, 0, 0, 1, 256), "scan32_plain_words_twin": (1, 0, 1, 0, 1, 256),
+         "scan32_plain_units_no_twin": (1, 0, 0, 0, 0, 256), "scan32_plain_units_twin": (1, 0, 1, 0, 0, 256),
+         "scan64": (0, 0, 0, 0, 1, 256)}
 DEFAULTS = {k: N.get_tuning(k) for k in KNOBS}
 
 
