@@ -783,8 +783,8 @@ int g_extra_lds = 0;   // bytes of unused dynamic LDS per scan block (occupancy 
 int g_stage = 2;       // bp_scan32 LDS staging: 0 never, 1 always, 2 read-order batch over a large genome
 int g_twin = 2;        // units_twin: 0 never, 1 always, 2 for batches not flagged locus-ordered
 int g_words = 1;       // read-order STAGE scan uses the word-pair layout when the view carries one
-int g_persist = 0;
-int g_stage_block = 512;  // threads per block of the LDS-staging word-pair scan (FC2_TUNE_STAGE_BLOCK)     // persistent STAGE kernel: 0 off, -1 occupancy-sized grid, k > 0 k blocks per CU
+int g_persist = 0;      // persistent STAGE kernel: 0 off, -1 occupancy-sized grid, k > 0 k blocks per CU
+int g_stage_block = 512; // threads per block of the LDS-staging word-pair scan (FC2_TUNE_STAGE_BLOCK)
 inline bool stream_nt() { return g_stream_nt != 0; }
 
 }  // namespace
