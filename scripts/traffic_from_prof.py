@@ -32,11 +32,12 @@ def agg(prof, name):
 def kstats(prof, name):
     p = os.path.join(prof, name, "kt_kernel_stats.csv")
     if not os.path.exists(p):
-        return None, 0
+        return None, 0, None
     for r in csv.DictReader(open(p)):
         if KERN in r["Name"]:
-            return float(r["AverageNs"]), int(r["Calls"])
-    return None, 0
+            return float(r["AverageNs"]), int(r["Calls"]), r["Name"].split("(fc2_params")[0].replace(
+                "void (anonymous namespace)::", "")
+    return None, 0, None
 
 
 def main():
@@ -46,12 +47,11 @@ def main():
     for w, key in (("hg19", "hg19"), ("hg19o", "hg19_locus_ordered"), ("cdr1as", "cdr1as_50M_calibration")):
         f, wr, h = agg(prof, "fetch_" + w), agg(prof, "write_" + w), agg(prof, "hit_" + w)
         rq = agg(prof, "req_" + w)
-        ns, calls = kstats(prof, "kt_" + w)
+        ns, calls, kname = kstats(prof, "kt_" + w)
         if not f:
             continue
         hbm = 2 * f["FETCH_SIZE"] * 1024 + wr.get("WRITE_SIZE", 0) * 1024
-        out[key] = {"pairs_per_launch": N_PAIRS, "kernel": ("bp_scan32_kernel<4,NT,STAGE>" if w == "hg19"
-                                                             else "bp_scan32_kernel<4,NT>"),
+        out[key] = {"pairs_per_launch": N_PAIRS, "kernel": kname,
                     "avg_kernel_ns_rocprof": ns,
                     "FETCH_SIZE_kB_raw": f["FETCH_SIZE"], "WRITE_SIZE_kB": wr.get("WRITE_SIZE"),
                     "TCC_HIT_sum": h.get("TCC_HIT_sum"), "TCC_MISS_sum": h.get("TCC_MISS_sum"),
