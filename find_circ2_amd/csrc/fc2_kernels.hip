@@ -785,6 +785,7 @@ int g_twin = 2;        // units_twin: 0 never, 1 always, 2 for batches not flagg
 int g_words = 1;       // read-order STAGE scan uses the word-pair layout when the view carries one
 int g_persist = 0;      // persistent STAGE kernel: 0 off, -1 occupancy-sized grid, k > 0 k blocks per CU
 int g_stage_block = 512; // threads per block of the LDS-staging word-pair scan (FC2_TUNE_STAGE_BLOCK)
+int g_tri = 2;           // three-lane window loads: 0 never, 1 always, 2 when windows exceed 97 bases (FC2_TUNE_TRI)
 inline bool stream_nt() { return g_stream_nt != 0; }
 
 }  // namespace
@@ -839,8 +840,10 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         const bool stage = g_stage == 2 ? (big && !ordered) : g_stage != 0;
         const int opts = sw ? fc2::kOptSwizzle : 0;
         const int nq = (ml + 2 + 31) / 32;
-        if (stage && g_stage_block != 256 && g_persist == 0 && fc2::stage_bt_ok(nq, gv)) {
-            fc2::launch_scan32_stage_bt(g_stage_block, nt, s, *p, gv, *b, out, tiemask, tw);
+        if (stage && (g_stage_block != 256 || g_tri == 1 || (g_tri == 2 && ml + 2 > 97)) && g_persist == 0 &&
+            fc2::stage_bt_ok(nq, gv)) {
+            const bool tri = g_tri == 1 || (g_tri == 2 && ml + 2 > 97);   // 5-pair windows: three-lane loads
+            fc2::launch_scan32_stage_bt(g_stage_block, tri, nt, s, *p, gv, *b, out, tiemask, tw);
             return hip_check(hipGetLastError(), "bp_scan32_stage_bt_kernel launch");
         }
         if (stage && g_persist != 0 && fc2::persist_ok(nq, gv)) {
@@ -1008,6 +1011,9 @@ extern "C" int fc2_set_tuning(int key, int value) {
             if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: twin is 0, 1 or 2");
             g_twin = value; return FC2_OK;
         case FC2_TUNE_WORDS: g_words = value ? 1 : 0; return FC2_OK;
+        case FC2_TUNE_TRI:
+            if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: tri is 0, 1 or 2");
+            g_tri = value; return FC2_OK;
         case FC2_TUNE_STAGE_BLOCK:
             if (value != 256 && value != 512 && value != 1024)
                 return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: stage block is 256, 512 or 1024");
@@ -1040,6 +1046,7 @@ extern "C" int fc2_get_tuning(int key, int *value) {
         case FC2_TUNE_PERSIST: *value = g_persist; return FC2_OK;
         case FC2_TUNE_WORDS: *value = g_words; return FC2_OK;
         case FC2_TUNE_STAGE_BLOCK: *value = g_stage_block; return FC2_OK;
+        case FC2_TUNE_TRI: *value = g_tri; return FC2_OK;
         case FC2_TUNE_REORDER_SHIFT: *value = fc2::g_reorder_shift; return FC2_OK;
         default: return fc2::fail(FC2_E_PARAM, "fc2_get_tuning: unknown key");
     }

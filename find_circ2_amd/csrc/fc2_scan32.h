@@ -20,7 +20,8 @@ void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc
                            int blocks_per_cu);   // 0: the occupancy limit
 // STAGE + cooperative word-pair form with bt-thread blocks (256/512/1024); usable when stage_bt_ok().
 bool stage_bt_ok(int nq, const fc2_genome_view &g);
-void launch_scan32_stage_bt(int bt, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+// tri: three-lane window loads (batches with windows longer than 97 bases)
+void launch_scan32_stage_bt(int bt, bool tri, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                             const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw);
 // Window-carrying batches (b.win_words): PW = plane words, 1..4.
 void launch_scan32_win(int pw, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,

@@ -16,7 +16,7 @@ namespace {
 
 // Measurement-only ablations (scripts/ablate_build.sh; WRONG results, never in the shipped library):
 // bit 0 skips the owner's third-unit loads, bit 1 skips N-plane loads of flagged windows, bit 2
-// skips the canonical candidate walk.
+// skips the canonical candidate walk, bit 3 skips the fifth word pair of windows with W > 97.
 #ifndef FC2_ABLATE
 #define FC2_ABLATE 0
 #endif
@@ -386,13 +386,18 @@ struct WinW {
     uint32_t n4;        // N-plane word q0+4
 };
 
-__device__ __forceinline__ void window_geom_w(const fc2_genome_view &g, uint64_t cstart, int64_t ws, int W, WinW &R) {
+// tri: the window is read as a 48-B region from its run start, so the run must start within the
+// first 80 B of its line: the copy is chosen by start offset (main copy if <= 80 B into the line,
+// else the shifted copy, where it starts 16..64 B in) instead of by run end.
+__device__ __forceinline__ void window_geom_w(const fc2_genome_view &g, uint64_t cstart, int64_t ws, int W, WinW &R,
+                                              bool tri = false) {
     const int64_t g0 = (int64_t)cstart + ws;
     const int32_t q0 = (int32_t)(g0 >> 5);
     R.q0 = (uint32_t)q0;
     R.sh = (unsigned)(g0 & 31);
     R.nwd = ((int)R.sh + W + 31) >> 5;
-    const bool twin = (int)(q0 & 15) + R.nwd > 16;          // would cross a 128-B line of the main copy
+    const bool twin = tri ? (q0 & 15) > 10                   // would start more than 80 B into a main line
+                          : (int)(q0 & 15) + R.nwd > 16;     // would cross a 128-B line of the main copy
     R.off = twin ? (uint32_t)g.wt_twin_off + (uint32_t)(q0 + 8) * 8u : 128u + (uint32_t)q0 * 8u;   // main copy: 16 zero pairs in front
 }
 
@@ -440,7 +445,7 @@ __device__ __forceinline__ void windows_issue_w(const fc2_genome_view &g, __amdg
     for (int x = 0; x < 2; ++x) {
         WinW &Q = *R[x];
         Q.v4 = u32x2{0u, 0u};
-        if (active && Q.nwd > 4) Q.v4 = __builtin_amdgcn_raw_buffer_load_b64(rs, Q.off + 32u, 0, 0);
+        if (!(FC2_ABLATE & 8) && active && Q.nwd > 4) Q.v4 = __builtin_amdgcn_raw_buffer_load_b64(rs, Q.off + 32u, 0, 0);
     }
 #pragma unroll
     for (int x = 0; x < 2; ++x) {
@@ -528,6 +533,101 @@ __device__ __forceinline__ void window_nwords_plain(const fc2_genome_view &g, __
         }
         R.n03 = u32x4{nw[0], nw[1], nw[2], nw[3]};
         R.n4 = nw[4];
+    }
+}
+
+// Three-lane form of the cooperative word-pair loads, for batches with windows longer than 97
+// bases (150-bp reads: a window needs 5 pairs = 40 B, more than two 16-B lane loads).  Each window is
+// read as the 48 B from its run start r -- inside one 128-B line because the copy is picked so
+// that r lies at most 80 B into its line (window_geom_w, tri) -- by three consecutive lanes of ONE
+// instruction: 21 windows per
+// instruction, 7 instructions for the wave's 128 windows, one L2 request per window (the two-lane
+// form spends a second request on the owner's fifth-pair load: +13 % at 150 bp, ab_fifth_pair.jsonl).
+__device__ __forceinline__ void windows_issue_w3(const fc2_genome_view &g, __amdgpu_buffer_rsrc_t rs,
+                                                 __amdgpu_buffer_rsrc_t rn, const uint32_t *s_nsuper,
+                                                 uint64_t cstart, int64_t wsA, int64_t wsB, int W, bool active,
+                                                 WinW &rA, WinW &rB, u32x4 (&cl)[7]) {
+    window_geom_w(g, cstart, wsA, W, rA, true);
+    window_geom_w(g, cstart, wsB, W, rB, true);
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t wsx[2] = {wsA, wsB};
+    WinW *R[2] = {&rA, &rB};
+    const uint32_t sA = rA.off, sB = rB.off;                // region = [off, off + 48), inside one line
+    uint32_t src[7];
+    int part[7];
+    bool ok[7];
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+        const int w = 21 * c + lane / 3;                  // window served by this lane in instruction c
+        ok[c] = lane < 63 && w < 128;
+        part[c] = lane % 3;
+        const int owner = w & 63;
+        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sA);
+        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sB);
+        src[c] = (w >> 6) ? b : a;
+    }
+    uint32_t sw[2][2] = {{0u, 0u}, {0u, 0u}}, sb[2][2] = {{0u, 0u}, {0u, 0u}};
+    bool sv[2] = {false, false};
+    if (!(FC2_ABLATE & 2) && s_nsuper) {
+        const int64_t top = (int64_t)(g.n_units * 64) - 1;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            int64_t lo = (int64_t)cstart + wsx[x], hi = lo + W - 1;
+            lo = lo < 0 ? 0 : lo;
+            hi = hi > top ? top : hi;
+            sv[x] = active && lo <= hi;
+            const uint32_t k0 = sv[x] ? (uint32_t)((uint64_t)lo >> g.nsuper_shift) : 0u,
+                           k1 = sv[x] ? (uint32_t)((uint64_t)hi >> g.nsuper_shift) : 0u;
+            sw[x][0] = s_nsuper[k0 >> 5];
+            sw[x][1] = s_nsuper[k1 >> 5];
+            sb[x][0] = k0 & 31u;
+            sb[x][1] = k1 & 31u;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 7; ++c) {
+        cl[c] = u32x4{0u, 0u, 0u, 0u};
+        if (ok[c]) cl[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, src[c] + 16u * (uint32_t)part[c], 0, 0);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        WinW &Q = *R[x];
+        Q.v4 = u32x2{0u, 0u};
+        const bool nflag = sv[x] && (((sw[x][0] >> sb[x][0]) | (sw[x][1] >> sb[x][1])) & 1u);
+        Q.n03 = u32x4{0u, 0u, 0u, 0u};
+        Q.n4 = 0u;
+        if (nflag) {
+            uint32_t nw[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int32_t wj = (int32_t)Q.q0 + j;
+                nw[j] = 0u;
+                if (wj >= 0 && j < Q.nwd) nw[j] = __builtin_amdgcn_raw_buffer_load_b32(rn, (uint32_t)wj * 4u, 0, 0);
+            }
+            Q.n03 = u32x4{nw[0], nw[1], nw[2], nw[3]};
+            Q.n4 = nw[4];
+        }
+    }
+}
+
+// Owner side: the first 40 B of each window's three 16-B pieces from the wave's LDS slots.
+__device__ __forceinline__ void windows_exchange_w3(u32x4 *xchg, const u32x4 (&cl)[7], WinW &rA, WinW &rB) {
+    const int lane = (int)(threadIdx.x & 63);
+#pragma unroll
+    for (int c = 0; c < 7; ++c) xchg[c * 64 + lane] = cl[c];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    WinW *R[2] = {&rA, &rB};
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        WinW &Q = *R[x];
+        const int w = 64 * x + lane;
+        const int base = (w / 21) * 64 + 3 * (w % 21);
+        const u32x4 p0 = xchg[base], p1 = xchg[base + 1], p2 = xchg[base + 2];
+        Q.v0 = p0;
+        Q.v1 = p1;
+        Q.v4 = u32x2{p2.x, p2.y};
     }
 }
 
@@ -622,7 +722,7 @@ __device__ __forceinline__ uint64_t xcd_block(uint32_t b, uint32_t nwg) {
 // exchange, so exits are deferred through `active`.  xchg: this wave's 4 x 64 LDS slots.
 // PW > 0: window-carrying batch (fc2_batch_view.win_words, pw = PW): the windows arrive with the
 // record in round trip 1 and nothing is gathered from the genome (NQ == 4, !COOP, !WL).
-template <int NQ, bool NT, bool COOP, bool WL = false, int PW = 0>
+template <int NQ, bool NT, bool COOP, bool WL = false, int PW = 0, bool TRI = false>
 __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &bv,
                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask, uint32_t tw,
                                           uint64_t i, const uint64_t *s_cstart, const int64_t *s_csize, bool lds_tab,
@@ -695,6 +795,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     ulonglong2 cl[2][2];
     WinW wA, wB;
     u32x4 wcl[2][2];
+    u32x4 wcl3[TRI ? 7 : 1];
     uint64_t cwA = 0, cwB = 0;
     __amdgpu_buffer_rsrc_t rs, rn;
     if constexpr (WL) {
@@ -703,7 +804,12 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         rn = __builtin_amdgcn_make_buffer_rsrc((void *)g.nplane, 0,
                                                (int)(uint32_t)(nb > 0xFFFFFFFFull ? 0xFFFFFFFFull : nb), 0x00020000);
     }
-    if constexpr (COOP && WL) {
+    if constexpr (COOP && WL && TRI) {
+        static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
+        if (!active) W = 2;
+        windows_issue_w3(g, rs, rn, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active, wA,
+                         wB, wcl3);
+    } else if constexpr (COOP && WL) {
         static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
         if (!active) W = 2;
         windows_issue_w(g, rs, rn, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active, wA,
@@ -782,6 +888,11 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
             B.n[k] = k < PW ? n32[PW + (k < PW ? k : 0)] : 0u;
         }
         if (!active) return;
+    } else if constexpr (COOP && WL && TRI) {
+        windows_exchange_w3(reinterpret_cast<u32x4 *>(xchg), wcl3, wA, wB);
+        if (!active) return;
+        window_finish_w<NQ>(wA, csize, wsA, W, A);
+        window_finish_w<NQ>(wB, csize, wsB, W, B);
     } else if constexpr (COOP && WL) {
         windows_exchange_w(reinterpret_cast<u32x4 *>(xchg), wcl, wA, wB);
         if (!active) return;
@@ -1101,14 +1212,14 @@ __global__ __launch_bounds__(kBlock) void gather_windows_kernel(fc2_params p, fc
 
 // The STAGE + cooperative word-pair form with BT-thread blocks (FC2_TUNE_STAGE_BLOCK): the LDS
 // tables are staged once per BT pairs instead of once per 256 (each staging is ~60 L2 requests).
-template <int BT, bool NT>
+template <int BT, bool NT, bool TRI>
 __global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
                                                                 uint64_t *__restrict__ out,
                                                                 uint64_t *__restrict__ tiemask, uint32_t tw) {
     __shared__ uint64_t s_cstart[kChromLds];
     __shared__ int64_t s_csize[kChromLds];
     __shared__ __attribute__((aligned(16))) uint32_t s_nsuper_buf[kSuperLds];
-    __shared__ ulonglong2 s_xchg[BT / 64][4 * 64];
+    __shared__ ulonglong2 s_xchg[BT / 64][(TRI ? 7 : 4) * 64];
     // the launcher guarantees: genome not dummy, word-pair table, tables fit in LDS
     for (uint32_t w = 4 * threadIdx.x; w < (uint32_t)kSuperLds; w += 4 * BT) {
         uint4 q = uint4{0u, 0u, 0u, 0u};
@@ -1122,8 +1233,8 @@ __global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc
     }
     __syncthreads();
     const uint64_t i = (uint64_t)blockIdx.x * BT + threadIdx.x;
-    scan_pair<4, NT, true, true>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, true, s_nsuper_buf,
-                                 s_xchg[threadIdx.x >> 6]);
+    scan_pair<4, NT, true, true, 0, TRI>(p, g, bv, out, tiemask, tw, i, s_cstart, s_csize, true, s_nsuper_buf,
+                                         s_xchg[threadIdx.x >> 6]);
 }
 
 // Persistent form of the STAGE + cooperative kernel (read-order batch over a large genome, l + 2
@@ -1270,19 +1381,25 @@ bool stage_bt_ok(int nq, const fc2_genome_view &g) {
            g.nsuper_words <= (uint32_t)kSuperLds;
 }
 
-void launch_scan32_stage_bt(int bt, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+void launch_scan32_stage_bt(int bt, bool tri, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                             const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
-#define FC2_LBT(BTV)                                                                                          \
+#define FC2_LBT(BTV, TRV)                                                                                     \
     do {                                                                                                      \
         const dim3 grid((unsigned)((b.n + BTV - 1) / BTV));                                                   \
-        if (nt) hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<BTV, true>), grid, dim3(BTV), 0, s, p, g, b, out,  \
-                                   tiemask, tw);                                                              \
-        else hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<BTV, false>), grid, dim3(BTV), 0, s, p, g, b, out,    \
-                                tiemask, tw);                                                                 \
+        if (nt) hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<BTV, true, TRV>), grid, dim3(BTV), 0, s, p, g, b,  \
+                                   out, tiemask, tw);                                                         \
+        else hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<BTV, false, TRV>), grid, dim3(BTV), 0, s, p, g, b,    \
+                                out, tiemask, tw);                                                            \
     } while (0)
-    if (bt >= 1024) FC2_LBT(1024);
-    else if (bt >= 512) FC2_LBT(512);
-    else FC2_LBT(256);
+    if (tri) {
+        if (bt >= 1024) FC2_LBT(1024, true);
+        else if (bt >= 512) FC2_LBT(512, true);
+        else FC2_LBT(256, true);
+    } else {
+        if (bt >= 1024) FC2_LBT(1024, false);
+        else if (bt >= 512) FC2_LBT(512, false);
+        else FC2_LBT(256, false);
+    }
 #undef FC2_LBT
 }
 

@@ -225,6 +225,8 @@ int         fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_view 
 #define FC2_TUNE_WORDS 11      /* 1 (default): the LDS-staging scan reads windows from the view's
                                   word-pair layout (wt) when present; 0: from the unit planes */
 #define FC2_TUNE_STAGE_BLOCK 13  /* threads per block of the LDS-staging word-pair scan: 256, 512 (default), 1024 */
+#define FC2_TUNE_TRI 14         /* three lanes load each window of the LDS-staging word-pair scan: 0 never,
+                                   1 always, 2 (default) when a batch's windows exceed 97 bases */
 #define FC2_TUNE_REORDER_SHIFT 12 /* fc2_reorder_plan bucket size 2^shift bases (16..40; raised until
                                      <= 1024 buckets); 0 (default): ~1024 buckets over the genome */
 int         fc2_set_tuning(int key, int value);

@@ -52,6 +52,7 @@ def main():
         N.lib().fc2_set_tuning(11, 0 if "wo0" in v else 1)                       # FC2_TUNE_WORDS
         mb = re.search(r"bt(\d+)", v)                                            # FC2_TUNE_STAGE_BLOCK
         N.lib().fc2_set_tuning(13, int(mb.group(1)) if mb else 512)
+        N.lib().fc2_set_tuning(14, 0 if "tri0" in v else (1 if "tri1" in v else 2))   # FC2_TUNE_TRI
         N.lib().fc2_set_tuning(10, 0 if not m else (-1 if m.group(1) == "A" else int(m.group(1))))
 
     import ctypes

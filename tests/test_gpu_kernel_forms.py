@@ -21,16 +21,20 @@ pytestmark = pytest.mark.gpu
 from find_circ2_amd import Genome, Options, PairBatch, SynthConfig, scan, sq_table  # noqa: E402
 from find_circ2_amd import _native as N  # noqa: E402
 
-# knob values per form: FC2_TUNE_KERNEL32 (2), STAGE (7), TWIN (6), PERSIST (10), WORDS (11), STAGE_BLOCK (13)
-KNOBS = (2, 7, 6, 10, 11, 13)
-FORMS = {"scan32_staged_coop_words": (1, 1, 1, 0, 1, 256), "scan32_staged_coop_words_512": (1, 1, 1, 0, 1, 512),
-         "scan32_staged_coop_words_1024": (1, 1, 1, 0, 1, 1024),
-         "scan32_staged_coop_units_twin": (1, 1, 1, 0, 0, 256),
-         "scan32_persistent_coop_words": (1, 1, 1, -1, 1, 256), "scan32_persistent_coop_twin": (1, 1, 1, -1, 0, 256),
-         "scan32_persistent_3_per_cu": (1, 1, 1, 3, 0, 256),
-         "scan32_plain_words_no_twin": (1, 0, 0, 0, 1, 256), "scan32_plain_words_twin": (1, 0, 1, 0, 1, 256),
-         "scan32_plain_units_no_twin": (1, 0, 0, 0, 0, 256), "scan32_plain_units_twin": (1, 0, 1, 0, 0, 256),
-         "scan64": (0, 0, 0, 0, 1, 256)}
+# knob values per form: FC2_TUNE_KERNEL32 (2), STAGE (7), TWIN (6), PERSIST (10), WORDS (11), STAGE_BLOCK (13),
+# TRI (14)
+KNOBS = (2, 7, 6, 10, 11, 13, 14)
+FORMS = {"scan32_staged_coop_words": (1, 1, 1, 0, 1, 256, 0), "scan32_staged_coop_words_512": (1, 1, 1, 0, 1, 512, 0),
+         "scan32_staged_coop_words_1024": (1, 1, 1, 0, 1, 1024, 0),
+         "scan32_staged_tri_words_512": (1, 1, 1, 0, 1, 512, 1),
+         "scan32_staged_tri_words_256": (1, 1, 1, 0, 1, 256, 1),
+         "scan32_staged_coop_units_twin": (1, 1, 1, 0, 0, 256, 0),
+         "scan32_persistent_coop_words": (1, 1, 1, -1, 1, 256, 0),
+         "scan32_persistent_coop_twin": (1, 1, 1, -1, 0, 256, 0),
+         "scan32_persistent_3_per_cu": (1, 1, 1, 3, 0, 256, 0),
+         "scan32_plain_words_no_twin": (1, 0, 0, 0, 1, 256, 0), "scan32_plain_words_twin": (1, 0, 1, 0, 1, 256, 0),
+         "scan32_plain_units_no_twin": (1, 0, 0, 0, 0, 256, 0), "scan32_plain_units_twin": (1, 0, 1, 0, 0, 256, 0),
+         "scan64": (0, 0, 0, 0, 1, 256, 0)}
 DEFAULTS = {k: N.get_tuning(k) for k in KNOBS}
 
 
@@ -80,6 +84,32 @@ def test_forms_agree_full_size(hg19, ordered):
     finally:
         _reset()
         del b, ref
+        torch.cuda.empty_cache()
+
+
+def test_forms_agree_150bp(hg19):
+    """BASELINE configs[4] shape: 120-150 bp reads (windows up to 126 bases, five word pairs): the
+    three-lane form (default there), the two-lane form with the fifth-pair load and the plain form agree."""
+    opt = Options()
+    n = 25_000_000
+    b = PairBatch.synthetic(opt, hg19, n, SynthConfig(seed=4242, len_min=120, len_max=150, span_max=20000))
+    ref = None
+    try:
+        for form in ("scan32_staged_tri_words_512", "scan32_staged_coop_words_512", "scan32_staged_coop_words",
+                     "scan32_plain_words_twin", "scan32_plain_units_twin", "scan64"):
+            _set(form)
+            out = scan(opt, hg19, b)
+            torch.cuda.synchronize()
+            res = out.results[:n].clone()
+            del out
+            if ref is None:
+                ref = res
+                assert float(((ref & 0xFFFF) != 0xFFFF).float().mean()) > 0.4
+            else:
+                neq = int((res != ref).sum())
+                assert neq == 0, "%s differs on %d of %d pairs" % (form, neq, n)
+    finally:
+        _reset()
         torch.cuda.empty_cache()
 
 
