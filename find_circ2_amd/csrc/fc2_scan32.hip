@@ -6,6 +6,19 @@
 // dinucleotide shift) is ONE v_alignbit_b32 and each popcount ONE v_bcnt_u32,
 // instead of the 64-bit shift/or/select sequences.  NQ = 32-bit words per
 // plane: 4 / 8 / 16 <-> l + 2 <= 128 / 256 / 512.
+//
+// Kernel forms (fc2_bp_scan_launch picks one per batch; every form gives identical results,
+// tests/test_gpu_kernel_forms.py):
+//   bp_scan32_stage_bt_kernel<BT, NT, TRI>  read-order batch, genome >= 64 MiB, l + 2 <= 128: LDS
+//        tables, cooperative word-pair window loads (two lanes per window, or three for windows
+//        longer than 97 bases); the headline form
+//   bp_scan32_kernel<NQ, NT, STAGE>          the same with 256-pair blocks (STAGE), the unit-plane
+//        cooperative loads (no word-pair table), and the plain form for locus-ordered or
+//        cache-resident batches (STAGE = false)
+//   bp_scan32_win_kernel<PW, NT>             window-carrying batches: windows streamed with the record
+//   bp_scan32_persist_kernel<NT>             persistent-grid experiment (FC2_TUNE_PERSIST, off)
+//   probe_pattern_kernel                     measurement: the headline form's memory traffic only
+//   gather_windows_kernel<PW>                builds window rows from the resident genome
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -366,8 +379,9 @@ __device__ __forceinline__ void window_finish(const fc2_genome_view &g, const ui
 // of W <= 128 bases starting at base g0 needs the nwd = ceil(((g0 & 31) + W) / 32) <= 5 pairs from
 // q0 = g0 >> 5: ONE contiguous 32 B (nwd <= 4: every 100-bp pair) or 40 B run that lies inside one
 // line of either copy.  Both copies carry zero pairs in front (q0 >= -4 for any window the scan
-// evaluates), so no offset is negative.  Lanes 2m, 2m+1 load its two 16-B halves in one instruction (one L2 request,
-// like the cooperative unit loads); the owner adds the fifth pair only when nwd = 5.  Loads are
+// evaluates), so no offset is negative.  Lanes 2m, 2m+1 load its two 16-B halves in one
+// instruction (one L2 request, like the cooperative unit loads); the owner adds the fifth pair only
+// when nwd = 5 (or three lanes load 48 B, windows_issue_w3).  Loads are
 // buffer loads with 32-bit offsets: the hardware range check returns 0 past the table, and windows
 // outside the chromosome are masked to 'N' in window_finish_w whatever was read, so no index is
 // clamped.  Compared with the 64-base unit layout there is no word-parity select, no third unit
@@ -540,9 +554,9 @@ __device__ __forceinline__ void window_nwords_plain(const fc2_genome_view &g, __
 // bases (150-bp reads: a window needs 5 pairs = 40 B, more than two 16-B lane loads).  Each window is
 // read as the 48 B from its run start r -- inside one 128-B line because the copy is picked so
 // that r lies at most 80 B into its line (window_geom_w, tri) -- by three consecutive lanes of ONE
-// instruction: 21 windows per
-// instruction, 7 instructions for the wave's 128 windows, one L2 request per window (the two-lane
-// form spends a second request on the owner's fifth-pair load: +13 % at 150 bp, ab_fifth_pair.jsonl).
+// instruction: 21 windows per instruction, 7 instructions for the wave's 128 windows, one L2
+// request per window (the two-lane form spends a second request on the owner's fifth-pair load:
+// +13 % at 150 bp, profiles/r01/ab_fifth_pair.jsonl).
 __device__ __forceinline__ void windows_issue_w3(const fc2_genome_view &g, __amdgpu_buffer_rsrc_t rs,
                                                  __amdgpu_buffer_rsrc_t rn, const uint32_t *s_nsuper,
                                                  uint64_t cstart, int64_t wsA, int64_t wsB, int W, bool active,
