@@ -32,6 +32,7 @@ PAIR_READ_N = 0x04
 PAIR_BYTEPATH = 0x08
 PAIR_SKIP = 0x10
 PAIR_WIN_N = 0x20
+PAIR_READ_N1 = 0x40
 
 RES_MINUS = 0x0001
 RES_GTAG_SHIFT = 1
@@ -41,7 +42,7 @@ RES_ERR_WIN = 0x4000
 RES_DONE = 0x8000
 
 PAIR_DTYPE = np.dtype([("a_pos", "<i4"), ("b_aend", "<i4"), ("chrom", "<u4"), ("read_len", "<u2"),
-                       ("flags", "u1"), ("_pad", "u1")])
+                       ("flags", "u1"), ("npos", "u1")])
 RESULT_DTYPE = np.dtype([("best_x", "<i2"), ("dist", "u1"), ("ov", "u1"), ("n_ties", "<u2"), ("info", "<u2")])
 assert PAIR_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 8
 

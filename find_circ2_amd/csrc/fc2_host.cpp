@@ -621,7 +621,7 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
         for (uint64_t i = b; i < en; ++i) {
             fc2_pair &pr = pairs[i];
             pr.flags &= (uint8_t)(FC2_PAIR_BACKSPLICE | FC2_PAIR_PRIMARY_REV | FC2_PAIR_SKIP);
-            pr._pad = 0;
+            pr.npos = 0;
             for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = 0;
             for (uint32_t j = 0; j < nw; ++j) read_nwords[(uint64_t)j * stride + i] = 0;
             if (pr.flags & FC2_PAIR_SKIP) continue;
@@ -632,6 +632,7 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
             if (p->maxdist > 255 && l > 255) { int64_t x = -1; bad_dist.compare_exchange_strong(x, (int64_t)i); }
             const uint8_t *I = reads + read_off[i] + e;
             bool bytepath = l > kMaxFastL, anyN = false;
+            int n_count = 0, n_first = 0;
             if (!bytepath) {
                 if ((uint64_t)2 * l > (uint64_t)rw * 64 || (uint64_t)l > (uint64_t)nw * 64) {
                     int64_t x = -1; bad_rows.compare_exchange_strong(x, (int64_t)i); continue;
@@ -643,6 +644,7 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
                     const int cl = (pc & 4u) ? 4 : (int)pc;
                     if (cl == 4) {
                         anyN = true;
+                        if (n_count++ == 0) n_first = j;
                         read_nwords[(uint64_t)(j >> 6) * stride + i] |= 1ull << (j & 63);
                         continue;
                     }
@@ -672,6 +674,10 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
                 ++local_bp;
             } else if (anyN) {
                 pr.flags |= FC2_PAIR_READ_N;
+                if (n_count == 1 && n_first < 256) {      // the scan takes it from the record
+                    pr.flags |= FC2_PAIR_READ_N1;
+                    pr.npos = (uint8_t)n_first;
+                }
             }
         }
         nbp += local_bp;

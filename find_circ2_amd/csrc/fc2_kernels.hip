@@ -678,13 +678,14 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
     pr.read_len = (uint16_t)Lp;
     pr.flags = (uint8_t)((bs ? FC2_PAIR_BACKSPLICE : 0u) | ((R.next() & 1ull) ? FC2_PAIR_PRIMARY_REV : 0u) |
                          (ok ? 0u : FC2_PAIR_SKIP));
-    pr._pad = 0;
+    pr.npos = 0;
     if (truth) { truth[2 * i] = ok ? (int32_t)t0 : -1; truth[2 * i + 1] = ok ? (int32_t)t1 : -1; }
 
     // internal bases I[j] = read[c0 + e + j], j < l ; read[t] = t < kA ? G[A0+t] : G[B0+t-kA]
     uint64_t wlo = 0, whi_first = 0;
     (void)whi_first;
     bool anyN = false;
+    int n_count = 0, n_first = 0;
     // pass 1: low plane bits [0,l) and N words; pass 2: high plane bits [l,2l)
     uint32_t wi = 0;   // next read word to store
     uint64_t acc = 0;
@@ -707,7 +708,11 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
                 ++wi; acc = 0; accn = 0;
             }
             if (pass == 0) {
-                if (c == 4u) { anyN = true; nacc |= 1ull << (j & 63); }
+                if (c == 4u) {
+                    anyN = true;
+                    nacc |= 1ull << (j & 63);
+                    if (n_count++ == 0) n_first = j;
+                }
                 if ((j & 63) == 63 || j == lim - 1) {
                     if (ni < nw && read_nwords) read_nwords[(uint64_t)ni * stride + i] = nacc;
                     ++ni; nacc = 0;
@@ -721,6 +726,10 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
         for (; ni < nw; ++ni) read_nwords[(uint64_t)ni * stride + i] = 0;
     (void)wlo;
     if (anyN) pr.flags |= FC2_PAIR_READ_N;
+    if (n_count == 1 && n_first < 256) {
+        pr.flags |= FC2_PAIR_READ_N1;
+        pr.npos = (uint8_t)n_first;
+    }
     pairs[i] = pr;
 }
 

@@ -29,7 +29,8 @@ namespace {
 
 // Measurement-only ablations (scripts/ablate_build.sh; WRONG results, never in the shipped library):
 // bit 0 skips the owner's third-unit loads, bit 1 skips N-plane loads of flagged windows, bit 2
-// skips the canonical candidate walk, bit 3 skips the fifth word pair of windows with W > 97.
+// skips the canonical candidate walk, bit 3 skips the fifth word pair of windows with W > 97, bit 4
+// skips the read N-row loads.
 #ifndef FC2_ABLATE
 #define FC2_ABLATE 0
 #endif
@@ -862,7 +863,11 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         const unsigned s = (unsigned)(l & 31);
 #pragma unroll
         for (int k = 0; k < NQ; ++k) Ihi[k] = alignr(h[k + 1], h[k], s) & rmask32(0, l, k);
-        if (active && (pr.flags & FC2_PAIR_READ_N)) {
+        if (active && (pr.flags & (FC2_PAIR_READ_N | FC2_PAIR_READ_N1)) == (FC2_PAIR_READ_N | FC2_PAIR_READ_N1)) {
+            // a single 'N': its position came with the record, no N-row request
+#pragma unroll
+            for (int k = 0; k < NQ; ++k) In[k] = ((int)pr.npos >> 5) == k ? 1u << (pr.npos & 31) : 0u;
+        } else if (!(FC2_ABLATE & 16) && active && (pr.flags & FC2_PAIR_READ_N)) {
 #pragma unroll
             for (int j = 0; j < (NQ + 1) / 2; ++j) {
                 const uint64_t v =

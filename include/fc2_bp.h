@@ -64,6 +64,8 @@ typedef struct fc2_params {
                                        irregular FASTA line layout, very long reads) */
 #define FC2_PAIR_SKIP        0x10u  /* not evaluated (e.g. not is_uniq, :1299): no hit */
 #define FC2_PAIR_WIN_N       0x20u  /* window-carrying batch: this pair's window N rows are present */
+#define FC2_PAIR_READ_N1     0x40u  /* with READ_N: the read part holds exactly ONE 'N', at position npos
+                                       (< 256); the scan then skips the N row (which is filled all the same) */
 
 typedef struct fc2_pair {
     int32_t  a_pos;     /* align_A.pos  (0-based)                                    */
@@ -71,7 +73,7 @@ typedef struct fc2_pair {
     uint32_t chrom;     /* index into the genome's chromosome table                  */
     uint16_t read_len;  /* L = len(read_part)                                        */
     uint8_t  flags;     /* FC2_PAIR_*                                                */
-    uint8_t  _pad;
+    uint8_t  npos;      /* FC2_PAIR_READ_N1: position of the read part's single 'N'; else 0 */
 } fc2_pair;
 
 /* ---- per-pair result, 8 bytes ------------------------------------------- */

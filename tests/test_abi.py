@@ -259,6 +259,10 @@ def test_pair_pack_roundtrip(L):
             n_bp += 1
             continue
         assert bool(flags & N.PAIR_READ_N) == (b"N" in internal), i
+        # a single 'N' travels in the record (FC2_PAIR_READ_N1 + npos); the N row is filled all the same
+        single = internal.count(b"N") == 1 and internal.index(b"N") < 256
+        assert bool(flags & N.PAIR_READ_N1) == single, i
+        assert int(hp["npos"][i]) == (internal.index(b"N") if single else 0), i
         assert decode_read(words, nwords, stride, i, l, bool(flags & N.PAIR_READ_N)) == internal, i
     assert n_bp == nbp == 3
     L.fc2_fasta_close(h)
