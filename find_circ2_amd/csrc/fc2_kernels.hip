@@ -893,7 +893,9 @@ extern "C" int fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_vi
     if (!g || !b || !out || g->dummy || !g->wt || !g->chrom_start || !b->pairs || !b->read_words)
         return fc2::fail(FC2_E_PARAM, "fc2_probe_pattern_launch: needs a genome with a word-pair table and a batch");
     if (b->n == 0) return FC2_OK;
-    if (fc2::launch_probe_pattern((hipStream_t)stream, *p, *g, *b, out))
+    const int ml = b->max_l < 0 ? 0 : b->max_l;
+    const bool tri = g_tri == 1 || (g_tri == 2 && ml + 2 > 97);     // the scan's window form (fc2_bp_scan_launch)
+    if (fc2::launch_probe_pattern((hipStream_t)stream, *p, *g, *b, out, tri))
         return fc2::fail(FC2_E_HIP, "probe_pattern_kernel launch failed");
     return FC2_OK;
 }

@@ -30,5 +30,5 @@ void launch_gather_windows(hipStream_t s, const fc2_params &p, const fc2_genome_
                            fc2_pair *pairs, uint64_t *win_words, uint64_t *win_nwords, uint32_t pw);
 // Measurement kernel: the read-order scan's memory pattern without its arithmetic (needs g.wt).
 int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b,
-                         uint64_t *out);
+                         uint64_t *out, bool tri);
 }  // namespace fc2

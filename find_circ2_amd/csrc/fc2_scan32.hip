@@ -577,9 +577,16 @@ __device__ __forceinline__ void windows_issue_w3(const fc2_genome_view &g, __amd
         ok[c] = lane < 63 && w < 128;
         part[c] = lane % 3;
         const int owner = w & 63;
-        const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sA);
-        const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sB);
-        src[c] = (w >> 6) ? b : a;
+        // instructions 0-2 serve only A windows (w <= 62), 4-6 only B windows (w >= 84): one permute
+        if (21 * c + 20 < 64) {
+            src[c] = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sA);
+        } else if (21 * c >= 64) {
+            src[c] = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sB);
+        } else {
+            const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sA);
+            const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sB);
+            src[c] = (w >> 6) ? b : a;
+        }
     }
     uint32_t sw[2][2] = {{0u, 0u}, {0u, 0u}}, sb[2][2] = {{0u, 0u}, {0u, 0u}};
     bool sv[2] = {false, false};
@@ -1303,11 +1310,11 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_persist_kernel(fc2_params p,
 // Speed-of-light probe of the read-order scan (measurement only, fc2_probe_pattern_launch): the
 // kernel's exact memory pattern on the same batch and genome -- NT-streamed 16-B records and read
 // rows, chromosome table staged in LDS, both windows' word pairs loaded by lane pairs from the same
-// table offsets (main or shifted copy), 8-B result stored -- with none of the search's arithmetic,
-// no N words and no fifth pair.  Its time bounds what any kernel with this access pattern can reach
-// on this GPU (bench.py: roofline.access_pattern_ceiling).
+// table offsets (main or shifted copy), 8-B result stored -- with none of the search's arithmetic
+// and no N words (`tri`, windows > 97 bases: the three-lane 48-B loads).  Its time bounds what
+// any kernel with this access pattern can reach on this GPU (bench.py: roofline.access_pattern_ceiling).
 __global__ __launch_bounds__(kBlock) void probe_pattern_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
-                                                               uint64_t *__restrict__ out) {
+                                                               uint64_t *__restrict__ out, bool tri) {
     __shared__ uint64_t s_cstart[kChromLds];
     const bool lds_tab = g.n_chrom <= (uint32_t)kChromLds;
     if (lds_tab) {
@@ -1333,20 +1340,34 @@ __global__ __launch_bounds__(kBlock) void probe_pattern_kernel(fc2_params p, fc2
     const uint32_t c = active ? pr.chrom : 0u;
     const uint64_t cstart = lds_tab ? s_cstart[c] : g.chrom_start[c];
     WinW wA, wB;
-    window_geom_w(g, active ? cstart : 0, active ? (int64_t)pr.a_pos + e : 0, W, wA);
-    window_geom_w(g, active ? cstart : 0, active ? (int64_t)pr.b_aend - e - W : 0, W, wB);
+    window_geom_w(g, active ? cstart : 0, active ? (int64_t)pr.a_pos + e : 0, W, wA, tri);
+    window_geom_w(g, active ? cstart : 0, active ? (int64_t)pr.b_aend - e - W : 0, W, wB, tri);
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)g.wt, 0, (int)(uint32_t)g.wt_bytes,
                                                                          0x00020000);
     const int lane = (int)(threadIdx.x & 63);
     const uint32_t offs[2] = {wA.off, wB.off};
+    if (tri) {                                 // the scan's three-lane form (windows_issue_w3): 48 B per window
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-        for (int cc = 0; cc < 2; ++cc) {
-            const uint32_t src = (uint32_t)__builtin_amdgcn_ds_bpermute((32 * cc + (lane >> 1)) << 2, (int)offs[x]);
-            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, src + 16u * (uint32_t)(lane & 1), 0, 0);
-            acc ^= (uint64_t)(v.x + v.y) | ((uint64_t)(v.z ^ v.w) << 32);
+        for (int c = 0; c < 7; ++c) {
+            const int w = 21 * c + lane / 3;
+            const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute((w & 63) << 2, (int)offs[0]);
+            const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute((w & 63) << 2, (int)offs[1]);
+            if (lane < 63 && w < 128) {
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, ((w >> 6) ? b : a) + 16u * (uint32_t)(lane % 3),
+                                                                      0, 0);
+                acc ^= (uint64_t)(v.x + v.y) | ((uint64_t)(v.z ^ v.w) << 32);
+            }
         }
+    } else {
+#pragma unroll
+        for (int x = 0; x < 2; ++x)
+#pragma unroll
+            for (int cc = 0; cc < 2; ++cc) {
+                const uint32_t src = (uint32_t)__builtin_amdgcn_ds_bpermute((32 * cc + (lane >> 1)) << 2, (int)offs[x]);
+                const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, src + 16u * (uint32_t)(lane & 1), 0, 0);
+                acc ^= (uint64_t)(v.x + v.y) | ((uint64_t)(v.z ^ v.w) << 32);
+            }
+    }
     if (live) st_stream<true>(out + i, acc);
 }
 
@@ -1355,9 +1376,9 @@ __global__ __launch_bounds__(kBlock) void probe_pattern_kernel(fc2_params p, fc2
 namespace fc2 {
 
 int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b,
-                         uint64_t *out) {
+                         uint64_t *out, bool tri) {
     hipLaunchKernelGGL(probe_pattern_kernel, dim3((unsigned)((b.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p, g,
-                       b, out);
+                       b, out, tri);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

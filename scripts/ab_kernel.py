@@ -5,6 +5,7 @@ usage: python scripts/ab_kernel.py [--workload hg19|cdr1as] [--pairs N] [--round
 Prints one JSON line per variant: median / min kernel ms over rounds, pairs/s.
 """
 import argparse
+import ctypes
 import json
 import re
 import os
@@ -25,6 +26,10 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--read-len", type=int, default=100)
     ap.add_argument("--no-check", action="store_true", help="measurement-only libraries (ablations) change results")
+    ap.add_argument("--second", default="",
+                    help="NAME: also load find_circ2_amd/libfc2_NAME.so into THIS process; a variant prefixed "
+                         "'2:' (e.g. 2:k32nt1) launches through that library on the same device buffers, so two "
+                         "builds are compared without the between-process allocation spread")
     ap.add_argument("--variants", default="k32nt1,k64nt1",
                     help="comma list of k32|k64 + nt1|nt0 + sw0|sw1 + tw0|tw1 (FC2_TUNE_KERNEL32 / STREAM_NT / "
                          "XCD_SWIZZLE (default auto) / TWIN)")
@@ -40,22 +45,36 @@ def main():
     ref = out.results[:b.n].clone()
     variants = a.variants.split(",")
 
+    lib2 = None
+    if a.second:
+        lib2 = ctypes.CDLL(os.path.join(ROOT, "find_circ2_amd", "libfc2_%s.so" % a.second))
+        lib2.fc2_bp_scan_launch.restype = ctypes.c_int
+        lib2.fc2_bp_scan_launch.argtypes = [ctypes.POINTER(N.Params), ctypes.POINTER(N.GenomeView),
+                                            ctypes.POINTER(N.BatchView), ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_uint32, ctypes.c_void_p]
+        lib2.fc2_set_tuning.argtypes = [ctypes.c_int, ctypes.c_int]
+
     def apply(v):
-        N.lib().fc2_set_tuning(1, 0 if "nt0" in v else 1)
-        N.lib().fc2_set_tuning(2, 0 if "k64" in v else 1)
-        N.lib().fc2_set_tuning(3, 0 if "sw0" in v else (1 if "sw1" in v else 2))
-        N.lib().fc2_set_tuning(6, 0 if "tw0" in v else (1 if "tw1" in v else 2))
-        N.lib().fc2_set_tuning(7, 0 if "st0" in v else (1 if "st1" in v else 2))
-        N.lib().fc2_set_tuning(9, 8192 if "lds8k" in v else (65536 if "lds64k" in v else 0))
+        if v.startswith("2:"):
+            set_knobs(lib2, v[2:])
+        else:
+            set_knobs(N.lib(), v)
+
+    def set_knobs(L, v):
+        L.fc2_set_tuning(1, 0 if "nt0" in v else 1)
+        L.fc2_set_tuning(2, 0 if "k64" in v else 1)
+        L.fc2_set_tuning(3, 0 if "sw0" in v else (1 if "sw1" in v else 2))
+        L.fc2_set_tuning(6, 0 if "tw0" in v else (1 if "tw1" in v else 2))
+        L.fc2_set_tuning(7, 0 if "st0" in v else (1 if "st1" in v else 2))
+        L.fc2_set_tuning(9, 8192 if "lds8k" in v else (65536 if "lds64k" in v else 0))
         m = re.search(r"pe(A|\d+)", v)   # FC2_TUNE_PERSIST: peA = occupancy-sized grid, peK = K blocks/CU
         # knobs an older library (FC2_LIB_VARIANT) may not have: set unchecked, default when absent
-        N.lib().fc2_set_tuning(11, 0 if "wo0" in v else 1)                       # FC2_TUNE_WORDS
+        L.fc2_set_tuning(11, 0 if "wo0" in v else 1)                       # FC2_TUNE_WORDS
         mb = re.search(r"bt(\d+)", v)                                            # FC2_TUNE_STAGE_BLOCK
-        N.lib().fc2_set_tuning(13, int(mb.group(1)) if mb else 512)
-        N.lib().fc2_set_tuning(14, 0 if "tri0" in v else (1 if "tri1" in v else 2))   # FC2_TUNE_TRI
-        N.lib().fc2_set_tuning(10, 0 if not m else (-1 if m.group(1) == "A" else int(m.group(1))))
+        L.fc2_set_tuning(13, int(mb.group(1)) if mb else 512)
+        L.fc2_set_tuning(14, 0 if "tri0" in v else (1 if "tri1" in v else 2))   # FC2_TUNE_TRI
+        L.fc2_set_tuning(10, 0 if not m else (-1 if m.group(1) == "A" else int(m.group(1))))
 
-    import ctypes
     junk = torch.empty(b.n, dtype=torch.int64, device=dev)
 
     win = {}
@@ -74,6 +93,12 @@ def main():
             N.check(N.lib().fc2_bp_scan_launch(ctypes.byref(pv), ctypes.byref(win["gv"]), ctypes.byref(win["bv"]),
                                                out.results.data_ptr(), None, b.tw,
                                                torch.cuda.current_stream(dev).cuda_stream))
+            return
+        if v.startswith("2:"):
+            gv, bv, pv = g.view(), b.view(), opt.params()
+            N.check(lib2.fc2_bp_scan_launch(ctypes.byref(pv), ctypes.byref(gv), ctypes.byref(bv),
+                                            out.results.data_ptr(), None, b.tw,
+                                            torch.cuda.current_stream(dev).cuda_stream))
             return
         if v == "probe":          # the scan's access pattern without its arithmetic (fc2_probe_pattern_launch)
             gv, bv, pv = g.view(), b.view(), opt.params()
