@@ -632,25 +632,36 @@ __device__ __forceinline__ void windows_issue_w3(const fc2_genome_view &g, __amd
     }
 }
 
-// Owner side: the first 40 B of each window's three 16-B pieces from the wave's LDS slots.
-__device__ __forceinline__ void windows_exchange_w3(u32x4 *xchg, const u32x4 (&cl)[7], WinW &rA, WinW &rB) {
-    const int lane = (int)(threadIdx.x & 63);
-#pragma unroll
-    for (int c = 0; c < 7; ++c) xchg[c * 64 + lane] = cl[c];
+// Owner side: the first 40 B of each window's three 16-B pieces, in two phases through 4 LDS slots
+// (4 KB per wave instead of 7; 1.5 % faster at 150 bp, profiles/r01/ab_tri_4slot.jsonl): instructions
+// 0-3 hold every A window and B windows 64..83, then instructions 4-6 overwrite slots 0-2 with B
+// windows 84..127.
+__device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    WinW *R[2] = {&rA, &rB};
+}
+__device__ __forceinline__ void take_w3(const u32x4 *xchg, int slot, int w, WinW &Q) {
+    const int base = slot * 64 + 3 * (w % 21);
+    const u32x4 p0 = xchg[base], p1 = xchg[base + 1];
+    const u32x2 p2 = *reinterpret_cast<const u32x2 *>(xchg + base + 2);
+    Q.v0 = p0;
+    Q.v1 = p1;
+    Q.v4 = p2;
+}
+__device__ __forceinline__ void windows_exchange_w3(u32x4 *xchg, const u32x4 (&cl)[7], WinW &rA, WinW &rB) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int wB = 64 + lane;
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
-        WinW &Q = *R[x];
-        const int w = 64 * x + lane;
-        const int base = (w / 21) * 64 + 3 * (w % 21);
-        const u32x4 p0 = xchg[base], p1 = xchg[base + 1], p2 = xchg[base + 2];
-        Q.v0 = p0;
-        Q.v1 = p1;
-        Q.v4 = u32x2{p2.x, p2.y};
-    }
+    for (int c = 0; c < 4; ++c) xchg[c * 64 + lane] = cl[c];
+    wave_sync_lds();
+    take_w3(xchg, lane / 21, lane, rA);
+    if (wB < 84) take_w3(xchg, 3, wB, rB);
+    wave_sync_lds();                           // every phase-1 read done before slots 0-2 are reused
+#pragma unroll
+    for (int c = 4; c < 7; ++c) xchg[(c - 4) * 64 + lane] = cl[c];
+    wave_sync_lds();
+    if (wB >= 84) take_w3(xchg, wB / 21 - 4, wB, rB);
 }
 
 template <int NQ>
@@ -1245,7 +1256,7 @@ __global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc
     __shared__ uint64_t s_cstart[kChromLds];
     __shared__ int64_t s_csize[kChromLds];
     __shared__ __attribute__((aligned(16))) uint32_t s_nsuper_buf[kSuperLds];
-    __shared__ ulonglong2 s_xchg[BT / 64][(TRI ? 7 : 4) * 64];
+    __shared__ ulonglong2 s_xchg[BT / 64][4 * 64];
     // the launcher guarantees: genome not dummy, word-pair table, tables fit in LDS
     for (uint32_t w = 4 * threadIdx.x; w < (uint32_t)kSuperLds; w += 4 * BT) {
         uint4 q = uint4{0u, 0u, 0u, 0u};
