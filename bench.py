@@ -128,47 +128,57 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
     """BASELINE.md's 'device pipeline' number: pinned host SoA -> H2D -> scan -> D2H.
 
     The batch is split into `chunks` slices, each laid out contiguously in pinned
-    host memory in the device SoA layout (untimed setup), and streamed on two HIP
+    host memory in the device SoA layout with its N rows in the sparse form PairBatch.pack
+    uploads (hotpath.sparse_nrows; untimed setup), and streamed on two HIP
     streams so that one slice's copies overlap another's kernel (PCIe is full
     duplex).  Returns pairs/s and ms per batch (median of `reps`).
     """
     import torch
     from find_circ2_amd import PairBatch, scan
-    from find_circ2_amd.hotpath import ScanOutput
+    from find_circ2_amd import _native as N
+    from find_circ2_amd.hotpath import ScanOutput, scatter_nrows
     dev = b.device
     n = b.n
     step = (n + chunks - 1) // chunks
     words = b.read_words[:b.rw * b.stride].view(b.rw, b.stride)
     nwords = b.read_nwords[:b.nw * b.stride].view(b.nw, b.stride)
-    host = []                             # per slice: one pinned buffer [pairs | words | nwords]
+    flags = b.pairs[:16 * n].view(n, 16)[:, 14]
+    host = []     # per slice: one pinned buffer [pairs | read rows | N-row pair index | N rows of those pairs]
     for c in range(chunks):
         lo, hi = c * step, min(n, (c + 1) * step)
         if lo >= hi:
             break
         m = hi - lo
-        parts = [b.pairs[16 * lo:16 * hi].view(torch.int64), words[:, lo:hi].reshape(-1), nwords[:, lo:hi].reshape(-1)]
-        host.append((lo, m, torch.cat([t.cpu() for t in parts]).pin_memory()))
+        # the N rows travel sparsely, as PairBatch.pack uploads them (hotpath.sparse_nrows)
+        idx = torch.nonzero((flags[lo:hi] & N.PAIR_READ_N) != 0).flatten().to(torch.int64)
+        parts = [b.pairs[16 * lo:16 * hi].view(torch.int64), words[:, lo:hi].reshape(-1), idx,
+                 nwords[:, lo:hi][:, idx].reshape(-1)]
+        host.append((lo, m, int(idx.numel()), torch.cat([t.cpu() for t in parts]).pin_memory()))
+    kmax = max(k for _, _, k, _ in host)
     host_out = torch.empty(n, dtype=torch.int64).pin_memory()
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-    dbuf = [torch.empty((2 + b.rw + b.nw) * step, dtype=torch.int64, device=dev) for _ in range(2)]
+    dbuf = [torch.empty((2 + b.rw) * step + (1 + b.nw) * kmax, dtype=torch.int64, device=dev) for _ in range(2)]
+    nbuf = [torch.zeros(b.nw * step, dtype=torch.int64, device=dev) for _ in range(2)]
     dres = [torch.empty(step, dtype=torch.int64, device=dev) for _ in range(2)]
 
-    def slice_batch(buf, m):
+    def slice_batch(buf, nb, m, k):
         sb = PairBatch()
         sb.options, sb.device = b.options, dev
         sb.rw, sb.nw, sb.tw, sb.max_l, sb.layout = b.rw, b.nw, b.tw, b.max_l, b.layout
         sb.n = sb.stride = m
         sb.pairs = buf[:2 * m].view(torch.uint8)
         sb.read_words = buf[2 * m:(2 + b.rw) * m]
-        sb.read_nwords = buf[(2 + b.rw) * m:(2 + b.rw + b.nw) * m]
+        sb.read_nwords = nb[:b.nw * m]
+        o = (2 + b.rw) * m
+        scatter_nrows(sb.read_nwords, buf[o:o + k], buf[o + k:o + k + b.nw * k].view(b.nw, k), b.nw, m)
         return sb
 
     def run_once():
-        for c, (lo, m, hbuf) in enumerate(host):
+        for c, (lo, m, k, hbuf) in enumerate(host):
             st = streams[c & 1]
             with torch.cuda.stream(st):
                 dbuf[c & 1][:hbuf.numel()].copy_(hbuf, non_blocking=True)
-                sb = slice_batch(dbuf[c & 1], m)
+                sb = slice_batch(dbuf[c & 1], nbuf[c & 1], m, k)
                 scan(opt, g, sb, out=ScanOutput(dres[c & 1], None, sb.tw, m), stream=st.cuda_stream)
                 host_out[lo:lo + m].copy_(dres[c & 1][:m], non_blocking=True)
         torch.cuda.synchronize(dev)
@@ -181,12 +191,16 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
         ts.append(time.perf_counter() - t0)
     ms = float(np.median(ts)) * 1e3
     ok = bool(torch.equal(host_out, b._bench_ref_results)) if hasattr(b, "_bench_ref_results") else None
-    h2d = (16 + 8 * b.rw + 8 * b.nw) * n
+    kn = sum(k for _, _, k, _ in host)
+    h2d = sum(h.numel() * 8 for _, _, _, h in host)
     return {"value": round(n / (ms * 1e-3), 1), "unit": "anchor-pairs/s", "ms_per_batch": round(ms, 3),
             "pcie_GBs": round((h2d + 8 * n) / (ms * 1e-3) / 1e9, 1),
+            "h2d_bytes_per_pair": round(h2d / n, 2),
             "results_equal_device_resident_scan": ok,
-            "note": "pinned host SoA (16 B record + %d B read row + %d B read N row) -> H2D -> bp_scan -> D2H 8 B "
-                    "result, %d slices on 2 HIP streams; %d pairs" % (8 * b.rw, 8 * b.nw, len(host), n)}
+            "note": "pinned host SoA (16 B record + %d B read row; the N rows of the %.2f %% of pairs flagged "
+                    "READ_N as index + %d B rows, scattered on the device) -> H2D -> bp_scan -> D2H 8 B result, "
+                    "%d slices on 2 HIP streams; %d pairs" % (8 * b.rw, 100.0 * kn / max(n, 1), 8 * b.nw,
+                                                              len(host), n)}
 
 
 def timed_scans(opt, g, b, steps, warmup, ws, dev):

@@ -80,6 +80,32 @@ class SynthConfig:
 # ---------------------------------------------------------------------------
 # batches
 # ---------------------------------------------------------------------------
+def sparse_nrows(host_pairs: np.ndarray, nwords: np.ndarray, nw: int, stride: int):
+    """The read N rows of the pairs that carry them (FC2_PAIR_READ_N): (pair index [k] int64,
+    rows [nw, k] int64).  Every other pair's N row is zero, and the scan reads a pair's N row only
+    when its READ_N flag is set, so this is all the N information a batch has to move."""
+    idx = np.nonzero((host_pairs["flags"] & N.PAIR_READ_N) != 0)[0].astype(np.int64)
+    rows = nwords.view(np.int64).reshape(nw, stride)[:, idx]
+    return idx, np.ascontiguousarray(rows)
+
+
+def scatter_nrows(dst, idx, rows, nw: int, stride: int) -> None:
+    """Device side of sparse_nrows: dst (torch int64 [nw*stride]) row j, column idx[t] = rows[j, t]."""
+    if idx.numel():
+        dst.view(nw, stride)[:, idx] = rows
+
+
+def upload_nrows(host_pairs: np.ndarray, nwords: np.ndarray, nw: int, stride: int, dev):
+    """Device N rows of a packed batch: zeros plus the flagged pairs' rows scattered in.  At 100 bp
+    the dense rows are 16 of the 56 B a pair moves over PCIe; the sparse form moves 8 + 8*nw B per
+    pair with an 'N' (a few percent of reads) instead."""
+    torch = _torch()
+    out = torch.zeros(nw * stride, dtype=torch.int64, device=dev)
+    idx, rows = sparse_nrows(host_pairs, nwords, nw, stride)
+    scatter_nrows(out, torch.from_numpy(idx).to(dev), torch.from_numpy(rows).to(dev), nw, stride)
+    return out
+
+
 class PairBatch:
     """A batch of anchor pairs resident in device memory (layout: include/fc2_bp.h)."""
 
@@ -172,7 +198,7 @@ class PairBatch:
         b.device = dev
         b.pairs = torch.from_numpy(hp.view(np.uint8)).to(dev)
         b.read_words = torch.from_numpy(words.view(np.int64)).to(dev)
-        b.read_nwords = torch.from_numpy(nwords.view(np.int64)).to(dev)
+        b.read_nwords = upload_nrows(hp, nwords, b.nw, b.stride, dev)
         b.m_bytepath = int(nbp.value)
         if b.m_bytepath and genome.fasta is None and not genome.dummy:
             raise RuntimeError("%d pairs need byte-exact windows, which come from a FASTA-backed genome"
