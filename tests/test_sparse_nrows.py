@@ -26,3 +26,17 @@ def test_sparse_rows_rebuild_dense_rows(n, nw, p):
     assert rows.shape == (nw, len(idx))
     got = upload_nrows(hp, dense.view(np.uint64).ravel(), nw, stride, "cpu")
     assert torch.equal(got, torch.from_numpy(dense.ravel()))
+
+
+@pytest.mark.parametrize("rw,stride,tail_bits", [(3, 1000, 20), (3, 5, 32), (2, 17, 33), (1, 9, 10), (4, 1, 0)])
+def test_read_rows_narrow_tail(rw, stride, tail_bits):
+    """upload_read_rows sends the last row as uint32 only when every value fits, and the device
+    rows equal the packed rows either way."""
+    from find_circ2_amd.hotpath import narrow_tail, upload_read_rows
+    rng = np.random.default_rng(rw * 100 + stride)
+    w = rng.integers(0, 2**63, size=(rw, stride), dtype=np.int64).view(np.uint64)
+    w[rw - 1] &= np.uint64((1 << tail_bits) - 1) if tail_bits < 64 else np.uint64(2**64 - 1)
+    words = w.ravel()
+    assert narrow_tail(words, rw, stride) == (rw > 1 and tail_bits <= 32 and True)
+    got = upload_read_rows(words, rw, stride, "cpu")
+    assert torch.equal(got, torch.from_numpy(words.view(np.int64)))
