@@ -143,8 +143,9 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
     words = b.read_words[:b.rw * b.stride].view(b.rw, b.stride)
     nwords = b.read_nwords[:b.nw * b.stride].view(b.nw, b.stride)
     flags = b.pairs[:16 * n].view(n, 16)[:, 14]
-    host = []     # per slice: one pinned buffer [pairs | read rows but the last | last row as uint32 | N-row
-                  # pair index | N rows of those pairs]
+    narrow = b.rw > 1 and not bool((words[b.rw - 1] >> 32).any())
+    host = []     # per slice: one pinned buffer [pairs | read rows but the last | last row (as uint32 when
+                  # narrow) | N-row pair index | N rows of those pairs]
     for c in range(chunks):
         lo, hi = c * step, min(n, (c + 1) * step)
         if lo >= hi:
@@ -153,17 +154,19 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
         # the N rows travel sparsely, as PairBatch.pack uploads them (hotpath.sparse_nrows)
         idx = torch.nonzero((flags[lo:hi] & N.PAIR_READ_N) != 0).flatten().to(torch.int64)
         # the last read row crosses as uint32 when it fits (hotpath.narrow_tail), as PairBatch.pack sends it
-        tail = words[b.rw - 1, lo:hi].contiguous().view(torch.int32)[0::2].contiguous()
-        tail = torch.cat([tail, tail.new_zeros(m & 1)]).view(torch.int64)
+        tail = words[b.rw - 1, lo:hi].contiguous()
+        if narrow:
+            tail = tail.view(torch.int32)[0::2].contiguous()
+            tail = torch.cat([tail, tail.new_zeros(m & 1)]).view(torch.int64)
         head = [b.pairs[16 * lo:16 * hi].view(torch.int64), words[:b.rw - 1, lo:hi].reshape(-1)]
         rest = [tail, idx, nwords[:, lo:hi][:, idx].reshape(-1)]
         hb = torch.cat([t.cpu() for t in head + rest]).pin_memory()
         host.append((lo, m, int(idx.numel()), (1 + b.rw) * m, hb))
-    assert b.rw > 1 and not bool((words[b.rw - 1] >> 32).any()), "bench rows: the last row must be narrow"
     kmax = max(h[2] for h in host)
     host_out = torch.empty(n, dtype=torch.int64).pin_memory()
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
-    dbuf = [torch.empty((2 + b.rw) * step + (step + 1) // 2 + (1 + b.nw) * kmax, dtype=torch.int64, device=dev)
+    tail_words = (step + 1) // 2 if narrow else step
+    dbuf = [torch.empty((2 + b.rw) * step + tail_words + (1 + b.nw) * kmax, dtype=torch.int64, device=dev)
             for _ in range(2)]
     nbuf = [torch.zeros(b.nw * step, dtype=torch.int64, device=dev) for _ in range(2)]
     dres = [torch.empty(step, dtype=torch.int64, device=dev) for _ in range(2)]
@@ -175,9 +178,12 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
         sb.n = sb.stride = m
         sb.pairs = buf[:2 * m].view(torch.uint8)
         sb.read_words = buf[2 * m:(2 + b.rw) * m]
-        o = (2 + b.rw) * m                         # staging: tail32 | N-row index | N rows
-        t2 = (m + 1) // 2
-        widen_tail(sb.read_words[(b.rw - 1) * m:], buf[o:o + t2].view(torch.int32)[:m])
+        o = (2 + b.rw) * m                         # staging: last row | N-row index | N rows
+        t2 = (m + 1) // 2 if narrow else m
+        if narrow:
+            widen_tail(sb.read_words[(b.rw - 1) * m:], buf[o:o + t2].view(torch.int32)[:m])
+        else:
+            sb.read_words[(b.rw - 1) * m:].copy_(buf[o:o + m])
         sb.read_nwords = nb[:b.nw * m]
         o += t2
         scatter_nrows(sb.read_nwords, buf[o:o + k], buf[o + k:o + k + b.nw * k].view(b.nw, k), b.nw, m)
@@ -209,10 +215,11 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
             "pcie_GBs": round((h2d + 8 * n) / (ms * 1e-3) / 1e9, 1),
             "h2d_bytes_per_pair": round(h2d / n, 2),
             "results_equal_device_resident_scan": ok,
-            "note": "pinned host SoA (16 B record + %d B read rows, the last one as uint32; the N rows of the %.2f %% "
+            "note": "pinned host SoA (16 B record + %d B read rows%s; the N rows of the %.2f %% "
                     "of pairs flagged READ_N as index + %d B rows, scattered on the device) -> H2D -> bp_scan -> "
                     "D2H 8 B result, %d slices on 2 HIP streams; %d pairs"
-                    % (8 * b.rw - 4, 100.0 * kn / max(n, 1), 8 * b.nw, len(host), n)}
+                    % (8 * b.rw - (4 if narrow else 0), ", the last one as uint32" if narrow else "",
+                       100.0 * kn / max(n, 1), 8 * b.nw, len(host), n)}
 
 
 def timed_scans(opt, g, b, steps, warmup, ws, dev):
