@@ -54,6 +54,7 @@ def parse():
                     help="lay the batch out by A-window locus (PairBatch.pack(locus_order=True)); default read order")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
+    ap.add_argument("--no-strong", action="store_true", help="skip the configs[3] strong-scaling / ordered-merge run")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
     return ap.parse_args()
@@ -91,6 +92,58 @@ def setup_dist(args):
             os.dup2(saved, 1)
             os.close(saved)
     return ws, rank, dev_index
+
+
+def spawn_ranks(args) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script (one per GPU, the env
+    torch.distributed.run would give them) BEFORE this process touches the GPU, forward rank 0's
+    JSON line, and fail unless every rank finished and rank 0 reports n_gpus == N.  The parent
+    never initialises HIP and never execs; it only waits on its children."""
+    import socket
+    import subprocess
+    with socket.socket() as s:                  # a free rendezvous port on the loopback interface
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr.fileno()))
+    out0 = [b""]
+    reader = threading.Thread(target=lambda: out0.__setitem__(0, procs[0].stdout.read()), daemon=True)
+    reader.start()
+    rcs = [None] * len(procs)
+    while any(rc is None for rc in rcs):
+        for r, p in enumerate(procs):
+            if rcs[r] is None:
+                rcs[r] = p.poll()
+        if any(rc not in (None, 0) for rc in rcs):
+            bad = [r for r, rc in enumerate(rcs) if rc not in (None, 0)]
+            print("bench: rank(s) %s failed (exit %s); stopping the others" % (bad, [rcs[r] for r in bad]),
+                  file=sys.stderr)
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+            return 1
+        time.sleep(0.05)
+    reader.join()
+    lines = [l for l in out0[0].decode("utf-8", "replace").splitlines() if l.startswith("{")]
+    if not lines:
+        print("bench: rank 0 printed no JSON line", file=sys.stderr)
+        return 1
+    line = json.loads(lines[-1])
+    if int(line.get("n_gpus", 0)) != args.gpus:
+        print("bench: rank 0 reports n_gpus %s, asked for %d" % (line.get("n_gpus"), args.gpus), file=sys.stderr)
+        return 1
+    print(lines[-1], flush=True)
+    return 0
 
 
 def barrier(ws):
@@ -244,6 +297,83 @@ def timed_scans(opt, g, b, steps, warmup, ws, dev):
     t1 = time.perf_counter()
     kms = [s.elapsed_time(e) for s, e in ev]
     return t1 - t0, float(np.mean(kms)), out
+
+
+def strong_scaling(opt, g, sb, ref64, ws, rank, dev, steps, warmup):
+    """configs[3]: ONE pair stream (the 50M pairs rank 0 scans in the weak run, seed 1337) cut into
+    contiguous batches dealt round-robin to the ranks (shard.my_batches); every rank holds the
+    stream in HBM, scans only its batches (PairBatch.sub views, no copy) and copies their 8-B
+    results to the batch's input offset of ONE node-local pinned host buffer (shard.SharedResults),
+    which rank 0 then holds in input order: the host-side ordered merge junction naming needs
+    (find_circ.py:681-690, weights :544/:563/:579).  Timed twice: scans only, and scans + merge
+    (D2H into the shared buffer + a barrier per step, so rank 0 could consume every step's merged
+    results).  Then a checked pass: rank 0 poisons the buffer, every rank scans and copies, and the
+    merged buffer must equal rank 0's single-rank scan of the whole stream byte for byte."""
+    import torch
+    from find_circ2_amd import scan
+    from find_circ2_amd.hotpath import ScanOutput
+    from find_circ2_amd.shard import SharedResults, batch_bounds, broadcast_name, my_batches, round_robin_batch
+    n = sb.n
+    bsz = round_robin_batch(n, ws)
+    mine = my_batches(n, bsz, rank, ws)
+    n_batches = len(batch_bounds(n, bsz))
+    merged = SharedResults(n, create=True, pin=True) if rank == 0 else None
+    name = broadcast_name(merged.name if rank == 0 else None) if ws > 1 else merged.name
+    if rank != 0:
+        merged = SharedResults(n, name=name, pin=True)
+    barrier(ws)                                  # every rank attached before rank 0 may unlink at the end
+    res = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
+    subs = [(lo, hi, sb.sub(lo, hi)) for _, lo, hi in mine]
+    stream = torch.cuda.current_stream(dev)
+
+    def step(copy: bool):
+        for lo, hi, s in subs:
+            scan(opt, g, s, out=ScanOutput(res[lo:hi], None, s.tw, s.stride), stream=stream.cuda_stream)
+            if copy:
+                merged.tensor[lo:hi].copy_(res[lo:hi], non_blocking=True)
+
+    for _ in range(max(1, warmup)):
+        step(True)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(False)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    scan_s = max_over_ranks(time.perf_counter() - t0, ws, dev)
+    barrier(ws)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step(True)
+        torch.cuda.synchronize(dev)
+        barrier(ws)
+    merge_s = max_over_ranks(time.perf_counter() - t0, ws, dev)
+    # checked pass
+    if rank == 0:
+        merged.array[:] = 0x5A5A5A5A5A5A5A5A
+    barrier(ws)
+    step(True)
+    torch.cuda.synchronize(dev)
+    barrier(ws)
+    out = None
+    if rank == 0:
+        equal = bool(np.array_equal(merged.array, ref64))
+        out = {
+            "value": round(n * steps / merge_s, 1), "unit": "anchor-pairs/s", "scaling": "strong",
+            "ms_per_step": round(merge_s / steps * 1e3, 4),
+            "scan_only": {"value": round(n * steps / scan_s, 1), "ms_per_step": round(scan_s / steps * 1e3, 4)},
+            "merge_ms_per_step": round((merge_s - scan_s) / steps * 1e3, 4),
+            "pairs_total": n, "batch_pairs": bsz, "n_batches": n_batches, "ranks": ws,
+            "merged_equals_single_rank": equal,
+            "note": "one %d-pair stream in %d contiguous batches of %d dealt round-robin to %d rank(s); each "
+                    "rank scans its batches and copies the 8-B results into a node-local pinned shared-memory "
+                    "buffer at their input offsets (host-side ordered merge, no collective on the data path); "
+                    "value = stream pairs / (scans + merge + per-step barrier), max over ranks; "
+                    "merge_ms_per_step = that minus the scan-only time" % (n, n_batches, bsz, ws)}
+    barrier(ws)
+    merged.close()
+    return out
 
 
 # ---------------------------------------------------------------------------
@@ -501,9 +631,14 @@ def window_carrying(opt, g, b, steps, dev, bpp):
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))              # before anything touches the GPU
     import torch
     ws, rank, local = setup_dist(args)
-    if args.gpus != ws and ws > 1:
+    if ws < args.gpus:
+        print("bench: --gpus %d but only %d rank(s) were started" % (args.gpus, ws), file=sys.stderr)
+        sys.exit(1)
+    if ws > args.gpus:
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, ws), file=sys.stderr)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
@@ -527,6 +662,16 @@ def main():
     res = out.host(b.n)
     hits = int((res["best_x"] >= 0).sum())
     b._bench_ref_results = torch.from_numpy(res.view(np.int64).copy())
+    # configs[3]: the same stream strong-scaled over the ranks with the host-side ordered merge
+    if args.no_strong:
+        strong = None
+    else:
+        sb = b if rank == 0 else build_workload(args, 0, dev)[2]
+        strong = strong_scaling(opt, g, sb, b._bench_ref_results.numpy() if rank == 0 else None, ws, rank, dev,
+                                args.steps, args.warmup)
+        if sb is not b:
+            del sb
+            torch.cuda.empty_cache()
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -554,6 +699,7 @@ def main():
                      "kernel_ms": round(kernel_ms, 4), "algo_bytes_per_pair": bpp,
                      "kernel": kernel_label(g, args.locus_ordered)},
         "cpu_baseline": None,
+        "strong_scaling": strong,
     }
     if args.workload == "hg19" and not args.locus_ordered and b.n == 50_000_000:
         line["roofline"]["access_pattern_ceiling"] = pattern_ceiling(opt, g, b, dev)

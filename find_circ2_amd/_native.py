@@ -101,7 +101,7 @@ class SynthCfg(ctypes.Structure):
 
 # every symbol include/fc2_bp.h declares (checked by tests/test_abi.py)
 EXPORTED = [
-    "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_set_tuning", "fc2_get_tuning", "fc2_max_fast_l",
+    "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_host_register", "fc2_host_unregister", "fc2_set_tuning", "fc2_get_tuning", "fc2_max_fast_l",
     "fc2_batch_geometry",
     "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch", "fc2_probe_pattern_launch",
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
@@ -177,6 +177,8 @@ def lib() -> ctypes.CDLL:
         "fc2_last_error": (ctypes.c_char_p, []),
         "fc2_device_count": (ctypes.c_int, [P(ctypes.c_int)]),
         "fc2_max_fast_l": (ctypes.c_int, []),
+        "fc2_host_register": (ctypes.c_int, [vp, u64]),
+        "fc2_host_unregister": (ctypes.c_int, [vp]),
         "fc2_set_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.c_int]),
         "fc2_get_tuning": (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_int)]),
         "fc2_batch_geometry": (ctypes.c_int, [P(Params), i32, P(u32), P(u32), P(u32)]),

@@ -1069,3 +1069,17 @@ extern "C" int fc2_device_count(int *count) {
     if (count) *count = (e == hipSuccess) ? c : 0;
     return FC2_OK;
 }
+
+extern "C" int fc2_host_register(void *ptr, uint64_t bytes) {
+    if (!ptr || !bytes) return fc2::fail(FC2_E_PARAM, "fc2_host_register: empty range");
+    const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterPortable);
+    if (e != hipSuccess) return fc2::fail(FC2_E_HIP, std::string("hipHostRegister: ") + hipGetErrorString(e));
+    return FC2_OK;
+}
+
+extern "C" int fc2_host_unregister(void *ptr) {
+    if (!ptr) return fc2::fail(FC2_E_PARAM, "fc2_host_unregister: null pointer");
+    const hipError_t e = hipHostUnregister(ptr);
+    if (e != hipSuccess) return fc2::fail(FC2_E_HIP, std::string("hipHostUnregister: ") + hipGetErrorString(e));
+    return FC2_OK;
+}

@@ -291,6 +291,25 @@ class PairBatch:
         b.host_pairs = None   # fetched lazily
         return b
 
+    def sub(self, lo: int, hi: int) -> "PairBatch":
+        """Pairs [lo, hi) of this batch as a batch of their own, sharing its device memory (no copy):
+        the SoA rows keep the parent's stride, so the view only moves each base pointer by lo.  This
+        is how a rank scans its contiguous share of a pair stream (shard.my_batches)."""
+        if not 0 <= lo <= hi <= self.n:
+            raise ValueError("sub-batch [%d, %d) outside [0, %d)" % (lo, hi, self.n))
+        if self.m_bytepath or self.perm is not None or self.slot is not None or self.win_words is not None:
+            raise ValueError("sub-batches of byte-path, reordered or window-carrying batches are not supported")
+        s = PairBatch()
+        s.options, s.device = self.options, self.device
+        s.n, s.stride = hi - lo, self.stride
+        s.rw, s.nw, s.tw, s.max_l, s.layout = self.rw, self.nw, self.tw, self.max_l, self.layout
+        s.pairs = self.pairs[16 * lo:16 * hi]
+        s.read_words = self.read_words[lo:]
+        s.read_nwords = self.read_nwords[lo:]
+        if self.host_pairs is not None:
+            s.host_pairs = self.host_pairs[lo:hi]
+        return s
+
     def fetch_host_pairs(self) -> np.ndarray:
         if self.host_pairs is None:
             self.host_pairs = self.pairs[:16 * self.n].cpu().numpy().view(N.PAIR_DTYPE).copy()

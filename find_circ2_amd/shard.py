@@ -64,6 +64,74 @@ def gather_ordered(local: Sequence[Tuple[int, np.ndarray]], n_batches: int, grou
     return ordered_merge(out, n_batches)
 
 
+def round_robin_batch(n: int, world: int, per_rank: int = 4, align: int = 512) -> int:
+    """Batch size for dealing n pairs round-robin: about `per_rank` batches per rank (balanced to
+    one batch), rounded up to `align` pairs so every batch starts on a 512-pair scan block."""
+    if n <= 0:
+        return align
+    b = -(-n // (max(1, world) * max(1, per_rank)))
+    return -(-b // align) * align
+
+
+class SharedResults:
+    """Node-local ordered merge of per-pair results: ONE host buffer of n 8-byte ``fc2_result``
+    records in /dev/shm that every rank on the node maps.  A rank copies each of its batches'
+    results (D2H, on its own stream) straight to the batch's input offset, so after a barrier rank
+    0 holds every result in input order without gathering or reordering anything -- the order
+    ``SpliceSiteStorage`` naming (find_circ.py:681-690) and the float weight sums (:544, :563,
+    :579) need.  The buffer is page-locked with ``fc2_host_register`` when a GPU is present, so the
+    copies run asynchronously at PCIe rate.
+
+    Create on rank 0 (``create=True``), then the others attach by ``name`` (broadcast it);
+    ``close()`` on every rank, rank 0 last (it unlinks)."""
+
+    def __init__(self, n: int, name: str = None, create: bool = False, pin: bool = False):
+        from multiprocessing import resource_tracker, shared_memory
+        self.n = int(n)
+        self.creator = create
+        self.shm = shared_memory.SharedMemory(name=name, create=create, size=max(8, 8 * self.n))
+        if not create:
+            # the attaching process must not unlink the segment when it exits (Python < 3.13 tracks
+            # every attach as if it owned the segment)
+            try:
+                resource_tracker.unregister(self.shm._name, "shared_memory")
+            except Exception:
+                pass
+        self.name = self.shm.name
+        self.array = np.ndarray((self.n,), np.int64, buffer=self.shm.buf)
+        self._pinned = False
+        if pin and self.n:
+            from . import _native as N
+            N.check(N.lib().fc2_host_register(self.array.ctypes.data, 8 * self.n))
+            self._pinned = True
+        import torch
+        self.tensor = torch.from_numpy(self.array)
+
+    def close(self):
+        if self.shm is None:
+            return
+        if self._pinned:
+            from . import _native as N
+            N.lib().fc2_host_unregister(self.array.ctypes.data)
+            self._pinned = False
+        self.tensor = None
+        self.array = None
+        self.shm.close()
+        if self.creator:
+            self.shm.unlink()
+        self.shm = None
+
+
+def broadcast_name(name, group=None) -> str:
+    """Rank 0's shared-memory segment name on every rank (host group)."""
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized():
+        return name
+    obj = [name]
+    dist.broadcast_object_list(obj, src=0, group=group)
+    return obj[0]
+
+
 def max_over_ranks(x: float, device=None, group=None) -> float:
     """Max of a scalar over ranks (timing); works on the nccl (GPU tensor) and gloo (CPU tensor) backends."""
     import torch

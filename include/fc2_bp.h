@@ -193,6 +193,13 @@ int         fc2_abi_version(void);
 const char *fc2_last_error(void);
 /* Returns FC2_OK and the device count (0 on a host without GPUs is not an error). */
 int         fc2_device_count(int *count);
+/* Page-lock (hipHostRegister, portable to every device) / release caller-owned host memory, e.g.
+ * a node-local shared-memory merge buffer that several per-GPU processes copy results into
+ * (find_circ2_amd/shard.py SharedResults): device-to-host copies into it then run at full PCIe rate
+ * and asynchronously on a side stream.  Replaces nothing in the reference (find_circ.py is one
+ * process); it backs the host-side ordered merge of SURVEY.md 8(e). */
+int         fc2_host_register(void *ptr, uint64_t bytes);
+int         fc2_host_unregister(void *ptr);
 
 /* Device side of the window-carrying form: the same rows as fc2_pack_windows, gathered from the
  * resident genome (needs g->wt); b supplies pairs/n/stride/max_l, pairs (device, = b->pairs) get

@@ -1,0 +1,48 @@
+"""bench.py's own rank launcher (``--gpus N`` without torch.distributed.run) and the configs[3]
+strong-scaling run with the host-side ordered merge (bench.strong_scaling, shard.SharedResults).
+
+CPU: the launcher must fail non-zero when its ranks cannot run (no GPU here) instead of quietly
+measuring one rank.  GPU: two ranks sharing cuda:0 scan one pair stream round-robin through the
+real kernel, merge the results in input order and must equal the single-rank scan byte for byte.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _env():
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    return env
+
+
+def test_launcher_fails_when_ranks_fail():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("checks the failure path on a host without GPUs")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                        "--warmup", "1", "--no-cpu-baseline", "--no-extra"], env=_env(), cwd=ROOT,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert "failed" in r.stderr
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+@pytest.mark.gpu
+def test_two_ranks_strong_scaling_merge_equals_single_rank():
+    r = subprocess.run([sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--workload", "cdr1as",
+                        "--pairs", "1000000", "--steps", "3", "--warmup", "1", "--no-cpu-baseline", "--no-extra"],
+                       env=_env(), cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert line["n_gpus"] == 2
+    st = line["strong_scaling"]
+    assert st["ranks"] == 2 and st["pairs_total"] == 1_000_000
+    assert st["merged_equals_single_rank"] is True
+    assert st["value"] > 0 and line["value"] > 0

@@ -76,3 +76,55 @@ def test_batches_cover_and_partition():
         shard.ordered_merge([[(0, np.zeros(1))], [(0, np.zeros(1))]], 1)
     with pytest.raises(ValueError):
         shard.ordered_merge([[(0, np.zeros(1))]], 2)
+
+
+def _shm_worker(rank, world, port, n, batch, q):
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pairs = np.arange(n, dtype=np.int64) * 31 + 7
+    merged = shard.SharedResults(n, create=True) if rank == 0 else None
+    name = shard.broadcast_name(merged.name if rank == 0 else None)
+    if rank != 0:
+        merged = shard.SharedResults(n, name=name)
+    dist.barrier()
+    if rank == 0:
+        merged.array[:] = -1                     # poison: every slot must be written by some rank
+    dist.barrier()
+    for _, s, e in shard.my_batches(n, batch, rank, world):
+        merged.array[s:e] = fake_scan(pairs[s:e]).view(np.int64)
+    dist.barrier()
+    if rank == 0:
+        q.put(merged.array.copy())
+    dist.barrier()
+    merged.close()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [1000, 1, 0])
+def test_gloo_two_ranks_shared_memory_merge(n):
+    """bench.py's configs[3] merge (shard.SharedResults): ranks write their round-robin batches'
+    results into one node-local buffer at input offsets; rank 0 reads them in input order."""
+    world = 2
+    batch = shard.round_robin_batch(n, world, per_rank=3, align=64)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shm_worker, args=(r, world, port, n, batch, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    merged = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert np.array_equal(merged, fake_scan(np.arange(n, dtype=np.int64) * 31 + 7).view(np.int64))
+
+
+def test_round_robin_batch_balance():
+    for n, world in [(50_000_000, 1), (50_000_000, 8), (1_000_000, 2), (513, 4), (1, 8)]:
+        b = shard.round_robin_batch(n, world)
+        assert b % 512 == 0 and b > 0
+        counts = [sum(e - s for _, s, e in shard.my_batches(n, b, r, world)) for r in range(world)]
+        assert sum(counts) == n
+        assert max(counts) - min(counts) <= b
