@@ -26,6 +26,8 @@ FC2_E_RANGE = -4
 FC2_E_IO = -5
 FC2_E_KEY = -6
 
+MAX_READ_LEN = 32767          # FC2_MAX_READ_LEN: longest read_part (x < 2^15 fits best_x, 2(l+1) ties fit n_ties)
+
 PAIR_BACKSPLICE = 0x01
 PAIR_PRIMARY_REV = 0x02
 PAIR_READ_N = 0x04

@@ -1063,8 +1063,9 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         }
     }
     for (const Span &s : h->spans)
-        if (s.eval >= 0 && s.read_len > 65535)
-            return fc2::fail(FC2_E_RANGE, "read_part longer than 65535 bases");
+        if (s.eval >= 0 && s.read_len > FC2_MAX_READ_LEN)
+            return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
+                                              " bases (fc2_result.best_x is 16-bit)");
     h->n_pairs += h->b_pairs.size();
     b->n = h->b_pairs.size();
     b->reads = (const uint8_t *)h->arena.data();

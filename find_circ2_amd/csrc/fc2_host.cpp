@@ -614,7 +614,7 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
     const int e = eff_anchor(p);
     const int T = n_workers(n_threads);
     std::atomic<uint64_t> nbp{0};
-    std::atomic<int64_t> bad_chrom{-1}, bad_rows{-1}, bad_dist{-1};
+    std::atomic<int64_t> bad_chrom{-1}, bad_rows{-1}, bad_dist{-1}, bad_len{-1};
     const int nch = f ? (int)f->chroms.size() : 0;
     parallel_for(n, T, [&](uint64_t b, uint64_t en) {
         uint64_t local_bp = 0;
@@ -625,6 +625,7 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
             for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = 0;
             for (uint32_t j = 0; j < nw; ++j) read_nwords[(uint64_t)j * stride + i] = 0;
             if (pr.flags & FC2_PAIR_SKIP) continue;
+            if (pr.read_len > FC2_MAX_READ_LEN) { int64_t x = -1; bad_len.compare_exchange_strong(x, (int64_t)i); continue; }
             if (f && (int)pr.chrom >= nch) { int64_t x = -1; bad_chrom.compare_exchange_strong(x, (int64_t)i); continue; }
             const int L = pr.read_len;
             const int l = L - 2 * e;
@@ -685,6 +686,9 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
     if (bad_chrom.load() >= 0)
         return fail(FC2_E_KEY, "pair " + std::to_string(bad_chrom.load()) +
                                    ": chromosome not in the genome index (reference KeyError, find_circ.py:193)");
+    if (bad_len.load() >= 0)
+        return fail(FC2_E_RANGE, "pair " + std::to_string(bad_len.load()) + ": read_part longer than " +
+                                     std::to_string(FC2_MAX_READ_LEN) + " bases (fc2_result.best_x is 16-bit)");
     if (bad_rows.load() >= 0) return fail(FC2_E_PARAM, "pair " + std::to_string(bad_rows.load()) + ": read rows too narrow");
     if (bad_dist.load() >= 0) return fail(FC2_E_RANGE, "maxdist > 255 with reads whose l > 255 is not supported");
     if (n_bytepath) *n_bytepath = nbp.load();

@@ -184,8 +184,8 @@ class PairBatch:
                 off[1:] = np.cumsum(lens[:-1]).astype(np.uint64)
             buf = np.frombuffer(b"".join(reads) + b"\0" * 16, np.uint8)
         n = len(lens)
-        if n and lens.max() > 65535:
-            raise ValueError("read_part longer than 65535 bases")
+        if n and lens.max() > N.MAX_READ_LEN:
+            raise ValueError("read_part longer than %d bases (fc2_result.best_x is 16-bit)" % N.MAX_READ_LEN)
         hp = np.zeros(n, N.PAIR_DTYPE)
         hp["a_pos"] = np.asarray(a_pos, np.int64)
         hp["b_aend"] = np.asarray(b_aend, np.int64)
@@ -702,17 +702,34 @@ class JunctionSpan:
         self.read_part = primary.seq[q_start:q_end]
         self.chrom = chrom
 
+    min_uniq_qual = 2   # options.min_uniq_qual (find_circ.py:393), read by is_uniq like the reference
+
     def is_uniq_for(self, min_uniq_qual: int) -> bool:        # find_circ.py:846-848
         return self.uniq >= min_uniq_qual
+
+    @property
+    def is_uniq(self) -> bool:                                # find_circ.py:846-848
+        return self.uniq >= self.min_uniq_qual
 
     @property
     def is_backsplice(self):                                  # find_circ.py:850-852
         return self.dist < 0
 
     def find_breakpoints(self):                               # find_circ.py:854
+        """The reference method: the list of ties, or the exception the reference raises for this
+        span (KeyError for a chromosome missing from the FASTA, :193, or a non-ACGTN splice
+        signal, :927)."""
         if JunctionSpan.engine is None:
             raise RuntimeError("no BreakpointEngine installed (BreakpointEngine(...).install())")
-        return JunctionSpan.engine.find_breakpoints_batch([self])[0]
+        return splices_or_raise(JunctionSpan.engine.find_breakpoints_batch([self])[0])
+
+
+def splices_or_raise(r):
+    """A ``find_breakpoints_batch`` entry as the reference method returns it: raises the
+    per-span exception, else returns the tie list."""
+    if isinstance(r, BaseException):
+        raise r
+    return r
 
 
 class BreakpointEngine:
@@ -726,17 +743,25 @@ class BreakpointEngine:
         JunctionSpan.engine = self
         return self
 
-    def find_breakpoints_batch(self, spans: Sequence[JunctionSpan]) -> List[List[Splice]]:
+    def find_breakpoints_batch(self, spans: Sequence[JunctionSpan]) -> List:
+        """``find_breakpoints()`` of every span in ONE launch.  Entry i is span i's tie list, or
+        -- where the reference method would raise -- the exception instance, so a caller that
+        evaluates spans speculatively raises it only when ``record_hits`` reaches that span
+        (``splices_or_raise``): KeyError(chrom) for a chromosome missing from the FASTA
+        (indexed_fasta.get_data, find_circ.py:193; the pair is not scanned), KeyError for a
+        non-ACGTN splice signal (:927), BreakpointError for windows outside get_data's range."""
         if not spans:
             return []
         reads = []
         for s in spans:
             r = s.read_part
             reads.append(r if isinstance(r, bytes) else r.encode("latin-1"))
+        missing = 0xFFFFFFFF
         chrom = [self.genome.chrom_index_or_missing(s.chrom) for s in spans]
-        flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.strand == '-' else 0)
-                 for s in spans]
+        flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.strand == '-' else 0) |
+                 (N.PAIR_SKIP if c == missing else 0) for s, c in zip(spans, chrom)]
         b = PairBatch.pack(self.options, self.genome, reads, [s.align_A.pos for s in spans],
-                           [s.align_B.aend for s in spans], chrom, flags)
+                           [s.align_B.aend for s in spans], [0 if c == missing else c for c in chrom], flags)
         out = scan(self.options, self.genome, b)
-        return decode_splices(self.options, self.genome, b, out, spans)
+        res = decode_splices(self.options, self.genome, b, out, spans, raise_errors=False)
+        return [KeyError(s.chrom) if c == missing else r for s, r, c in zip(spans, res, chrom)]

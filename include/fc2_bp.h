@@ -76,6 +76,11 @@ typedef struct fc2_pair {
     uint8_t  npos;      /* FC2_PAIR_READ_N1: position of the read part's single 'N'; else 0 */
 } fc2_pair;
 
+/* Longest read_part the library accepts (fc2_pack_pairs / fc2_caller_next fail with FC2_E_RANGE
+ * above it): every breakpoint index x <= l < 2^15 fits fc2_result.best_x, and the at most
+ * 2(l+1) ties of --non-canonical fit n_ties. */
+#define FC2_MAX_READ_LEN 32767
+
 /* ---- per-pair result, 8 bytes ------------------------------------------- */
 /* best_x = breakpoint index x of ties[0] (the Splice record_hits keeps,
  * find_circ.py:1312-1317), -1 if find_breakpoints returned [].

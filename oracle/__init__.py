@@ -185,3 +185,27 @@ def scan_windows(p: OrcParams, reads, wins: np.ndarray, win_off: np.ndarray, a_p
                            _ptr(a_pos), _ptr(b_aend), _ptr(is_bs), _ptr(primary_rev), int(use_fast),
                            _ptr(n_ties), _ptr(first), _ptr(at), cap, _ptr(ao))
     return OracleResult(n_ties, first, at, ao)
+
+
+def scan_planes(p: OrcParams, units: np.ndarray, nplane: np.ndarray, chrom_start: np.ndarray,
+                chrom_size: np.ndarray, pairs: np.ndarray, read_words: np.ndarray, read_nwords: np.ndarray,
+                rw: int, nw: int, stride: int, n: int, n_threads: int = 16):
+    """First tie of every pair of a batch in the device layouts of include/fc2_bp.h (packed rows +
+    2-bit genome planes), encoded as the kernel's 8-byte fc2_result words (uint64 [n]); see
+    orc_scan_planes.  Returns (words, number of pairs that could not be checked)."""
+    L = lib()
+    if not hasattr(L, "_planes_sig"):
+        vp = ctypes.c_void_p
+        L.orc_scan_planes.restype = ctypes.c_int64
+        L.orc_scan_planes.argtypes = [ctypes.POINTER(OrcParams), vp, vp, vp, vp, ctypes.c_int, vp, vp, vp,
+                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int64, vp,
+                                      ctypes.c_int]
+        L._planes_sig = True
+    arrs = [np.ascontiguousarray(a) for a in (units, nplane, chrom_start, chrom_size, pairs, read_words, read_nwords)]
+    assert arrs[0].dtype.itemsize * arrs[0].size >= 16 and arrs[4].nbytes >= 16 * n
+    assert arrs[5].nbytes >= 8 * rw * stride and arrs[6].nbytes >= 8 * nw * stride
+    out = np.zeros(n, np.uint64)
+    skipped = L.orc_scan_planes(ctypes.byref(p), *[a.ctypes.data for a in arrs[:4]], len(chrom_size),
+                                *[a.ctypes.data for a in arrs[4:]], rw, nw, stride, n, out.ctypes.data,
+                                int(n_threads))
+    return out, int(skipped)

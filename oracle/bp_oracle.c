@@ -405,3 +405,125 @@ int64_t orc_scan_windows(const orc_params *p, int64_t n,
     free(tmp); free(ties);
     return total_all;
 }
+
+/* ------------------------------------------------------------------ */
+/* whole-batch check straight from the device layouts (full-size parity) */
+/* ------------------------------------------------------------------ */
+/* The same search, fed from the documented device layouts of include/fc2_bp.h instead of a
+ * FASTA: the internal read part I is decoded from the tight bit-sliced rows (low code bits at
+ * [0,l), high at [l,2l), 'N' from the N row of READ_N pairs), the windows Af/Bf from the 2-bit
+ * genome unit planes + N plane (get_data's 'N' padding outside [0, size), find_circ.py:194-211),
+ * and the first tie is encoded as the 8-byte fc2_result word the kernel writes (best_x, dist, ov,
+ * n_ties, info = DONE | MINUS | 3-bit codes of A[x]A[x+1]B[x]B[x+1] | KEY error).  Threads split
+ * the batch.  Returns the number of pairs it could not check (BYTEPATH pairs, chromosome index
+ * out of range: their word is left 0). */
+#include <pthread.h>
+
+typedef struct {            /* fc2_pair */
+    int32_t a_pos, b_aend;
+    uint32_t chrom;
+    uint16_t read_len;
+    uint8_t flags, npos;
+} orc_pair;
+
+typedef struct {
+    const orc_params *p;
+    const uint64_t *units, *nplane, *chrom_start;
+    const int64_t *chrom_size;
+    int n_chrom;
+    const orc_pair *pairs;
+    const uint64_t *rows, *nrows;
+    uint64_t stride;
+    uint32_t rw, nw;
+    int64_t lo, hi;
+    uint64_t *out;
+    int64_t skipped;
+} orc_plane_job;
+
+static unsigned char orc_base(const orc_plane_job *J, int c, int64_t pos) {
+    static const unsigned char code[4] = {'A', 'C', 'G', 'T'};
+    if (pos < 0 || pos >= J->chrom_size[c]) return 'N';
+    const uint64_t g = J->chrom_start[c] + (uint64_t)pos, u = g >> 6, b = g & 63;
+    if ((J->nplane[u] >> b) & 1) return 'N';
+    return code[((J->units[2 * u] >> b) & 1) | (((J->units[2 * u + 1] >> b) & 1) << 1)];
+}
+
+static unsigned orc_code3(unsigned char c) {
+    switch (c) { case 'A': return 0; case 'C': return 1; case 'G': return 2; case 'T': return 3; default: return 4; }
+}
+
+static void *orc_plane_worker(void *arg) {
+    orc_plane_job *J = (orc_plane_job *)arg;
+    const orc_params *p = J->p;
+    const int e = p->asize - p->margin;
+    int maxL = 0;
+    for (int64_t i = J->lo; i < J->hi; i++) if (J->pairs[i].read_len > maxL) maxL = J->pairs[i].read_len;
+    const int hcap = 2 * (maxL + 2) + 4;
+    unsigned char *read = (unsigned char *)malloc((size_t)maxL + 8);
+    unsigned char *Af = (unsigned char *)malloc((size_t)maxL + 8);
+    unsigned char *Bf = (unsigned char *)malloc((size_t)maxL + 8);
+    orc_hit *tmp = (orc_hit *)malloc(sizeof(orc_hit) * (size_t)hcap);
+    orc_hit *ties = (orc_hit *)malloc(sizeof(orc_hit) * (size_t)hcap);
+    const uint64_t none = 0xFFFFull | ((uint64_t)0x8000u << 48);
+    for (int64_t i = J->lo; i < J->hi; i++) {
+        const orc_pair pr = J->pairs[i];
+        J->out[i] = 0;
+        if (pr.flags & 0x10) { J->out[i] = none; continue; }                     /* SKIP */
+        if ((pr.flags & 0x08) || (int)pr.chrom >= J->n_chrom) { J->skipped++; continue; }   /* BYTEPATH */
+        const int L = pr.read_len, l = L - 2 * e;
+        if (l < 0 || e <= 0) { J->out[i] = none; continue; }
+        for (int k = 0; k < e; k++) read[k] = read[e + l + k] = 'A';
+        for (int j = 0; j < l; j++) {
+            const int t = l + j;
+            const unsigned lo = (unsigned)(J->rows[(uint64_t)(j >> 6) * J->stride + i] >> (j & 63)) & 1u;
+            const unsigned hi = (unsigned)(J->rows[(uint64_t)(t >> 6) * J->stride + i] >> (t & 63)) & 1u;
+            unsigned char c = "ACGT"[lo | (hi << 1)];
+            if ((pr.flags & 0x04) && ((J->nrows[(uint64_t)(j >> 6) * J->stride + i] >> (j & 63)) & 1)) c = 'N';
+            read[e + j] = c;
+        }
+        const int W = l + 2;
+        const int64_t as = (int64_t)pr.a_pos + e, bs = (int64_t)pr.b_aend - e - W;
+        for (int k = 0; k < W; k++) { Af[k] = orc_base(J, (int)pr.chrom, as + k); Bf[k] = orc_base(J, (int)pr.chrom, bs + k); }
+        const int r = orc_find_breakpoints_fast(p, read, L, Af, Bf, pr.a_pos, pr.b_aend, pr.flags & 1,
+                                                (pr.flags >> 1) & 1, tmp, ties, hcap);
+        if (r < 0) { J->out[i] = none | ((uint64_t)(r == -ORC_ERR_KEY ? 0x2000u : 0x4000u) << 48); continue; }
+        if (r == 0) { J->out[i] = none; continue; }
+        const orc_hit *h = &ties[0];
+        const int x = h->x;
+        const unsigned g12 = orc_code3(Af[x]) | (orc_code3(Af[x + 1]) << 3) | (orc_code3(Bf[x]) << 6) |
+                             (orc_code3(Bf[x + 1]) << 9);
+        const unsigned info = 0x8000u | (h->strand == '-' ? 1u : 0u) | ((g12 << 1) & 0x1FFEu);
+        const unsigned nt = r > 0xFFFF ? 0xFFFFu : (unsigned)r;
+        const unsigned dist = h->dist > 255 ? 255u : (unsigned)h->dist;
+        J->out[i] = (uint64_t)(uint16_t)(int16_t)x | ((uint64_t)(dist & 0xFF) << 16) | ((uint64_t)(h->ov & 0xFF) << 24) |
+                    ((uint64_t)nt << 32) | ((uint64_t)info << 48);
+    }
+    free(read); free(Af); free(Bf); free(tmp); free(ties);
+    return NULL;
+}
+
+int64_t orc_scan_planes(const orc_params *p, const uint64_t *units, const uint64_t *nplane,
+                        const uint64_t *chrom_start, const int64_t *chrom_size, int n_chrom,
+                        const void *pairs, const uint64_t *read_words, const uint64_t *read_nwords,
+                        uint32_t rw, uint32_t nw, uint64_t stride, int64_t n, uint64_t *out, int n_threads) {
+    (void)rw; (void)nw;
+    if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
+    orc_plane_job jobs[256];
+    pthread_t th[256];
+    const int64_t per = (n + n_threads - 1) / n_threads;
+    int started = 0;
+    for (int t = 0; t < n_threads; t++) {
+        orc_plane_job *J = &jobs[t];
+        J->p = p; J->units = units; J->nplane = nplane; J->chrom_start = chrom_start; J->chrom_size = chrom_size;
+        J->n_chrom = n_chrom; J->pairs = (const orc_pair *)pairs; J->rows = read_words; J->nrows = read_nwords;
+        J->stride = stride; J->rw = rw; J->nw = nw; J->out = out; J->skipped = 0;
+        J->lo = t * per; J->hi = (t + 1) * per < n ? (t + 1) * per : n;
+        if (J->lo >= J->hi) break;
+        pthread_create(&th[t], NULL, orc_plane_worker, J);
+        started++;
+    }
+    int64_t skipped = 0;
+    for (int t = 0; t < started; t++) { pthread_join(th[t], NULL); skipped += jobs[t].skipped; }
+    return skipped;
+}

@@ -1,0 +1,68 @@
+"""Every pair of the bench batches against the oracle (full-size parity).
+
+bench.py's headline batch (configs[2]: 50M synthetic 100 bp pairs, seed 1337, read order, on the
+hg19-shaped synthetic genome) and its configs[4] share (25M pairs, read lengths 120..150 bp) are
+generated exactly as bench.build_workload makes them, scanned by the product kernel, and every
+one of the 8-byte result words is compared with the oracle's (oracle.scan_planes: the C
+restatement of find_circ.py:854-974 fed from the batch's packed rows and the genome's 2-bit
+planes, on 16 host threads).  Integer work: bit-exact, no tolerance.
+"""
+import argparse
+import os
+import sys
+import time
+
+import numpy as np
+import pytest
+
+import oracle
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from find_circ2_amd import _native as N, scan  # noqa: E402
+
+
+def _check(args):
+    import bench
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    dev = torch.device("cuda", 0)
+    opt, g, b = bench.build_workload(args, 0, dev)
+    res = scan(opt, g, b).results[:b.n].cpu().numpy().view(np.uint64)
+    torch.cuda.synchronize(dev)
+    hp = b.pairs[:16 * b.n].cpu().numpy()
+    words = b.read_words[:b.rw * b.stride].cpu().numpy()
+    nwords = b.read_nwords[:b.nw * b.stride].cpu().numpy()
+    units = g.units.cpu().numpy().view(np.uint64)
+    nplane = g.nplane.cpu().numpy().view(np.uint64)
+    p = oracle.params(opt.asize, opt.margin, opt.maxdist, opt.noncanonical, opt.strandpref, opt.allhits)
+    t0 = time.time()
+    exp, skipped = oracle.scan_planes(p, units, nplane, np.asarray(g.chrom_start, np.uint64),
+                                      np.asarray(g.sizes, np.int64), hp, words, nwords, b.rw, b.nw, b.stride, b.n,
+                                      n_threads=16)
+    print("oracle: %d pairs in %.1f s" % (b.n, time.time() - t0))
+    assert skipped == 0
+    err = (exp >> np.uint64(48)) & np.uint64(0x6000)
+    ok = err == 0
+    mism = np.nonzero(res[ok] != exp[ok])[0]
+    assert mism.size == 0, (mism.size, np.nonzero(ok)[0][mism[:5]], res[ok][mism[:5]], exp[ok][mism[:5]])
+    assert np.array_equal((res[~ok] >> np.uint64(48)) & np.uint64(0x6000), err[~ok])
+    hits = int(((res & np.uint64(0xFFFF)) != np.uint64(0xFFFF)).sum())
+    assert hits > b.n // 3
+    return b.n, hits
+
+
+def test_configs2_bench_batch_every_pair():
+    a = argparse.Namespace(workload="hg19", pairs=50_000_000, read_len=100, locus_ordered=False)
+    n, hits = _check(a)
+    assert n == 50_000_000
+
+
+def test_configs4_share_every_pair():
+    a = argparse.Namespace(workload="hg19", pairs=25_000_000, read_len=150, read_len_min=120, locus_ordered=False)
+    n, hits = _check(a)
+    assert n == 25_000_000
