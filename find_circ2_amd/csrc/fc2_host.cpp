@@ -361,7 +361,8 @@ extern "C" int fc2_batch_geometry(const fc2_params *p, int32_t max_read_len, uin
     const int lfast = lmax > kMaxFastL ? kMaxFastL : lmax;
     if (rw) *rw = (uint32_t)std::max(1, (2 * lfast + 63) / 64);
     if (nw) *nw = (uint32_t)std::max(1, (lfast + 63) / 64);
-    if (tw) *tw = (uint32_t)(2 * std::max(1, (lmax + 1 + 63) / 64));
+    // the register kernels write (l + 2 + 63) / 64 tie words per strand (fc2_bp_scan_launch checks it)
+    if (tw) *tw = (uint32_t)(2 * std::max(1, (lmax + 2 + 63) / 64));
     return FC2_OK;
 }
 

@@ -43,6 +43,10 @@ def test_info_calls(L):
     assert (rw.value, nw.value, tw.value) == (3, 2, 4)      # l=74: 148 bits, 74 bits, 75 x-bits
     assert L.fc2_batch_geometry(ctypes.byref(p), 150, ctypes.byref(rw), ctypes.byref(nw), ctypes.byref(tw)) == 0
     assert (rw.value, nw.value, tw.value) == (4, 2, 4)      # l=124
+    # l = 63 / 127: the kernels write (l + 2 + 63) // 64 tie words per strand (r2 fix: was l + 1)
+    for L_, t in ((26 + 62, 2), (26 + 63, 4), (26 + 127, 6), (26 + 126, 4)):
+        assert L.fc2_batch_geometry(ctypes.byref(p), L_, ctypes.byref(rw), ctypes.byref(nw), ctypes.byref(tw)) == 0
+        assert tw.value == t, (L_, tw.value)
     bad = N.Params(2, 2, 2, 0, 0, 0, 0)
     assert L.fc2_batch_geometry(ctypes.byref(bad), 100, None, None, None) == N.FC2_E_PARAM
     assert b"asize - margin" in L.fc2_last_error()
