@@ -118,7 +118,7 @@ EXPORTED = [
     "fc2_ingest_next", "fc2_ingest_counts_get", "fc2_ingest_set_bam_out", "fc2_ingest_close_bam_out",
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
-    "fc2_caller_submit", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
+    "fc2_caller_submit", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
 ]
 
 
@@ -230,6 +230,7 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_close": (None, [vp]),
         "fc2_caller_next": (ctypes.c_int, [vp, P(CallerBatch), P(ctypes.c_int)]),
         "fc2_caller_submit": (ctypes.c_int, [vp, vp, vp, u32, u64]),
+        "fc2_caller_queued": (ctypes.c_int, [vp]),
         "fc2_caller_take": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_rows": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_counter": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(ctypes.c_double)]),

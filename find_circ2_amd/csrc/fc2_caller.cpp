@@ -213,12 +213,22 @@ struct fc2_caller {
     std::vector<int32_t> tid2chrom;
     const fc2_fasta *fasta = nullptr;
     bool eof = false;
-    // the pending chunk
+    // the chunk being formed (fc2_caller_next) or recorded (fc2_caller_submit)
     std::vector<Frag> frags;
     std::vector<Span> spans;
     std::string arena;                          // read_part bytes
     std::vector<uint64_t> b_off;
     std::vector<fc2_pair> b_pairs;
+    // chunks handed out by fc2_caller_next and not yet submitted, oldest first: the caller may
+    // read ahead (form chunk k+1 while chunk k is on the GPU); submit always records the oldest
+    struct Chunk {
+        std::vector<Frag> frags;
+        std::vector<Span> spans;
+        std::string arena;
+        std::vector<uint64_t> b_off;
+        std::vector<fc2_pair> b_pairs;
+    };
+    std::deque<Chunk> queued;
     // aggregation
     struct Storage {
         std::string prefix;
@@ -1019,6 +1029,8 @@ extern "C" void fc2_caller_close(fc2_caller *h) {
 
 extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     if (!h || !b) return fc2::fail(FC2_E_PARAM, "fc2_caller_next: null argument");
+    if (h->queued.size() >= FC2_CALLER_MAX_QUEUED)
+        return fc2::fail(FC2_E_PARAM, "fc2_caller_next: too many chunks not submitted");
     h->frags.clear();
     h->spans.clear();
     h->arena.clear();
@@ -1067,17 +1079,36 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
                                               " bases (fc2_result.best_x is 16-bit)");
     h->n_pairs += h->b_pairs.size();
-    b->n = h->b_pairs.size();
-    b->reads = (const uint8_t *)h->arena.data();
-    b->read_off = h->b_off.data();
-    b->pairs = h->b_pairs.data();
+    h->queued.emplace_back();
+    fc2_caller::Chunk &c = h->queued.back();
+    c.frags.swap(h->frags);
+    c.spans.swap(h->spans);
+    c.arena.swap(h->arena);
+    c.b_off.swap(h->b_off);
+    c.b_pairs.swap(h->b_pairs);
+    b->n = c.b_pairs.size();
+    b->reads = (const uint8_t *)c.arena.data();
+    b->read_off = c.b_off.data();
+    b->pairs = c.b_pairs.data();
     if (eof) *eof = h->eof ? 1 : 0;
     return FC2_OK;
 }
 
+extern "C" int fc2_caller_queued(const fc2_caller *h) { return h ? (int)h->queued.size() : 0; }
+
 extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const uint64_t *tiemask, uint32_t tw,
                                  uint64_t stride) {
     if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: null argument");
+    if (h->queued.empty()) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: no chunk handed out by fc2_caller_next");
+    {
+        fc2_caller::Chunk &c = h->queued.front();
+        h->frags.swap(c.frags);
+        h->spans.swap(c.spans);
+        h->arena.swap(c.arena);
+        h->b_off.swap(c.b_off);
+        h->b_pairs.swap(c.b_pairs);
+        h->queued.pop_front();
+    }
     if (!h->b_pairs.empty() && !results) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: results missing");
     if (h->o.allhits && !h->b_pairs.empty() && (!tiemask || tw < 2 || stride < h->b_pairs.size()))
         return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: --all-hits needs the tie mask");
