@@ -67,6 +67,9 @@ def build_parser() -> optparse.OptionParser:
     a("", "--no-linear", dest="nolinear", default=False, action="store_true", help="skip linear junctions")
     a("", "--no-multi", dest="multi_events", default=True, action="store_false", help="do not record multi-events")
     a("", "--device", dest="device", default="cuda:0", help="HIP device (find_circ2_amd extension)")
+    a("", "--gpus", dest="gpus", type=int, default=1,
+      help="spread the breakpoint search over this many GPUs from --device on (chunks dealt round-robin, "
+           "results merged in input order; more GPUs than present share devices round-robin)")
     a("", "--python-ingest", dest="python_ingest", default=False, action="store_true",
       help="parse and group alignments in Python instead of the native ingest (implies --python-caller)")
     a("", "--python-caller", dest="python_caller", default=False, action="store_true",
@@ -227,12 +230,25 @@ def _finish(options, seconds, n_reads, logger, counters, n_spans, eval_seconds):
     logger.info('breakpoint search: {0} spans, {1:.3f} s incl. pack/transfer/decode'.format(n_spans, eval_seconds))
 
 
+def _devices(options):
+    """--gpus N devices starting at --device (cuda:k, cuda:k+1, ...), wrapping round the devices
+    present (a 1-GPU box runs N scanners on cuda:0)."""
+    import torch
+    if options.gpus <= 1:
+        return [options.device]
+    base = torch.device(options.device)
+    ndev = max(1, torch.cuda.device_count())
+    first = base.index or 0
+    return ["cuda:%d" % ((first + k) % ndev) for k in range(options.gpus)]
+
+
 def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path="") -> int:
     """The read loop in C++ (include/fc2_caller.h); only the breakpoint search is called from here."""
     from .caller import BED_HEADER, MULTI_HEADER
     from .native_caller import NativeCaller, gpu_batch_evaluator
     if evaluator_factory is None:
-        evaluate, names, fasta, dummy = gpu_batch_evaluator(genome, hp), genome.names, genome.fasta, genome.dummy
+        evaluate = gpu_batch_evaluator(genome, hp, devices=_devices(options))
+        names, fasta, dummy = genome.names, genome.fasta, genome.dummy
     else:
         engine = getattr(evaluator_factory, "batch", None)
         if engine is None:

@@ -1079,6 +1079,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
                                               " bases (fc2_result.best_x is 16-bit)");
     h->n_pairs += h->b_pairs.size();
+    h->arena.append(16, '\0');                 // readers of the batch may load whole words past the end
     h->queued.emplace_back();
     fc2_caller::Chunk &c = h->queued.back();
     c.frags.swap(h->frags);

@@ -639,21 +639,47 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
                 if ((uint64_t)2 * l > (uint64_t)rw * 64 || (uint64_t)l > (uint64_t)nw * 64) {
                     int64_t x = -1; bad_rows.compare_exchange_strong(x, (int64_t)i); continue;
                 }
-                // tight bit-sliced row: low bits at [0, l), high bits at [l, 2l)
-                for (int j = 0; j < l; ++j) {
-                    const uint32_t pc = pack_code(I[j]);
-                    if (pc & 8u) { bytepath = true; break; }
-                    const int cl = (pc & 4u) ? 4 : (int)pc;
-                    if (cl == 4) {
-                        anyN = true;
-                        if (n_count++ == 0) n_first = j;
-                        read_nwords[(uint64_t)(j >> 6) * stride + i] |= 1ull << (j & 63);
-                        continue;
+                // tight bit-sliced row: low bits at [0, l), high bits at [l, 2l); the row words are
+                // built in registers 64 bases at a time and stored once (no strided read-modify-write)
+                uint64_t lo_w[(kMaxFastL + 63) / 64] = {0}, hi_w[(kMaxFastL + 63) / 64] = {0},
+                         n_w[(kMaxFastL + 63) / 64] = {0};
+                uint32_t any_exotic = 0;
+                for (int j0 = 0; j0 < l; j0 += 64) {
+                    const int m = std::min(64, l - j0);
+                    uint64_t lo = 0, hi = 0, nn = 0;
+                    for (int j = 0; j < m; ++j) {
+                        const uint32_t pc = pack_code(I[j0 + j]);
+                        lo |= (uint64_t)(pc & 1u) << j;
+                        hi |= (uint64_t)((pc >> 1) & 1u) << j;
+                        nn |= (uint64_t)((pc >> 2) & 1u) << j;
+                        any_exotic |= pc;
                     }
-                    if (cl & 1) read_words[(uint64_t)(j >> 6) * stride + i] |= 1ull << (j & 63);
-                    if (cl & 2) {
-                        const int t = l + j;
-                        read_words[(uint64_t)(t >> 6) * stride + i] |= 1ull << (t & 63);
+                    lo_w[j0 >> 6] = lo & ~nn;              // 'N' is code 00 plus its N bit
+                    hi_w[j0 >> 6] = hi & ~nn;
+                    n_w[j0 >> 6] = nn;
+                }
+                if (any_exotic & 8u) {
+                    bytepath = true;
+                } else {
+                    // low plane at bit offset 0, high plane at bit offset l, both into the row words
+                    const int nlw = (l + 63) / 64;
+                    uint64_t row[2 * ((kMaxFastL + 63) / 64) + 1] = {0};
+                    for (int k = 0; k < nlw; ++k) row[k] = lo_w[k];
+                    // clear bits >= l of the low plane's last word is implicit (they were never set)
+                    const int sh = l & 63, wo = l >> 6;
+                    for (int k = 0; k < nlw; ++k) {
+                        row[wo + k] |= sh ? (hi_w[k] << sh) : hi_w[k];
+                        if (sh) row[wo + k + 1] |= hi_w[k] >> (64 - sh);
+                    }
+                    for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = row[j];
+                    for (int k = 0; k < nlw && any_exotic & 4u; ++k) {
+                        read_nwords[(uint64_t)k * stride + i] = n_w[k];
+                        if (n_w[k]) {
+                            anyN = true;
+                            const int c = __builtin_popcountll(n_w[k]);
+                            if (n_count == 0) n_first = k * 64 + __builtin_ctzll(n_w[k]);
+                            n_count += c;
+                        }
                     }
                 }
             }

@@ -129,6 +129,24 @@ class Genome:
         g.dummy = True
         return g
 
+    def replicate(self, device) -> "Genome":
+        """The same genome resident on another device (one copy per GPU): device
+        tables copied device to device, the host FASTA handle shared (this object keeps owning it;
+        the replica must not outlive it)."""
+        torch = _torch()
+        g = Genome()
+        g.device = torch.device(device)
+        for k in ("names", "sizes", "chrom_start", "n_units", "nsuper_shift", "nsuper_words", "wt_bytes",
+                  "wt_twin_off", "dummy", "n_exotic", "regular", "_index"):
+            setattr(g, k, getattr(self, k))
+        for k in ("units", "nplane", "ncoarse", "units_twin", "nsuper", "wt", "d_chrom_start", "d_chrom_size"):
+            t = getattr(self, k)
+            setattr(g, k, None if t is None else t.to(g.device, copy=True))
+        g.fasta = self.fasta
+        g._owner = self                  # keeps the FASTA handle alive; close() leaves it to the owner
+        torch.cuda.synchronize(g.device)
+        return g
+
     def _read_chroms(self):
         L = N.lib()
         n = L.fc2_fasta_n_chrom(self.fasta)
@@ -218,6 +236,9 @@ class Genome:
         return (self.units.cpu().numpy().view(np.uint64), self.nplane.cpu().numpy().view(np.uint64))
 
     def close(self):
+        if getattr(self, "_owner", None) is not None:      # a replica: the owner closes the FASTA
+            self.fasta = None
+            return
         if self.fasta is not None:
             N.lib().fc2_fasta_close(self.fasta)
             self.fasta = None

@@ -17,6 +17,7 @@ from __future__ import annotations
 import ctypes
 import sys
 import time
+from collections import deque
 from typing import Callable, Dict, Optional
 
 import numpy as np
@@ -46,32 +47,13 @@ def _check(rc: int):
         _raise_native(rc)
 
 
-def gpu_batch_evaluator(genome, hp) -> Callable:
-    """One fc2_bp_scan_launch per chunk, the batch packed in locus order; results in input order."""
-    from .hotpath import PairBatch, scan
-
-    def evaluate(reads, read_off, pairs):
-        n = len(pairs)
-        lens = pairs["read_len"].astype(np.int64)
-        b = PairBatch.pack(hp, genome, (reads, read_off, lens), pairs["a_pos"], pairs["b_aend"], pairs["chrom"],
-                           pairs["flags"], locus_order=True)
-        out = scan(hp, genome, b)
-        res = out.results[:n].cpu().numpy()
-        perm = b.fetch_perm()
-        if perm is not None:
-            r = np.empty_like(res)
-            r[perm] = res
-            res = r
-        tm = None
-        if hp.allhits:
-            t = out.tiemask[:b.tw * b.stride].cpu().numpy().view(np.uint64).reshape(b.tw, b.stride)[:, :n]
-            if perm is not None:
-                t2 = np.empty_like(t)
-                t2[:, perm] = t
-                t = t2
-            tm = np.ascontiguousarray(t)
-        return np.ascontiguousarray(res), tm
-    return evaluate
+def gpu_batch_evaluator(genome, hp, devices=None, n_threads: int = 0):
+    """The MI355X evaluator of the native read loop: a ScanPipeline (pinned staging, one side
+    stream per device, chunks dealt round-robin over ``devices``, results in input order).  It
+    has ``submit``/``result`` (NativeCaller.run reads ahead with them) and is callable as a plain
+    synchronous ``evaluate(reads, read_off, pairs)``."""
+    from .pipeline import ScanPipeline
+    return ScanPipeline(genome, hp, devices=devices, n_threads=n_threads)
 
 
 class NativeCaller:
@@ -149,33 +131,59 @@ class NativeCaller:
             if txt and outputs.get(key) is not None:
                 outputs[key].write(txt)
 
-    def run(self, evaluate: Callable, outputs: Dict, stderr=sys.stderr, throughput=False, chunksize=100000):
-        """Process the whole input; returns (seconds, n_reads, n_pairs, evaluate_seconds)."""
+    def run(self, evaluate, outputs: Dict, stderr=sys.stderr, throughput=False, chunksize=100000):
+        """Process the whole input; returns (seconds, n_reads, n_pairs, evaluate_seconds).
+
+        ``evaluate`` is either a plain ``evaluate(reads, read_off, pairs) -> (results, tiemask)``
+        or a pipelined evaluator with ``submit(reads_ptr, read_off, pairs) -> ticket``,
+        ``result(ticket)`` and ``depth`` (pipeline.ScanPipeline): then the loop reads up to
+        ``depth`` chunks ahead (fc2_caller_next queues them) so the search of chunk k runs on the
+        GPU while the host forms chunk k+1; results are still submitted in input order.  With
+        -B/--bam (records written while reading) it does not read ahead: the reference stops
+        writing at a failing fragment.  ``evaluate_seconds``: host time spent packing, queueing
+        and waiting for the search."""
         L = N.lib()
         t0 = time.time()
         t_last, last_reads = t0, 0
         eval_s = 0.
-        batch = N.CallerBatch()
-        eof = ctypes.c_int(0)
+        pipelined = hasattr(evaluate, "submit") and hasattr(evaluate, "result")
+        depth = max(1, int(getattr(evaluate, "depth", 1))) if pipelined and not self.bam_out else 1
+        queue = deque()                      # (ticket or (results, tiemask), n) in input order
+        eof = False
+        deferred = None                      # an error of fc2_caller_next, raised after the queued chunks
+        eof_c = ctypes.c_int(0)
         while True:
-            rc = L.fc2_caller_next(self.h, ctypes.byref(batch), ctypes.byref(eof))
-            if rc != N.FC2_OK:
-                _raise_native(rc)
-            n = int(batch.n)
+            while not eof and deferred is None and len(queue) < depth:
+                batch = N.CallerBatch()
+                rc = L.fc2_caller_next(self.h, ctypes.byref(batch), ctypes.byref(eof_c))
+                if rc != N.FC2_OK:
+                    try:
+                        _raise_native(rc)
+                    except Exception as ex:   # the reference reaches the queued fragments first
+                        deferred = ex
+                    break
+                eof = bool(eof_c.value)
+                n = int(batch.n)
+                te = time.perf_counter()
+                if not n:
+                    item = (None, None)
+                elif pipelined:
+                    pairs = np.ctypeslib.as_array(ctypes.cast(batch.pairs, ctypes.POINTER(ctypes.c_uint8)),
+                                                  (16 * n,)).view(N.PAIR_DTYPE)
+                    off = np.ctypeslib.as_array(ctypes.cast(batch.read_off, ctypes.POINTER(ctypes.c_uint64)), (n,))
+                    item = evaluate.submit(batch.reads, off, pairs)
+                else:
+                    item = evaluate(*self._host_batch(batch, n))
+                eval_s += time.perf_counter() - te
+                queue.append((item, n))
+            if not queue:
+                break
+            item, n = queue.popleft()
             res_ptr = tm_ptr = None
             tw = 0
             if n:
-                pairs = np.ctypeslib.as_array(ctypes.cast(batch.pairs, ctypes.POINTER(ctypes.c_uint8)),
-                                              (16 * n,)).view(N.PAIR_DTYPE).copy()
-                off = np.ctypeslib.as_array(ctypes.cast(batch.read_off, ctypes.POINTER(ctypes.c_uint64)),
-                                            (n,)).copy()
-                total = int((off + pairs["read_len"].astype(np.uint64)).max())
-                reads = np.zeros(total + 16, np.uint8)          # zero tail: the packer reads whole words
-                if total:
-                    reads[:total] = np.ctypeslib.as_array(
-                        ctypes.cast(batch.reads, ctypes.POINTER(ctypes.c_uint8)), (total,))
                 te = time.perf_counter()
-                res, tm = evaluate(reads, off, pairs)
+                res, tm = evaluate.result(item) if pipelined else item
                 eval_s += time.perf_counter() - te
                 res = np.ascontiguousarray(res, dtype=np.int64)
                 res_ptr = res.ctypes.data
@@ -197,13 +205,25 @@ class NativeCaller:
                                                                (nr.value - last_reads) / max(t1 - t_last, 1e-9)
                                                                / 1000.))
                     t_last, last_reads = t1, nr.value
-            if eof.value:
-                break
+        if deferred is not None:
+            raise deferred
         if throughput:
             stderr.write('\n')
         nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
         L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
         return time.time() - t0, int(nr.value), int(npairs.value), eval_s
+
+    @staticmethod
+    def _host_batch(batch, n):
+        """(reads, read_off, pairs) numpy copies of a handed-out chunk for a plain evaluator."""
+        pairs = np.ctypeslib.as_array(ctypes.cast(batch.pairs, ctypes.POINTER(ctypes.c_uint8)),
+                                      (16 * n,)).view(N.PAIR_DTYPE).copy()
+        off = np.ctypeslib.as_array(ctypes.cast(batch.read_off, ctypes.POINTER(ctypes.c_uint64)), (n,)).copy()
+        total = int((off + pairs["read_len"].astype(np.uint64)).max())
+        reads = np.zeros(total + 16, np.uint8)          # zero tail: the packer reads whole words
+        if total:
+            reads[:total] = np.ctypeslib.as_array(ctypes.cast(batch.reads, ctypes.POINTER(ctypes.c_uint8)), (total,))
+        return reads, off, pairs
 
     def counters(self) -> Dict[str, float]:
         L = N.lib()

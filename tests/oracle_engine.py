@@ -113,3 +113,51 @@ def oracle_batch_engine(options, hp):
 
 
 oracle_evaluator_factory.batch = oracle_batch_engine
+
+
+class DeferredEvaluator:
+    """The oracle batch engine behind the pipelined interface (submit / result / depth) of
+    find_circ2_amd.pipeline.ScanPipeline: submit only copies the chunk the native caller handed
+    out (so the caller reads ahead, fc2_caller_next queueing chunks), result evaluates it."""
+
+    def __init__(self, evaluate, depth):
+        self.evaluate = evaluate
+        self.depth = depth
+        self.max_in_flight = 0
+        self._in_flight = 0
+
+    def submit(self, reads_ptr, read_off, pairs):
+        import ctypes
+
+        import numpy as np
+        pairs = np.array(pairs, copy=True)
+        off = np.array(read_off, dtype=np.uint64, copy=True)
+        total = int((off + pairs["read_len"].astype(np.uint64)).max()) if len(pairs) else 0
+        reads = np.zeros(total + 16, np.uint8)
+        if total:
+            reads[:total] = np.ctypeslib.as_array(ctypes.cast(reads_ptr, ctypes.POINTER(ctypes.c_uint8)), (total,))
+        self._in_flight += 1
+        self.max_in_flight = max(self.max_in_flight, self._in_flight)
+        return (reads, off, pairs)
+
+    def result(self, ticket):
+        self._in_flight -= 1
+        return self.evaluate(*ticket)
+
+
+def pipelined_factory(depth):
+    """oracle_evaluator_factory whose native-caller batch hook reads `depth` chunks ahead."""
+    made = []
+
+    def factory(options, hp):
+        return oracle_evaluator_factory(options, hp)
+
+    def batch(options, hp):
+        evaluate, names, h, dummy = oracle_batch_engine(options, hp)
+        ev = DeferredEvaluator(evaluate, depth)
+        made.append(ev)
+        return ev, names, h, dummy
+
+    factory.batch = batch
+    factory.made = made
+    return factory
