@@ -275,6 +275,87 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
                        100.0 * kn / max(n, 1), 8 * b.nw, len(host), n)}
 
 
+def host_read_arrays(opt, b, chunk: int = 4_000_000):
+    """The batch as the read loop hands pairs out (fc2_caller_next): ASCII read_part bytes (anchors
+    'A', the internal part decoded from the packed rows, 'N' from the N rows) at read_off[i] =
+    i * max_len, and the 16-B records without the packer's flags.  Decoded on the device, untimed."""
+    import torch
+    from find_circ2_amd import _native as N
+    dev = b.device
+    n = b.n
+    e = opt.eff_a
+    hp = b.fetch_host_pairs().copy()
+    has_n = torch.from_numpy((hp["flags"] & N.PAIR_READ_N) != 0).to(dev)
+    hp["flags"] &= (N.PAIR_BACKSPLICE | N.PAIR_PRIMARY_REV | N.PAIR_SKIP)
+    hp["npos"] = 0
+    Lmax = int(hp["read_len"].max())
+    reads = np.empty(n * Lmax + 16, np.uint8)
+    code = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=dev)
+    W = b.read_words[:b.rw * b.stride].view(b.rw, b.stride)
+    NW = b.read_nwords[:b.nw * b.stride].view(b.nw, b.stride)
+    lens = torch.from_numpy(hp["read_len"].astype(np.int64)).to(dev)
+    shifts = torch.arange(64, device=dev, dtype=torch.int64)
+    for lo in range(0, n, chunk):
+        hi = min(n, lo + chunk)
+        m = hi - lo
+        bits = ((W[:, lo:hi].t().unsqueeze(2) >> shifts) & 1).reshape(m, -1).to(torch.uint8)    # [m, rw*64]
+        nbits = ((NW[:, lo:hi].t().unsqueeze(2) >> shifts) & 1).reshape(m, -1).to(torch.bool)
+        l = (lens[lo:hi] - 2 * e).clamp(min=0)
+        j = torch.arange(Lmax - 2 * e, device=dev).unsqueeze(0)
+        jj = j.clamp(max=bits.shape[1] - 1).expand(m, -1)
+        lob = torch.gather(bits, 1, jj)
+        hib = torch.gather(bits, 1, (l.unsqueeze(1) + j).clamp(max=bits.shape[1] - 1))
+        I = code[(lob | (hib << 1)).long()]
+        I[torch.gather(nbits, 1, j.clamp(max=nbits.shape[1] - 1).expand(m, -1)) & has_n[lo:hi].unsqueeze(1)] = ord("N")
+        out = torch.full((m, Lmax), ord("A"), dtype=torch.uint8, device=dev)
+        out[:, e:Lmax - e] = I
+        reads[lo * Lmax:hi * Lmax] = out.cpu().numpy().reshape(-1)
+    reads[n * Lmax:] = 0
+    off = np.arange(n, dtype=np.uint64) * np.uint64(Lmax)
+    return reads, off, hp
+
+
+def host_pipeline(opt, g, b, chunk: int = 2_000_000, reps: int = 3):
+    """The product transfer path (find_circ2_amd.pipeline.ScanPipeline, what the CLI's read loop
+    drives) from host pair arrays: per chunk the C++ packer writes records + read rows into
+    page-locked staging, then async H2D, scan and D2H of the 8-B results on the scanner's side
+    stream, two chunks in flight.  Timed from the host arrays to every raw result word in host
+    memory in input order (what fc2_caller_submit consumes); must equal the device-resident scan."""
+    from find_circ2_amd.pipeline import ScanPipeline
+    reads, off, hp = host_read_arrays(opt, b)
+    n = b.n
+    pipe = ScanPipeline(g, opt)
+    out = np.empty(n, np.int64)
+
+    def run_once():
+        pending = []
+        for lo in range(0, n, chunk):
+            hi = min(n, lo + chunk)
+            pending.append((lo, hi, pipe.submit(reads.ctypes.data, off[lo:hi], hp[lo:hi])))
+            while len(pending) >= pipe.depth:
+                a, z, t = pending.pop(0)
+                out[a:z] = pipe.result(t)[0]
+        for a, z, t in pending:
+            out[a:z] = pipe.result(t)[0]
+
+    run_once()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        run_once()
+        ts.append(time.perf_counter() - t0)
+    s = float(np.median(ts))
+    ok = bool(np.array_equal(out, b._bench_ref_results.numpy())) if hasattr(b, "_bench_ref_results") else None
+    import os as _os
+    return {"value": round(n / s, 1), "unit": "anchor-pairs/s", "ms_per_batch": round(s * 1e3, 1),
+            "results_equal_device_resident_scan": ok, "chunk_pairs": chunk,
+            "pack_threads": int(_os.environ.get("OMP_NUM_THREADS", "0") or 0) or "all cores (<= 64)",
+            "note": "host pair arrays (read_part bytes + 16-B records, as fc2_caller_next hands them out) -> "
+                    "C++ pack into pinned staging -> H2D -> scan -> D2H raw results, chunks of %d pairs, two per "
+                    "side stream in flight (find_circ2_amd.pipeline, the CLI's evaluator); median of %d passes "
+                    "over %d pairs" % (chunk, reps, n)}
+
+
 def timed_scans(opt, g, b, steps, warmup, ws, dev):
     """Warmup, then exactly `steps` scans bracketed by barrier + synchronize; per-launch HIP events."""
     import torch
@@ -710,6 +791,7 @@ def main():
                                       "cpu_model": cb["cpu_model"]}
     if rank == 0 and ws == 1 and not args.no_extra and args.workload == "hg19":
         line["extra"] = {"device_pipeline_pcie": device_pipeline(opt, g, b, reps=5)}
+        line["extra"]["host_pipeline_from_pair_arrays"] = host_pipeline(opt, g, b)
         line["extra"]["configs[2]_window_carrying_batch"] = window_carrying(opt, g, b, args.steps, dev, bpp)
         del b, out
         torch.cuda.empty_cache()

@@ -104,3 +104,45 @@ def test_gpu_native_caller_on_mutated_input(tmp_path, seed):
     rc2 = cli.main(["-G", fa, "-o", o2, "-q"] + extra + [sam])
     assert rc1 == rc2 == 0
     same(o1, o2)
+
+
+@pytest.mark.parametrize("extra", [[], ["--all-hits", "--non-canonical", "--chunk-size", "37"],
+                                   ["--chunk-size", "11", "-d", "0"]])
+def test_gpu_cli_two_gpus_equals_one(tmp_path, extra):
+    """--gpus 2 (chunks dealt round-robin to two scanners -- two devices, or two streams sharing
+    cuda:0 on a one-GPU box -- results merged in input order) writes the files --gpus 1 writes,
+    byte for byte, and both equal the Python loop with the CPU oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd import cli
+    from oracle_engine import oracle_evaluator_factory
+    from test_ingest import same
+    from test_native_caller import _rich_sam
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 2500, seed=1234)
+    outs = {}
+    for tag, more in (("g1", ["--gpus", "1"]), ("g2", ["--gpus", "2"]), ("g3", ["--gpus", "3"])):
+        o = str(tmp_path / tag)
+        assert cli.main(["-G", fa, "-o", o, "-n", "mix", "-q"] + extra + more + [sam]) == 0
+        outs[tag] = o
+    o = str(tmp_path / "oracle_py")
+    assert cli.main(["-G", fa, "-o", o, "-n", "mix", "-q", "--python-caller"] + extra + [sam],
+                    evaluator_factory=oracle_evaluator_factory) == 0
+    same(outs["g1"], outs["g2"])
+    same(outs["g1"], outs["g3"])
+    same(o, outs["g2"])
+
+
+def test_gpu_pipeline_readahead_many_chunks(tmp_path):
+    """ScanPipeline through the native loop with tiny chunks (hundreds of chunks, two in flight
+    per scanner, staging slots reused) on the golden reads: the same files as the oracle CLI."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    fa = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    rd = _sim_reads(fa, 1200, seed=5)
+    for extra in (["--chunk-size", "3"], ["--chunk-size", "5", "--gpus", "2", "--all-hits", "--non-canonical"]):
+        rc1, o1 = run_cli(tmp_path, fa, rd, extra=[e for e in extra if e not in ("--gpus", "2")], tag="oracle")
+        rc2, o2 = run_cli(tmp_path, fa, rd, extra=extra, evaluator=None, tag="gpu")
+        assert rc1 == rc2
+        if rc1 == 0:
+            _compare(o1, o2)
