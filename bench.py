@@ -334,9 +334,9 @@ def host_pipeline(opt, g, b, chunk: int = 2_000_000, reps: int = 3):
             pending.append((lo, hi, pipe.submit(reads.ctypes.data, off[lo:hi], hp[lo:hi])))
             while len(pending) >= pipe.depth:
                 a, z, t = pending.pop(0)
-                out[a:z] = pipe.result(t)[0]
+                out[a:z] = pipe.result(t, copy=False)[0]
         for a, z, t in pending:
-            out[a:z] = pipe.result(t)[0]
+            out[a:z] = pipe.result(t, copy=False)[0]
 
     run_once()
     ts = []

@@ -98,6 +98,14 @@ struct PackTable {
 static const PackTable kPackTable;
 static inline uint32_t pack_code(uint8_t c) { return kPackTable.t[c]; }
 
+// every byte of u (already upper-cased with & 0xDF) is one of 'A' 'C' 'G' 'T' (exact zero-byte tests)
+static inline bool acgt8(uint64_t u) {
+    auto zero = [](uint64_t y) { return ~(((y & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | y | 0x7F7F7F7F7F7F7F7Full); };
+    const uint64_t m = zero(u ^ 0x4141414141414141ull) | zero(u ^ 0x4343434343434343ull) |
+                       zero(u ^ 0x4747474747474747ull) | zero(u ^ 0x5454545454545454ull);
+    return m == 0x8080808080808080ull;
+}
+
 static inline bool py_isspace(uint8_t c) {
     return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f';
 }
@@ -617,96 +625,105 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
     std::atomic<uint64_t> nbp{0};
     std::atomic<int64_t> bad_chrom{-1}, bad_rows{-1}, bad_dist{-1}, bad_len{-1};
     const int nch = f ? (int)f->chroms.size() : 0;
+    const int maxdist = p->maxdist;
     parallel_for(n, T, [&](uint64_t b, uint64_t en) {
         uint64_t local_bp = 0;
+        constexpr int kW = (kMaxFastL + 63) / 64;
         for (uint64_t i = b; i < en; ++i) {
             fc2_pair &pr = pairs[i];
-            pr.flags &= (uint8_t)(FC2_PAIR_BACKSPLICE | FC2_PAIR_PRIMARY_REV | FC2_PAIR_SKIP);
-            pr.npos = 0;
-            for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = 0;
-            for (uint32_t j = 0; j < nw; ++j) read_nwords[(uint64_t)j * stride + i] = 0;
-            if (pr.flags & FC2_PAIR_SKIP) continue;
-            if (pr.read_len > FC2_MAX_READ_LEN) { int64_t x = -1; bad_len.compare_exchange_strong(x, (int64_t)i); continue; }
-            if (f && (int)pr.chrom >= nch) { int64_t x = -1; bad_chrom.compare_exchange_strong(x, (int64_t)i); continue; }
+            uint8_t flags = (uint8_t)(pr.flags & (FC2_PAIR_BACKSPLICE | FC2_PAIR_PRIMARY_REV | FC2_PAIR_SKIP));
+            uint8_t npos = 0;
+            // the pair's row words, built in registers and stored once at the end (zero unless packed)
+            uint64_t row[2 * kW + 1] = {0}, nrow[kW] = {0};
             const int L = pr.read_len;
             const int l = L - 2 * e;
-            if (l < 0) continue;  // range(l+1) is empty: no hit, no window use
-            if (p->maxdist > 255 && l > 255) { int64_t x = -1; bad_dist.compare_exchange_strong(x, (int64_t)i); }
-            const uint8_t *I = reads + read_off[i] + e;
-            bool bytepath = l > kMaxFastL, anyN = false;
-            int n_count = 0, n_first = 0;
-            if (!bytepath) {
+            bool bytepath = false;
+            do {
+                if (flags & FC2_PAIR_SKIP) break;
+                if (L > FC2_MAX_READ_LEN) { int64_t x = -1; bad_len.compare_exchange_strong(x, (int64_t)i); break; }
+                if (f && (int)pr.chrom >= nch) { int64_t x = -1; bad_chrom.compare_exchange_strong(x, (int64_t)i); break; }
+                if (l < 0) break;  // range(l+1) is empty: no hit, no window use
+                if (maxdist > 255 && l > 255) { int64_t x = -1; bad_dist.compare_exchange_strong(x, (int64_t)i); }
+                if (l > kMaxFastL) { bytepath = true; break; }
                 if ((uint64_t)2 * l > (uint64_t)rw * 64 || (uint64_t)l > (uint64_t)nw * 64) {
-                    int64_t x = -1; bad_rows.compare_exchange_strong(x, (int64_t)i); continue;
+                    int64_t x = -1; bad_rows.compare_exchange_strong(x, (int64_t)i); break;
                 }
-                // tight bit-sliced row: low bits at [0, l), high bits at [l, 2l); the row words are
-                // built in registers 64 bases at a time and stored once (no strided read-modify-write)
-                uint64_t lo_w[(kMaxFastL + 63) / 64] = {0}, hi_w[(kMaxFastL + 63) / 64] = {0},
-                         n_w[(kMaxFastL + 63) / 64] = {0};
-                uint32_t any_exotic = 0;
-                for (int j0 = 0; j0 < l; j0 += 64) {
-                    const int m = std::min(64, l - j0);
-                    uint64_t lo = 0, hi = 0, nn = 0;
-                    for (int j = 0; j < m; ++j) {
-                        const uint32_t pc = pack_code(I[j0 + j]);
-                        lo |= (uint64_t)(pc & 1u) << j;
-                        hi |= (uint64_t)((pc >> 1) & 1u) << j;
-                        nn |= (uint64_t)((pc >> 2) & 1u) << j;
-                        any_exotic |= pc;
+                const uint8_t *I = reads + read_off[i] + e;
+                // tight bit-sliced row: low code bits at [0, l), high bits at [l, 2l), 'N' = code 00 +
+                // an N bit.  Fast path: 8 bases per step (SWAR) while every byte is one of ACGTacgt
+                // (code = ((c >> 2) ^ (c >> 1)) & 3: A0 C1 G2 T3 either case); anything else (N, IUPAC,
+                // other bytes) takes the per-byte table for the rest of the read.
+                uint64_t lo_w[kW] = {0}, hi_w[kW] = {0}, n_w[kW] = {0};
+                uint32_t any = 0;
+                int j = 0;
+                for (; j + 8 <= l; j += 8) {
+                    uint64_t x;
+                    memcpy(&x, I + j, 8);
+                    const uint64_t u = x & 0xDFDFDFDFDFDFDFDFull;            // upper case
+                    if (!acgt8(u)) break;
+                    const uint64_t v = ((x >> 2) ^ (x >> 1)) & 0x0303030303030303ull;
+                    const uint64_t lo8 = ((v & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56;
+                    const uint64_t hi8 = (((v >> 1) & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56;
+                    lo_w[j >> 6] |= lo8 << (j & 63);
+                    hi_w[j >> 6] |= hi8 << (j & 63);
+                }
+                for (; j < l; ++j) {
+                    const uint32_t pc = pack_code(I[j]);
+                    const uint64_t bit = 1ull << (j & 63);
+                    if (pc & 4u) n_w[j >> 6] |= bit;                        // 'N' (or exotic)
+                    else {
+                        if (pc & 1u) lo_w[j >> 6] |= bit;
+                        if (pc & 2u) hi_w[j >> 6] |= bit;
                     }
-                    lo_w[j0 >> 6] = lo & ~nn;              // 'N' is code 00 plus its N bit
-                    hi_w[j0 >> 6] = hi & ~nn;
-                    n_w[j0 >> 6] = nn;
+                    any |= pc;
                 }
-                if (any_exotic & 8u) {
-                    bytepath = true;
-                } else {
-                    // low plane at bit offset 0, high plane at bit offset l, both into the row words
-                    const int nlw = (l + 63) / 64;
-                    uint64_t row[2 * ((kMaxFastL + 63) / 64) + 1] = {0};
-                    for (int k = 0; k < nlw; ++k) row[k] = lo_w[k];
-                    // clear bits >= l of the low plane's last word is implicit (they were never set)
-                    const int sh = l & 63, wo = l >> 6;
+                if (any & 8u) { bytepath = true; break; }
+                const int nlw = (l + 63) / 64;
+                for (int k = 0; k < nlw; ++k) row[k] = lo_w[k];
+                const int sh = l & 63, wo = l >> 6;
+                for (int k = 0; k < nlw; ++k) {
+                    row[wo + k] |= sh ? (hi_w[k] << sh) : hi_w[k];
+                    if (sh) row[wo + k + 1] |= hi_w[k] >> (64 - sh);
+                }
+                if (any & 4u) {
+                    int n_count = 0, n_first = 0;
                     for (int k = 0; k < nlw; ++k) {
-                        row[wo + k] |= sh ? (hi_w[k] << sh) : hi_w[k];
-                        if (sh) row[wo + k + 1] |= hi_w[k] >> (64 - sh);
-                    }
-                    for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = row[j];
-                    for (int k = 0; k < nlw && any_exotic & 4u; ++k) {
-                        read_nwords[(uint64_t)k * stride + i] = n_w[k];
+                        nrow[k] = n_w[k];
                         if (n_w[k]) {
-                            anyN = true;
-                            const int c = __builtin_popcountll(n_w[k]);
                             if (n_count == 0) n_first = k * 64 + __builtin_ctzll(n_w[k]);
-                            n_count += c;
+                            n_count += __builtin_popcountll(n_w[k]);
                         }
                     }
+                    flags |= FC2_PAIR_READ_N;
+                    if (n_count == 1 && n_first < 256) {      // the scan takes it from the record
+                        flags |= FC2_PAIR_READ_N1;
+                        npos = (uint8_t)n_first;
+                    }
                 }
-            }
-            if (!bytepath && f) {
-                const fc2_chrom_rec &c = f->chroms[pr.chrom];
-                const int64_t W = l + 2;
-                const int64_t wsA = (int64_t)pr.a_pos + e, wsB = (int64_t)pr.b_aend - e - W;
-                if (c.regular != 1) bytepath = true;
-                else if (wsA > c.size || wsA + W < 0 || wsB > c.size || wsB + W < 0) bytepath = true;
-                else {
-                    auto clampg = [&](int64_t s) { return (uint64_t)std::min<int64_t>(std::max<int64_t>(s, 0), c.size) + c.gstart; };
-                    if (touches_exotic(f, clampg(wsA), clampg(wsA + W)) || touches_exotic(f, clampg(wsB), clampg(wsB + W)))
-                        bytepath = true;
+                if (f) {
+                    const fc2_chrom_rec &c = f->chroms[pr.chrom];
+                    const int64_t W = l + 2;
+                    const int64_t wsA = (int64_t)pr.a_pos + e, wsB = (int64_t)pr.b_aend - e - W;
+                    if (c.regular != 1) bytepath = true;
+                    else if (wsA > c.size || wsA + W < 0 || wsB > c.size || wsB + W < 0) bytepath = true;
+                    else {
+                        auto clampg = [&](int64_t s) { return (uint64_t)std::min<int64_t>(std::max<int64_t>(s, 0), c.size) + c.gstart; };
+                        if (touches_exotic(f, clampg(wsA), clampg(wsA + W)) || touches_exotic(f, clampg(wsB), clampg(wsB + W)))
+                            bytepath = true;
+                    }
                 }
-            }
+            } while (false);
             if (bytepath) {
-                pr.flags |= FC2_PAIR_BYTEPATH;
-                for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = 0;
-                for (uint32_t j = 0; j < nw; ++j) read_nwords[(uint64_t)j * stride + i] = 0;
+                flags = (uint8_t)((flags & ~(FC2_PAIR_READ_N | FC2_PAIR_READ_N1)) | FC2_PAIR_BYTEPATH);
+                npos = 0;
+                for (auto &w : row) w = 0;
+                for (auto &w : nrow) w = 0;
                 ++local_bp;
-            } else if (anyN) {
-                pr.flags |= FC2_PAIR_READ_N;
-                if (n_count == 1 && n_first < 256) {      // the scan takes it from the record
-                    pr.flags |= FC2_PAIR_READ_N1;
-                    pr.npos = (uint8_t)n_first;
-                }
             }
+            pr.flags = flags;
+            pr.npos = npos;
+            for (uint32_t j = 0; j < rw; ++j) read_words[(uint64_t)j * stride + i] = j < 2 * kW + 1 ? row[j] : 0;
+            for (uint32_t j = 0; j < nw; ++j) read_nwords[(uint64_t)j * stride + i] = j < kW ? nrow[j] : 0;
         }
         nbp += local_bp;
     });

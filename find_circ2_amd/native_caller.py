@@ -183,7 +183,7 @@ class NativeCaller:
             tw = 0
             if n:
                 te = time.perf_counter()
-                res, tm = evaluate.result(item) if pipelined else item
+                res, tm = evaluate.result(item, copy=False) if pipelined else item   # consumed by submit below
                 eval_s += time.perf_counter() - te
                 res = np.ascontiguousarray(res, dtype=np.int64)
                 res_ptr = res.ctypes.data

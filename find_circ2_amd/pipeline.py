@@ -120,7 +120,8 @@ class DeviceScanner:
         rw, nw, tw = rw.value, nw.value, tw.value
         slot.ensure(torch, self.dev, n, rw, nw, tw, opt.allhits)
         hp = slot.np_pairs[:n]
-        hp[:] = pairs
+        # 16-B records into page-locked staging (torch's CPU copy runs on its thread pool)
+        slot.h_pairs[:16 * n].copy_(torch.from_numpy(np.ascontiguousarray(pairs).view(np.uint8).reshape(-1)))
         off = np.ascontiguousarray(read_off, np.uint64)
         nbp = ctypes.c_uint64()
         g = self.genome
@@ -196,18 +197,28 @@ class DeviceScanner:
         slot.busy = False
         slot.keep = None
 
-    def _copy_out(self, t: Ticket):
+    def _copy_out(self, t: Ticket, copy: bool = True):
         slot = self.slots[t.slot]
-        t.res = slot.np_res[:t.n].copy()
-        if self.options.allhits:
-            t.tm = slot.np_tm[:t.tw * t.n].reshape(t.tw, t.n).view(np.uint64).copy()
+        res = slot.np_res[:t.n]
+        tm = slot.np_tm[:t.tw * t.n].reshape(t.tw, t.n).view(np.uint64) if self.options.allhits else None
+        if copy:
+            res = res.copy()
+            tm = tm.copy() if tm is not None else None
+        t.res, t.tm = res, tm
 
-    def result(self, t: Ticket):
-        """(results int64 [n] = raw fc2_result words, tie mask uint64 [tw, n] or None) of a chunk."""
+    def result(self, t: Ticket, copy: bool = True):
+        """(results int64 [n] = raw fc2_result words, tie mask uint64 [tw, n] or None) of a chunk.
+        ``copy=False`` returns views of the page-locked result buffers: valid until the next
+        ``submit`` to this scanner (the native read loop hands them straight to fc2_caller_submit)."""
         if t.res is None:
             if self._gen[t.slot] != t.gen:
                 raise RuntimeError("ticket's slot was reused before its results were taken")
-            self._drain(t.slot)
+            slot = self.slots[t.slot]
+            slot.event.synchronize()
+            self._pending.pop(t.slot, None)
+            self._copy_out(t, copy)
+            slot.busy = False
+            slot.keep = None
         return t.res, t.tm
 
 
@@ -236,8 +247,8 @@ class ScanPipeline:
         self.k += 1
         return sc.submit(reads_ptr, read_off, pairs)
 
-    def result(self, t: Ticket):
-        return t.scanner.result(t)
+    def result(self, t: Ticket, copy: bool = True):
+        return t.scanner.result(t, copy)
 
     def __call__(self, reads, read_off, pairs):
         """Synchronous form (evaluate(reads, read_off, pairs) of native_caller)."""

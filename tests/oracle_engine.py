@@ -140,7 +140,7 @@ class DeferredEvaluator:
         self.max_in_flight = max(self.max_in_flight, self._in_flight)
         return (reads, off, pairs)
 
-    def result(self, ticket):
+    def result(self, ticket, copy=True):
         self._in_flight -= 1
         return self.evaluate(*ticket)
 
