@@ -127,8 +127,8 @@ def main():
     t_gen = time.time() - t0
     res = {"reads": a.reads, "bases": int(sum(sizes)), "gen_s": round(t_gen, 1)}
     outs = {}
-    for tag, extra in (("native", []), ("python_caller", ["--python-caller"]), ("native_allhits",
-                                                                              ["--all-hits", "--non-canonical"]),
+    for tag, extra in (("native", []), ("native_gpus2", ["--gpus", "2"]), ("python_caller", ["--python-caller"]),
+                       ("native_allhits", ["--all-hits", "--non-canonical"]),
                        ("python_caller_allhits", ["--python-caller", "--all-hits", "--non-canonical"])):
         out = os.path.join(a.out, tag)
         t0 = time.time()
@@ -141,7 +141,7 @@ def main():
         outs[tag] = out
         print("done", tag, res[tag + "_s"], file=sys.stderr, flush=True)
     same = True
-    for x, y in (("native", "python_caller"), ("native_allhits", "python_caller_allhits")):
+    for x, y in (("native", "python_caller"), ("native", "native_gpus2"), ("native_allhits", "python_caller_allhits")):
         for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
             if open(os.path.join(outs[x], f)).read() != open(os.path.join(outs[y], f)).read():
                 same = False
