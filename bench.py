@@ -315,7 +315,7 @@ def host_read_arrays(opt, b, chunk: int = 4_000_000):
     return reads, off, hp
 
 
-def host_pipeline(opt, g, b, chunk: int = 2_000_000, reps: int = 3):
+def host_pipeline(opt, g, b, chunk: int = 4_000_000, reps: int = 3):
     """The product transfer path (find_circ2_amd.pipeline.ScanPipeline, what the CLI's read loop
     drives) from host pair arrays: per chunk the C++ packer writes records + read rows into
     page-locked staging, then async H2D, scan and D2H of the 8-B results on the scanner's side

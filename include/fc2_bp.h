@@ -178,6 +178,15 @@ typedef struct fc2_batch_view {
 } fc2_batch_view;
 #define FC2_BATCH_LOCUS_ORDERED 0x1u  /* pairs are sorted by genome locus (fc2_reorder_launch output or a
                                          host-sorted batch): the scan deals each XCD a contiguous range */
+/* Per-call form hints (results never depend on them; by default fc2_bp_scan_launch picks the form from
+ * the batch and the genome -- LDS-staged for a read-order batch over a genome >= 64 MiB of code planes,
+ * plain otherwise; word-pair windows when the view carries wt and l + 2 <= 128; three-lane loads for
+ * windows > 97 bases).  They let a caller (the test suite) run every form on any data: */
+#define FC2_BATCH_FORM_STAGED  0x02u  /* the LDS-staged form (chromosome table + N super map in LDS)   */
+#define FC2_BATCH_FORM_PLAIN   0x04u  /* the plain form (tables from L2, one lane per window)           */
+#define FC2_BATCH_FORM_UNITS   0x08u  /* windows from the 64-base unit planes even if wt is present      */
+#define FC2_BATCH_FORM_TWOLANE 0x10u  /* staged word-pair form: two-lane window loads at any length     */
+#define FC2_BATCH_FORM_TRI     0x20u  /* staged word-pair form: three-lane window loads at any length   */
 
 /* ---- pairs that need byte-exact evaluation ------------------------------ */
 /* Block for pair k at arena[off[k]]: int32 lenI, lenA, lenB, then
@@ -220,7 +229,13 @@ int         fc2_gather_windows_launch(const fc2_params *p, const fc2_genome_view
 int         fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
                                      uint64_t *out, void *stream);
 
-/* Performance knobs (results never depend on them); used for A/B measurements. */
+/* Performance knobs (results never depend on them) for A/B measurements, process-global.  They exist
+ * only in A/B builds of the library (-DFC2_AB_FORMS=1: `make -C find_circ2_amd/csrc ab` ->
+ * libfc2_ab.so), together with the measured-and-rejected kernel forms they select (64-bit words,
+ * persistent grid, 256/1024-pair staged blocks, cached streaming, extra LDS, forced swizzle/twin).
+ * The shipped libfc2.so keeps no mutable tuning state: fc2_set_tuning fails with FC2_E_PARAM there and
+ * fc2_get_tuning reports the fixed defaults; per-call form choices go through the FC2_BATCH_FORM_*
+ * hints of fc2_batch_view.layout. */
 #define FC2_TUNE_STREAM_NT 1   /* 1 (default): per-pair inputs/results use non-temporal loads/stores */
 #define FC2_TUNE_KERNEL32  2   /* 1 (default): 32-bit-word scan kernel; 0: 64-bit-word scan kernel */
 #define FC2_TUNE_XCD_SWIZZLE 3 /* each XCD scans a contiguous range of the batch: 0 never, 1 always,
