@@ -80,6 +80,12 @@ class BatchView(ctypes.Structure):
 
 
 BATCH_LOCUS_ORDERED = 0x1
+# per-call form hints (fc2_batch_view.layout, include/fc2_bp.h); results never depend on them
+BATCH_FORM_STAGED = 0x02
+BATCH_FORM_PLAIN = 0x04
+BATCH_FORM_UNITS = 0x08
+BATCH_FORM_TWOLANE = 0x10
+BATCH_FORM_TRI = 0x20
 
 
 class ReorderInfo(ctypes.Structure):

@@ -5,6 +5,12 @@
 
 #include "../../include/fc2_bp.h"
 
+// 1 only in A/B builds (libfc2_ab.so, `make ab`): fc2_set_tuning and the measured-and-rejected kernel
+// forms it selects (64-bit words, persistent grid, 256/1024-pair staged blocks, cached streaming).
+#ifndef FC2_AB_FORMS
+#define FC2_AB_FORMS 0
+#endif
+
 namespace fc2 {
 
 // Thread-local message behind fc2_last_error().

@@ -35,12 +35,12 @@ __device__ __forceinline__ uint64_t lowbits(int n) {  // n in any range; bits [0
 }
 
 // bits [s, s+64) of the 128-bit value hi:lo, s in [0, 63]
-__device__ __forceinline__ uint64_t fsh(uint64_t lo, uint64_t hi, unsigned s) {
+[[maybe_unused]] __device__ __forceinline__ uint64_t fsh(uint64_t lo, uint64_t hi, unsigned s) {
     return s ? ((lo >> s) | (hi << (64u - s))) : lo;
 }
 
 // positions [a, b) restricted to word k (positions 64k .. 64k+63)
-__device__ __forceinline__ uint64_t rmask(int a, int b, int k) {
+[[maybe_unused]] __device__ __forceinline__ uint64_t rmask(int a, int b, int k) {
     const int lo = a - 64 * k, hi = b - 64 * k;
     if (hi <= 0 || lo >= 64 || hi <= lo) return 0ull;
     return lowbits(hi) & ~lowbits(lo);
@@ -783,8 +783,10 @@ __global__ void nsuper_kernel(const uint32_t *__restrict__ ncoarse, uint64_t n_u
 
 inline unsigned grid_for(uint64_t n, unsigned block) { return (unsigned)((n + block - 1) / block); }
 
-// Tuning knobs (fc2_set_tuning): non-temporal streaming of the per-pair
-// inputs/outputs, default on.
+// Tuning knobs (fc2_set_tuning) exist only in A/B builds (-DFC2_AB_FORMS=1, libfc2_ab.so), with the
+// measured-and-rejected forms they select; the shipped library has the defaults as constants, so it
+// keeps no mutable process-global state and instantiates only the forms the defaults pick.
+#if FC2_AB_FORMS
 int g_stream_nt = 1;
 int g_kernel32 = 1;   // 1: bp_scan32_kernel (32-bit plane words), 0: bp_scan_kernel (64-bit)
 int g_xcd_swizzle = 2; // XCD-contiguous block order in bp_scan32_kernel: 0 never, 1 always, 2 for locus-ordered batches
@@ -795,6 +797,10 @@ int g_words = 1;       // read-order STAGE scan uses the word-pair layout when t
 int g_persist = 0;      // persistent STAGE kernel: 0 off, -1 occupancy-sized grid, k > 0 k blocks per CU
 int g_stage_block = 512; // threads per block of the LDS-staging word-pair scan (FC2_TUNE_STAGE_BLOCK)
 int g_tri = 2;           // three-lane window loads: 0 never, 1 always, 2 when windows exceed 97 bases (FC2_TUNE_TRI)
+#else
+constexpr int g_stream_nt = 1, g_kernel32 = 1, g_xcd_swizzle = 2, g_extra_lds = 0, g_stage = 2, g_twin = 2,
+              g_words = 1, g_persist = 0, g_stage_block = 512, g_tri = 2;
+#endif
 inline bool stream_nt() { return g_stream_nt != 0; }
 
 }  // namespace
@@ -842,27 +848,34 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         // locus-ordered batches re-read their lines from L2: the twin only doubles the footprint there
         const bool ordered = (b->layout & FC2_BATCH_LOCUS_ORDERED) != 0;
         if (g_twin == 0 || (g_twin == 2 && ordered)) gv.units_twin = nullptr;
-        if (!g_words || !gv.wt || gv.wt_bytes == 0 || ml + 2 > 128) gv.wt = nullptr;
+        const bool words = g_words && !(b->layout & FC2_BATCH_FORM_UNITS);
+        if (!words || !gv.wt || gv.wt_bytes == 0 || ml + 2 > 128) gv.wt = nullptr;
         // LDS staging pays where every L2 request counts: read-order batch over a genome far larger
-        // than the caches (profiles/r01/ab_stage.jsonl)
+        // than the caches (profiles/r01/ab_stage.jsonl); the per-call hints force a form
         const bool big = !g->dummy && g->n_units * 16 >= (64ull << 20);
-        const bool stage = g_stage == 2 ? (big && !ordered) : g_stage != 0;
+        const bool stage = (b->layout & FC2_BATCH_FORM_STAGED) ? true
+                         : (b->layout & FC2_BATCH_FORM_PLAIN) ? false
+                         : g_stage == 2 ? (big && !ordered) : g_stage != 0;
+        const bool tri = (b->layout & FC2_BATCH_FORM_TRI) ? true
+                       : (b->layout & FC2_BATCH_FORM_TWOLANE) ? false
+                       : g_tri == 1 || (g_tri == 2 && ml + 2 > 97);   // 5-pair windows: three-lane loads
         const int opts = sw ? fc2::kOptSwizzle : 0;
         const int nq = (ml + 2 + 31) / 32;
-        if (stage && (g_stage_block != 256 || g_tri == 1 || (g_tri == 2 && ml + 2 > 97)) && g_persist == 0 &&
-            fc2::stage_bt_ok(nq, gv)) {
-            const bool tri = g_tri == 1 || (g_tri == 2 && ml + 2 > 97);   // 5-pair windows: three-lane loads
+        if (stage && (g_stage_block != 256 || tri) && g_persist == 0 && fc2::stage_bt_ok(nq, gv)) {
             fc2::launch_scan32_stage_bt(g_stage_block, tri, nt, s, *p, gv, *b, out, tiemask, tw);
             return hip_check(hipGetLastError(), "bp_scan32_stage_bt_kernel launch");
         }
+#if FC2_AB_FORMS
         if (stage && g_persist != 0 && fc2::persist_ok(nq, gv)) {
             fc2::launch_scan32_persist(nt, s, *p, gv, *b, out, tiemask, tw, g_persist < 0 ? 0 : g_persist);
             return hip_check(hipGetLastError(), "bp_scan32_persist_kernel launch");
         }
+#endif
         fc2::launch_scan32((ml + 2 + 31) / 32, nt, opts, stage, grid, s, *p, gv, *b, out, tiemask, tw,
                            (unsigned)g_extra_lds);
         return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
     }
+#if FC2_AB_FORMS
 #define FC2_LAUNCH(NWV, NTV) \
     hipLaunchKernelGGL((bp_scan_kernel<NWV, NTV>), dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw)
     if (nwords <= 2) { if (nt) FC2_LAUNCH(2, true); else FC2_LAUNCH(2, false); }
@@ -870,6 +883,11 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     else { if (nt) FC2_LAUNCH(8, true); else FC2_LAUNCH(8, false); }
 #undef FC2_LAUNCH
     return hip_check(hipGetLastError(), "bp_scan_kernel launch");
+#else
+    (void)grid;
+    (void)nwords;
+    return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: unreachable form");
+#endif
 }
 
 extern "C" int fc2_gather_windows_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
@@ -894,7 +912,9 @@ extern "C" int fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_vi
         return fc2::fail(FC2_E_PARAM, "fc2_probe_pattern_launch: needs a genome with a word-pair table and a batch");
     if (b->n == 0) return FC2_OK;
     const int ml = b->max_l < 0 ? 0 : b->max_l;
-    const bool tri = g_tri == 1 || (g_tri == 2 && ml + 2 > 97);     // the scan's window form (fc2_bp_scan_launch)
+    const bool tri = (b->layout & FC2_BATCH_FORM_TRI) ? true                // the scan's window form
+                   : (b->layout & FC2_BATCH_FORM_TWOLANE) ? false           // (fc2_bp_scan_launch)
+                   : g_tri == 1 || (g_tri == 2 && ml + 2 > 97);
     if (fc2::launch_probe_pattern((hipStream_t)stream, *p, *g, *b, out, tri))
         return fc2::fail(FC2_E_HIP, "probe_pattern_kernel launch failed");
     return FC2_OK;
@@ -1005,6 +1025,7 @@ extern "C" int fc2_synth_pairs_launch(const fc2_params *p, const fc2_synth_cfg *
 }
 
 extern "C" int fc2_set_tuning(int key, int value) {
+#if FC2_AB_FORMS
     switch (key) {
         case FC2_TUNE_STREAM_NT: g_stream_nt = value ? 1 : 0; return FC2_OK;
         case FC2_TUNE_KERNEL32: g_kernel32 = value ? 1 : 0; return FC2_OK;
@@ -1041,6 +1062,12 @@ extern "C" int fc2_set_tuning(int key, int value) {
             g_xcd_swizzle = value; return FC2_OK;
         default: return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: unknown key");
     }
+#else
+    (void)key;
+    (void)value;
+    return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: tuning knobs exist only in A/B builds of the library "
+                                  "(FC2_AB_FORMS=1, make -C find_circ2_amd/csrc ab); use the FC2_BATCH_FORM_* hints");
+#endif
 }
 
 extern "C" int fc2_get_tuning(int key, int *value) {

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #include "../../include/fc2_bp.h"
+#include "fc2_common.h"
 
 namespace fc2 {
 // nq: 32-bit words per plane needed by the batch (rounded up to 4/8/16 inside); grid: one
@@ -13,11 +14,14 @@ constexpr int kOptSwizzle = 1;     // XCD-contiguous block order
 void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
                    const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
                    unsigned extra_lds = 0);   // occupancy experiments only (FC2_TUNE_EXTRA_LDS)
+#if FC2_AB_FORMS
 // Persistent STAGE + cooperative form (grid = CUs x resident blocks); usable when persist_ok().
+// Measured and rejected (profiles/r01/ab_persist*.jsonl): A/B builds only.
 bool persist_ok(int nq, const fc2_genome_view &g);
 void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                            const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
                            int blocks_per_cu);   // 0: the occupancy limit
+#endif
 // STAGE + cooperative word-pair form with bt-thread blocks (256/512/1024); usable when stage_bt_ok().
 bool stage_bt_ok(int nq, const fc2_genome_view &g);
 // tri: three-lane window loads (batches with windows longer than 97 bases)

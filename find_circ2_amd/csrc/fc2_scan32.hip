@@ -1274,6 +1274,7 @@ __global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc
                                          s_xchg[threadIdx.x >> 6]);
 }
 
+#if FC2_AB_FORMS
 // Persistent form of the STAGE + cooperative kernel (read-order batch over a large genome, l + 2
 // <= 128): the grid is sized to the resident capacity of the chip, each block stages the LDS
 // tables ONCE and then walks the batch's 256-pair tiles t = blockIdx.x + k * gridDim.x.  At
@@ -1317,6 +1318,8 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_persist_kernel(fc2_params p,
                                            true, s_nsuper_buf, s_xchg[threadIdx.x >> 6]);
     }
 }
+
+#endif
 
 // Speed-of-light probe of the read-order scan (measurement only, fc2_probe_pattern_launch): the
 // kernel's exact memory pattern on the same batch and genome -- NT-streamed 16-B records and read
@@ -1396,6 +1399,7 @@ int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_vi
 void launch_scan32_win(int pw, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                        const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
     const unsigned grid = (unsigned)((b.n + kBlock - 1) / kBlock);
+#if FC2_AB_FORMS
 #define FC2_LW(PWV)                                                                                          \
     do {                                                                                                     \
         if (nt) hipLaunchKernelGGL((bp_scan32_win_kernel<PWV, true>), dim3(grid), dim3(kBlock), 0, s, p, g, b,  \
@@ -1403,6 +1407,11 @@ void launch_scan32_win(int pw, bool nt, hipStream_t s, const fc2_params &p, cons
         else hipLaunchKernelGGL((bp_scan32_win_kernel<PWV, false>), dim3(grid), dim3(kBlock), 0, s, p, g, b,    \
                                 out, tiemask, tw);                                                           \
     } while (0)
+#else
+    (void)nt;
+#define FC2_LW(PWV) hipLaunchKernelGGL((bp_scan32_win_kernel<PWV, true>), dim3(grid), dim3(kBlock), 0, s, p, g, b, \
+                                       out, tiemask, tw)
+#endif
     switch (pw) {
         case 1: FC2_LW(1); break;
         case 2: FC2_LW(2); break;
@@ -1434,6 +1443,7 @@ bool stage_bt_ok(int nq, const fc2_genome_view &g) {
 
 void launch_scan32_stage_bt(int bt, bool tri, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                             const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
+#if FC2_AB_FORMS
 #define FC2_LBT(BTV, TRV)                                                                                     \
     do {                                                                                                      \
         const dim3 grid((unsigned)((b.n + BTV - 1) / BTV));                                                   \
@@ -1452,8 +1462,18 @@ void launch_scan32_stage_bt(int bt, bool tri, bool nt, hipStream_t s, const fc2_
         else FC2_LBT(256, false);
     }
 #undef FC2_LBT
+#else
+    (void)bt;
+    (void)nt;
+    const dim3 grid((unsigned)((b.n + 511) / 512));      // 512-pair blocks, non-temporal streaming
+    if (tri) hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<512, true, true>), grid, dim3(512), 0, s, p, g, b, out,
+                                tiemask, tw);
+    else hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<512, true, false>), grid, dim3(512), 0, s, p, g, b, out,
+                            tiemask, tw);
+#endif
 }
 
+#if FC2_AB_FORMS
 bool persist_ok(int nq, const fc2_genome_view &g) {
     return nq <= 4 && !g.dummy && g.n_chrom <= (uint32_t)kChromLds && g.nsuper &&
            g.nsuper_words <= (uint32_t)kSuperLds;
@@ -1487,6 +1507,8 @@ void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc
                            tiemask, tw, n_tiles);
 }
 
+#endif
+
 void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
                    const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
                    unsigned extra_lds) {
@@ -1494,9 +1516,16 @@ void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStre
     hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV, STV>), dim3(grid), dim3(kBlock), extra_lds, s, p, g, b, out, tiemask, \
                        tw, opts)
 #define FC2_L32S(NQV, NTV) do { if (stage) FC2_L32(NQV, NTV, true); else FC2_L32(NQV, NTV, false); } while (0)
+#if FC2_AB_FORMS
     if (nq <= 4) { if (nt) FC2_L32S(4, true); else FC2_L32S(4, false); }
     else if (nq <= 8) { if (nt) FC2_L32S(8, true); else FC2_L32S(8, false); }
     else { if (nt) FC2_L32S(16, true); else FC2_L32S(16, false); }
+#else
+    (void)nt;
+    if (nq <= 4) FC2_L32S(4, true);
+    else if (nq <= 8) FC2_L32S(8, true);
+    else FC2_L32S(16, true);
+#endif
 #undef FC2_L32S
 #undef FC2_L32
 }

@@ -7,7 +7,13 @@ ROOT=$(cd "$(dirname "$0")/.." && pwd)
 WT=/tmp/fc2_wt_$NAME
 rm -rf $WT
 git -C $ROOT worktree add --detach $WT $REV > /dev/null 2>&1
-make -s -C $WT/find_circ2_amd/csrc > /dev/null
-cp $WT/find_circ2_amd/libfc2.so $ROOT/find_circ2_amd/libfc2_$NAME.so
+# A/B build (FC2_AB_FORMS=1 where the revision has it: fc2_set_tuning + every kernel form)
+if grep -q "^ab:" $WT/find_circ2_amd/csrc/Makefile; then
+  make -s -C $WT/find_circ2_amd/csrc ab > /dev/null
+  cp $WT/find_circ2_amd/libfc2_ab.so $ROOT/find_circ2_amd/libfc2_$NAME.so
+else
+  make -s -C $WT/find_circ2_amd/csrc > /dev/null
+  cp $WT/find_circ2_amd/libfc2.so $ROOT/find_circ2_amd/libfc2_$NAME.so
+fi
 git -C $ROOT worktree remove --force $WT
 echo built $ROOT/find_circ2_amd/libfc2_$NAME.so from $REV

@@ -1,5 +1,6 @@
 #!/usr/bin/env python
-"""Interleaved A/B timing of bp_scan_kernel tuning knobs in ONE process (guide §5.4 rule 24).
+"""Interleaved A/B timing of bp_scan_kernel tuning knobs in ONE process (guide §5.4 rule 24), on A/B
+builds of the library (-DFC2_AB_FORMS=1).
 
 usage: python scripts/ab_kernel.py [--workload hg19|cdr1as] [--pairs N] [--rounds R] [--reps K]
 Prints one JSON line per variant: median / min kernel ms over rounds, pairs/s.
@@ -15,6 +16,9 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+# the knobs (fc2_set_tuning) exist only in A/B builds: libfc2_ab.so (make -C find_circ2_amd/csrc ab) unless
+# FC2_LIB_VARIANT names another A/B build (scripts/ab_build.sh)
+os.environ.setdefault("FC2_LIB_VARIANT", "ab")
 
 
 def main():

@@ -330,3 +330,15 @@ def test_bytepath_arena_matches_reference_windows(L, tmp_path):
             rb = ref.get_data(s.chrom, s.b_aend - e - l - 2, s.b_aend - e).upper()
             assert A == ra[:l + 3] and B == rb[:l + 3]
     L.fc2_fasta_close(h)
+
+
+def test_shipped_library_has_no_tuning_state():
+    """The shipped libfc2.so keeps no process-global knobs: fc2_set_tuning fails,
+    fc2_get_tuning reports the fixed defaults; forms are chosen per call (FC2_BATCH_FORM_*)."""
+    L = N.lib()
+    for key in (1, 2, 3, 6, 7, 9, 10, 11, 13, 14):
+        assert L.fc2_set_tuning(key, 0) == N.FC2_E_PARAM
+    assert b"A/B builds" in L.fc2_last_error()
+    defaults = {1: 1, 2: 1, 3: 2, 6: 2, 7: 2, 9: 0, 10: 0, 11: 1, 13: 512, 14: 2}
+    for key, v in defaults.items():
+        assert N.get_tuning(key) == v, key

@@ -2,10 +2,10 @@
 
 Every case draws find_circ.py options (``-a/--asize``, ``-m/--margin``, ``-d/--maxdist``,
 ``--non-canonical``, ``--strand-pref``, ``--all-hits``; find_circ.py:393-404) and a kernel form
-through the FC2_TUNE_* knobs (64- or 32-bit words, LDS staging on/off, 256/512/1024-pair blocks,
-three-lane window loads never/always/auto, persistent grid), then requires results bit-identical to
+through the per-call FC2_BATCH_FORM_* hints (LDS-staged / plain / automatic, word pairs or unit
+planes, two- or three-lane window loads, locus-ordered flag), then requires results bit-identical to
 the oracle's literal restatement of find_breakpoints (find_circ.py:854-974), ties included.
-Results never depend on the kernel form; the knobs are restored afterwards.
+Results never depend on the kernel form.
 """
 import os
 
@@ -19,33 +19,41 @@ from synth_small import load_genome, make_spans
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
-from find_circ2_amd import Options, decode_splices  # noqa: E402
+from find_circ2_amd import Options, PairBatch, decode_splices  # noqa: E402
 from find_circ2_amd import _native as N  # noqa: E402
 from test_gpu_parity import genome, oracle_spans, run_spans  # noqa: E402
 
-# FC2_TUNE_* (include/fc2_bp.h): knob -> value drawn per case
-KNOBS = {2: (0, 1), 7: (0, 1), 13: (256, 512, 1024), 14: (0, 1, 2), 10: (0, 0, -1)}
+# per-call form hints (fc2_batch_view.layout, include/fc2_bp.h): one drawn from each group per case
+HINTS = ((0, N.BATCH_FORM_STAGED, N.BATCH_FORM_PLAIN), (0, 0, N.BATCH_FORM_UNITS),
+         (0, N.BATCH_FORM_TWOLANE, N.BATCH_FORM_TRI), (0, 0, N.BATCH_LOCUS_ORDERED))
 
 
 @pytest.fixture
-def restore_knobs():
-    before = {k: N.get_tuning(k) for k in KNOBS}
-    yield
-    for k, v in before.items():
-        N.lib().fc2_set_tuning(k, v)
+def form_hint(monkeypatch):
+    """Every scan of the case runs with the drawn hints ORed into its batch view."""
+    box = {"hint": 0}
+    orig = PairBatch.view
+
+    def view(self):
+        v = orig(self)
+        v.layout |= box["hint"]
+        return v
+    monkeypatch.setattr(PairBatch, "view", view)
+    return box
 
 
 @pytest.mark.parametrize("seed", range(40))
-def test_random_options_and_kernel_forms(seed, restore_knobs):
+def test_random_options_and_kernel_forms(seed, form_hint):
     rng = np.random.default_rng(90210 + seed)
     asize = int(rng.integers(6, 26))
     margin = int(rng.integers(0, min(asize - 1, 7) + 1))
     opt = Options(asize=asize, margin=margin, maxdist=int(rng.choice([0, 1, 2, 3, 5, 8])),
                   noncanonical=bool(rng.random() < 0.3), strandpref=bool(rng.random() < 0.3),
                   allhits=bool(rng.random() < 0.3))
-    knobs = {k: int(rng.choice(v)) for k, v in KNOBS.items()}
-    for k, v in knobs.items():
-        N.lib().fc2_set_tuning(k, v)
+    knobs = 0
+    for group in HINTS:
+        knobs |= int(rng.choice(group))
+    form_hint["hint"] = knobs
     fa = ["CDR1as_locus.fa", "test_ref.fa"][seed % 2]
     path = os.path.join(GOLDEN, fa)
     g = genome(path)
@@ -56,7 +64,7 @@ def test_random_options_and_kernel_forms(seed, restore_knobs):
     b, out = run_spans(opt, g, spans)
     r = oracle_spans(opt, path, spans, g.names)
     ga = gpu_arrays(opt, b.host_pairs, out.host(b.n))
-    label = "seed %d %s knobs %s" % (seed, vars(opt), knobs)
+    label = "seed %d %s form hints 0x%x" % (seed, vars(opt), knobs)
     assert ga["done"].all(), label
     hits = assert_same(ga, oracle_arrays(r), label=label)
     assert hits > 20, label

@@ -60,22 +60,18 @@ def _n_heavy(path, seed=6):
 
 
 def _run(opt, g, spans, stage, twin, words=1):
-    L = N.lib()
-    N.check(L.fc2_set_tuning(7, stage))
-    N.check(L.fc2_set_tuning(6, twin))
-    N.check(L.fc2_set_tuning(11, words))
-    try:
-        flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.primary_reverse else 0)
-                 for s in spans]
-        b = PairBatch.pack(opt, g, [s.read_part for s in spans], [s.a_pos for s in spans],
-                           [s.b_aend for s in spans], [g.chrom_index_or_missing(s.chrom) for s in spans], flags)
-        out = scan(opt, g, b)
-        torch.cuda.synchronize()
-        return b, out
-    finally:
-        L.fc2_set_tuning(7, 2)
-        L.fc2_set_tuning(6, 2)
-        L.fc2_set_tuning(11, 1)
+    """Scan through one kernel form, chosen per call by fc2_batch_view.layout hints: stage -> the
+    LDS-staged or the plain form, words=0 -> the 64-base unit planes, twin=0 -> the batch flagged
+    locus-ordered (no shifted twin, XCD-contiguous blocks; results never depend on the flag)."""
+    flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.primary_reverse else 0)
+             for s in spans]
+    b = PairBatch.pack(opt, g, [s.read_part for s in spans], [s.a_pos for s in spans],
+                       [s.b_aend for s in spans], [g.chrom_index_or_missing(s.chrom) for s in spans], flags)
+    b.layout |= (N.BATCH_FORM_STAGED if stage else N.BATCH_FORM_PLAIN) | (0 if words else N.BATCH_FORM_UNITS) | \
+        (0 if twin else N.BATCH_LOCUS_ORDERED)
+    out = scan(opt, g, b)
+    torch.cuda.synchronize()
+    return b, out
 
 
 def _oracle(opt, path, spans):

@@ -1,12 +1,13 @@
 """GPU: every form of the scan kernel agrees bit for bit at the bench's full size.
 
-bp_scan32 has an LDS-staged form with cooperative window loads (read-order
-batches over a large genome) and a plain form (locus-ordered batches, small
-genomes); bp_scan is the 64-bit-word variant; the genome twin is optional.  They
-share no window-loading code path, so identical raw results on all 50M pairs of
-the BASELINE configs[2] workload (read order and locus order) are a
-size-independent parity property on top of the oracle comparisons of
-test_gpu_parity.py, which run at sizes the oracle finishes in seconds.
+bp_scan32 has an LDS-staged form with cooperative window loads (read-order batches over a large
+genome; two- or three-lane loads of the word-pair table, or the 64-base unit planes) and a plain
+form (locus-ordered batches, small genomes; word pairs or unit planes).  fc2_bp_scan_launch picks
+one per batch; the per-call FC2_BATCH_FORM_* hints of fc2_batch_view.layout force each of them
+(the shipped library has no process-global knobs; the measured-and-rejected forms live only in A/B
+builds, libfc2_ab.so).  They share no window-loading code path, so identical raw results on all
+50M pairs of the BASELINE configs[2] workload (read order and locus order) are a size-independent
+parity property on top of the oracle comparisons of test_gpu_parity.py / test_gpu_fullsize.py.
 """
 import os
 
@@ -21,33 +22,21 @@ pytestmark = pytest.mark.gpu
 from find_circ2_amd import Genome, Options, PairBatch, SynthConfig, scan, sq_table  # noqa: E402
 from find_circ2_amd import _native as N  # noqa: E402
 
-# knob values per form: FC2_TUNE_KERNEL32 (2), STAGE (7), TWIN (6), PERSIST (10), WORDS (11), STAGE_BLOCK (13),
-# TRI (14)
-KNOBS = (2, 7, 6, 10, 11, 13, 14)
-FORMS = {"scan32_staged_coop_words": (1, 1, 1, 0, 1, 256, 0), "scan32_staged_coop_words_512": (1, 1, 1, 0, 1, 512, 0),
-         "scan32_staged_coop_words_1024": (1, 1, 1, 0, 1, 1024, 0),
-         "scan32_staged_tri_words_512": (1, 1, 1, 0, 1, 512, 1),
-         "scan32_staged_tri_words_256": (1, 1, 1, 0, 1, 256, 1),
-         "scan32_staged_coop_units_twin": (1, 1, 1, 0, 0, 256, 0),
-         "scan32_persistent_coop_words": (1, 1, 1, -1, 1, 256, 0),
-         "scan32_persistent_coop_twin": (1, 1, 1, -1, 0, 256, 0),
-         "scan32_persistent_3_per_cu": (1, 1, 1, 3, 0, 256, 0),
-         "scan32_plain_words_no_twin": (1, 0, 0, 0, 1, 256, 0), "scan32_plain_words_twin": (1, 0, 1, 0, 1, 256, 0),
-         "scan32_plain_units_no_twin": (1, 0, 0, 0, 0, 256, 0), "scan32_plain_units_twin": (1, 0, 1, 0, 0, 256, 0),
-         "scan64": (0, 0, 0, 0, 1, 256, 0)}
-DEFAULTS = {k: N.get_tuning(k) for k in KNOBS}
+FORMS = {"default": 0,
+         "staged_words_twolane": N.BATCH_FORM_STAGED | N.BATCH_FORM_TWOLANE,
+         "staged_words_tri": N.BATCH_FORM_STAGED | N.BATCH_FORM_TRI,
+         "staged_units": N.BATCH_FORM_STAGED | N.BATCH_FORM_UNITS,
+         "plain_words": N.BATCH_FORM_PLAIN,
+         "plain_units": N.BATCH_FORM_PLAIN | N.BATCH_FORM_UNITS}
 
 
-def _set(form):
-    L = N.lib()
-    for k, v in zip(KNOBS, FORMS[form]):
-        N.check(L.fc2_set_tuning(k, v))
-
-
-def _reset():
-    L = N.lib()
-    for k, v in DEFAULTS.items():
-        L.fc2_set_tuning(k, v)
+def _scan_form(opt, g, b, form):
+    keep = b.layout
+    b.layout = keep | FORMS[form]
+    try:
+        return scan(opt, g, b)
+    finally:
+        b.layout = keep
 
 
 @pytest.fixture(scope="module")
@@ -66,8 +55,7 @@ def test_forms_agree_full_size(hg19, ordered):
     ref = None
     try:
         for form in FORMS:
-            _set(form)
-            out = scan(opt, hg19, b)
+            out = _scan_form(opt, hg19, b, form)
             torch.cuda.synchronize()
             res = out.results[:n].clone()
             del out
@@ -82,7 +70,6 @@ def test_forms_agree_full_size(hg19, ordered):
                 assert neq == 0, "%s differs from %s on %d of %d pairs" % (form, next(iter(FORMS)), neq, n)
             del res
     finally:
-        _reset()
         del b, ref
         torch.cuda.empty_cache()
 
@@ -95,10 +82,8 @@ def test_forms_agree_150bp(hg19):
     b = PairBatch.synthetic(opt, hg19, n, SynthConfig(seed=4242, len_min=120, len_max=150, span_max=20000))
     ref = None
     try:
-        for form in ("scan32_staged_tri_words_512", "scan32_staged_coop_words_512", "scan32_staged_coop_words",
-                     "scan32_plain_words_twin", "scan32_plain_units_twin", "scan64"):
-            _set(form)
-            out = scan(opt, hg19, b)
+        for form in ("default", "staged_words_twolane", "staged_units", "plain_words", "plain_units"):
+            out = _scan_form(opt, hg19, b, form)
             torch.cuda.synchronize()
             res = out.results[:n].clone()
             del out
@@ -109,7 +94,6 @@ def test_forms_agree_150bp(hg19):
                 neq = int((res != ref).sum())
                 assert neq == 0, "%s differs on %d of %d pairs" % (form, neq, n)
     finally:
-        _reset()
         torch.cuda.empty_cache()
 
 
@@ -121,8 +105,7 @@ def test_forms_agree_all_hits_ties(hg19):
     ref = None
     try:
         for form in FORMS:
-            _set(form)
-            out = scan(opt, hg19, b)
+            out = _scan_form(opt, hg19, b, form)
             torch.cuda.synchronize()
             cur = (out.results[:n].clone(), out.tiemask.view(out.tw, out.stride)[:, :n].clone())
             if ref is None:
@@ -132,5 +115,4 @@ def test_forms_agree_all_hits_ties(hg19):
                 assert torch.equal(cur[0], ref[0]), form
                 assert torch.equal(cur[1], ref[1]), form
     finally:
-        _reset()
         torch.cuda.empty_cache()

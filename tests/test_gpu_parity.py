@@ -23,13 +23,19 @@ from find_circ2_amd import _native as N  # noqa: E402
 from oracle.bp_oracle import Options as ROptions, RefIndexedFasta, Span, find_breakpoints  # noqa: E402
 
 
-@pytest.fixture(params=[1, 0], ids=["stage", "nostage"], autouse=True)
-def scan_variant(request):
+@pytest.fixture(params=[N.BATCH_FORM_STAGED, N.BATCH_FORM_PLAIN], ids=["stage", "nostage"], autouse=True)
+def scan_variant(request, monkeypatch):
     """Every parity case runs through both bp_scan32 forms: LDS-staged (chromosome table +
-    super-coarse N map) and unstaged (coarse map from L2); the default picks per batch."""
-    N.lib().fc2_set_tuning(7, request.param)
+    super-coarse N map) and unstaged (coarse map from L2), forced per call by the
+    FC2_BATCH_FORM_* hint in the batch view; the default picks per batch."""
+    orig = PairBatch.view
+
+    def view(self):
+        v = orig(self)
+        v.layout |= request.param
+        return v
+    monkeypatch.setattr(PairBatch, "view", view)
     yield request.param
-    N.lib().fc2_set_tuning(7, 2)
 
 
 def _dev():
