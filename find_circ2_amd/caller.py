@@ -350,7 +350,7 @@ class SpliceSiteStorage:
 
     def _load_known(self, path):
         n = 0
-        with open(path) as f:
+        with open(path, encoding="latin-1") as f:
             for line in f:
                 if line.startswith('#'):
                     continue

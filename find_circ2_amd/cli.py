@@ -129,11 +129,14 @@ def main(argv=None, evaluator_factory=None) -> int:
     from .hotpath import Options as HPOptions
     from .samio import AlignmentFile
 
-    out = {"circs": open(os.path.join(options.output, "circ_splice_sites.bed"), "w"),
-           "lins": open(os.path.join(options.output, "lin_splice_sites.bed"), "w"),
+    # latin-1 both ways (readers decode input bytes as latin-1): the output bytes are the input bytes,
+    # as the Python-2 reference writes them
+    out = {"circs": open(os.path.join(options.output, "circ_splice_sites.bed"), "w", encoding="latin-1"),
+           "lins": open(os.path.join(options.output, "lin_splice_sites.bed"), "w", encoding="latin-1"),
            "reads": ParallelGzipWriter(os.path.join(options.output, "spliced_reads.fastq.gz")),
-           "multi": open(os.path.join(options.output, "multi_events.tsv"), "w"),
-           "test": open(os.path.join(options.output, "test_results.tsv"), "w") if options.test else None}
+           "multi": open(os.path.join(options.output, "multi_events.tsv"), "w", encoding="latin-1"),
+           "test": open(os.path.join(options.output, "test_results.tsv"), "w", encoding="latin-1")
+           if options.test else None}
     if options.stdout:
         out[options.stdout].write('# redirected to stdout\n')
         out[options.stdout].close()

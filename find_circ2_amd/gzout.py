@@ -4,7 +4,9 @@ The reference writes the file through one GzipFile at level 9 (find_circ.py:445)
 at genome scale costs more than the whole native read loop.  Here the text is cut into
 ~4 MiB pieces, each compressed as its own gzip member on a thread pool (zlib releases the
 GIL) and written in order; concatenated members are one valid gzip stream (RFC 1952 2.2),
-so every gzip reader returns the same text.
+so every gzip reader returns the same text.  Text is encoded as latin-1, the decoding every
+reader of this package uses, so input bytes >= 0x80 (qnames, SEQ/QUAL) are written back as the
+same single bytes, as the Python-2 reference writes its byte strings.
 """
 from __future__ import annotations
 
@@ -21,7 +23,7 @@ def _member(data: bytes, level: int) -> bytes:
 
 
 class ParallelGzipWriter(io.TextIOBase):
-    def __init__(self, path: str, level: int = 6, threads: int = 0, piece: int = 4 << 20, encoding: str = "utf-8"):
+    def __init__(self, path: str, level: int = 6, threads: int = 0, piece: int = 4 << 20, encoding: str = "latin-1"):
         self._f = open(path, "wb")
         self._level = level
         self._piece = piece

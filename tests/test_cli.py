@@ -143,3 +143,23 @@ def test_cmp_bed_semantics(tmp_path, capsys):
     assert not cmp_bed.compare(ref, str(other))
     cap = capsys.readouterr()
     assert cap.out.startswith("MISSING\tCDR1as_locus\t728\t2213") and "input2_not_in_input1\t1" in cap.err
+
+
+@pytest.mark.parametrize("mode", [[], ["--python-caller"], ["--python-ingest"]])
+def test_non_ascii_bytes_written_back_unchanged(tmp_path, mode):
+    """a qname byte >= 0x80 (here 0xE9) comes back as that single byte in
+    spliced_reads.fastq.gz and as the same byte in the BED read lists (no UTF-8 re-encoding),
+    in all three read loops."""
+    import gzip
+    fa = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    reads = [("r\xe9ad%d_%s" % (i, n), s) for i, (n, s) in enumerate(_reads(os.path.join(GOLDEN, "cdr1as_reads.fa")))]
+    genome = read_fasta(fa)
+    sam = str(tmp_path / "in.sam")
+    with open(sam, "wb") as f:
+        f.write(sam_text(genome, reads).encode("latin-1"))
+    out = str(tmp_path / "o")
+    assert cli.main(["-G", fa, "-o", out, "-q"] + mode + [sam], evaluator_factory=oracle_evaluator_factory) == 0
+    raw = gzip.open(os.path.join(out, "spliced_reads.fastq.gz"), "rb").read()
+    assert b"r\xe9ad" in raw and b"r\xc3\xa9ad" not in raw
+    bed = open(os.path.join(out, "circ_splice_sites.bed"), "rb").read()
+    assert b"\xc3\xa9" not in bed
