@@ -61,6 +61,13 @@ def main():
                                                    if rq.get("TCC_EA0_RDREQ_sum") else None),
                     "hbm_bytes_per_launch": round(hbm), "hbm_bytes_per_pair": round(hbm / N_PAIRS, 1),
                     "moved_TBps": round(hbm / (ns * 1e-9) / 1e12, 3) if ns else None}
+    import subprocess
+    try:
+        commit = subprocess.check_output(["git", "-C", ROOT, "rev-parse", "HEAD"], text=True).strip()
+    except Exception:
+        commit = None
+    for v in out.values():
+        v["commit"] = commit        # the tree the passes ran on (stamped when the JSON is built, locally)
     out["correction"] = ("reads = 2 x FETCH_SIZE x 1024 (gfx950 128-B fills tallied at 64 B), writes = WRITE_SIZE x "
                          "1024 (exact: 8 B x pairs)")
     out["source"] = ("rocprofv3 --kernel-trace --stats and separate --pmc passes (scripts/profile_round.sh): bench.py "
