@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
     ap.add_argument("--no-strong", action="store_true", help="skip the configs[3] strong-scaling / ordered-merge run")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r01.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     return ap.parse_args()
 
 
@@ -731,13 +731,21 @@ def main():
     value = total_pairs / elapsed
     bpp = algo_bytes_per_pair(args.read_len, opt.asize, opt.margin)
     achieved = bpp * b.n / (kernel_ms * 1e-3) / 1e9
-    traffic = None
+    # HBM bytes per launch from the PMC passes of scripts/profile_round.sh (a --pmc pass cannot run
+    # inside this process); used only for the same workload, and stamped with the commit, kernel and
+    # rocprof duration it was measured on, next to this run's kernel time, so a stale value shows
+    traffic, traffic_src = None, None
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             w = tj.get(args.workload + ("_locus_ordered" if args.locus_ordered else ""))
             if w and int(w.get("pairs_per_launch", -1)) == b.n:
                 traffic = w.get("hbm_bytes_per_launch")
+                ns = w.get("avg_kernel_ns_rocprof")
+                traffic_src = {"file": os.path.relpath(args.traffic_json, ROOT), "commit": w.get("commit"),
+                               "kernel": w.get("kernel"), "profiled_kernel_ms": round(ns / 1e6, 4) if ns else None,
+                               "this_run_kernel_ms": round(kernel_ms, 4),
+                               "hbm_bytes_per_pair": w.get("hbm_bytes_per_pair")}
         except Exception:
             traffic = None
     res = out.host(b.n)
@@ -777,6 +785,7 @@ def main():
         },
         "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "kernel_ms": round(kernel_ms, 4), "algo_bytes_per_pair": bpp,
                      "kernel": kernel_label(g, args.locus_ordered)},
         "cpu_baseline": None,
