@@ -561,7 +561,7 @@ __device__ __forceinline__ void window_nwords_plain(const fc2_genome_view &g, __
 __device__ __forceinline__ void windows_issue_w3(const fc2_genome_view &g, __amdgpu_buffer_rsrc_t rs,
                                                  __amdgpu_buffer_rsrc_t rn, const uint32_t *s_nsuper,
                                                  uint64_t cstart, int64_t wsA, int64_t wsB, int W, bool active,
-                                                 WinW &rA, WinW &rB, u32x4 *dma) {
+                                                 WinW &rA, WinW &rB, u32x4 (&cl)[7]) {
     window_geom_w(g, cstart, wsA, W, rA, true);
     window_geom_w(g, cstart, wsB, W, rB, true);
     const int lane = (int)(threadIdx.x & 63);
@@ -606,15 +606,10 @@ __device__ __forceinline__ void windows_issue_w3(const fc2_genome_view &g, __amd
             sb[x][1] = k1 & 31u;
         }
     }
-    // LDS-DMA (buffer_load_dwordx4 ... lds): instruction c writes lane L's 16 B to dma[c * 64 + L], so
-    // window 21c + k lands as 48 contiguous bytes at dma[c * 64 + 3k] -- no VGPR round trip and no
-    // ds_write pass (the two-phase register exchange cost 1.6x the LDS instructions of the 100-bp
-    // form and 4.7x its LDS issue stalls, profiles/r01/pmc150/summary.json)
 #pragma unroll
     for (int c = 0; c < 7; ++c) {
-        if (ok[c])
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void *)(dma + c * 64), 16,
-                                                     src[c] + 16u * (uint32_t)part[c], 0, 0, 0);
+        cl[c] = u32x4{0u, 0u, 0u, 0u};
+        if (ok[c]) cl[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, src[c] + 16u * (uint32_t)part[c], 0, 0);
     }
 #pragma unroll
     for (int x = 0; x < 2; ++x) {
@@ -637,6 +632,10 @@ __device__ __forceinline__ void windows_issue_w3(const fc2_genome_view &g, __amd
     }
 }
 
+// Owner side: the first 40 B of each window's three 16-B pieces, in two phases through 4 LDS slots
+// (4 KB per wave instead of 7; 1.5 % faster at 150 bp, profiles/r01/ab_tri_4slot.jsonl): instructions
+// 0-3 hold every A window and B windows 64..83, then instructions 4-6 overwrite slots 0-2 with B
+// windows 84..127.
 __device__ __forceinline__ void wave_sync_lds() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -650,17 +649,19 @@ __device__ __forceinline__ void take_w3(const u32x4 *xchg, int slot, int w, WinW
     Q.v1 = p1;
     Q.v4 = p2;
 }
-// Owner side of the three-lane loads: the first 40 B of each window from the wave's LDS-DMA image
-// (7 x 1 KB).  The compiler does not track LDS-DMA writes, so the wait for them (vmcnt(0): this
-// wave's loads, DMA included, have landed) is explicit, followed by a fence so no LDS read is
-// scheduled above it.
-__device__ __forceinline__ void windows_take_w3(const u32x4 *dma, WinW &rA, WinW &rB) {
+__device__ __forceinline__ void windows_exchange_w3(u32x4 *xchg, const u32x4 (&cl)[7], WinW &rA, WinW &rB) {
     const int lane = (int)(threadIdx.x & 63);
-    __builtin_amdgcn_s_waitcnt(0x0F70);        // vmcnt(0) (expcnt / lgkmcnt left at their maxima)
-    wave_sync_lds();
-    take_w3(dma, lane / 21, lane, rA);
     const int wB = 64 + lane;
-    take_w3(dma, wB / 21, wB, rB);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) xchg[c * 64 + lane] = cl[c];
+    wave_sync_lds();
+    take_w3(xchg, lane / 21, lane, rA);
+    if (wB < 84) take_w3(xchg, 3, wB, rB);
+    wave_sync_lds();                           // every phase-1 read done before slots 0-2 are reused
+#pragma unroll
+    for (int c = 4; c < 7; ++c) xchg[(c - 4) * 64 + lane] = cl[c];
+    wave_sync_lds();
+    if (wB >= 84) take_w3(xchg, wB / 21 - 4, wB, rB);
 }
 
 template <int NQ>
@@ -827,6 +828,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     ulonglong2 cl[2][2];
     WinW wA, wB;
     u32x4 wcl[2][2];
+    u32x4 wcl3[TRI ? 7 : 1];
     uint64_t cwA = 0, cwB = 0;
     __amdgpu_buffer_rsrc_t rs, rn;
     if constexpr (WL) {
@@ -839,7 +841,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
         if (!active) W = 2;
         windows_issue_w3(g, rs, rn, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active, wA,
-                         wB, reinterpret_cast<u32x4 *>(xchg));
+                         wB, wcl3);
     } else if constexpr (COOP && WL) {
         static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
         if (!active) W = 2;
@@ -924,7 +926,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         }
         if (!active) return;
     } else if constexpr (COOP && WL && TRI) {
-        windows_take_w3(reinterpret_cast<const u32x4 *>(xchg), wA, wB);
+        windows_exchange_w3(reinterpret_cast<u32x4 *>(xchg), wcl3, wA, wB);
         if (!active) return;
         window_finish_w<NQ>(wA, csize, wsA, W, A);
         window_finish_w<NQ>(wB, csize, wsB, W, B);
@@ -1254,7 +1256,7 @@ __global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc
     __shared__ uint64_t s_cstart[kChromLds];
     __shared__ int64_t s_csize[kChromLds];
     __shared__ __attribute__((aligned(16))) uint32_t s_nsuper_buf[kSuperLds];
-    __shared__ __attribute__((aligned(16))) ulonglong2 s_xchg[BT / 64][(TRI ? 7 : 4) * 64];   // TRI: LDS-DMA image
+    __shared__ ulonglong2 s_xchg[BT / 64][4 * 64];
     // the launcher guarantees: genome not dummy, word-pair table, tables fit in LDS
     for (uint32_t w = 4 * threadIdx.x; w < (uint32_t)kSuperLds; w += 4 * BT) {
         uint4 q = uint4{0u, 0u, 0u, 0u};
