@@ -10,6 +10,7 @@
 #include <deque>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <set>
 #include <string>
 #include <tuple>
@@ -213,14 +214,22 @@ struct fc2_caller {
     std::vector<int32_t> tid2chrom;
     const fc2_fasta *fasta = nullptr;
     bool eof = false;
-    // the chunk being formed (fc2_caller_next) or recorded (fc2_caller_submit)
-    std::vector<Frag> frags;
+    // Two sides that may run on two threads at once: fc2_caller_next forms chunks (ingest,
+    // process_mate, the pairs) into the bf_* fields, fc2_caller_submit records the oldest queued chunk
+    // (record_hits, tables, writers) from the plain fields.  They share only the queue (mutex) and
+    // read-only state (options, genome map, reference names); each side has its own counters.
+    std::vector<Frag> bf_frags;                 // the chunk being formed (next)
+    std::vector<Span> bf_spans;
+    std::string bf_arena;                       // read_part bytes
+    std::vector<uint64_t> bf_off;
+    std::vector<fc2_pair> bf_pairs;
+    std::vector<Frag> frags;                    // the chunk being recorded (submit)
     std::vector<Span> spans;
-    std::string arena;                          // read_part bytes
+    std::string arena;
     std::vector<uint64_t> b_off;
     std::vector<fc2_pair> b_pairs;
     // chunks handed out by fc2_caller_next and not yet submitted, oldest first: the caller may
-    // read ahead (form chunk k+1 while chunk k is on the GPU); submit always records the oldest
+    // read ahead (form chunk k+1 while chunk k is on the GPU or being recorded)
     struct Chunk {
         std::vector<Frag> frags;
         std::vector<Span> spans;
@@ -229,6 +238,7 @@ struct fc2_caller {
         std::vector<fc2_pair> b_pairs;
     };
     std::deque<Chunk> queued;
+    std::mutex qmu;
     // aggregation
     struct Storage {
         std::string prefix;
@@ -238,6 +248,7 @@ struct fc2_caller {
     } st[2];                                    // 0 circ, 1 lin
     std::vector<std::pair<const char *, double>> N;   // the reference's counters, keyed by literal
                                                       // (merged by name into sorted keys on output)
+    std::vector<std::pair<const char *, double>> N_in; // the same for the counters the next side bumps
     std::string out[3];                         // reads, multi, test text since the last take
     std::string rows_text;
     std::vector<std::pair<std::string, double>> counters_snapshot;
@@ -246,11 +257,15 @@ struct fc2_caller {
 
 namespace {
 
-void incN(fc2_caller *h, const char *k, double v = 1.) {
-    for (auto &kv : h->N)
+void incN_into(std::vector<std::pair<const char *, double>> &N, const char *k, double v) {
+    for (auto &kv : N)
         if (kv.first == k) { kv.second += v; return; }
-    h->N.emplace_back(k, v);
+    N.emplace_back(k, v);
 }
+// record side (fc2_caller_submit and the output functions)
+void incN(fc2_caller *h, const char *k, double v = 1.) { incN_into(h->N, k, v); }
+// next side (process_mate)
+void incN_in(fc2_caller *h, const char *k, double v = 1.) { incN_into(h->N_in, k, v); }
 
 // ---- Hit / SpliceSiteStorage ----------------------------------------------------------
 void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
@@ -480,7 +495,7 @@ const char *kNoneLen = "TypeError: object of type 'NoneType' has no len()";
 void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
     const Rec &prim = m.recs[0];
     if (m.proper.size() < 2) {
-        incN(h, "unspliced_mates");
+        incN_in(h, "unspliced_mates");
         fr.unspliced.push_back(make_align(prim));
         return;
     }
@@ -502,7 +517,7 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
     for (size_t k = 0; k + 1 < n; ++k) {
         const size_t a = order[k], b = order[k + 1];
         if (ends[a] - starts[a] < h->o.asize || ends[b] - starts[b] < h->o.asize) {
-            incN(h, "seg_too_short_skip");
+            incN_in(h, "seg_too_short_skip");
             continue;
         }
         const Rec &A = m.recs[m.proper[a]], &B = m.recs[m.proper[b]];
@@ -523,11 +538,11 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
         s.a_rev = s.circ ? B.reverse() : A.reverse();
         // read_part = primary.seq[q_start:q_end] (Python slice)
         const int64_t lo = std::max<int64_t>(0, std::min(q_start, L)), hi = std::max(lo, std::min(q_end, L));
-        s.read_off = h->arena.size();
+        s.read_off = h->bf_arena.size();
         s.read_len = (uint32_t)(hi - lo);
-        h->arena.append(prim.seq, (size_t)lo, (size_t)(hi - lo));
-        h->spans.push_back(s);
-        (s.circ ? fr.circ : fr.lin).push_back((int)h->spans.size() - 1);
+        h->bf_arena.append(prim.seq, (size_t)lo, (size_t)(hi - lo));
+        h->bf_spans.push_back(s);
+        (s.circ ? fr.circ : fr.lin).push_back((int)h->bf_spans.size() - 1);
         min_s = std::min(min_s, q_start);
         max_e = std::max(max_e, q_end);
     }
@@ -544,7 +559,7 @@ int on_fragment(fc2_caller *h, const Mate *m1, const Mate *m2) {
     Frag fr;
     fr.name = m2->recs[0].qname;               // Fragment(mate2.primary.qname, ...)
     const Mate *ms[2] = {m1, m2};
-    const size_t span0 = h->spans.size(), arena0 = h->arena.size();
+    const size_t span0 = h->bf_spans.size(), arena0 = h->bf_arena.size();
     for (int k = 0; k < 2; ++k) {
         if (!ms[k]) continue;
         fr.has[k] = true;
@@ -552,11 +567,11 @@ int on_fragment(fc2_caller *h, const Mate *m1, const Mate *m2) {
         process_mate(h, *ms[k], k, fr);
     }
     if ((fr.circ.empty() && h->o.nolinear) || (fr.circ.empty() && fr.lin.empty())) {
-        h->spans.resize(span0);                // not pending: its spans are never evaluated
-        h->arena.resize(arena0);
+        h->bf_spans.resize(span0);                // not pending: its spans are never evaluated
+        h->bf_arena.resize(arena0);
         return FC2_OK;
     }
-    h->frags.push_back(std::move(fr));
+    h->bf_frags.push_back(std::move(fr));
     return FC2_OK;
 }
 
@@ -1029,13 +1044,16 @@ extern "C" void fc2_caller_close(fc2_caller *h) {
 
 extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     if (!h || !b) return fc2::fail(FC2_E_PARAM, "fc2_caller_next: null argument");
-    if (h->queued.size() >= FC2_CALLER_MAX_QUEUED)
-        return fc2::fail(FC2_E_PARAM, "fc2_caller_next: too many chunks not submitted");
-    h->frags.clear();
-    h->spans.clear();
-    h->arena.clear();
-    h->b_off.clear();
-    h->b_pairs.clear();
+    {
+        std::lock_guard<std::mutex> lk(h->qmu);
+        if (h->queued.size() >= FC2_CALLER_MAX_QUEUED)
+            return fc2::fail(FC2_E_PARAM, "fc2_caller_next: too many chunks not submitted");
+    }
+    h->bf_frags.clear();
+    h->bf_spans.clear();
+    h->bf_arena.clear();
+    h->bf_off.clear();
+    h->bf_pairs.clear();
     Fatal err{0, ""};
     const fc2::ing::FragSink sink = [&](const Mate *m1, const Mate *m2, bool) -> int {
         try {
@@ -1045,17 +1063,17 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             return f.code ? f.code : FC2_E_FORMAT;
         }
     };
-    while (!h->eof && h->frags.size() < h->o.chunksize) {
+    while (!h->eof && h->bf_frags.size() < h->o.chunksize) {
         int e = 0;
         const int rc = fc2::ing::pull(h->ing, &h->ip, h->o.chunksize, sink, &e);
         if (rc) return err.code ? fc2::fail(err.code, err.msg) : rc;
         h->eof = e != 0;
     }
     // the spans record_hits will evaluate, in fragment order (Caller._flush)
-    for (const Frag &fr : h->frags) {
+    for (const Frag &fr : h->bf_frags) {
         for (int pass = 0; pass < 2; ++pass) {
             for (int si : pass ? fr.lin : fr.circ) {
-                Span &s = h->spans[si];
+                Span &s = h->bf_spans[si];
                 if (!(s.uniq >= h->o.min_uniq_qual)) continue;
                 fc2_pair pr{};
                 pr.a_pos = (int32_t)s.a_pos;
@@ -1068,40 +1086,48 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
                                                    "or a number, not 'NoneType'");
                 pr.flags = (uint8_t)((s.circ ? FC2_PAIR_BACKSPLICE : 0) |
                                      (fr.prim[s.mate].rev ? FC2_PAIR_PRIMARY_REV : 0) | (c < 0 ? FC2_PAIR_SKIP : 0));
-                s.eval = (int64_t)h->b_pairs.size();
-                h->b_pairs.push_back(pr);
-                h->b_off.push_back(s.read_off);
+                s.eval = (int64_t)h->bf_pairs.size();
+                h->bf_pairs.push_back(pr);
+                h->bf_off.push_back(s.read_off);
             }
         }
     }
-    for (const Span &s : h->spans)
+    for (const Span &s : h->bf_spans)
         if (s.eval >= 0 && s.read_len > FC2_MAX_READ_LEN)
             return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
                                               " bases (fc2_result.best_x is 16-bit)");
-    h->n_pairs += h->b_pairs.size();
-    h->arena.append(16, '\0');                 // readers of the batch may load whole words past the end
-    h->queued.emplace_back();
-    fc2_caller::Chunk &c = h->queued.back();
-    c.frags.swap(h->frags);
-    c.spans.swap(h->spans);
-    c.arena.swap(h->arena);
-    c.b_off.swap(h->b_off);
-    c.b_pairs.swap(h->b_pairs);
-    b->n = c.b_pairs.size();
-    b->reads = (const uint8_t *)c.arena.data();
-    b->read_off = c.b_off.data();
-    b->pairs = c.b_pairs.data();
+    h->n_pairs += h->bf_pairs.size();
+    h->bf_arena.append(16, '\0');                 // readers of the batch may load whole words past the end
+    fc2_caller::Chunk c;
+    c.frags.swap(h->bf_frags);
+    c.spans.swap(h->bf_spans);
+    c.arena.swap(h->bf_arena);
+    c.b_off.swap(h->bf_off);
+    c.b_pairs.swap(h->bf_pairs);
+    std::lock_guard<std::mutex> lk(h->qmu);
+    h->queued.push_back(std::move(c));           // moved vectors keep their buffers: *b stays valid
+    const fc2_caller::Chunk &q = h->queued.back();
+    b->n = q.b_pairs.size();
+    b->reads = (const uint8_t *)q.arena.data();
+    b->read_off = q.b_off.data();
+    b->pairs = q.b_pairs.data();
     if (eof) *eof = h->eof ? 1 : 0;
     return FC2_OK;
 }
 
-extern "C" int fc2_caller_queued(const fc2_caller *h) { return h ? (int)h->queued.size() : 0; }
+extern "C" int fc2_caller_queued(fc2_caller *h) {
+    if (!h) return 0;
+    std::lock_guard<std::mutex> lk(h->qmu);
+    return (int)h->queued.size();
+}
 
 extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const uint64_t *tiemask, uint32_t tw,
                                  uint64_t stride) {
     if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: null argument");
-    if (h->queued.empty()) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: no chunk handed out by fc2_caller_next");
     {
+        std::lock_guard<std::mutex> lk(h->qmu);
+        if (h->queued.empty())
+            return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: no chunk handed out by fc2_caller_next");
         fc2_caller::Chunk &c = h->queued.front();
         h->frags.swap(c.frags);
         h->spans.swap(c.spans);
@@ -1157,6 +1183,7 @@ extern "C" int fc2_caller_counter(fc2_caller *h, int i, const char **name, doubl
         // over (Caller.run_native adds the non-zero ones)
         std::map<std::string, double> m;
         for (const auto &kv : h->N) m[kv.first] += kv.second;
+        for (const auto &kv : h->N_in) m[kv.first] += kv.second;
         fc2_ingest_counts c{};
         fc2_ingest_counts_get(h->ing, &c);
         const std::pair<const char *, uint64_t> ing[4] = {{"total_mates", c.total_mates},

@@ -17,6 +17,8 @@ from __future__ import annotations
 import ctypes
 import sys
 import time
+import queue
+import threading
 from collections import deque
 from typing import Callable, Dict, Optional
 
@@ -131,8 +133,116 @@ class NativeCaller:
             if txt and outputs.get(key) is not None:
                 outputs[key].write(txt)
 
-    def run(self, evaluate, outputs: Dict, stderr=sys.stderr, throughput=False, chunksize=100000):
+    def run(self, evaluate, outputs: Dict, stderr=sys.stderr, throughput=False, chunksize=100000, threads=None):
         """Process the whole input; returns (seconds, n_reads, n_pairs, evaluate_seconds).
+
+        By default (``threads`` None/True, no -B/--bam) the loop runs on two threads: a reader
+        thread forms chunks (``fc2_caller_next``: ingest, process_mate, the pairs) and queues their
+        search, while this thread records them in input order (``fc2_caller_submit``: record_hits,
+        tables, writers) -- the two halves of the reference's per-fragment loop overlap, and the
+        outputs are those of the sequential loop (``_run_sequential``, used with -B, where records
+        are written while reading, or ``threads=False``).
+        """
+        if self.bam_out or threads is False:
+            return self._run_sequential(evaluate, outputs, stderr, throughput, chunksize)
+        return self._run_threaded(evaluate, outputs, stderr, throughput, chunksize)
+
+    def _run_threaded(self, evaluate, outputs: Dict, stderr, throughput, chunksize):
+        L = N.lib()
+        t0 = time.time()
+        pipelined = hasattr(evaluate, "submit") and hasattr(evaluate, "result")
+        depth = max(2, int(getattr(evaluate, "depth", 2)))
+        q: "queue.Queue" = queue.Queue()
+        # at most `depth` chunks between being handed out and being recorded: a ScanPipeline slot is
+        # only reused once its chunk's results were taken
+        slots = threading.Semaphore(depth)
+        stop = threading.Event()
+        eval_s = [0.0, 0.0]                  # reader (pack/queue), recorder (waits for results)
+
+        def reader():
+            try:
+                while True:
+                    slots.acquire()
+                    if stop.is_set():
+                        return
+                    batch = N.CallerBatch()
+                    eof_c = ctypes.c_int(0)
+                    rc = L.fc2_caller_next(self.h, ctypes.byref(batch), ctypes.byref(eof_c))
+                    if rc != N.FC2_OK:
+                        try:
+                            _raise_native(rc)           # fc2_last_error is per thread: read it here
+                        except Exception as ex:
+                            q.put(("err", ex, 0))
+                        return
+                    n = int(batch.n)
+                    te = time.perf_counter()
+                    if not n:
+                        item = None
+                    elif pipelined:
+                        pairs = np.ctypeslib.as_array(ctypes.cast(batch.pairs, ctypes.POINTER(ctypes.c_uint8)),
+                                                      (16 * n,)).view(N.PAIR_DTYPE)
+                        off = np.ctypeslib.as_array(ctypes.cast(batch.read_off, ctypes.POINTER(ctypes.c_uint64)),
+                                                    (n,))
+                        item = evaluate.submit(batch.reads, off, pairs)
+                    else:
+                        item = evaluate(*self._host_batch(batch, n))
+                    eval_s[0] += time.perf_counter() - te
+                    q.put(("chunk", item, n))
+                    if eof_c.value:
+                        q.put(("eof", None, 0))
+                        return
+            except BaseException as ex:         # noqa: BLE001 -- handed to the recording thread
+                q.put(("err", ex, 0))
+
+        th = threading.Thread(target=reader, name="fc2-reader", daemon=True)
+        th.start()
+        t_last, last_reads = t0, 0
+        try:
+            while True:
+                kind, item, n = q.get()
+                if kind == "err":
+                    raise item
+                if kind == "eof":
+                    break
+                res_ptr = tm_ptr = None
+                tw = 0
+                if n:
+                    te = time.perf_counter()
+                    res, tm = evaluate.result(item, copy=False) if pipelined else item
+                    eval_s[1] += time.perf_counter() - te
+                    res = np.ascontiguousarray(res, dtype=np.int64)
+                    res_ptr = res.ctypes.data
+                    if tm is not None:
+                        tm = np.ascontiguousarray(tm, dtype=np.uint64)
+                        tw = tm.shape[0]
+                        tm_ptr = tm.ctypes.data
+                rc = L.fc2_caller_submit(self.h, res_ptr, tm_ptr, tw, n)
+                self._write_outputs(outputs)
+                slots.release()
+                if rc != N.FC2_OK:
+                    _raise_native(rc)
+                if throughput:
+                    nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
+                    L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
+                    if nr.value // chunksize > last_reads // chunksize:
+                        t1 = time.time()
+                        stderr.write("\rprocessed {0:.1f}M (paired-end) reads in {1:.1f} minutes ({2:.2f}k "
+                                     "reads/second)       \r".format(nr.value / 1e6, (t1 - t0) / 60.,
+                                                                   (nr.value - last_reads) / max(t1 - t_last, 1e-9)
+                                                                   / 1000.))
+                        t_last, last_reads = t1, nr.value
+        finally:
+            stop.set()
+            slots.release()                     # a reader blocked on the semaphore sees `stop`
+            th.join()
+        if throughput:
+            stderr.write('\n')
+        nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
+        L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
+        return time.time() - t0, int(nr.value), int(npairs.value), eval_s[0] + eval_s[1]
+
+    def _run_sequential(self, evaluate, outputs: Dict, stderr=sys.stderr, throughput=False, chunksize=100000):
+        """One thread; reads ahead up to the evaluator's depth (none with -B/--bam).
 
         ``evaluate`` is either a plain ``evaluate(reads, read_off, pairs) -> (results, tiemask)``
         or a pipelined evaluator with ``submit(reads_ptr, read_off, pairs) -> ticket``,

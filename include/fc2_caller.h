@@ -68,7 +68,9 @@ fc2_ingest *fc2_caller_ingest(fc2_caller *h);    /* reference names, header */
 void fc2_caller_close(fc2_caller *h);
 
 /* Read on until `chunksize` fragments carry pairs (or the input ends); *b = the pairs
- * to evaluate (n may be 0), *eof = 1 once the input is exhausted.  The chunk stays queued
+ * to evaluate (n may be 0), *eof = 1 once the input is exhausted.  fc2_caller_next and
+ * fc2_caller_submit may run concurrently on two threads (one caller of each): they share only
+ * the chunk queue.  fc2_last_error() is per thread.  The chunk stays queued
  * (and *b valid) until fc2_caller_submit records it, so a caller may read ahead: form
  * chunk k+1 while chunk k is being searched (at most FC2_CALLER_MAX_QUEUED chunks).
  * Reading ahead changes nothing in the outputs, which submit writes in input order;
@@ -77,7 +79,7 @@ void fc2_caller_close(fc2_caller *h);
 #define FC2_CALLER_MAX_QUEUED 64
 int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof);
 /* Chunks handed out by fc2_caller_next and not yet submitted. */
-int fc2_caller_queued(const fc2_caller *h);
+int fc2_caller_queued(fc2_caller *h);
 /* Results of the OLDEST queued batch, in its order: fc2_result [n] and, with --all-hits,
  * the tie mask [tw][stride] (x-major 64-bit words, '+' rows then '-' rows). */
 int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const uint64_t *tiemask, uint32_t tw,
