@@ -288,6 +288,8 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             return 1
         nc.close_bam_out()
         _finish(options, seconds, n_reads, logger, nc.counters(), n_pairs, eval_s)
+        if nc.loop_profile:
+            logger.info("read loop stages: " + ", ".join("%s=%.3f" % kv for kv in sorted(nc.loop_profile.items())))
         for kind, key in ((0, "circs"), (1, "lins")):
             out[key].write(BED_HEADER)
             out[key].write(nc.rows(kind))

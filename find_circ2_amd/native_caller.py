@@ -82,6 +82,7 @@ class NativeCaller:
         self._is_bam = is_bam
         self.bam_out = bam_out
         self.opened = False
+        self.loop_profile = {}       # seconds per stage of the last run (two-thread loop)
 
     def open(self):
         """Open the input, map its reference ids to genome indices, load the known sites.
@@ -167,7 +168,9 @@ class NativeCaller:
                         return
                     batch = N.CallerBatch()
                     eof_c = ctypes.c_int(0)
+                    tn = time.perf_counter()
                     rc = L.fc2_caller_next(self.h, ctypes.byref(batch), ctypes.byref(eof_c))
+                    self.loop_profile["next_s"] += time.perf_counter() - tn
                     if rc != N.FC2_OK:
                         try:
                             _raise_native(rc)           # fc2_last_error is per thread: read it here
@@ -194,12 +197,15 @@ class NativeCaller:
             except BaseException as ex:         # noqa: BLE001 -- handed to the recording thread
                 q.put(("err", ex, 0))
 
+        self.loop_profile = {"next_s": 0.0, "queue_wait_s": 0.0, "submit_s": 0.0, "write_s": 0.0}
         th = threading.Thread(target=reader, name="fc2-reader", daemon=True)
         th.start()
         t_last, last_reads = t0, 0
         try:
             while True:
+                tq = time.perf_counter()
                 kind, item, n = q.get()
+                self.loop_profile["queue_wait_s"] += time.perf_counter() - tq
                 if kind == "err":
                     raise item
                 if kind == "eof":
@@ -216,8 +222,12 @@ class NativeCaller:
                         tm = np.ascontiguousarray(tm, dtype=np.uint64)
                         tw = tm.shape[0]
                         tm_ptr = tm.ctypes.data
+                ts = time.perf_counter()
                 rc = L.fc2_caller_submit(self.h, res_ptr, tm_ptr, tw, n)
+                tw_ = time.perf_counter()
                 self._write_outputs(outputs)
+                self.loop_profile["submit_s"] += tw_ - ts
+                self.loop_profile["write_s"] += time.perf_counter() - tw_
                 slots.release()
                 if rc != N.FC2_OK:
                     _raise_native(rc)
@@ -237,6 +247,7 @@ class NativeCaller:
             th.join()
         if throughput:
             stderr.write('\n')
+        self.loop_profile.update(eval_pack_s=eval_s[0], eval_wait_s=eval_s[1])
         nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
         L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
         return time.time() - t0, int(nr.value), int(npairs.value), eval_s[0] + eval_s[1]

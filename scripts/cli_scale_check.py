@@ -109,6 +109,7 @@ def main():
     ap.add_argument("--reads", type=int, default=1_000_000)
     ap.add_argument("--scale", type=float, default=1.0)
     ap.add_argument("--out", default="/tmp/fc2_scale")
+    ap.add_argument("--only", default="", help="comma list of run tags (timing only; the identity check needs all)")
     a = ap.parse_args()
     from find_circ2_amd import cli, sq_table
     rng = np.random.default_rng(2024)
@@ -130,6 +131,8 @@ def main():
     for tag, extra in (("native", []), ("native_gpus2", ["--gpus", "2"]), ("python_caller", ["--python-caller"]),
                        ("native_allhits", ["--all-hits", "--non-canonical"]),
                        ("python_caller_allhits", ["--python-caller", "--all-hits", "--non-canonical"])):
+        if a.only and tag not in a.only.split(","):
+            continue
         out = os.path.join(a.out, tag)
         t0 = time.time()
         rc = cli.main(["-G", fa, "-o", out, "-n", "scale", "-q"] + extra + [sam])
@@ -137,9 +140,12 @@ def main():
         res[tag + "_rc"] = rc
         log = open(os.path.join(out, "run.log")).read().splitlines()
         res[tag + "_log"] = [l.split("\t")[-1] for l in log if "processed" in l or "breakpoint search" in l
-                             or "reading from" in l]
+                             or "reading from" in l or "read loop stages" in l]
         outs[tag] = out
         print("done", tag, res[tag + "_s"], file=sys.stderr, flush=True)
+    if a.only:
+        print(json.dumps(res))
+        return 0
     same = True
     for x, y in (("native", "python_caller"), ("native", "native_gpus2"), ("native_allhits", "python_caller_allhits")):
         for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
