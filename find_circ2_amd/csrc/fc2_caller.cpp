@@ -12,6 +12,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <stdexcept>
 #include <string>
 #include <tuple>
 #include <unordered_map>
@@ -140,12 +141,67 @@ struct Frag {
 
 using Coord = std::tuple<std::string, int64_t, int64_t, std::string>;   // (chrom, start, end, strand)
 
-std::string coord_key(const Coord &c) {
-    return std::get<0>(c) + '\t' + i2s(std::get<1>(c)) + '\t' + i2s(std::get<2>(c)) + '\t' + std::get<3>(c);
-}
+// SpliceSiteStorage's dict key (the coord tuple), without building a string: the chromosome and the
+// strand interned to small ids, the two positions as they are
+struct CKey {
+    int64_t start, end;
+    uint32_t chrom, strand;
+    bool operator==(const CKey &o) const {
+        return start == o.start && end == o.end && chrom == o.chrom && strand == o.strand;
+    }
+};
+struct CKeyHash {
+    size_t operator()(const CKey &k) const {
+        uint64_t x = (uint64_t)k.start * 0x9E3779B97F4A7C15ull ^ ((uint64_t)k.end + 0x632BE59BD9B4E019ull);
+        x ^= ((uint64_t)k.chrom << 32 | k.strand) * 0xD6E8FEB86659FD93ull;
+        return (size_t)(x ^ (x >> 29));
+    }
+};
+
+// Open-addressing CKey -> index table (linear probing, power-of-two capacity, load <= 1/2): one flat
+// array instead of a node per junction
+class CIndex {
+  public:
+    // the index of k, inserting v for a new key; second = inserted
+    std::pair<size_t, bool> try_emplace(const CKey &k, size_t v) {
+        if (2 * (n_ + 1) > slots_.size()) grow();
+        size_t i = CKeyHash()(k) & (slots_.size() - 1);
+        for (;; i = (i + 1) & (slots_.size() - 1)) {
+            Slot &s = slots_[i];
+            if (!s.used) { s.used = true; s.k = k; s.v = v; ++n_; return {v, true}; }
+            if (s.k == k) return {s.v, false};
+        }
+    }
+    const size_t *find(const CKey &k) const {
+        if (slots_.empty()) return nullptr;
+        for (size_t i = CKeyHash()(k) & (slots_.size() - 1);; i = (i + 1) & (slots_.size() - 1)) {
+            const Slot &s = slots_[i];
+            if (!s.used) return nullptr;
+            if (s.k == k) return &s.v;
+        }
+    }
+    size_t at(const CKey &k) const {
+        const size_t *p = find(k);
+        if (!p) throw std::out_of_range("CIndex::at");
+        return *p;
+    }
+  private:
+    struct Slot { CKey k; size_t v; bool used = false; };
+    std::vector<Slot> slots_;
+    size_t n_ = 0;
+    void grow() {
+        std::vector<Slot> old;
+        old.swap(slots_);
+        slots_.assign(old.empty() ? 1024 : 2 * old.size(), Slot{});
+        n_ = 0;
+        for (const Slot &s : old)
+            if (s.used) try_emplace(s.k, s.v);
+    }
+};
 
 struct Splice {                                // Splice (:766-806)
     int span = -1;                             // -1: a known site (junc_span None)
+    int64_t cid = -1;                          // interned chrom (fc2_caller::ids), -1: not yet
     std::string chrom, strand, gtag;
     int64_t start = 0, end = 0;
     int64_t dist = 0;
@@ -186,11 +242,29 @@ struct StrSet {
     size_t size() const { return big ? big->size() : v.size(); }
 };
 
+// Hit.uniq (:579-580, :590): the set of (read, rc(read)) of every spliced read; only
+// len(uniq) / 2 is read.  Stored as the set C of canonical forms min(read, rc(read)) plus the number
+// of palindromic members (read == rc(read)), so len(uniq) = 2|C| - palindromes exactly, with one
+// string per distinct read instead of two.
+struct CanonSet {
+    StrSet canon;
+    int64_t palindromes = 0;
+    void insert(const std::string &read, const std::string &rc) {
+        const bool pal = read == rc;
+        const std::string &c = pal || read < rc ? read : rc;
+        const size_t before = canon.size();
+        canon.insert(c);
+        if (pal && canon.size() != before) palindromes += 1;
+    }
+    int64_t size() const { return 2 * (int64_t)canon.size() - palindromes; }
+};
+
 struct Hit {                                   // Hit (:486-654)
     std::string name;
     Coord coord;
     int64_t n_reads = 0;
-    StrSet readnames, uniq;
+    StrSet readnames;
+    CanonSet uniq;
     bool has_mq = false;
     int64_t mq_a = 0, mq_b = 0;                // max of mapquals_A / _B
     double n_weighted = 0.;
@@ -243,9 +317,11 @@ struct fc2_caller {
     struct Storage {
         std::string prefix;
         std::deque<Hit> hits;                   // insertion (= dict) order; never relocated
-        std::unordered_map<std::string, size_t> index;
+        CIndex index;
         int64_t novel = 0;
     } st[2];                                    // 0 circ, 1 lin
+    std::unordered_map<std::string, uint32_t> ids;    // interned chromosome / strand strings (submit side)
+    std::vector<int64_t> tid_cid;                     // reference id -> interned chromosome (submit side)
     std::vector<std::pair<const char *, double>> N;   // the reference's counters, keyed by literal
                                                       // (merged by name into sorted keys on output)
     std::vector<std::pair<const char *, double>> N_in; // the same for the counters the next side bumps
@@ -266,6 +342,30 @@ void incN_into(std::vector<std::pair<const char *, double>> &N, const char *k, d
 void incN(fc2_caller *h, const char *k, double v = 1.) { incN_into(h->N, k, v); }
 // next side (process_mate)
 void incN_in(fc2_caller *h, const char *k, double v = 1.) { incN_into(h->N_in, k, v); }
+
+uint32_t intern(fc2_caller *h, const std::string &v) {
+    auto it = h->ids.find(v);
+    if (it != h->ids.end()) return it->second;
+    const uint32_t id = (uint32_t)h->ids.size();
+    h->ids.emplace(v, id);
+    return id;
+}
+
+uint32_t strand_id(fc2_caller *h, const std::string &strand) {
+    if (strand.size() == 1 && (strand[0] == '+' || strand[0] == '-')) return strand[0] == '-' ? 1u : 0u;
+    return 2u + intern(h, strand);
+}
+
+CKey coord_key(fc2_caller *h, const Coord &c) {
+    return CKey{std::get<1>(c), std::get<2>(c), intern(h, std::get<0>(c)), strand_id(h, std::get<3>(c))};
+}
+
+// the same key straight from a Splice (Splice.coord, :801-806), without building the tuple
+CKey coord_key(fc2_caller *h, const Splice &sp) {
+    const uint32_t c = sp.cid >= 0 ? (uint32_t)sp.cid : intern(h, sp.chrom);
+    return sp.start < sp.end ? CKey{sp.start, sp.end, c, strand_id(h, sp.strand)}
+                             : CKey{sp.end, sp.start, c, strand_id(h, sp.strand)};
+}
 
 // ---- Hit / SpliceSiteStorage ----------------------------------------------------------
 void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
@@ -296,8 +396,7 @@ void hit_add_read(fc2_caller *h, Hit &t, const Span &s, const Align &prim) {
     (void)h;
     t.has_tissue = true;
     t.tissue += s.weight;
-    t.uniq.insert(read);
-    t.uniq.insert(rc);
+    t.uniq.insert(read, rc);
 }
 
 Hit make_hit(fc2_caller *h, const std::string &name, const Splice &sp) {
@@ -310,8 +409,8 @@ Hit make_hit(fc2_caller *h, const std::string &name, const Splice &sp) {
 
 size_t storage_add(fc2_caller *h, int kind, const Splice &sp, const Align *prim) {
     auto &S = h->st[kind];
-    auto ins = S.index.try_emplace(coord_key(sp.coord()), S.hits.size());
-    const size_t k = ins.first->second;
+    const auto ins = S.index.try_emplace(coord_key(h, sp), S.hits.size());
+    const size_t k = ins.first;
     if (ins.second) {                           // a new junction: named by first appearance (:684-686)
         S.novel += 1;
         char nm[64];
@@ -395,7 +494,7 @@ void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :69
         col(std::get<3>(t.coord));
         col(py2_float(t.n_weighted));
         col(i2s(t.n_spanned));
-        col(i2s((int64_t)(t.uniq.size() / 2)));
+        col(i2s(t.uniq.size() / 2));
         col(py2_float(t.n_uniq_bridges));
         col(i2s(qa));
         col(i2s(qb));
@@ -460,15 +559,13 @@ uint64_t load_known(fc2_caller *h, int kind, const std::string &path) {
         sp.dist = 10;
         sp.ov = 10;
         sp.gtag = "NNNN";
-        const std::string key = coord_key(sp.coord());
+        const CKey key = coord_key(h, sp);
         Hit t = make_hit(h, fl[3], sp);
-        auto it = S.index.find(key);
-        if (it == S.index.end()) {              // a repeated coordinate keeps its first dict position
+        const auto ins = S.index.try_emplace(key, S.hits.size());
+        if (ins.second)                         // a repeated coordinate keeps its first dict position
             S.hits.push_back(std::move(t));
-            S.index[key] = S.hits.size() - 1;
-        } else {
-            S.hits[it->second] = std::move(t);
-        }
+        else
+            S.hits[ins.first] = std::move(t);
         ++n;
     }
     fclose(f);
@@ -598,6 +695,9 @@ Eval decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
     const Span &s = h->spans[si];
     const fc2_pair &pr = h->b_pairs[(size_t)s.eval];
     const std::string chrom = chrom_of(h, s.tid);
+    if ((size_t)s.tid >= h->tid_cid.size()) h->tid_cid.resize((size_t)s.tid + 1, -1);
+    int64_t &cid = h->tid_cid[(size_t)s.tid];
+    if (cid < 0) cid = intern(h, chrom);
     if (pr.flags & FC2_PAIR_SKIP) {            // chromosome missing from the genome (get_data, :193)
         ev.err = FC2_E_KEY;
         ev.msg = "KeyError: " + py_repr(chrom);
@@ -628,6 +728,7 @@ Eval decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
     Splice best;
     best.span = si;
     best.chrom = chrom;
+    best.cid = cid;
     coords(x, best.start, best.end);
     best.strand = (r.info & FC2_RES_MINUS) ? "-" : "+";
     best.gtag = best.strand == "-" ? rev_comp4(g) : g;
@@ -651,6 +752,7 @@ Eval decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
             Splice t;
             t.span = si;
             t.chrom = chrom;
+            t.cid = cid;
             coords(xx, t.start, t.end);
             t.strand = strand ? "-" : "+";
             int64_t ov = 0;
@@ -897,7 +999,7 @@ void record_hits(fc2_caller *h, Frag &fr, const Results &R, std::set<HitRef> &ju
     if (circ_coords.size() > 1) {
         for (const Coord &c : circ_coords) {
             warns.insert("WARN_MULTI_BACKSPLICE");
-            const size_t idx = h->st[0].index.at(coord_key(c));
+            const size_t idx = h->st[0].index.at(coord_key(h, c));
             add_flag(h->st[0].hits[idx], "WARN_MULTI_BACKSPLICE", fr.name);
             junctions.insert(HitRef(0, idx));
         }
