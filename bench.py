@@ -55,6 +55,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
     ap.add_argument("--no-strong", action="store_true", help="skip the configs[3] strong-scaling / ordered-merge run")
+    ap.add_argument("--no-config4", action="store_true", help="skip the configs[4] 200M x 120-150 bp run")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     return ap.parse_args()
@@ -354,6 +355,33 @@ def host_pipeline(opt, g, b, chunk: int = 4_000_000, reps: int = 3):
                     "C++ pack into pinned staging -> H2D -> scan -> D2H raw results, chunks of %d pairs, two per "
                     "side stream in flight (find_circ2_amd.pipeline, the CLI's evaluator); median of %d passes "
                     "over %d pairs" % (chunk, reps, n)}
+
+
+def configs4(opt, g, ws, rank, dev, steps, warmup, total=200_000_000):
+    """BASELINE configs[4]: 200M pairs of 120-150 bp reads (anchors of varying length, SURVEY.md 8(d)
+    config 5) over the ranks -- total fixed (strong scaling), each rank generates and scans its
+    share (seed per rank) on the resident hg19-shaped genome; value = 200M / max-over-ranks time.
+    At N = 1 the whole 200M-pair batch (14 GB of SoA) is scanned by one GPU."""
+    import torch
+    from find_circ2_amd import PairBatch, SynthConfig
+    n = total // ws + (1 if rank < total % ws else 0)
+    cfg = SynthConfig(seed=4242 + 7919 * rank, len_min=120, len_max=150, p_backsplice=1.0, p_planted=0.5,
+                      mut_rate=0.005, n_rate=0.0005, span_min=150, span_max=20000)
+    b = PairBatch.synthetic(opt, g, n, cfg)
+    elapsed, kms, out = timed_scans(opt, g, b, steps, warmup, ws, dev)
+    elapsed = max_over_ranks(elapsed, ws, dev)
+    kms = max_over_ranks(kms, ws, dev)
+    hits = int(((out.results[:n] & 0xFFFF) != 0xFFFF).sum())
+    del b, out
+    torch.cuda.empty_cache()
+    bpp = algo_bytes_per_pair(150, opt.asize, opt.margin)
+    return {"value": round(total * steps / elapsed, 1), "unit": "anchor-pairs/s", "scaling": "strong",
+            "ms_per_step": round(elapsed / steps * 1e3, 4), "kernel_ms_max_rank": round(kms, 4),
+            "pairs_total": total, "pairs_per_rank": n, "ranks": ws, "rank0_pairs_with_hit": hits,
+            "achieved_algo_GBs_per_rank_at_150bp": round(bpp * n / (kms * 1e-3) / 1e9, 1),
+            "note": "configs[4]: 200M pairs, read lengths uniform in 120..150 bp, split evenly over the ranks "
+                    "(each its own seeded share), hg19-shaped genome, read order; algorithmic bytes priced at "
+                    "150 bp (%d B/pair)" % bpp}
 
 
 def reorder_then_scan(opt, g, b, steps, dev, bpp):
@@ -787,6 +815,9 @@ def main():
     res = out.host(b.n)
     hits = int((res["best_x"] >= 0).sum())
     b._bench_ref_results = torch.from_numpy(res.view(np.int64).copy())
+    c4 = None
+    if args.workload == "hg19" and not args.no_config4 and not args.pairs:
+        c4 = configs4(opt, g, ws, rank, dev, args.steps, args.warmup)
     # configs[3]: the same stream strong-scaled over the ranks with the host-side ordered merge
     if args.no_strong:
         strong = None
@@ -826,6 +857,7 @@ def main():
                      "kernel": kernel_label(g, args.locus_ordered)},
         "cpu_baseline": None,
         "strong_scaling": strong,
+        "configs4_200M_150bp": c4,
     }
     if args.workload == "hg19" and not args.locus_ordered and b.n == 50_000_000:
         line["roofline"]["access_pattern_ceiling"] = pattern_ceiling(opt, g, b, dev)

@@ -31,6 +31,6 @@ for ch in (2_000_000, 4_000_000, 8_000_000):
 " > gpurun_out/host_pipe.log 2>&1 && echo PIPE_OK ;;
   rocprof)
     mkdir -p gpurun_out/prof_kt && export TMPDIR=/tmp && cd /tmp &&
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt/kt_hg19 -o kt --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra --no-strong > $R/gpurun_out/prof_kt/kt_hg19.out 2>&1 && echo PROF_OK ;;
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt/kt_hg19 -o kt --output-format csv -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra --no-strong --no-config4 > $R/gpurun_out/prof_kt/kt_hg19.out 2>&1 && echo PROF_OK ;;
   *) echo "usage: $0 bench|dist2|cli|pipeline|rocprof"; exit 2 ;;
 esac

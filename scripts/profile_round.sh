@@ -7,7 +7,7 @@ OUT=$R/gpurun_out/prof
 mkdir -p $OUT
 export TMPDIR=/tmp
 cd /tmp
-B="python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra --no-strong"
+B="python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-extra --no-strong --no-config4"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt_hg19 -o kt --output-format csv -- $B > $OUT/kt_hg19.out 2>&1
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch_hg19 -o pmc --output-format csv -- $B > $OUT/fetch_hg19.out 2>&1
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $OUT/write_hg19 -o pmc --output-format csv -- $B > $OUT/write_hg19.out 2>&1
