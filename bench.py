@@ -470,12 +470,19 @@ def strong_scaling(opt, g, sb, ref64, ws, rank, dev, steps, warmup):
     res = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
     subs = [(lo, hi, sb.sub(lo, hi)) for _, lo, hi in mine]
     stream = torch.cuda.current_stream(dev)
+    copier = torch.cuda.Stream(dev)              # D2H of batch k overlaps the scan of batch k+1
+    done = [torch.cuda.Event() for _ in subs]
 
     def step(copy: bool):
-        for lo, hi, s in subs:
+        for j, (lo, hi, s) in enumerate(subs):
             scan(opt, g, s, out=ScanOutput(res[lo:hi], None, s.tw, s.stride), stream=stream.cuda_stream)
             if copy:
-                merged.tensor[lo:hi].copy_(res[lo:hi], non_blocking=True)
+                done[j].record(stream)
+                copier.wait_event(done[j])
+                with torch.cuda.stream(copier):
+                    merged.tensor[lo:hi].copy_(res[lo:hi], non_blocking=True)
+        if copy:                                 # the next step's scans overwrite res
+            stream.wait_stream(copier)
 
     for _ in range(max(1, warmup)):
         step(True)
