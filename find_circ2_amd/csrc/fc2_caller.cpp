@@ -710,7 +710,8 @@ Eval decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
     }
     if (r.info & FC2_RES_ERR_WIN) {
         ev.err = FC2_E_FORMAT;
-        ev.msg = "BreakpointError: genome window outside get_data's defined range (find_circ.py:194-211)";
+        // numpy 1.x (Python 2): unequal-length `!=` gives the scalar True, whose .sum() fails (:861-863)
+        ev.msg = "AttributeError: 'bool' object has no attribute 'sum'";
         return ev;
     }
     if (r.best_x < 0) return ev;

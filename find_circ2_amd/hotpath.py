@@ -502,8 +502,17 @@ class Splice:
             self.chrom, self.start, self.end, self.strand, self.dist, self.ov, self.gtag, self.n_hits)
 
 
-class BreakpointError(RuntimeError):
-    pass
+# What find_breakpoints raises for windows outside the range where indexed_fasta.get_data is defined
+# (find_circ.py:194-211), when the spliced string and the internal read part differ in length: under
+# the reference's Python 2 / numpy 1.x, ``fromstring(a) != fromstring(b)`` of unequal lengths returns
+# the scalar True (a DeprecationWarning) and ``.sum()`` then fails (find_circ.py:861-863).  With -d 0
+# (simple_match, :865-871) nothing is raised.  The numpy version is not pinned by the reference, so
+# this parity is unpinned; the exception type and message follow numpy <= 1.16 (the last Python-2 one).
+WINDOW_SHAPE_MESSAGE = "'bool' object has no attribute 'sum'"
+
+
+class BreakpointError(AttributeError):
+    """The reference's AttributeError for windows of unexpected length (see WINDOW_SHAPE_MESSAGE)."""
 
 
 def first_tie_arrays(options: Options, host_pairs: np.ndarray, res: np.ndarray):
@@ -547,8 +556,7 @@ def raise_reference_errors(options: Options, host_pairs: np.ndarray, res: np.nda
     if info[i] & N.RES_ERR_KEY:
         raise KeyError("pair %d: splice signal with a byte outside ACGTN (reference KeyError in fast_4mer_RC, "
                        "find_circ.py:927)" % i)
-    raise BreakpointError("pair %d: genome window outside the range where indexed_fasta.get_data is defined "
-                          "(find_circ.py:194-211)" % i)
+    raise BreakpointError(WINDOW_SHAPE_MESSAGE)
 
 
 def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: ScanOutput,
@@ -580,8 +588,7 @@ def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: Scan
         span = spans[i] if spans is not None else None
         if evaluated[i] and (a["err_key"][i] or a["err_win"][i]):
             result.append(KeyError("splice signal with a byte outside ACGTN (find_circ.py:927)") if a["err_key"][i]
-                          else BreakpointError("genome window outside get_data's defined range "
-                                               "(find_circ.py:194-211)"))
+                          else BreakpointError(WINDOW_SHAPE_MESSAGE))
             continue
         if not a["hit"][i] or not evaluated[i]:
             result.append([])

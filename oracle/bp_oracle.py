@@ -76,7 +76,7 @@ class ReferenceKeyError(KeyError):
     """The reference would raise KeyError here (fatal, find_circ.py:1578-1583)."""
 
 
-class ReferenceShapeError(ValueError):
+class ReferenceShapeError(AttributeError):
     """The reference's numpy comparison would fail (window of wrong length)."""
 
 
@@ -269,7 +269,9 @@ class Hit:
 def _mismatches(a: bytes, b: bytes) -> int:
     """find_circ.py:861-863 -- numpy byte compare + sum."""
     if len(a) != len(b):
-        raise ReferenceShapeError("elementwise comparison of %d vs %d bytes" % (len(a), len(b)))
+        # numpy 1.x (Python 2): `!=` of unequal lengths returns the scalar True (DeprecationWarning),
+        # and True.sum() raises AttributeError (find_circ.py:861-863)
+        raise ReferenceShapeError("'bool' object has no attribute 'sum'")
     return int((np.frombuffer(a, dtype=np.int8) != np.frombuffer(b, dtype=np.int8)).sum())
 
 

@@ -6,7 +6,7 @@ without a GPU and (b) on a GPU box the outputs of the GPU evaluator can be
 compared file-for-file with this one.
 """
 import oracle
-from find_circ2_amd.hotpath import Splice
+from find_circ2_amd.hotpath import WINDOW_SHAPE_MESSAGE, BreakpointError, Splice
 
 
 def oracle_evaluator_factory(options, hp):
@@ -26,7 +26,7 @@ def oracle_evaluator_factory(options, hp):
             elif nt == -oracle.ORC_ERR_CHROM:
                 s.result = KeyError(s.chrom)
             elif nt < 0:
-                s.result = RuntimeError("shape")
+                s.result = BreakpointError(WINDOW_SHAPE_MESSAGE)
             else:
                 out = []
                 for t in r.ties_of(i):

@@ -108,7 +108,7 @@ def _expected(span, path, opt, fasta):
                                           opt.allhits))
     except KeyError:
         return KeyError
-    except ValueError:                       # ReferenceShapeError: windows outside get_data's range
+    except AttributeError:                   # ReferenceShapeError: windows outside get_data's range
         return "shape"
     if not opt.allhits:
         hits = hits[:1]
