@@ -146,3 +146,27 @@ def test_gpu_pipeline_readahead_many_chunks(tmp_path):
         assert rc1 == rc2
         if rc1 == 0:
             _compare(o1, o2)
+
+
+@pytest.mark.parametrize("gpus", ["1", "2"])
+def test_gpu_bam_out_equals_oracle(tmp_path, gpus):
+    """-B (the sequential loop: the BAM writer needs each chunk's verdicts before the next chunk's
+    records are written) through the HIP scan, on one or two scanners: the same
+    spliced_alignments.bam records and the same text files as the oracle run."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd import cli
+    from oracle_engine import oracle_evaluator_factory
+    from test_bam_out import read_bam
+    from test_ingest import same
+    from test_native_caller import _rich_sam
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 1500, seed=31)
+    o1, o2 = str(tmp_path / "oracle"), str(tmp_path / "gpu")
+    common = ["-G", fa, "-q", "-B", "--chunk-size", "13"]
+    assert cli.main(common + ["-o", o1, sam], evaluator_factory=oracle_evaluator_factory) == 0
+    assert cli.main(common + ["-o", o2, "--gpus", gpus, sam]) == 0
+    same(o1, o2)
+    b1 = read_bam(os.path.join(o1, "spliced_alignments.bam"))
+    b2 = read_bam(os.path.join(o2, "spliced_alignments.bam"))
+    assert len(b1[2]) > 1000 and b1 == b2
