@@ -17,6 +17,7 @@
 #include <tuple>
 #include <unordered_map>
 #include <unordered_set>
+#include <string_view>
 #include <utility>
 #include <vector>
 
@@ -79,12 +80,21 @@ char comp(char c) {
     }
 }
 
+struct CompTable {                             // comp() as a byte table
+    char t[256];
+    CompTable() { for (int c = 0; c < 256; ++c) t[c] = comp((char)c); }
+};
+const CompTable kComp;
+
 void rev_comp_into(const std::string &s, std::string &r) {
-    r.resize(s.size());
-    for (size_t k = 0; k < s.size(); ++k) {
-        const char c = comp(s[s.size() - 1 - k]);
-        if (!c) throw Fatal{FC2_E_KEY, std::string("KeyError: ") + py_repr(std::string(1, s[s.size() - 1 - k]))};
-        r[k] = c;
+    const size_t n = s.size();
+    r.resize(n);
+    const unsigned char *in = (const unsigned char *)s.data();
+    char *out = &r[0];
+    for (size_t k = 0; k < n; ++k) {
+        const char c = kComp.t[in[n - 1 - k]];
+        if (!c) throw Fatal{FC2_E_KEY, std::string("KeyError: ") + py_repr(std::string(1, (char)in[n - 1 - k]))};
+        out[k] = c;
     }
 }
 
@@ -95,26 +105,34 @@ std::string rev_comp(const std::string &s) {
 }
 
 // ---- data ----------------------------------------------------------------------
-struct Align {                                 // what record_hits and the writers read of an alignment
-    std::string qname, seq, qual;
-    bool has_seq = false, has_qual = false;
+struct APos {                                  // where an alignment sits (unspliced / broken segments)
     int32_t tid = -1;
     int64_t pos = -1, aend = -1;               // aend -1: None
     bool rev = false;
 };
 
-Align make_align(const Rec &r) {
-    Align a;
-    a.qname = r.qname;
-    a.seq = r.seq;
-    a.qual = r.qual;
-    a.has_seq = r.has_seq;
-    a.has_qual = r.has_qual;
+struct Align : APos {                          // a primary: what record_hits and the writers read of it
+    std::string qname, seq, qual;
+    bool has_seq = false, has_qual = false;
+};
+
+APos apos_of(const Rec &r) {
+    APos a;
     a.tid = r.tid;
     a.pos = r.pos;
     a.aend = r.aend;
     a.rev = r.reverse();
     return a;
+}
+
+// assign in place: a recycled Align keeps its strings' capacity (no allocation per fragment)
+void set_align(Align &a, const Rec &r) {
+    static_cast<APos &>(a) = apos_of(r);
+    a.qname.assign(r.qname);
+    a.seq.assign(r.seq);
+    a.qual.assign(r.qual);
+    a.has_seq = r.has_seq;
+    a.has_qual = r.has_qual;
 }
 
 struct Span {                                  // JunctionSpan (:821-852)
@@ -136,7 +154,7 @@ struct Frag {
     bool has[2] = {false, false};
     Align prim[2];
     std::vector<int> circ, lin;                // indices into the chunk's spans
-    std::vector<Align> unspliced, broken;
+    std::vector<APos> unspliced, broken;
 };
 
 using Coord = std::tuple<std::string, int64_t, int64_t, std::string>;   // (chrom, start, end, strand)
@@ -223,23 +241,58 @@ struct PyMin {
     std::string str() const { return is_bool ? (v ? "True" : "False") : i2s(v); }
 };
 
-// A set of strings of which only the size is read (Hit.readnames / Hit.uniq): a short vector
-// for the usual handful of members, a hash set past 16 (no per-hit hash table otherwise).
-struct StrSet {
-    std::vector<std::string> v;
-    std::unique_ptr<std::unordered_set<std::string>> big;
-    void insert(const std::string &s) {
-        if (big) { big->insert(s); return; }
-        for (const std::string &x : v)
-            if (x == s) return;
-        v.push_back(s);
-        if (v.size() > 16) {
-            big.reset(new std::unordered_set<std::string>(v.begin(), v.end()));
-            v.clear();
-            v.shrink_to_fit();
+// Append-only byte store for the strings the junction tables keep (read names, canonical reads,
+// flagged fragment names): one allocation per MiB instead of one per string; the bytes stay where
+// they are until the caller is closed, as the tables themselves do.
+class Arena {
+  public:
+    std::string_view put(const char *p, size_t n) {
+        if (blocks_.empty() || used_ + n > cap_) {
+            cap_ = std::max<size_t>(n, size_t(1) << 20);
+            blocks_.emplace_back(new char[cap_]);
+            used_ = 0;
         }
+        char *d = blocks_.back().get() + used_;
+        if (n) memcpy(d, p, n);
+        used_ += n;
+        return std::string_view(d, n);
     }
-    size_t size() const { return big ? big->size() : v.size(); }
+    std::string_view put(std::string_view v) { return put(v.data(), v.size()); }
+  private:
+    std::vector<std::unique_ptr<char[]>> blocks_;
+    size_t used_ = 0, cap_ = 0;
+};
+
+// A set of strings of which only the size is read (Hit.readnames / Hit.uniq): the first member
+// inline, a short vector up to 16, a hash set past that; members live in the Arena.
+struct StrSet {
+    std::string_view first;
+    size_t n = 0;
+    std::vector<std::string_view> more;
+    std::unique_ptr<std::unordered_set<std::string_view>> big;
+    bool contains(std::string_view s) const {
+        if (big) return big->count(s) != 0;
+        if (n && first == s) return true;
+        for (const std::string_view &x : more)
+            if (x == s) return true;
+        return false;
+    }
+    // true if s was new
+    bool insert(std::string_view s, Arena &a) {
+        if (contains(s)) return false;
+        const std::string_view v = a.put(s);
+        if (big) { big->insert(v); ++n; return true; }
+        if (!n) first = v;
+        else more.push_back(v);
+        if (++n > 16) {
+            big.reset(new std::unordered_set<std::string_view>(more.begin(), more.end()));
+            big->insert(first);
+            more.clear();
+            more.shrink_to_fit();
+        }
+        return true;
+    }
+    size_t size() const { return n; }
 };
 
 // Hit.uniq (:579-580, :590): the set of (read, rc(read)) of every spliced read; only
@@ -249,18 +302,59 @@ struct StrSet {
 struct CanonSet {
     StrSet canon;
     int64_t palindromes = 0;
-    void insert(const std::string &read, const std::string &rc) {
+    void insert(const std::string &read, const std::string &rc, Arena &a) {
         const bool pal = read == rc;
         const std::string &c = pal || read < rc ? read : rc;
-        const size_t before = canon.size();
-        canon.insert(c);
-        if (pal && canon.size() != before) palindromes += 1;
+        if (canon.insert(c, a) && pal) palindromes += 1;
     }
     int64_t size() const { return 2 * (int64_t)canon.size() - palindromes; }
 };
 
+// The flags record_hits attaches to a circ junction (find_circ.py:1319-1439), in sorted order:
+// sets of them print sorted (Python sorts / iterates these sets' sorted keys), so a bit mask
+// walked from bit 0 up gives the same order.
+enum Warn : uint32_t {
+    W_BROKEN_SEGMENTS, W_SUPPORT_CLOSURE, W_SUPPORT_INSIDE_MATE, W_SUPPORT_INSIDE_SPLICE_JUNCTION,
+    W_WARN_MULTI_BACKSPLICE, W_WARN_OTHER_CHROM_MATE, W_WARN_OUTSIDE_MATE, W_WARN_OUTSIDE_SPLICE_JUNCTION,
+    W_WARN_UNRESOLVED_EXTRA_BACKSPLICE, W_WARN_UNRESOLVED_LINSPLICE, kNumWarn
+};
+const char *const kWarnName[kNumWarn] = {
+    "BROKEN_SEGMENTS", "SUPPORT_CLOSURE", "SUPPORT_INSIDE_MATE", "SUPPORT_INSIDE_SPLICE_JUNCTION",
+    "WARN_MULTI_BACKSPLICE", "WARN_OTHER_CHROM_MATE", "WARN_OUTSIDE_MATE", "WARN_OUTSIDE_SPLICE_JUNCTION",
+    "WARN_UNRESOLVED_EXTRA_BACKSPLICE", "WARN_UNRESOLVED_LINSPLICE"};
+constexpr uint32_t kWarnNotWarn = (1u << W_BROKEN_SEGMENTS) | (1u << W_SUPPORT_CLOSURE) |
+                                  (1u << W_SUPPORT_INSIDE_MATE) | (1u << W_SUPPORT_INSIDE_SPLICE_JUNCTION);
+
+// Hit.read_flags: fragment name -> its set of flags (a mask); the first fragment inline
+struct FlagReads {
+    std::string_view first;
+    uint32_t first_mask = 0;
+    size_t n = 0;
+    std::unique_ptr<std::unordered_map<std::string_view, uint32_t>> more;
+    void add(const std::string &frag, uint32_t bit, Arena &a) {
+        if (n && first == frag) { first_mask |= bit; return; }
+        if (n && more) {
+            auto it = more->find(std::string_view(frag));
+            if (it != more->end()) { it->second |= bit; return; }
+        }
+        const std::string_view v = a.put(frag);
+        if (!n) { first = v; first_mask = bit; }
+        else {
+            if (!more) more.reset(new std::unordered_map<std::string_view, uint32_t>());
+            more->emplace(v, bit);
+        }
+        ++n;
+    }
+    template <class F> void each(F f) const {
+        if (n) f(first_mask);
+        if (more)
+            for (const auto &kv : *more) f(kv.second);
+    }
+};
+
 struct Hit {                                   // Hit (:486-654)
-    std::string name;
+    int64_t novel = 0;                         // > 0: named <name>_<prefix>_<novel:06d> (:684-686)
+    std::string known_name;                    // novel == 0: the name a known-sites file gave
     Coord coord;
     int64_t n_reads = 0;
     StrSet readnames;
@@ -272,10 +366,26 @@ struct Hit {                                   // Hit (:486-654)
     double n_uniq_bridges = 0.;
     PyMin edits, overlaps, n_hits;
     std::string signal = "NNNN", strandmatch = "NA";
-    std::map<std::string, int64_t> flags;
-    std::unordered_map<std::string, std::set<std::string>> read_flags;
+    int64_t flag_n[kNumWarn] = {};             // Hit.flags: count per flag (present iff > 0)
+    FlagReads read_flags;
     bool has_tissue = false;
     double tissue = 0.;
+};
+
+// Hits in insertion (= dict) order, in blocks that never move (references stay valid)
+class HitVec {
+  public:
+    size_t size() const { return n_; }
+    Hit &operator[](size_t k) { return blocks_[k >> kShift][k & (kBlock - 1)]; }
+    const Hit &operator[](size_t k) const { return blocks_[k >> kShift][k & (kBlock - 1)]; }
+    Hit &emplace_back() {
+        if ((n_ >> kShift) == blocks_.size()) blocks_.emplace_back(new Hit[kBlock]);
+        return (*this)[n_++];
+    }
+  private:
+    static constexpr size_t kShift = 10, kBlock = size_t(1) << kShift;
+    std::vector<std::unique_ptr<Hit[]>> blocks_;
+    size_t n_ = 0;
 };
 
 }  // namespace
@@ -292,12 +402,16 @@ struct fc2_caller {
     // process_mate, the pairs) into the bf_* fields, fc2_caller_submit records the oldest queued chunk
     // (record_hits, tables, writers) from the plain fields.  They share only the queue (mutex) and
     // read-only state (options, genome map, reference names); each side has its own counters.
-    std::vector<Frag> bf_frags;                 // the chunk being formed (next)
+    std::vector<Frag> bf_frags;                 // the chunk being formed (next): its first bf_nfrags
+    size_t bf_nfrags = 0;                       // entries (the rest are recycled objects)
     std::vector<Span> bf_spans;
     std::string bf_arena;                       // read_part bytes
     std::vector<uint64_t> bf_off;
     std::vector<fc2_pair> bf_pairs;
-    std::vector<Frag> frags;                    // the chunk being recorded (submit)
+    std::vector<int64_t> bf_starts, bf_ends;    // process_mate scratch
+    std::vector<size_t> bf_order;
+    std::vector<Frag> frags;                    // the chunk being recorded (submit): first nfrags
+    size_t nfrags = 0;
     std::vector<Span> spans;
     std::string arena;
     std::vector<uint64_t> b_off;
@@ -306,17 +420,23 @@ struct fc2_caller {
     // read ahead (form chunk k+1 while chunk k is on the GPU or being recorded)
     struct Chunk {
         std::vector<Frag> frags;
+        size_t nfrags = 0;
         std::vector<Span> spans;
         std::string arena;
         std::vector<uint64_t> b_off;
         std::vector<fc2_pair> b_pairs;
     };
     std::deque<Chunk> queued;
-    std::mutex qmu;
+    // recorded chunks handed back to the next side: their fragments' strings and vectors keep their
+    // capacity, so forming a chunk allocates nothing in steady state, and nothing allocated on one
+    // thread is freed on the other
+    std::vector<Chunk> spare;
+    std::mutex qmu;                             // guards queued and spare
     // aggregation
     struct Storage {
         std::string prefix;
-        std::deque<Hit> hits;                   // insertion (= dict) order; never relocated
+        HitVec hits;                            // insertion (= dict) order; never relocated
+        Arena strings;                          // the hits' read names, canonical reads, fragment names
         CIndex index;
         int64_t novel = 0;
     } st[2];                                    // 0 circ, 1 lin
@@ -326,6 +446,7 @@ struct fc2_caller {
                                                       // (merged by name into sorted keys on output)
     std::vector<std::pair<const char *, double>> N_in; // the same for the counters the next side bumps
     std::string out[3];                         // reads, multi, test text since the last take
+    std::string taken[3];                       // fc2_caller_take's buffers (valid until the next take)
     std::string rows_text;
     std::vector<std::pair<std::string, double>> counters_snapshot;
     uint64_t n_pairs = 0;
@@ -356,10 +477,6 @@ uint32_t strand_id(fc2_caller *h, const std::string &strand) {
     return 2u + intern(h, strand);
 }
 
-CKey coord_key(fc2_caller *h, const Coord &c) {
-    return CKey{std::get<1>(c), std::get<2>(c), intern(h, std::get<0>(c)), strand_id(h, std::get<3>(c))};
-}
-
 // the same key straight from a Splice (Splice.coord, :801-806), without building the tuple
 CKey coord_key(fc2_caller *h, const Splice &sp) {
     const uint32_t c = sp.cid >= 0 ? (uint32_t)sp.cid : intern(h, sp.chrom);
@@ -387,24 +504,36 @@ void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
 }
 
 // the span-dependent part of Hit.add that needs the fragment's primary
-void hit_add_read(fc2_caller *h, Hit &t, const Span &s, const Align &prim) {
-    t.readnames.insert(prim.qname);
+void hit_add_read(fc2_caller *h, int kind, Hit &t, const Span &s, const Align &prim) {
+    Arena &a = h->st[kind].strings;
+    t.readnames.insert(prim.qname, a);
     const std::string &read = prim.seq;
     static thread_local std::string rc;
     rev_comp_into(read, rc);
     t.n_reads += 1;
-    (void)h;
     t.has_tissue = true;
     t.tissue += s.weight;
-    t.uniq.insert(read, rc);
+    t.uniq.insert(read, rc, a);
 }
 
-Hit make_hit(fc2_caller *h, const std::string &name, const Splice &sp) {
-    Hit t;
-    t.name = name;
-    t.coord = sp.coord();
-    hit_add(h, t, sp);
-    return t;
+// the junction's name (find_circ.py:684-686), appended to out
+void hit_name(const fc2_caller *h, int kind, const Hit &t, std::string &out) {
+    if (!t.novel) { out += t.known_name; return; }
+    out += h->name;                             // name + "_%s_%06d" % (prefix, novel)
+    out += '_';
+    out += h->st[kind].prefix;
+    out += '_';
+    char d[24];
+    int n = 0;
+    for (uint64_t v = (uint64_t)t.novel; v; v /= 10) d[n++] = (char)('0' + v % 10);
+    while (n < 6) d[n++] = '0';
+    while (n) out += d[--n];
+}
+
+std::string hit_name(const fc2_caller *h, int kind, const Hit &t) {
+    std::string r;
+    hit_name(h, kind, t, r);
+    return r;
 }
 
 size_t storage_add(fc2_caller *h, int kind, const Splice &sp, const Align *prim) {
@@ -413,54 +542,52 @@ size_t storage_add(fc2_caller *h, int kind, const Splice &sp, const Align *prim)
     const size_t k = ins.first;
     if (ins.second) {                           // a new junction: named by first appearance (:684-686)
         S.novel += 1;
-        char nm[64];
-        snprintf(nm, sizeof nm, "_%s_%06lld", S.prefix.c_str(), (long long)S.novel);
         Hit &t = S.hits.emplace_back();
-        t.name = h->name + nm;
+        t.novel = S.novel;
         t.coord = sp.coord();
         hit_add(h, t, sp);
     } else {
         hit_add(h, S.hits[k], sp);
     }
-    if (sp.span >= 0) hit_add_read(h, S.hits[k], h->spans[sp.span], *prim);
+    if (sp.span >= 0) hit_add_read(h, kind, S.hits[k], h->spans[sp.span], *prim);
     return k;
 }
 
-void add_flag(Hit &t, const std::string &flag, const std::string &frag) {
-    t.flags[flag] += 1;
-    t.read_flags[frag].insert(flag);
+void add_flag(fc2_caller *h, Hit &t, uint32_t w, const std::string &frag) {
+    t.flag_n[w] += 1;
+    t.read_flags.add(frag, 1u << w, h->st[0].strings);
 }
 
-std::vector<std::string> categories(fc2_caller *h, const Hit &t) {   // :601-654
+// categories (:601-654) as literals, into cats[]; returns how many
+int categories(const fc2_caller *h, const Hit &t, const char *cats[8]) {
     const auto &o = h->o;
-    std::vector<std::string> cats;
-    if (t.signal != "GTAG") cats.push_back("NON_CANONICAL");
-    if (t.mq_a == 0 || t.mq_b == 0) cats.push_back("WARN_NON_UNIQUE_ANCHOR");
-    if (t.n_uniq_bridges == 0) cats.push_back("WARN_NO_UNIQ_BRIDGES");
-    if (t.n_hits.v > 1) cats.push_back("WARN_AMBIGUOUS_BP");
+    int n = 0;
+    if (t.signal != "GTAG") cats[n++] = "NON_CANONICAL";
+    if (t.mq_a == 0 || t.mq_b == 0) cats[n++] = "WARN_NON_UNIQUE_ANCHOR";
+    if (t.n_uniq_bridges == 0) cats[n++] = "WARN_NO_UNIQ_BRIDGES";
+    if (t.n_hits.v > 1) cats[n++] = "WARN_AMBIGUOUS_BP";
     const int64_t mov = t.overlaps.v, med = t.edits.v;
     if (mov == 0 && med == 0) {
     } else if (mov < 2 && med < 2) {
-        cats.push_back("WARN_EXT_1MM");
+        cats[n++] = "WARN_EXT_1MM";
     } else if (mov >= 2 || med >= 2) {
-        cats.push_back("WARN_EXT_2MM+");
+        cats[n++] = "WARN_EXT_2MM+";
     }
     const int64_t start = std::get<1>(t.coord), end = std::get<2>(t.coord);
-    if (end - start < o.short_threshold) cats.push_back("SHORT");
-    else if (end - start > o.huge_threshold) cats.push_back("HUGE");
+    if (end - start < o.short_threshold) cats[n++] = "SHORT";
+    else if (end - start > o.huge_threshold) cats[n++] = "HUGE";
     int64_t unbroken = 0, unwarned = 0;
     double total = 0.;
-    for (const auto &kv : t.read_flags) {
+    t.read_flags.each([&](uint32_t mask) {
         total += 1.;
-        if (!kv.second.count("BROKEN_SEGMENTS")) unbroken += 1;
-        for (const auto &w : kv.second)
-            if (w.compare(0, 4, "WARN") != 0) unwarned += 1;
-    }
+        if (!(mask & (1u << W_BROKEN_SEGMENTS))) unbroken += 1;
+        unwarned += __builtin_popcount(mask & kWarnNotWarn);
+    });
     if (total) {
-        if (!unbroken) cats.push_back("WARN_ALWAYS_BROKEN");
-        if (!unwarned) cats.push_back("WARN_ALWAYS_WARN");
+        if (!unbroken) cats[n++] = "WARN_ALWAYS_BROKEN";
+        if (!unwarned) cats[n++] = "WARN_ALWAYS_WARN";
     }
-    return cats;
+    return n;
 }
 
 std::string join(const std::vector<std::string> &v, const char *sep) {
@@ -472,9 +599,34 @@ std::string join(const std::vector<std::string> &v, const char *sep) {
     return r;
 }
 
+void app_int(std::string &out, int64_t v) {   // str(int)
+    char d[24];
+    int n = 0;
+    uint64_t u = v < 0 ? 0 - (uint64_t)v : (uint64_t)v;
+    do { d[n++] = (char)('0' + u % 10); u /= 10; } while (u);
+    if (v < 0) out += '-';
+    while (n) out += d[--n];
+}
+
+void app_py2_float(std::string &out, double v) {   // py2_float, integral values without snprintf
+    if (v == v && v > -1e12 && v < 1e12 && v == (double)(int64_t)v && !(v == 0 && signbit(v))) {
+        app_int(out, (int64_t)v);                  // '%.12g' of an integer below 1e12 is its digits
+        out += ".0";
+        return;
+    }
+    out += py2_float(v);
+}
+
+void app_pymin(std::string &out, const PyMin &m) {
+    if (m.is_bool) out += m.v ? "True" : "False";
+    else app_int(out, m.v);
+}
+
 void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :690-730
     const auto &o = h->o;
-    for (const Hit &t : h->st[kind].hits) {
+    const HitVec &hits = h->st[kind].hits;
+    for (size_t k = 0; k < hits.size(); ++k) {
+        const Hit &t = hits[k];
         if (!t.n_reads) continue;
         const int64_t qa = t.mq_a, qb = t.mq_b;
         if (o.halfunique) {
@@ -485,35 +637,46 @@ void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :69
         }
         if (t.n_uniq_bridges == 0 && !o.report_nobridges) { incN(h, "no_uniq_bridges"); continue; }
         // the 22 columns of find_circ.py:712-730, appended in place
-        auto col = [&](const std::string &v) { outs += v; outs += '\t'; };
-        col(std::get<0>(t.coord));
-        col(i2s(std::get<1>(t.coord)));
-        col(i2s(std::get<2>(t.coord)));
-        col(t.name);
-        col(i2s((int64_t)t.readnames.size()));
-        col(std::get<3>(t.coord));
-        col(py2_float(t.n_weighted));
-        col(i2s(t.n_spanned));
-        col(i2s(t.uniq.size() / 2));
-        col(py2_float(t.n_uniq_bridges));
-        col(i2s(qa));
-        col(i2s(qb));
-        col(t.has_tissue ? h->name : std::string());
-        col(t.has_tissue ? py2_float(t.tissue) : std::string());
-        col(t.edits.str());
-        col(t.overlaps.str());
-        col(t.n_hits.str());
-        col(t.signal);
-        col(t.strandmatch);
-        std::vector<std::string> cats = categories(h, t);
-        std::sort(cats.begin(), cats.end());
-        col(join(cats, ","));
-        if (!t.flags.empty()) {
+        const char tab = '\t';
+        outs += std::get<0>(t.coord); outs += tab;
+        app_int(outs, std::get<1>(t.coord)); outs += tab;
+        app_int(outs, std::get<2>(t.coord)); outs += tab;
+        hit_name(h, kind, t, outs); outs += tab;
+        app_int(outs, (int64_t)t.readnames.size()); outs += tab;
+        outs += std::get<3>(t.coord); outs += tab;
+        app_py2_float(outs, t.n_weighted); outs += tab;
+        app_int(outs, t.n_spanned); outs += tab;
+        app_int(outs, t.uniq.size() / 2); outs += tab;
+        app_py2_float(outs, t.n_uniq_bridges); outs += tab;
+        app_int(outs, qa); outs += tab;
+        app_int(outs, qb); outs += tab;
+        if (t.has_tissue) outs += h->name;
+        outs += tab;
+        if (t.has_tissue) app_py2_float(outs, t.tissue);
+        outs += tab;
+        app_pymin(outs, t.edits); outs += tab;
+        app_pymin(outs, t.overlaps); outs += tab;
+        app_pymin(outs, t.n_hits); outs += tab;
+        outs += t.signal; outs += tab;
+        outs += t.strandmatch; outs += tab;
+        const char *cats[8];
+        const int nc = categories(h, t, cats);
+        std::sort(cats, cats + nc, [](const char *x, const char *y) { return strcmp(x, y) < 0; });
+        for (int c = 0; c < nc; ++c) {
+            if (c) outs += ',';
+            outs += cats[c];
+        }
+        outs += tab;
+        bool any_flag = false;
+        for (uint32_t w = 0; w < kNumWarn; ++w) any_flag |= t.flag_n[w] > 0;
+        if (any_flag) {
             bool first = true;
-            for (const auto &kv : t.flags) { if (!first) outs += ','; outs += kv.first; first = false; }
-            outs += '\t';
+            for (uint32_t w = 0; w < kNumWarn; ++w)
+                if (t.flag_n[w]) { if (!first) outs += ','; outs += kWarnName[w]; first = false; }
+            outs += tab;
             first = true;
-            for (const auto &kv : t.flags) { if (!first) outs += ','; outs += i2s(kv.second); first = false; }
+            for (uint32_t w = 0; w < kNumWarn; ++w)
+                if (t.flag_n[w]) { if (!first) outs += ','; app_int(outs, t.flag_n[w]); first = false; }
         } else {
             outs += "N/A\t0";
         }
@@ -560,12 +723,13 @@ uint64_t load_known(fc2_caller *h, int kind, const std::string &path) {
         sp.ov = 10;
         sp.gtag = "NNNN";
         const CKey key = coord_key(h, sp);
-        Hit t = make_hit(h, fl[3], sp);
         const auto ins = S.index.try_emplace(key, S.hits.size());
-        if (ins.second)                         // a repeated coordinate keeps its first dict position
-            S.hits.push_back(std::move(t));
-        else
-            S.hits[ins.first] = std::move(t);
+        // a repeated coordinate keeps its first dict position, with the later line's Hit
+        Hit &t = ins.second ? S.hits.emplace_back() : S.hits[ins.first];
+        t = Hit();
+        t.known_name = fl[3];
+        t.coord = sp.coord();
+        hit_add(h, t, sp);
         ++n;
     }
     fclose(f);
@@ -593,23 +757,31 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
     const Rec &prim = m.recs[0];
     if (m.proper.size() < 2) {
         incN_in(h, "unspliced_mates");
-        fr.unspliced.push_back(make_align(prim));
+        fr.unspliced.push_back(apos_of(prim));
         return;
     }
     if (!prim.has_seq) throw Fatal{FC2_E_FORMAT, kNoneLen};      // L = len(mate.full_seq)
     const int64_t L = (int64_t)prim.seq.size();
     const size_t n = m.proper.size();
     const double weight = 1. / ((double)n - 1.);
-    std::vector<int64_t> starts(n), ends(n);
+    std::vector<int64_t> &starts = h->bf_starts, &ends = h->bf_ends;
+    std::vector<size_t> &order = h->bf_order;
+    starts.resize(n);
+    ends.resize(n);
+    order.resize(n);
     for (size_t k = 0; k < n; ++k) {
         const Rec &s = m.recs[m.proper[k]];
         if (s.qlen < 0) throw Fatal{FC2_E_FORMAT, kNoneLen};     // len(s.query)
         starts[k] = s.astart;
         ends[k] = s.astart + s.qlen;
+        order[k] = k;
     }
-    std::vector<size_t> order(n);
-    for (size_t k = 0; k < n; ++k) order[k] = k;
-    std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return starts[a] < starts[b]; });
+    for (size_t i = 1; i < n; ++i) {           // stable insertion sort by query start (n is small)
+        const size_t v = order[i];
+        size_t j = i;
+        while (j > 0 && starts[order[j - 1]] > starts[v]) { order[j] = order[j - 1]; --j; }
+        order[j] = v;
+    }
     int64_t min_s = L, max_e = 0;
     for (size_t k = 0; k + 1 < n; ++k) {
         const size_t a = order[k], b = order[k + 1];
@@ -645,30 +817,36 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
     }
     if (max_e < L - h->o.asize || min_s > h->o.asize) {
         for (size_t k = 1; k < m.recs.size(); ++k)
-            if (m.recs[k].tid != prim.tid) fr.broken.push_back(make_align(m.recs[k]));
+            if (m.recs[k].tid != prim.tid) fr.broken.push_back(apos_of(m.recs[k]));
         for (size_t k = 1; k < m.recs.size(); ++k)
             if (m.recs[k].tid == prim.tid && m.recs[k].reverse() != prim.reverse())
-                fr.broken.push_back(make_align(m.recs[k]));
+                fr.broken.push_back(apos_of(m.recs[k]));
     }
 }
 
 int on_fragment(fc2_caller *h, const Mate *m1, const Mate *m2) {
-    Frag fr;
-    fr.name = m2->recs[0].qname;               // Fragment(mate2.primary.qname, ...)
+    // the next slot of the chunk; a recycled Frag is reset field by field (capacity kept)
+    if (h->bf_nfrags == h->bf_frags.size()) h->bf_frags.emplace_back();
+    Frag &fr = h->bf_frags[h->bf_nfrags];
+    fr.name.assign(m2->recs[0].qname);          // Fragment(mate2.primary.qname, ...)
+    fr.circ.clear();
+    fr.lin.clear();
+    fr.unspliced.clear();
+    fr.broken.clear();
     const Mate *ms[2] = {m1, m2};
     const size_t span0 = h->bf_spans.size(), arena0 = h->bf_arena.size();
     for (int k = 0; k < 2; ++k) {
+        fr.has[k] = ms[k] != nullptr;
         if (!ms[k]) continue;
-        fr.has[k] = true;
-        fr.prim[k] = make_align(ms[k]->recs[0]);
+        set_align(fr.prim[k], ms[k]->recs[0]);
         process_mate(h, *ms[k], k, fr);
     }
     if ((fr.circ.empty() && h->o.nolinear) || (fr.circ.empty() && fr.lin.empty())) {
         h->bf_spans.resize(span0);                // not pending: its spans are never evaluated
         h->bf_arena.resize(arena0);
-        return FC2_OK;
+        return FC2_OK;                            // the slot is reused by the next fragment
     }
-    h->bf_frags.push_back(std::move(fr));
+    ++h->bf_nfrags;
     return FC2_OK;
 }
 
@@ -690,8 +868,12 @@ int score_of(const fc2_caller *h, const std::string &sig, int64_t dist, int64_t 
     return (int)sc;
 }
 
-Eval decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask, uint32_t tw, uint64_t stride) {
-    Eval ev;
+// fills ev (a reused scratch object: its vectors keep their capacity)
+void decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask, uint32_t tw, uint64_t stride,
+            Eval &ev) {
+    ev.err = 0;
+    ev.msg.clear();
+    ev.ties.clear();
     const Span &s = h->spans[si];
     const fc2_pair &pr = h->b_pairs[(size_t)s.eval];
     const std::string chrom = chrom_of(h, s.tid);
@@ -701,20 +883,20 @@ Eval decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
     if (pr.flags & FC2_PAIR_SKIP) {            // chromosome missing from the genome (get_data, :193)
         ev.err = FC2_E_KEY;
         ev.msg = "KeyError: " + py_repr(chrom);
-        return ev;
+        return;
     }
     if (r.info & FC2_RES_ERR_KEY) {
         ev.err = FC2_E_KEY;
         ev.msg = "KeyError: splice signal with a byte outside ACGTN (find_circ.py:927)";
-        return ev;
+        return;
     }
     if (r.info & FC2_RES_ERR_WIN) {
         ev.err = FC2_E_FORMAT;
         // numpy 1.x (Python 2): unequal-length `!=` gives the scalar True, whose .sum() fails (:861-863)
         ev.msg = "AttributeError: 'bool' object has no attribute 'sum'";
-        return ev;
+        return;
     }
-    if (r.best_x < 0) return ev;
+    if (r.best_x < 0) return;
     const int64_t e = h->o.asize - h->o.margin;
     const int64_t L = pr.read_len, l = L - 2 * e, x = r.best_x;
     const bool bs = pr.flags & FC2_PAIR_BACKSPLICE, prim_rev = pr.flags & FC2_PAIR_PRIMARY_REV;
@@ -741,7 +923,7 @@ Eval decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
     const int best_score = score_of(h, best.gtag, r.dist, r.ov, best.strand, prim_rev);
     if (!(h->o.allhits && r.n_ties > 1)) {
         ev.ties.push_back(best);
-        return ev;
+        return;
     }
     // all ties in (x asc, '+' before '-') order from the tie mask (hotpath._expand_ties)
     const uint32_t half = tw / 2;
@@ -805,7 +987,6 @@ Eval decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
             ev.ties.push_back(t);
         }
     }
-    return ev;
 }
 
 
@@ -933,11 +1114,10 @@ std::string test_row(fc2_caller *h, const Frag &fr, const std::set<Coord> &lin_c
 std::string multi_row(fc2_caller *h, const Frag &fr, const Hit &circ, const std::set<Coord> &lin_cons,
                       const std::set<Coord> &lin_incons, const std::set<UCoord> &un_cons,
                       const std::set<UCoord> &un_incons) {                    // :733-763
-    (void)h;
     const int64_t score = (int64_t)lin_cons.size() - 10 * (int64_t)lin_incons.size() + (int64_t)un_cons.size() -
                           10 * (int64_t)un_incons.size();
     std::vector<std::string> cols = {std::get<0>(circ.coord), i2s(std::get<1>(circ.coord)),
-                                     i2s(std::get<2>(circ.coord)), "ME:" + circ.name, i2s(score),
+                                     i2s(std::get<2>(circ.coord)), "ME:" + hit_name(h, 0, circ), i2s(score),
                                      std::get<3>(circ.coord), fr.name};
     std::vector<std::string> v;
     for (const Coord &c : lin_cons) v.push_back(i2s(std::get<1>(c)) + "-" + i2s(std::get<2>(c)));
@@ -963,29 +1143,58 @@ struct Results {
     uint64_t stride;
 };
 
-const std::vector<Splice> &find_breakpoints(fc2_caller *h, int si, const Results &R,
-                                            std::unordered_map<int, Eval> &cache) {
-    auto it = cache.find(si);
-    if (it == cache.end()) it = cache.emplace(si, decode(h, si, R.res[h->spans[si].eval], R.tiemask, R.tw, R.stride)).first;
-    if (it->second.err) throw Fatal{it->second.err, it->second.msg};
-    return it->second.ties;
+// record_hits' per-fragment scratch (find_circ.py:1276-1439): reused objects, so recording a
+// fragment allocates nothing beyond what the junction tables keep
+struct FragScratch {
+    std::vector<int> ev_si;                     // find_breakpoints' results of this fragment, by span
+    std::vector<Eval> evs;
+    size_t n_ev = 0;
+    std::vector<size_t> circ_idx, lin_idx;      // distinct circ / linear junctions (their coords)
+    std::vector<std::pair<int, size_t>> junc;   // every junction the fragment's reads support
+    uint32_t warns = 0;                         // Warn bits
+    std::vector<std::string> names;             // write_read
+    void reset() { n_ev = 0; circ_idx.clear(); lin_idx.clear(); junc.clear(); warns = 0; }
+};
+
+const std::vector<Splice> &find_breakpoints(fc2_caller *h, int si, const Results &R, FragScratch &F) {
+    size_t k = 0;
+    while (k < F.n_ev && F.ev_si[k] != si) ++k;
+    if (k == F.n_ev) {                          // first evaluation of this span in the fragment
+        if (F.n_ev == F.evs.size()) { F.evs.emplace_back(); F.ev_si.push_back(0); }
+        F.ev_si[k] = si;
+        decode(h, si, R.res[h->spans[si].eval], R.tiemask, R.tw, R.stride, F.evs[k]);
+        ++F.n_ev;
+    }
+    const Eval &ev = F.evs[k];
+    if (ev.err) throw Fatal{ev.err, ev.msg};
+    return ev.ties;
 }
 
 using HitRef = std::pair<int, size_t>;          // (storage, index)
 
-void record_hits(fc2_caller *h, Frag &fr, const Results &R, std::set<HitRef> &junctions,
-                 std::set<std::string> &warns) {
+void add_unique(std::vector<size_t> &v, size_t x) {
+    for (size_t y : v)
+        if (y == x) return;
+    v.push_back(x);
+}
+
+void add_unique(std::vector<HitRef> &v, const HitRef &x) {
+    for (const HitRef &y : v)
+        if (y == x) return;
+    v.push_back(x);
+}
+
+void record_hits(fc2_caller *h, Frag &fr, const Results &R, FragScratch &F) {
     const auto &o = h->o;
-    std::unordered_map<int, Eval> cache;
-    std::set<Coord> circ_coords;
+    F.reset();
     HitRef circ{-1, 0};
     for (int si : fr.circ) {
         const Span &span = h->spans[si];
         if (!(span.uniq >= o.min_uniq_qual)) { incN(h, "circ_junc_not_unique"); continue; }
-        const std::vector<Splice> &splices = find_breakpoints(h, si, R, cache);
+        const std::vector<Splice> &splices = find_breakpoints(h, si, R, F);
         if (splices.empty()) {
             incN(h, "circ_no_bp");
-            warns.insert("WARN_UNRESOLVED_EXTRA_BACKSPLICE");
+            F.warns |= 1u << W_WARN_UNRESOLVED_EXTRA_BACKSPLICE;
             continue;
         }
         incN(h, "circ_spliced");
@@ -993,37 +1202,36 @@ void record_hits(fc2_caller *h, Frag &fr, const Results &R, std::set<HitRef> &ju
         for (size_t k = 0; k < n; ++k) {
             const size_t idx = storage_add(h, 0, splices[k], &fr.prim[span.mate]);
             circ = HitRef(0, idx);
-            circ_coords.insert(h->st[0].hits[idx].coord);
-            junctions.insert(circ);
+            add_unique(F.circ_idx, idx);        // circ_coords: one coordinate per junction
+            add_unique(F.junc, circ);
         }
     }
-    if (circ_coords.size() > 1) {
-        for (const Coord &c : circ_coords) {
-            warns.insert("WARN_MULTI_BACKSPLICE");
-            const size_t idx = h->st[0].index.at(coord_key(h, c));
-            add_flag(h->st[0].hits[idx], "WARN_MULTI_BACKSPLICE", fr.name);
-            junctions.insert(HitRef(0, idx));
+    if (F.circ_idx.size() > 1) {
+        for (size_t idx : F.circ_idx) {
+            F.warns |= 1u << W_WARN_MULTI_BACKSPLICE;
+            add_flag(h, h->st[0].hits[idx], W_WARN_MULTI_BACKSPLICE, fr.name);
+            add_unique(F.junc, HitRef(0, idx));
         }
         return;
     }
-    if (circ_coords.empty() && o.nolinear) return;
+    if (F.circ_idx.empty() && o.nolinear) return;
     int64_t circ_start = 0, circ_end = 0;
     int circ_span = -1;
-    if (!circ_coords.empty()) {
+    if (!F.circ_idx.empty()) {
         const Coord &cc = h->st[0].hits[circ.second].coord;
         circ_start = std::get<1>(cc);
         circ_end = std::get<2>(cc);
         circ_span = fr.circ[0];
-        if (fr.circ.size() > 1) warns.insert("SUPPORT_CLOSURE");
+        if (fr.circ.size() > 1) F.warns |= 1u << W_SUPPORT_CLOSURE;
     }
-    std::set<Coord> lin_cons, lin_incons, lin_coords;
+    std::set<Coord> lin_cons, lin_incons;
     for (int si : fr.lin) {
         const Span &span = h->spans[si];
         if (!(span.uniq >= o.min_uniq_qual)) { incN(h, "lin_junc_not_unique"); continue; }
-        const std::vector<Splice> &splices = find_breakpoints(h, si, R, cache);
+        const std::vector<Splice> &splices = find_breakpoints(h, si, R, F);
         if (splices.empty()) {
             incN(h, "lin_no_bp");
-            warns.insert("WARN_UNRESOLVED_LINSPLICE");
+            F.warns |= 1u << W_WARN_UNRESOLVED_LINSPLICE;
             continue;
         }
         incN(h, "lin_spliced");
@@ -1031,66 +1239,88 @@ void record_hits(fc2_caller *h, Frag &fr, const Results &R, std::set<HitRef> &ju
         for (size_t k = 0; k < n; ++k) {
             const Splice &sp = splices[k];
             const size_t idx = storage_add(h, 1, sp, &fr.prim[span.mate]);
-            junctions.insert(HitRef(1, idx));
-            lin_coords.insert(h->st[1].hits[idx].coord);
-            if (!circ_coords.empty()) {
+            add_unique(F.junc, HitRef(1, idx));
+            if (o.test) add_unique(F.lin_idx, idx);
+            if (!F.circ_idx.empty()) {
                 if (sp.start <= circ_start || sp.end >= circ_end) {
-                    warns.insert("WARN_OUTSIDE_SPLICE_JUNCTION");
+                    F.warns |= 1u << W_WARN_OUTSIDE_SPLICE_JUNCTION;
                     lin_incons.insert(sp.coord());
                 } else {
                     lin_cons.insert(sp.coord());
-                    warns.insert("SUPPORT_INSIDE_SPLICE_JUNCTION");
+                    F.warns |= 1u << W_SUPPORT_INSIDE_SPLICE_JUNCTION;
                 }
             }
         }
     }
     if (o.test) {
-        auto coords = [&](const Align &a) {
+        auto coords = [&](const APos &a) {
             const std::string s = o.stranded ? (a.rev ? "-" : "+") : "*";
             return UCoord{chrom_of(h, a.tid), a.pos, a.aend < 0 ? kNone : a.aend, s};
         };
         std::vector<UCoord> un, br;
-        for (const Align &a : fr.unspliced) un.push_back(coords(a));
-        for (const Align &a : fr.broken) br.push_back(coords(a));
+        for (const APos &a : fr.unspliced) un.push_back(coords(a));
+        for (const APos &a : fr.broken) br.push_back(coords(a));
+        std::set<Coord> lin_coords, circ_coords;
+        for (size_t idx : F.lin_idx) lin_coords.insert(h->st[1].hits[idx].coord);
+        for (size_t idx : F.circ_idx) circ_coords.insert(h->st[0].hits[idx].coord);
         h->out[2] += test_row(h, fr, lin_coords, circ_coords, un, br);
     }
-    if (!circ_coords.empty()) {
+    if (!F.circ_idx.empty()) {
         std::set<UCoord> un_cons, un_incons;
         const int32_t circ_tid = fr.prim[h->spans[circ_span].mate].tid;
-        for (const Align &a : fr.unspliced) {
+        for (const APos &a : fr.unspliced) {
             const UCoord c{chrom_of(h, a.tid), a.pos, a.aend < 0 ? kNone : a.aend, "*"};
             if (circ_tid != a.tid) {
-                warns.insert("WARN_OTHER_CHROM_MATE");
+                F.warns |= 1u << W_WARN_OTHER_CHROM_MATE;
                 un_incons.insert(c);
             } else if (a.pos + o.asize <= circ_start || need_int(c.aend) - o.asize >= circ_end) {
-                warns.insert("WARN_OUTSIDE_MATE");
+                F.warns |= 1u << W_WARN_OUTSIDE_MATE;
                 un_incons.insert(c);
             } else {
-                warns.insert("SUPPORT_INSIDE_MATE");
+                F.warns |= 1u << W_SUPPORT_INSIDE_MATE;
                 un_cons.insert(c);
             }
         }
-        if (!fr.broken.empty()) warns.insert("BROKEN_SEGMENTS");
+        if (!fr.broken.empty()) F.warns |= 1u << W_BROKEN_SEGMENTS;
         if ((!un_cons.empty() || !un_incons.empty() || !lin_cons.empty() || !lin_incons.empty()) && o.multi_events &&
             o.write_multi)
             h->out[1] += multi_row(h, fr, h->st[0].hits[circ.second], lin_cons, lin_incons, un_cons, un_incons);
-        for (const std::string &w : warns) add_flag(h->st[0].hits[circ.second], w, fr.name);
+        for (uint32_t w = 0; w < kNumWarn; ++w)
+            if (F.warns & (1u << w)) add_flag(h, h->st[0].hits[circ.second], w, fr.name);
     }
 }
 
-void write_read(fc2_caller *h, const Align &m, const std::set<HitRef> &junctions,
-                const std::set<std::string> &flags) {                          // :1442-1447
+void write_read(fc2_caller *h, const Align &m, FragScratch &F) {       // :1442-1447
     if (!h->o.write_reads) return;
-    std::vector<std::string> names;
-    for (const HitRef &j : junctions) names.push_back(h->st[j.first].hits[j.second].name);
-    std::sort(names.begin(), names.end());
-    const std::string name = m.qname + " " + join(names, ",") + " " +
-                             join(std::vector<std::string>(flags.begin(), flags.end()), ",");
+    // '@<qname> <sorted junction names> <sorted flags>' , seq, '+' + the same name, qual
+    const size_t nj = F.junc.size();
+    if (F.names.size() < nj) F.names.resize(nj);
+    for (size_t k = 0; k < nj; ++k) {
+        F.names[k].clear();
+        hit_name(h, F.junc[k].first, h->st[F.junc[k].first].hits[F.junc[k].second], F.names[k]);
+    }
+    if (nj > 1) std::sort(F.names.begin(), F.names.begin() + (std::ptrdiff_t)nj);
     std::string &o = h->out[0];
-    o += '@'; o += name; o += '\n';
-    o += m.has_seq ? m.seq : std::string("None"); o += "\n+";
-    o += name; o += '\n';
-    o += m.has_qual ? m.qual : std::string("None"); o += '\n';
+    o += '@';
+    const size_t n0 = o.size();
+    o += m.qname;
+    o += ' ';
+    for (size_t k = 0; k < nj; ++k) {
+        if (k) o += ',';
+        o += F.names[k];
+    }
+    o += ' ';
+    bool first = true;
+    for (uint32_t w = 0; w < kNumWarn; ++w)
+        if (F.warns & (1u << w)) { if (!first) o += ','; o += kWarnName[w]; first = false; }
+    const size_t n1 = o.size();
+    o += '\n';
+    o += m.has_seq ? m.seq : std::string("None");
+    o += "\n+";
+    o.append(o, n0, n1 - n0);
+    o += '\n';
+    o += m.has_qual ? m.qual : std::string("None");
+    o += '\n';
 }
 
 }  // namespace
@@ -1152,7 +1382,19 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         if (h->queued.size() >= FC2_CALLER_MAX_QUEUED)
             return fc2::fail(FC2_E_PARAM, "fc2_caller_next: too many chunks not submitted");
     }
-    h->bf_frags.clear();
+    {
+        std::lock_guard<std::mutex> lk(h->qmu);
+        if (!h->spare.empty()) {                   // a recorded chunk's buffers (see fc2_caller::spare)
+            fc2_caller::Chunk &c = h->spare.back();
+            h->bf_frags.swap(c.frags);
+            h->bf_spans.swap(c.spans);
+            h->bf_arena.swap(c.arena);
+            h->bf_off.swap(c.b_off);
+            h->bf_pairs.swap(c.b_pairs);
+            h->spare.pop_back();
+        }
+    }
+    h->bf_nfrags = 0;
     h->bf_spans.clear();
     h->bf_arena.clear();
     h->bf_off.clear();
@@ -1166,14 +1408,15 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             return f.code ? f.code : FC2_E_FORMAT;
         }
     };
-    while (!h->eof && h->bf_frags.size() < h->o.chunksize) {
+    while (!h->eof && h->bf_nfrags < h->o.chunksize) {
         int e = 0;
         const int rc = fc2::ing::pull(h->ing, &h->ip, h->o.chunksize, sink, &e);
         if (rc) return err.code ? fc2::fail(err.code, err.msg) : rc;
         h->eof = e != 0;
     }
     // the spans record_hits will evaluate, in fragment order (Caller._flush)
-    for (const Frag &fr : h->bf_frags) {
+    for (size_t f = 0; f < h->bf_nfrags; ++f) {
+        const Frag &fr = h->bf_frags[f];
         for (int pass = 0; pass < 2; ++pass) {
             for (int si : pass ? fr.lin : fr.circ) {
                 Span &s = h->bf_spans[si];
@@ -1203,6 +1446,8 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     h->bf_arena.append(16, '\0');                 // readers of the batch may load whole words past the end
     fc2_caller::Chunk c;
     c.frags.swap(h->bf_frags);
+    c.nfrags = h->bf_nfrags;
+    h->bf_nfrags = 0;
     c.spans.swap(h->bf_spans);
     c.arena.swap(h->bf_arena);
     c.b_off.swap(h->bf_off);
@@ -1233,6 +1478,7 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
             return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: no chunk handed out by fc2_caller_next");
         fc2_caller::Chunk &c = h->queued.front();
         h->frags.swap(c.frags);
+        h->nfrags = c.nfrags;
         h->spans.swap(c.spans);
         h->arena.swap(c.arena);
         h->b_off.swap(c.b_off);
@@ -1243,30 +1489,41 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
     if (h->o.allhits && !h->b_pairs.empty() && (!tiemask || tw < 2 || stride < h->b_pairs.size()))
         return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: --all-hits needs the tie mask");
     const Results R{results, tiemask, tw, stride};
+    int rc = FC2_OK;
     try {
-        for (Frag &fr : h->frags) {
-            std::set<HitRef> junctions;
-            std::set<std::string> warns;
-            record_hits(h, fr, R, junctions, warns);
-            if (!junctions.empty()) {
-                if (fr.has[0]) write_read(h, fr.prim[0], junctions, warns);
-                if (fr.has[1]) write_read(h, fr.prim[1], junctions, warns);
+        static thread_local FragScratch F;
+        for (size_t f = 0; f < h->nfrags; ++f) {
+            Frag &fr = h->frags[f];
+            record_hits(h, fr, R, F);
+            if (!F.junc.empty()) {
+                if (fr.has[0]) write_read(h, fr.prim[0], F);
+                if (fr.has[1]) write_read(h, fr.prim[1], F);
             }
         }
     } catch (const Fatal &f) {
-        h->frags.clear();
-        return fc2::fail(f.code, f.msg);
+        rc = fc2::fail(f.code, f.msg);
     }
-    h->frags.clear();
-    return FC2_OK;
+    // hand the chunk's buffers back to the next side (fc2_caller::spare)
+    fc2_caller::Chunk c;
+    c.frags.swap(h->frags);
+    c.spans.swap(h->spans);
+    c.arena.swap(h->arena);
+    c.b_off.swap(h->b_off);
+    c.b_pairs.swap(h->b_pairs);
+    h->nfrags = 0;
+    std::lock_guard<std::mutex> lk(h->qmu);
+    if (h->spare.size() < 4) h->spare.push_back(std::move(c));
+    return rc;
 }
 
 extern "C" int fc2_caller_take(fc2_caller *h, int stream, const char **text, uint64_t *len) {
     if (!h || stream < 0 || stream > 2 || !text || !len) return fc2::fail(FC2_E_PARAM, "fc2_caller_take: bad arguments");
-    h->rows_text.swap(h->out[stream]);
+    // each stream has its own hand-out buffer, so both keep their capacity (no regrowth per chunk)
+    std::string &t = h->taken[stream];
+    t.swap(h->out[stream]);
     h->out[stream].clear();
-    *text = h->rows_text.c_str();
-    *len = h->rows_text.size();
+    *text = t.c_str();
+    *len = t.size();
     return FC2_OK;
 }
 

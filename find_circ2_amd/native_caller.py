@@ -273,10 +273,13 @@ class NativeCaller:
         eof = False
         deferred = None                      # an error of fc2_caller_next, raised after the queued chunks
         eof_c = ctypes.c_int(0)
+        prof = self.loop_profile = {"next_s": 0.0, "submit_s": 0.0, "write_s": 0.0}
         while True:
             while not eof and deferred is None and len(queue) < depth:
                 batch = N.CallerBatch()
+                tn = time.perf_counter()
                 rc = L.fc2_caller_next(self.h, ctypes.byref(batch), ctypes.byref(eof_c))
+                prof["next_s"] += time.perf_counter() - tn
                 if rc != N.FC2_OK:
                     try:
                         _raise_native(rc)
@@ -312,8 +315,12 @@ class NativeCaller:
                     tm = np.ascontiguousarray(tm, dtype=np.uint64)
                     tw = tm.shape[0]
                     tm_ptr = tm.ctypes.data
+            ts = time.perf_counter()
             rc = L.fc2_caller_submit(self.h, res_ptr, tm_ptr, tw, n)
+            tw_ = time.perf_counter()
             self._write_outputs(outputs)        # what record_hits wrote before any failure
+            prof["submit_s"] += tw_ - ts
+            prof["write_s"] += time.perf_counter() - tw_
             if rc != N.FC2_OK:
                 _raise_native(rc)
             if throughput:
@@ -330,6 +337,7 @@ class NativeCaller:
             raise deferred
         if throughput:
             stderr.write('\n')
+        prof["eval_s"] = eval_s
         nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
         L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
         return time.time() - t0, int(nr.value), int(npairs.value), eval_s

@@ -1,0 +1,87 @@
+// sampler.c -- a tiny in-process PC sampler for host-side profiling (dev tool; no perf in the image).
+// Loaded with ctypes (never preloaded): sampler_start(usec) arms a CLOCK_MONOTONIC timer that raises
+// SIGPROF; the handler records the interrupted PC while sampler_phase(tag > 0) is set.  sampler_stop
+// writes "tag pc object base symbol" lines (dladdr) for scripts/prof/report.py to attribute.
+// build: gcc -O2 -fPIC -shared -o /tmp/libfc2_sampler.so scripts/prof/sampler.c -lrt -ldl
+#define _GNU_SOURCE
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+#include <time.h>
+#include <ucontext.h>
+
+#define MAXS (1 << 20)
+#define DEPTH 12
+static uintptr_t ips[MAXS];
+static void *stk[MAXS][DEPTH];
+static unsigned char nstk[MAXS];
+static unsigned char tags[MAXS];
+static volatile int n_samples;
+static volatile int cur_tag;
+static timer_t tid;
+
+static void on_prof(int sig, siginfo_t *si, void *ucv) {
+    (void)sig; (void)si;
+    const int t = cur_tag;
+    if (t <= 0) return;
+    const ucontext_t *uc = (const ucontext_t *)ucv;
+    const int i = __sync_fetch_and_add(&n_samples, 1);
+    if (i < MAXS) {
+        ips[i] = (uintptr_t)uc->uc_mcontext.gregs[REG_RIP];
+        tags[i] = (unsigned char)t;
+        nstk[i] = (unsigned char)backtrace(stk[i], DEPTH);   // handler, trampoline, then the interrupted frames
+    }
+}
+
+int sampler_start(int usec) {
+    void *warm[4];
+    backtrace(warm, 4);                          // loads the unwinder outside the signal handler
+    struct sigaction sa;
+    memset(&sa, 0, sizeof sa);
+    sa.sa_sigaction = on_prof;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    if (sigaction(SIGPROF, &sa, 0)) return -1;
+    struct sigevent ev;
+    memset(&ev, 0, sizeof ev);
+    ev.sigev_notify = SIGEV_SIGNAL;
+    ev.sigev_signo = SIGPROF;
+    if (timer_create(CLOCK_MONOTONIC, &ev, &tid)) return -2;
+    struct itimerspec it;
+    it.it_interval.tv_sec = 0;
+    it.it_interval.tv_nsec = (long)usec * 1000L;
+    it.it_value = it.it_interval;
+    return timer_settime(tid, 0, &it, 0);
+}
+
+void sampler_phase(int tag) { cur_tag = tag; }
+
+int sampler_stop(const char *path) {
+    cur_tag = 0;
+    timer_delete(tid);
+    FILE *f = fopen(path, "w");
+    if (!f) return -1;
+    const int n = n_samples < MAXS ? n_samples : MAXS;
+    for (int i = 0; i < n; ++i) {
+        Dl_info d;
+        memset(&d, 0, sizeof d);
+        dladdr((void *)ips[i], &d);
+        fprintf(f, "%d %lx %s %lx %s", tags[i], (unsigned long)ips[i], d.dli_fname ? d.dli_fname : "?",
+                (unsigned long)(uintptr_t)d.dli_fbase, d.dli_sname ? d.dli_sname : "?");
+        // the callers: frames after the interrupted PC, as object+offset
+        int k = 0;
+        while (k < nstk[i] && (uintptr_t)stk[i][k] != ips[i]) ++k;
+        for (++k; k < nstk[i]; ++k) {
+            Dl_info c;
+            memset(&c, 0, sizeof c);
+            dladdr(stk[i][k], &c);
+            fprintf(f, " %s+%lx", c.dli_fname ? c.dli_fname : "?",
+                    (unsigned long)((uintptr_t)stk[i][k] - (uintptr_t)c.dli_fbase));
+        }
+        fputc('\n', f);
+    }
+    fclose(f);
+    return n;
+}
