@@ -750,6 +750,13 @@ int64_t uniqness(const Rec &a) {                                  // :809-819
     return a.as - (a.has_xs ? a.xs : 0);
 }
 
+// Hit.add's anchor quality (find_circ.py:556-559): dict(tags) keeps the LAST AS / XS of a record
+int64_t dict_quality(const Rec &a) {
+    if (!a.as_last_int || (a.has_xs && !a.xs_last_int))
+        throw Fatal{FC2_E_FORMAT, "native caller: AS / XS tags must be integers (use --python-caller)"};
+    return a.as_last - (a.has_xs ? a.xs_last : 0);
+}
+
 const char *kNoneLen = "TypeError: object of type 'NoneType' has no len()";
 
 // process_mate (:1492-1527) with adjacent_segment_pairs (:1058-1140)
@@ -802,8 +809,9 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
         s.b_aend = B.aend;
         s.weight = weight;
         s.uniq = std::min(ua, ub);
-        s.qA = s.circ ? ub : ua;
-        s.qB = s.circ ? ua : ub;
+        const int64_t qa = dict_quality(A), qb = dict_quality(B);
+        s.qA = s.circ ? qb : qa;
+        s.qB = s.circ ? qa : qb;
         s.a_rev = s.circ ? B.reverse() : A.reverse();
         // read_part = primary.seq[q_start:q_end] (Python slice)
         const int64_t lo = std::max<int64_t>(0, std::min(q_start, L)), hi = std::max(lo, std::min(q_end, L));

@@ -8,6 +8,7 @@
 // closes the fragment.  Pairing follows MateSegments.add_segment /
 // adjacent_segment_pairs / process_mate (:1039-1140, 1492-1527).
 #include <ctype.h>
+#include <emmintrin.h>
 #include <errno.h>
 #include <fcntl.h>
 #include <stdio.h>
@@ -363,11 +364,17 @@ void note_tag(Rec &r, const char *t, const char *e) {
     if (e - t < 5 || t[2] != ':' || t[4] != ':') return;
     const bool as = t[0] == 'A' && t[1] == 'S', xs = t[0] == 'X' && t[1] == 'S';
     if (!as && !xs) return;
-    if ((as && r.has_as) || (xs && r.has_xs)) return;
     const bool isint = t[3] == 'i';
     const int64_t v = isint ? to_i64(t + 5, e) : 0;
-    if (as) { r.has_as = true; r.as_int = isint; r.as = v; }
-    else { r.has_xs = true; r.xs_int = isint; r.xs = v; }
+    if (as) {
+        if (!r.has_as) { r.has_as = true; r.as_int = isint; r.as = v; }
+        r.as_last_int = isint;
+        r.as_last = v;
+    } else {
+        if (!r.has_xs) { r.has_xs = true; r.xs_int = isint; r.xs = v; }
+        r.xs_last_int = isint;
+        r.xs_last = v;
+    }
 }
 
 void scan_sam_tags(Rec &r, const char *p, const char *end) {
@@ -379,24 +386,33 @@ void scan_sam_tags(Rec &r, const char *p, const char *end) {
     }
 }
 
+// the tabs of [b, e) in order, up to maxn of them (16 bytes per SSE2 compare; every x86-64 has it)
+int find_tabs(const char *b, const char *e, const char **t, int maxn) {
+    int n = 0;
+    const char *p = b;
+    const __m128i tab = _mm_set1_epi8('\t');
+    while (p + 16 <= e && n < maxn) {
+        unsigned m = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(_mm_loadu_si128((const __m128i *)p), tab));
+        while (m && n < maxn) { t[n++] = p + __builtin_ctz(m); m &= m - 1; }
+        p += 16;
+    }
+    for (; p < e && n < maxn; ++p)
+        if (*p == '\t') t[n++] = p;
+    return n;
+}
+
 int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r) {
-    // fields 1-11 (and the start of the tags)
+    // every tab of the line in one pass: fields 1-11, then the tags
+    constexpr int kMaxTabs = 64;
+    const char *tabs[kMaxTabs];
+    const int nt = find_tabs(ls, le, tabs, kMaxTabs);
     const char *f[13];
     int nf = 0;
     f[nf++] = ls;
-    for (const char *p = ls; nf < 12;) {
-        const char *t = (const char *)memchr(p, '\t', (size_t)(le - p));
-        if (!t) break;
-        f[nf++] = t + 1;
-        p = t + 1;
-    }
+    for (int k = 0; k < nt && nf < 12; ++k) f[nf++] = tabs[k] + 1;
     if (nf < 11) return fc2::fail(FC2_E_FORMAT, "malformed SAM line: " + std::string(ls, std::min<size_t>(80, le - ls)));
     auto fb = [&](int k) { return f[k]; };
-    auto fe = [&](int k) {
-        if (k + 1 < nf) return f[k + 1] - 1;
-        const char *t = (const char *)memchr(f[k], '\t', (size_t)(le - f[k]));
-        return t ? t : le;
-    };
+    auto fe = [&](int k) { return k < nt ? tabs[k] : le; };
     if (h->need_text || h->bam_out) r.text.assign(ls, le);
     r.qname.assign(fb(0), fe(0));
     r.flag = (uint32_t)to_i64(fb(1), fe(1));
@@ -432,8 +448,14 @@ int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r) {
     r.has_as = r.has_xs = false;
     r.as_int = r.xs_int = true;
     r.as = r.xs = 0;
+    r.as_last_int = r.xs_last_int = true;
+    r.as_last = r.xs_last = 0;
     finish_rec(r, ops, r.has_seq ? (int64_t)r.seq.size() : 0);
-    if (nf == 12) scan_sam_tags(r, f[11], le);
+    if (nf == 12) {                                 // tags: [tabs[k] + 1, next tab or line end), k >= 10
+        const int last = nt == kMaxTabs ? nt - 1 : nt;
+        for (int k = 10; k < last; ++k) note_tag(r, tabs[k] + 1, k + 1 < nt ? tabs[k + 1] : le);
+        if (nt == kMaxTabs) scan_sam_tags(r, tabs[kMaxTabs - 1] + 1, le);   // more tabs than were collected
+    }
     return FC2_OK;
 }
 
@@ -523,6 +545,8 @@ void scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
         const bool as = t0 == 'A' && t1 == 'S', xs = t0 == 'X' && t1 == 'S';
         if (as && !r.has_as) { r.has_as = true; r.as_int = isint; r.as = v; }
         if (xs && !r.has_xs) { r.has_xs = true; r.xs_int = isint; r.xs = v; }
+        if (as) { r.as_last_int = isint; r.as_last = v; }
+        if (xs) { r.xs_last_int = isint; r.xs_last = v; }
         p += adv;
     }
 }
@@ -577,6 +601,8 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     r.has_as = r.has_xs = false;
     r.as_int = r.xs_int = true;
     r.as = r.xs = 0;
+    r.as_last_int = r.xs_last_int = true;
+    r.as_last = r.xs_last = 0;
     scan_bam_tags(r, p, e);
     r.has_qual = !(qual.size() == 1 && qual[0] == '*');
     if (!h->need_text) {

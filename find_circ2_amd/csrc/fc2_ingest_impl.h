@@ -29,6 +29,9 @@ struct Rec {
     // AS / XS tags as pysam's get_tag returns them: present?, integer-typed?, value
     bool has_as = false, has_xs = false, as_int = true, xs_int = true;
     int64_t as = 0, xs = 0;
+    // the LAST occurrence of each, as dict(read.tags) gives it (Hit.add, find_circ.py:556-557)
+    bool as_last_int = true, xs_last_int = true;
+    int64_t as_last = 0, xs_last = 0;
     bool unmapped() const { return flag & 0x4; }
     bool read1() const { return flag & 0x40; }
     bool reverse() const { return flag & 0x10; }

@@ -376,3 +376,37 @@ def test_native_caller_degenerate_inputs(tmp_path, body):
     same(outs[0], outs[2])
     rows = [l for l in open(os.path.join(outs[2], "circ_splice_sites.bed")) if not l.startswith("#")]
     assert rows == []
+
+
+@pytest.mark.parametrize("n_filler", [0, 9, 62, 70])
+def test_native_caller_many_sam_tags(tmp_path, n_filler):
+    """The SAM parser collects a line's tabs in one pass (64 at most, then it falls back to a
+    per-tag scan): AS / XS found after many filler tags, first occurrence winning, the same files
+    as the Python ingest."""
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, 300, seed=4242)
+    out_lines = []
+    for line in open(sam0).read().splitlines():
+        if line.startswith("@"):
+            out_lines.append(line)
+            continue
+        f = line.split("\t")
+        filler = ["Z%d:i:%d" % (k % 10, k) for k in range(n_filler)]
+        # a second, later AS: uniqness() reads the first (get_tag, find_circ.py:814), Hit.add the
+        # last (dict(tags), :556-557) -- the anchor-quality columns show which one was used
+        first_as = [int(t[5:]) for t in f[11:] if t.startswith("AS:i:")][:1]
+        dup = ["AS:i:%d" % (first_as[0] + 5)] if first_as else []
+        out_lines.append("\t".join(f[:11] + filler + f[11:] + dup))
+    sam = str(tmp_path / "t.sam")
+    open(sam, "w").write("\n".join(out_lines) + "\n")
+    o1, o2 = str(tmp_path / "py"), str(tmp_path / "native")
+    rc1 = cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory)
+    rc2 = cli.main(["-G", fa, "-o", o2, "-q", sam], evaluator_factory=oracle_evaluator_factory)
+    assert rc1 == rc2 == 0
+    same(o1, o2)
+    assert sum(1 for l in open(os.path.join(o2, "circ_splice_sites.bed")) if l[0] != "#") > 20
+    bam = str(tmp_path / "t.bam")                  # the BAM aux parser: same rule
+    sam_to_bam(open(sam).read(), bam)
+    o3 = str(tmp_path / "native_bam")
+    assert cli.main(["-G", fa, "-o", o3, "-q", bam], evaluator_factory=oracle_evaluator_factory) == 0
+    same(o1, o3)
