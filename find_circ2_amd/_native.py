@@ -125,6 +125,7 @@ EXPORTED = [
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
     "fc2_caller_submit", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
+    "fc2_caller_set_reads_gz", "fc2_caller_close_reads",
 ]
 
 
@@ -238,6 +239,8 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_submit": (ctypes.c_int, [vp, vp, vp, u32, u64]),
         "fc2_caller_queued": (ctypes.c_int, [vp]),
         "fc2_caller_take": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
+        "fc2_caller_set_reads_gz": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, u64]),
+        "fc2_caller_close_reads": (ctypes.c_int, [vp]),
         "fc2_caller_rows": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_counter": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(ctypes.c_double)]),
         "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),

@@ -248,6 +248,7 @@ def _devices(options):
 def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path="") -> int:
     """The read loop in C++ (include/fc2_caller.h); only the breakpoint search is called from here."""
     from .caller import BED_HEADER, MULTI_HEADER
+    from .gzout import ParallelGzipWriter
     from .native_caller import NativeCaller, gpu_batch_evaluator
     if evaluator_factory is None:
         evaluate = gpu_batch_evaluator(genome, hp, devices=_devices(options))
@@ -257,9 +258,14 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
         if engine is None:
             raise ValueError("evaluator_factory has no batch form for the native caller (use --python-caller)")
         evaluate, names, fasta, dummy = engine(options, hp)
+    reads_gz = None
+    if isinstance(out.get("reads"), ParallelGzipWriter):   # compressed by the read loop itself
+        w = out["reads"]
+        reads_gz = (w.hand_over(), w.level, w.threads, w.piece)
     nc = NativeCaller(path, is_bam, options, names, fasta, write_reads=out.get("reads") is not None,
                       write_multi=out.get("multi") is not None, genome_dummy=dummy,
-                      known_circ=options.known_circ, known_lin=options.known_lin, bam_out=bam_path)
+                      known_circ=options.known_circ, known_lin=options.known_lin, bam_out=bam_path,
+                      reads_gz=reads_gz)
     try:
         n_kc, n_kl = nc.open()
         for n, p in ((n_kc, options.known_circ), (n_kl, options.known_lin)):
@@ -294,7 +300,10 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             out[key].write(BED_HEADER)
             out[key].write(nc.rows(kind))
     finally:
-        nc.close()
+        try:
+            nc.finish_reads()
+        finally:
+            nc.close()
         for k, fh in out.items():
             if fh is not None and fh is not sys.stdout:
                 fh.close()

@@ -23,6 +23,7 @@
 
 #include "../../include/fc2_caller.h"
 #include "fc2_common.h"
+#include "fc2_gzpieces.h"
 #include "fc2_ingest_impl.h"
 
 using fc2::ing::Mate;
@@ -446,6 +447,7 @@ struct fc2_caller {
                                                       // (merged by name into sorted keys on output)
     std::vector<std::pair<const char *, double>> N_in; // the same for the counters the next side bumps
     std::string out[3];                         // reads, multi, test text since the last take
+    fc2::GzPieces reads_gz;                     // fc2_caller_set_reads_gz: out[0] goes here
     std::string taken[3];                       // fc2_caller_take's buffers (valid until the next take)
     std::string rows_text;
     std::vector<std::pair<std::string, double>> counters_snapshot;
@@ -1511,6 +1513,7 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
     } catch (const Fatal &f) {
         rc = fc2::fail(f.code, f.msg);
     }
+    if (h->reads_gz.is_open() && !h->out[0].empty()) h->reads_gz.append(h->out[0]);
     // hand the chunk's buffers back to the next side (fc2_caller::spare)
     fc2_caller::Chunk c;
     c.frags.swap(h->frags);
@@ -1532,6 +1535,23 @@ extern "C" int fc2_caller_take(fc2_caller *h, int stream, const char **text, uin
     h->out[stream].clear();
     *text = t.c_str();
     *len = t.size();
+    return FC2_OK;
+}
+
+extern "C" int fc2_caller_set_reads_gz(fc2_caller *h, const char *path, int level, int threads, uint64_t piece) {
+    if (!h || !path || level < 0 || level > 9) return fc2::fail(FC2_E_PARAM, "fc2_caller_set_reads_gz: bad arguments");
+    if (h->reads_gz.is_open() || h->n_pairs) return fc2::fail(FC2_E_PARAM, "fc2_caller_set_reads_gz: call once, before reading");
+    std::string err;
+    if (!h->reads_gz.open(path, level, threads, piece ? (size_t)piece : size_t(4) << 20, err))
+        return fc2::fail(FC2_E_IO, err);
+    return FC2_OK;
+}
+
+extern "C" int fc2_caller_close_reads(fc2_caller *h) {
+    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_close_reads: null argument");
+    if (h->reads_gz.is_open() && !h->out[0].empty()) h->reads_gz.append(h->out[0]);
+    std::string err;
+    if (!h->reads_gz.close(err)) return fc2::fail(FC2_E_IO, err);
     return FC2_OK;
 }
 

@@ -24,13 +24,17 @@ def _member(data: bytes, level: int) -> bytes:
 
 class ParallelGzipWriter(io.TextIOBase):
     def __init__(self, path: str, level: int = 6, threads: int = 0, piece: int = 4 << 20, encoding: str = "latin-1"):
+        self.path = path
+        self.level = level
+        self.piece = piece
+        self.threads = threads or min(8, os.cpu_count() or 1)
         self._f = open(path, "wb")
         self._level = level
         self._piece = piece
         self._enc = encoding
         self._buf = []
         self._n = 0
-        n = threads or min(8, os.cpu_count() or 1)
+        n = self.threads
         self._pool = ThreadPoolExecutor(max_workers=n)
         self._max_pending = 2 * n
         self._pending = deque()
@@ -56,6 +60,16 @@ class ParallelGzipWriter(io.TextIOBase):
 
     def flush(self):
         pass            # pieces are written as they complete; close() writes the rest
+
+    def hand_over(self) -> str:
+        """Give the file to another writer (the native read loop, fc2_caller_set_reads_gz) before
+        anything was written: this object then writes nothing, and close() only releases it."""
+        if self._buf or self._pending:
+            raise ValueError("hand_over after text was written")
+        self._f.close()
+        self._f = None
+        self._pool.shutdown()
+        return self.path
 
     def close(self):
         if self._f is None:

@@ -63,7 +63,7 @@ class NativeCaller:
 
     def __init__(self, path: str, is_bam: bool, copts, genome_names, fasta_handle=None, write_reads=True,
                  write_multi=True, genome_dummy=False, known_circ: str = "", known_lin: str = "",
-                 bam_out: str = ""):
+                 bam_out: str = "", reads_gz=None):
         o = copts
         # the strings must outlive the handle's open call (fc2_caller_open copies them)
         self._keep = [o.name.encode(), known_circ.encode() if known_circ else None,
@@ -81,6 +81,7 @@ class NativeCaller:
         self._path = path
         self._is_bam = is_bam
         self.bam_out = bam_out
+        self.reads_gz = reads_gz     # (path, level, threads, piece): spliced_reads.fastq.gz written natively
         self.opened = False
         self.loop_profile = {}       # seconds per stage of the last run (two-thread loop)
 
@@ -95,6 +96,9 @@ class NativeCaller:
         ing = L.fc2_caller_ingest(self.h)
         if self.bam_out:
             N.check(L.fc2_ingest_set_bam_out(ing, self.bam_out.encode()))
+        if self.reads_gz:
+            path, level, threads, piece = self.reads_gz
+            N.check(L.fc2_caller_set_reads_gz(self.h, path.encode(), int(level), int(threads), int(piece)))
         n_ref = L.fc2_ingest_n_refs(ing)
         self.refs = [L.fc2_ingest_ref_name(ing, t).decode("latin-1") for t in range(n_ref)]
         index = {nm: k for k, nm in enumerate(self.genome_names)}
@@ -117,6 +121,11 @@ class NativeCaller:
         nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
         N.check(N.lib().fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs)))
         return int(nr.value), int(npairs.value)
+
+    def finish_reads(self):
+        """Compress and write the rest of spliced_reads.fastq.gz (when written natively)."""
+        if self.opened and self.reads_gz:
+            N.check(N.lib().fc2_caller_close_reads(self.h))
 
     def close(self):
         if self.opened:

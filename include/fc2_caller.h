@@ -88,6 +88,14 @@ int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const uint64_t *
 /* Output text produced since the last call: 0 = spliced_reads.fastq, 1 =
  * multi_events.tsv rows, 2 = test_results.tsv rows. */
 int fc2_caller_take(fc2_caller *h, int stream, const char **text, uint64_t *len);
+/* Write spliced_reads.fastq.gz here instead (find_circ.py:445): the text of stream 0 is cut into
+ * pieces of `piece` bytes (0: 4 MiB), each compressed at `level` as its own gzip member on
+ * `threads` worker threads and written in order (one valid gzip stream); stream 0 of
+ * fc2_caller_take then stays empty.  Call before the first fc2_caller_submit. */
+int fc2_caller_set_reads_gz(fc2_caller *h, const char *path, int level, int threads, uint64_t piece);
+/* Compress and write what is left and close the file (also done, errors ignored, by
+ * fc2_caller_close); FC2_E_IO if a write failed. */
+int fc2_caller_close_reads(fc2_caller *h);
 /* The BED rows (no header) of 0 = circ_splice_sites.bed, 1 = lin_splice_sites.bed
  * (call once, at the end). */
 int fc2_caller_rows(fc2_caller *h, int kind, const char **text, uint64_t *len);

@@ -22,5 +22,5 @@ cd $ROOT/find_circ2_amd/csrc
     fc2_caller.cpp fc2_bamout.cpp -lpthread -lz
 cd $ROOT
 shift || true
-FC2_LIB_VARIANT=$KIND LD_PRELOAD=$PRE python -m pytest ${@:-tests} -x -q -m "not gpu" -p no:xdist
+FC2_LIB_VARIANT=$KIND LD_PRELOAD="$PRE${LD_PRELOAD:+:$LD_PRELOAD}" python -m pytest ${@:-tests} -x -q -m "not gpu" -p no:xdist
 rm -f find_circ2_amd/libfc2_$KIND.so

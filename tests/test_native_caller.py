@@ -410,3 +410,33 @@ def test_native_caller_many_sam_tags(tmp_path, n_filler):
     o3 = str(tmp_path / "native_bam")
     assert cli.main(["-G", fa, "-o", o3, "-q", bam], evaluator_factory=oracle_evaluator_factory) == 0
     same(o1, o3)
+
+
+def test_native_reads_gz_members(tmp_path, monkeypatch):
+    """spliced_reads.fastq.gz compressed by the native loop (fc2_caller_set_reads_gz) in small
+    pieces -- many gzip members, written in order on worker threads -- reads back as the text the
+    Python loop writes."""
+    import gzip
+    import zlib
+    from find_circ2_amd import gzout
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 800, seed=77)
+    o1, o2 = str(tmp_path / "py"), str(tmp_path / "native")
+    assert cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    orig = gzout.ParallelGzipWriter.__init__
+
+    def small_pieces(self, path, level=6, threads=0, piece=4 << 20, encoding="latin-1"):
+        orig(self, path, level=level, threads=3, piece=4096, encoding=encoding)
+    monkeypatch.setattr(gzout.ParallelGzipWriter, "__init__", small_pieces)
+    assert cli.main(["-G", fa, "-o", o2, "-q", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    same(o1, o2)
+    raw = open(os.path.join(o2, "spliced_reads.fastq.gz"), "rb").read()
+    members, text = 0, b""
+    while raw:                                      # walk the members one by one
+        d = zlib.decompressobj(16 + zlib.MAX_WBITS)
+        text += d.decompress(raw)
+        raw = d.unused_data
+        members += 1
+    assert members > 20
+    with gzip.open(os.path.join(o1, "spliced_reads.fastq.gz"), "rb") as f:
+        assert text == f.read()
