@@ -18,7 +18,11 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <future>
+#include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -246,6 +250,40 @@ struct fc2_ingest {
     std::vector<Rec> pool;       // recycled records: their strings keep their capacity
     std::string last_rn;         // RNAME -> tid cache (consecutive records share a chromosome)
     int last_tid = -1;
+    // SAM records parsed one batch ahead on a thread of their own (native caller pulls, no -B
+    // writer): the reading and parsing state above then belongs to that thread
+    struct SamAhead;
+    std::unique_ptr<SamAhead> ahead;
+    ~fc2_ingest();
+};
+
+// The parse-ahead thread: batches of parsed records, handed over in input order.  Records travel
+// back with their buffers (the consumer swaps in a recycled record), so steady state allocates
+// nothing.  A parse or read error ends the stream at that record, where the consumer reports it.
+struct fc2_ingest::SamAhead {
+    struct Batch {
+        std::vector<Rec> recs;
+        size_t n = 0;
+        int rc = FC2_OK;
+        std::string err;
+        bool eof = false;
+    };
+    static constexpr size_t kRecs = 4096, kDepth = 4;
+    std::mutex m;
+    std::condition_variable cv;
+    std::deque<std::unique_ptr<Batch>> full, spare;
+    std::unique_ptr<Batch> cur;                 // the consumer's batch
+    size_t pos = 0;
+    bool stop = false;
+    std::thread th;
+    ~SamAhead() {
+        {
+            std::lock_guard<std::mutex> lk(m);
+            stop = true;
+        }
+        cv.notify_all();
+        if (th.joinable()) th.join();
+    }
 };
 
 namespace {
@@ -685,8 +723,72 @@ int read_header(fc2_ingest *h) {
     return FC2_OK;
 }
 
+void sam_ahead_loop(fc2_ingest *h) {
+    auto &A = *h->ahead;
+    for (;;) {
+        std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
+        {
+            std::unique_lock<std::mutex> lk(A.m);
+            A.cv.wait(lk, [&] { return A.stop || A.full.size() < A.kDepth; });
+            if (A.stop) return;
+            if (!A.spare.empty()) { b = std::move(A.spare.back()); A.spare.pop_back(); }
+        }
+        if (!b) b.reset(new fc2_ingest::SamAhead::Batch());
+        b->n = 0;
+        b->rc = FC2_OK;
+        b->err.clear();
+        b->eof = false;
+        while (b->n < A.kRecs) {
+            const char *ls, *le;
+            if (!next_line_view(h, ls, le)) { b->eof = true; break; }
+            bool blank = true;
+            for (const char *c = ls; c < le; ++c) if (!isspace((unsigned char)*c)) { blank = false; break; }
+            if (blank) continue;
+            if (b->n == b->recs.size()) b->recs.emplace_back();
+            const int rc = parse_sam_record(h, ls, le, b->recs[b->n]);
+            if (rc) { b->rc = rc; b->err = fc2_last_error(); break; }
+            ++b->n;
+        }
+        const bool last = b->eof || b->rc;
+        {
+            std::lock_guard<std::mutex> lk(A.m);
+            A.full.push_back(std::move(b));
+        }
+        A.cv.notify_all();
+        if (last) return;
+    }
+}
+
+// the consumer side of next_record: the next parsed record swapped into r
+bool next_ahead(fc2_ingest *h, Rec &r, int &rc) {
+    auto &A = *h->ahead;
+    for (;;) {
+        if (!A.cur) {
+            std::unique_lock<std::mutex> lk(A.m);
+            A.cv.wait(lk, [&] { return !A.full.empty(); });
+            A.cur = std::move(A.full.front());
+            A.full.pop_front();
+            A.pos = 0;
+            lk.unlock();
+            A.cv.notify_all();
+        }
+        if (A.pos < A.cur->n) {
+            std::swap(r, A.cur->recs[A.pos++]);
+            return true;
+        }
+        if (A.cur->rc) { rc = fc2::fail(A.cur->rc, A.cur->err); return false; }   // stays: reported again
+        if (A.cur->eof) return false;
+        {
+            std::lock_guard<std::mutex> lk(A.m);
+            A.spare.push_back(std::move(A.cur));
+        }
+        A.cv.notify_all();
+    }
+}
+
 bool next_record(fc2_ingest *h, Rec &r, int &rc) {
     rc = FC2_OK;
+    if (h->ahead) return next_ahead(h, r, rc);
     if (h->bam) {
         bool got;
         rc = parse_bam_record(h, r, got);
@@ -890,8 +992,11 @@ extern "C" int fc2_ingest_close_bam_out(fc2_ingest *h) {
     return ok ? FC2_OK : fc2::fail(FC2_E_IO, err);
 }
 
+fc2_ingest::~fc2_ingest() { ahead.reset(); }
+
 extern "C" void fc2_ingest_close(fc2_ingest *h) {
     if (!h) return;
+    h->ahead.reset();                  // stops the parse-ahead thread before the fd goes
     if (h->bam_out) {
         std::string err;
         fc2::bam::close_writer(h->bam_out, err);
@@ -974,7 +1079,11 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
 
 int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof) {
     if (!h || !p) return fc2::fail(FC2_E_PARAM, "ingest pull: null argument");
-    h->need_text = false;
+    if (h->need_text) h->need_text = false;     // (written once: the parse thread reads it)
+    if (!h->ahead && !h->bam && !h->bam_out && !h->finished) {   // SAM: parse on a thread of its own
+        h->ahead.reset(new fc2_ingest::SamAhead());
+        h->ahead->th = std::thread(sam_ahead_loop, h);
+    }
     return run_loop(h, p, max_frags, &sink, nullptr, eof);
 }
 

@@ -13,7 +13,7 @@ case $KIND in
   ubsan) SAN="-Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=undefined"
          PRE=$RT/libclang_rt.ubsan_standalone-x86_64.so; export UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 ;;
   tsan)  SAN="-Xarch_host -fsanitize=thread"
-         PRE=$RT/libclang_rt.tsan-x86_64.so; export TSAN_OPTIONS=halt_on_error=1:report_signal_unsafe=0 ;;
+         PRE=$RT/libclang_rt.tsan-x86_64.so; export TSAN_OPTIONS=${TSAN_OPTIONS:-halt_on_error=1:report_signal_unsafe=0} ;;
   *) echo "usage: $0 asan|ubsan|tsan"; exit 2 ;;
 esac
 cd $ROOT/find_circ2_amd/csrc
