@@ -199,6 +199,9 @@ class CIndex {
             if (s.k == k) return &s.v;
         }
     }
+    void prefetch(const CKey &k) const {        // the slot a lookup of k starts at
+        if (!slots_.empty()) __builtin_prefetch(&slots_[CKeyHash()(k) & (slots_.size() - 1)]);
+    }
     size_t at(const CKey &k) const {
         const size_t *p = find(k);
         if (!p) throw std::out_of_range("CIndex::at");
@@ -1300,6 +1303,27 @@ void record_hits(fc2_caller *h, Frag &fr, const Results &R, FragScratch &F) {
     }
 }
 
+// the junction-table slots a fragment's best splices will look up (decode's coordinates, computed
+// early from the raw results): issued a few fragments ahead, they hide the tables' cache misses
+void prefetch_frag(const fc2_caller *h, const Frag &fr, const Results &R) {
+    const int64_t e = h->o.asize - h->o.margin;
+    for (int kind = 0; kind < 2; ++kind) {
+        for (int si : kind ? fr.lin : fr.circ) {
+            const Span &s = h->spans[si];
+            if (s.eval < 0 || (size_t)s.tid >= h->tid_cid.size() || h->tid_cid[(size_t)s.tid] < 0) continue;
+            const fc2_result &r = R.res[s.eval];
+            const fc2_pair &pr = h->b_pairs[(size_t)s.eval];
+            if (r.best_x < 0 || (r.info & (FC2_RES_ERR_KEY | FC2_RES_ERR_WIN)) || (pr.flags & FC2_PAIR_SKIP)) continue;
+            const int64_t l = (int64_t)pr.read_len - 2 * e;
+            const int64_t s0 = pr.b_aend - e - l + r.best_x, e0 = pr.a_pos + e + r.best_x + 1;
+            int64_t st = std::min(s0, e0), en = std::max(s0, e0);
+            if (pr.flags & FC2_PAIR_BACKSPLICE) en -= 1; else st -= 1;
+            const uint32_t c = (uint32_t)h->tid_cid[(size_t)s.tid], strand = (r.info & FC2_RES_MINUS) ? 1u : 0u;
+            h->st[kind].index.prefetch(st < en ? CKey{st, en, c, strand} : CKey{en, st, c, strand});
+        }
+    }
+}
+
 void write_read(fc2_caller *h, const Align &m, FragScratch &F) {       // :1442-1447
     if (!h->o.write_reads) return;
     // '@<qname> <sorted junction names> <sorted flags>' , seq, '+' + the same name, qual
@@ -1502,7 +1526,9 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
     int rc = FC2_OK;
     try {
         static thread_local FragScratch F;
+        constexpr size_t kAhead = 8;
         for (size_t f = 0; f < h->nfrags; ++f) {
+            if (f + kAhead < h->nfrags) prefetch_frag(h, h->frags[f + kAhead], R);
             Frag &fr = h->frags[f];
             record_hits(h, fr, R, F);
             if (!F.junc.empty()) {
