@@ -3,6 +3,7 @@
 // which cites find_circ.py line by line; the comments here point at the
 // reference where the semantics are subtle.
 #include <math.h>
+#include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
 
@@ -177,47 +178,63 @@ struct CKeyHash {
     }
 };
 
+// Memory for the large per-run tables, cache-line aligned.  (Marking it for transparent huge pages
+// cut the recording side's TLB misses but stalled the other thread's allocations behind the
+// compaction it triggered: slower overall on the GPU box, so not done.)
+void *table_alloc(size_t bytes) {
+    void *p = aligned_alloc(64, (bytes + 63) / 64 * 64);
+    if (!p) throw std::bad_alloc();
+    return p;
+}
+
 // Open-addressing CKey -> index table (linear probing, power-of-two capacity, load <= 1/2): one flat
-// array instead of a node per junction
+// array of 32-byte slots (two per cache line) instead of a node per junction
 class CIndex {
   public:
+    CIndex() = default;
+    CIndex(const CIndex &) = delete;
+    CIndex &operator=(const CIndex &) = delete;
+    ~CIndex() { free(slots_); }
     // the index of k, inserting v for a new key; second = inserted
     std::pair<size_t, bool> try_emplace(const CKey &k, size_t v) {
-        if (2 * (n_ + 1) > slots_.size()) grow();
-        size_t i = CKeyHash()(k) & (slots_.size() - 1);
-        for (;; i = (i + 1) & (slots_.size() - 1)) {
+        if (2 * (n_ + 1) > cap_) grow();
+        for (size_t i = CKeyHash()(k) & (cap_ - 1);; i = (i + 1) & (cap_ - 1)) {
             Slot &s = slots_[i];
-            if (!s.used) { s.used = true; s.k = k; s.v = v; ++n_; return {v, true}; }
-            if (s.k == k) return {s.v, false};
-        }
-    }
-    const size_t *find(const CKey &k) const {
-        if (slots_.empty()) return nullptr;
-        for (size_t i = CKeyHash()(k) & (slots_.size() - 1);; i = (i + 1) & (slots_.size() - 1)) {
-            const Slot &s = slots_[i];
-            if (!s.used) return nullptr;
-            if (s.k == k) return &s.v;
+            if (!s.v1) { s.k = k; s.v1 = (uint32_t)(v + 1); ++n_; return {v, true}; }
+            if (s.k == k) return {(size_t)s.v1 - 1, false};
         }
     }
     void prefetch(const CKey &k) const {        // the slot a lookup of k starts at
-        if (!slots_.empty()) __builtin_prefetch(&slots_[CKeyHash()(k) & (slots_.size() - 1)]);
+        if (cap_) __builtin_prefetch(&slots_[CKeyHash()(k) & (cap_ - 1)]);
     }
     size_t at(const CKey &k) const {
-        const size_t *p = find(k);
-        if (!p) throw std::out_of_range("CIndex::at");
-        return *p;
+        if (cap_)
+            for (size_t i = CKeyHash()(k) & (cap_ - 1);; i = (i + 1) & (cap_ - 1)) {
+                const Slot &s = slots_[i];
+                if (!s.v1) break;
+                if (s.k == k) return (size_t)s.v1 - 1;
+            }
+        throw std::out_of_range("CIndex::at");
     }
   private:
-    struct Slot { CKey k; size_t v; bool used = false; };
-    std::vector<Slot> slots_;
-    size_t n_ = 0;
+    struct Slot {
+        CKey k;
+        uint32_t v1;                            // index + 1; 0 = empty
+        uint32_t pad;
+    };
+    static_assert(sizeof(Slot) == 32, "two slots per cache line");
+    Slot *slots_ = nullptr;
+    size_t cap_ = 0, n_ = 0;
     void grow() {
-        std::vector<Slot> old;
-        old.swap(slots_);
-        slots_.assign(old.empty() ? 1024 : 2 * old.size(), Slot{});
+        Slot *old = slots_;
+        const size_t old_cap = cap_;
+        cap_ = old_cap ? 2 * old_cap : 1024;
+        slots_ = (Slot *)table_alloc(cap_ * sizeof(Slot));
+        memset((void *)slots_, 0, cap_ * sizeof(Slot));
         n_ = 0;
-        for (const Slot &s : old)
-            if (s.used) try_emplace(s.k, s.v);
+        for (size_t j = 0; j < old_cap; ++j)
+            if (old[j].v1) try_emplace(old[j].k, (size_t)old[j].v1 - 1);
+        free(old);
     }
 };
 
@@ -376,19 +393,30 @@ struct Hit {                                   // Hit (:486-654)
     double tissue = 0.;
 };
 
-// Hits in insertion (= dict) order, in blocks that never move (references stay valid)
+// Hits in insertion (= dict) order, in blocks that never move (references stay valid);
+// a Hit is constructed when it is added
 class HitVec {
   public:
+    HitVec() = default;
+    HitVec(const HitVec &) = delete;
+    HitVec &operator=(const HitVec &) = delete;
+    ~HitVec() {
+        for (size_t k = 0; k < n_; ++k) (*this)[k].~Hit();
+        for (Hit *b : blocks_) free(b);
+    }
     size_t size() const { return n_; }
     Hit &operator[](size_t k) { return blocks_[k >> kShift][k & (kBlock - 1)]; }
     const Hit &operator[](size_t k) const { return blocks_[k >> kShift][k & (kBlock - 1)]; }
     Hit &emplace_back() {
-        if ((n_ >> kShift) == blocks_.size()) blocks_.emplace_back(new Hit[kBlock]);
-        return (*this)[n_++];
+        if ((n_ >> kShift) == blocks_.size()) blocks_.push_back((Hit *)table_alloc(kBlock * sizeof(Hit)));
+        Hit *h = &(*this)[n_];
+        new (h) Hit();
+        ++n_;
+        return *h;
     }
   private:
-    static constexpr size_t kShift = 10, kBlock = size_t(1) << kShift;
-    std::vector<std::unique_ptr<Hit[]>> blocks_;
+    static constexpr size_t kShift = 12, kBlock = size_t(1) << kShift;
+    std::vector<Hit *> blocks_;
     size_t n_ = 0;
 };
 
