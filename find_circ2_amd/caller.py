@@ -637,8 +637,22 @@ class Caller:
     def run(self, records, stderr=sys.stderr):
         o = self.o
         t0 = time.time()
-        t_last = t0
         pending: List[Fragment] = []
+        try:
+            self._run_loop(records, stderr, pending, t0)
+        except BaseException:
+            # the reference records every fragment before it reads the next: those of this chunk
+            # are recorded before the failure propagates (a failure of their own comes first)
+            self._flush(pending)
+            raise
+        self._flush(pending)
+        if o.throughput:
+            stderr.write('\n')
+        return time.time() - t0
+
+    def _run_loop(self, records, stderr, pending, t0):
+        o = self.o
+        t_last = t0
         for line_num, mate1, mate2 in group_alignments(records, self.N):
             self.n_reads += 1
             if o.throughput and not (self.n_reads % o.chunksize):
@@ -660,10 +674,6 @@ class Caller:
                 pending.append(frag)
                 if len(pending) >= o.chunksize:
                     self._flush(pending)
-        self._flush(pending)
-        if o.throughput:
-            stderr.write('\n')
-        return time.time() - t0
 
     def run_native(self, ingest, stderr=sys.stderr):
         """Same loop with the native ingest (include/fc2_ingest.h): only fragments carrying
@@ -673,6 +683,18 @@ class Caller:
         t_last = t0
         scratch = defaultdict(float)      # grouping counters of handed-back fragments are counted natively
         pending: List[Fragment] = []
+        try:
+            self._run_native_loop(ingest, stderr, pending, scratch, t0)
+        except BaseException:
+            self._flush(pending)        # as in run(): the fragments before the failure are recorded
+            raise
+        self._flush(pending)
+        c = ingest.counts
+        return self._finish_native(c, stderr, t0)
+
+    def _run_native_loop(self, ingest, stderr, pending, scratch, t0):
+        o = self.o
+        t_last = t0
         last_reads = 0
         while not ingest.eof:
             for recs in ingest.next_chunk(o.asize, o.nolinear, o.noop, o.chunksize):
@@ -695,13 +717,13 @@ class Caller:
                              "       \r".format(self.n_reads / 1e6, (t1 - t0) / 60.,
                                                 (self.n_reads - last_reads) / max(t1 - t_last, 1e-9) / 1000.))
                 t_last, last_reads = t1, self.n_reads
-        self._flush(pending)
-        c = ingest.counts
+
+    def _finish_native(self, c, stderr, t0):
         for key, v in (("total_mates", c.total_mates), ("unmapped_reads", c.unmapped_reads),
                        ("unspliced_mates", c.unspliced_mates), ("seg_too_short_skip", c.seg_too_short_skip)):
             if v:
                 self.N[key] += float(v)
         self.n_reads = int(c.n_reads)
-        if o.throughput:
+        if self.o.throughput:
             stderr.write('\n')
         return time.time() - t0

@@ -430,6 +430,11 @@ struct fc2_caller {
     std::vector<int32_t> tid2chrom;
     const fc2_fasta *fasta = nullptr;
     bool eof = false;
+    // an error of the input or of process_mate met while forming a chunk: the fragments before it
+    // are handed out first (the reference records each fragment before reading the next), the
+    // error comes with the following fc2_caller_next
+    int next_err = FC2_OK;
+    std::string next_err_msg;
     // Two sides that may run on two threads at once: fc2_caller_next forms chunks (ingest,
     // process_mate, the pairs) into the bf_* fields, fc2_caller_submit records the oldest queued chunk
     // (record_hits, tables, writers) from the plain fields.  They share only the queue (mutex) and
@@ -1456,6 +1461,11 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             h->spare.pop_back();
         }
     }
+    if (h->next_err) {
+        const int code = h->next_err;
+        h->next_err = FC2_OK;
+        return fc2::fail(code, h->next_err_msg);
+    }
     h->bf_nfrags = 0;
     h->bf_spans.clear();
     h->bf_arena.clear();
@@ -1473,7 +1483,14 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     while (!h->eof && h->bf_nfrags < h->o.chunksize) {
         int e = 0;
         const int rc = fc2::ing::pull(h->ing, &h->ip, h->o.chunksize, sink, &e);
-        if (rc) return err.code ? fc2::fail(err.code, err.msg) : rc;
+        if (rc) {
+            const int code = err.code ? err.code : rc;
+            const std::string msg = err.code ? err.msg : std::string(fc2_last_error());
+            if (!h->bf_nfrags) return fc2::fail(code, msg);
+            h->next_err = code;                    // hand out the fragments before it first
+            h->next_err_msg = msg;
+            break;
+        }
         h->eof = e != 0;
     }
     // the spans record_hits will evaluate, in fragment order (Caller._flush)

@@ -21,6 +21,7 @@
 #include <condition_variable>
 #include <deque>
 #include <future>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -245,44 +246,64 @@ struct fc2_ingest {
     fc2_ingest_counts counts{};
     bool finished = false;
     bool need_text = true;       // false once a native caller pulls structured fragments
+    // fc2_ingest_next: an error met after some fragments were formed is returned by the next call,
+    // after those fragments (the reference records each fragment before it reads the next)
+    int deferred_rc = FC2_OK;
+    std::string deferred_msg;
     // parse scratch, reused across records (no per-record allocation in steady state)
+    struct ParseScratch {
+        std::vector<std::pair<int, int>> ops;
+        std::string last_rn;     // RNAME -> tid cache (consecutive records share a chromosome)
+        int last_tid = -1;
+    } ps;
     std::vector<std::pair<int, int>> ops;
     std::vector<Rec> pool;       // recycled records: their strings keep their capacity
-    std::string last_rn;         // RNAME -> tid cache (consecutive records share a chromosome)
-    int last_tid = -1;
-    // SAM records parsed one batch ahead on a thread of their own (native caller pulls, no -B
-    // writer): the reading and parsing state above then belongs to that thread
+    // SAM records parsed ahead on threads of their own (native caller pulls, no -B writer): a
+    // splitter thread owns the input from then on and cuts it into newline-aligned blocks, parser
+    // threads turn blocks into record batches, the consumer takes the batches in input order
     struct SamAhead;
     std::unique_ptr<SamAhead> ahead;
     ~fc2_ingest();
 };
 
-// The parse-ahead thread: batches of parsed records, handed over in input order.  Records travel
-// back with their buffers (the consumer swaps in a recycled record), so steady state allocates
-// nothing.  A parse or read error ends the stream at that record, where the consumer reports it.
+// The parse-ahead threads.  The splitter reads the input into blocks cut after the last newline
+// (4 MiB each, numbered), parser threads turn each block into a batch of records, and the consumer
+// (next_record) takes the batches in block order.  Records travel back with their buffers (the
+// consumer swaps in a recycled record), so steady state allocates nothing.  A read or parse error
+// ends the stream at that record, where the consumer reports it.
 struct fc2_ingest::SamAhead {
     struct Batch {
+        uint64_t seq = 0;
+        std::string block;                      // the block's bytes (whole lines)
         std::vector<Rec> recs;
         size_t n = 0;
         int rc = FC2_OK;
         std::string err;
-        bool eof = false;
+        bool eof = false;                       // the last block of the input
     };
-    static constexpr size_t kRecs = 4096, kDepth = 4;
+    static constexpr size_t kBlock = size_t(4) << 20;
+    static constexpr int kParsers = 2;
+    static constexpr size_t kInflight = 8;      // blocks read but not yet consumed
     std::mutex m;
     std::condition_variable cv;
-    std::deque<std::unique_ptr<Batch>> full, spare;
+    std::deque<std::unique_ptr<Batch>> todo;    // read, not yet parsed (block order)
+    std::map<uint64_t, std::unique_ptr<Batch>> done;   // parsed, by block number
+    std::vector<std::unique_ptr<Batch>> spare;
+    size_t inflight = 0;
+    uint64_t next_consume = 0;
     std::unique_ptr<Batch> cur;                 // the consumer's batch
     size_t pos = 0;
     bool stop = false;
-    std::thread th;
+    std::thread splitter;
+    std::vector<std::thread> parsers;
     ~SamAhead() {
         {
             std::lock_guard<std::mutex> lk(m);
             stop = true;
         }
         cv.notify_all();
-        if (th.joinable()) th.join();
+        if (splitter.joinable()) splitter.join();
+        for (std::thread &t : parsers) t.join();
     }
 };
 
@@ -439,7 +460,7 @@ int find_tabs(const char *b, const char *e, const char **t, int maxn) {
     return n;
 }
 
-int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r) {
+int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r, fc2_ingest::ParseScratch &ps) {
     // every tab of the line in one pass: fields 1-11, then the tags
     constexpr int kMaxTabs = 64;
     const char *tabs[kMaxTabs];
@@ -456,15 +477,15 @@ int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r) {
     r.flag = (uint32_t)to_i64(fb(1), fe(1));
     const char *rb = fb(2), *re = fe(2);
     if (re - rb == 1 && *rb == '*') r.tid = -1;
-    else if ((size_t)(re - rb) == h->last_rn.size() && memcmp(rb, h->last_rn.data(), h->last_rn.size()) == 0) {
-        r.tid = h->last_tid;
+    else if ((size_t)(re - rb) == ps.last_rn.size() && memcmp(rb, ps.last_rn.data(), ps.last_rn.size()) == 0) {
+        r.tid = ps.last_tid;
     } else {
-        h->last_rn.assign(rb, re);
-        auto it = h->tid_of.find(h->last_rn);
-        r.tid = h->last_tid = it == h->tid_of.end() ? -1 : it->second;
+        ps.last_rn.assign(rb, re);
+        auto it = h->tid_of.find(ps.last_rn);
+        r.tid = ps.last_tid = it == h->tid_of.end() ? -1 : it->second;
     }
     r.pos = to_i64(fb(3), fe(3)) - 1;
-    std::vector<std::pair<int, int>> &ops = h->ops;
+    std::vector<std::pair<int, int>> &ops = ps.ops;
     ops.clear();
     const char *cb = fb(5), *ce = fe(5);
     if (!(ce - cb == 1 && *cb == '*')) {
@@ -723,39 +744,98 @@ int read_header(fc2_ingest *h) {
     return FC2_OK;
 }
 
-void sam_ahead_loop(fc2_ingest *h) {
+// splitter: the input from where the header ended, in newline-aligned numbered blocks
+void sam_split_loop(fc2_ingest *h) {
     auto &A = *h->ahead;
-    for (;;) {
+    std::string carry(h->buf.data() + h->beg, h->end - h->beg);   // bytes read with the header
+    h->beg = h->end;
+    bool in_eof = h->eof_in;
+    for (uint64_t seq = 0;; ++seq) {
         std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
         {
             std::unique_lock<std::mutex> lk(A.m);
-            A.cv.wait(lk, [&] { return A.stop || A.full.size() < A.kDepth; });
+            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.kInflight; });
             if (A.stop) return;
+            ++A.inflight;
             if (!A.spare.empty()) { b = std::move(A.spare.back()); A.spare.pop_back(); }
         }
         if (!b) b.reset(new fc2_ingest::SamAhead::Batch());
+        b->seq = seq;
         b->n = 0;
         b->rc = FC2_OK;
         b->err.clear();
         b->eof = false;
-        while (b->n < A.kRecs) {
-            const char *ls, *le;
-            if (!next_line_view(h, ls, le)) { b->eof = true; break; }
+        std::string &blk = b->block;
+        blk.swap(carry);
+        carry.clear();
+        // read until the block holds kBlock bytes and a newline, or the input ends
+        bool has_nl = memchr(blk.data(), '\n', blk.size()) != nullptr;
+        while (!in_eof && (blk.size() < A.kBlock || !has_nl)) {
+            const size_t have = blk.size();
+            blk.resize(have + A.kBlock);
+            ssize_t k;
+            do { k = read(h->fd, &blk[have], A.kBlock); } while (k < 0 && errno == EINTR);
+            if (k < 0) {
+                blk.resize(have);
+                b->rc = FC2_E_IO;
+                b->err = std::string("read error: ") + strerror(errno);
+                in_eof = true;
+                break;
+            }
+            blk.resize(have + (size_t)k);
+            if (k == 0) in_eof = true;
+            else if (!has_nl) has_nl = memchr(&blk[have], '\n', (size_t)k) != nullptr;
+        }
+        if (!in_eof) {                          // whole lines only; the rest starts the next block
+            const size_t nl = blk.rfind('\n');   // exists: the loop above read up to one
+            carry.assign(blk, nl + 1, std::string::npos);
+            blk.resize(nl + 1);
+        } else {
+            b->eof = true;
+        }
+        const bool last = b->eof;
+        {
+            std::lock_guard<std::mutex> lk(A.m);
+            A.todo.push_back(std::move(b));
+        }
+        A.cv.notify_all();
+        if (last) return;
+    }
+}
+
+// parser: blocks to record batches (own RNAME cache and CIGAR scratch)
+void sam_parse_loop(fc2_ingest *h) {
+    auto &A = *h->ahead;
+    fc2_ingest::ParseScratch ps;
+    for (;;) {
+        std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
+        {
+            std::unique_lock<std::mutex> lk(A.m);
+            A.cv.wait(lk, [&] { return A.stop || !A.todo.empty(); });
+            if (A.stop) return;
+            b = std::move(A.todo.front());
+            A.todo.pop_front();
+        }
+        const char *p = b->block.data(), *end = p + b->block.size();
+        while (p < end && b->rc == FC2_OK) {
+            const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
+            const char *ls = p, *le = nl ? nl : end;
+            p = nl ? nl + 1 : end;
+            if (le > ls && le[-1] == '\r') --le;
             bool blank = true;
             for (const char *c = ls; c < le; ++c) if (!isspace((unsigned char)*c)) { blank = false; break; }
             if (blank) continue;
             if (b->n == b->recs.size()) b->recs.emplace_back();
-            const int rc = parse_sam_record(h, ls, le, b->recs[b->n]);
+            const int rc = parse_sam_record(h, ls, le, b->recs[b->n], ps);
             if (rc) { b->rc = rc; b->err = fc2_last_error(); break; }
             ++b->n;
         }
-        const bool last = b->eof || b->rc;
         {
             std::lock_guard<std::mutex> lk(A.m);
-            A.full.push_back(std::move(b));
+            const uint64_t seq = b->seq;
+            A.done.emplace(seq, std::move(b));
         }
         A.cv.notify_all();
-        if (last) return;
     }
 }
 
@@ -765,12 +845,12 @@ bool next_ahead(fc2_ingest *h, Rec &r, int &rc) {
     for (;;) {
         if (!A.cur) {
             std::unique_lock<std::mutex> lk(A.m);
-            A.cv.wait(lk, [&] { return !A.full.empty(); });
-            A.cur = std::move(A.full.front());
-            A.full.pop_front();
+            A.cv.wait(lk, [&] { return A.done.count(A.next_consume) != 0; });
+            auto it = A.done.find(A.next_consume);
+            A.cur = std::move(it->second);
+            A.done.erase(it);
+            ++A.next_consume;
             A.pos = 0;
-            lk.unlock();
-            A.cv.notify_all();
         }
         if (A.pos < A.cur->n) {
             std::swap(r, A.cur->recs[A.pos++]);
@@ -780,6 +860,7 @@ bool next_ahead(fc2_ingest *h, Rec &r, int &rc) {
         if (A.cur->eof) return false;
         {
             std::lock_guard<std::mutex> lk(A.m);
+            --A.inflight;
             A.spare.push_back(std::move(A.cur));
         }
         A.cv.notify_all();
@@ -800,7 +881,7 @@ bool next_record(fc2_ingest *h, Rec &r, int &rc) {
         bool blank = true;
         for (const char *c = ls; c < le; ++c) if (!isspace((unsigned char)*c)) { blank = false; break; }
         if (blank) continue;
-        rc = parse_sam_record(h, ls, le, r);
+        rc = parse_sam_record(h, ls, le, r, h->ps);
         return rc == FC2_OK;
     }
 }
@@ -1082,7 +1163,8 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
     if (h->need_text) h->need_text = false;     // (written once: the parse thread reads it)
     if (!h->ahead && !h->bam && !h->bam_out && !h->finished) {   // SAM: parse on a thread of its own
         h->ahead.reset(new fc2_ingest::SamAhead());
-        h->ahead->th = std::thread(sam_ahead_loop, h);
+        h->ahead->splitter = std::thread(sam_split_loop, h);
+        for (int k = 0; k < fc2_ingest::SamAhead::kParsers; ++k) h->ahead->parsers.emplace_back(sam_parse_loop, h);
     }
     return run_loop(h, p, max_frags, &sink, nullptr, eof);
 }
@@ -1091,9 +1173,19 @@ extern "C" int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64
                                fc2_ingest_counts *counts, const char **text, uint64_t *text_len, uint64_t *n_handed,
                                int *eof) {
     if (!h || !p) return fc2::fail(FC2_E_PARAM, "fc2_ingest_next: null argument");
+    if (h->deferred_rc) {
+        const int code = h->deferred_rc;
+        h->deferred_rc = FC2_OK;
+        return fc2::fail(code, h->deferred_msg);
+    }
     h->out.clear();
     const int rc = run_loop(h, p, max_frags, nullptr, n_handed, eof);
-    if (rc) return rc;
+    if (rc) {
+        if (h->out.empty()) return rc;
+        h->deferred_rc = rc;                   // hand out the fragments before it first
+        h->deferred_msg = fc2_last_error();
+        if (eof) *eof = 0;
+    }
     if (counts) *counts = h->counts;
     if (text) *text = h->out.c_str();
     if (text_len) *text_len = h->out.size();

@@ -75,7 +75,9 @@ void fc2_caller_close(fc2_caller *h);
  * chunk k+1 while chunk k is being searched (at most FC2_CALLER_MAX_QUEUED chunks).
  * Reading ahead changes nothing in the outputs, which submit writes in input order;
  * if next fails, the caller submits the chunks it holds first, then raises (the
- * reference reaches those fragments' record_hits before the failing one). */
+ * reference reaches those fragments' record_hits before the failing one).  An input or
+ * process_mate error met after some fragments of a chunk were formed ends that chunk there:
+ * it is handed out as usual and the error is returned by the following call. */
 #define FC2_CALLER_MAX_QUEUED 64
 int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof);
 /* Chunks handed out by fc2_caller_next and not yet submitted. */

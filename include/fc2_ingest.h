@@ -53,7 +53,8 @@ const char *fc2_ingest_header(const fc2_ingest *h);
  * empty line; valid until the next call.  *n_handed: fragments in *text.
  * *eof = 1 when the input is exhausted.  Returns FC2_OK or a negative status
  * (FC2_E_FORMAT for malformed input; the reference's UnboundLocalError on
- * single-record input is FC2_E_FORMAT with that message). */
+ * single-record input is FC2_E_FORMAT with that message).  An error met after some fragments
+ * of the call were formed is returned by the following call, after those fragments. */
 int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, fc2_ingest_counts *counts,
                     const char **text, uint64_t *text_len, uint64_t *n_handed, int *eof);
 

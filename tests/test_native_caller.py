@@ -440,3 +440,44 @@ def test_native_reads_gz_members(tmp_path, monkeypatch):
     assert members > 20
     with gzip.open(os.path.join(o1, "spliced_reads.fastq.gz"), "rb") as f:
         assert text == f.read()
+
+
+def _large_sam(tmp_path, n_frag, seed, crlf_every=7, blank_every=997):
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, n_frag, seed=seed)
+    lines = open(sam0).read().splitlines()
+    hdr = [l for l in lines if l.startswith("@")]
+    body = []
+    for k, l in enumerate(l for l in lines if not l.startswith("@")):
+        body.append(l + ("\r" if k % crlf_every == 3 else ""))
+        if k % blank_every == 5:
+            body.append("")
+    return fa, hdr, body
+
+
+@pytest.mark.parametrize("case", ["ok", "no_final_newline", "bad_line_late"])
+def test_native_caller_multi_block_sam(tmp_path, case):
+    """A SAM of several 4 MiB blocks (the native ingest's splitter cuts the input at newlines, two
+    parser threads parse blocks, the loop takes them in order), with CRLF and blank lines: the same
+    files as the Python loop; a malformed line in a late block fails both the same way."""
+    fa, hdr, body = _large_sam(tmp_path, 20000, seed=2718)
+    if case == "bad_line_late":
+        body.insert(int(len(body) * 0.85), "broken\tline")
+    text = "\n".join(hdr + body) + ("" if case == "no_final_newline" else "\n")
+    assert len(text) > (9 << 20)
+    sam = str(tmp_path / "big.sam")
+    open(sam, "w").write(text)
+    o1, o2 = str(tmp_path / "py"), str(tmp_path / "native")
+    rc1 = cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory)
+    rc2 = cli.main(["-G", fa, "-o", o2, "-q", sam], evaluator_factory=oracle_evaluator_factory)
+    assert rc1 == rc2 == (1 if case == "bad_line_late" else 0)
+    if rc1 == 0:
+        same(o1, o2)
+    else:
+        import gzip
+        for f in ("multi_events.tsv",):
+            assert open(os.path.join(o1, f)).read() == open(os.path.join(o2, f)).read()
+        with gzip.open(os.path.join(o1, "spliced_reads.fastq.gz"), "rt") as a, \
+                gzip.open(os.path.join(o2, "spliced_reads.fastq.gz"), "rt") as b:
+            ta, tb = a.read(), b.read()
+        assert ta == tb and len(ta) > 1000
