@@ -1571,7 +1571,8 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
     int rc = FC2_OK;
     try {
         static thread_local FragScratch F;
-        constexpr size_t kAhead = 8;
+        constexpr size_t kAhead = 16;          // sequential profile on the box: 0 / 8 / 16 ahead ->
+                                                // 0.354 / 0.347 / 0.344 s per 2M reads
         for (size_t f = 0; f < h->nfrags; ++f) {
             if (f + kAhead < h->nfrags) prefetch_frag(h, h->frags[f + kAhead], R);
             Frag &fr = h->frags[f];
