@@ -257,7 +257,7 @@ struct fc2_ingest {
         int last_tid = -1;
     } ps;
     std::vector<std::pair<int, int>> ops;
-    std::vector<Rec> pool;       // recycled records: their strings keep their capacity
+    Rec scratch;                 // the record being parsed (sequential path); mates swap theirs back
     // SAM records parsed ahead on threads of their own (native caller pulls, no -B writer): a
     // splitter thread owns the input from then on and cuts it into newline-aligned blocks, parser
     // threads turn blocks into record batches, the consumer takes the batches in input order
@@ -839,8 +839,9 @@ void sam_parse_loop(fc2_ingest *h) {
     }
 }
 
-// the consumer side of next_record: the next parsed record swapped into r
-bool next_ahead(fc2_ingest *h, Rec &r, int &rc) {
+// the consumer side of next_record: the next parsed record, in place in its batch (valid until the
+// next call; open_mate / add_segment swap it out)
+Rec *next_ahead(fc2_ingest *h, int &rc) {
     auto &A = *h->ahead;
     for (;;) {
         if (!A.cur) {
@@ -852,12 +853,9 @@ bool next_ahead(fc2_ingest *h, Rec &r, int &rc) {
             ++A.next_consume;
             A.pos = 0;
         }
-        if (A.pos < A.cur->n) {
-            std::swap(r, A.cur->recs[A.pos++]);
-            return true;
-        }
-        if (A.cur->rc) { rc = fc2::fail(A.cur->rc, A.cur->err); return false; }   // stays: reported again
-        if (A.cur->eof) return false;
+        if (A.pos < A.cur->n) return &A.cur->recs[A.pos++];
+        if (A.cur->rc) { rc = fc2::fail(A.cur->rc, A.cur->err); return nullptr; }   // stays: reported again
+        if (A.cur->eof) return nullptr;
         {
             std::lock_guard<std::mutex> lk(A.m);
             --A.inflight;
@@ -869,7 +867,6 @@ bool next_ahead(fc2_ingest *h, Rec &r, int &rc) {
 
 bool next_record(fc2_ingest *h, Rec &r, int &rc) {
     rc = FC2_OK;
-    if (h->ahead) return next_ahead(h, r, rc);
     if (h->bam) {
         bool got;
         rc = parse_bam_record(h, r, got);
@@ -887,27 +884,27 @@ bool next_record(fc2_ingest *h, Rec &r, int &rc) {
 }
 
 // ---- fragment logic ----------------------------------------------------------
-// records go back to the pool instead of being freed: their strings keep their capacity
+// a mate's records stay in place for reuse (RecList): their strings keep their capacity
 void recycle(fc2_ingest *h, Mate &m) {
-    for (Rec &r : m.recs) h->pool.push_back(std::move(r));
+    (void)h;
     m.recs.clear();
     m.proper.clear();
     m.valid = false;
 }
 
-void open_mate(fc2_ingest *h, Mate &m, Rec &&r) {
+// r's record opens / joins the mate; r gets back a recycled record
+void open_mate(fc2_ingest *h, Mate &m, Rec &r) {
     h->counts.total_mates++;
     recycle(h, m);
-    m.proper.clear();
-    m.recs.push_back(std::move(r));
+    m.recs.take(r);
     m.proper.push_back(0);
     m.valid = true;
 }
 
-void add_segment(Mate &m, Rec &&r) {
+void add_segment(Mate &m, Rec &r) {
     const Rec &p = m.recs[0];
     const bool proper = r.tid == p.tid && r.reverse() == p.reverse();
-    m.recs.push_back(std::move(r));
+    m.recs.take(r);
     if (proper) m.proper.push_back((int)m.recs.size() - 1);
 }
 
@@ -1100,17 +1097,13 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
     uint64_t handed = 0, frags = 0;
     int rc = FC2_OK;
     bool done = h->finished;
-    Rec r;
-    bool moved = true;               // r was handed to a mate: take a recycled one
     while (!done && frags < max_frags) {
-        if (moved) {
-            if (!h->pool.empty()) {
-                r = std::move(h->pool.back());
-                h->pool.pop_back();
-            }
-            moved = false;
-        }
-        if (!next_record(h, r, rc)) {
+        // the next record: in its parse batch, or parsed here into the scratch record
+        Rec *rp = nullptr;
+        rc = FC2_OK;
+        if (h->ahead) rp = next_ahead(h, rc);
+        else if (next_record(h, h->scratch, rc)) rp = &h->scratch;
+        if (!rp) {
             if (rc) return rc;
             // end of input: the final yield (:1486)
             if (h->started) {
@@ -1126,29 +1119,26 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
         }
         h->n_records++;
         h->counts.records++;
+        Rec &r = *rp;
         if (!h->started) {           // first record always opens a mate (:1462-1463)
-            open_mate(h, h->current, std::move(r));
-            moved = true;
+            open_mate(h, h->current, r);
             h->started = true;
             continue;
         }
         if (r.unmapped()) { h->counts.unmapped_reads++; continue; }   // r is reused
         const Rec &prim = h->current.recs[0];
         if (r.read1() == prim.read1() && r.qname == prim.qname) {
-            add_segment(h->current, std::move(r));
-            moved = true;
+            add_segment(h->current, r);
         } else if (r.read1() != prim.read1() && r.qname == prim.qname) {
             std::swap(h->other, h->current);
             h->have_other = true;
-            open_mate(h, h->current, std::move(r));
-            moved = true;
+            open_mate(h, h->current, r);
         } else {
             rc = emit_or_count(h, p, handed, sink);
             ++frags;
             h->have_other = false;
             recycle(h, h->other);
-            open_mate(h, h->current, std::move(r));
-            moved = true;
+            open_mate(h, h->current, r);
             if (rc) return rc;
         }
     }

@@ -6,6 +6,7 @@
 
 #include <functional>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/fc2_ingest.h"
@@ -37,8 +38,31 @@ struct Rec {
     bool reverse() const { return flag & 0x10; }
 };
 
+// A mate's records.  Slots past size() stay constructed: take() swaps a parsed record into the next
+// slot and hands the slot's previous contents (strings with their capacity) back to the caller, so
+// a record is moved once on its way from the parser into a mate, and nothing is freed.
+class RecList {
+  public:
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    Rec &operator[](size_t k) { return v_[k]; }
+    const Rec &operator[](size_t k) const { return v_[k]; }
+    Rec *begin() { return v_.data(); }
+    Rec *end() { return v_.data() + n_; }
+    const Rec *begin() const { return v_.data(); }
+    const Rec *end() const { return v_.data() + n_; }
+    void clear() { n_ = 0; }
+    void take(Rec &r) {
+        if (n_ == v_.size()) v_.emplace_back();
+        std::swap(v_[n_++], r);
+    }
+  private:
+    std::vector<Rec> v_;
+    size_t n_ = 0;
+};
+
 struct Mate {
-    std::vector<Rec> recs;       // primary first, then every added segment (for hand-back)
+    RecList recs;                // primary first, then every added segment (for hand-back)
     std::vector<int> proper;     // indices into recs
     bool valid = false;
 };
