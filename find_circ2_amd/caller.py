@@ -31,8 +31,9 @@ _COMP = {'a': 't', 't': 'a', 'c': 'g', 'g': 'c', 'k': 'm', 'm': 'k', 'r': 'y', '
 
 
 def rev_comp(seq: str) -> str:
-    """find_circ.py:54-58 (KeyError on bytes outside the IUPAC table, as there)."""
-    return "".join(_COMP[c] for c in reversed(seq))
+    """find_circ.py:54-58: complement() walks the sequence forward, so the KeyError names the first
+    byte outside the IUPAC table."""
+    return "".join([_COMP[c] for c in seq])[::-1]
 
 
 def py2_str(v) -> str:

@@ -88,16 +88,21 @@ struct CompTable {                             // comp() as a byte table
 };
 const CompTable kComp;
 
+// complement() walks the sequence forward (find_circ.py:54-55): a KeyError names the first byte
+// outside the table
+void check_comp(const std::string &s) {
+    const unsigned char *in = (const unsigned char *)s.data();
+    for (size_t k = 0; k < s.size(); ++k)
+        if (!kComp.t[in[k]]) throw Fatal{FC2_E_KEY, std::string("KeyError: ") + py_repr(std::string(1, (char)in[k]))};
+}
+
 void rev_comp_into(const std::string &s, std::string &r) {
+    check_comp(s);
     const size_t n = s.size();
     r.resize(n);
     const unsigned char *in = (const unsigned char *)s.data();
     char *out = &r[0];
-    for (size_t k = 0; k < n; ++k) {
-        const char c = kComp.t[in[n - 1 - k]];
-        if (!c) throw Fatal{FC2_E_KEY, std::string("KeyError: ") + py_repr(std::string(1, (char)in[n - 1 - k]))};
-        out[k] = c;
-    }
+    for (size_t k = 0; k < n; ++k) out[k] = kComp.t[in[n - 1 - k]];
 }
 
 std::string rev_comp(const std::string &s) {
@@ -323,11 +328,8 @@ struct StrSet {
 struct CanonSet {
     StrSet canon;
     int64_t palindromes = 0;
-    void insert(const std::string &read, const std::string &rc, Arena &a) {
-        const bool pal = read == rc;
-        const std::string &c = pal || read < rc ? read : rc;
-        if (canon.insert(c, a) && pal) palindromes += 1;
-    }
+    // read must hold table bytes only (check_comp); rc(read) is built only when it is the smaller
+    void insert(const std::string &read, Arena &a);
     int64_t size() const { return 2 * (int64_t)canon.size() - palindromes; }
 };
 
@@ -541,17 +543,34 @@ void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
     return;
 }
 
+void CanonSet::insert(const std::string &read, Arena &a) {
+    const size_t n = read.size();
+    const unsigned char *in = (const unsigned char *)read.data();
+    int cmp = 0;                                // read vs rc(read), bytewise as std::string compares
+    for (size_t k = 0; k < n && !cmp; ++k) {
+        const unsigned char x = in[k], y = (unsigned char)kComp.t[in[n - 1 - k]];
+        cmp = x < y ? -1 : (x > y ? 1 : 0);
+    }
+    if (cmp <= 0) {
+        if (canon.insert(read, a) && cmp == 0) palindromes += 1;
+        return;
+    }
+    static thread_local std::string rc;
+    rc.resize(n);
+    for (size_t k = 0; k < n; ++k) rc[k] = kComp.t[in[n - 1 - k]];
+    canon.insert(rc, a);
+}
+
 // the span-dependent part of Hit.add that needs the fragment's primary
 void hit_add_read(fc2_caller *h, int kind, Hit &t, const Span &s, const Align &prim) {
     Arena &a = h->st[kind].strings;
     t.readnames.insert(prim.qname, a);
     const std::string &read = prim.seq;
-    static thread_local std::string rc;
-    rev_comp_into(read, rc);
+    check_comp(read);                           // rev_comp(read) raises here (:573, :582)
     t.n_reads += 1;
     t.has_tissue = true;
     t.tissue += s.weight;
-    t.uniq.insert(read, rc, a);
+    t.uniq.insert(read, a);
 }
 
 // the junction's name (find_circ.py:684-686), appended to out
@@ -1198,7 +1217,8 @@ struct FragScratch {
     std::vector<size_t> circ_idx, lin_idx;      // distinct circ / linear junctions (their coords)
     std::vector<std::pair<int, size_t>> junc;   // every junction the fragment's reads support
     uint32_t warns = 0;                         // Warn bits
-    std::vector<std::string> names;             // write_read
+    std::vector<std::string> names;             // write_read: the junction names, sorted
+    std::string tail;                           // ... and the name part both mates share
     void reset() { n_ev = 0; circ_idx.clear(); lin_idx.clear(); junc.clear(); warns = 0; }
 };
 
@@ -1357,9 +1377,8 @@ void prefetch_frag(const fc2_caller *h, const Frag &fr, const Results &R) {
     }
 }
 
-void write_read(fc2_caller *h, const Align &m, FragScratch &F) {       // :1442-1447
-    if (!h->o.write_reads) return;
-    // '@<qname> <sorted junction names> <sorted flags>' , seq, '+' + the same name, qual
+// ' <sorted junction names> <sorted flags>': the part of the read names both mates share
+void read_name_tail(fc2_caller *h, FragScratch &F) {
     const size_t nj = F.junc.size();
     if (F.names.size() < nj) F.names.resize(nj);
     for (size_t k = 0; k < nj; ++k) {
@@ -1367,19 +1386,25 @@ void write_read(fc2_caller *h, const Align &m, FragScratch &F) {       // :1442-
         hit_name(h, F.junc[k].first, h->st[F.junc[k].first].hits[F.junc[k].second], F.names[k]);
     }
     if (nj > 1) std::sort(F.names.begin(), F.names.begin() + (std::ptrdiff_t)nj);
+    std::string &t = F.tail;
+    t.assign(1, ' ');
+    for (size_t k = 0; k < nj; ++k) {
+        if (k) t += ',';
+        t += F.names[k];
+    }
+    t += ' ';
+    bool first = true;
+    for (uint32_t w = 0; w < kNumWarn; ++w)
+        if (F.warns & (1u << w)) { if (!first) t += ','; t += kWarnName[w]; first = false; }
+}
+
+void write_read(fc2_caller *h, const Align &m, const FragScratch &F) {       // :1442-1447
+    // '@<qname> <sorted junction names> <sorted flags>' , seq, '+' + the same name, qual
     std::string &o = h->out[0];
     o += '@';
     const size_t n0 = o.size();
     o += m.qname;
-    o += ' ';
-    for (size_t k = 0; k < nj; ++k) {
-        if (k) o += ',';
-        o += F.names[k];
-    }
-    o += ' ';
-    bool first = true;
-    for (uint32_t w = 0; w < kNumWarn; ++w)
-        if (F.warns & (1u << w)) { if (!first) o += ','; o += kWarnName[w]; first = false; }
+    o += F.tail;
     const size_t n1 = o.size();
     o += '\n';
     o += m.has_seq ? m.seq : std::string("None");
@@ -1578,8 +1603,9 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
             Frag &fr = h->frags[f];
             record_hits(h, fr, R, F);
             if (!F.junc.empty()) {
-                if (fr.has[0]) write_read(h, fr.prim[0], F);
-                if (fr.has[1]) write_read(h, fr.prim[1], F);
+                if (h->o.write_reads) read_name_tail(h, F);
+                if (h->o.write_reads && fr.has[0]) write_read(h, fr.prim[0], F);
+                if (h->o.write_reads && fr.has[1]) write_read(h, fr.prim[1], F);
             }
         }
     } catch (const Fatal &f) {

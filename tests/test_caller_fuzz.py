@@ -191,3 +191,34 @@ def test_sam_and_bam_inputs_agree_on_mutated_input(tmp_path, seed):
     if rcs[0] == 0:
         same(outs[0], outs[1])
         same(outs[0], outs[2])
+
+
+def test_rev_comp_keyerror_names_first_bad_byte(tmp_path):
+    """Hit.add's rev_comp (find_circ.py:54-58, :573/:582) complements the read forward, so a read
+    with two bytes outside the table raises KeyError for the first one.  The breakpoint search
+    compares bytes (the pair takes the byte path) and still finds the junction, so the failure
+    comes from Hit.add, in all three loops."""
+    from samgen import sam_text
+    from test_cli import _reads
+    from find_circ2_amd.caller import rev_comp
+    with pytest.raises(KeyError) as e:
+        rev_comp("AC=GT.A")
+    assert e.value.args[0] == "="
+    fa = os.path.join(os.path.dirname(__file__), "golden", "CDR1as_locus.fa")
+    reads = _reads(os.path.join(os.path.dirname(__file__), "golden", "cdr1as_reads.fa"))
+    from bwa_emul import read_fasta
+    lines = sam_text(read_fasta(fa), reads).splitlines()
+    out, hit = [], False
+    for l in lines:
+        f = l.split("\t")
+        if not hit and not l.startswith("@") and re.match(r"^\d+M\d+S$", f[5]) and int(f[1]) & 0x900 == 0:
+            # the primary of a spliced read: two of its first bases become bytes outside the table
+            f[9] = "=" + f[9][1:4] + "." + f[9][5:]
+            hit = True
+        out.append("\t".join(f))
+    assert hit
+    sam = str(tmp_path / "junk.sam")
+    open(sam, "w").write("\n".join(out) + "\n")
+    rc, outs = _agree(tmp_path, fa, sam, [])
+    logs = [open(os.path.join(o, "run.log")).read() for o in outs]
+    assert rc == 1 and all("KeyError: '='" in l for l in logs), [l[-300:] for l in logs]
