@@ -170,3 +170,22 @@ def test_gpu_bam_out_equals_oracle(tmp_path, gpus):
     b1 = read_bam(os.path.join(o1, "spliced_alignments.bam"))
     b2 = read_bam(os.path.join(o2, "spliced_alignments.bam"))
     assert len(b1[2]) > 1000 and b1 == b2
+
+
+def test_gpu_cli_multi_block_sam(tmp_path):
+    """A 9 MiB SAM (several 4 MiB blocks for the splitter and the two parser threads) through the
+    shipped CLI with the HIP scan on two scanners: the same files as the Python loop + oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd import cli
+    from oracle_engine import oracle_evaluator_factory
+    from test_ingest import same
+    from test_native_caller import _large_sam
+    fa, hdr, body = _large_sam(tmp_path, 20000, seed=31415)
+    sam = str(tmp_path / "big.sam")
+    open(sam, "w").write("\n".join(hdr + body) + "\n")
+    assert os.path.getsize(sam) > (9 << 20)
+    o1, o2 = str(tmp_path / "oracle_py"), str(tmp_path / "gpu")
+    assert cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    assert cli.main(["-G", fa, "-o", o2, "-q", "--gpus", "2", sam]) == 0
+    same(o1, o2)
