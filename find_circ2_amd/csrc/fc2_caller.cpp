@@ -378,7 +378,7 @@ struct FlagReads {
 struct Hit {                                   // Hit (:486-654)
     int64_t novel = 0;                         // > 0: named <name>_<prefix>_<novel:06d> (:684-686)
     std::string known_name;                    // novel == 0: the name a known-sites file gave
-    Coord coord;
+    CKey key;                                  // the coordinate (chrom, start, end, strand) as ids
     int64_t n_reads = 0;
     StrSet readnames;
     CanonSet uniq;
@@ -388,8 +388,9 @@ struct Hit {                                   // Hit (:486-654)
     int64_t n_spanned = 0;
     double n_uniq_bridges = 0.;
     PyMin edits, overlaps, n_hits;
-    std::string signal = "NNNN", strandmatch = "NA";
-    int64_t flag_n[kNumWarn] = {};             // Hit.flags: count per flag (present iff > 0)
+    std::string signal = "NNNN";
+    bool added = false;                        // Hit.add ran: strandmatch 'N/A' (else 'NA', :504, :532)
+    uint32_t flag_n[kNumWarn] = {};            // Hit.flags: count per flag (present iff > 0)
     FlagReads read_flags;
     bool has_tissue = false;
     double tissue = 0.;
@@ -480,6 +481,7 @@ struct fc2_caller {
         int64_t novel = 0;
     } st[2];                                    // 0 circ, 1 lin
     std::unordered_map<std::string, uint32_t> ids;    // interned chromosome / strand strings (submit side)
+    std::vector<std::string> id_names;                // ... and back
     std::vector<int64_t> tid_cid;                     // reference id -> interned chromosome (submit side)
     std::vector<std::pair<const char *, double>> N;   // the reference's counters, keyed by literal
                                                       // (merged by name into sorted keys on output)
@@ -509,6 +511,7 @@ uint32_t intern(fc2_caller *h, const std::string &v) {
     if (it != h->ids.end()) return it->second;
     const uint32_t id = (uint32_t)h->ids.size();
     h->ids.emplace(v, id);
+    h->id_names.push_back(v);
     return id;
 }
 
@@ -524,10 +527,18 @@ CKey coord_key(fc2_caller *h, const Splice &sp) {
                              : CKey{sp.end, sp.start, c, strand_id(h, sp.strand)};
 }
 
+// a junction's coordinate strings back from its key
+const std::string &key_chrom(const fc2_caller *h, const CKey &k) { return h->id_names[k.chrom]; }
+const std::string &key_strand(const fc2_caller *h, const CKey &k) {
+    static const std::string plus("+"), minus("-");
+    return k.strand == 0 ? plus : k.strand == 1 ? minus : h->id_names[k.strand - 2];
+}
+Coord key_coord(const fc2_caller *h, const CKey &k) { return Coord(key_chrom(h, k), k.start, k.end, key_strand(h, k)); }
+
 // ---- Hit / SpliceSiteStorage ----------------------------------------------------------
 void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
     t.signal = sp.gtag;
-    t.strandmatch = "N/A";
+    t.added = true;
     if (h->o.stranded)   // Splice has no strandmatch attribute (:532-533)
         throw Fatal{FC2_E_FORMAT, "AttributeError: 'Splice' object has no attribute 'strandmatch'"};
     t.edits.add(sp.dist, sp.dist_bool);
@@ -595,13 +606,14 @@ std::string hit_name(const fc2_caller *h, int kind, const Hit &t) {
 
 size_t storage_add(fc2_caller *h, int kind, const Splice &sp, const Align *prim) {
     auto &S = h->st[kind];
-    const auto ins = S.index.try_emplace(coord_key(h, sp), S.hits.size());
+    const CKey key = coord_key(h, sp);
+    const auto ins = S.index.try_emplace(key, S.hits.size());
     const size_t k = ins.first;
     if (ins.second) {                           // a new junction: named by first appearance (:684-686)
         S.novel += 1;
         Hit &t = S.hits.emplace_back();
         t.novel = S.novel;
-        t.coord = sp.coord();
+        t.key = key;
         hit_add(h, t, sp);
     } else {
         hit_add(h, S.hits[k], sp);
@@ -630,7 +642,7 @@ int categories(const fc2_caller *h, const Hit &t, const char *cats[8]) {
     } else if (mov >= 2 || med >= 2) {
         cats[n++] = "WARN_EXT_2MM+";
     }
-    const int64_t start = std::get<1>(t.coord), end = std::get<2>(t.coord);
+    const int64_t start = t.key.start, end = t.key.end;
     if (end - start < o.short_threshold) cats[n++] = "SHORT";
     else if (end - start > o.huge_threshold) cats[n++] = "HUGE";
     int64_t unbroken = 0, unwarned = 0;
@@ -695,12 +707,12 @@ void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :69
         if (t.n_uniq_bridges == 0 && !o.report_nobridges) { incN(h, "no_uniq_bridges"); continue; }
         // the 22 columns of find_circ.py:712-730, appended in place
         const char tab = '\t';
-        outs += std::get<0>(t.coord); outs += tab;
-        app_int(outs, std::get<1>(t.coord)); outs += tab;
-        app_int(outs, std::get<2>(t.coord)); outs += tab;
+        outs += key_chrom(h, t.key); outs += tab;
+        app_int(outs, t.key.start); outs += tab;
+        app_int(outs, t.key.end); outs += tab;
         hit_name(h, kind, t, outs); outs += tab;
         app_int(outs, (int64_t)t.readnames.size()); outs += tab;
-        outs += std::get<3>(t.coord); outs += tab;
+        outs += key_strand(h, t.key); outs += tab;
         app_py2_float(outs, t.n_weighted); outs += tab;
         app_int(outs, t.n_spanned); outs += tab;
         app_int(outs, t.uniq.size() / 2); outs += tab;
@@ -715,7 +727,7 @@ void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :69
         app_pymin(outs, t.overlaps); outs += tab;
         app_pymin(outs, t.n_hits); outs += tab;
         outs += t.signal; outs += tab;
-        outs += t.strandmatch; outs += tab;
+        outs += t.added ? "N/A" : "NA"; outs += tab;
         const char *cats[8];
         const int nc = categories(h, t, cats);
         std::sort(cats, cats + nc, [](const char *x, const char *y) { return strcmp(x, y) < 0; });
@@ -785,7 +797,7 @@ uint64_t load_known(fc2_caller *h, int kind, const std::string &path) {
         Hit &t = ins.second ? S.hits.emplace_back() : S.hits[ins.first];
         t = Hit();
         t.known_name = fl[3];
-        t.coord = sp.coord();
+        t.key = key;
         hit_add(h, t, sp);
         ++n;
     }
@@ -941,10 +953,13 @@ void decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
     ev.ties.clear();
     const Span &s = h->spans[si];
     const fc2_pair &pr = h->b_pairs[(size_t)s.eval];
-    const std::string chrom = chrom_of(h, s.tid);
-    if ((size_t)s.tid >= h->tid_cid.size()) h->tid_cid.resize((size_t)s.tid + 1, -1);
-    int64_t &cid = h->tid_cid[(size_t)s.tid];
-    if (cid < 0) cid = intern(h, chrom);
+    if (s.tid < 0 || (size_t)s.tid >= h->tid_cid.size() || h->tid_cid[(size_t)s.tid] < 0) {
+        const std::string name = chrom_of(h, s.tid);        // raises for an id outside the header
+        if ((size_t)s.tid >= h->tid_cid.size()) h->tid_cid.resize((size_t)s.tid + 1, -1);
+        h->tid_cid[(size_t)s.tid] = intern(h, name);
+    }
+    const int64_t cid = h->tid_cid[(size_t)s.tid];
+    const std::string &chrom = h->id_names[(size_t)cid];    // (nothing below interns a new name)
     if (pr.flags & FC2_PAIR_SKIP) {            // chromosome missing from the genome (get_data, :193)
         ev.err = FC2_E_KEY;
         ev.msg = "KeyError: " + py_repr(chrom);
@@ -1181,9 +1196,8 @@ std::string multi_row(fc2_caller *h, const Frag &fr, const Hit &circ, const std:
                       const std::set<UCoord> &un_incons) {                    // :733-763
     const int64_t score = (int64_t)lin_cons.size() - 10 * (int64_t)lin_incons.size() + (int64_t)un_cons.size() -
                           10 * (int64_t)un_incons.size();
-    std::vector<std::string> cols = {std::get<0>(circ.coord), i2s(std::get<1>(circ.coord)),
-                                     i2s(std::get<2>(circ.coord)), "ME:" + hit_name(h, 0, circ), i2s(score),
-                                     std::get<3>(circ.coord), fr.name};
+    std::vector<std::string> cols = {key_chrom(h, circ.key), i2s(circ.key.start), i2s(circ.key.end),
+                                     "ME:" + hit_name(h, 0, circ), i2s(score), key_strand(h, circ.key), fr.name};
     std::vector<std::string> v;
     for (const Coord &c : lin_cons) v.push_back(i2s(std::get<1>(c)) + "-" + i2s(std::get<2>(c)));
     cols.push_back(v.empty() ? "NO_LIN_CONS" : join(v, ","));
@@ -1284,9 +1298,9 @@ void record_hits(fc2_caller *h, Frag &fr, const Results &R, FragScratch &F) {
     int64_t circ_start = 0, circ_end = 0;
     int circ_span = -1;
     if (!F.circ_idx.empty()) {
-        const Coord &cc = h->st[0].hits[circ.second].coord;
-        circ_start = std::get<1>(cc);
-        circ_end = std::get<2>(cc);
+        const CKey &cc = h->st[0].hits[circ.second].key;
+        circ_start = cc.start;
+        circ_end = cc.end;
         circ_span = fr.circ[0];
         if (fr.circ.size() > 1) F.warns |= 1u << W_SUPPORT_CLOSURE;
     }
@@ -1327,8 +1341,8 @@ void record_hits(fc2_caller *h, Frag &fr, const Results &R, FragScratch &F) {
         for (const APos &a : fr.unspliced) un.push_back(coords(a));
         for (const APos &a : fr.broken) br.push_back(coords(a));
         std::set<Coord> lin_coords, circ_coords;
-        for (size_t idx : F.lin_idx) lin_coords.insert(h->st[1].hits[idx].coord);
-        for (size_t idx : F.circ_idx) circ_coords.insert(h->st[0].hits[idx].coord);
+        for (size_t idx : F.lin_idx) lin_coords.insert(key_coord(h, h->st[1].hits[idx].key));
+        for (size_t idx : F.circ_idx) circ_coords.insert(key_coord(h, h->st[0].hits[idx].key));
         h->out[2] += test_row(h, fr, lin_coords, circ_coords, un, br);
     }
     if (!F.circ_idx.empty()) {
