@@ -132,12 +132,13 @@ APos apos_of(const Rec &r) {
     return a;
 }
 
-// assign in place: a recycled Align keeps its strings' capacity (no allocation per fragment)
-void set_align(Align &a, const Rec &r) {
+// the primary's strings are swapped in, not copied: the record gets the recycled Align's buffers
+// back (the ingest reads nothing of a handed-over fragment's records, FragSink)
+void take_align(Align &a, Rec &r) {
     static_cast<APos &>(a) = apos_of(r);
-    a.qname.assign(r.qname);
-    a.seq.assign(r.seq);
-    a.qual.assign(r.qual);
+    a.qname.swap(r.qname);
+    a.seq.swap(r.seq);
+    a.qual.swap(r.qual);
     a.has_seq = r.has_seq;
     a.has_qual = r.has_qual;
 }
@@ -901,7 +902,7 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
     }
 }
 
-int on_fragment(fc2_caller *h, const Mate *m1, const Mate *m2) {
+int on_fragment(fc2_caller *h, Mate *m1, Mate *m2) {
     // the next slot of the chunk; a recycled Frag is reset field by field (capacity kept)
     if (h->bf_nfrags == h->bf_frags.size()) h->bf_frags.emplace_back();
     Frag &fr = h->bf_frags[h->bf_nfrags];
@@ -910,13 +911,13 @@ int on_fragment(fc2_caller *h, const Mate *m1, const Mate *m2) {
     fr.lin.clear();
     fr.unspliced.clear();
     fr.broken.clear();
-    const Mate *ms[2] = {m1, m2};
+    Mate *ms[2] = {m1, m2};
     const size_t span0 = h->bf_spans.size(), arena0 = h->bf_arena.size();
     for (int k = 0; k < 2; ++k) {
         fr.has[k] = ms[k] != nullptr;
         if (!ms[k]) continue;
-        set_align(fr.prim[k], ms[k]->recs[0]);
-        process_mate(h, *ms[k], k, fr);
+        process_mate(h, *ms[k], k, fr);          // reads the records first
+        take_align(fr.prim[k], ms[k]->recs[0]);
     }
     if ((fr.circ.empty() && h->o.nolinear) || (fr.circ.empty() && fr.lin.empty())) {
         h->bf_spans.resize(span0);                // not pending: its spans are never evaluated
@@ -1511,7 +1512,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     h->bf_off.clear();
     h->bf_pairs.clear();
     Fatal err{0, ""};
-    const fc2::ing::FragSink sink = [&](const Mate *m1, const Mate *m2, bool) -> int {
+    const fc2::ing::FragSink sink = [&](Mate *m1, Mate *m2, bool) -> int {
         try {
             return on_fragment(h, m1, m2);
         } catch (const Fatal &f) {

@@ -1010,7 +1010,7 @@ int emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed,
     }
     ++n_handed;
     h->counts.handed_back++;
-    if (sink) return (*sink)(mates[0], mates[1], must);
+    if (sink) return (*sink)(h->have_other ? &h->other : nullptr, &h->current, must);
     for (int k = 0; k < 2; ++k) {
         if (!mates[k]) continue;
         for (const Rec &r : mates[k]->recs) { h->out += r.text; h->out += '\n'; }

@@ -69,7 +69,9 @@ struct Mate {
 
 // Fragments that carry anchor pairs (or that the reference would fail on: must_see) are passed
 // to the sink in input order; m1 = the other mate (may be null), m2 = the current mate.
-using FragSink = std::function<int(const Mate *m1, const Mate *m2, bool must_see)>;
+// The sink may take the mates' strings (swap them out): the loop reads nothing of a fragment's
+// records after handing it over.
+using FragSink = std::function<int(Mate *m1, Mate *m2, bool must_see)>;
 
 // The loop of fc2_ingest_next with a sink instead of SAM text; a non-zero return of the sink
 // stops the loop and is returned.
