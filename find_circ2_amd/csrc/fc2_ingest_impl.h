@@ -14,18 +14,15 @@
 namespace fc2 {
 namespace ing {
 
-struct Rec {
-    std::string text;      // SAM line (no newline): for the Python hand-back and the -B writer
-    std::string raw;       // BAM input with a -B writer: block_size + record bytes
-    std::string qname;
+// the plain fields of a record (swapped as one block, see swap(Rec &, Rec &))
+struct RecFields {
     uint32_t flag = 0;
     int32_t tid = -1;
     int64_t pos = -1;
     int64_t aend = -1;     // -1: None (unmapped / no cigar)
     int32_t astart = 0;    // aligned_start_from_cigar (:1086-1097)
     int32_t qlen = -1;     // len(query); -1: query is None (SEQ '*')
-    bool has_seq = false;
-    std::string seq, qual;  // SEQ / QUAL ("*" -> has_seq false / has_qual false)
+    bool has_seq = false;  // SEQ / QUAL "*" -> false
     bool has_qual = false;
     // AS / XS tags as pysam's get_tag returns them: present?, integer-typed?, value
     bool has_as = false, has_xs = false, as_int = true, xs_int = true;
@@ -33,10 +30,28 @@ struct Rec {
     // the LAST occurrence of each, as dict(read.tags) gives it (Hit.add, find_circ.py:556-557)
     bool as_last_int = true, xs_last_int = true;
     int64_t as_last = 0, xs_last = 0;
+};
+
+struct Rec : RecFields {
+    std::string text;      // SAM line (no newline): for the Python hand-back and the -B writer
+    std::string raw;       // BAM input with a -B writer: block_size + record bytes
+    std::string qname;
+    std::string seq, qual;  // SEQ / QUAL
     bool unmapped() const { return flag & 0x4; }
     bool read1() const { return flag & 0x40; }
     bool reverse() const { return flag & 0x10; }
 };
+
+// member-wise: the strings swap their buffers, the plain fields swap as one block (cheaper than
+// std::swap's three moves of every member)
+inline void swap(Rec &a, Rec &b) noexcept {
+    std::swap(static_cast<RecFields &>(a), static_cast<RecFields &>(b));
+    a.text.swap(b.text);
+    a.raw.swap(b.raw);
+    a.qname.swap(b.qname);
+    a.seq.swap(b.seq);
+    a.qual.swap(b.qual);
+}
 
 // A mate's records.  Slots past size() stay constructed: take() swaps a parsed record into the next
 // slot and hands the slot's previous contents (strings with their capacity) back to the caller, so
@@ -54,7 +69,7 @@ class RecList {
     void clear() { n_ = 0; }
     void take(Rec &r) {
         if (n_ == v_.size()) v_.emplace_back();
-        std::swap(v_[n_++], r);
+        swap(v_[n_++], r);
     }
   private:
     std::vector<Rec> v_;
