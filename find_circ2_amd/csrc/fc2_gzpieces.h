@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <zlib.h>
 
+#include <algorithm>
 #include <condition_variable>
 #include <deque>
 #include <memory>
@@ -37,16 +38,24 @@ class GzPieces {
         return true;
     }
 
-    // takes the bytes of text (text is left empty); whole pieces go to the workers
+    // takes the bytes of text (text is left empty, its capacity kept for the caller's next chunk);
+    // whole pieces go to the workers, each byte is copied once
     void append(std::string &text) {
-        if (buf_.empty()) buf_.swap(text);
-        else { buf_ += text; text.clear(); }
         size_t at = 0;
-        while (buf_.size() - at >= piece_) {
-            submit(buf_.substr(at, piece_));
+        if (!buf_.empty()) {                    // top up the partial piece left by the last call
+            at = std::min(piece_ - buf_.size(), text.size());
+            buf_.append(text, 0, at);
+            if (buf_.size() >= piece_) {
+                submit(std::move(buf_));
+                buf_.clear();
+            }
+        }
+        while (text.size() - at >= piece_) {
+            submit(text.substr(at, piece_));
             at += piece_;
         }
-        if (at) buf_.erase(0, at);
+        buf_.append(text, at, std::string::npos);
+        text.clear();
     }
 
     // compresses what is left, writes every member, stops the workers; false on a write error
