@@ -481,3 +481,24 @@ def test_native_caller_multi_block_sam(tmp_path, case):
                 gzip.open(os.path.join(o2, "spliced_reads.fastq.gz"), "rt") as b:
             ta, tb = a.read(), b.read()
         assert ta == tb and len(ta) > 1000
+
+
+def test_native_reads_gz_unwritable_path(tmp_path):
+    """fc2_caller_set_reads_gz on a path that cannot be created fails at open (FC2_E_IO), before
+    any input is read."""
+    from find_circ2_amd import _native as N
+    from find_circ2_amd.native_caller import NativeCaller
+    from oracle_engine import oracle_batch_engine
+    from find_circ2_amd.hotpath import Options as HPOptions
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 20, seed=5)
+    options, _ = cli.build_parser().parse_args(["-G", fa, "-o", str(tmp_path / "o"), sam])
+    hp = HPOptions(asize=options.asize, margin=options.margin, maxdist=options.maxdist)
+    _, names, fasta, dummy = oracle_batch_engine(options, hp)
+    nc = NativeCaller(sam, False, options, names, fasta, genome_dummy=dummy,
+                      reads_gz=(str(tmp_path / "no_such_dir" / "r.fastq.gz"), 2, 2, 0))
+    try:
+        with pytest.raises(N.Fc2Error):
+            nc.open()
+    finally:
+        nc.close()
