@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
     ap.add_argument("--no-strong", action="store_true", help="skip the configs[3] strong-scaling / ordered-merge run")
     ap.add_argument("--no-config4", action="store_true", help="skip the configs[4] 200M x 120-150 bp run")
+    ap.add_argument("--no-cli", action="store_true", help="skip the end-to-end CLI extra (2M reads from SAM)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     return ap.parse_args()
@@ -781,6 +782,54 @@ def window_carrying(opt, g, b, steps, dev, bpp):
     return out
 
 
+def cli_end_to_end(reads=2_000_000):
+    """The product end to end (an extra, never `value`): scripts/cli_scale_check.py's generator writes an
+    hg19-shaped genome FASTA and a bwa-mem-like SAM of `reads` reads, then `python -m find_circ2_amd.cli`
+    runs as its own process (C++ read loop on two threads + SAM parser threads, HIP search through
+    pipeline.ScanPipeline, gzip members on worker threads).  The first run builds the .byo_index; the
+    second is reported: the loop's own reads/s (run.log) and the process wall time."""
+    import re
+    import shutil
+    import subprocess
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from cli_scale_check import make_genome, write_fasta, write_sam
+    from find_circ2_amd import sq_table
+    d = tempfile.mkdtemp(prefix="fc2_bench_cli_", dir="/tmp")
+    try:
+        fa, sam = os.path.join(d, "genome.fa"), os.path.join(d, "reads.sam")
+        rng = np.random.default_rng(2024)
+        names, sizes = sq_table(os.path.join(ROOT, "tests", "golden", "test_norm.sam"))
+        seqs = make_genome(fa, names, sizes, rng)
+        write_sam(sam, seqs, reads, rng)
+        write_fasta(fa, seqs)
+        del seqs
+        res = {}
+        for k in range(2):
+            out = os.path.join(d, "out%d" % k)
+            t0 = time.time()
+            rc = subprocess.run([sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", out, "-q", sam],
+                                cwd=ROOT, timeout=600).returncode
+            wall = time.time() - t0
+            if rc != 0:
+                return {"error": "cli exit status %d" % rc}
+            log = open(os.path.join(out, "run.log")).read()
+            m = re.search(r"overall ([0-9.]+)k reads/second", log)
+            st = re.search(r"read loop stages: (.*)", log)
+            res = {"value": round(float(m.group(1)) * 1e3, 1) if m else None, "unit": "reads/s",
+                   "process_wall_s": round(wall, 2), "reads": reads,
+                   "stages": st.group(1) if st else None}
+        res["note"] = ("whole CLI from SAM on an hg19-shaped genome (2nd run, .byo_index present): value = the "
+                       "read loop's reads/s from run.log; process_wall_s includes interpreter start, genome load "
+                       "and upload; outputs are checked against the Python loop in tests and "
+                       "scripts/cli_scale_check.py, not here")
+        return res
+    except Exception as e:          # an extra must not cost the bench line
+        return {"error": repr(e)}
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
+
+
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -918,6 +967,10 @@ def main():
             "note": "25M pairs (the per-GPU share of configs[4]'s 200M over 8 GPUs), read lengths uniform in "
                     "120..150 bp (anchors of varying length, SURVEY.md 8(d) config 5), hg19-shaped genome, read order; algorithmic bytes "
                     "priced at 150 bp (%d B)" % bpp4}
+        del b4, g4
+        torch.cuda.empty_cache()
+        if not args.no_cli:
+            line["extra"]["cli_end_to_end_2M_reads"] = cli_end_to_end()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if ws > 1:
