@@ -493,6 +493,7 @@ struct fc2_caller {
     std::string rows_text;
     std::vector<std::pair<std::string, double>> counters_snapshot;
     uint64_t n_pairs = 0;
+    uint64_t n_chunks = 0;                      // chunks formed (next side)
 };
 
 namespace {
@@ -1520,9 +1521,13 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             return f.code ? f.code : FC2_E_FORMAT;
         }
     };
-    while (!h->eof && h->bf_nfrags < h->o.chunksize) {
+    // the first chunks ramp up (1/16, 1/8, 1/4, 1/2 of chunksize): the recording side starts early
+    // instead of waiting for a whole first chunk; chunk boundaries change nothing in the outputs
+    const uint64_t limit = std::max<uint64_t>(1, (uint64_t)h->o.chunksize >> (h->n_chunks < 4 ? 4 - h->n_chunks : 0));
+    ++h->n_chunks;
+    while (!h->eof && h->bf_nfrags < limit) {
         int e = 0;
-        const int rc = fc2::ing::pull(h->ing, &h->ip, h->o.chunksize, sink, &e);
+        const int rc = fc2::ing::pull(h->ing, &h->ip, limit, sink, &e);
         if (rc) {
             const int code = err.code ? err.code : rc;
             const std::string msg = err.code ? err.msg : std::string(fc2_last_error());
