@@ -122,6 +122,7 @@ EXPORTED = [
     # include/fc2_ingest.h
     "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
     "fc2_ingest_next", "fc2_ingest_counts_get", "fc2_ingest_set_bam_out", "fc2_ingest_close_bam_out",
+    "fc2_ingest_format",
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
     "fc2_caller_submit", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
@@ -231,6 +232,7 @@ def lib() -> ctypes.CDLL:
         "fc2_ingest_counts_get": (ctypes.c_int, [vp, P(IngestCounts)]),
         "fc2_ingest_set_bam_out": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "fc2_ingest_close_bam_out": (ctypes.c_int, [vp]),
+        "fc2_ingest_format": (ctypes.c_int, [vp, P(ctypes.c_int)]),
         "fc2_caller_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(CallerOpts), P(vp)]),
         "fc2_caller_set_genome": (ctypes.c_int, [vp, vp, i32, vp, P(u64), P(u64)]),
         "fc2_caller_ingest": (vp, [vp]),

@@ -161,7 +161,9 @@ def main(argv=None, evaluator_factory=None) -> int:
         evaluate = evaluator_factory(options, hp)
 
     path = args[0] if args else "-"
-    is_bam = bool(args) and not args[0].endswith("sam")          # find_circ.py:461-469
+    # the reference's pysam mode ('r' for stdin and *sam names, else 'rb', find_circ.py:461-469) is only a
+    # hint: as htslib does, both readers detect BAM / SAM and BGZF / gzip / plain from the bytes themselves
+    is_bam = bool(args) and not args[0].endswith("sam")
     logger.info('reading from {0}'.format(args[0]) if args else 'reading from stdin')
     if not (options.python_ingest or options.python_caller):
         return _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path)

@@ -11,6 +11,7 @@
 #include <emmintrin.h>
 #include <errno.h>
 #include <fcntl.h>
+#include <poll.h>
 #include <stdio.h>
 #include <string.h>
 #include <unistd.h>
@@ -213,8 +214,16 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
 
 struct fc2_ingest {
     int fd = -1;
+    // what the bytes are, detected from the bytes themselves (never from the file name), as
+    // htslib's hts_detect_format does for pysam.Samfile(path_or_'-', 'r'|'rb') (find_circ.py:461-469):
+    // the byte source (plain, BGZF blocks, or any other gzip stream) and, below it, BAM or SAM text
+    enum Src { SRC_RAW, SRC_BGZF, SRC_GZIP } src = SRC_RAW;
     bool bam = false;
     bool eof_in = false;
+    // an input error met by the sequential reader (read(2) failure, corrupt gzip stream); reported
+    // after the records before it, where the input ends
+    int in_rc = 0;
+    std::string in_err;
     // raw input buffer (SAM text or inflated BAM)
     std::vector<char> buf;
     size_t beg = 0, end = 0;
@@ -223,6 +232,7 @@ struct fc2_ingest {
     bool z_init = false;
     std::vector<char> zin;
     bool z_done = false;
+    bool z_mid = false;          // inside a gzip member (its end not yet seen)
     // BGZF (the BAM case): batches inflated in parallel, one batch ahead of the parser
     bool bgzf = false;
     int bgzf_nt = 1;
@@ -279,6 +289,8 @@ struct fc2_ingest::SamAhead {
         size_t n = 0;
         int rc = FC2_OK;
         std::string err;
+        int read_rc = FC2_OK;                   // read(2) failed after the block's lines: reported
+        std::string read_err;                   // once they are parsed (records before an error first)
         bool eof = false;                       // the last block of the input
     };
     static constexpr size_t kBlock = size_t(4) << 20;
@@ -296,14 +308,27 @@ struct fc2_ingest::SamAhead {
     bool stop = false;
     std::thread splitter;
     std::vector<std::thread> parsers;
+    // the splitter waits for input in poll() on the input and this pipe, so closing the ingest
+    // never waits for a slow or stalled writer upstream (an aligner feeding stdin)
+    int wake[2] = {-1, -1};
+    SamAhead() {
+        if (pipe(wake) != 0) wake[0] = wake[1] = -1;
+    }
     ~SamAhead() {
         {
             std::lock_guard<std::mutex> lk(m);
             stop = true;
         }
         cv.notify_all();
+        if (wake[1] >= 0) {
+            const char c = 1;
+            ssize_t k;
+            do { k = write(wake[1], &c, 1); } while (k < 0 && errno == EINTR);
+        }
         if (splitter.joinable()) splitter.join();
         for (std::thread &t : parsers) t.join();
+        for (int fd : wake)
+            if (fd >= 0) close(fd);
     }
 };
 
@@ -316,6 +341,7 @@ bool fill_raw(fc2_ingest *h, std::vector<char> &dst, size_t want) {
     dst.resize(old + want);
     ssize_t k;
     do { k = read(h->fd, dst.data() + old, want); } while (k < 0 && errno == EINTR);
+    if (k < 0) { h->in_rc = FC2_E_IO; h->in_err = std::string("read error: ") + strerror(errno); }
     if (k <= 0) { dst.resize(old); return false; }
     dst.resize(old + (size_t)k);
     return true;
@@ -330,13 +356,14 @@ bool ensure(fc2_ingest *h, size_t n) {
             h->beg = 0;
         }
         if (h->buf.size() < h->end + (1 << 22)) h->buf.resize(h->end + (1 << 22));
-        if (!h->bam) {
+        if (h->src == fc2_ingest::SRC_RAW) {
             if (h->eof_in) return false;
             ssize_t k;
             do { k = read(h->fd, h->buf.data() + h->end, h->buf.size() - h->end); } while (k < 0 && errno == EINTR);
+            if (k < 0) { h->in_rc = FC2_E_IO; h->in_err = std::string("read error: ") + strerror(errno); }
             if (k <= 0) { h->eof_in = true; return false; }
             h->end += (size_t)k;
-        } else if (h->bgzf) {
+        } else if (h->src == fc2_ingest::SRC_BGZF) {
             if (h->z_done) return false;
             BgzfBatch b = h->bgzf_next.get();
             if (!b.err.empty()) { h->z_err = b.err; h->z_done = true; return false; }
@@ -351,7 +378,11 @@ bool ensure(fc2_ingest *h, size_t n) {
             // inflate more
             if (h->zs.avail_in == 0) {
                 h->zin.clear();
-                if (!fill_raw(h, h->zin, 1 << 20)) { h->z_done = true; return false; }
+                if (!fill_raw(h, h->zin, 1 << 20)) {
+                    h->z_done = true;
+                    if (h->z_mid) h->z_err = "truncated gzip stream";
+                    return false;
+                }
                 h->zs.next_in = (Bytef *)h->zin.data();
                 h->zs.avail_in = (uInt)h->zin.size();
             }
@@ -359,15 +390,26 @@ bool ensure(fc2_ingest *h, size_t n) {
             h->zs.avail_out = (uInt)(h->buf.size() - h->end);
             int rc = inflate(&h->zs, Z_NO_FLUSH);
             h->end = h->buf.size() - h->zs.avail_out;
+            h->z_mid = true;
             if (rc == Z_STREAM_END) {
-                // concatenated gzip members (BGZF blocks): restart on the remaining input
-                if (inflateReset(&h->zs) != Z_OK) return false;
+                // concatenated gzip members: restart on the remaining input
+                h->z_mid = false;
+                if (inflateReset(&h->zs) != Z_OK) { h->z_done = true; h->z_err = "zlib reset"; return false; }
             } else if (rc != Z_OK && rc != Z_BUF_ERROR) {
+                h->z_done = true;
+                h->z_err = "corrupt gzip stream";
                 return false;
             }
         }
     }
     return true;
+}
+
+// the error that ended the input early, if any (FC2_OK at a clean end of input)
+int input_rc(fc2_ingest *h) {
+    if (h->in_rc) return fc2::fail(h->in_rc, h->in_err);
+    if (!h->z_err.empty()) return fc2::fail(FC2_E_FORMAT, std::string(h->bam ? "BAM" : "SAM") + " input: " + h->z_err);
+    return FC2_OK;
 }
 
 // SAM: next line as [*s, *e) inside the input buffer (without newline; valid until the next
@@ -612,7 +654,10 @@ void scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
 
 int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     got = false;
-    if (!ensure(h, 4)) return h->z_err.empty() ? FC2_OK : fc2::fail(FC2_E_FORMAT, "BAM input: " + h->z_err);
+    if (!ensure(h, 4)) {
+        if (int rc = input_rc(h)) return rc;
+        return h->end > h->beg ? fc2::fail(FC2_E_FORMAT, "truncated BAM record") : FC2_OK;
+    }
     int32_t bs;
     memcpy(&bs, h->buf.data() + h->beg, 4);
     if (bs < 32 || !ensure(h, 4 + (size_t)bs))
@@ -698,9 +743,9 @@ int read_header(fc2_ingest *h) {
         std::string line;
         for (;;) {
             // peek: header lines start with '@'
-            if (!ensure(h, 1)) return FC2_OK;
+            if (!ensure(h, 1)) return input_rc(h);
             if (h->buf[h->beg] != '@') return FC2_OK;
-            if (!next_line(h, line)) return FC2_OK;
+            if (!next_line(h, line)) return input_rc(h);
             h->header += line;
             h->header += '\n';
             if (line.compare(0, 3, "@SQ") == 0) {
@@ -764,6 +809,8 @@ void sam_split_loop(fc2_ingest *h) {
         b->n = 0;
         b->rc = FC2_OK;
         b->err.clear();
+        b->read_rc = FC2_OK;
+        b->read_err.clear();
         b->eof = false;
         std::string &blk = b->block;
         blk.swap(carry);
@@ -771,14 +818,20 @@ void sam_split_loop(fc2_ingest *h) {
         // read until the block holds kBlock bytes and a newline, or the input ends
         bool has_nl = memchr(blk.data(), '\n', blk.size()) != nullptr;
         while (!in_eof && (blk.size() < A.kBlock || !has_nl)) {
+            if (A.wake[0] >= 0) {
+                pollfd pf[2] = {{h->fd, POLLIN, 0}, {A.wake[0], POLLIN, 0}};
+                int pr;
+                do { pr = poll(pf, 2, -1); } while (pr < 0 && errno == EINTR);
+                if (pr > 0 && pf[1].revents) return;       // the ingest is closing
+            }
             const size_t have = blk.size();
             blk.resize(have + A.kBlock);
             ssize_t k;
             do { k = read(h->fd, &blk[have], A.kBlock); } while (k < 0 && errno == EINTR);
             if (k < 0) {
                 blk.resize(have);
-                b->rc = FC2_E_IO;
-                b->err = std::string("read error: ") + strerror(errno);
+                b->read_rc = FC2_E_IO;
+                b->read_err = std::string("read error: ") + strerror(errno);
                 in_eof = true;
                 break;
             }
@@ -792,6 +845,10 @@ void sam_split_loop(fc2_ingest *h) {
             blk.resize(nl + 1);
         } else {
             b->eof = true;
+            if (b->read_rc) {                   // a line cut short by the failed read is not a record
+                const size_t nl = blk.rfind('\n');
+                blk.resize(nl == std::string::npos ? 0 : nl + 1);
+            }
         }
         const bool last = b->eof;
         {
@@ -830,6 +887,7 @@ void sam_parse_loop(fc2_ingest *h) {
             if (rc) { b->rc = rc; b->err = fc2_last_error(); break; }
             ++b->n;
         }
+        if (b->rc == FC2_OK && b->read_rc) { b->rc = b->read_rc; b->err = b->read_err; }
         {
             std::lock_guard<std::mutex> lk(A.m);
             const uint64_t seq = b->seq;
@@ -874,7 +932,7 @@ bool next_record(fc2_ingest *h, Rec &r, int &rc) {
     }
     const char *ls, *le;
     for (;;) {
-        if (!next_line_view(h, ls, le)) return false;
+        if (!next_line_view(h, ls, le)) { rc = input_rc(h); return false; }
         bool blank = true;
         for (const char *c = ls; c < le; ++c) if (!isspace((unsigned char)*c)) { blank = false; break; }
         if (blank) continue;
@@ -1022,36 +1080,70 @@ int emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed,
 }  // namespace
 
 extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
+    // is_bam is the reference's mode hint ('rb' unless the name ends in "sam", find_circ.py:463-466);
+    // like htslib's hts_open, reading never trusts it: the format comes from the bytes
+    (void)is_bam;
     if (!path || !out) return fc2::fail(FC2_E_PARAM, "fc2_ingest_open: null argument");
     *out = nullptr;
     int fd = strcmp(path, "-") == 0 ? dup(0) : open(path, O_RDONLY);
     if (fd < 0) return fc2::fail(FC2_E_IO, std::string("cannot open '") + path + "': " + strerror(errno));
     fc2_ingest *h = new fc2_ingest();
     h->fd = fd;
-    h->bam = is_bam != 0;
     h->buf.resize(1 << 22);
-    if (h->bam) {
-        // BGZF? (peek the first header; the bytes go to the first batch or to the zlib stream)
-        std::vector<uint8_t> pre(18);
-        size_t got = 0;
-        if (!read_full(fd, pre.data(), 18, got)) { close(fd); delete h; return fc2::fail(FC2_E_IO, "read error"); }
-        pre.resize(got);
-        if (got == 18 && pre[0] == 0x1f && pre[1] == 0x8b && (pre[3] & 4) && pre[12] == 'B' && pre[13] == 'C') {
+    // 1. the byte source: peek one gzip header's worth (a pipe cannot be rewound, so the peeked
+    //    bytes start the first BGZF batch, the zlib stream or the plain buffer)
+    std::vector<uint8_t> pre(18);
+    size_t got = 0;
+    if (!read_full(fd, pre.data(), 18, got)) {
+        const std::string e = std::string("read error: ") + strerror(errno);
+        close(fd);
+        delete h;
+        return fc2::fail(FC2_E_IO, e);
+    }
+    pre.resize(got);
+    if (got >= 2 && pre[0] == 0x1f && pre[1] == 0x8b) {
+        if (got == 18 && bgzf_block_size(pre.data(), got) != 0) {
+            // BGZF (BAM, or bgzip'ed SAM): blocks inflated in parallel, one batch ahead
+            h->src = fc2_ingest::SRC_BGZF;
             h->bgzf = true;
             h->bgzf_nt = bgzf_threads();
             h->bgzf_next = std::async(std::launch::async, bgzf_batch, fd, std::move(pre), 16, h->bgzf_nt);
         } else {
-            if (inflateInit2(&h->zs, 15 + 32) != Z_OK) { close(fd); delete h; return fc2::fail(FC2_E_IO, "zlib init"); }
+            // any other gzip stream (gzip -c, concatenated members)
+            h->src = fc2_ingest::SRC_GZIP;
+            if (inflateInit2(&h->zs, 15 + 16) != Z_OK) { close(fd); delete h; return fc2::fail(FC2_E_IO, "zlib init"); }
             h->z_init = true;
             h->zin.assign(pre.begin(), pre.end());
             h->zs.next_in = (Bytef *)h->zin.data();
             h->zs.avail_in = (uInt)h->zin.size();
         }
+    } else {
+        h->src = fc2_ingest::SRC_RAW;
+        memcpy(h->buf.data(), pre.data(), got);
+        h->end = got;
     }
-    int rc = read_header(h);
+    // 2. the format, from the first (decompressed) bytes: BAM magic or SAM text
+    ensure(h, 4);
+    const size_t have = h->end - h->beg;
+    const char *b = h->buf.data() + h->beg;
+    int rc = FC2_OK;
+    if (have >= 4 && memcmp(b, "BAM\1", 4) == 0) h->bam = true;
+    else if (have >= 4 && memcmp(b, "CRAM", 4) == 0)
+        rc = fc2::fail(FC2_E_FORMAT, std::string("'") + path + "' is CRAM, which this ingest does not read (convert "
+                                     "it to BAM or SAM)");
+    else if (h->in_rc || !h->z_err.empty()) rc = input_rc(h);
+    if (!rc) rc = read_header(h);
     if (rc) { fc2_ingest_close(h); return rc; }
     *out = h;
     return FC2_OK;
+}
+
+extern "C" int fc2_ingest_format(const fc2_ingest *h, int *compression) {
+    if (!h) return -1;
+    if (compression)
+        *compression = h->src == fc2_ingest::SRC_BGZF ? FC2_INGEST_BGZF
+                     : h->src == fc2_ingest::SRC_GZIP ? FC2_INGEST_GZIP : FC2_INGEST_PLAIN;
+    return h->bam ? FC2_INGEST_BAM : FC2_INGEST_SAM;
 }
 
 extern "C" int fc2_ingest_set_bam_out(fc2_ingest *h, const char *path) {
@@ -1151,7 +1243,8 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
 int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof) {
     if (!h || !p) return fc2::fail(FC2_E_PARAM, "ingest pull: null argument");
     if (h->need_text) h->need_text = false;     // (written once: the parse thread reads it)
-    if (!h->ahead && !h->bam && !h->bam_out && !h->finished) {   // SAM: parse on a thread of its own
+    // plain SAM text: parsed on threads of their own (compressed SAM stays on the sequential reader)
+    if (!h->ahead && !h->bam && h->src == fc2_ingest::SRC_RAW && !h->bam_out && !h->finished) {
         h->ahead.reset(new fc2_ingest::SamAhead());
         h->ahead->splitter = std::thread(sam_split_loop, h);
         for (int k = 0; k < fc2_ingest::SamAhead::kParsers; ++k) h->ahead->parsers.emplace_back(sam_parse_loop, h);

@@ -21,6 +21,12 @@ class NativeIngest:
         self.counts = N.IngestCounts()
         self.eof = False
 
+    def format(self) -> Tuple[str, str]:
+        """(``"sam"`` | ``"bam"``, ``"plain"`` | ``"bgzf"`` | ``"gzip"``), detected from the bytes."""
+        comp = ctypes.c_int()
+        fmt = N.lib().fc2_ingest_format(self.h, ctypes.byref(comp))
+        return ("sam", "bam")[fmt], ("plain", "bgzf", "gzip")[comp.value]
+
     def getrname(self, tid: int) -> str:
         return self.references[tid]
 

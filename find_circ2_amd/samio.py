@@ -129,8 +129,61 @@ def _tag_value(typ: str, val: str):
     return val            # Z, A, H
 
 
+class _Prefixed(io.RawIOBase):
+    """``head`` bytes (already read to detect the format: a pipe cannot be rewound), then ``rest``."""
+
+    def __init__(self, head: bytes, rest):
+        self._head = memoryview(head)
+        self._rest = rest
+
+    def readable(self):
+        return True
+
+    def readinto(self, b):
+        if len(self._head):
+            n = min(len(b), len(self._head))
+            b[:n] = self._head[:n]
+            self._head = self._head[n:]
+            return n
+        data = self._rest.read(len(b))
+        b[:len(data)] = data
+        return len(data)
+
+
+def _read_upto(fh, n: int) -> bytes:
+    out = b""
+    while len(out) < n:
+        d = fh.read(n - len(out))
+        if not d:
+            break
+        out += d
+    return out
+
+
+def sniff(raw) -> Tuple[str, str, object]:
+    """Detect the input format from its first bytes, as htslib's hts_detect_format does for the
+    reference's pysam.Samfile(path | '-', 'r' | 'rb') (find_circ.py:461-469): gzip (BGZF or not)
+    or plain bytes, holding BAM ("BAM\\1") or SAM text.  Returns (format, compression, stream of
+    the decompressed bytes from the start)."""
+    head = _read_upto(raw, 18)
+    stream = io.BufferedReader(_Prefixed(head, raw), 1 << 20)
+    comp = "plain"
+    if head[:2] == b"\x1f\x8b":
+        comp = "bgzf" if (len(head) >= 14 and head[3] & 4 and head[12:14] == b"BC") else "gzip"
+        stream = io.BufferedReader(gzip.GzipFile(fileobj=stream, mode="rb"), 1 << 20)
+    magic = stream.peek(4)[:4]
+    if len(magic) < 4 and magic:
+        magic = _read_upto(stream, 4)
+        stream = io.BufferedReader(_Prefixed(magic, stream), 1 << 20)
+    if magic == b"CRAM":
+        raise ValueError("CRAM input is not supported (convert it to BAM or SAM)")
+    return ("bam" if magic == b"BAM\1" else "sam"), comp, stream
+
+
 class AlignmentFile:
-    """Sequential reader of SAM text (path or '-' for stdin) or BAM (BGZF)."""
+    """Sequential reader of SAM text or BAM, from a path or '-' (stdin).  ``mode`` is the
+    reference's hint ('r' / 'rb', find_circ.py:463-469); as in htslib it does not decide the
+    format, the bytes do (``sniff``)."""
 
     def __init__(self, path: str, mode: str = "r"):
         self.path = path
@@ -138,17 +191,19 @@ class AlignmentFile:
         self.lengths: List[int] = []
         self.header_lines: List[str] = []
         self._tid: Dict[str, int] = {}
-        self._bam = "b" in mode
         if path == "-":
             raw = sys.stdin.buffer
         else:
             raw = open(path, "rb")
         self._raw = raw
+        fmt, self.compression, stream = sniff(raw)
+        self.format = fmt
+        self._bam = fmt == "bam"
         if self._bam:
-            self._fh = gzip.GzipFile(fileobj=raw, mode="rb")
+            self._fh = stream
             self._read_bam_header()
         else:
-            self._fh = io.TextIOWrapper(raw, encoding="latin-1", newline="\n")
+            self._fh = io.TextIOWrapper(stream, encoding="latin-1", newline="\n")
             self._pending = None
             self._read_sam_header()
 
@@ -169,10 +224,18 @@ class AlignmentFile:
         return parse_sam_line(line, self._tid)
 
     # ------------------------------------------------------------------ BAM
-    def _read(self, n):
-        b = self._fh.read(n)
+    def _read(self, n, at_record=False):
+        """n bytes of the BAM stream.  EOFError only for a clean end (nothing left where a record
+        would start); a stream cut short inside a record or a gzip member is an IOError, as
+        htslib reports a truncated file."""
+        try:
+            b = self._fh.read(n)
+        except EOFError as ex:          # gzip: "Compressed file ended before the end-of-stream marker ..."
+            raise IOError("truncated file: %s" % ex)
         if len(b) != n:
-            raise EOFError
+            if at_record and not b:
+                raise EOFError
+            raise IOError("truncated file")
         return b
 
     def _read_bam_header(self):
@@ -243,7 +306,7 @@ class AlignmentFile:
         if self._bam:
             while True:
                 try:
-                    n, = struct.unpack("<i", self._read(4))
+                    n, = struct.unpack("<i", self._read(4, at_record=True))
                 except EOFError:
                     return
                 yield self._parse_bam(self._read(n))

@@ -10,7 +10,11 @@
  * one anchor pair are handed back (as SAM text) for the per-fragment logic.
  * Counters the reference keeps for the others are accumulated here.
  *
- * Reads SAM text (path or "-" for stdin) and BAM (BGZF, via zlib).
+ * Reads a path or "-" (stdin).  The format is detected from the bytes, never
+ * from the file name, as htslib's hts_open does for the reference's
+ * pysam.Samfile(path | '-', 'r' | 'rb') (find_circ.py:461-469): the byte source
+ * is plain, BGZF (parallel block inflate) or any other gzip stream, and what it
+ * holds is BAM ("BAM\1") or SAM text.  CRAM is rejected (FC2_E_FORMAT).
  */
 #ifndef FC2_INGEST_H
 #define FC2_INGEST_H
@@ -40,8 +44,16 @@ typedef struct fc2_ingest_counts {  /* cumulative since open (the reference's N[
     uint64_t handed_back;           /* fragments returned to the caller */
 } fc2_ingest_counts;
 
-/* is_bam: 0 = SAM text, 1 = BAM; path "-" reads stdin. */
+/* path "-" reads stdin.  is_bam is the reference's mode hint ('rb' unless the name ends in
+ * "sam", find_circ.py:463-466) and, as in htslib, does not decide anything: a BAM named x.sam,
+ * SAM named x.bam, bgzip'ed or gzip'ed SAM and BAM on stdin are all read by what they are. */
 int  fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out);
+
+/* What fc2_ingest_open found: FC2_INGEST_SAM or FC2_INGEST_BAM (-1 for a null handle);
+ * *compression (optional) = FC2_INGEST_PLAIN / _BGZF / _GZIP. */
+enum { FC2_INGEST_SAM = 0, FC2_INGEST_BAM = 1 };
+enum { FC2_INGEST_PLAIN = 0, FC2_INGEST_BGZF = 1, FC2_INGEST_GZIP = 2 };
+int  fc2_ingest_format(const fc2_ingest *h, int *compression);
 void fc2_ingest_close(fc2_ingest *h);
 int  fc2_ingest_n_refs(const fc2_ingest *h);
 const char *fc2_ingest_ref_name(const fc2_ingest *h, int tid);

@@ -72,9 +72,11 @@ def bgzf_compress(data: bytes, block: int = 65280, level: int = 6) -> bytes:
     return bytes(out)
 
 
-def sam_to_bam(sam: str, path: str, bgzf: bool = True):
+def sam_to_bam(sam: str, path: str, bgzf: bool = True, compress: str = ""):
     """Minimal BAM writer: BGZF blocks (as samtools writes them) or, with ``bgzf=False``,
-    one plain gzip member (some tools do; readers must accept both)."""
+    one plain gzip member (some tools do; readers must accept both).  ``compress="none"``
+    writes the bare BAM bytes (no gzip framing at all; htslib reads that too)."""
+    compress = compress or ("bgzf" if bgzf else "gzip")
     import re
     refs, recs = [], []
     for line in sam.splitlines():
@@ -111,9 +113,12 @@ def sam_to_bam(sam: str, path: str, bgzf: bool = True):
                            int(f[1]), len(seq), -1, -1, 0)
         body += qn + b"".join(struct.pack("<I", (n << 4) | op) for n, op in cig) + bytes(sb) + qual + bytes(aux)
         out += struct.pack("<i", len(body)) + body
-    if bgzf:
+    if compress == "bgzf":
         with open(path, "wb") as fh:
             fh.write(bgzf_compress(bytes(out)))
-    else:
+    elif compress == "gzip":
         with gzip.open(path, "wb") as fh:
+            fh.write(bytes(out))
+    else:
+        with open(path, "wb") as fh:
             fh.write(bytes(out))
