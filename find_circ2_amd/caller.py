@@ -620,7 +620,12 @@ class Caller:
                              ",".join(sorted(flags)))
         fh.write("@%s\n%s\n+%s\n%s\n" % (name, mate.primary.seq, name, mate.primary.qual))
 
-    def _flush(self, frags: List[Fragment]):
+    def _flush(self, pending: List[Fragment]):
+        # the chunk leaves `pending` before anything runs: if evaluate or record_hits raises, the
+        # fragments recorded so far stay recorded exactly once and nothing after the failing one
+        # is recorded (the reference stops at the fragment that raises, find_circ.py:1578-1583)
+        frags = list(pending)
+        pending.clear()
         spans = [s for f in frags for s in f.circ + f.lin if s.uniq >= self.o.min_uniq_qual]
         if spans:
             t0 = time.perf_counter()
@@ -633,7 +638,6 @@ class Caller:
                 self._write_read(f.mate1, junctions, flags)
             if f.mate2 and junctions:
                 self._write_read(f.mate2, junctions, flags)
-        frags.clear()
 
     def run(self, records, stderr=sys.stderr):
         o = self.o

@@ -208,6 +208,10 @@ def main(argv=None, evaluator_factory=None) -> int:
         exc = traceback.format_exc()
         logging.error(exc)
         sys.stderr.write(exc)
+        # sys.exit(1) in the reference (find_circ.py:1583) flushes what was written so far
+        for fh in out.values():
+            if fh is not None and fh is not sys.stdout:
+                fh.close()
         return 1
     if bam_path:
         sam.close_bam_out()

@@ -8,6 +8,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <deque>
 #include <map>
 #include <memory>
@@ -151,6 +152,7 @@ struct Span {                                  // JunctionSpan (:821-852)
     double weight;
     int64_t uniq;
     int64_t qA, qB;                            // Hit.add's anchor qualities (after the backsplice swap)
+    bool q_int;                                // both from integer last AS / XS tags (else Hit.add needs Python)
     bool a_rev;                                // A.is_reverse after the swap
     uint64_t read_off;
     uint32_t read_len;
@@ -473,6 +475,9 @@ struct fc2_caller {
     // thread is freed on the other
     std::vector<Chunk> spare;
     std::mutex qmu;                             // guards queued and spare
+    // fc2_caller_stats' values, published by fc2_caller_next on the thread that advances the input
+    // (a recording thread may ask for them while the reader runs)
+    std::atomic<uint64_t> st_reads{0}, st_pairs{0};
     // aggregation
     struct Storage {
         std::string prefix;
@@ -548,6 +553,9 @@ void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
     t.n_hits.add(sp.n_hits, false);
     if (sp.span < 0) return;
     const Span &s = h->spans[sp.span];
+    if (!s.q_int)        // a float / string last AS or XS: Python arithmetic (:558-566)
+        throw Fatal{FC2_E_FORMAT, "native caller: the last AS / XS tags of a junction's anchors must be integers "
+                                  "(use --python-caller)"};
     t.n_spanned += 1;
     t.n_weighted += s.weight;
     if (s.qA && s.qB) t.n_uniq_bridges += s.weight;
@@ -821,11 +829,14 @@ int64_t uniqness(const Rec &a) {                                  // :809-819
     return a.as - (a.has_xs ? a.xs : 0);
 }
 
-// Hit.add's anchor quality (find_circ.py:556-559): dict(tags) keeps the LAST AS / XS of a record
-int64_t dict_quality(const Rec &a) {
-    if (!a.as_last_int || (a.has_xs && !a.xs_last_int))
-        throw Fatal{FC2_E_FORMAT, "native caller: AS / XS tags must be integers (use --python-caller)"};
-    return a.as_last - (a.has_xs ? a.xs_last : 0);
+// Hit.add's anchor quality (find_circ.py:556-559): dict(tags) keeps the LAST AS / XS of a record.
+// Only Hit.add reads it, so a non-integer last tag matters only for a span that reaches a Hit
+// (hit_add raises there); false when it is not an integer
+bool dict_quality(const Rec &a, int64_t &q) {
+    q = 0;
+    if (!a.as_last_int || (a.has_xs && !a.xs_last_int)) return false;
+    q = a.as_last - (a.has_xs ? a.xs_last : 0);
+    return true;
 }
 
 const char *kNoneLen = "TypeError: object of type 'NoneType' has no len()";
@@ -880,7 +891,9 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
         s.b_aend = B.aend;
         s.weight = weight;
         s.uniq = std::min(ua, ub);
-        const int64_t qa = dict_quality(A), qb = dict_quality(B);
+        int64_t qa, qb;
+        const bool qa_int = dict_quality(A, qa), qb_int = dict_quality(B, qb);   // both computed, as both set
+        s.q_int = qa_int && qb_int;
         s.qA = s.circ ? qb : qa;
         s.qB = s.circ ? qa : qb;
         s.a_rev = s.circ ? B.reverse() : A.reverse();
@@ -1485,6 +1498,15 @@ extern "C" void fc2_caller_close(fc2_caller *h) {
 
 extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     if (!h || !b) return fc2::fail(FC2_E_PARAM, "fc2_caller_next: null argument");
+    struct PublishStats {                          // on every way out of this call
+        fc2_caller *h;
+        ~PublishStats() {
+            fc2_ingest_counts c{};
+            fc2_ingest_counts_get(h->ing, &c);
+            h->st_reads.store(c.n_reads, std::memory_order_relaxed);
+            h->st_pairs.store(h->n_pairs, std::memory_order_relaxed);
+        }
+    } publish{h};
     {
         std::lock_guard<std::mutex> lk(h->qmu);
         if (h->queued.size() >= FC2_CALLER_MAX_QUEUED)
@@ -1708,9 +1730,7 @@ extern "C" int fc2_caller_counter(fc2_caller *h, int i, const char **name, doubl
 
 extern "C" int fc2_caller_stats(fc2_caller *h, uint64_t *n_reads, uint64_t *n_pairs) {
     if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_stats: null argument");
-    fc2_ingest_counts c{};
-    fc2_ingest_counts_get(h->ing, &c);
-    if (n_reads) *n_reads = c.n_reads;
-    if (n_pairs) *n_pairs = h->n_pairs;
+    if (n_reads) *n_reads = h->st_reads.load(std::memory_order_relaxed);
+    if (n_pairs) *n_pairs = h->st_pairs.load(std::memory_order_relaxed);
     return FC2_OK;
 }

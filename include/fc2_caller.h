@@ -104,7 +104,8 @@ int fc2_caller_rows(fc2_caller *h, int kind, const char **text, uint64_t *len);
 /* The reference's N[...] counters in sorted key order: i-th name and value;
  * FC2_E_RANGE past the end. */
 int fc2_caller_counter(fc2_caller *h, int i, const char **name, double *value);
-/* fragments read (n_reads) and anchor pairs evaluated so far. */
+/* fragments read (n_reads) and anchor pairs evaluated so far, as of the last fc2_caller_next to
+ * return (safe to call from a thread other than the one calling fc2_caller_next). */
 int fc2_caller_stats(fc2_caller *h, uint64_t *n_reads, uint64_t *n_pairs);
 
 #ifdef __cplusplus

@@ -90,7 +90,8 @@ def _exc_type(out):
 
 
 @pytest.mark.parametrize("seed", list(range(12)))
-@pytest.mark.parametrize("extra", [[], ["--all-hits", "--non-canonical", "--half-unique"]], ids=["default", "allhits"])
+@pytest.mark.parametrize("extra", [[], ["--all-hits", "--non-canonical", "--half-unique"], ["--chunk-size", "5"]],
+                         ids=["default", "allhits", "chunk5"])
 def test_three_loops_agree_on_mutated_input(tmp_path, seed, extra):
     sam0 = str(tmp_path / "base.sam")
     fa = _rich_sam(sam0, 400, seed=1000 + seed)
@@ -222,3 +223,35 @@ def test_rev_comp_keyerror_names_first_bad_byte(tmp_path):
     rc, outs = _agree(tmp_path, fa, sam, [])
     logs = [open(os.path.join(o, "run.log")).read() for o in outs]
     assert rc == 1 and all("KeyError: '='" in l for l in logs), [l[-300:] for l in logs]
+
+
+@pytest.mark.parametrize("chunk", ["2", "3", "7"])
+def test_failure_inside_a_flushed_chunk_records_each_fragment_once(tmp_path, chunk):
+    """A fragment whose span raises at record time (its chromosome is in the SAM header but not in
+    the FASTA: KeyError at find_circ.py:193) in the middle of a chunk: the fragments before it are
+    recorded once, nothing after it, in all three loops (the reference stops there, :1578-1583)."""
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, 200, seed=77)
+    lines = open(sam0).read().splitlines()
+    hdr = [l for l in lines if l.startswith("@")] + ["@SQ\tSN:chrU\tLN:500000"]
+    body = [l for l in lines if not l.startswith("@")]
+    # the 12th read with a supplementary record (a split read) moves to chrU, all its records
+    split = []
+    for l in body:
+        f = l.split("\t")
+        if int(f[1]) & 0x800 and f[0] not in split:
+            split.append(f[0])
+    victim = split[11]
+    body = ["\t".join(f[:2] + ["chrU"] + f[3:]) if f[0] == victim else "\t".join(f)
+            for f in (l.split("\t") for l in body)]
+    sam = str(tmp_path / "u.sam")
+    open(sam, "w").write("\n".join(hdr + body) + "\n")
+    rc, outs = _agree(tmp_path, fa, sam, ["--chunk-size", chunk])
+    assert rc == 1
+    assert _exc_type(outs[0]) == _exc_type(outs[1]) == _exc_type(outs[2]) == "KeyError"
+    parts = [_partial(o) for o in outs]
+    assert parts[0] == parts[1] == parts[2]
+    # fragments in input order, each once (a paired fragment writes its two mates)
+    from collections import Counter
+    ids = [int(l.split()[0][2:]) for l in parts[0][0].splitlines()[::4]]
+    assert ids and ids == sorted(ids) and max(Counter(ids).values()) <= 2

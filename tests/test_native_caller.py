@@ -502,3 +502,42 @@ def test_native_reads_gz_unwritable_path(tmp_path):
             nc.open()
     finally:
         nc.close()
+
+
+def test_native_caller_float_last_as_only_matters_in_hit_add(tmp_path):
+    """A non-integer LAST AS tag (after an integer first one) is read only by Hit.add
+    (dict(tags), find_circ.py:556-559): on spans that never reach a Hit the native loop completes
+    with the Python loop's files; on a span that does, it stops with a pointer to --python-caller
+    (the float arithmetic of best_qual_* is left to the Python loop)."""
+    import gzip
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, 300, seed=5150)
+    o0 = str(tmp_path / "base_out")
+    assert cli.main(["-G", fa, "-o", o0, "-q", "--python-caller", sam0], evaluator_factory=oracle_evaluator_factory) == 0
+    with gzip.open(os.path.join(o0, "spliced_reads.fastq.gz"), "rt") as fh:
+        hit_reads = {l[1:].split()[0] for l in fh.read().splitlines()[::4]}
+    lines = open(sam0).read().splitlines()
+    qnames = [l.split("\t")[0] for l in lines if not l.startswith("@")]
+    spliced = {q for q in qnames if qnames.count(q) > 1} - hit_reads
+    assert hit_reads and spliced
+
+    def with_float_as(targets):
+        out = []
+        for l in lines:
+            f = l.split("\t")
+            if not l.startswith("@") and f[0] in targets and any(t.startswith("AS:i:") for t in f[11:]):
+                l += "\tAS:f:7.5"
+            out.append(l)
+        p = str(tmp_path / ("f%d.sam" % len(targets)))
+        open(p, "w").write("\n".join(out) + "\n")
+        return p
+
+    sam = with_float_as(spliced)
+    o1, o2 = str(tmp_path / "py"), str(tmp_path / "nat")
+    assert cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    assert cli.main(["-G", fa, "-o", o2, "-q", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    same(o1, o2)
+    sam = with_float_as({sorted(hit_reads)[0]})
+    o3 = str(tmp_path / "nat_hit")
+    assert cli.main(["-G", fa, "-o", o3, "-q", sam], evaluator_factory=oracle_evaluator_factory) == 1
+    assert "--python-caller" in open(os.path.join(o3, "run.log")).read()
