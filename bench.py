@@ -56,7 +56,8 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
     ap.add_argument("--no-strong", action="store_true", help="skip the configs[3] strong-scaling / ordered-merge run")
     ap.add_argument("--no-config4", action="store_true", help="skip the configs[4] 200M x 120-150 bp run")
-    ap.add_argument("--no-cli", action="store_true", help="skip the end-to-end CLI extra (2M reads from SAM)")
+    ap.add_argument("--config4-pairs", type=int, default=0, help="configs[4] stream length (default 200M; tests)")
+    ap.add_argument("--no-cli", action="store_true", help="skip the end-to-end CLI extra (2M reads, BAM on stdin)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r02.json"))
     return ap.parse_args()
@@ -159,23 +160,27 @@ def max_over_ranks(x: float, ws: int, dev) -> float:
     return x if ws == 1 else _mor(x, device=dev)
 
 
+def workload_cfg(args, rank: int):
+    """(pairs per GPU, SynthConfig keywords) of the workload: rank r's weak-scaling batch is the stream
+    seeded 1337 + 7919 r; rank 0's stream is also configs[3]'s strong-scaling stream."""
+    span = (150, 20000) if args.workload == "hg19" else (150, 2500)
+    n = args.pairs or (50_000_000 if args.workload == "hg19" else 1_000_000)
+    kw = dict(seed=1337 + 7919 * rank, len_min=getattr(args, "read_len_min", None) or args.read_len,
+              len_max=args.read_len, p_backsplice=1.0, p_planted=0.5, mut_rate=0.005, n_rate=0.0005,
+              span_min=span[0], span_max=span[1], locus_ordered=bool(getattr(args, "locus_ordered", False)))
+    return n, kw
+
+
 def build_workload(args, rank, dev):
     from find_circ2_amd import Genome, Options, PairBatch, SynthConfig, sq_table
     opt = Options()
     if args.workload == "hg19":
         names, sizes = sq_table(os.path.join(GOLDEN, "test_norm.sam"))
         g = Genome.synthetic(names, sizes, seed=4711, device=dev)
-        n = args.pairs or 50_000_000
-        span = (150, 20000)
     else:
         g = Genome.from_fasta(os.path.join(GOLDEN, "CDR1as_locus.fa"), device=dev)
-        n = args.pairs or 1_000_000
-        span = (150, 2500)
-    cfg = SynthConfig(seed=1337 + 7919 * rank, len_min=getattr(args, "read_len_min", None) or args.read_len,
-                      len_max=args.read_len, p_backsplice=1.0,
-                      p_planted=0.5, mut_rate=0.005, n_rate=0.0005, span_min=span[0], span_max=span[1],
-                      locus_ordered=bool(getattr(args, "locus_ordered", False)))
-    b = PairBatch.synthetic(opt, g, n, cfg)
+    n, kw = workload_cfg(args, rank)
+    b = PairBatch.synthetic(opt, g, n, SynthConfig(**kw))
     return opt, g, b
 
 
@@ -358,31 +363,55 @@ def host_pipeline(opt, g, b, chunk: int = 4_000_000, reps: int = 3):
                     "over %d pairs" % (chunk, reps, n)}
 
 
-def configs4(opt, g, ws, rank, dev, steps, warmup, total=200_000_000):
-    """BASELINE configs[4]: 200M pairs of 120-150 bp reads (anchors of varying length, SURVEY.md 8(d)
-    config 5) over the ranks -- total fixed (strong scaling), each rank generates and scans its
-    share (seed per rank) on the resident hg19-shaped genome; value = 200M / max-over-ranks time.
-    At N = 1 the whole 200M-pair batch (14 GB of SoA) is scanned by one GPU."""
-    import torch
+def stream_share(opt, g, cfg_kw, lo: int, hi: int):
+    """Pairs [lo, hi) of a seeded synthetic stream, generated on this rank's device only (each pair
+    depends on the seed and its stream index alone, fc2_synth_cfg.first): a rank holds its share of
+    a stream, never the whole stream."""
     from find_circ2_amd import PairBatch, SynthConfig
-    n = total // ws + (1 if rank < total % ws else 0)
-    cfg = SynthConfig(seed=4242 + 7919 * rank, len_min=120, len_max=150, p_backsplice=1.0, p_planted=0.5,
-                      mut_rate=0.005, n_rate=0.0005, span_min=150, span_max=20000)
-    b = PairBatch.synthetic(opt, g, n, cfg)
+    return PairBatch.synthetic(opt, g, hi - lo, SynthConfig(first=lo, **cfg_kw))
+
+
+def results_checksum(res, first: int) -> int:
+    """Order-sensitive checksum of result words res (device int64) at stream indices first..:
+    sum over i of mix(word_i, index_i) mod 2^64, so shares of one stream add up to the whole."""
+    import torch
+    idx = torch.arange(first, first + res.numel(), device=res.device, dtype=torch.int64)
+    h = res * -7046029254386353131 + idx * -4417276706812531889          # 0x9E37..., 0xC2B2... as int64
+    h = h ^ ((h >> 29) & 0x7FFFFFFFF)
+    return int(h.sum().item()) & 0xFFFFFFFFFFFFFFFF
+
+
+def configs4(opt, g, ws, rank, dev, steps, warmup, total=200_000_000):
+    """BASELINE configs[4]: ONE stream of `total` pairs of 120-150 bp reads (anchors of varying length,
+    SURVEY.md 8(d) config 5, seed 4242), split into contiguous shares over the ranks -- total fixed
+    (strong scaling); each rank generates and scans only its share on its resident hg19-shaped genome;
+    value = total / max-over-ranks time.  At N = 1 one GPU holds and scans the whole stream (14 GB of
+    SoA at 200M).  results_checksum: the stream's result words summed over the shares (order
+    sensitive, shard-invariant): the same at every N."""
+    import torch
+    from find_circ2_amd.shard import gather_ints
+    lo = total * rank // ws
+    hi = total * (rank + 1) // ws
+    n = hi - lo
+    kw = dict(seed=4242, len_min=120, len_max=150, p_backsplice=1.0, p_planted=0.5, mut_rate=0.005, n_rate=0.0005,
+              span_min=150, span_max=20000)
+    b = stream_share(opt, g, kw, lo, hi)
     elapsed, kms, out = timed_scans(opt, g, b, steps, warmup, ws, dev)
     elapsed = max_over_ranks(elapsed, ws, dev)
     kms = max_over_ranks(kms, ws, dev)
     hits = int(((out.results[:n] & 0xFFFF) != 0xFFFF).sum())
+    csum = sum(gather_ints(results_checksum(out.results[:n], lo))) & 0xFFFFFFFFFFFFFFFF
     del b, out
     torch.cuda.empty_cache()
     bpp = algo_bytes_per_pair(150, opt.asize, opt.margin)
     return {"value": round(total * steps / elapsed, 1), "unit": "anchor-pairs/s", "scaling": "strong",
             "ms_per_step": round(elapsed / steps * 1e3, 4), "kernel_ms_max_rank": round(kms, 4),
             "pairs_total": total, "pairs_per_rank": n, "ranks": ws, "rank0_pairs_with_hit": hits,
+            "results_checksum": "%016x" % csum,
             "achieved_algo_GBs_per_rank_at_150bp": round(bpp * n / (kms * 1e-3) / 1e9, 1),
-            "note": "configs[4]: 200M pairs, read lengths uniform in 120..150 bp, split evenly over the ranks "
-                    "(each its own seeded share), hg19-shaped genome, read order; algorithmic bytes priced at "
-                    "150 bp (%d B/pair)" % bpp}
+            "note": "configs[4]: one %d-pair stream (seed 4242), read lengths uniform in 120..150 bp, cut into "
+                    "contiguous shares over the ranks, each generated and scanned on its own rank's GPU; "
+                    "hg19-shaped genome, read order; algorithmic bytes priced at 150 bp (%d B/pair)" % (total, bpp)}
 
 
 def reorder_then_scan(opt, g, b, steps, dev, bpp):
@@ -445,87 +474,117 @@ def timed_scans(opt, g, b, steps, warmup, ws, dev):
     return t1 - t0, float(np.mean(kms)), out
 
 
-def strong_scaling(opt, g, sb, ref64, ws, rank, dev, steps, warmup):
-    """configs[3]: ONE pair stream (the 50M pairs rank 0 scans in the weak run, seed 1337) cut into
-    contiguous batches dealt round-robin to the ranks (shard.my_batches); every rank holds the
-    stream in HBM, scans only its batches (PairBatch.sub views, no copy) and copies their 8-B
-    results to the batch's input offset of ONE node-local pinned host buffer (shard.SharedResults),
-    which rank 0 then holds in input order: the host-side ordered merge junction naming needs
-    (find_circ.py:681-690, weights :544/:563/:579).  Timed twice: scans only, and scans + merge
-    (D2H into the shared buffer + a barrier per step, so rank 0 could consume every step's merged
-    results).  Then a checked pass: rank 0 poisons the buffer, every rank scans and copies, and the
-    merged buffer must equal rank 0's single-rank scan of the whole stream byte for byte."""
+def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw):
+    """configs[3]: ONE pair stream (the `n` pairs rank 0 scans in the weak run, seed 1337) cut into
+    contiguous batches dealt round-robin to the ranks (shard.my_batches).  Rank 0 scans views of its
+    own weak batch; every other rank generates only its batches of the stream (stream_share).  Each
+    batch's results are packed on the device into their 4-byte transfer form (fc2_result_compact_launch,
+    canonical mode) and copied to the batch's input offset of ONE node-local pinned host buffer
+    (shard.SharedCompactResults), which rank 0 then holds in input order: the host-side ordered merge
+    junction naming needs (find_circ.py:681-690, weights :544/:563/:579).  Timed three ways: scans only;
+    scans + the compact merge (pack, D2H into the shared buffer, a barrier per step, so rank 0 could
+    consume every step's merged results); and scans + the 8-byte merge (the raw words copied), for
+    comparison.  Then a checked pass: rank 0 poisons the buffer, every rank scans, packs and copies, and
+    the merged buffer expanded on the host (fc2_result_expand, what fc2_caller_submit32 does per chunk)
+    must equal rank 0's single-rank scan of the whole stream word for word."""
     import torch
-    from find_circ2_amd import scan
+    from find_circ2_amd import CompactResults, compact, scan
     from find_circ2_amd.hotpath import ScanOutput
-    from find_circ2_amd.shard import SharedResults, batch_bounds, broadcast_name, my_batches, round_robin_batch
-    n = sb.n
+    from find_circ2_amd.shard import (SharedCompactResults, SharedResults, batch_bounds, broadcast_name, my_batches,
+                                      round_robin_batch)
     bsz = round_robin_batch(n, ws)
+    bounds = batch_bounds(n, bsz)
     mine = my_batches(n, bsz, rank, ws)
-    n_batches = len(batch_bounds(n, bsz))
-    merged = SharedResults(n, create=True, pin=True) if rank == 0 else None
-    name = broadcast_name(merged.name if rank == 0 else None) if ws > 1 else merged.name
+    cap = max(1024, bsz // 256)
+    merged = SharedCompactResults(n, bounds, cap, create=True, pin=True) if rank == 0 else None
+    raw = SharedResults(n, create=True, pin=True) if rank == 0 else None
+    names = broadcast_name((merged.name, raw.name) if rank == 0 else None) if ws > 1 else (merged.name, raw.name)
     if rank != 0:
-        merged = SharedResults(n, name=name, pin=True)
+        merged = SharedCompactResults(n, bounds, cap, name=names[0], pin=True)
+        raw = SharedResults(n, name=names[1], pin=True)
     barrier(ws)                                  # every rank attached before rank 0 may unlink at the end
-    res = torch.empty(max(n, 1), dtype=torch.int64, device=dev)
-    subs = [(lo, hi, sb.sub(lo, hi)) for _, lo, hi in mine]
+    subs = []
+    for k, lo, hi in mine:
+        s = b0.sub(lo, hi) if rank == 0 else stream_share(opt, g, cfg_kw, lo, hi)
+        subs.append((k, lo, hi, s, torch.empty(hi - lo, dtype=torch.int64, device=dev),
+                     CompactResults(hi - lo, dev, cap)))
     stream = torch.cuda.current_stream(dev)
     copier = torch.cuda.Stream(dev)              # D2H of batch k overlaps the scan of batch k+1
     done = [torch.cuda.Event() for _ in subs]
 
-    def step(copy: bool):
-        for j, (lo, hi, s) in enumerate(subs):
-            scan(opt, g, s, out=ScanOutput(res[lo:hi], None, s.tw, s.stride), stream=stream.cuda_stream)
-            if copy:
-                done[j].record(stream)
-                copier.wait_event(done[j])
-                with torch.cuda.stream(copier):
-                    merged.tensor[lo:hi].copy_(res[lo:hi], non_blocking=True)
-        if copy:                                 # the next step's scans overwrite res
+    def step(mode: str):
+        for j, (k, lo, hi, s, res, comp) in enumerate(subs):
+            scan(opt, g, s, out=ScanOutput(res, None, s.tw, s.stride), stream=stream.cuda_stream)
+            if mode == "none":
+                continue
+            if mode == "compact":
+                compact(opt, res, hi - lo, into=comp, stream=stream.cuda_stream)
+            done[j].record(stream)
+            copier.wait_event(done[j])
+            with torch.cuda.stream(copier):
+                if mode == "compact":
+                    merged.words_t[lo:hi].copy_(comp.words[:hi - lo], non_blocking=True)
+                    merged.esc_t[k].copy_(comp.esc.view(torch.uint8), non_blocking=True)
+                    merged.count_t[k:k + 1].copy_(comp.count, non_blocking=True)
+                else:
+                    raw.tensor[lo:hi].copy_(res, non_blocking=True)
+        if mode != "none":                       # the next step's scans overwrite res / comp
             stream.wait_stream(copier)
 
-    for _ in range(max(1, warmup)):
-        step(True)
-    torch.cuda.synchronize(dev)
-    barrier(ws)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step(False)
-    torch.cuda.synchronize(dev)
-    barrier(ws)
-    scan_s = max_over_ranks(time.perf_counter() - t0, ws, dev)
-    barrier(ws)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        step(True)
+    def timed(mode: str) -> float:
+        barrier(ws)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step(mode)
+            if mode != "none":                   # rank 0 could consume this step's merged results
+                torch.cuda.synchronize(dev)
+                barrier(ws)
         torch.cuda.synchronize(dev)
         barrier(ws)
-    merge_s = max_over_ranks(time.perf_counter() - t0, ws, dev)
+        return max_over_ranks(time.perf_counter() - t0, ws, dev)
+
+    for mode in ("compact", "raw"):
+        for _ in range(max(1, warmup)):
+            step(mode)
+    torch.cuda.synchronize(dev)
+    scan_s = timed("none")
+    merge_s = timed("compact")
+    raw_s = timed("raw")
     # checked pass
     if rank == 0:
-        merged.array[:] = 0x5A5A5A5A5A5A5A5A
+        merged.words[:] = 0x5A5A5A5A
+        merged.esc_count[:] = -1
     barrier(ws)
-    step(True)
+    step("compact")
     torch.cuda.synchronize(dev)
     barrier(ws)
     out = None
     if rank == 0:
-        equal = bool(np.array_equal(merged.array, ref64))
+        try:
+            m = merged.merged(opt)
+            equal = bool(np.array_equal(m, ref64))
+            n_esc = int(merged.esc_count.sum())
+        except Exception as ex:                  # an overflowed escape area or a bad escape list
+            equal, n_esc = repr(ex), None
         out = {
             "value": round(n * steps / merge_s, 1), "unit": "anchor-pairs/s", "scaling": "strong",
             "ms_per_step": round(merge_s / steps * 1e3, 4),
             "scan_only": {"value": round(n * steps / scan_s, 1), "ms_per_step": round(scan_s / steps * 1e3, 4)},
             "merge_ms_per_step": round((merge_s - scan_s) / steps * 1e3, 4),
-            "pairs_total": n, "batch_pairs": bsz, "n_batches": n_batches, "ranks": ws,
+            "merge_bytes_per_pair": 4, "escapes": n_esc,
+            "merge_8B_words": {"value": round(n * steps / raw_s, 1), "ms_per_step": round(raw_s / steps * 1e3, 4),
+                               "merge_ms_per_step": round((raw_s - scan_s) / steps * 1e3, 4)},
+            "pairs_total": n, "batch_pairs": bsz, "n_batches": len(bounds), "ranks": ws,
             "merged_equals_single_rank": equal,
-            "note": "one %d-pair stream in %d contiguous batches of %d dealt round-robin to %d rank(s); each "
-                    "rank scans its batches and copies the 8-B results into a node-local pinned shared-memory "
-                    "buffer at their input offsets (host-side ordered merge, no collective on the data path); "
-                    "value = stream pairs / (scans + merge + per-step barrier), max over ranks; "
-                    "merge_ms_per_step = that minus the scan-only time" % (n, n_batches, bsz, ws)}
+            "note": "one %d-pair stream in %d contiguous batches of %d dealt round-robin to %d rank(s), each rank "
+                    "holding only its batches; each batch's results packed on the device to 4 B/pair "
+                    "(fc2_result_compact_launch) and copied into a node-local pinned shared-memory buffer at "
+                    "their input offsets (host-side ordered merge, no collective on the data path); value = "
+                    "stream pairs / (scans + pack + merge + per-step barrier), max over ranks; merge_8B_words = "
+                    "the same with the raw 8-B words copied" % (n, len(bounds), bsz, ws)}
     barrier(ws)
     merged.close()
+    raw.close()
     return out
 
 
@@ -782,12 +841,25 @@ def window_carrying(opt, g, b, steps, dev, bpp):
     return out
 
 
+def _cli_outputs(out):
+    import gzip
+    files = {}
+    for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
+        files[f] = open(os.path.join(out, f), "rb").read()
+    with gzip.open(os.path.join(out, "spliced_reads.fastq.gz")) as fh:
+        files["spliced_reads.fastq"] = fh.read()
+    return files
+
+
 def cli_end_to_end(reads=2_000_000):
-    """The product end to end (an extra, never `value`): scripts/cli_scale_check.py's generator writes an
-    hg19-shaped genome FASTA and a bwa-mem-like SAM of `reads` reads, then `python -m find_circ2_amd.cli`
-    runs as its own process (C++ read loop on two threads + SAM parser threads, HIP search through
-    pipeline.ScanPipeline, gzip members on worker threads).  The first run builds the .byo_index; the
-    second is reported: the loop's own reads/s (run.log) and the process wall time."""
+    """The product end to end (an extra, never `value`), in north_star's form ``samtools view -b ... |
+    find_circ -G genome.fa -o out``: scripts/cli_scale_check.py's generator writes an hg19-shaped genome
+    FASTA and a bwa-mem-like SAM of `reads` reads, fc2_sam_to_bam turns it into a BGZF BAM, and
+    `python -m find_circ2_amd.cli` runs as its own process reading that BAM from a stdin pipe (format
+    detected from the bytes; BGZF blocks inflated on worker threads, C++ read loop on two threads, HIP
+    search through pipeline.ScanPipeline, gzip members on worker threads).  The same reads as SAM text
+    by path run too; both runs must write identical files.  The first run builds the .byo_index; the
+    runs after it are reported: the loop's own reads/s (run.log) and the process wall time."""
     import re
     import shutil
     import subprocess
@@ -795,34 +867,50 @@ def cli_end_to_end(reads=2_000_000):
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     from cli_scale_check import make_genome, write_fasta, write_sam
     from find_circ2_amd import sq_table
+    from find_circ2_amd.ingest import sam_to_bam
     d = tempfile.mkdtemp(prefix="fc2_bench_cli_", dir="/tmp")
     try:
-        fa, sam = os.path.join(d, "genome.fa"), os.path.join(d, "reads.sam")
+        fa, sam, bam = os.path.join(d, "genome.fa"), os.path.join(d, "reads.sam"), os.path.join(d, "reads.bam")
         rng = np.random.default_rng(2024)
         names, sizes = sq_table(os.path.join(ROOT, "tests", "golden", "test_norm.sam"))
         seqs = make_genome(fa, names, sizes, rng)
         write_sam(sam, seqs, reads, rng)
         write_fasta(fa, seqs)
         del seqs
-        res = {}
-        for k in range(2):
-            out = os.path.join(d, "out%d" % k)
+        sam_to_bam(sam, bam)
+
+        def run(tag, stdin_bam):
+            out = os.path.join(d, tag)
+            cmd = [sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", out, "-q"]
             t0 = time.time()
-            rc = subprocess.run([sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", out, "-q", sam],
-                                cwd=ROOT, timeout=600).returncode
+            if stdin_bam:                      # a real pipe, as from samtools / an aligner
+                feeder = subprocess.Popen(["cat", bam], stdout=subprocess.PIPE)
+                rc = subprocess.run(cmd, cwd=ROOT, stdin=feeder.stdout, timeout=600).returncode
+                feeder.stdout.close()
+                feeder.wait()
+            else:
+                rc = subprocess.run(cmd + [sam], cwd=ROOT, timeout=600).returncode
             wall = time.time() - t0
             if rc != 0:
-                return {"error": "cli exit status %d" % rc}
+                raise RuntimeError("cli exit status %d (%s)" % (rc, tag))
             log = open(os.path.join(out, "run.log")).read()
             m = re.search(r"overall ([0-9.]+)k reads/second", log)
             st = re.search(r"read loop stages: (.*)", log)
-            res = {"value": round(float(m.group(1)) * 1e3, 1) if m else None, "unit": "reads/s",
-                   "process_wall_s": round(wall, 2), "reads": reads,
-                   "stages": st.group(1) if st else None}
-        res["note"] = ("whole CLI from SAM on an hg19-shaped genome (2nd run, .byo_index present): value = the "
-                       "read loop's reads/s from run.log; process_wall_s includes interpreter start, genome load "
-                       "and upload; outputs are checked against the Python loop in tests and "
-                       "scripts/cli_scale_check.py, not here")
+            return out, {"value": round(float(m.group(1)) * 1e3, 1) if m else None, "unit": "reads/s",
+                         "process_wall_s": round(wall, 2), "stages": st.group(1) if st else None}
+
+        run("warm", False)                     # builds genome.fa.byo_index
+        o_bam, res = run("bam_stdin", True)
+        o_sam, res_sam = run("sam_path", False)
+        res["reads"] = reads
+        res["bam_bytes"] = os.path.getsize(bam)
+        res["outputs_identical_to_sam_path_run"] = _cli_outputs(o_bam) == _cli_outputs(o_sam)
+        res["sam_by_path"] = res_sam
+        res["note"] = ("whole CLI, BGZF BAM piped on stdin (cat reads.bam | python -m find_circ2_amd.cli -G genome.fa "
+                       "-o out), hg19-shaped genome, .byo_index present: value = the read loop's reads/s from "
+                       "run.log; process_wall_s includes interpreter start, genome load and upload; sam_by_path = "
+                       "the same reads as SAM text by path; outputs of the two runs compared here, and against "
+                       "the Python loop in tests and scripts/cli_scale_check.py")
         return res
     except Exception as e:          # an extra must not cost the bench line
         return {"error": repr(e)}
@@ -872,18 +960,15 @@ def main():
     hits = int((res["best_x"] >= 0).sum())
     b._bench_ref_results = torch.from_numpy(res.view(np.int64).copy())
     c4 = None
-    if args.workload == "hg19" and not args.no_config4 and not args.pairs:
-        c4 = configs4(opt, g, ws, rank, dev, args.steps, args.warmup)
-    # configs[3]: the same stream strong-scaled over the ranks with the host-side ordered merge
-    if args.no_strong:
-        strong = None
-    else:
-        sb = b if rank == 0 else build_workload(args, 0, dev)[2]
-        strong = strong_scaling(opt, g, sb, b._bench_ref_results.numpy() if rank == 0 else None, ws, rank, dev,
-                                args.steps, args.warmup)
-        if sb is not b:
-            del sb
-            torch.cuda.empty_cache()
+    if args.workload == "hg19" and not args.no_config4 and (args.config4_pairs or not args.pairs):
+        c4 = configs4(opt, g, ws, rank, dev, args.steps, args.warmup, total=args.config4_pairs or 200_000_000)
+    # configs[3]: rank 0's stream strong-scaled over the ranks with the host-side ordered merge
+    strong = None
+    if not args.no_strong:
+        n0, kw0 = workload_cfg(args, 0)
+        strong = strong_scaling(opt, g, b if rank == 0 else None, b._bench_ref_results.numpy() if rank == 0 else None,
+                                ws, rank, dev, args.steps, args.warmup, n0, kw0)
+        torch.cuda.empty_cache()
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -970,7 +1055,7 @@ def main():
         del b4, g4
         torch.cuda.empty_cache()
         if not args.no_cli:
-            line["extra"]["cli_end_to_end_2M_reads"] = cli_end_to_end()
+            line["extra"]["cli_end_to_end_2M_reads_bam_stdin"] = cli_end_to_end()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if ws > 1:

@@ -47,6 +47,8 @@ PAIR_DTYPE = np.dtype([("a_pos", "<i4"), ("b_aend", "<i4"), ("chrom", "<u4"), ("
                        ("flags", "u1"), ("npos", "u1")])
 RESULT_DTYPE = np.dtype([("best_x", "<i2"), ("dist", "u1"), ("ov", "u1"), ("n_ties", "<u2"), ("info", "<u2")])
 assert PAIR_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 8
+ESCAPE_DTYPE = np.dtype([("index", "<u8"), ("result", RESULT_DTYPE)])     # fc2_result_escape
+R32_ESCAPE = 0x80000000
 
 
 class Fc2Error(RuntimeError):
@@ -104,7 +106,7 @@ class SynthCfg(ctypes.Structure):
                 ("p_planted", ctypes.c_float), ("p_minus_site", ctypes.c_float),
                 ("p_backsplice", ctypes.c_float), ("mut_rate", ctypes.c_float), ("n_rate", ctypes.c_float),
                 ("p_clip", ctypes.c_float), ("span_min", ctypes.c_int32), ("span_max", ctypes.c_int32),
-                ("locus_ordered", ctypes.c_int32), ("_pad", ctypes.c_int32)]
+                ("locus_ordered", ctypes.c_int32), ("_pad", ctypes.c_int32), ("first", ctypes.c_uint64)]
 
 
 # every symbol include/fc2_bp.h declares (checked by tests/test_abi.py)
@@ -112,6 +114,7 @@ EXPORTED = [
     "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_host_register", "fc2_host_unregister", "fc2_set_tuning", "fc2_get_tuning", "fc2_max_fast_l",
     "fc2_batch_geometry",
     "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch", "fc2_probe_pattern_launch",
+    "fc2_result_compact_launch", "fc2_result_expand",
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill", "fc2_window_geometry", "fc2_pack_windows",
@@ -122,10 +125,10 @@ EXPORTED = [
     # include/fc2_ingest.h
     "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
     "fc2_ingest_next", "fc2_ingest_counts_get", "fc2_ingest_set_bam_out", "fc2_ingest_close_bam_out",
-    "fc2_ingest_format",
+    "fc2_ingest_format", "fc2_sam_to_bam",
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
-    "fc2_caller_submit", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
+    "fc2_caller_submit", "fc2_caller_submit32", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
     "fc2_caller_set_reads_gz", "fc2_caller_close_reads",
 ]
 
@@ -195,6 +198,8 @@ def lib() -> ctypes.CDLL:
         "fc2_bp_scan_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp, u32, vp]),
         "fc2_bp_scan_bytes_launch": (ctypes.c_int, [P(Params), P(BytesView), vp, vp, u32, u64, vp]),
         "fc2_probe_pattern_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp]),
+        "fc2_result_compact_launch": (ctypes.c_int, [P(Params), vp, u64, vp, vp, u32, vp, vp]),
+        "fc2_result_expand": (ctypes.c_int, [P(Params), vp, u64, vp, u64, vp, ctypes.c_int]),
         "fc2_fasta_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(vp)]),
         "fc2_fasta_close": (None, [vp]),
         "fc2_fasta_n_chrom": (ctypes.c_int, [vp]),
@@ -233,12 +238,14 @@ def lib() -> ctypes.CDLL:
         "fc2_ingest_set_bam_out": (ctypes.c_int, [vp, ctypes.c_char_p]),
         "fc2_ingest_close_bam_out": (ctypes.c_int, [vp]),
         "fc2_ingest_format": (ctypes.c_int, [vp, P(ctypes.c_int)]),
+        "fc2_sam_to_bam": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_char_p]),
         "fc2_caller_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(CallerOpts), P(vp)]),
         "fc2_caller_set_genome": (ctypes.c_int, [vp, vp, i32, vp, P(u64), P(u64)]),
         "fc2_caller_ingest": (vp, [vp]),
         "fc2_caller_close": (None, [vp]),
         "fc2_caller_next": (ctypes.c_int, [vp, P(CallerBatch), P(ctypes.c_int)]),
         "fc2_caller_submit": (ctypes.c_int, [vp, vp, vp, u32, u64]),
+        "fc2_caller_submit32": (ctypes.c_int, [vp, vp, vp, u64, vp, u32, u64]),
         "fc2_caller_queued": (ctypes.c_int, [vp]),
         "fc2_caller_take": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_set_reads_gz": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, u64]),

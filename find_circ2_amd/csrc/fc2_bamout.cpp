@@ -90,7 +90,7 @@ struct Writer {
 };
 
 Writer *open_writer(const std::string &path, const std::string &text, const std::vector<std::string> &names,
-                    const std::vector<int64_t> &lens, std::string &err) {
+                    const std::vector<int64_t> &lens, std::string &err, int level) {
     FILE *fp = fopen(path.c_str(), "wb");
     if (!fp) {
         err = "IOError: cannot open '" + path + "': " + strerror(errno);
@@ -98,7 +98,7 @@ Writer *open_writer(const std::string &path, const std::string &text, const std:
     }
     Writer *w = new Writer();
     w->fp = fp;
-    if (deflateInit2(&w->zs, 6, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
+    if (deflateInit2(&w->zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
         fclose(fp);
         delete w;
         err = "zlib init failed";

@@ -15,9 +15,10 @@ namespace bam {
 
 struct Writer;
 
-// header: the input's header text and its reference names / lengths (pysam template=)
+// header: the input's header text and its reference names / lengths (pysam template=); level: zlib
+// level of the BGZF blocks (htslib's default is 6)
 Writer *open_writer(const std::string &path, const std::string &text, const std::vector<std::string> &names,
-                    const std::vector<int64_t> &lens, std::string &err);
+                    const std::vector<int64_t> &lens, std::string &err, int level = 6);
 // one BAM record: block_size (4 B) + body, as found in a BAM stream
 bool write_raw(Writer *w, const uint8_t *rec, size_t n);
 // one SAM text line (no newline); tid_of maps RNAME/RNEXT to reference ids

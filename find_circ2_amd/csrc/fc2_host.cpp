@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "fc2_common.h"
+#include "fc2_r32.h"
 
 namespace fc2 {
 
@@ -871,5 +872,38 @@ extern "C" int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64
         pos += block_bytes(l);
         ++k;
     }
+    return FC2_OK;
+}
+
+// ---- compact results (include/fc2_bp.h) --------------------------------------------------------
+extern "C" int fc2_result_expand(const fc2_params *p, const uint32_t *words, uint64_t n, const fc2_result_escape *esc,
+                                 uint64_t n_esc, fc2_result *out, int n_threads) {
+    if (int rc = fc2::validate_params(p)) return rc;
+    if (p->noncanonical) return fc2::fail(FC2_E_PARAM, "fc2_result_expand: the 4-byte form holds canonical-mode results only");
+    if ((n && (!words || !out)) || (n_esc && !esc)) return fc2::fail(FC2_E_PARAM, "fc2_result_expand: bad args");
+    std::atomic<uint64_t> flagged{0};
+    parallel_for(n, n_workers(n_threads), [&](uint64_t b, uint64_t e) {
+        uint64_t f = 0;
+        uint64_t *o = (uint64_t *)out;
+        for (uint64_t i = b; i < e; ++i) {
+            const uint32_t c = words[i];
+            f += c >> 31;
+            o[i] = (c & FC2_R32_ESCAPE) ? 0 : fc2::r32_unpack(c);
+        }
+        flagged += f;
+    });
+    if (flagged.load() != n_esc)
+        return fc2::fail(FC2_E_FORMAT, "fc2_result_expand: " + std::to_string(flagged.load()) + " escaped words, " +
+                                           std::to_string(n_esc) + " escapes");
+    std::vector<uint64_t> idx(n_esc);
+    for (uint64_t k = 0; k < n_esc; ++k) {
+        if (esc[k].index >= n || !(words[esc[k].index] & FC2_R32_ESCAPE))
+            return fc2::fail(FC2_E_FORMAT, "fc2_result_expand: escape " + std::to_string(k) + " has no escaped word");
+        idx[k] = esc[k].index;
+        out[esc[k].index] = esc[k].result;
+    }
+    std::sort(idx.begin(), idx.end());
+    if (std::adjacent_find(idx.begin(), idx.end()) != idx.end())
+        return fc2::fail(FC2_E_FORMAT, "fc2_result_expand: an escaped word has two escapes");
     return FC2_OK;
 }

@@ -1177,6 +1177,28 @@ extern "C" void fc2_ingest_close(fc2_ingest *h) {
     delete h;
 }
 
+extern "C" int fc2_sam_to_bam(const char *sam_path, const char *bam_path) {
+    if (!sam_path || !bam_path) return fc2::fail(FC2_E_PARAM, "fc2_sam_to_bam: null argument");
+    fc2_ingest *h = nullptr;
+    if (int rc = fc2_ingest_open(sam_path, 0, &h)) return rc;
+    int rc = FC2_OK;
+    if (h->bam) rc = fc2::fail(FC2_E_FORMAT, std::string("fc2_sam_to_bam: '") + sam_path + "' is BAM already");
+    std::string err;
+    fc2::bam::Writer *w = rc ? nullptr : fc2::bam::open_writer(bam_path, h->header, h->refs, h->ref_len, err, 1);
+    if (!rc && !w) rc = fc2::fail(FC2_E_IO, err);
+    const char *ls, *le;
+    while (!rc && next_line_view(h, ls, le)) {
+        bool blank = true;
+        for (const char *c = ls; c < le; ++c) if (!isspace((unsigned char)*c)) { blank = false; break; }
+        if (blank) continue;
+        if (!fc2::bam::write_sam(w, ls, le, h->tid_of, err)) rc = fc2::fail(FC2_E_FORMAT, err);
+    }
+    if (!rc) rc = input_rc(h);
+    if (w && !fc2::bam::close_writer(w, err) && !rc) rc = fc2::fail(FC2_E_IO, err);
+    fc2_ingest_close(h);
+    return rc;
+}
+
 extern "C" int fc2_ingest_n_refs(const fc2_ingest *h) { return h ? (int)h->refs.size() : 0; }
 extern "C" const char *fc2_ingest_ref_name(const fc2_ingest *h, int tid) {
     return (h && tid >= 0 && tid < (int)h->refs.size()) ? h->refs[tid].c_str() : nullptr;

@@ -24,6 +24,7 @@
 #include <stdint.h>
 
 #include "fc2_common.h"
+#include "fc2_r32.h"
 #include "fc2_scan32.h"
 
 namespace {
@@ -598,7 +599,7 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
                                    uint64_t *read_nwords, uint32_t nw, uint64_t stride, int32_t *truth) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    Rng R{smix(cfg.seed ^ smix(i + 0x51ED2701ull))};
+    Rng R{smix(cfg.seed ^ smix(cfg.first + i + 0x51ED2701ull))};
     const int e = p.asize - p.margin;
     const int amin = p.asize;
     int L = cfg.len_min + (int)R.below(cfg.len_max - cfg.len_min + 1);
@@ -1022,6 +1023,42 @@ extern "C" int fc2_synth_pairs_launch(const fc2_params *p, const fc2_synth_cfg *
     hipLaunchKernelGGL(synth_pairs_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream, *p, *cfg, *g,
                        chrom_cum, n, pairs, read_words, rw, read_nwords, nw, stride, truth);
     return hip_check(hipGetLastError(), "synth_pairs_kernel launch");
+}
+
+// compact results (include/fc2_bp.h): 8 B in, 4 B out per pair, streamed; escapes are rare
+__global__ void __launch_bounds__(256) result_compact_kernel(const uint64_t *__restrict__ res, uint64_t n,
+                                                             uint32_t *__restrict__ words, fc2_result_escape *esc,
+                                                             uint32_t cap, uint32_t *count) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t w = __builtin_nontemporal_load(res + i);
+    uint32_t c = fc2::r32_pack(w);
+    if (fc2::r32_unpack(c) != w) {
+        c = FC2_R32_ESCAPE;
+        const uint32_t k = atomicAdd(count, 1u);
+        if (k < cap) {
+            esc[k].index = i;
+            memcpy(&esc[k].result, &w, sizeof w);
+        }
+    }
+    __builtin_nontemporal_store(c, words + i);
+}
+
+extern "C" int fc2_result_compact_launch(const fc2_params *p, const fc2_result *results, uint64_t n, uint32_t *words,
+                                         fc2_result_escape *esc, uint32_t esc_cap, uint32_t *esc_count,
+                                         void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (p->noncanonical)
+        return fc2::fail(FC2_E_PARAM, "fc2_result_compact_launch: the 4-byte form holds canonical-mode results only");
+    if (!esc_count || (n && (!results || !words)) || (esc_cap && !esc))
+        return fc2::fail(FC2_E_PARAM, "fc2_result_compact_launch: bad args");
+    hipError_t e = hipMemsetAsync(esc_count, 0, sizeof(uint32_t), (hipStream_t)stream);
+    if (e != hipSuccess) return hip_check(e, "result_compact count reset");
+    if (n == 0) return FC2_OK;
+    hipLaunchKernelGGL(result_compact_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                       (const uint64_t *)results, n, words, esc, esc_cap, esc_count);
+    return hip_check(hipGetLastError(), "result_compact_kernel launch");
 }
 
 extern "C" int fc2_set_tuning(int key, int value) {

@@ -69,12 +69,13 @@ class SynthConfig:
     span_min: int = 150
     span_max: int = 5000
     locus_ordered: bool = False
+    first: int = 0          # generate pairs [first, first + n) of the seeded stream
 
     def cfg(self) -> N.SynthCfg:
         return N.SynthCfg(int(self.seed), int(self.len_min), int(self.len_max), float(self.p_planted),
                           float(self.p_minus_site), float(self.p_backsplice), float(self.mut_rate),
                           float(self.n_rate), float(self.p_clip), int(self.span_min), int(self.span_max),
-                          int(bool(self.locus_ordered)), 0)
+                          int(bool(self.locus_ordered)), 0, int(self.first))
 
 
 # ---------------------------------------------------------------------------
@@ -389,6 +390,48 @@ class ScanOutput:
 
     def host(self, n: int) -> np.ndarray:
         return self.results[:n].cpu().numpy().view(N.RESULT_DTYPE).copy()
+
+
+class CompactResults:
+    """The 4-byte transfer form of a run of results (include/fc2_bp.h "compact results"): device
+    words [n] (uint32), escape slots [cap] (``N.ESCAPE_DTYPE`` as 16 bytes each) and the escape count."""
+
+    def __init__(self, n: int, device, cap: int = 0):
+        torch = _torch()
+        self.n = n
+        self.cap = cap or max(1024, n // 256)
+        self.words = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+        self.esc = torch.empty(2 * self.cap, dtype=torch.int64, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+
+
+def compact(options: Options, results, n: int, into: CompactResults = None, stream=None) -> CompactResults:
+    """Pack the first ``n`` 8-byte results of the device tensor ``results`` into the 4-byte form
+    (``fc2_result_compact_launch``, asynchronous on ``stream``); canonical mode only."""
+    torch = _torch()
+    c = into if into is not None else CompactResults(n, results.device)
+    if c.n < n:
+        raise ValueError("compact buffers hold %d results, %d given" % (c.n, n))
+    s = stream if stream is not None else torch.cuda.current_stream(results.device).cuda_stream
+    p = options.params()
+    N.check(N.lib().fc2_result_compact_launch(ctypes.byref(p), results.data_ptr(), n, c.words.data_ptr(),
+                                              c.esc.data_ptr(), c.cap, c.count.data_ptr(), s))
+    return c
+
+
+def expand(options: Options, words: np.ndarray, esc: np.ndarray, out: np.ndarray = None,
+           n_threads: int = 0) -> np.ndarray:
+    """Host: the 8-byte result words (int64) back from the 4-byte words (uint32 / int32 array) and
+    the escapes (``N.ESCAPE_DTYPE``), ``fc2_result_expand``."""
+    words = np.ascontiguousarray(words).view(np.uint32)
+    esc = np.ascontiguousarray(esc, dtype=N.ESCAPE_DTYPE) if len(esc) else np.zeros(0, N.ESCAPE_DTYPE)
+    n = len(words)
+    if out is None:
+        out = np.empty(n, np.int64)
+    p = options.params()
+    N.check(N.lib().fc2_result_expand(ctypes.byref(p), words.ctypes.data, n, esc.ctypes.data if len(esc) else None,
+                                      len(esc), out.ctypes.data, int(n_threads)))
+    return out
 
 
 def scan(options: Options, genome: Genome, batch: PairBatch, out: ScanOutput = None, stream=None) -> ScanOutput:

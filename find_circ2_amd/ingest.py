@@ -65,3 +65,8 @@ class NativeIngest:
             self.close()
         except Exception:
             pass
+
+
+def sam_to_bam(sam_path: str, bam_path: str) -> None:
+    """BGZF BAM of a SAM file, records encoded as htslib's sam_parse1 does (include/fc2_ingest.h)."""
+    N.check(N.lib().fc2_sam_to_bam(sam_path.encode(), bam_path.encode()))

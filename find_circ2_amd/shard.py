@@ -122,6 +122,69 @@ class SharedResults:
         self.shm = None
 
 
+class SharedCompactResults(SharedResults):
+    """The same node-local ordered merge in the results' 4-byte transfer form (include/fc2_bp.h
+    "compact results", canonical mode): one /dev/shm segment holding ``words`` [n] (uint32, at each
+    batch's input offset), per batch ``cap`` escape slots (``N.ESCAPE_DTYPE``, indices relative to
+    the batch start) and the batch's escape count.  Half the bytes of the 8-byte merge cross PCIe
+    and land in host memory; ``merged()`` expands the whole stream (fc2_result_expand) where a
+    consumer wants 8-byte words, and fc2_caller_submit32 takes the form as it is."""
+
+    def __init__(self, n: int, bounds: Sequence[Tuple[int, int]], cap: int, name: str = None, create: bool = False,
+                 pin: bool = False):
+        from multiprocessing import resource_tracker, shared_memory
+        from . import _native as N
+        self.n, self.bounds, self.cap = int(n), list(bounds), int(cap)
+        nb = len(self.bounds)
+        self._w_bytes = (4 * self.n + 63) // 64 * 64
+        self._e_bytes = 16 * self.cap * nb
+        size = max(64, self._w_bytes + self._e_bytes + 8 * nb)
+        self.creator = create
+        self.shm = shared_memory.SharedMemory(name=name, create=create, size=size)
+        if not create:
+            try:
+                resource_tracker.unregister(self.shm._name, "shared_memory")
+            except Exception:
+                pass
+        self.name = self.shm.name
+        buf = self.shm.buf
+        self.words = np.ndarray((self.n,), np.uint32, buffer=buf)
+        self.esc = np.ndarray((nb, self.cap), N.ESCAPE_DTYPE, buffer=buf, offset=self._w_bytes)
+        self.esc_count = np.ndarray((nb,), np.int32, buffer=buf, offset=self._w_bytes + self._e_bytes)
+        self.array = np.ndarray((size,), np.uint8, buffer=buf)      # the whole segment (pinning, poisoning)
+        self._pinned = False
+        if pin and size:
+            N.check(N.lib().fc2_host_register(self.array.ctypes.data, size))
+            self._pinned = True
+        import torch
+        self.tensor = torch.from_numpy(self.array)
+        self.words_t = torch.from_numpy(self.words.view(np.int32))
+        self.esc_t = torch.from_numpy(self.esc.view(np.uint8).reshape(nb, 16 * self.cap))
+        self.count_t = torch.from_numpy(self.esc_count)
+
+    def escapes(self) -> np.ndarray:
+        """Every batch's escapes with stream indices; ValueError if a batch overflowed its slots."""
+        parts = []
+        for k, (lo, _) in enumerate(self.bounds):
+            c = int(self.esc_count[k])
+            if c > self.cap:
+                raise ValueError("batch %d has %d escapes, %d slots" % (k, c, self.cap))
+            e = self.esc[k, :c].copy()
+            e["index"] += lo
+            parts.append(e)
+        from . import _native as N
+        return np.concatenate(parts) if parts else np.zeros(0, N.ESCAPE_DTYPE)
+
+    def merged(self, options, n_threads: int = 0) -> np.ndarray:
+        from .hotpath import expand
+        return expand(options, self.words, self.escapes(), n_threads=n_threads)
+
+    def close(self):
+        self.words = self.esc = self.esc_count = None
+        self.words_t = self.esc_t = self.count_t = None
+        super().close()
+
+
 def broadcast_name(name, group=None) -> str:
     """Rank 0's shared-memory segment name on every rank (host group)."""
     import torch.distributed as dist
@@ -130,6 +193,16 @@ def broadcast_name(name, group=None) -> str:
     obj = [name]
     dist.broadcast_object_list(obj, src=0, group=group)
     return obj[0]
+
+
+def gather_ints(x: int, group=None) -> List[int]:
+    """Every rank's Python int, in rank order, on every rank (host group); [x] without one."""
+    import torch.distributed as dist
+    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size(group) == 1:
+        return [int(x)]
+    out = [None] * dist.get_world_size(group)
+    dist.all_gather_object(out, int(x), group=group)
+    return [int(v) for v in out]
 
 
 def max_over_ranks(x: float, device=None, group=None) -> float:

@@ -106,6 +106,31 @@ typedef struct fc2_result {
     uint16_t info;      /* FC2_RES_*                              */
 } fc2_result;
 
+/* ---- compact results: the 4-byte transfer form ---------------------------- */
+/* What moves a batch's results off the device (the ordered merge of a strong-scaled stream,
+ * find_circ.py:681-690 naming + :544/:563/:579 weight sums in input order) at 4 B per pair
+ * instead of 8.  Canonical mode only (no --non-canonical): a hit's signal is implied by its
+ * strand ('+' GTAG, '-' CTAC, :924-954), so words[i] =
+ *   bits 0-7 best_x + 1 (0: no hit) | 8-15 n_ties | 16-19 dist | 20-23 ov | 24 '-' |
+ *   25 FC2_RES_ERR_KEY | 26 FC2_RES_ERR_WIN | 27 FC2_RES_DONE | 31 FC2_R32_ESCAPE.
+ * A result that would not come back unchanged (x > 254, n_ties > 255, dist or ov > 15, ...)
+ * gets FC2_R32_ESCAPE and travels whole as an escape (its index, its fc2_result), in no
+ * particular order.  *esc_count (device) is zeroed by the launch and counts every escape;
+ * only the first esc_cap are stored: a count above esc_cap means the caller must move the
+ * 8-byte results instead. */
+#define FC2_R32_ESCAPE 0x80000000u
+typedef struct fc2_result_escape {
+    uint64_t   index;
+    fc2_result result;
+} fc2_result_escape;
+int fc2_result_compact_launch(const fc2_params *p, const fc2_result *results, uint64_t n, uint32_t *words,
+                              fc2_result_escape *esc, uint32_t esc_cap, uint32_t *esc_count, void *stream);
+/* Host: the 8-byte results back from words[n] and the n_esc escapes (indices < n), on
+ * n_threads threads (<= 0: all cores, at most 64).  FC2_E_FORMAT if the escapes do not match
+ * the FC2_R32_ESCAPE words one to one. */
+int fc2_result_expand(const fc2_params *p, const uint32_t *words, uint64_t n, const fc2_result_escape *esc,
+                      uint64_t n_esc, fc2_result *out, int n_threads);
+
 /* ---- device-resident genome (2-bit bit-sliced + N plane) ---------------- */
 /* Bases of all chromosomes are concatenated, each chromosome starting at a
  * multiple of 64.  Unit u covers global bases [64u, 64u+64):
@@ -385,6 +410,9 @@ typedef struct fc2_synth_cfg {
     int32_t  locus_ordered;        /* 1: pair i's locus is drawn from the i-th of n equal genome
                                       strata (a batch ordered by position); 0: uniform (read order) */
     int32_t  _pad;
+    uint64_t first;                /* pair i of the call is pair first + i of the seeded stream
+                                      (each pair depends only on seed and its stream index): a
+                                      rank generates just its share of a stream */
 } fc2_synth_cfg;
 
 /* Fill a synthetic genome on the device: random bases from a counter-based

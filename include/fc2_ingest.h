@@ -81,6 +81,11 @@ int fc2_ingest_counts_get(const fc2_ingest *h, fc2_ingest_counts *counts);
  * finished (EOF block) by fc2_ingest_close_bam_out or fc2_ingest_close. */
 int fc2_ingest_set_bam_out(fc2_ingest *h, const char *path);
 int fc2_ingest_close_bam_out(fc2_ingest *h);
+
+/* ``samtools view -b`` for SAM text (any compression): every record encoded as htslib's
+ * sam_parse1 does (the -B encoder above), BGZF blocks (zlib level 1, as samtools view -1) + EOF block.  Used to make BAM inputs for
+ * tests and the bench's stdin-BAM CLI run. */
+int fc2_sam_to_bam(const char *sam_path, const char *bam_path);
 #ifdef __cplusplus
 }
 #endif

@@ -189,3 +189,35 @@ def test_gpu_cli_multi_block_sam(tmp_path):
     assert cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory) == 0
     assert cli.main(["-G", fa, "-o", o2, "-q", "--gpus", "2", sam]) == 0
     same(o1, o2)
+
+
+@pytest.mark.parametrize("extra", [[], ["--all-hits", "--non-canonical", "--gpus", "2"]])
+def test_gpu_cli_bam_on_stdin_equals_oracle_cli(tmp_path, extra):
+    """north_star's form: ``samtools view -b ... | python -m find_circ2_amd.cli -G g.fa -o out`` -- a
+    BGZF BAM piped into the shipped CLI (its own process, HIP scan) writes the files the Python loop
+    with the CPU oracle writes from the SAM by path (find_circ.py:467-469: stdin read by what it is)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import subprocess
+    import sys
+    from conftest import ROOT
+    from find_circ2_amd import cli
+    from find_circ2_amd.ingest import sam_to_bam
+    from oracle_engine import oracle_evaluator_factory
+    from test_ingest import same
+    from test_native_caller import _large_sam
+    fa, hdr, body = _large_sam(tmp_path, 8000, seed=2718)
+    sam = str(tmp_path / "in.sam")
+    open(sam, "w").write("\n".join(hdr + body) + "\n")
+    bam = str(tmp_path / "in.bam")
+    sam_to_bam(sam, bam)
+    o1, o2 = str(tmp_path / "oracle_py"), str(tmp_path / "gpu_stdin")
+    assert cli.main(["-G", fa, "-o", o1, "-q", "--python-caller"] + [e for e in extra if e not in ("--gpus", "2")]
+                    + [sam], evaluator_factory=oracle_evaluator_factory) == 0
+    feeder = subprocess.Popen(["cat", bam], stdout=subprocess.PIPE)
+    r = subprocess.run([sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", o2, "-q"] + extra, cwd=ROOT,
+                       stdin=feeder.stdout, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    feeder.stdout.close()
+    feeder.wait()
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    same(o1, o2)

@@ -53,6 +53,17 @@ def _check(args):
     assert np.array_equal((res[~ok] >> np.uint64(48)) & np.uint64(0x6000), err[~ok])
     hits = int(((res & np.uint64(0xFFFF)) != np.uint64(0xFFFF)).sum())
     assert hits > b.n // 3
+    # the 4-byte transfer form (fc2_result_compact_launch -> fc2_result_expand) of every result word
+    from find_circ2_amd import compact, expand
+    dres = torch.from_numpy(res.view(np.int64)).to(dev)
+    c = compact(opt, dres, b.n)
+    torch.cuda.synchronize(dev)
+    n_esc = int(c.count.item())
+    assert n_esc <= c.cap
+    esc = c.esc.cpu().numpy().view(N.ESCAPE_DTYPE)[:n_esc]
+    back = expand(opt, c.words[:b.n].cpu().numpy(), esc)
+    assert np.array_equal(back.view(np.uint64), res)
+    print("compact form: %d escapes of %d" % (n_esc, b.n))
     return b.n, hits
 
 
@@ -66,3 +77,24 @@ def test_configs4_share_every_pair():
     a = argparse.Namespace(workload="hg19", pairs=25_000_000, read_len=150, read_len_min=120, locus_ordered=False)
     n, hits = _check(a)
     assert n == 25_000_000
+
+
+def test_stream_share_equals_slice_of_whole_stream():
+    """bench.stream_share: pairs [lo, hi) of a seeded stream generated on their own (fc2_synth_cfg.first)
+    are byte for byte the same rows as in the whole stream -- what lets each rank hold only its share."""
+    import bench
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    dev = torch.device("cuda", 0)
+    a = argparse.Namespace(workload="hg19", pairs=3_000_000, read_len=100, locus_ordered=False)
+    opt, g, b = bench.build_workload(a, 0, dev)
+    n, kw = bench.workload_cfg(a, 0)
+    for lo, hi in ((0, 1000), (1_234_567, 2_000_000), (2_999_488, 3_000_000)):
+        s = bench.stream_share(opt, g, kw, lo, hi)
+        assert torch.equal(s.pairs[:16 * (hi - lo)], b.pairs[16 * lo:16 * hi])
+        for j in range(b.rw):
+            assert torch.equal(s.read_words[j * s.stride:j * s.stride + hi - lo],
+                               b.read_words[j * b.stride + lo:j * b.stride + hi])
+        for j in range(b.nw):
+            assert torch.equal(s.read_nwords[j * s.stride:j * s.stride + hi - lo],
+                               b.read_nwords[j * b.stride + lo:j * b.stride + hi])

@@ -157,3 +157,21 @@ def test_golden_known_answers_through_stdin_bam(tmp_path):
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     circ = bed_rows(os.path.join(out, "circ_splice_sites.bed"))
     assert {("testbed_plus", 240, 320, "+"), ("testbed_plus", 80, 640, "+")} <= set(circ)
+
+
+def test_native_sam_to_bam_reads_back_as_the_sam(inputs, tmp_path):
+    """fc2_sam_to_bam (the bench's BAM maker) against the Python test encoder: the CLI on either BAM
+    writes the SAM run's files."""
+    from find_circ2_amd.ingest import sam_to_bam as native_sam_to_bam
+    d, fa, data, base = inputs
+    sam = _write(tmp_path, "in.sam", data["sam_gzip"])
+    bam = str(tmp_path / "n.bam")
+    native_sam_to_bam(sam, bam)
+    ing = NativeIngest(bam, True)
+    assert ing.format() == ("bam", "bgzf")
+    ing.close()
+    r = _pipe(["-G", fa, "-o", str(tmp_path / "o"), "-n", "fmt", "-q"], open(bam, "rb").read())
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    same(base["native"], str(tmp_path / "o"))
+    with pytest.raises(Exception, match="BAM already"):
+        native_sam_to_bam(bam, str(tmp_path / "again.bam"))
