@@ -645,52 +645,107 @@ def _decode_sample(opt, g, b, idx):
     return hp, reads, wins, woff, ls
 
 
+def subset_fasta(g, d: str, k: int = 3):
+    """The k largest chromosomes of the device genome written as a FASTA with 50-nt lines (as UCSC
+    hg19) plus its .byo_index (fc2_fasta_open, the reference's store_index format,
+    find_circ.py:157-179): the file the reference's Track/GenomeAccessor would mmap.  Decoded from
+    the device planes in 16M-base pieces.  Returns (path, chromosome indices)."""
+    import ctypes
+    import torch
+    from find_circ2_amd import _native as N
+    order = [int(i) for i in np.argsort(-np.asarray(g.sizes, np.int64), kind="stable")[:k]]
+    path = os.path.join(d, "subset.fa")
+    code = torch.tensor(list(b"ACGTN"), dtype=torch.uint8, device=g.device)
+    width = 50
+    with open(path, "wb") as f:
+        for c in order:
+            f.write(b">" + g.names[c].encode() + b"\n")
+            cs, size = int(g.chrom_start[c]), int(g.sizes[c])
+            step = (1 << 24) // width * width
+            for lo in range(0, size, step):
+                hi = min(size, lo + step)
+                pos = torch.arange(cs + lo, cs + hi, device=g.device, dtype=torch.int64)
+                u, bit = pos >> 6, pos & 63
+                lo_b = (g.units[2 * u] >> bit) & 1
+                hi_b = (g.units[2 * u + 1] >> bit) & 1
+                nn = (g.nplane[u] >> bit) & 1
+                s = code[torch.where(nn == 1, 4, lo_b | (hi_b << 1))].cpu().numpy()
+                full = len(s) // width
+                f.write(np.concatenate([s[:full * width].reshape(full, width),
+                                        np.full((full, 1), 10, np.uint8)], axis=1).tobytes())
+                if len(s) % width:
+                    f.write(s[full * width:].tobytes() + b"\n")
+    h = ctypes.c_void_p()
+    N.check(N.lib().fc2_fasta_open(path.encode(), 1, ctypes.byref(h)))     # writes subset.fa.byo_index
+    N.lib().fc2_fasta_close(h)
+    return path, order
+
+
 def cpu_baselines(opt, g, b, budget_s):
+    """The reported CPU baselines (never the target): (1) the reference's own per-pair path restated
+    literally in Python -- find_breakpoints' O(l^2) string + numpy idiom (find_circ.py:854-974) with
+    BOTH windows fetched per pair through Track.get -> GenomeAccessor.get_data -> indexed_fasta.get_data
+    + .upper() (:900-902, :274-312, :362-368, :189-215) from an mmap'd FASTA of the bench genome (its
+    three largest chromosomes, written from the device planes, with the .byo_index the reference
+    loads), one core, on a sample of this batch's pairs on those chromosomes -- and its first ties
+    checked against the GPU's results; (2) the C literal O(l^2) restatement, one core; (3) the C O(l)
+    restatement on the box's CPU share, both on pre-decoded windows."""
+    import shutil
+    import tempfile
+    import torch
     import oracle
-    from oracle.bp_oracle import Options as ROpt, find_breakpoints as py_find, Span
+    from oracle.bp_oracle import (Options as ROpt, RefGenomeTrack, RefIndexedFasta, Span,
+                                  find_breakpoints as py_find)
 
     rng = np.random.default_rng(99)
-    n_sample = min(b.n, 200_000)
-    idx = np.sort(rng.choice(b.n, n_sample, replace=False))
-    hp, reads, wins, woff, ls = _decode_sample(opt, g, b, idx)
-    e = opt.eff_a
-    bs = (hp["flags"] & 1) != 0
-    rev = (hp["flags"] & 2) != 0
-    skip = (hp["flags"] & 0x10) != 0
+    d = tempfile.mkdtemp(prefix="fc2_cpu_base_", dir="/tmp")
+    try:
+        t_fa = time.perf_counter()
+        fa, subset = subset_fasta(g, d)
+        fa_s = time.perf_counter() - t_fa
+        chrom_col = b.pairs[:16 * b.n].view(torch.int32).view(b.n, 4)[:, 2]
+        on_subset = torch.isin(chrom_col, torch.tensor(subset, dtype=torch.int32, device=b.device))
+        cand = torch.nonzero(on_subset).flatten().cpu().numpy()
+        n_sample = min(len(cand), 200_000)
+        idx = np.sort(rng.choice(cand, n_sample, replace=False))
+        hp, reads, wins, woff, ls = _decode_sample(opt, g, b, idx)
+        bs = (hp["flags"] & 1) != 0
+        rev = (hp["flags"] & 2) != 0
+        skip = (hp["flags"] & 0x10) != 0
+        gpu = b._bench_ref_results.numpy()[idx].view(np.uint64) if hasattr(b, "_bench_ref_results") else None
 
-    # (1) literal Python restatement (the reference's own idiom: string concat + numpy compare per x)
-    class _Win:
-        def __init__(self):
-            self.k = 0
+        # (1) the reference's path, literally: per pair two windows through the Track chain of an mmap'd
+        # FASTA, then the per-x string concat + numpy compare
+        track = RefGenomeTrack(RefIndexedFasta(fa, use_existing_index=True, use_mmap=True))
+        ro = ROpt()
+        done = agree = errors = 0
+        t0 = time.perf_counter()
+        for k in range(len(reads)):
+            if skip[k]:
+                continue
+            # is_backsplice = B.pos - A.aend < 0 (find_circ.py:842): encode the flag through these two
+            a_aend, b_pos = (1, 0) if bs[k] else (0, 1)
+            sp = Span(g.names[int(hp["chrom"][k])], int(hp["a_pos"][k]), a_aend, b_pos, int(hp["b_aend"][k]),
+                      reads[k], bool(rev[k]))
+            try:
+                ties = py_find(sp, track, ro)
+                x = ties[0].x if ties else -1
+                if gpu is not None:
+                    gx = int(gpu[k] & np.uint64(0xFFFF))
+                    gx = gx - 65536 if gx >= 32768 else gx
+                    gt = int((gpu[k] >> np.uint64(32)) & np.uint64(0xFFFF))
+                    agree += int(gx == x and gt == (ties[0].n_hits if ties else 0))
+            except Exception:
+                errors += 1
+                agree += int(gpu is not None and int(gpu[k] >> np.uint64(48)) & 0x6000 != 0)
+            done += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        py_rate = done / (time.perf_counter() - t0)
+    finally:
+        shutil.rmtree(d, ignore_errors=True)
 
-        def get_data(self, chrom, start, end, sense="+"):
-            # hand out the pre-decoded windows in call order: A then B (find_circ.py:901-902)
-            k = self.k
-            self.k += 1
-            pair, which = divmod(k, 2)
-            lw = int(ls[pair]) + 2
-            o = int(woff[pair]) + which * lw
-            return wins[o:o + lw].tobytes()
-
-    wg = _Win()
-    ro = ROpt()
-    t0 = time.perf_counter()
-    done = 0
-    for k in range(len(reads)):
-        if skip[k]:
-            wg.k += 2
-            continue
-        # is_backsplice = B.pos - A.aend < 0 (find_circ.py:842): encode the flag through these two
-        a_aend, b_pos = (1, 0) if bs[k] else (0, 1)
-        sp = Span("c", int(hp["a_pos"][k]), a_aend, b_pos, int(hp["b_aend"][k]), reads[k], bool(rev[k]))
-        py_find(sp, wg, ro)
-        done += 1
-        if time.perf_counter() - t0 > budget_s:
-            break
-    py_rate = done / (time.perf_counter() - t0)
-    py_sample = done
-
-    # (2) C, literal O(l^2), one core;  (3) C, O(l), all host cores (ctypes releases the GIL)
+    # (2) C, literal O(l^2), one core;  (3) C, O(l), the box's CPU share (ctypes releases the GIL)
     p = oracle.params()
 
     def run_c(use_fast, lo, hi):
@@ -704,8 +759,9 @@ def cpu_baselines(opt, g, b, budget_s):
         run_c(False, k, min(len(reads), k + chunk))
         k += chunk
     naive_rate = min(k, len(reads)) / (time.perf_counter() - t0)
-    cores = len(os.sched_getaffinity(0))
-    cores = min(cores, 16)         # the GPU box's CPU share for one GPU
+    visible = len(os.sched_getaffinity(0))
+    # the GPU box grants 16 CPUs per GPU; sched_getaffinity lists the whole machine's CPUs there
+    cores = min(visible, 16)
     t0 = time.perf_counter()
     done_fast = 0
     rounds = 0
@@ -727,14 +783,20 @@ def cpu_baselines(opt, g, b, budget_s):
         model = "unknown"
     return dict(
         main={"value": round(py_rate, 1), "unit": "anchor-pairs/s", "cores": 1, "kind": "port",
-              "sample": "%d pairs of this batch, literal Python restatement of find_circ.py:854-974 "
-                        "(per-x string concat + numpy byte compare, oracle/bp_oracle.py), windows pre-decoded"
-                        % py_sample},
+              "sample": "%d pairs of this batch on %s (its 3 largest chromosomes), literal Python restatement "
+                        "of find_circ.py:854-974 (per-x string concat + numpy byte compare, oracle/bp_oracle.py) "
+                        "with both windows per pair fetched through Track.get -> GenomeAccessor.get_data -> "
+                        "indexed_fasta.get_data + .upper() (find_circ.py:900-902) from an mmap'd FASTA of the "
+                        "bench genome with its .byo_index (written in %.1f s, untimed); first ties agree with the "
+                        "GPU on %d of %d pairs (%d raised, as the GPU flagged)"
+                        % (done, ",".join(g.names[c] for c in subset), fa_s, agree, done, errors)},
         c_naive={"value": round(naive_rate, 1), "unit": "anchor-pairs/s", "cores": 1, "kind": "port",
-                 "sample": "C literal O(l^2) restatement (oracle/bp_oracle.c) on the same sample"},
+                 "sample": "C literal O(l^2) restatement (oracle/bp_oracle.c) on the same sample, windows "
+                           "pre-decoded"},
         c_fast={"value": round(fast_rate, 1), "unit": "anchor-pairs/s", "cores": cores, "kind": "port",
-                "sample": "C O(l) prefix-sum restatement, %d threads, %d pairs x %d rounds" % (
-                    cores, len(reads), rounds)},
+                "sample": "C O(l) prefix-sum restatement, %d threads (the GPU box's CPU share per GPU; "
+                          "sched_getaffinity lists %d), %d pairs x %d rounds, windows pre-decoded" % (
+                              cores, visible, len(reads), rounds)},
         cpu_model=model)
 
 

@@ -695,7 +695,7 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
     uint32_t ni = 0;
     const int lim = l > 0 ? l : 0;
     for (int pass = 0; pass < 2; ++pass) {
-        Rng R2{smix(cfg.seed ^ smix(i * 0x9E37ull + 0xABCDEFull))};   // same mutation stream both passes
+        Rng R2{smix(cfg.seed ^ smix((cfg.first + i) * 0x9E37ull + 0xABCDEFull))};   // same mutation stream both passes
         for (int j = 0; j < lim; ++j) {
             const int t = c0 + e + j;
             unsigned c = t < kA ? gbase(g, cs, sz, A0 + t) : gbase(g, cs, sz, B0 + t - kA);

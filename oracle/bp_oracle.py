@@ -90,10 +90,14 @@ class RefIndexedFasta:
     The index maps chrom -> (ofs, ldata, skip, skipchar, size).
     """
 
-    def __init__(self, fname: str, use_existing_index: bool = False):
+    def __init__(self, fname: str, use_existing_index: bool = False, use_mmap: bool = False):
         self.fname = fname
         with open(fname, 'rb') as f:
-            self.data = f.read()
+            if use_mmap:                    # as the reference does (find_circ.py:104-118): slices copy out
+                import mmap
+                self.data = mmap.mmap(f.fileno(), 0, access=mmap.ACCESS_READ)
+            else:
+                self.data = f.read()
         self.chrom_stats: Dict[str, tuple] = {}
         ipath = fname + '.byo_index'
         if use_existing_index and os.access(ipath, os.R_OK):
@@ -167,6 +171,49 @@ class RefIndexedFasta:
         if sense == '-':
             s = rev_comp(s.decode('latin-1')).encode('latin-1')
         return s
+
+
+class RefGenomeTrack:
+    """``genome = Track(options.genome, accessor=GenomeAccessor)`` (find_circ.py:435-436) as
+    ``find_breakpoints`` calls it per window (``genome.get(chrom, start, end, '+')``, :900-902):
+    ``Track.get`` -> ``Track.load`` (accessor cache keyed by chrom + sense, :274-297, :310-312) ->
+    ``GenomeAccessor.get_data`` (:362-368) -> ``indexed_fasta.get_data`` (:189-215).  The CPU
+    baseline times this chain; ``get_data`` is ``get`` under the name this module's
+    ``find_breakpoints`` calls."""
+
+    def __init__(self, fasta: "RefIndexedFasta"):
+        self.fasta = fasta
+        self.acc_cache: Dict[str, object] = {}
+        self.auto_flush = False              # Track's default (:253)
+        self.last_chrom = ""
+
+    class _Accessor:                         # GenomeAccessor (:329-368)
+        def __init__(self, data):
+            self.data = data
+
+        def get_data(self, chrom, start, end, sense):
+            seq = self.data.get_data(chrom, start, end, "+")
+            if sense == "-":
+                seq = complement(seq.decode("latin-1")).encode("latin-1")
+            return seq
+
+    def load(self, chrom, sense):
+        if self.auto_flush and chrom != self.last_chrom:
+            self.acc_cache = {}
+        self.last_chrom = chrom
+        ID = chrom + sense
+        if ID not in self.acc_cache:
+            acc = RefGenomeTrack._Accessor(self.fasta)
+            covered = [c + '+' for c in self.fasta.chrom_stats] + [c + '-' for c in self.fasta.chrom_stats]   # :348
+            for ID in covered:               # the loop rebinds ID, as at :294-295: a chromosome missing
+                self.acc_cache[ID] = acc     # from the index gets an accessor and fails in get_data (:193)
+        return self.acc_cache[ID]
+
+    def get(self, chrom, start, end, sense):
+        acc = self.load(chrom, sense)
+        return acc.get_data(chrom, start, end, sense)
+
+    get_data = get
 
 
 def _py2_file_lines(data: bytes):

@@ -93,3 +93,41 @@ def test_c_oracle_matches_python_on_known_answers():
                     f = r.first[i]
                     assert (f['x'], f['start'], f['end'], f['strand'].decode(), f['gtag'].decode()) == \
                            (hits[0].x, hits[0].start, hits[0].end, hits[0].strand, hits[0].gtag)
+
+
+def test_ref_track_chain_equals_indexed_fasta(tmp_path):
+    """oracle.bp_oracle.RefGenomeTrack (Track.get -> GenomeAccessor.get_data -> indexed_fasta.get_data,
+    find_circ.py:274-312, 362-368, 189-215), the chain bench.py's CPU baseline times, over an mmap'd
+    FASTA with its .byo_index: the same windows as RefIndexedFasta itself, and the same
+    find_breakpoints results on the CDR1as known answer; a chromosome missing from the index raises
+    KeyError('chrom') from get_data (:193), not from the accessor cache."""
+    import ctypes
+    import shutil
+    from find_circ2_amd import _native as N
+    from oracle.bp_oracle import Options, RefGenomeTrack, RefIndexedFasta, Span, find_breakpoints
+    fa = str(tmp_path / "c.fa")
+    shutil.copy(os.path.join(GOLDEN, "CDR1as_locus.fa"), fa)
+    h = ctypes.c_void_p()
+    N.check(N.lib().fc2_fasta_open(fa.encode(), 1, ctypes.byref(h)))
+    N.lib().fc2_fasta_close(h)
+    plain = RefIndexedFasta(fa)
+    track = RefGenomeTrack(RefIndexedFasta(fa, use_existing_index=True, use_mmap=True))
+    rng = np.random.default_rng(3)
+    for _ in range(300):
+        a = int(rng.integers(-100, 3000))
+        e = a + int(rng.integers(0, 200))
+        assert track.get("CDR1as_locus", a, e, "+") == plain.get_data("CDR1as_locus", a, e, "+")
+    with pytest.raises(KeyError) as ex:
+        track.get("chrX", 10, 20, "+")
+    assert ex.value.args[0] == "chrX"
+    genome = read_fasta(os.path.join(GOLDEN, "CDR1as_locus.fa"))
+    reads = read_fasta(os.path.join(GOLDEN, "cdr1as_reads.fa"))
+    n = 0
+    for name, seq in reads.items():
+        for s in emulate_pairs(name, seq, genome):
+            sp = Span(s.chrom, s.a_pos, s.a_aend, s.b_pos, s.b_aend, s.read_part.encode(), s.primary_reverse)
+            h1 = find_breakpoints(sp, track, Options())
+            h2 = find_breakpoints(sp, plain, Options())
+            assert [(t.x, t.coord) for t in h1] == [(t.x, t.coord) for t in h2]
+            n += bool(h1)
+    assert n >= 3
