@@ -20,7 +20,7 @@ import time
 import queue
 import threading
 from collections import deque
-from typing import Callable, Dict, Optional
+from typing import Callable, Dict, NamedTuple, Optional
 
 import numpy as np
 
@@ -57,6 +57,13 @@ def gpu_batch_evaluator(genome, hp, devices=None, n_threads: int = 0):
     from .pipeline import ScanPipeline
     return ScanPipeline(genome, hp, devices=devices, n_threads=n_threads)
 
+
+
+class CompactChunk(NamedTuple):
+    """A chunk's results in the 4-byte transfer form (include/fc2_bp.h "compact results"): words
+    [n] uint32 and the escapes (N.ESCAPE_DTYPE, indices into the chunk)."""
+    words: np.ndarray
+    escapes: np.ndarray
 
 class NativeCaller:
     """One pass over an alignment file (path or '-') with the native read loop."""
@@ -219,20 +226,13 @@ class NativeCaller:
                     raise item
                 if kind == "eof":
                     break
-                res_ptr = tm_ptr = None
-                tw = 0
+                res = tm = None
                 if n:
                     te = time.perf_counter()
                     res, tm = evaluate.result(item, copy=False) if pipelined else item
                     eval_s[1] += time.perf_counter() - te
-                    res = np.ascontiguousarray(res, dtype=np.int64)
-                    res_ptr = res.ctypes.data
-                    if tm is not None:
-                        tm = np.ascontiguousarray(tm, dtype=np.uint64)
-                        tw = tm.shape[0]
-                        tm_ptr = tm.ctypes.data
                 ts = time.perf_counter()
-                rc = L.fc2_caller_submit(self.h, res_ptr, tm_ptr, tw, n)
+                rc = self._submit(L, res, tm, n)
                 tw_ = time.perf_counter()
                 self._write_outputs(outputs)
                 self.loop_profile["submit_s"] += tw_ - ts
@@ -312,20 +312,13 @@ class NativeCaller:
             if not queue:
                 break
             item, n = queue.popleft()
-            res_ptr = tm_ptr = None
-            tw = 0
+            res = tm = None
             if n:
                 te = time.perf_counter()
                 res, tm = evaluate.result(item, copy=False) if pipelined else item   # consumed by submit below
                 eval_s += time.perf_counter() - te
-                res = np.ascontiguousarray(res, dtype=np.int64)
-                res_ptr = res.ctypes.data
-                if tm is not None:
-                    tm = np.ascontiguousarray(tm, dtype=np.uint64)
-                    tw = tm.shape[0]
-                    tm_ptr = tm.ctypes.data
             ts = time.perf_counter()
-            rc = L.fc2_caller_submit(self.h, res_ptr, tm_ptr, tw, n)
+            rc = self._submit(L, res, tm, n)
             tw_ = time.perf_counter()
             self._write_outputs(outputs)        # what record_hits wrote before any failure
             prof["submit_s"] += tw_ - ts
@@ -350,6 +343,25 @@ class NativeCaller:
         nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
         L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
         return time.time() - t0, int(nr.value), int(npairs.value), eval_s
+
+    def _submit(self, L, res, tm, n):
+        """fc2_caller_submit of one chunk's results: raw 8-byte words, or a CompactChunk (the 4-byte
+        transfer form, fc2_caller_submit32); tm = the --all-hits tie mask [tw, n] or None."""
+        tm_ptr, tw = None, 0
+        if tm is not None:
+            tm = np.ascontiguousarray(tm, dtype=np.uint64)
+            tw = tm.shape[0]
+            tm_ptr = tm.ctypes.data
+        if isinstance(res, CompactChunk):
+            words = np.ascontiguousarray(res.words).view(np.uint32)
+            esc = np.ascontiguousarray(res.escapes, dtype=N.ESCAPE_DTYPE)
+            return L.fc2_caller_submit32(self.h, words.ctypes.data if n else None,
+                                         esc.ctypes.data if len(esc) else None, len(esc), tm_ptr, tw, n)
+        res_ptr = None
+        if n:
+            res = np.ascontiguousarray(res, dtype=np.int64)
+            res_ptr = res.ctypes.data
+        return L.fc2_caller_submit(self.h, res_ptr, tm_ptr, tw, n)
 
     @staticmethod
     def _host_batch(batch, n):

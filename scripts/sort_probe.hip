@@ -265,8 +265,9 @@ int main(int argc, char **argv) {
     CK(hipMalloc((void **)&wt, wt_bytes));
     CK(hipMalloc((void **)&key, n * 4));
     CK(hipMalloc((void **)&perm, n * 4));
-    CK(hipMalloc((void **)&count, 8192 * 4));
-    CK(hipMalloc((void **)&cursor, 8192 * 4));
+    constexpr uint32_t kMaxBuckets = 1u << 16;      // count / cursor capacity; every nb below is checked
+    CK(hipMalloc((void **)&count, kMaxBuckets * 4));
+    CK(hipMalloc((void **)&cursor, kMaxBuckets * 4));
     CK(hipMemset(rows, 1, n * 64));
     CK(hipMemset(src, 2, n * 8));
     CK(hipMemset(wt, 3, wt_bytes));
@@ -284,6 +285,7 @@ int main(int argc, char **argv) {
          "");
     for (int shift : {22, 20, 18}) {               // 748 / 2992 / 11968 buckets of 4 / 1 / 0.25 Mbp
         const uint32_t nb = (uint32_t)((kGenome >> shift) + 1);
+        if (nb > kMaxBuckets) continue;
         bucket_keys<<<grid, 256>>>(key, n, shift);
         const uint32_t sgrid = (uint32_t)((n + kSortT - 1) / kSortT);
         const size_t lds1 = nb * 4, lds2 = (2 * (size_t)nb + kSortT) * 4;
@@ -291,7 +293,7 @@ int main(int argc, char **argv) {
         CK(hipFuncSetAttribute((const void *)k1_hist, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds1));
         CK(hipFuncSetAttribute((const void *)k2_scatter, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds2));
         const float ms_sort = timed([&] {
-            (void)hipMemsetAsync(count, 0, nb * 4);
+                CK(hipMemsetAsync(count, 0, nb * 4));
             k1_hist<<<sgrid, 256, lds1>>>(key, n, nb, count);
             k_prefix<<<1, 64>>>(count, nb, cursor);
             k2_scatter<<<sgrid, 256, lds2>>>(key, n, nb, cursor, perm);

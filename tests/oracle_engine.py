@@ -161,3 +161,30 @@ def pipelined_factory(depth):
     factory.batch = batch
     factory.made = made
     return factory
+
+
+def compact_factory():
+    """oracle_evaluator_factory whose native-caller batch hook hands each chunk's results over in the
+    4-byte transfer form (native_caller.CompactChunk -> fc2_caller_submit32), packed by the numpy
+    restatement of fc2_result_compact_launch's rule (tests/test_compact_results.py); canonical mode
+    only -- with --non-canonical the raw words go as before."""
+    from find_circ2_amd.native_caller import CompactChunk
+    from test_compact_results import pack_restated
+
+    def factory(options, hp):
+        return oracle_evaluator_factory(options, hp)
+
+    def batch(options, hp):
+        evaluate, names, h, dummy = oracle_batch_engine(options, hp)
+
+        def ev(reads, read_off, pairs):
+            res, tm = evaluate(reads, read_off, pairs)
+            if hp.noncanonical:
+                return res, tm
+            words, esc = pack_restated(res.view(np.int64) if hasattr(res, "view") else res)
+            return CompactChunk(words, esc), tm
+        return ev, names, h, dummy
+
+    import numpy as np
+    factory.batch = batch
+    return factory
