@@ -652,19 +652,12 @@ void scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
     }
 }
 
-int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
-    got = false;
-    if (!ensure(h, 4)) {
-        if (int rc = input_rc(h)) return rc;
-        return h->end > h->beg ? fc2::fail(FC2_E_FORMAT, "truncated BAM record") : FC2_OK;
-    }
-    int32_t bs;
-    memcpy(&bs, h->buf.data() + h->beg, 4);
-    if (bs < 32 || !ensure(h, 4 + (size_t)bs))
-        return fc2::fail(FC2_E_FORMAT, "truncated BAM record" + (h->z_err.empty() ? "" : " (" + h->z_err + ")"));
-    const uint8_t *b = (const uint8_t *)h->buf.data() + h->beg + 4;
+// one BAM record body (b: the bs bytes after block_size) into r; thread-safe (reads only the
+// header's reference names), so parser threads can call it.  ops: CIGAR scratch
+void parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
+                    std::vector<std::pair<int, int>> &ops, bool need_text, bool keep_raw) {
     const uint8_t *e = b + bs;
-    if (h->bam_out) r.raw.assign((const char *)b - 4, 4 + (size_t)bs);
+    if (keep_raw) r.raw.assign((const char *)b - 4, 4 + (size_t)bs);
     int32_t ref_id, pos, l_seq, nref, npos, tlen;
     uint8_t l_name, mapq;
     uint16_t bin, n_cig, flag;
@@ -674,7 +667,6 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     const uint8_t *p = b + 32;
     r.qname.assign((const char *)p, l_name ? l_name - 1 : 0);
     p += l_name;
-    std::vector<std::pair<int, int>> &ops = h->ops;
     ops.resize(n_cig);
     for (int k = 0; k < n_cig; ++k) {
         uint32_t c; memcpy(&c, p + 4 * k, 4);
@@ -682,15 +674,18 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     }
     const uint8_t *cigp = p;
     p += 4 * n_cig;
-    static const char *SEQ = "=ACMGRSVTWYHKDBN";
+    // two bases per byte through a 256-entry table of base pairs
+    static const struct Pairs {
+        char t[256][2];
+        Pairs() {
+            static const char *SEQ = "=ACMGRSVTWYHKDBN";
+            for (int v = 0; v < 256; ++v) { t[v][0] = SEQ[v >> 4]; t[v][1] = SEQ[v & 0xF]; }
+        }
+    } kPairs;
     std::string &seq = r.seq;
     seq.resize((size_t)l_seq);
-    for (int k = 0; k + 1 < l_seq; k += 2) {
-        const uint8_t b2 = p[k >> 1];
-        seq[k] = SEQ[b2 >> 4];
-        seq[k + 1] = SEQ[b2 & 0xF];
-    }
-    if (l_seq & 1) seq[l_seq - 1] = SEQ[p[(l_seq - 1) >> 1] >> 4];
+    for (int k = 0; k + 1 < l_seq; k += 2) memcpy(&seq[k], kPairs.t[p[k >> 1]], 2);
+    if (l_seq & 1) seq[l_seq - 1] = kPairs.t[p[(l_seq - 1) >> 1]][0];
     p += (l_seq + 1) / 2;
     std::string &qual = r.qual;
     if (l_seq == 0 || p[0] == 0xFF) qual.assign(1, '*');
@@ -709,11 +704,7 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     r.as_last = r.xs_last = 0;
     scan_bam_tags(r, p, e);
     r.has_qual = !(qual.size() == 1 && qual[0] == '*');
-    if (!h->need_text) {
-        h->beg += 4 + (size_t)bs;
-        got = true;
-        return FC2_OK;
-    }
+    if (!need_text) return;
     std::string cig;
     char tmp[32];
     for (int k = 0; k < n_cig; ++k) {
@@ -733,6 +724,19 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     t += '\t';
     t += qual;
     append_bam_tags(t, p, e);
+}
+
+int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
+    got = false;
+    if (!ensure(h, 4)) {
+        if (int rc = input_rc(h)) return rc;
+        return h->end > h->beg ? fc2::fail(FC2_E_FORMAT, "truncated BAM record") : FC2_OK;
+    }
+    int32_t bs;
+    memcpy(&bs, h->buf.data() + h->beg, 4);
+    if (bs < 32 || !ensure(h, 4 + (size_t)bs))
+        return fc2::fail(FC2_E_FORMAT, "truncated BAM record" + (h->z_err.empty() ? "" : " (" + h->z_err + ")"));
+    parse_bam_body(h, (const uint8_t *)h->buf.data() + h->beg + 4, bs, r, h->ops, h->need_text, h->bam_out != nullptr);
     h->beg += 4 + (size_t)bs;
     got = true;
     return FC2_OK;
