@@ -190,13 +190,14 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
             inflateReset(&zs);
             zs.next_in = (Bytef *)(blk + 12 + xl);
             zs.avail_in = (uInt)(bsz[i] - 12 - xl - 8);
-            zs.next_out = (Bytef *)(B.out.data() + ooff[i]);
+            uint8_t none = 0;                   // an empty block (the EOF marker): zlib wants a real pointer
+            zs.next_out = ooff[i + 1] > ooff[i] ? (Bytef *)(B.out.data() + ooff[i]) : (Bytef *)&none;
             zs.avail_out = (uInt)(ooff[i + 1] - ooff[i]);
             const int rc = inflate(&zs, Z_FINISH);
             const uint8_t *t = blk + bsz[i] - 8;
             const uint32_t crc = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
             if (rc != Z_STREAM_END || zs.avail_out != 0 ||
-                crc32(0L, (const Bytef *)(B.out.data() + ooff[i]), (uInt)(ooff[i + 1] - ooff[i])) != crc)
+                crc32(0L, (const Bytef *)zs.next_out - (ooff[i + 1] - ooff[i]), (uInt)(ooff[i + 1] - ooff[i])) != crc)
                 bad = true;
         }
         inflateEnd(&zs);
@@ -371,7 +372,7 @@ bool ensure(fc2_ingest *h, size_t n) {
             else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), 256,
                                            h->bgzf_nt);
             if (h->buf.size() < h->end + b.out.size()) h->buf.resize(h->end + b.out.size());
-            memcpy(h->buf.data() + h->end, b.out.data(), b.out.size());
+            if (!b.out.empty()) memcpy(h->buf.data() + h->end, b.out.data(), b.out.size());
             h->end += b.out.size();
         } else {
             if (h->z_done) return false;

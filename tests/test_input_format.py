@@ -175,3 +175,69 @@ def test_native_sam_to_bam_reads_back_as_the_sam(inputs, tmp_path):
     same(base["native"], str(tmp_path / "o"))
     with pytest.raises(Exception, match="BAM already"):
         native_sam_to_bam(bam, str(tmp_path / "again.bam"))
+
+
+def _bgzf_blocks(data: bytes, cuts):
+    """BGZF with block boundaries at `cuts` (and an empty block at each cut listed twice)."""
+    import struct
+    import zlib
+    out = bytearray()
+    edges = [0] + list(cuts) + [len(data)]
+    for a, b in zip(edges, edges[1:]):
+        chunk = data[a:b]
+        co = zlib.compressobj(6, zlib.DEFLATED, -15)
+        cdata = co.compress(chunk) + co.flush()
+        bsize = 18 + len(cdata) + 8
+        out += b"\x1f\x8b\x08\x04\x00\x00\x00\x00\x00\xff\x06\x00BC\x02\x00" + struct.pack("<H", bsize - 1)
+        out += cdata + struct.pack("<II", zlib.crc32(chunk) & 0xFFFFFFFF, len(chunk))
+    return bytes(out)
+
+
+def test_edge_forms_read_like_the_plain_sam(inputs, tmp_path):
+    """BGZF with empty blocks and record-splitting block edges, no EOF marker; concatenated gzip
+    members of SAM; the same bytes on a stdin pipe: the SAM run's files, both loops."""
+    d, fa, data, base = inputs
+    sam = data["sam"]
+    bam = gzip.decompress(data["bam_gzip"])
+    forms = {
+        "bam_odd_blocks": _bgzf_blocks(bam, [1, 7, 7, 5000, 65000, 65000, len(bam) - 3]),
+        "sam_odd_blocks": _bgzf_blocks(sam, [10, 10, len(sam) // 2]),
+        "sam_gzip_members": gzip.compress(sam[:len(sam) // 3]) + gzip.compress(sam[len(sam) // 3:]),
+    }
+    for name, blob in forms.items():
+        p = _write(tmp_path, name, blob)
+        for loop, ing in (("native", []), ("py", ["--python-ingest"])):
+            out = str(tmp_path / (name + loop))
+            assert cli.main(["-G", fa, "-o", out, "-n", "fmt", "-q"] + ing + [p],
+                            evaluator_factory=oracle_evaluator_factory) == 0, (name, loop)
+            same(base[loop], out)
+    r = _pipe(["-G", fa, "-o", str(tmp_path / "pipe_odd"), "-n", "fmt", "-q"], forms["bam_odd_blocks"])
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    same(base["native"], str(tmp_path / "pipe_odd"))
+
+
+@pytest.mark.parametrize("form", ["empty", "sam_header_only", "bam_header_only", "bgzf_eof_only"])
+def test_inputs_without_records(tmp_path, form):
+    """No alignment records at all: both loops finish with empty tables (no UnboundLocalError, which
+    the reference raises only for exactly one record, find_circ.py:1486)."""
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    hdr = "@SQ\tSN:testbed_plus\tLN:720\n@SQ\tSN:testbed_minus\tLN:720\n"
+    if form == "empty":
+        blob = b""
+    elif form == "sam_header_only":
+        blob = hdr.encode()
+    elif form == "bam_header_only":
+        p = str(tmp_path / "h.bam")
+        sam_to_bam(hdr, p)
+        blob = open(p, "rb").read()
+    else:
+        blob = bytes.fromhex("1f8b08040000000000ff0600424302001b0003000000000000000000")
+    outs = []
+    for loop, ing in (("native", []), ("py", ["--python-ingest"])):
+        out = str(tmp_path / loop)
+        r = _pipe(["-G", fa, "-o", out, "-q"] + ing, blob)
+        assert r.returncode == 0, (form, loop, r.stderr.decode()[-2000:])
+        outs.append(out)
+        rows = [l for l in open(os.path.join(out, "circ_splice_sites.bed")) if not l.startswith("#")]
+        assert rows == []
+    same(outs[0], outs[1])
