@@ -478,15 +478,15 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw):
     """configs[3]: ONE pair stream (the `n` pairs rank 0 scans in the weak run, seed 1337) cut into
     contiguous batches dealt round-robin to the ranks (shard.my_batches).  Rank 0 scans views of its
     own weak batch; every other rank generates only its batches of the stream (stream_share).  Each
-    batch's results are packed on the device into their 4-byte transfer form (fc2_result_compact_launch,
+    batch's results are packed on the device into their 2-byte transfer form (fc2_result_compact_launch,
     canonical mode) and copied to the batch's input offset of ONE node-local pinned host buffer
     (shard.SharedCompactResults), which rank 0 then holds in input order: the host-side ordered merge
-    junction naming needs (find_circ.py:681-690, weights :544/:563/:579).  Timed three ways: scans only;
-    scans + the compact merge (pack, D2H into the shared buffer, a barrier per step, so rank 0 could
-    consume every step's merged results); and scans + the 8-byte merge (the raw words copied), for
-    comparison.  Then a checked pass: rank 0 poisons the buffer, every rank scans, packs and copies, and
-    the merged buffer expanded on the host (fc2_result_expand, what fc2_caller_submit32 does per chunk)
-    must equal rank 0's single-rank scan of the whole stream word for word."""
+    junction naming needs (find_circ.py:681-690, weights :544/:563/:579).  Timed: scans only; scans +
+    the 2-byte merge (pack, D2H into the shared buffer, a barrier per step, so rank 0 could consume
+    every step's merged results); and, for comparison, the same with the 4-byte form and with the raw
+    8-byte words.  Then checked passes: rank 0 poisons the buffer, every rank scans, packs and copies,
+    and the merged buffer expanded on the host (fc2_result_expand, what fc2_caller_submit_compact does
+    per chunk) must equal rank 0's single-rank scan of the whole stream word for word (both widths)."""
     import torch
     from find_circ2_amd import CompactResults, compact, scan
     from find_circ2_amd.hotpath import ScanOutput
@@ -496,94 +496,105 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw):
     bounds = batch_bounds(n, bsz)
     mine = my_batches(n, bsz, rank, ws)
     cap = max(1024, bsz // 256)
-    merged = SharedCompactResults(n, bounds, cap, create=True, pin=True) if rank == 0 else None
-    raw = SharedResults(n, create=True, pin=True) if rank == 0 else None
-    names = broadcast_name((merged.name, raw.name) if rank == 0 else None) if ws > 1 else (merged.name, raw.name)
+    widths = (2, 4)
+    if rank == 0:
+        merged = {w: SharedCompactResults(n, bounds, cap, create=True, pin=True, width=w) for w in widths}
+        raw = SharedResults(n, create=True, pin=True)
+        names = [merged[w].name for w in widths] + [raw.name]
+    names = broadcast_name(names if rank == 0 else None) if ws > 1 else names
     if rank != 0:
-        merged = SharedCompactResults(n, bounds, cap, name=names[0], pin=True)
-        raw = SharedResults(n, name=names[1], pin=True)
+        merged = {w: SharedCompactResults(n, bounds, cap, name=names[k], pin=True, width=w)
+                  for k, w in enumerate(widths)}
+        raw = SharedResults(n, name=names[-1], pin=True)
     barrier(ws)                                  # every rank attached before rank 0 may unlink at the end
     subs = []
     for k, lo, hi in mine:
         s = b0.sub(lo, hi) if rank == 0 else stream_share(opt, g, cfg_kw, lo, hi)
         subs.append((k, lo, hi, s, torch.empty(hi - lo, dtype=torch.int64, device=dev),
-                     CompactResults(hi - lo, dev, cap)))
+                     {w: CompactResults(hi - lo, dev, cap, width=w) for w in widths}))
     stream = torch.cuda.current_stream(dev)
     copier = torch.cuda.Stream(dev)              # D2H of batch k overlaps the scan of batch k+1
     done = [torch.cuda.Event() for _ in subs]
 
-    def step(mode: str):
+    def step(mode):                              # mode: None (scans only), 2, 4 (compact widths), 8 (raw)
         for j, (k, lo, hi, s, res, comp) in enumerate(subs):
             scan(opt, g, s, out=ScanOutput(res, None, s.tw, s.stride), stream=stream.cuda_stream)
-            if mode == "none":
+            if mode is None:
                 continue
-            if mode == "compact":
-                compact(opt, res, hi - lo, into=comp, stream=stream.cuda_stream)
+            if mode != 8:
+                compact(opt, res, hi - lo, into=comp[mode], stream=stream.cuda_stream)
             done[j].record(stream)
             copier.wait_event(done[j])
             with torch.cuda.stream(copier):
-                if mode == "compact":
-                    merged.words_t[lo:hi].copy_(comp.words[:hi - lo], non_blocking=True)
-                    merged.esc_t[k].copy_(comp.esc.view(torch.uint8), non_blocking=True)
-                    merged.count_t[k:k + 1].copy_(comp.count, non_blocking=True)
+                if mode != 8:
+                    m, c = merged[mode], comp[mode]
+                    m.words_t[lo:hi].copy_(c.words[:hi - lo], non_blocking=True)
+                    m.esc_t[k].copy_(c.esc.view(torch.uint8), non_blocking=True)
+                    m.count_t[k:k + 1].copy_(c.count, non_blocking=True)
                 else:
                     raw.tensor[lo:hi].copy_(res, non_blocking=True)
-        if mode != "none":                       # the next step's scans overwrite res / comp
+        if mode is not None:                     # the next step's scans overwrite res / comp
             stream.wait_stream(copier)
 
-    def timed(mode: str) -> float:
+    def timed(mode) -> float:
         barrier(ws)
         t0 = time.perf_counter()
         for _ in range(steps):
             step(mode)
-            if mode != "none":                   # rank 0 could consume this step's merged results
+            if mode is not None:                 # rank 0 could consume this step's merged results
                 torch.cuda.synchronize(dev)
                 barrier(ws)
         torch.cuda.synchronize(dev)
         barrier(ws)
         return max_over_ranks(time.perf_counter() - t0, ws, dev)
 
-    for mode in ("compact", "raw"):
+    for mode in (2, 4, 8):
         for _ in range(max(1, warmup)):
             step(mode)
     torch.cuda.synchronize(dev)
-    scan_s = timed("none")
-    merge_s = timed("compact")
-    raw_s = timed("raw")
-    # checked pass
-    if rank == 0:
-        merged.words[:] = 0x5A5A5A5A
-        merged.esc_count[:] = -1
-    barrier(ws)
-    step("compact")
-    torch.cuda.synchronize(dev)
-    barrier(ws)
+    scan_s = timed(None)
+    t = {mode: timed(mode) for mode in (2, 4, 8)}
+    # checked passes, one per width
+    equal, n_esc = {}, {}
+    for w in widths:
+        if rank == 0:
+            merged[w].words[:] = 0x5A5A
+            merged[w].esc_count[:] = -1
+        barrier(ws)
+        step(w)
+        torch.cuda.synchronize(dev)
+        barrier(ws)
+        if rank == 0:
+            try:
+                equal[w] = bool(np.array_equal(merged[w].merged(opt), ref64))
+                n_esc[w] = int(merged[w].esc_count.sum())
+            except Exception as ex:              # an overflowed escape area or a bad escape list
+                equal[w], n_esc[w] = repr(ex), None
     out = None
     if rank == 0:
-        try:
-            m = merged.merged(opt)
-            equal = bool(np.array_equal(m, ref64))
-            n_esc = int(merged.esc_count.sum())
-        except Exception as ex:                  # an overflowed escape area or a bad escape list
-            equal, n_esc = repr(ex), None
+        def form(mode):
+            return {"value": round(n * steps / t[mode], 1), "ms_per_step": round(t[mode] / steps * 1e3, 4),
+                    "merge_ms_per_step": round((t[mode] - scan_s) / steps * 1e3, 4)}
         out = {
-            "value": round(n * steps / merge_s, 1), "unit": "anchor-pairs/s", "scaling": "strong",
-            "ms_per_step": round(merge_s / steps * 1e3, 4),
+            "value": round(n * steps / t[2], 1), "unit": "anchor-pairs/s", "scaling": "strong",
+            "ms_per_step": round(t[2] / steps * 1e3, 4),
             "scan_only": {"value": round(n * steps / scan_s, 1), "ms_per_step": round(scan_s / steps * 1e3, 4)},
-            "merge_ms_per_step": round((merge_s - scan_s) / steps * 1e3, 4),
-            "merge_bytes_per_pair": 4, "escapes": n_esc,
-            "merge_8B_words": {"value": round(n * steps / raw_s, 1), "ms_per_step": round(raw_s / steps * 1e3, 4),
-                               "merge_ms_per_step": round((raw_s - scan_s) / steps * 1e3, 4)},
+            "merge_ms_per_step": round((t[2] - scan_s) / steps * 1e3, 4),
+            "merge_bytes_per_pair": 2, "escapes": n_esc[2],
+            "merge_4B_words": dict(form(4), escapes=n_esc[4], merged_equals_single_rank=equal[4]),
+            "merge_8B_words": form(8),
             "pairs_total": n, "batch_pairs": bsz, "n_batches": len(bounds), "ranks": ws,
-            "merged_equals_single_rank": equal,
+            "merged_equals_single_rank": equal[2],
             "note": "one %d-pair stream in %d contiguous batches of %d dealt round-robin to %d rank(s), each rank "
-                    "holding only its batches; each batch's results packed on the device to 4 B/pair "
-                    "(fc2_result_compact_launch) and copied into a node-local pinned shared-memory buffer at "
-                    "their input offsets (host-side ordered merge, no collective on the data path); value = "
-                    "stream pairs / (scans + pack + merge + per-step barrier), max over ranks; merge_8B_words = "
-                    "the same with the raw 8-B words copied" % (n, len(bounds), bsz, ws)}
+                    "holding only its batches; each batch's results packed on the device to 2 B/pair "
+                    "(fc2_result_compact_launch, canonical mode, escapes for the rest) and copied into a node-local "
+                    "pinned shared-memory buffer at their input offsets (host-side ordered merge, no collective on "
+                    "the data path); value = stream pairs / (scans + pack + merge + per-step barrier), max over "
+                    "ranks; merge_4B_words / merge_8B_words = the same with the 4-byte form / the raw 8-B words"
+                    % (n, len(bounds), bsz, ws)}
     barrier(ws)
-    merged.close()
+    for m in merged.values():
+        m.close()
     raw.close()
     return out
 

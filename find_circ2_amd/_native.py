@@ -49,6 +49,7 @@ RESULT_DTYPE = np.dtype([("best_x", "<i2"), ("dist", "u1"), ("ov", "u1"), ("n_ti
 assert PAIR_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 8
 ESCAPE_DTYPE = np.dtype([("index", "<u8"), ("result", RESULT_DTYPE)])     # fc2_result_escape
 R32_ESCAPE = 0x80000000
+R16_ESCAPE = 0x007F
 
 
 class Fc2Error(RuntimeError):
@@ -128,7 +129,7 @@ EXPORTED = [
     "fc2_ingest_format", "fc2_sam_to_bam",
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
-    "fc2_caller_submit", "fc2_caller_submit32", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
+    "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
     "fc2_caller_set_reads_gz", "fc2_caller_close_reads",
 ]
 
@@ -198,8 +199,8 @@ def lib() -> ctypes.CDLL:
         "fc2_bp_scan_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp, u32, vp]),
         "fc2_bp_scan_bytes_launch": (ctypes.c_int, [P(Params), P(BytesView), vp, vp, u32, u64, vp]),
         "fc2_probe_pattern_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp]),
-        "fc2_result_compact_launch": (ctypes.c_int, [P(Params), vp, u64, vp, vp, u32, vp, vp]),
-        "fc2_result_expand": (ctypes.c_int, [P(Params), vp, u64, vp, u64, vp, ctypes.c_int]),
+        "fc2_result_compact_launch": (ctypes.c_int, [P(Params), vp, u64, ctypes.c_int, vp, vp, u32, vp, vp]),
+        "fc2_result_expand": (ctypes.c_int, [P(Params), vp, ctypes.c_int, u64, vp, u64, vp, ctypes.c_int]),
         "fc2_fasta_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(vp)]),
         "fc2_fasta_close": (None, [vp]),
         "fc2_fasta_n_chrom": (ctypes.c_int, [vp]),
@@ -245,7 +246,7 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_close": (None, [vp]),
         "fc2_caller_next": (ctypes.c_int, [vp, P(CallerBatch), P(ctypes.c_int)]),
         "fc2_caller_submit": (ctypes.c_int, [vp, vp, vp, u32, u64]),
-        "fc2_caller_submit32": (ctypes.c_int, [vp, vp, vp, u64, vp, u32, u64]),
+        "fc2_caller_submit_compact": (ctypes.c_int, [vp, vp, ctypes.c_int, vp, u64, vp, u32, u64]),
         "fc2_caller_queued": (ctypes.c_int, [vp]),
         "fc2_caller_take": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_set_reads_gz": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, u64]),

@@ -1667,14 +1667,14 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
     return rc;
 }
 
-extern "C" int fc2_caller_submit32(fc2_caller *h, const uint32_t *words, const fc2_result_escape *esc, uint64_t n_esc,
-                                   const uint64_t *tiemask, uint32_t tw, uint64_t stride) {
-    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit32: null argument");
+extern "C" int fc2_caller_submit_compact(fc2_caller *h, const void *words, int width, const fc2_result_escape *esc,
+                                         uint64_t n_esc, const uint64_t *tiemask, uint32_t tw, uint64_t stride) {
+    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_compact: null argument");
     size_t n = 0;
     {
         std::lock_guard<std::mutex> lk(h->qmu);
         if (h->queued.empty())
-            return fc2::fail(FC2_E_PARAM, "fc2_caller_submit32: no chunk handed out by fc2_caller_next");
+            return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_compact: no chunk handed out by fc2_caller_next");
         n = h->queued.front().b_pairs.size();
     }
     // the chunk's 8-byte results back from the transfer form, into per-thread scratch (a chunk's
@@ -1687,7 +1687,7 @@ extern "C" int fc2_caller_submit32(fc2_caller *h, const uint32_t *words, const f
         p.margin = h->o.margin;
         p.maxdist = h->o.maxdist;
         p.noncanonical = h->o.noncanonical;
-        if (int rc = fc2_result_expand(&p, words, n, esc, n_esc, scratch.data(), 1)) return rc;
+        if (int rc = fc2_result_expand(&p, words, width, n, esc, n_esc, scratch.data(), 1)) return rc;
     }
     return fc2_caller_submit(h, n ? scratch.data() : nullptr, tiemask, tw, stride);
 }

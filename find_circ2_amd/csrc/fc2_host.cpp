@@ -22,7 +22,7 @@
 #include <vector>
 
 #include "fc2_common.h"
-#include "fc2_r32.h"
+#include "fc2_compact.h"
 
 namespace fc2 {
 
@@ -876,19 +876,35 @@ extern "C" int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64
 }
 
 // ---- compact results (include/fc2_bp.h) --------------------------------------------------------
-extern "C" int fc2_result_expand(const fc2_params *p, const uint32_t *words, uint64_t n, const fc2_result_escape *esc,
-                                 uint64_t n_esc, fc2_result *out, int n_threads) {
+extern "C" int fc2_result_expand(const fc2_params *p, const void *words, int width, uint64_t n,
+                                 const fc2_result_escape *esc, uint64_t n_esc, fc2_result *out, int n_threads) {
     if (int rc = fc2::validate_params(p)) return rc;
-    if (p->noncanonical) return fc2::fail(FC2_E_PARAM, "fc2_result_expand: the 4-byte form holds canonical-mode results only");
+    if (p->noncanonical) return fc2::fail(FC2_E_PARAM, "fc2_result_expand: the compact forms hold canonical-mode results only");
+    if (width != 2 && width != 4) return fc2::fail(FC2_E_PARAM, "fc2_result_expand: width is 2 or 4");
     if ((n && (!words || !out)) || (n_esc && !esc)) return fc2::fail(FC2_E_PARAM, "fc2_result_expand: bad args");
     std::atomic<uint64_t> flagged{0};
+    auto escaped = [&](uint64_t i) {
+        return width == 2 ? (((const uint16_t *)words)[i] & 0x7Fu) == FC2_R16_ESCAPE
+                          : (((const uint32_t *)words)[i] & FC2_R32_ESCAPE) != 0;
+    };
     parallel_for(n, n_workers(n_threads), [&](uint64_t b, uint64_t e) {
         uint64_t f = 0;
         uint64_t *o = (uint64_t *)out;
-        for (uint64_t i = b; i < e; ++i) {
-            const uint32_t c = words[i];
-            f += c >> 31;
-            o[i] = (c & FC2_R32_ESCAPE) ? 0 : fc2::r32_unpack(c);
+        if (width == 2) {
+            const uint16_t *w = (const uint16_t *)words;
+            for (uint64_t i = b; i < e; ++i) {
+                const uint16_t c = w[i];
+                const bool x = (c & 0x7Fu) == FC2_R16_ESCAPE;
+                f += x;
+                o[i] = x ? 0 : fc2::r16_unpack(c);
+            }
+        } else {
+            const uint32_t *w = (const uint32_t *)words;
+            for (uint64_t i = b; i < e; ++i) {
+                const uint32_t c = w[i];
+                f += c >> 31;
+                o[i] = (c & FC2_R32_ESCAPE) ? 0 : fc2::r32_unpack(c);
+            }
         }
         flagged += f;
     });
@@ -897,7 +913,7 @@ extern "C" int fc2_result_expand(const fc2_params *p, const uint32_t *words, uin
                                            std::to_string(n_esc) + " escapes");
     std::vector<uint64_t> idx(n_esc);
     for (uint64_t k = 0; k < n_esc; ++k) {
-        if (esc[k].index >= n || !(words[esc[k].index] & FC2_R32_ESCAPE))
+        if (esc[k].index >= n || !escaped(esc[k].index))
             return fc2::fail(FC2_E_FORMAT, "fc2_result_expand: escape " + std::to_string(k) + " has no escaped word");
         idx[k] = esc[k].index;
         out[esc[k].index] = esc[k].result;

@@ -24,7 +24,7 @@
 #include <stdint.h>
 
 #include "fc2_common.h"
-#include "fc2_r32.h"
+#include "fc2_compact.h"
 #include "fc2_scan32.h"
 
 namespace {
@@ -1025,39 +1025,46 @@ extern "C" int fc2_synth_pairs_launch(const fc2_params *p, const fc2_synth_cfg *
     return hip_check(hipGetLastError(), "synth_pairs_kernel launch");
 }
 
-// compact results (include/fc2_bp.h): 8 B in, 4 B out per pair, streamed; escapes are rare
+// compact results (include/fc2_bp.h): 8 B in, 4 or 2 B out per pair, streamed; escapes are rare
+template <int WIDTH>
 __global__ void __launch_bounds__(256) result_compact_kernel(const uint64_t *__restrict__ res, uint64_t n,
-                                                             uint32_t *__restrict__ words, fc2_result_escape *esc,
+                                                             void *__restrict__ words, fc2_result_escape *esc,
                                                              uint32_t cap, uint32_t *count) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const uint64_t w = __builtin_nontemporal_load(res + i);
-    uint32_t c = fc2::r32_pack(w);
-    if (fc2::r32_unpack(c) != w) {
-        c = FC2_R32_ESCAPE;
+    bool escape;
+    const uint32_t c = fc2::compact_pack(w, WIDTH, escape);
+    if (escape) {
         const uint32_t k = atomicAdd(count, 1u);
         if (k < cap) {
             esc[k].index = i;
             memcpy(&esc[k].result, &w, sizeof w);
         }
     }
-    __builtin_nontemporal_store(c, words + i);
+    if constexpr (WIDTH == 2) __builtin_nontemporal_store((uint16_t)c, (uint16_t *)words + i);
+    else __builtin_nontemporal_store(c, (uint32_t *)words + i);
 }
 
-extern "C" int fc2_result_compact_launch(const fc2_params *p, const fc2_result *results, uint64_t n, uint32_t *words,
-                                         fc2_result_escape *esc, uint32_t esc_cap, uint32_t *esc_count,
+extern "C" int fc2_result_compact_launch(const fc2_params *p, const fc2_result *results, uint64_t n, int width,
+                                         void *words, fc2_result_escape *esc, uint32_t esc_cap, uint32_t *esc_count,
                                          void *stream) {
     int rc = fc2::validate_params(p);
     if (rc) return rc;
     if (p->noncanonical)
-        return fc2::fail(FC2_E_PARAM, "fc2_result_compact_launch: the 4-byte form holds canonical-mode results only");
+        return fc2::fail(FC2_E_PARAM, "fc2_result_compact_launch: the compact forms hold canonical-mode results only");
+    if (width != 2 && width != 4) return fc2::fail(FC2_E_PARAM, "fc2_result_compact_launch: width is 2 or 4");
     if (!esc_count || (n && (!results || !words)) || (esc_cap && !esc))
         return fc2::fail(FC2_E_PARAM, "fc2_result_compact_launch: bad args");
     hipError_t e = hipMemsetAsync(esc_count, 0, sizeof(uint32_t), (hipStream_t)stream);
     if (e != hipSuccess) return hip_check(e, "result_compact count reset");
     if (n == 0) return FC2_OK;
-    hipLaunchKernelGGL(result_compact_kernel, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
-                       (const uint64_t *)results, n, words, esc, esc_cap, esc_count);
+    if (width == 2)
+        hipLaunchKernelGGL(result_compact_kernel<2>, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                           (const uint64_t *)results, n, words, esc, esc_cap, esc_count);
+    else
+        hipLaunchKernelGGL(result_compact_kernel<4>, dim3(grid_for(n, 256)), dim3(256), 0, (hipStream_t)stream,
+                           (const uint64_t *)results, n, words, esc, esc_cap, esc_count);
     return hip_check(hipGetLastError(), "result_compact_kernel launch");
 }
 

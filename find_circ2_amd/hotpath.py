@@ -393,44 +393,52 @@ class ScanOutput:
 
 
 class CompactResults:
-    """The 4-byte transfer form of a run of results (include/fc2_bp.h "compact results"): device
-    words [n] (uint32), escape slots [cap] (``N.ESCAPE_DTYPE`` as 16 bytes each) and the escape count."""
+    """A compact transfer form of a run of results (include/fc2_bp.h "compact results"): device
+    words [n] (int32 for width 4, int16 for width 2), escape slots [cap] (``N.ESCAPE_DTYPE`` as
+    16 bytes each) and the escape count."""
 
-    def __init__(self, n: int, device, cap: int = 0):
+    def __init__(self, n: int, device, cap: int = 0, width: int = 4):
         torch = _torch()
-        self.n = n
+        if width not in (2, 4):
+            raise ValueError("width is 2 or 4")
+        self.n, self.width = n, width
         self.cap = cap or max(1024, n // 256)
-        self.words = torch.empty(max(n, 1), dtype=torch.int32, device=device)
+        self.words = torch.empty(max(n, 1), dtype=torch.int16 if width == 2 else torch.int32, device=device)
         self.esc = torch.empty(2 * self.cap, dtype=torch.int64, device=device)
         self.count = torch.zeros(1, dtype=torch.int32, device=device)
 
 
-def compact(options: Options, results, n: int, into: CompactResults = None, stream=None) -> CompactResults:
-    """Pack the first ``n`` 8-byte results of the device tensor ``results`` into the 4-byte form
-    (``fc2_result_compact_launch``, asynchronous on ``stream``); canonical mode only."""
+def compact(options: Options, results, n: int, into: CompactResults = None, stream=None,
+            width: int = 4) -> CompactResults:
+    """Pack the first ``n`` 8-byte results of the device tensor ``results`` into a compact form
+    (``fc2_result_compact_launch``, asynchronous on ``stream``); canonical mode only.  ``into``
+    decides the width when given."""
     torch = _torch()
-    c = into if into is not None else CompactResults(n, results.device)
+    c = into if into is not None else CompactResults(n, results.device, width=width)
     if c.n < n:
         raise ValueError("compact buffers hold %d results, %d given" % (c.n, n))
     s = stream if stream is not None else torch.cuda.current_stream(results.device).cuda_stream
     p = options.params()
-    N.check(N.lib().fc2_result_compact_launch(ctypes.byref(p), results.data_ptr(), n, c.words.data_ptr(),
+    N.check(N.lib().fc2_result_compact_launch(ctypes.byref(p), results.data_ptr(), n, c.width, c.words.data_ptr(),
                                               c.esc.data_ptr(), c.cap, c.count.data_ptr(), s))
     return c
 
 
 def expand(options: Options, words: np.ndarray, esc: np.ndarray, out: np.ndarray = None,
            n_threads: int = 0) -> np.ndarray:
-    """Host: the 8-byte result words (int64) back from the 4-byte words (uint32 / int32 array) and
-    the escapes (``N.ESCAPE_DTYPE``), ``fc2_result_expand``."""
-    words = np.ascontiguousarray(words).view(np.uint32)
+    """Host: the 8-byte result words (int64) back from compact words (a 4-byte dtype: width 4, a
+    2-byte dtype: width 2) and the escapes (``N.ESCAPE_DTYPE``), ``fc2_result_expand``."""
+    words = np.ascontiguousarray(words)
+    width = words.dtype.itemsize
+    if width not in (2, 4):
+        raise ValueError("compact words are 2 or 4 bytes, not %d" % width)
     esc = np.ascontiguousarray(esc, dtype=N.ESCAPE_DTYPE) if len(esc) else np.zeros(0, N.ESCAPE_DTYPE)
     n = len(words)
     if out is None:
         out = np.empty(n, np.int64)
     p = options.params()
-    N.check(N.lib().fc2_result_expand(ctypes.byref(p), words.ctypes.data, n, esc.ctypes.data if len(esc) else None,
-                                      len(esc), out.ctypes.data, int(n_threads)))
+    N.check(N.lib().fc2_result_expand(ctypes.byref(p), words.ctypes.data, width, n,
+                                      esc.ctypes.data if len(esc) else None, len(esc), out.ctypes.data, int(n_threads)))
     return out
 
 

@@ -60,8 +60,8 @@ def gpu_batch_evaluator(genome, hp, devices=None, n_threads: int = 0):
 
 
 class CompactChunk(NamedTuple):
-    """A chunk's results in the 4-byte transfer form (include/fc2_bp.h "compact results"): words
-    [n] uint32 and the escapes (N.ESCAPE_DTYPE, indices into the chunk)."""
+    """A chunk's results in a compact transfer form (include/fc2_bp.h "compact results"): words [n]
+    (a 4- or 2-byte dtype: the width) and the escapes (N.ESCAPE_DTYPE, indices into the chunk)."""
     words: np.ndarray
     escapes: np.ndarray
 
@@ -345,18 +345,18 @@ class NativeCaller:
         return time.time() - t0, int(nr.value), int(npairs.value), eval_s
 
     def _submit(self, L, res, tm, n):
-        """fc2_caller_submit of one chunk's results: raw 8-byte words, or a CompactChunk (the 4-byte
-        transfer form, fc2_caller_submit32); tm = the --all-hits tie mask [tw, n] or None."""
+        """fc2_caller_submit of one chunk's results: raw 8-byte words, or a CompactChunk (a compact
+        transfer form, fc2_caller_submit_compact); tm = the --all-hits tie mask [tw, n] or None."""
         tm_ptr, tw = None, 0
         if tm is not None:
             tm = np.ascontiguousarray(tm, dtype=np.uint64)
             tw = tm.shape[0]
             tm_ptr = tm.ctypes.data
         if isinstance(res, CompactChunk):
-            words = np.ascontiguousarray(res.words).view(np.uint32)
+            words = np.ascontiguousarray(res.words)
             esc = np.ascontiguousarray(res.escapes, dtype=N.ESCAPE_DTYPE)
-            return L.fc2_caller_submit32(self.h, words.ctypes.data if n else None,
-                                         esc.ctypes.data if len(esc) else None, len(esc), tm_ptr, tw, n)
+            return L.fc2_caller_submit_compact(self.h, words.ctypes.data if n else None, words.dtype.itemsize,
+                                               esc.ctypes.data if len(esc) else None, len(esc), tm_ptr, tw, n)
         res_ptr = None
         if n:
             res = np.ascontiguousarray(res, dtype=np.int64)

@@ -123,20 +123,23 @@ class SharedResults:
 
 
 class SharedCompactResults(SharedResults):
-    """The same node-local ordered merge in the results' 4-byte transfer form (include/fc2_bp.h
-    "compact results", canonical mode): one /dev/shm segment holding ``words`` [n] (uint32, at each
-    batch's input offset), per batch ``cap`` escape slots (``N.ESCAPE_DTYPE``, indices relative to
-    the batch start) and the batch's escape count.  Half the bytes of the 8-byte merge cross PCIe
-    and land in host memory; ``merged()`` expands the whole stream (fc2_result_expand) where a
-    consumer wants 8-byte words, and fc2_caller_submit32 takes the form as it is."""
+    """The same node-local ordered merge in a compact transfer form of the results (include/fc2_bp.h
+    "compact results", canonical mode, `width` 4 or 2 bytes per pair): one /dev/shm segment holding
+    ``words`` [n] (at each batch's input offset), per batch ``cap`` escape slots (``N.ESCAPE_DTYPE``,
+    indices relative to the batch start) and the batch's escape count.  A half or a quarter of the
+    bytes of the 8-byte merge cross PCIe and land in host memory; ``merged()`` expands the whole
+    stream (fc2_result_expand) where a consumer wants 8-byte words, and fc2_caller_submit_compact
+    takes the form as it is."""
 
     def __init__(self, n: int, bounds: Sequence[Tuple[int, int]], cap: int, name: str = None, create: bool = False,
-                 pin: bool = False):
+                 pin: bool = False, width: int = 4):
         from multiprocessing import resource_tracker, shared_memory
         from . import _native as N
-        self.n, self.bounds, self.cap = int(n), list(bounds), int(cap)
+        if width not in (2, 4):
+            raise ValueError("width is 2 or 4")
+        self.n, self.bounds, self.cap, self.width = int(n), list(bounds), int(cap), width
         nb = len(self.bounds)
-        self._w_bytes = (4 * self.n + 63) // 64 * 64
+        self._w_bytes = (width * self.n + 63) // 64 * 64
         self._e_bytes = 16 * self.cap * nb
         size = max(64, self._w_bytes + self._e_bytes + 8 * nb)
         self.creator = create
@@ -148,7 +151,7 @@ class SharedCompactResults(SharedResults):
                 pass
         self.name = self.shm.name
         buf = self.shm.buf
-        self.words = np.ndarray((self.n,), np.uint32, buffer=buf)
+        self.words = np.ndarray((self.n,), np.uint16 if width == 2 else np.uint32, buffer=buf)
         self.esc = np.ndarray((nb, self.cap), N.ESCAPE_DTYPE, buffer=buf, offset=self._w_bytes)
         self.esc_count = np.ndarray((nb,), np.int32, buffer=buf, offset=self._w_bytes + self._e_bytes)
         self.array = np.ndarray((size,), np.uint8, buffer=buf)      # the whole segment (pinning, poisoning)
@@ -158,7 +161,7 @@ class SharedCompactResults(SharedResults):
             self._pinned = True
         import torch
         self.tensor = torch.from_numpy(self.array)
-        self.words_t = torch.from_numpy(self.words.view(np.int32))
+        self.words_t = torch.from_numpy(self.words.view(np.int16 if width == 2 else np.int32))
         self.esc_t = torch.from_numpy(self.esc.view(np.uint8).reshape(nb, 16 * self.cap))
         self.count_t = torch.from_numpy(self.esc_count)
 
@@ -167,6 +170,8 @@ class SharedCompactResults(SharedResults):
         parts = []
         for k, (lo, _) in enumerate(self.bounds):
             c = int(self.esc_count[k])
+            if c < 0:
+                raise ValueError("batch %d: its escape count was never written" % k)
             if c > self.cap:
                 raise ValueError("batch %d has %d escapes, %d slots" % (k, c, self.cap))
             e = self.esc[k, :c].copy()

@@ -106,29 +106,32 @@ typedef struct fc2_result {
     uint16_t info;      /* FC2_RES_*                              */
 } fc2_result;
 
-/* ---- compact results: the 4-byte transfer form ---------------------------- */
-/* What moves a batch's results off the device (the ordered merge of a strong-scaled stream,
- * find_circ.py:681-690 naming + :544/:563/:579 weight sums in input order) at 4 B per pair
- * instead of 8.  Canonical mode only (no --non-canonical): a hit's signal is implied by its
- * strand ('+' GTAG, '-' CTAC, :924-954), so words[i] =
- *   bits 0-7 best_x + 1 (0: no hit) | 8-15 n_ties | 16-19 dist | 20-23 ov | 24 '-' |
- *   25 FC2_RES_ERR_KEY | 26 FC2_RES_ERR_WIN | 27 FC2_RES_DONE | 31 FC2_R32_ESCAPE.
- * A result that would not come back unchanged (x > 254, n_ties > 255, dist or ov > 15, ...)
- * gets FC2_R32_ESCAPE and travels whole as an escape (its index, its fc2_result), in no
- * particular order.  *esc_count (device) is zeroed by the launch and counts every escape;
- * only the first esc_cap are stored: a count above esc_cap means the caller must move the
- * 8-byte results instead. */
+/* ---- compact results: the 4- and 2-byte transfer forms ------------------------ */
+/* What moves a batch's results off the device in bulk (the ordered merge of a strong-scaled
+ * stream, find_circ.py:681-690 naming + :544/:563/:579 weight sums in input order) at `width` = 4
+ * or 2 bytes per pair instead of 8.  Canonical mode only (no --non-canonical): a hit's signal is
+ * implied by its strand ('+' GTAG, '-' CTAC, :924-954), and FC2_RES_DONE is implied.
+ *   width 4, uint32 words[i] = bits 0-7 best_x + 1 (0: no hit) | 8-15 n_ties | 16-19 dist |
+ *     20-23 ov | 24 '-' | 25 FC2_RES_ERR_KEY | 26 FC2_RES_ERR_WIN | 27 FC2_RES_DONE | 31 escape.
+ *   width 2, uint16 words[i] = bits 0-6 best_x + 1 (0: no hit, 0x7F: escape) | 7 '-' |
+ *     8-9 dist | 10-11 ov | 12-15 n_ties - 1; a result with an error bit escapes.
+ * A result that would not come back unchanged (too large a field, an error bit in the 2-byte form,
+ * ...) gets the escape word and travels whole as an escape (its index, its fc2_result), in no
+ * particular order.  *esc_count (device) is zeroed by the launch and counts every escape; only
+ * the first esc_cap are stored: a count above esc_cap means the caller must move the 8-byte
+ * results instead. */
 #define FC2_R32_ESCAPE 0x80000000u
+#define FC2_R16_ESCAPE 0x007Fu
 typedef struct fc2_result_escape {
     uint64_t   index;
     fc2_result result;
 } fc2_result_escape;
-int fc2_result_compact_launch(const fc2_params *p, const fc2_result *results, uint64_t n, uint32_t *words,
+int fc2_result_compact_launch(const fc2_params *p, const fc2_result *results, uint64_t n, int width, void *words,
                               fc2_result_escape *esc, uint32_t esc_cap, uint32_t *esc_count, void *stream);
-/* Host: the 8-byte results back from words[n] and the n_esc escapes (indices < n), on
- * n_threads threads (<= 0: all cores, at most 64).  FC2_E_FORMAT if the escapes do not match
- * the FC2_R32_ESCAPE words one to one. */
-int fc2_result_expand(const fc2_params *p, const uint32_t *words, uint64_t n, const fc2_result_escape *esc,
+/* Host: the 8-byte results back from words[n] (width 4 or 2) and the n_esc escapes (indices < n),
+ * on n_threads threads (<= 0: all cores, at most 64).  FC2_E_FORMAT if the escapes do not match
+ * the escaped words one to one. */
+int fc2_result_expand(const fc2_params *p, const void *words, int width, uint64_t n, const fc2_result_escape *esc,
                       uint64_t n_esc, fc2_result *out, int n_threads);
 
 /* ---- device-resident genome (2-bit bit-sliced + N plane) ---------------- */

@@ -163,13 +163,13 @@ def pipelined_factory(depth):
     return factory
 
 
-def compact_factory():
-    """oracle_evaluator_factory whose native-caller batch hook hands each chunk's results over in the
-    4-byte transfer form (native_caller.CompactChunk -> fc2_caller_submit32), packed by the numpy
-    restatement of fc2_result_compact_launch's rule (tests/test_compact_results.py); canonical mode
-    only -- with --non-canonical the raw words go as before."""
+def compact_factory(width=4):
+    """oracle_evaluator_factory whose native-caller batch hook hands each chunk's results over in a
+    compact transfer form (native_caller.CompactChunk -> fc2_caller_submit_compact), packed by the
+    numpy restatement of fc2_result_compact_launch's rules (tests/test_compact_results.py); canonical
+    mode only -- with --non-canonical the raw words go as before."""
     from find_circ2_amd.native_caller import CompactChunk
-    from test_compact_results import pack_restated
+    from test_compact_results import pack
 
     def factory(options, hp):
         return oracle_evaluator_factory(options, hp)
@@ -181,7 +181,7 @@ def compact_factory():
             res, tm = evaluate(reads, read_off, pairs)
             if hp.noncanonical:
                 return res, tm
-            words, esc = pack_restated(res.view(np.int64) if hasattr(res, "view") else res)
+            words, esc = pack(res.view(np.int64) if hasattr(res, "view") else res, width)
             return CompactChunk(words, esc), tm
         return ev, names, h, dummy
 

@@ -61,7 +61,7 @@ def test_two_ranks_configs3_and_configs4_on_hg19():
     """configs[3] and configs[4] on their own workload (hg19-shaped genome) through the real kernel with
     two ranks (both on the box's GPU; an 8-GPU node runs the same code with one GPU each):
     configs[3] -- an 8M-pair stream dealt round-robin, each rank generating only its batches, merged in
-    the 4-byte form -- equals the single-rank scan word for word; configs[4] -- an 8M-pair 120-150 bp
+    the 2- and 4-byte forms -- equals the single-rank scan word for word; configs[4] -- an 8M-pair 120-150 bp
     stream in two contiguous shares -- has the same order-sensitive results checksum as one rank."""
     extra = ["--pairs", "8000000", "--config4-pairs", "8000000"]
     one = _bench(1, extra)
@@ -70,7 +70,7 @@ def test_two_ranks_configs3_and_configs4_on_hg19():
         st = line["strong_scaling"]
         assert line["n_gpus"] == ranks and st["ranks"] == ranks and st["pairs_total"] == 8_000_000
         assert st["merged_equals_single_rank"] is True
-        assert st["merge_bytes_per_pair"] == 4
+        assert st["merge_bytes_per_pair"] == 2 and st["merge_4B_words"]["merged_equals_single_rank"] is True
         c4 = line["configs4_200M_150bp"]
         assert c4["ranks"] == ranks and c4["pairs_total"] == 8_000_000
     assert one["configs4_200M_150bp"]["results_checksum"] == two["configs4_200M_150bp"]["results_checksum"]

@@ -1,10 +1,11 @@
-"""The 4-byte transfer form of the results (include/fc2_bp.h "compact results").
+"""The 4- and 2-byte transfer forms of the results (include/fc2_bp.h "compact results").
 
-CPU: fc2_result_expand against a numpy restatement of the packing rule, on words of every shape
+CPU: fc2_result_expand against a numpy restatement of the packing rules, on words of every shape
 the scan writes (no hit, '+' GTAG and '-' CTAC hits, error bits, ties) plus words that must escape
-(x > 254, n_ties > 255, dist / ov > 15, a no-hit word with a strand bit), and its refusal of
-escape lists that do not match the escaped words.  GPU (tests/test_gpu_fullsize.py): the device
-packer on all 50M results of the bench batch, expanded back bit for bit.
+(4 B: x > 254, n_ties > 255, dist / ov > 15, a no-hit word with a strand bit; 2 B also x > 125,
+n_ties > 16, dist / ov > 3, any error bit), and its refusal of escape lists that do not match the
+escaped words.  GPU (tests/test_gpu_fullsize.py): the device packer on all 50M results of the bench
+batch, both widths, expanded back bit for bit.
 """
 import numpy as np
 import pytest
@@ -47,6 +48,33 @@ def pack_restated(w):
     return c, e
 
 
+def pack16_restated(w):
+    """numpy restatement of fc2::r16_pack / r16_unpack + the escape rule (width 2)."""
+    w = w.astype(np.uint64)
+    x = (w & 0xFFFF).astype(np.uint16).view(np.int16).astype(np.int64)
+    dist, ov = (w >> 16) & 0xFF, (w >> 24) & 0xFF
+    nt, info = (w >> 32) & 0xFFFF, (w >> 48) & 0xFFFF
+    minus = (info & 1)
+    c = np.where(x < 0, 0, ((x + 1) & 0x7F).astype(np.uint64) | (minus << 7) | ((dist & 3) << 8) | ((ov & 3) << 10) |
+                 (((nt - 1) & 15) << 12)).astype(np.uint64)
+    x1 = c & 0x7F
+    m = (c >> 7) & 1
+    hit = ((x1 - 1) & 0xFFFF) | (((c >> 8) & 3) << 16) | (((c >> 10) & 3) << 24) | ((((c >> 12) & 15) + 1) << 32) | \
+        ((np.uint64(0x8000) | m | (np.where(m == 1, CTAC, GTAG).astype(np.uint64) << 1)) << 48)
+    back = np.where(x1 == 0, np.uint64(0xFFFF) | (np.uint64(0x8000) << 48), hit)
+    esc = (back != w) | (x1 == 0x7F)
+    c = np.where(esc, np.uint64(N.R16_ESCAPE), c).astype(np.uint16)
+    idx = np.nonzero(esc)[0]
+    e = np.zeros(len(idx), N.ESCAPE_DTYPE)
+    e["index"] = idx
+    e["result"] = w[idx].astype(np.int64).view(N.RESULT_DTYPE)
+    return c, e
+
+
+def pack(w, width):
+    return pack16_restated(w) if width == 2 else pack_restated(w)
+
+
 def sample_words(n, seed):
     rng = np.random.default_rng(seed)
     kind = rng.integers(0, 10, n)
@@ -75,11 +103,12 @@ def sample_words(n, seed):
     return w
 
 
+@pytest.mark.parametrize("width", [4, 2])
 @pytest.mark.parametrize("n,seed", [(0, 1), (1, 2), (1000, 3), (300_001, 4)])
-def test_expand_restores_every_word(n, seed):
+def test_expand_restores_every_word(n, seed, width):
     w = sample_words(n, seed)
-    c, e = pack_restated(w)
-    assert n < 1000 or 0 < len(e) < n // 5
+    c, e = pack(w, width)
+    assert n < 1000 or 0 < len(e) < (n // 5 if width == 4 else n)
     rng = np.random.default_rng(seed)
     e = e[rng.permutation(len(e))]                     # escapes arrive in no particular order
     for threads in (1, 0):
@@ -87,9 +116,10 @@ def test_expand_restores_every_word(n, seed):
         assert np.array_equal(out, w)
 
 
-def test_expand_refuses_mismatched_escapes():
+@pytest.mark.parametrize("width", [4, 2])
+def test_expand_refuses_mismatched_escapes(width):
     w = sample_words(5000, 9)
-    c, e = pack_restated(w)
+    c, e = pack(w, width)
     assert len(e) > 2
     with pytest.raises(Exception, match="escape"):
         expand(Options(), c, e[:-1])                    # an escaped word without its escape
@@ -98,8 +128,24 @@ def test_expand_refuses_mismatched_escapes():
     with pytest.raises(Exception, match="escape"):
         expand(Options(), c, dup)                       # one word escaped twice, another not at all
     bad = e.copy()
-    bad["index"][0] = np.nonzero((c & N.R32_ESCAPE) == 0)[0][0]
+    flagged = (c & 0x7F) == N.R16_ESCAPE if width == 2 else (c & N.R32_ESCAPE) != 0
+    bad["index"][0] = np.nonzero(~flagged)[0][0]
     with pytest.raises(Exception, match="escape"):
         expand(Options(), c, bad)                       # an escape for a word that was not escaped
     with pytest.raises(Exception, match="canonical"):
         expand(Options(noncanonical=True), c, e)
+
+
+def test_two_byte_form_holds_the_default_options_words():
+    """Default options (margin 2, maxdist 2) at l <= 124: every canonical hit with n_ties <= 16 and
+    every error-free miss fits 2 bytes; only error bits and ties beyond 16 escape."""
+    rng = np.random.default_rng(5)
+    n = 20000
+    x = rng.integers(0, 125, n)
+    minus = rng.integers(0, 2, n)
+    info = 0x8000 | minus | (np.where(minus == 1, CTAC, GTAG) << 1)
+    w = words8(x, rng.integers(0, 3, n), rng.integers(0, 3, n), rng.integers(1, 17, n), info)
+    w[:5000] = words8(np.full(5000, -1), np.zeros(5000), np.zeros(5000), np.zeros(5000), np.full(5000, 0x8000))
+    c, e = pack16_restated(w)
+    assert len(e) == 0
+    assert np.array_equal(expand(Options(), c, e), w)

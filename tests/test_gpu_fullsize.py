@@ -53,17 +53,18 @@ def _check(args):
     assert np.array_equal((res[~ok] >> np.uint64(48)) & np.uint64(0x6000), err[~ok])
     hits = int(((res & np.uint64(0xFFFF)) != np.uint64(0xFFFF)).sum())
     assert hits > b.n // 3
-    # the 4-byte transfer form (fc2_result_compact_launch -> fc2_result_expand) of every result word
+    # the compact transfer forms (fc2_result_compact_launch -> fc2_result_expand) of every result word
     from find_circ2_amd import compact, expand
     dres = torch.from_numpy(res.view(np.int64)).to(dev)
-    c = compact(opt, dres, b.n)
-    torch.cuda.synchronize(dev)
-    n_esc = int(c.count.item())
-    assert n_esc <= c.cap
-    esc = c.esc.cpu().numpy().view(N.ESCAPE_DTYPE)[:n_esc]
-    back = expand(opt, c.words[:b.n].cpu().numpy(), esc)
-    assert np.array_equal(back.view(np.uint64), res)
-    print("compact form: %d escapes of %d" % (n_esc, b.n))
+    for width in (4, 2):
+        c = compact(opt, dres, b.n, width=width)
+        torch.cuda.synchronize(dev)
+        n_esc = int(c.count.item())
+        assert n_esc <= c.cap
+        esc = c.esc.cpu().numpy().view(N.ESCAPE_DTYPE)[:n_esc]
+        back = expand(opt, c.words[:b.n].cpu().numpy(), esc)
+        assert np.array_equal(back.view(np.uint64), res)
+        print("compact form, %d B: %d escapes of %d" % (width, n_esc, b.n))
     return b.n, hits
 
 

@@ -543,15 +543,16 @@ def test_native_caller_float_last_as_only_matters_in_hit_add(tmp_path):
     assert "--python-caller" in open(os.path.join(o3, "run.log")).read()
 
 
+@pytest.mark.parametrize("width", [4, 2])
 @pytest.mark.parametrize("extra", [[], ["--all-hits"], ["--strand-pref", "-d", "0"], ["--chunk-size", "7"]])
-def test_native_caller_compact_results_equal_raw(tmp_path, extra):
-    """fc2_caller_submit32 (results in their 4-byte transfer form, expanded per chunk) records exactly
+def test_native_caller_compact_results_equal_raw(tmp_path, extra, width):
+    """fc2_caller_submit_compact (results in a compact transfer form, expanded per chunk) records exactly
     what fc2_caller_submit records from the 8-byte words."""
     from oracle_engine import compact_factory
     sam = str(tmp_path / "rich.sam")
     fa = _rich_sam(sam, 500, seed=3141)
     o1, o2 = str(tmp_path / "raw"), str(tmp_path / "compact")
     assert cli.main(["-G", fa, "-o", o1, "-q"] + extra + [sam], evaluator_factory=oracle_evaluator_factory) == 0
-    assert cli.main(["-G", fa, "-o", o2, "-q"] + extra + [sam], evaluator_factory=compact_factory()) == 0
+    assert cli.main(["-G", fa, "-o", o2, "-q"] + extra + [sam], evaluator_factory=compact_factory(width)) == 0
     same(o1, o2)
     assert sum(1 for l in open(os.path.join(o2, "circ_splice_sites.bed")) if l[0] != "#") > 10

@@ -130,28 +130,28 @@ def test_round_robin_batch_balance():
         assert max(counts) - min(counts) <= b
 
 
-def _compact_worker(rank, world, port, n, batch, q):
+def _compact_worker(rank, world, port, n, batch, q, width):
     import sys
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-    from test_compact_results import pack_restated, sample_words
+    from test_compact_results import pack, sample_words
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     words8 = sample_words(n, 77)                 # the stream's 8-byte results (every rank can derive them)
     bounds = shard.batch_bounds(n, batch)
     cap = max(1, batch)
-    merged = shard.SharedCompactResults(n, bounds, cap, create=True) if rank == 0 else None
+    merged = shard.SharedCompactResults(n, bounds, cap, create=True, width=width) if rank == 0 else None
     name = shard.broadcast_name(merged.name if rank == 0 else None)
     if rank != 0:
-        merged = shard.SharedCompactResults(n, bounds, cap, name=name)
+        merged = shard.SharedCompactResults(n, bounds, cap, name=name, width=width)
     dist.barrier()
     if rank == 0:
-        merged.words[:] = 0x5A5A5A5A
+        merged.words[:] = 0x5A5A
         merged.esc_count[:] = -1
     dist.barrier()
     for k, s, e in shard.my_batches(n, batch, rank, world):
-        c, esc = pack_restated(words8[s:e])     # what fc2_result_compact_launch writes for the batch
+        c, esc = pack(words8[s:e], width)       # what fc2_result_compact_launch writes for the batch
         merged.words[s:e] = c
         merged.esc[k, :len(esc)] = esc          # batch-relative indices, as the device writes them
         merged.esc_count[k] = len(esc)
@@ -165,16 +165,17 @@ def _compact_worker(rank, world, port, n, batch, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("width", [4, 2])
 @pytest.mark.parametrize("n", [5000, 700, 0])
-def test_gloo_two_ranks_compact_merge(n):
-    """bench.py's configs[3] merge in the 4-byte transfer form (shard.SharedCompactResults): words at
-    input offsets, escapes per batch; rank 0's expansion equals the stream's 8-byte results."""
+def test_gloo_two_ranks_compact_merge(n, width):
+    """bench.py's configs[3] merge in a compact transfer form (shard.SharedCompactResults, 4 and 2 bytes):
+    words at input offsets, escapes per batch; rank 0's expansion equals the stream's 8-byte results."""
     world = 2
     batch = shard.round_robin_batch(n, world, per_rank=3, align=64)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_compact_worker, args=(r, world, port, n, batch, q)) for r in range(world)]
+    procs = [ctx.Process(target=_compact_worker, args=(r, world, port, n, batch, q, width)) for r in range(world)]
     for p in procs:
         p.start()
     merged, words8, csum = q.get(timeout=120)
