@@ -18,6 +18,9 @@ KERN = "bp_scan"          # bp_scan32_kernel / bp_scan32_stage_bt_kernel / bp_sc
 N_PAIRS = 50_000_000
 
 
+PMC_KERNEL = {}      # pass name -> the scan kernel the PMC pass counted (its full name)
+
+
 def agg(prof, name):
     p = os.path.join(prof, name, "pmc_counter_collection.csv")
     if not os.path.exists(p):
@@ -26,10 +29,23 @@ def agg(prof, name):
     for r in csv.DictReader(open(p)):
         if KERN in r["Kernel_Name"]:
             a[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            PMC_KERNEL[name] = r["Kernel_Name"]
     return {k: sum(v) / len(v) for k, v in a.items()}
 
 
-def kstats(prof, name):
+def kstats(prof, name, kernel=None):
+    # the kernel trace, when present: only the dispatches of `kernel` (the one the PMC passes counted)
+    # over the whole N_PAIRS batch (the bench's other legs launch it over sub-batches, which the stats
+    # file averages in)
+    t = os.path.join(prof, name, "kt_kernel_trace.csv")
+    if os.path.exists(t):
+        ns, kname = [], None
+        for r in csv.DictReader(open(t)):
+            if (r["Kernel_Name"] == kernel if kernel else KERN in r["Kernel_Name"]) and int(r["Grid_Size_X"]) >= N_PAIRS:
+                ns.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+                kname = r["Kernel_Name"].split("(fc2_params")[0].replace("void (anonymous namespace)::", "")
+        if ns:
+            return sum(ns) / len(ns), len(ns), kname
     p = os.path.join(prof, name, "kt_kernel_stats.csv")
     if not os.path.exists(p):
         return None, 0, None
@@ -47,7 +63,7 @@ def main():
     for w, key in (("hg19", "hg19"), ("hg19o", "hg19_locus_ordered"), ("cdr1as", "cdr1as_50M_calibration")):
         f, wr, h = agg(prof, "fetch_" + w), agg(prof, "write_" + w), agg(prof, "hit_" + w)
         rq = agg(prof, "req_" + w)
-        ns, calls, kname = kstats(prof, "kt_" + w)
+        ns, calls, kname = kstats(prof, "kt_" + w, PMC_KERNEL.get("fetch_" + w))
         if not f:
             continue
         hbm = 2 * f["FETCH_SIZE"] * 1024 + wr.get("WRITE_SIZE", 0) * 1024
@@ -70,8 +86,9 @@ def main():
         v["commit"] = commit        # the tree the passes ran on (stamped when the JSON is built, locally)
     out["correction"] = ("reads = 2 x FETCH_SIZE x 1024 (gfx950 128-B fills tallied at 64 B), writes = WRITE_SIZE x "
                          "1024 (exact: 8 B x pairs)")
-    out["source"] = ("rocprofv3 --kernel-trace --stats and separate --pmc passes (scripts/profile_round.sh): bench.py "
-                     "--steps 10 --warmup 2; averages over the scan-kernel dispatches")
+    out["source"] = ("rocprofv3 --kernel-trace --stats (r03: of the default bench run itself, averaged over the "
+                     "dispatches on the whole 50M-pair batch) and separate --pmc passes of bench.py --steps 10 --warmup 2 "
+                     "(scripts/profile_round.sh, scripts/profile_r03.sh); PMC averages over the scan-kernel dispatches")
     path = os.path.join(ROOT, "profiles", "traffic_%s.json" % rnd)
     json.dump(out, open(path, "w"), indent=1)
     dst = os.path.join(ROOT, "profiles", rnd)
