@@ -184,17 +184,21 @@ def build_workload(args, rank, dev):
     return opt, g, b
 
 
-def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
+def device_pipeline(opt, g, b, reps: int, chunks: int = 8, width: int = 2):
     """BASELINE.md's 'device pipeline' number: pinned host SoA -> H2D -> scan -> D2H.
 
     The batch is split into `chunks` slices, each laid out contiguously in pinned
     host memory in the device SoA layout with its N rows in the sparse form PairBatch.pack
     uploads (hotpath.sparse_nrows; untimed setup), and streamed on two HIP
     streams so that one slice's copies overlap another's kernel (PCIe is full
-    duplex).  Returns pairs/s and ms per batch (median of `reps`).
+    duplex).  The results come back in the 2-byte compact form (`width` 2: packed on the device by
+    fc2_result_compact_launch, the slice's escape count and slots copied beside the words) or as
+    the raw 8-byte words (`width` 8).  Returns pairs/s and ms per batch (median of `reps`); the
+    check expands the compact words on the host (fc2_result_expand) and compares every result with
+    the device-resident scan.
     """
     import torch
-    from find_circ2_amd import PairBatch, scan
+    from find_circ2_amd import CompactResults, PairBatch, compact, expand, scan
     from find_circ2_amd import _native as N
     from find_circ2_amd.hotpath import ScanOutput, scatter_nrows, widen_tail
     dev = b.device
@@ -223,7 +227,13 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
         hb = torch.cat([t.cpu() for t in head + rest]).pin_memory()
         host.append((lo, m, int(idx.numel()), (1 + b.rw) * m, hb))
     kmax = max(h[2] for h in host)
-    host_out = torch.empty(n, dtype=torch.int64).pin_memory()
+    if width not in (2, 8):
+        raise ValueError("width is 2 or 8")
+    cap = max(1024, step // 1024)
+    host_out = torch.empty(n, dtype=torch.int64 if width == 8 else torch.int16).pin_memory()
+    host_esc = torch.empty((chunks, 16 * cap), dtype=torch.uint8).pin_memory()
+    host_cnt = torch.empty(chunks, dtype=torch.int32).pin_memory()
+    dcomp = [CompactResults(step, dev, cap, width=2) for _ in range(2)] if width == 2 else None
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     tail_words = (step + 1) // 2 if narrow else step
     dbuf = [torch.empty((2 + b.rw) * step + tail_words + (1 + b.nw) * kmax, dtype=torch.int64, device=dev)
@@ -258,7 +268,13 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
                 d[nh + m:nh + m + hbuf.numel() - nh].copy_(hbuf[nh:], non_blocking=True)   # tail32 + N
                 sb = slice_batch(d, nbuf[c & 1], m, k)
                 scan(opt, g, sb, out=ScanOutput(dres[c & 1], None, sb.tw, m), stream=st.cuda_stream)
-                host_out[lo:lo + m].copy_(dres[c & 1][:m], non_blocking=True)
+                if width == 8:
+                    host_out[lo:lo + m].copy_(dres[c & 1][:m], non_blocking=True)
+                else:
+                    cr = compact(opt, dres[c & 1], m, into=dcomp[c & 1], stream=st.cuda_stream, width=2)
+                    host_out[lo:lo + m].copy_(cr.words[:m], non_blocking=True)
+                    host_esc[c].copy_(cr.esc.view(torch.uint8), non_blocking=True)
+                    host_cnt[c:c + 1].copy_(cr.count, non_blocking=True)
         torch.cuda.synchronize(dev)
 
     run_once()
@@ -268,18 +284,34 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8):
         run_once()
         ts.append(time.perf_counter() - t0)
     ms = float(np.median(ts)) * 1e3
-    ok = bool(torch.equal(host_out, b._bench_ref_results)) if hasattr(b, "_bench_ref_results") else None
+    ok = None
+    if hasattr(b, "_bench_ref_results"):
+        if width == 8:
+            ok = bool(torch.equal(host_out, b._bench_ref_results))
+        else:
+            words = host_out.numpy().view(np.uint16)
+            esc = host_esc.numpy().view(N.ESCAPE_DTYPE)
+            got = np.empty(n, np.int64)
+            for c, (lo, m, _, _, _) in enumerate(host):
+                k = int(host_cnt[c])
+                if not 0 <= k <= cap:
+                    raise RuntimeError("device pipeline slice %d: %d escapes, %d slots" % (c, k, cap))
+                expand(opt, words[lo:lo + m], esc[c, :k], out=got[lo:lo + m])
+            ok = bool(np.array_equal(got, b._bench_ref_results.numpy()))
     kn = sum(h[2] for h in host)
     h2d = sum(h[4].numel() * 8 for h in host)
+    d2h = width * n + (0 if width == 8 else len(host) * (16 * cap + 4))
     return {"value": round(n / (ms * 1e-3), 1), "unit": "anchor-pairs/s", "ms_per_batch": round(ms, 3),
-            "pcie_GBs": round((h2d + 8 * n) / (ms * 1e-3) / 1e9, 1),
-            "h2d_bytes_per_pair": round(h2d / n, 2),
+            "pcie_GBs": round((h2d + d2h) / (ms * 1e-3) / 1e9, 1),
+            "h2d_bytes_per_pair": round(h2d / n, 2), "d2h_bytes_per_pair": round(d2h / n, 2),
             "results_equal_device_resident_scan": ok,
             "note": "pinned host SoA (16 B record + %d B read rows%s; the N rows of the %.2f %% "
                     "of pairs flagged READ_N as index + %d B rows, scattered on the device) -> H2D -> bp_scan -> "
-                    "D2H 8 B result, %d slices on 2 HIP streams; %d pairs"
+                    "D2H %s, %d slices on 2 HIP streams; %d pairs"
                     % (8 * b.rw - (4 if narrow else 0), ", the last one as uint32" if narrow else "",
-                       100.0 * kn / max(n, 1), 8 * b.nw, len(host), n)}
+                       100.0 * kn / max(n, 1), 8 * b.nw,
+                       "8 B result" if width == 8 else "2 B compact result (+ escape slots, expanded on the host "
+                       "for the check)", len(host), n)}
 
 
 def host_read_arrays(opt, b, chunk: int = 4_000_000):
@@ -1082,6 +1114,8 @@ def main():
                                       "cpu_model": cb["cpu_model"]}
     if rank == 0 and ws == 1 and not args.no_extra and args.workload == "hg19":
         line["extra"] = {"device_pipeline_pcie": device_pipeline(opt, g, b, reps=5)}
+        line["extra"]["device_pipeline_pcie"]["d2h_8B_words"] = {
+            k: v for k, v in device_pipeline(opt, g, b, reps=5, width=8).items() if k != "note"}
         line["extra"]["host_pipeline_from_pair_arrays"] = host_pipeline(opt, g, b)
         line["extra"]["configs[2]_window_carrying_batch"] = window_carrying(opt, g, b, args.steps, dev, bpp)
         # the honest price of locus order for a read-order stream: the device reorder (fc2_reorder_launch,
