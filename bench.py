@@ -56,6 +56,9 @@ def parse():
     ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
     ap.add_argument("--no-strong", action="store_true", help="skip the configs[3] strong-scaling / ordered-merge run")
     ap.add_argument("--no-config4", action="store_true", help="skip the configs[4] 200M x 120-150 bp run")
+    ap.add_argument("--strong-batches", type=int, default=0,
+                    help="configs[3]: batches per rank the stream is cut into (shard.round_robin_batch); 0: "
+                         "max(2, 8 // ranks)")
     ap.add_argument("--config4-pairs", type=int, default=0, help="configs[4] stream length (default 200M; tests)")
     ap.add_argument("--no-cli", action="store_true", help="skip the end-to-end CLI extra (2M reads, BAM on stdin)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
@@ -506,7 +509,7 @@ def timed_scans(opt, g, b, steps, warmup, ws, dev):
     return t1 - t0, float(np.mean(kms)), out
 
 
-def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw):
+def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, per_rank=4):
     """configs[3]: ONE pair stream (the `n` pairs rank 0 scans in the weak run, seed 1337) cut into
     contiguous batches dealt round-robin to the ranks (shard.my_batches).  Rank 0 scans views of its
     own weak batch; every other rank generates only its batches of the stream (stream_share).  Each
@@ -524,7 +527,7 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw):
     from find_circ2_amd.hotpath import ScanOutput
     from find_circ2_amd.shard import (SharedCompactResults, SharedResults, batch_bounds, broadcast_name, my_batches,
                                       round_robin_batch)
-    bsz = round_robin_batch(n, ws)
+    bsz = round_robin_batch(n, ws, per_rank=per_rank)
     bounds = batch_bounds(n, bsz)
     mine = my_batches(n, bsz, rank, ws)
     cap = max(1024, bsz // 256)
@@ -1072,7 +1075,7 @@ def main():
     if not args.no_strong:
         n0, kw0 = workload_cfg(args, 0)
         strong = strong_scaling(opt, g, b if rank == 0 else None, b._bench_ref_results.numpy() if rank == 0 else None,
-                                ws, rank, dev, args.steps, args.warmup, n0, kw0)
+                                ws, rank, dev, args.steps, args.warmup, n0, kw0, per_rank=args.strong_batches or max(2, 8 // ws))
         torch.cuda.empty_cache()
     line = {
         "metric": METRIC,
