@@ -89,6 +89,7 @@ BATCH_FORM_PLAIN = 0x04
 BATCH_FORM_UNITS = 0x08
 BATCH_FORM_TWOLANE = 0x10
 BATCH_FORM_TRI = 0x20
+BATCH_FORM_FIVE = 0x40
 
 
 class ReorderInfo(ctypes.Structure):

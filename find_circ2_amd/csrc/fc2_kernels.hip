@@ -797,12 +797,23 @@ int g_twin = 2;        // units_twin: 0 never, 1 always, 2 for batches not flagg
 int g_words = 1;       // read-order STAGE scan uses the word-pair layout when the view carries one
 int g_persist = 0;      // persistent STAGE kernel: 0 off, -1 occupancy-sized grid, k > 0 k blocks per CU
 int g_stage_block = 512; // threads per block of the LDS-staging word-pair scan (FC2_TUNE_STAGE_BLOCK)
-int g_tri = 2;           // three-lane window loads: 0 never, 1 always, 2 when windows exceed 97 bases (FC2_TUNE_TRI)
+int g_tri = 3;           // long-window loads (FC2_TUNE_TRI): 0 two-lane always, 1 three-lane always, 2 three-lane when
+                         // windows exceed 97 bases, 3 five-lane 8-B loads when windows exceed 97 bases
 #else
 constexpr int g_stream_nt = 1, g_kernel32 = 1, g_xcd_swizzle = 2, g_extra_lds = 0, g_stage = 2, g_twin = 2,
-              g_words = 1, g_persist = 0, g_stage_block = 512, g_tri = 2;
+              g_words = 1, g_persist = 0, g_stage_block = 512, g_tri = 3;
 #endif
 inline bool stream_nt() { return g_stream_nt != 0; }
+// The staged word-pair scan's window-load form: 0 two-lane, 1 three-lane 16-B, 2 five-lane 8-B (the
+// default for 5-pair windows, longer than 97 bases); the per-call hints force any of them.
+inline int long_window_form(uint32_t layout, int ml) {
+    if (layout & FC2_BATCH_FORM_FIVE) return 2;
+    if (layout & FC2_BATCH_FORM_TRI) return 1;
+    if (layout & FC2_BATCH_FORM_TWOLANE) return 0;
+    if (g_tri == 1) return 1;
+    if ((g_tri == 2 || g_tri == 3) && ml + 2 > 97) return g_tri == 3 ? 2 : 1;
+    return 0;
+}
 
 }  // namespace
 
@@ -857,9 +868,7 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         const bool stage = (b->layout & FC2_BATCH_FORM_STAGED) ? true
                          : (b->layout & FC2_BATCH_FORM_PLAIN) ? false
                          : g_stage == 2 ? (big && !ordered) : g_stage != 0;
-        const bool tri = (b->layout & FC2_BATCH_FORM_TRI) ? true
-                       : (b->layout & FC2_BATCH_FORM_TWOLANE) ? false
-                       : g_tri == 1 || (g_tri == 2 && ml + 2 > 97);   // 5-pair windows: three-lane loads
+        const int tri = long_window_form(b->layout, ml);
         const int opts = sw ? fc2::kOptSwizzle : 0;
         const int nq = (ml + 2 + 31) / 32;
         if (stage && (g_stage_block != 256 || tri) && g_persist == 0 && fc2::stage_bt_ok(nq, gv)) {
@@ -913,10 +922,7 @@ extern "C" int fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_vi
         return fc2::fail(FC2_E_PARAM, "fc2_probe_pattern_launch: needs a genome with a word-pair table and a batch");
     if (b->n == 0) return FC2_OK;
     const int ml = b->max_l < 0 ? 0 : b->max_l;
-    const bool tri = (b->layout & FC2_BATCH_FORM_TRI) ? true                // the scan's window form
-                   : (b->layout & FC2_BATCH_FORM_TWOLANE) ? false           // (fc2_bp_scan_launch)
-                   : g_tri == 1 || (g_tri == 2 && ml + 2 > 97);
-    if (fc2::launch_probe_pattern((hipStream_t)stream, *p, *g, *b, out, tri))
+    if (fc2::launch_probe_pattern((hipStream_t)stream, *p, *g, *b, out, long_window_form(b->layout, ml)))
         return fc2::fail(FC2_E_HIP, "probe_pattern_kernel launch failed");
     return FC2_OK;
 }
@@ -1088,7 +1094,7 @@ extern "C" int fc2_set_tuning(int key, int value) {
             g_twin = value; return FC2_OK;
         case FC2_TUNE_WORDS: g_words = value ? 1 : 0; return FC2_OK;
         case FC2_TUNE_TRI:
-            if (value < 0 || value > 2) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: tri is 0, 1 or 2");
+            if (value < 0 || value > 3) return fc2::fail(FC2_E_PARAM, "fc2_set_tuning: tri is 0, 1, 2 or 3");
             g_tri = value; return FC2_OK;
         case FC2_TUNE_STAGE_BLOCK:
             if (value != 256 && value != 512 && value != 1024)

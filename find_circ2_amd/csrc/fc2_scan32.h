@@ -24,8 +24,9 @@ void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc
 #endif
 // STAGE + cooperative word-pair form with bt-thread blocks (256/512/1024); usable when stage_bt_ok().
 bool stage_bt_ok(int nq, const fc2_genome_view &g);
-// tri: three-lane window loads (batches with windows longer than 97 bases)
-void launch_scan32_stage_bt(int bt, bool tri, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+// tri: 0 = two-lane window loads, 1 = three-lane 16-B loads, 2 = five-lane 8-B loads (the default for
+// batches with windows longer than 97 bases)
+void launch_scan32_stage_bt(int bt, int tri, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                             const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw);
 // Window-carrying batches (b.win_words): PW = plane words, 1..4.
 void launch_scan32_win(int pw, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
@@ -34,5 +35,5 @@ void launch_gather_windows(hipStream_t s, const fc2_params &p, const fc2_genome_
                            fc2_pair *pairs, uint64_t *win_words, uint64_t *win_nwords, uint32_t pw);
 // Measurement kernel: the read-order scan's memory pattern without its arithmetic (needs g.wt).
 int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b,
-                         uint64_t *out, bool tri);
+                         uint64_t *out, int tri);   // tri: the scan's window form, as above
 }  // namespace fc2

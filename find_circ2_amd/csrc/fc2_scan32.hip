@@ -664,6 +664,110 @@ __device__ __forceinline__ void windows_exchange_w3(u32x4 *xchg, const u32x4 (&c
     if (wB >= 84) take_w3(xchg, wB / 21 - 4, wB, rB);
 }
 
+// Five-lane form of the long-window loads (the default for windows longer than 97 bases since round
+// 3; FC2_TUNE_TRI = 3): each window's 40 B (its five word pairs from the run start, the copy chosen as
+// for the three-lane form) by five consecutive lanes of ONE 8-B load instruction: 12 windows per
+// instruction (lanes 60-63 idle), 11 instructions for the wave's 128 windows, still one L2 request
+// per window, but 22 VGPRs of loads in flight where the three-lane form holds 28: 74 instead of 84
+// VGPRs, 6 instead of 4 waves per SIMD, 3 % faster at 150 bp (profiles/r03/ab_tri5.jsonl).
+__device__ __forceinline__ void windows_issue_w5(const fc2_genome_view &g, __amdgpu_buffer_rsrc_t rs,
+                                                 __amdgpu_buffer_rsrc_t rn, const uint32_t *s_nsuper,
+                                                 uint64_t cstart, int64_t wsA, int64_t wsB, int W, bool active,
+                                                 WinW &rA, WinW &rB, u32x2 (&cl)[11]) {
+    window_geom_w(g, cstart, wsA, W, rA, true);
+    window_geom_w(g, cstart, wsB, W, rB, true);
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t wsx[2] = {wsA, wsB};
+    WinW *R[2] = {&rA, &rB};
+    const uint32_t sA = rA.off, sB = rB.off;                // region = [off, off + 40), inside one line
+    uint32_t src[11];
+    bool ok[11];
+    const uint32_t part = 8u * (uint32_t)(lane % 5);
+#pragma unroll
+    for (int c = 0; c < 11; ++c) {
+        const int w = 12 * c + lane / 5;                  // window served by this lane in instruction c
+        ok[c] = lane < 60 && w < 128;
+        const int owner = w & 63;
+        // instructions 0-4 serve only A windows (w <= 59), 6-10 only B windows (w >= 72)
+        if (12 * c + 11 < 64) {
+            src[c] = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sA);
+        } else if (12 * c >= 64) {
+            src[c] = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sB);
+        } else {
+            const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sA);
+            const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute(owner << 2, (int)sB);
+            src[c] = (w >> 6) ? b : a;
+        }
+    }
+    uint32_t sw[2][2] = {{0u, 0u}, {0u, 0u}}, sb[2][2] = {{0u, 0u}, {0u, 0u}};
+    bool sv[2] = {false, false};
+    if (s_nsuper) {
+        const int64_t top = (int64_t)(g.n_units * 64) - 1;
+#pragma unroll
+        for (int x = 0; x < 2; ++x) {
+            int64_t lo = (int64_t)cstart + wsx[x], hi = lo + W - 1;
+            lo = lo < 0 ? 0 : lo;
+            hi = hi > top ? top : hi;
+            sv[x] = active && lo <= hi;
+            const uint32_t k0 = sv[x] ? (uint32_t)((uint64_t)lo >> g.nsuper_shift) : 0u,
+                           k1 = sv[x] ? (uint32_t)((uint64_t)hi >> g.nsuper_shift) : 0u;
+            sw[x][0] = s_nsuper[k0 >> 5];
+            sw[x][1] = s_nsuper[k1 >> 5];
+            sb[x][0] = k0 & 31u;
+            sb[x][1] = k1 & 31u;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 11; ++c) {
+        cl[c] = u32x2{0u, 0u};
+        if (ok[c]) cl[c] = __builtin_amdgcn_raw_buffer_load_b64(rs, src[c] + part, 0, 0);
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        WinW &Q = *R[x];
+        Q.v4 = u32x2{0u, 0u};
+        const bool nflag = sv[x] && (((sw[x][0] >> sb[x][0]) | (sw[x][1] >> sb[x][1])) & 1u);
+        Q.n03 = u32x4{0u, 0u, 0u, 0u};
+        Q.n4 = 0u;
+        if (nflag) {
+            uint32_t nw[5];
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const int32_t wj = (int32_t)Q.q0 + j;
+                nw[j] = 0u;
+                if (wj >= 0 && j < Q.nwd) nw[j] = __builtin_amdgcn_raw_buffer_load_b32(rn, (uint32_t)wj * 4u, 0, 0);
+            }
+            Q.n03 = u32x4{nw[0], nw[1], nw[2], nw[3]};
+            Q.n4 = nw[4];
+        }
+    }
+}
+
+// Owner side of the five-lane form: the wave's 4 KB of LDS slots hold eight instructions' 8-B pieces
+// (64 each); instructions 0-7 carry every A window and B windows 64..95, then 8-10 overwrite slots
+// 0-2 with B windows 96..127.
+__device__ __forceinline__ void take_w5(const u32x2 *xchg, int slot, int w, WinW &Q) {
+    const int base = slot * 64 + 5 * (w % 12);
+    const u32x2 p0 = xchg[base], p1 = xchg[base + 1], p2 = xchg[base + 2], p3 = xchg[base + 3], p4 = xchg[base + 4];
+    Q.v0 = u32x4{p0.x, p0.y, p1.x, p1.y};
+    Q.v1 = u32x4{p2.x, p2.y, p3.x, p3.y};
+    Q.v4 = p4;
+}
+__device__ __forceinline__ void windows_exchange_w5(u32x2 *xchg, const u32x2 (&cl)[11], WinW &rA, WinW &rB) {
+    const int lane = (int)(threadIdx.x & 63);
+    const int wB = 64 + lane;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) xchg[c * 64 + lane] = cl[c];
+    wave_sync_lds();
+    take_w5(xchg, lane / 12, lane, rA);
+    if (wB < 96) take_w5(xchg, wB / 12, wB, rB);
+    wave_sync_lds();                           // every phase-1 read done before slots 0-2 are reused
+#pragma unroll
+    for (int c = 8; c < 11; ++c) xchg[(c - 8) * 64 + lane] = cl[c];
+    wave_sync_lds();
+    if (wB >= 96) take_w5(xchg, wB / 12 - 8, wB, rB);
+}
+
 template <int NQ>
 __device__ __forceinline__ void window_finish_w(const WinW &R, int64_t csize, int64_t ws, int W, P32<NQ> &P) {
     static_assert(NQ == 4, "word-pair windows cover W <= 128");
@@ -755,7 +859,7 @@ __device__ __forceinline__ uint64_t xcd_block(uint32_t b, uint32_t nwg) {
 // exchange, so exits are deferred through `active`.  xchg: this wave's 4 x 64 LDS slots.
 // PW > 0: window-carrying batch (fc2_batch_view.win_words, pw = PW): the windows arrive with the
 // record in round trip 1 and nothing is gathered from the genome (NQ == 4, !COOP, !WL).
-template <int NQ, bool NT, bool COOP, bool WL = false, int PW = 0, bool TRI = false>
+template <int NQ, bool NT, bool COOP, bool WL = false, int PW = 0, int TRI = 0>
 __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &bv,
                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask, uint32_t tw,
                                           uint64_t i, const uint64_t *s_cstart, const int64_t *s_csize, bool lds_tab,
@@ -828,7 +932,8 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     ulonglong2 cl[2][2];
     WinW wA, wB;
     u32x4 wcl[2][2];
-    u32x4 wcl3[TRI ? 7 : 1];
+    u32x4 wcl3[TRI == 1 ? 7 : 1];
+    u32x2 wcl5[TRI == 2 ? 11 : 1];
     uint64_t cwA = 0, cwB = 0;
     __amdgpu_buffer_rsrc_t rs, rn;
     if constexpr (WL) {
@@ -837,11 +942,16 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         rn = __builtin_amdgcn_make_buffer_rsrc((void *)g.nplane, 0,
                                                (int)(uint32_t)(nb > 0xFFFFFFFFull ? 0xFFFFFFFFull : nb), 0x00020000);
     }
-    if constexpr (COOP && WL && TRI) {
+    if constexpr (COOP && WL && TRI == 1) {
         static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
         if (!active) W = 2;
         windows_issue_w3(g, rs, rn, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active, wA,
                          wB, wcl3);
+    } else if constexpr (COOP && WL && TRI == 2) {
+        static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
+        if (!active) W = 2;
+        windows_issue_w5(g, rs, rn, s_nsuper, active ? cstart : 0, active ? wsA : 0, active ? wsB : 0, W, active, wA,
+                         wB, wcl5);
     } else if constexpr (COOP && WL) {
         static_assert(NQ == 4, "word-pair windows: l + 2 <= 128");
         if (!active) W = 2;
@@ -925,8 +1035,13 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
             B.n[k] = k < PW ? n32[PW + (k < PW ? k : 0)] : 0u;
         }
         if (!active) return;
-    } else if constexpr (COOP && WL && TRI) {
+    } else if constexpr (COOP && WL && TRI == 1) {
         windows_exchange_w3(reinterpret_cast<u32x4 *>(xchg), wcl3, wA, wB);
+        if (!active) return;
+        window_finish_w<NQ>(wA, csize, wsA, W, A);
+        window_finish_w<NQ>(wB, csize, wsB, W, B);
+    } else if constexpr (COOP && WL && TRI == 2) {
+        windows_exchange_w5(reinterpret_cast<u32x2 *>(xchg), wcl5, wA, wB);
         if (!active) return;
         window_finish_w<NQ>(wA, csize, wsA, W, A);
         window_finish_w<NQ>(wB, csize, wsB, W, B);
@@ -1249,7 +1364,7 @@ __global__ __launch_bounds__(kBlock) void gather_windows_kernel(fc2_params p, fc
 
 // The STAGE + cooperative word-pair form with BT-thread blocks (FC2_TUNE_STAGE_BLOCK): the LDS
 // tables are staged once per BT pairs instead of once per 256 (each staging is ~60 L2 requests).
-template <int BT, bool NT, bool TRI>
+template <int BT, bool NT, int TRI>
 __global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
                                                                 uint64_t *__restrict__ out,
                                                                 uint64_t *__restrict__ tiemask, uint32_t tw) {
@@ -1328,7 +1443,7 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_persist_kernel(fc2_params p,
 // and no N words (`tri`, windows > 97 bases: the three-lane 48-B loads).  Its time bounds what
 // any kernel with this access pattern can reach on this GPU (bench.py: roofline.access_pattern_ceiling).
 __global__ __launch_bounds__(kBlock) void probe_pattern_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
-                                                               uint64_t *__restrict__ out, bool tri) {
+                                                               uint64_t *__restrict__ out, int tri) {
     __shared__ uint64_t s_cstart[kChromLds];
     const bool lds_tab = g.n_chrom <= (uint32_t)kChromLds;
     if (lds_tab) {
@@ -1360,7 +1475,19 @@ __global__ __launch_bounds__(kBlock) void probe_pattern_kernel(fc2_params p, fc2
                                                                          0x00020000);
     const int lane = (int)(threadIdx.x & 63);
     const uint32_t offs[2] = {wA.off, wB.off};
-    if (tri) {                                 // the scan's three-lane form (windows_issue_w3): 48 B per window
+    if (tri == 2) {                            // the five-lane form (windows_issue_w5): 40 B per window
+#pragma unroll
+        for (int c = 0; c < 11; ++c) {
+            const int w = 12 * c + lane / 5;
+            const uint32_t a = (uint32_t)__builtin_amdgcn_ds_bpermute((w & 63) << 2, (int)offs[0]);
+            const uint32_t b = (uint32_t)__builtin_amdgcn_ds_bpermute((w & 63) << 2, (int)offs[1]);
+            if (lane < 60 && w < 128) {
+                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, ((w >> 6) ? b : a) + 8u * (uint32_t)(lane % 5),
+                                                                     0, 0);
+                acc ^= (uint64_t)v.x | ((uint64_t)v.y << 32);
+            }
+        }
+    } else if (tri) {                          // the scan's three-lane form (windows_issue_w3): 48 B per window
 #pragma unroll
         for (int c = 0; c < 7; ++c) {
             const int w = 21 * c + lane / 3;
@@ -1390,7 +1517,7 @@ __global__ __launch_bounds__(kBlock) void probe_pattern_kernel(fc2_params p, fc2
 namespace fc2 {
 
 int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b,
-                         uint64_t *out, bool tri) {
+                         uint64_t *out, int tri) {
     hipLaunchKernelGGL(probe_pattern_kernel, dim3((unsigned)((b.n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, p, g,
                        b, out, tri);
     return hipGetLastError() == hipSuccess ? 0 : -1;
@@ -1441,7 +1568,7 @@ bool stage_bt_ok(int nq, const fc2_genome_view &g) {
            g.nsuper_words <= (uint32_t)kSuperLds;
 }
 
-void launch_scan32_stage_bt(int bt, bool tri, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
+void launch_scan32_stage_bt(int bt, int tri, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
                             const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
 #if FC2_AB_FORMS
 #define FC2_LBT(BTV, TRV)                                                                                     \
@@ -1452,23 +1579,29 @@ void launch_scan32_stage_bt(int bt, bool tri, bool nt, hipStream_t s, const fc2_
         else hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<BTV, false, TRV>), grid, dim3(BTV), 0, s, p, g, b,    \
                                 out, tiemask, tw);                                                            \
     } while (0)
-    if (tri) {
-        if (bt >= 1024) FC2_LBT(1024, true);
-        else if (bt >= 512) FC2_LBT(512, true);
-        else FC2_LBT(256, true);
+    if (tri == 2) {
+        if (bt >= 1024) FC2_LBT(1024, 2);
+        else if (bt >= 512) FC2_LBT(512, 2);
+        else FC2_LBT(256, 2);
+    } else if (tri) {
+        if (bt >= 1024) FC2_LBT(1024, 1);
+        else if (bt >= 512) FC2_LBT(512, 1);
+        else FC2_LBT(256, 1);
     } else {
-        if (bt >= 1024) FC2_LBT(1024, false);
-        else if (bt >= 512) FC2_LBT(512, false);
-        else FC2_LBT(256, false);
+        if (bt >= 1024) FC2_LBT(1024, 0);
+        else if (bt >= 512) FC2_LBT(512, 0);
+        else FC2_LBT(256, 0);
     }
 #undef FC2_LBT
 #else
     (void)bt;
     (void)nt;
     const dim3 grid((unsigned)((b.n + 511) / 512));      // 512-pair blocks, non-temporal streaming
-    if (tri) hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<512, true, true>), grid, dim3(512), 0, s, p, g, b, out,
-                                tiemask, tw);
-    else hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<512, true, false>), grid, dim3(512), 0, s, p, g, b, out,
+    if (tri == 2) hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<512, true, 2>), grid, dim3(512), 0, s, p, g, b, out,
+                                     tiemask, tw);
+    else if (tri) hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<512, true, 1>), grid, dim3(512), 0, s, p, g, b, out,
+                                     tiemask, tw);
+    else hipLaunchKernelGGL((bp_scan32_stage_bt_kernel<512, true, 0>), grid, dim3(512), 0, s, p, g, b, out,
                             tiemask, tw);
 #endif
 }

@@ -208,13 +208,14 @@ typedef struct fc2_batch_view {
                                          host-sorted batch): the scan deals each XCD a contiguous range */
 /* Per-call form hints (results never depend on them; by default fc2_bp_scan_launch picks the form from
  * the batch and the genome -- LDS-staged for a read-order batch over a genome >= 64 MiB of code planes,
- * plain otherwise; word-pair windows when the view carries wt and l + 2 <= 128; three-lane loads for
+ * plain otherwise; word-pair windows when the view carries wt and l + 2 <= 128; five-lane loads for
  * windows > 97 bases).  They let a caller (the test suite) run every form on any data: */
 #define FC2_BATCH_FORM_STAGED  0x02u  /* the LDS-staged form (chromosome table + N super map in LDS)   */
 #define FC2_BATCH_FORM_PLAIN   0x04u  /* the plain form (tables from L2, one lane per window)           */
 #define FC2_BATCH_FORM_UNITS   0x08u  /* windows from the 64-base unit planes even if wt is present      */
 #define FC2_BATCH_FORM_TWOLANE 0x10u  /* staged word-pair form: two-lane window loads at any length     */
 #define FC2_BATCH_FORM_TRI     0x20u  /* staged word-pair form: three-lane window loads at any length   */
+#define FC2_BATCH_FORM_FIVE    0x40u  /* staged word-pair form: five-lane 8-B window loads at any length */
 
 /* ---- pairs that need byte-exact evaluation ------------------------------ */
 /* Block for pair k at arena[off[k]]: int32 lenI, lenA, lenB, then
@@ -282,8 +283,9 @@ int         fc2_probe_pattern_launch(const fc2_params *p, const fc2_genome_view 
 #define FC2_TUNE_WORDS 11      /* 1 (default): the LDS-staging scan reads windows from the view's
                                   word-pair layout (wt) when present; 0: from the unit planes */
 #define FC2_TUNE_STAGE_BLOCK 13  /* threads per block of the LDS-staging word-pair scan: 256, 512 (default), 1024 */
-#define FC2_TUNE_TRI 14         /* three lanes load each window of the LDS-staging word-pair scan: 0 never,
-                                   1 always, 2 (default) when a batch's windows exceed 97 bases */
+#define FC2_TUNE_TRI 14         /* long-window loads of the LDS-staging word-pair scan: 0 two lanes always,
+                                   1 three 16-B lanes always, 2 three lanes when a batch's windows exceed
+                                   97 bases, 3 (default) five 8-B lanes when they exceed 97 bases */
 #define FC2_TUNE_REORDER_SHIFT 12 /* fc2_reorder_plan bucket size 2^shift bases (16..40; raised until
                                      <= 1024 buckets); 0 (default): ~1024 buckets over the genome */
 int         fc2_set_tuning(int key, int value);

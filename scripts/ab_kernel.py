@@ -76,7 +76,8 @@ def main():
         L.fc2_set_tuning(11, 0 if "wo0" in v else 1)                       # FC2_TUNE_WORDS
         mb = re.search(r"bt(\d+)", v)                                            # FC2_TUNE_STAGE_BLOCK
         L.fc2_set_tuning(13, int(mb.group(1)) if mb else 512)
-        L.fc2_set_tuning(14, 0 if "tri0" in v else (1 if "tri1" in v else 2))   # FC2_TUNE_TRI
+        mt = re.search(r"tri(\d)", v)                                           # FC2_TUNE_TRI (default 3)
+        L.fc2_set_tuning(14, int(mt.group(1)) if mt else 3)
         L.fc2_set_tuning(10, 0 if not m else (-1 if m.group(1) == "A" else int(m.group(1))))
 
     junk = torch.empty(b.n, dtype=torch.int64, device=dev)
@@ -104,7 +105,7 @@ def main():
                                             out.results.data_ptr(), None, b.tw,
                                             torch.cuda.current_stream(dev).cuda_stream))
             return
-        if v == "probe":          # the scan's access pattern without its arithmetic (fc2_probe_pattern_launch)
+        if v.startswith("probe"):  # the scan's access pattern without its arithmetic (fc2_probe_pattern_launch)
             gv, bv, pv = g.view(), b.view(), opt.params()
             N.check(N.lib().fc2_probe_pattern_launch(ctypes.byref(pv), ctypes.byref(gv), ctypes.byref(bv),
                                                      junk.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
@@ -125,7 +126,7 @@ def main():
             e.record(stream)
             torch.cuda.synchronize()
             times[v].append(s.elapsed_time(e) / a.reps)
-            assert a.no_check or v == "probe" or torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
+            assert a.no_check or v.startswith("probe") or torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
     for v in variants:
         t = np.array(times[v])
         print(json.dumps({"variant": v, "workload": a.workload + ("-ordered" if a.ordered else ""), "pairs": b.n, "median_ms": round(float(np.median(t)), 4),

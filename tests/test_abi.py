@@ -339,6 +339,6 @@ def test_shipped_library_has_no_tuning_state():
     for key in (1, 2, 3, 6, 7, 9, 10, 11, 13, 14):
         assert L.fc2_set_tuning(key, 0) == N.FC2_E_PARAM
     assert b"A/B builds" in L.fc2_last_error()
-    defaults = {1: 1, 2: 1, 3: 2, 6: 2, 7: 2, 9: 0, 10: 0, 11: 1, 13: 512, 14: 2}
+    defaults = {1: 1, 2: 1, 3: 2, 6: 2, 7: 2, 9: 0, 10: 0, 11: 1, 13: 512, 14: 3}
     for key, v in defaults.items():
         assert N.get_tuning(key) == v, key

@@ -25,6 +25,7 @@ from find_circ2_amd import _native as N  # noqa: E402
 FORMS = {"default": 0,
          "staged_words_twolane": N.BATCH_FORM_STAGED | N.BATCH_FORM_TWOLANE,
          "staged_words_tri": N.BATCH_FORM_STAGED | N.BATCH_FORM_TRI,
+         "staged_words_five": N.BATCH_FORM_STAGED | N.BATCH_FORM_FIVE,
          "staged_units": N.BATCH_FORM_STAGED | N.BATCH_FORM_UNITS,
          "plain_words": N.BATCH_FORM_PLAIN,
          "plain_units": N.BATCH_FORM_PLAIN | N.BATCH_FORM_UNITS}
