@@ -99,3 +99,21 @@ def test_stream_share_equals_slice_of_whole_stream():
         for j in range(b.nw):
             assert torch.equal(s.read_nwords[j * s.stride:j * s.stride + hi - lo],
                                b.read_nwords[j * b.stride + lo:j * b.stride + hi])
+
+
+def test_device_pipeline_both_result_forms():
+    """bench.device_pipeline (pinned host SoA -> H2D -> scan -> D2H, 8 slices on two streams): the
+    results that come back, as 2-B compact words expanded on the host or as raw 8-B words, equal the
+    device-resident scan of the same batch for every pair."""
+    import bench
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    dev = torch.device("cuda", 0)
+    a = argparse.Namespace(workload="hg19", pairs=3_000_000, read_len=100, locus_ordered=False)
+    opt, g, b = bench.build_workload(a, 0, dev)
+    res = scan(opt, g, b).results[:b.n]
+    b._bench_ref_results = res.cpu().clone()
+    for width, d2h in ((2, 2), (8, 8)):
+        r = bench.device_pipeline(opt, g, b, reps=1, width=width)
+        assert r["results_equal_device_resident_scan"] is True, (width, r)
+        assert abs(r["d2h_bytes_per_pair"] - d2h) < 0.1
