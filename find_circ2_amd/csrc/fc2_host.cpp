@@ -329,10 +329,14 @@ static inline int64_t pyclip(int64_t i, int64_t n) {
     return i > n ? n : i;
 }
 
-static int get_upper_impl(const fc2_fasta *f, int ci, int64_t start, int64_t end, std::string &out) {
+// get_data(...).upper() of [start, end) (find_circ.py:189-215); at most `limit` bytes of it when the
+// caller only needs to know that a window is longer than that (a window far outside its chromosome
+// is padded with 'N' to its full, possibly huge, length by the reference)
+static int get_upper_impl(const fc2_fasta *f, int ci, int64_t start, int64_t end, std::string &out,
+                          size_t limit = SIZE_MAX) {
     out.clear();
     if (!f) {  // GenomeAccessor.get_dummy (find_circ.py:370-371)
-        if (end > start) out.assign((size_t)(end - start), 'N');
+        if (end > start) out.assign(std::min((size_t)(end - start), limit), 'N');
         return FC2_OK;
     }
     if (ci < 0 || ci >= (int)f->chroms.size()) return fail(FC2_E_KEY, "unknown chromosome index");
@@ -343,15 +347,15 @@ static int get_upper_impl(const fc2_fasta *f, int ci, int64_t start, int64_t end
     if (end > c.size) { pad_end = end - c.size; end = c.size; }
     const int64_t os = pyclip(floordiv(start, c.ldata) * c.skip + start + c.ofs, (int64_t)f->n);
     const int64_t oe = pyclip(floordiv(end, c.ldata) * c.skip + end + c.ofs, (int64_t)f->n);
-    out.reserve((size_t)(pad_start + pad_end + (oe > os ? oe - os : 0)));
-    out.append((size_t)pad_start, 'N');
+    out.reserve(std::min((size_t)(pad_start + pad_end + (oe > os ? oe - os : 0)), limit));
+    out.append(std::min((size_t)pad_start, limit), 'N');
     const size_t sl = c.skipchar.size();
-    for (int64_t p = os; p < oe;) {
+    for (int64_t p = os; p < oe && out.size() < limit;) {
         if (sl && p + (int64_t)sl <= oe && !memcmp(f->data + p, c.skipchar.data(), sl)) { p += (int64_t)sl; continue; }
         out.push_back((char)upc(f->data[p]));
         ++p;
     }
-    out.append((size_t)pad_end, 'N');
+    out.append(std::min((size_t)pad_end, limit - out.size()), 'N');
     return FC2_OK;
 }
 
@@ -776,8 +780,10 @@ extern "C" int fc2_pack_windows(const fc2_params *p, const fc2_fasta *f, uint64_
             const int W = l + 2;
             if (!(pr.flags & (FC2_PAIR_SKIP | FC2_PAIR_BYTEPATH)) && l >= 0 && W <= 32 * (int)pw &&
                 (int)pr.chrom < nch) {
-                const int r1 = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + W, A);
-                const int r2 = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - W, (int64_t)pr.b_aend - e, B);
+                const int r1 = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + W, A,
+                                              (size_t)W + 1);
+                const int r2 = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - W, (int64_t)pr.b_aend - e, B,
+                                              (size_t)W + 1);
                 if (r1 || r2) { err = r1 ? r1 : r2; continue; }
                 const std::string *win[2] = {&A, &B};
                 for (int x = 0; x < 2; ++x) {
@@ -846,9 +852,12 @@ extern "C" int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64
         A.clear(); B.clear();
         if (l >= 0) {
             const int64_t flank = l + 2;
-            rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + flank, A);
+            // only min(length, l + 3) bytes of a window are kept below
+            rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + flank, A,
+                                (size_t)flank + 1);
             if (rc) return rc;
-            rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - flank, (int64_t)pr.b_aend - e, B);
+            rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - flank, (int64_t)pr.b_aend - e, B,
+                                (size_t)flank + 1);
             if (rc) return rc;
         }
         // a window of unexpected length (outside get_data's defined range) is kept at

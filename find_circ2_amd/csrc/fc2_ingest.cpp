@@ -561,88 +561,104 @@ int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r, fc2_
     return FC2_OK;
 }
 
+// Bytes of one aux value of type ty at p (the record ends at end), or -1 where htslib reports
+// corrupted aux data: an unknown type, a value running past the record, a Z / H string without its
+// NUL, a B array with an unknown element type or a negative count.
+ptrdiff_t aux_value_size(char ty, const uint8_t *p, const uint8_t *end) {
+    const ptrdiff_t left = end - p;
+    ptrdiff_t n;
+    switch (ty) {
+        case 'c': case 'C': case 'A': n = 1; break;
+        case 's': case 'S': n = 2; break;
+        case 'i': case 'I': case 'f': n = 4; break;
+        case 'Z': case 'H': {
+            const uint8_t *z = left > 0 ? (const uint8_t *)memchr(p, 0, (size_t)left) : nullptr;
+            return z ? (z - p) + 1 : -1;
+        }
+        case 'B': {
+            if (left < 5) return -1;
+            const char sub = (char)p[0];
+            const int w = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2
+                        : (sub == 'i' || sub == 'I' || sub == 'f') ? 4 : 0;
+            int32_t cnt;
+            memcpy(&cnt, p + 1, 4);
+            if (!w || cnt < 0) return -1;
+            n = 5 + (ptrdiff_t)w * cnt;
+            break;
+        }
+        default: return -1;
+    }
+    return n <= left ? n : -1;
+}
+
+// SAM text of the aux fields [p, end), already checked by scan_bam_tags
 void append_bam_tags(std::string &t, const uint8_t *p, const uint8_t *end) {
     char tmp[64];
-    while (p + 3 <= end) {
+    while (end - p >= 3) {
+        const char ty = (char)p[2];
+        const ptrdiff_t adv = aux_value_size(ty, p + 3, end);
+        if (adv < 0) return;
         t += '\t';
         t.append((const char *)p, 2);
-        const char ty = (char)p[2];
         p += 3;
         auto ival = [&](long long v) { snprintf(tmp, sizeof tmp, ":i:%lld", v); t += tmp; };
         switch (ty) {
-            case 'c': ival(*(const int8_t *)p); p += 1; break;
-            case 'C': ival(*(const uint8_t *)p); p += 1; break;
-            case 's': { int16_t v; memcpy(&v, p, 2); ival(v); p += 2; break; }
-            case 'S': { uint16_t v; memcpy(&v, p, 2); ival(v); p += 2; break; }
-            case 'i': { int32_t v; memcpy(&v, p, 4); ival(v); p += 4; break; }
-            case 'I': { uint32_t v; memcpy(&v, p, 4); ival(v); p += 4; break; }
-            case 'f': { float v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, ":f:%g", v); t += tmp; p += 4; break; }
-            case 'A': t += ":A:"; t += (char)*p; p += 1; break;
-            case 'Z': case 'H': {
-                const uint8_t *z = (const uint8_t *)memchr(p, 0, (size_t)(end - p));
-                if (!z) z = end;
+            case 'c': ival(*(const int8_t *)p); break;
+            case 'C': ival(*(const uint8_t *)p); break;
+            case 's': { int16_t v; memcpy(&v, p, 2); ival(v); break; }
+            case 'S': { uint16_t v; memcpy(&v, p, 2); ival(v); break; }
+            case 'i': { int32_t v; memcpy(&v, p, 4); ival(v); break; }
+            case 'I': { uint32_t v; memcpy(&v, p, 4); ival(v); break; }
+            case 'f': { float v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, ":f:%g", v); t += tmp; break; }
+            case 'A': t += ":A:"; t += (char)*p; break;
+            case 'Z': case 'H':
                 t += ':'; t += ty; t += ':';
-                t.append((const char *)p, (size_t)(z - p));
-                p = z + 1;
+                t.append((const char *)p, (size_t)(adv - 1));
                 break;
-            }
             case 'B': {
                 const char sub = (char)p[0];
                 int32_t cnt; memcpy(&cnt, p + 1, 4);
-                p += 5;
+                const uint8_t *q = p + 5;
                 t += ":B:"; t += sub;
                 for (int32_t k = 0; k < cnt; ++k) {
                     t += ',';
                     switch (sub) {
-                        case 'c': snprintf(tmp, sizeof tmp, "%d", *(const int8_t *)p); p += 1; break;
-                        case 'C': snprintf(tmp, sizeof tmp, "%u", *(const uint8_t *)p); p += 1; break;
-                        case 's': { int16_t v; memcpy(&v, p, 2); snprintf(tmp, sizeof tmp, "%d", v); p += 2; break; }
-                        case 'S': { uint16_t v; memcpy(&v, p, 2); snprintf(tmp, sizeof tmp, "%u", v); p += 2; break; }
-                        case 'i': { int32_t v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, "%d", v); p += 4; break; }
-                        case 'I': { uint32_t v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, "%u", v); p += 4; break; }
-                        default: { float v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, "%g", v); p += 4; break; }
+                        case 'c': snprintf(tmp, sizeof tmp, "%d", *(const int8_t *)q); q += 1; break;
+                        case 'C': snprintf(tmp, sizeof tmp, "%u", *(const uint8_t *)q); q += 1; break;
+                        case 's': { int16_t v; memcpy(&v, q, 2); snprintf(tmp, sizeof tmp, "%d", v); q += 2; break; }
+                        case 'S': { uint16_t v; memcpy(&v, q, 2); snprintf(tmp, sizeof tmp, "%u", v); q += 2; break; }
+                        case 'i': { int32_t v; memcpy(&v, q, 4); snprintf(tmp, sizeof tmp, "%d", v); q += 4; break; }
+                        case 'I': { uint32_t v; memcpy(&v, q, 4); snprintf(tmp, sizeof tmp, "%u", v); q += 4; break; }
+                        default: { float v; memcpy(&v, q, 4); snprintf(tmp, sizeof tmp, "%g", v); q += 4; break; }
                     }
                     t += tmp;
                 }
                 break;
             }
-            default: return;
         }
+        p += adv;
     }
 }
 
-// AS / XS from binary BAM tags (integer types as ints, anything else marked non-int)
-void scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
-    while (p + 3 <= end) {
+// AS / XS from binary BAM tags (integer types as ints, anything else marked non-int); false when
+// the aux data is corrupt (aux_value_size) or ends inside a tag
+bool scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
+    while (p < end) {
+        if (end - p < 3) return false;
         const char t0 = (char)p[0], t1 = (char)p[1], ty = (char)p[2];
         p += 3;
+        const ptrdiff_t adv = aux_value_size(ty, p, end);
+        if (adv < 0) return false;
         int64_t v = 0;
         bool isint = true;
-        size_t adv = 0;
         switch (ty) {
-            case 'c': v = *(const int8_t *)p; adv = 1; break;
-            case 'C': v = *(const uint8_t *)p; adv = 1; break;
-            case 's': { int16_t x; memcpy(&x, p, 2); v = x; adv = 2; break; }
-            case 'S': { uint16_t x; memcpy(&x, p, 2); v = x; adv = 2; break; }
-            case 'i': { int32_t x; memcpy(&x, p, 4); v = x; adv = 4; break; }
-            case 'I': { uint32_t x; memcpy(&x, p, 4); v = x; adv = 4; break; }
-            case 'f': isint = false; adv = 4; break;
-            case 'A': isint = false; adv = 1; break;
-            case 'Z': case 'H': {
-                const uint8_t *z = (const uint8_t *)memchr(p, 0, (size_t)(end - p));
-                isint = false;
-                adv = (size_t)((z ? z : end) - p) + 1;
-                break;
-            }
-            case 'B': {
-                const char sub = (char)p[0];
-                int32_t cnt; memcpy(&cnt, p + 1, 4);
-                const size_t w = (sub == 'c' || sub == 'C') ? 1 : (sub == 's' || sub == 'S') ? 2 : 4;
-                isint = false;
-                adv = 5 + w * (size_t)(cnt < 0 ? 0 : cnt);
-                break;
-            }
-            default: return;
+            case 'c': v = *(const int8_t *)p; break;
+            case 'C': v = *(const uint8_t *)p; break;
+            case 's': { int16_t x; memcpy(&x, p, 2); v = x; break; }
+            case 'S': { uint16_t x; memcpy(&x, p, 2); v = x; break; }
+            case 'i': { int32_t x; memcpy(&x, p, 4); v = x; break; }
+            case 'I': { uint32_t x; memcpy(&x, p, 4); v = x; break; }
+            default: isint = false; break;
         }
         const bool as = t0 == 'A' && t1 == 'S', xs = t0 == 'X' && t1 == 'S';
         if (as && !r.has_as) { r.has_as = true; r.as_int = isint; r.as = v; }
@@ -651,22 +667,30 @@ void scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
         if (xs) { r.xs_last_int = isint; r.xs_last = v; }
         p += adv;
     }
+    return true;
 }
 
 // one BAM record body (b: the bs bytes after block_size) into r; thread-safe (reads only the
-// header's reference names), so parser threads can call it.  ops: CIGAR scratch
-void parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
-                    std::vector<std::pair<int, int>> &ops, bool need_text, bool keep_raw) {
+// header's reference names), so parser threads can call it.  ops: CIGAR scratch.  A record whose
+// fields do not fit its block, with an unterminated query name or corrupt aux data is an error, as
+// in htslib's bam_read1 / aux parsing.
+int parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
+                   std::vector<std::pair<int, int>> &ops, bool need_text, bool keep_raw) {
+    if (bs < 32) return fc2::fail(FC2_E_FORMAT, "invalid BAM record (block shorter than its fixed fields)");
     const uint8_t *e = b + bs;
-    if (keep_raw) r.raw.assign((const char *)b - 4, 4 + (size_t)bs);
     int32_t ref_id, pos, l_seq, nref, npos, tlen;
     uint8_t l_name, mapq;
     uint16_t bin, n_cig, flag;
     memcpy(&ref_id, b, 4); memcpy(&pos, b + 4, 4); l_name = b[8]; mapq = b[9]; memcpy(&bin, b + 10, 2);
     memcpy(&n_cig, b + 12, 2); memcpy(&flag, b + 14, 2); memcpy(&l_seq, b + 16, 4); memcpy(&nref, b + 20, 4);
     memcpy(&npos, b + 24, 4); memcpy(&tlen, b + 28, 4);
+    if (l_seq < 0 || 32 + (int64_t)l_name + 4 * (int64_t)n_cig + ((int64_t)l_seq + 1) / 2 + (int64_t)l_seq > bs)
+        return fc2::fail(FC2_E_FORMAT, "invalid BAM record (its fields exceed its block size)");
+    if (l_name == 0 || b[32 + l_name - 1] != 0)
+        return fc2::fail(FC2_E_FORMAT, "invalid BAM record (query name not NUL-terminated)");
+    if (keep_raw) r.raw.assign((const char *)b - 4, 4 + (size_t)bs);
     const uint8_t *p = b + 32;
-    r.qname.assign((const char *)p, l_name ? l_name - 1 : 0);
+    r.qname.assign((const char *)p, l_name - 1);
     p += l_name;
     ops.resize(n_cig);
     for (int k = 0; k < n_cig; ++k) {
@@ -703,9 +727,9 @@ void parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
     r.as = r.xs = 0;
     r.as_last_int = r.xs_last_int = true;
     r.as_last = r.xs_last = 0;
-    scan_bam_tags(r, p, e);
+    if (!scan_bam_tags(r, p, e)) return fc2::fail(FC2_E_FORMAT, "corrupted aux data in a BAM record");
     r.has_qual = !(qual.size() == 1 && qual[0] == '*');
-    if (!need_text) return;
+    if (!need_text) return FC2_OK;
     std::string cig;
     char tmp[32];
     for (int k = 0; k < n_cig; ++k) {
@@ -725,6 +749,7 @@ void parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
     t += '\t';
     t += qual;
     append_bam_tags(t, p, e);
+    return FC2_OK;
 }
 
 int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
@@ -737,7 +762,9 @@ int parse_bam_record(fc2_ingest *h, Rec &r, bool &got) {
     memcpy(&bs, h->buf.data() + h->beg, 4);
     if (bs < 32 || !ensure(h, 4 + (size_t)bs))
         return fc2::fail(FC2_E_FORMAT, "truncated BAM record" + (h->z_err.empty() ? "" : " (" + h->z_err + ")"));
-    parse_bam_body(h, (const uint8_t *)h->buf.data() + h->beg + 4, bs, r, h->ops, h->need_text, h->bam_out != nullptr);
+    if (int rc = parse_bam_body(h, (const uint8_t *)h->buf.data() + h->beg + 4, bs, r, h->ops, h->need_text,
+                                h->bam_out != nullptr))
+        return rc;
     h->beg += 4 + (size_t)bs;
     got = true;
     return FC2_OK;
@@ -770,6 +797,7 @@ int read_header(fc2_ingest *h) {
     if (memcmp(h->buf.data() + h->beg, "BAM\1", 4) != 0) return fc2::fail(FC2_E_FORMAT, "not a BAM file");
     int32_t lt;
     memcpy(&lt, h->buf.data() + h->beg + 4, 4);
+    if (lt < 0) return fc2::fail(FC2_E_FORMAT, "invalid BAM header (negative text length)");
     if (!ensure(h, 8 + (size_t)lt + 4))
         return fc2::fail(FC2_E_FORMAT, "truncated BAM header" + (h->z_err.empty() ? "" : " (" + h->z_err + ")"));
     h->header.assign(h->buf.data() + h->beg + 8, (size_t)lt);
@@ -782,8 +810,9 @@ int read_header(fc2_ingest *h) {
         if (!ensure(h, 4)) return fc2::fail(FC2_E_FORMAT, "truncated BAM refs");
         int32_t ln;
         memcpy(&ln, h->buf.data() + h->beg, 4);
+        if (ln <= 0) return fc2::fail(FC2_E_FORMAT, "invalid BAM header (reference name length)");
         if (!ensure(h, 4 + (size_t)ln + 4)) return fc2::fail(FC2_E_FORMAT, "truncated BAM refs");
-        std::string name(h->buf.data() + h->beg + 4, ln > 0 ? (size_t)ln - 1 : 0);
+        std::string name(h->buf.data() + h->beg + 4, (size_t)ln - 1);
         int32_t lref;
         memcpy(&lref, h->buf.data() + h->beg + 4 + ln, 4);
         h->ref_len.push_back(lref);

@@ -18,6 +18,7 @@ import io
 import re
 import struct
 import sys
+import zlib
 from typing import Dict, Iterator, List, Optional, Tuple
 
 _CIGAR_RE = re.compile(r"(\d+)([MIDNSHP=X])")
@@ -150,6 +151,34 @@ class _Prefixed(io.RawIOBase):
         return len(data)
 
 
+class _Inflated(io.RawIOBase):
+    """The decompressed bytes of a gzip / BGZF stream, its failures as htslib reports them: a
+    member cut short is an IOError ("truncated file"), a corrupt one an IOError too, not zlib's own
+    error class."""
+
+    def __init__(self, raw):
+        self._gz = gzip.GzipFile(fileobj=raw, mode="rb")
+
+    def readable(self):
+        return True
+
+    def readinto(self, b):
+        try:
+            data = self._gz.read(len(b))
+        except EOFError as ex:
+            raise IOError("truncated file: %s" % ex)
+        except zlib.error as ex:
+            raise IOError("corrupt compressed data: %s" % ex)
+        b[:len(data)] = data
+        return len(data)
+
+    def close(self):
+        try:
+            self._gz.close()
+        finally:
+            super().close()
+
+
 def _read_upto(fh, n: int) -> bytes:
     out = b""
     while len(out) < n:
@@ -170,7 +199,7 @@ def sniff(raw) -> Tuple[str, str, object]:
     comp = "plain"
     if head[:2] == b"\x1f\x8b":
         comp = "bgzf" if (len(head) >= 14 and head[3] & 4 and head[12:14] == b"BC") else "gzip"
-        stream = io.BufferedReader(gzip.GzipFile(fileobj=stream, mode="rb"), 1 << 20)
+        stream = io.BufferedReader(_Inflated(stream), 1 << 20)
     magic = stream.peek(4)[:4]
     if len(magic) < 4 and magic:
         magic = _read_upto(stream, 4)
@@ -221,15 +250,30 @@ class AlignmentFile:
                 self.lengths.append(int(d.get("LN", 0)))
 
     def _parse_sam(self, line: str) -> AlignedSegment:
-        return parse_sam_line(line, self._tid)
+        try:
+            return parse_sam_line(line, self._tid)
+        except (IndexError, KeyError) as ex:      # htslib: "parse error" / unrecognized reference name
+            raise ValueError("SAM parse error: %s in %r" % (ex, line[:80]))
 
     # ------------------------------------------------------------------ BAM
     def _read(self, n, at_record=False):
         """n bytes of the BAM stream.  EOFError only for a clean end (nothing left where a record
         would start); a stream cut short inside a record or a gzip member is an IOError, as
         htslib reports a truncated file."""
+        if n < 0:
+            raise ValueError("invalid BAM length field %d" % n)
         try:
-            b = self._fh.read(n)
+            if n <= 1 << 24:
+                b = self._fh.read(n)
+            else:                       # a corrupt length: no up-front allocation of its size
+                parts, got = [], 0
+                while got < n:
+                    part = self._fh.read(min(1 << 24, n - got))
+                    if not part:
+                        break
+                    parts.append(part)
+                    got += len(part)
+                b = b"".join(parts)
         except EOFError as ex:          # gzip: "Compressed file ended before the end-of-stream marker ..."
             raise IOError("truncated file: %s" % ex)
         if len(b) != n:
@@ -258,6 +302,11 @@ class AlignmentFile:
     def _parse_bam(self, buf: bytes) -> AlignedSegment:
         (ref_id, pos, l_name, mapq, _bin, n_cig, flag, l_seq, _nref, _npos, _tlen) = struct.unpack_from(
             "<iiBBHHHiiii", buf, 0)
+        # htslib's bam_read1 checks: the fields fit the block, the query name is NUL-terminated
+        if l_seq < 0 or 32 + l_name + 4 * n_cig + (l_seq + 1) // 2 + l_seq > len(buf):
+            raise ValueError("invalid BAM record (its fields exceed its block size)")
+        if l_name == 0 or buf[32 + l_name - 1] != 0:
+            raise ValueError("invalid BAM record (query name not NUL-terminated)")
         o = 32
         qname = buf[o:o + l_name - 1].decode("latin-1")
         o += l_name
@@ -309,7 +358,12 @@ class AlignmentFile:
                     n, = struct.unpack("<i", self._read(4, at_record=True))
                 except EOFError:
                     return
-                yield self._parse_bam(self._read(n))
+                buf = self._read(n)
+                try:
+                    rec = self._parse_bam(buf)
+                except (struct.error, IndexError, KeyError, UnicodeDecodeError) as ex:
+                    raise ValueError("corrupt BAM record: %s" % ex)
+                yield rec
         else:
             if self._pending is not None:
                 line, self._pending = self._pending, None

@@ -349,6 +349,11 @@ int64_t orc_scan_fasta(const orc_params *p, const orc_fasta *f, int64_t n,
         if (flank > 0 && flank <= wcap) {
             la = orc_get_upper(f, ci, as, as + flank, Af, wcap * 2);
             lb = orc_get_upper(f, ci, bs, bs + flank, Bf, wcap * 2);
+            /* a window longer than flank + 1 (far outside the chromosome: get_data pads it with 'N') acts
+             * in find_breakpoints exactly as one of flank + 1 bytes: only A[:x], A[x:x+2] (x <= l) and
+             * the length of B[x+2:] are read, and any length > flank gives the same shape mismatch */
+            if (la > flank + 1) la = flank + 1;
+            if (lb > flank + 1) lb = flank + 1;
         }
         int r;
         if (use_fast && e > 0 && la == flank && lb == flank)

@@ -1,0 +1,153 @@
+"""Damaged inputs through both readers and the native read loop: truncations, flipped bytes and
+inserted garbage in every input form (SAM / BAM, plain / BGZF / gzip).  A reader may reject such an
+input (htslib does: truncated file, bad magic, corrupt record), but it must do so with an error the
+caller sees -- never a crash, a hang or a read outside its buffers.  The seeds are fixed; under
+scripts/sanitize_host.sh (ASan / UBSan builds of the host code) the same cases check memory safety.
+"""
+import gzip
+import random
+import zlib
+
+import pytest
+
+from find_circ2_amd import cli
+from find_circ2_amd.ingest import NativeIngest
+from find_circ2_amd.samio import AlignmentFile
+from oracle_engine import oracle_evaluator_factory
+from samgen import bgzf_compress, sam_to_bam
+from test_ingest import _mixed_sam
+
+
+@pytest.fixture(scope="module")
+def forms(tmp_path_factory):
+    d = tmp_path_factory.mktemp("fuzz")
+    sam = str(d / "mixed.sam")
+    fa = _mixed_sam(sam, 160, seed=815)
+    text = open(sam, "rb").read()
+    data = {"sam": text, "sam_bgzf": bgzf_compress(text), "sam_gzip": gzip.compress(text)}
+    for form, comp in (("bam_bgzf", "bgzf"), ("bam_gzip", "gzip"), ("bam_raw", "none")):
+        p = str(d / (form + ".tmp"))
+        sam_to_bam(text.decode("latin-1"), p, compress=comp)
+        data[form] = open(p, "rb").read()
+    return d, fa, data
+
+
+def _damage(rng, data: bytes) -> bytes:
+    kind = rng.randrange(4)
+    if kind == 0:                                   # cut anywhere, the header included
+        return data[:rng.randrange(len(data))]
+    b = bytearray(data)
+    if kind == 1:                                   # flip bytes past the first block's header
+        for _ in range(rng.randint(1, 8)):
+            i = rng.randrange(min(18, len(b) - 1), len(b))
+            b[i] ^= 1 << rng.randrange(8)
+        return bytes(b)
+    if kind == 2:                                   # garbage spliced in
+        i = rng.randrange(len(b))
+        return bytes(b[:i]) + bytes(rng.randrange(256) for _ in range(rng.randint(1, 64))) + bytes(b[i:])
+    return bytes(rng.randrange(256) for _ in range(rng.randint(0, 300)))   # noise
+
+
+def _native_all(path):
+    ing = NativeIngest(path, True)
+    try:
+        n = 0
+        for _ in range(100000):
+            frags = ing.next_chunk(15, False, False, 64)
+            n += len(frags)
+            if ing.eof and not frags:
+                break
+        return n
+    finally:
+        ing.close()
+
+
+def _python_all(path):
+    af = AlignmentFile(path, "rb")
+    try:
+        return sum(1 for _ in af)
+    finally:
+        af.close()
+
+
+@pytest.mark.parametrize("form", ["sam", "sam_bgzf", "sam_gzip", "bam_bgzf", "bam_gzip", "bam_raw"])
+def test_damaged_inputs_fail_cleanly_in_both_readers(forms, tmp_path, form):
+    d, _, data = forms
+    rng = random.Random(zlib.crc32(form.encode()))
+    outcomes = {"ok": 0, "error": 0}
+    for k in range(12):
+        p = str(tmp_path / ("case%d" % k))
+        with open(p, "wb") as fh:
+            fh.write(_damage(rng, data[form]))
+        for reader in (_native_all, _python_all):
+            try:
+                reader(p)
+                outcomes["ok"] += 1
+            except (OSError, ValueError, RuntimeError) as ex:     # the native reader: Fc2Error (RuntimeError)
+                assert str(ex) or type(ex).__name__
+                outcomes["error"] += 1
+    assert outcomes["error"] > 0                 # the damage is seen, not read past
+
+
+@pytest.mark.parametrize("form", ["sam", "bam_bgzf"])
+def test_damaged_inputs_through_the_native_read_loop(forms, tmp_path, form):
+    """The CLI's default loop (C++ read loop, oracle evaluator): a damaged input exits 1 or completes;
+    its process survives either way."""
+    d, fa, data = forms
+    rng = random.Random(4711 + len(form))
+    for k in range(8):
+        p = str(tmp_path / ("in%d" % k))
+        with open(p, "wb") as fh:
+            fh.write(_damage(rng, data[form]))
+        try:
+            rc = cli.main(["-G", fa, "-o", str(tmp_path / ("o%d" % k)), "-q", p],
+                          evaluator_factory=oracle_evaluator_factory)
+        except (IOError, OSError, ValueError, RuntimeError, EOFError, KeyError, IndexError):
+            rc = 1
+        assert rc in (0, 1)
+
+
+def _raw_bam(records):
+    """Uncompressed BAM: one reference 'chr1' (1000 bp), then the given record bodies."""
+    import struct
+    text = b"@SQ\tSN:chr1\tLN:1000\n"
+    out = b"BAM\x01" + struct.pack("<i", len(text)) + text + struct.pack("<i", 1)
+    out += struct.pack("<i", 5) + b"chr1\x00" + struct.pack("<i", 1000)
+    for body in records:
+        out += struct.pack("<i", len(body)) + body
+    return out
+
+
+def _record(name=b"r1\x00", seq_len=4, tags=b"", l_seq=None, l_name=None):
+    import struct
+    cigar = struct.pack("<I", (seq_len << 4) | 0)                  # seq_len M
+    body = struct.pack("<iiBBHHHiiii", 0, 10, len(name) if l_name is None else l_name, 60, 0, 1, 0,
+                       seq_len if l_seq is None else l_seq, -1, -1, 0)
+    return body + name + cigar + b"\x12" * ((seq_len + 1) // 2) + b"\x1e" * seq_len + tags
+
+
+BAD_RECORDS = {
+    "int_tag_cut_short": _record(tags=b"ASi\x05\x00"),
+    "array_count_past_record": _record(tags=b"XBBi\x00\xca\x9a\x3b\x01\x00\x00\x00"),
+    "string_without_nul": _record(tags=b"XZZabc"),
+    "unknown_tag_type": _record(tags=b"ASq\x05\x00\x00\x00"),
+    "seq_past_block": _record(l_seq=400),
+    "name_without_nul": _record(name=b"r1x"),
+    "tag_header_cut": _record(tags=b"AS"),
+}
+
+
+@pytest.mark.parametrize("case", sorted(BAD_RECORDS))
+def test_corrupt_bam_records_are_errors(tmp_path, case):
+    """Records htslib rejects (bam_read1's layout checks, corrupted aux data): both readers raise,
+    neither reads past the record (the aux parser of round 3 did, found by the fuzz above)."""
+    good = tmp_path / "good.bam"
+    good.write_bytes(_raw_bam([_record(tags=b"ASC\x04"), _record(name=b"r2\x00", tags=b"ASi\x04\x00\x00\x00")]))
+    assert _python_all(str(good)) == 2
+    _native_all(str(good))
+    p = tmp_path / "bad.bam"
+    p.write_bytes(_raw_bam([_record(tags=b"ASC\x04"), BAD_RECORDS[case]]))
+    with pytest.raises(RuntimeError, match="invalid BAM record|corrupted aux data"):
+        _native_all(str(p))
+    with pytest.raises(ValueError):
+        _python_all(str(p))
