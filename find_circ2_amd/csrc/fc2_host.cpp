@@ -347,7 +347,11 @@ static int get_upper_impl(const fc2_fasta *f, int ci, int64_t start, int64_t end
     if (end > c.size) { pad_end = end - c.size; end = c.size; }
     const int64_t os = pyclip(floordiv(start, c.ldata) * c.skip + start + c.ofs, (int64_t)f->n);
     const int64_t oe = pyclip(floordiv(end, c.ldata) * c.skip + end + c.ofs, (int64_t)f->n);
-    out.reserve(std::min((size_t)(pad_start + pad_end + (oe > os ? oe - os : 0)), limit));
+    const uint64_t full = (uint64_t)pad_start + (uint64_t)pad_end + (uint64_t)(oe > os ? oe - os : 0);
+    if (limit == SIZE_MAX && full > (1ull << 32))   // an inconsistent index entry (e.g. a negative size)
+        return fail(FC2_E_RANGE, "window of " + std::to_string(full) + " bytes from chromosome '" + c.name +
+                                     "': the reference's get_data raises MemoryError");
+    out.reserve(std::min((size_t)full, limit));
     out.append(std::min((size_t)pad_start, limit), 'N');
     const size_t sl = c.skipchar.size();
     for (int64_t p = os; p < oe && out.size() < limit;) {
@@ -450,20 +454,27 @@ extern "C" int fc2_fasta_get_upper(const fc2_fasta *f, int chrom, int64_t start,
     return FC2_OK;
 }
 
-static void compute_layout(fc2_fasta *f, uint64_t *n_units) {
+// Unit-aligned genome coordinates of every chromosome; false when the sizes (a damaged .byo_index)
+// add up to more than 2^40 bases, which no device table is laid out for.
+static bool compute_layout(fc2_fasta *f, uint64_t *n_units) {
+    constexpr uint64_t kMaxBases = 1ull << 40;
     uint64_t g = 0;
     for (auto &c : f->chroms) {
         c.gstart = g;
-        g += ((uint64_t)std::max<int64_t>(c.size, 0) + 63) & ~63ull;
+        const uint64_t sz = (uint64_t)std::max<int64_t>(c.size, 0);
+        if (sz > kMaxBases || g + sz > kMaxBases) return false;
+        g += (sz + 63) & ~63ull;
     }
     *n_units = std::max<uint64_t>(1, g / 64);
+    return true;
 }
 
 extern "C" int fc2_fasta_layout(const fc2_fasta *cf, uint64_t *n_units, uint64_t *n_coarse_words, uint64_t *chrom_start) {
     if (!cf) return fail(FC2_E_PARAM, "fc2_fasta_layout: null");
     fc2_fasta *f = const_cast<fc2_fasta *>(cf);
     uint64_t nu;
-    compute_layout(f, &nu);
+    if (!compute_layout(f, &nu))
+        return fail(FC2_E_RANGE, "fc2_fasta_layout: chromosome sizes add up to more than 2^40 bases (a damaged index?)");
     if (n_units) *n_units = nu;
     if (n_coarse_words) *n_coarse_words = (((nu + 15) >> 4) + 31) >> 5;
     if (chrom_start)
@@ -477,6 +488,10 @@ static bool chrom_regular(const fc2_fasta *f, const fc2_chrom_rec &c) {
     if (c.size <= 0) return true;
     if (c.ldata <= 0) return false;
     if ((int64_t)c.skipchar.size() != c.skip) return false;
+    // an index entry (.byo_index) that points outside the file: get_data's Python slices clip or wrap
+    // there, which only the byte path restates; the loop below then never leaves [0, n]
+    const int64_t n = (int64_t)f->n;
+    if (c.ofs < 0 || c.ofs > n || c.ldata > n || c.size > n) return false;
     for (char ch : c.skipchar)
         if (!py_isspace((uint8_t)ch)) return false;
     const int64_t nfull = c.size / c.ldata, rem = c.size % c.ldata;
@@ -508,7 +523,8 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
     if (!cf || !units || !nplane || !ncoarse) return fail(FC2_E_PARAM, "fc2_fasta_pack: null argument");
     fc2_fasta *f = const_cast<fc2_fasta *>(cf);
     uint64_t nu;
-    compute_layout(f, &nu);
+    if (!compute_layout(f, &nu))
+        return fail(FC2_E_RANGE, "fc2_fasta_pack: chromosome sizes add up to more than 2^40 bases (a damaged index?)");
     const int T = n_workers(n_threads);
     // regularity per chromosome
     {
