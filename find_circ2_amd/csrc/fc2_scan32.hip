@@ -551,6 +551,55 @@ __device__ __forceinline__ void window_nwords_plain(const fc2_genome_view &g, __
     }
 }
 
+// Long-window forms (three- and five-lane): the N test of both windows from the LDS super map,
+// looked up before any load is issued (all LDS traffic of the issue phase first) ...
+struct SuperN {
+    uint32_t sw[2][2], sb[2][2];
+    bool sv[2];
+};
+__device__ __forceinline__ void super_lookup_long(const fc2_genome_view &g, const uint32_t *s_nsuper, uint64_t cstart,
+                                                  const int64_t (&wsx)[2], int W, bool active, SuperN &S) {
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        S.sv[x] = false;
+        S.sw[x][0] = S.sw[x][1] = S.sb[x][0] = S.sb[x][1] = 0u;
+    }
+    if ((FC2_ABLATE & 2) || !s_nsuper) return;
+    const int64_t top = (int64_t)(g.n_units * 64) - 1;
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+        int64_t lo = (int64_t)cstart + wsx[x], hi = lo + W - 1;
+        lo = lo < 0 ? 0 : lo;
+        hi = hi > top ? top : hi;
+        S.sv[x] = active && lo <= hi;
+        const uint32_t k0 = S.sv[x] ? (uint32_t)((uint64_t)lo >> g.nsuper_shift) : 0u,
+                       k1 = S.sv[x] ? (uint32_t)((uint64_t)hi >> g.nsuper_shift) : 0u;
+        S.sw[x][0] = s_nsuper[k0 >> 5];
+        S.sw[x][1] = s_nsuper[k1 >> 5];
+        S.sb[x][0] = k0 & 31u;
+        S.sb[x][1] = k1 & 31u;
+    }
+}
+// ... and, after the window loads are in flight, the N-plane words of the flagged windows (one
+// range-checked dword load each; words before base 0 are not loaded at all)
+__device__ __forceinline__ void window_nwords_long(__amdgpu_buffer_rsrc_t rn, const SuperN &S, int x, WinW &Q) {
+    Q.v4 = u32x2{0u, 0u};
+    const bool nflag = S.sv[x] && (((S.sw[x][0] >> S.sb[x][0]) | (S.sw[x][1] >> S.sb[x][1])) & 1u);
+    Q.n03 = u32x4{0u, 0u, 0u, 0u};
+    Q.n4 = 0u;
+    if (nflag) {
+        uint32_t nw[5];
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const int32_t wj = (int32_t)Q.q0 + j;
+            nw[j] = 0u;
+            if (wj >= 0 && j < Q.nwd) nw[j] = __builtin_amdgcn_raw_buffer_load_b32(rn, (uint32_t)wj * 4u, 0, 0);
+        }
+        Q.n03 = u32x4{nw[0], nw[1], nw[2], nw[3]};
+        Q.n4 = nw[4];
+    }
+}
+
 // Three-lane form of the cooperative word-pair loads, for batches with windows longer than 97
 // bases (150-bp reads: a window needs 5 pairs = 40 B, more than two 16-B lane loads).  Each window is
 // read as the 48 B from its run start r -- inside one 128-B line because the copy is picked so
@@ -588,48 +637,15 @@ __device__ __forceinline__ void windows_issue_w3(const fc2_genome_view &g, __amd
             src[c] = (w >> 6) ? b : a;
         }
     }
-    uint32_t sw[2][2] = {{0u, 0u}, {0u, 0u}}, sb[2][2] = {{0u, 0u}, {0u, 0u}};
-    bool sv[2] = {false, false};
-    if (!(FC2_ABLATE & 2) && s_nsuper) {
-        const int64_t top = (int64_t)(g.n_units * 64) - 1;
-#pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            int64_t lo = (int64_t)cstart + wsx[x], hi = lo + W - 1;
-            lo = lo < 0 ? 0 : lo;
-            hi = hi > top ? top : hi;
-            sv[x] = active && lo <= hi;
-            const uint32_t k0 = sv[x] ? (uint32_t)((uint64_t)lo >> g.nsuper_shift) : 0u,
-                           k1 = sv[x] ? (uint32_t)((uint64_t)hi >> g.nsuper_shift) : 0u;
-            sw[x][0] = s_nsuper[k0 >> 5];
-            sw[x][1] = s_nsuper[k1 >> 5];
-            sb[x][0] = k0 & 31u;
-            sb[x][1] = k1 & 31u;
-        }
-    }
+    SuperN S;
+    super_lookup_long(g, s_nsuper, cstart, wsx, W, active, S);
 #pragma unroll
     for (int c = 0; c < 7; ++c) {
         cl[c] = u32x4{0u, 0u, 0u, 0u};
         if (ok[c]) cl[c] = __builtin_amdgcn_raw_buffer_load_b128(rs, src[c] + 16u * (uint32_t)part[c], 0, 0);
     }
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
-        WinW &Q = *R[x];
-        Q.v4 = u32x2{0u, 0u};
-        const bool nflag = sv[x] && (((sw[x][0] >> sb[x][0]) | (sw[x][1] >> sb[x][1])) & 1u);
-        Q.n03 = u32x4{0u, 0u, 0u, 0u};
-        Q.n4 = 0u;
-        if (nflag) {
-            uint32_t nw[5];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const int32_t wj = (int32_t)Q.q0 + j;
-                nw[j] = 0u;
-                if (wj >= 0 && j < Q.nwd) nw[j] = __builtin_amdgcn_raw_buffer_load_b32(rn, (uint32_t)wj * 4u, 0, 0);
-            }
-            Q.n03 = u32x4{nw[0], nw[1], nw[2], nw[3]};
-            Q.n4 = nw[4];
-        }
-    }
+    for (int x = 0; x < 2; ++x) window_nwords_long(rn, S, x, *R[x]);
 }
 
 // Owner side: the first 40 B of each window's three 16-B pieces, in two phases through 4 LDS slots
@@ -699,48 +715,15 @@ __device__ __forceinline__ void windows_issue_w5(const fc2_genome_view &g, __amd
             src[c] = (w >> 6) ? b : a;
         }
     }
-    uint32_t sw[2][2] = {{0u, 0u}, {0u, 0u}}, sb[2][2] = {{0u, 0u}, {0u, 0u}};
-    bool sv[2] = {false, false};
-    if (s_nsuper) {
-        const int64_t top = (int64_t)(g.n_units * 64) - 1;
-#pragma unroll
-        for (int x = 0; x < 2; ++x) {
-            int64_t lo = (int64_t)cstart + wsx[x], hi = lo + W - 1;
-            lo = lo < 0 ? 0 : lo;
-            hi = hi > top ? top : hi;
-            sv[x] = active && lo <= hi;
-            const uint32_t k0 = sv[x] ? (uint32_t)((uint64_t)lo >> g.nsuper_shift) : 0u,
-                           k1 = sv[x] ? (uint32_t)((uint64_t)hi >> g.nsuper_shift) : 0u;
-            sw[x][0] = s_nsuper[k0 >> 5];
-            sw[x][1] = s_nsuper[k1 >> 5];
-            sb[x][0] = k0 & 31u;
-            sb[x][1] = k1 & 31u;
-        }
-    }
+    SuperN S;
+    super_lookup_long(g, s_nsuper, cstart, wsx, W, active, S);
 #pragma unroll
     for (int c = 0; c < 11; ++c) {
         cl[c] = u32x2{0u, 0u};
         if (ok[c]) cl[c] = __builtin_amdgcn_raw_buffer_load_b64(rs, src[c] + part, 0, 0);
     }
 #pragma unroll
-    for (int x = 0; x < 2; ++x) {
-        WinW &Q = *R[x];
-        Q.v4 = u32x2{0u, 0u};
-        const bool nflag = sv[x] && (((sw[x][0] >> sb[x][0]) | (sw[x][1] >> sb[x][1])) & 1u);
-        Q.n03 = u32x4{0u, 0u, 0u, 0u};
-        Q.n4 = 0u;
-        if (nflag) {
-            uint32_t nw[5];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const int32_t wj = (int32_t)Q.q0 + j;
-                nw[j] = 0u;
-                if (wj >= 0 && j < Q.nwd) nw[j] = __builtin_amdgcn_raw_buffer_load_b32(rn, (uint32_t)wj * 4u, 0, 0);
-            }
-            Q.n03 = u32x4{nw[0], nw[1], nw[2], nw[3]};
-            Q.n4 = nw[4];
-        }
-    }
+    for (int x = 0; x < 2; ++x) window_nwords_long(rn, S, x, *R[x]);
 }
 
 // Owner side of the five-lane form: the wave's 4 KB of LDS slots hold eight instructions' 8-B pieces
