@@ -132,6 +132,9 @@ EXPORTED = [
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
     "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
     "fc2_caller_set_reads_gz", "fc2_caller_close_reads",
+    # include/fc2_ctx.h
+    "fc2_ctx_create", "fc2_ctx_destroy", "fc2_ctx_genome_load", "fc2_ctx_genome_view", "fc2_ctx_scan_async",
+    "fc2_ctx_sync", "fc2_ctx_stream", "fc2_ctx_last_error",
 ]
 
 
@@ -255,6 +258,14 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_rows": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_counter": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(ctypes.c_double)]),
         "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),
+        "fc2_ctx_create": (ctypes.c_int, [ctypes.c_int, P(vp)]),
+        "fc2_ctx_destroy": (None, [vp]),
+        "fc2_ctx_genome_load": (ctypes.c_int, [vp, vp, ctypes.c_int]),
+        "fc2_ctx_genome_view": (ctypes.c_int, [vp, P(GenomeView)]),
+        "fc2_ctx_scan_async": (ctypes.c_int, [vp, P(Params), u64, vp, vp, vp, vp, vp, u32, ctypes.c_int]),
+        "fc2_ctx_sync": (ctypes.c_int, [vp]),
+        "fc2_ctx_stream": (vp, [vp]),
+        "fc2_ctx_last_error": (ctypes.c_char_p, [vp]),
     }
     for name, (res, args) in sig.items():
         if os.environ.get("FC2_LIB_VARIANT") and not hasattr(L, name):

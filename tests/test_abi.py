@@ -342,3 +342,20 @@ def test_shipped_library_has_no_tuning_state():
     defaults = {1: 1, 2: 1, 3: 2, 6: 2, 7: 2, 9: 0, 10: 0, 11: 1, 13: 512, 14: 3}
     for key, v in defaults.items():
         assert N.get_tuning(key) == v, key
+
+
+def test_ctx_arguments_without_a_device(L):
+    """fc2_ctx (include/fc2_ctx.h) checks its arguments before touching a device, and fails with
+    FC2_E_HIP, not a crash, where no MI355X is visible (this container)."""
+    c = ctypes.c_void_p()
+    assert L.fc2_ctx_create(-1, ctypes.byref(c)) == N.FC2_E_PARAM
+    assert L.fc2_ctx_create(0, None) == N.FC2_E_PARAM
+    n = ctypes.c_int(0)
+    assert L.fc2_device_count(ctypes.byref(n)) == 0
+    if n.value == 0:
+        assert L.fc2_ctx_create(0, ctypes.byref(c)) == N.FC2_E_HIP
+        assert not c.value
+    assert L.fc2_ctx_sync(None) == N.FC2_E_PARAM
+    assert L.fc2_ctx_genome_load(None, None, 0) == N.FC2_E_PARAM
+    assert L.fc2_ctx_last_error(None) == b""
+    L.fc2_ctx_destroy(None)
