@@ -5,7 +5,8 @@ the scan writes (no hit, '+' GTAG and '-' CTAC hits, error bits, ties) plus word
 (4 B: x > 254, n_ties > 255, dist / ov > 15, a no-hit word with a strand bit; 2 B also x > 125,
 n_ties > 16, dist / ov > 3, any error bit), and its refusal of escape lists that do not match the
 escaped words.  GPU (tests/test_gpu_fullsize.py): the device packer on all 50M results of the bench
-batch, both widths, expanded back bit for bit.
+batch, both widths, expanded back bit for bit; tests/test_gpu_compact.py: the device words and escapes
+equal these restatements word for word, on words that escape and on real results with escapes.
 """
 import numpy as np
 import pytest
