@@ -42,7 +42,8 @@ def form_hint(monkeypatch):
     return box
 
 
-@pytest.mark.parametrize("seed", range(40))
+# FC2_FUZZ_CASES widens the campaign (the suite runs 40; profiles/r03/gpu_fuzz_400.log ran 400)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("FC2_FUZZ_CASES", "40"))))
 def test_random_options_and_kernel_forms(seed, form_hint):
     rng = np.random.default_rng(90210 + seed)
     asize = int(rng.integers(6, 26))
