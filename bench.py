@@ -234,8 +234,7 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8, width: int = 2):
         raise ValueError("width is 2 or 8")
     cap = max(1024, step // 1024)
     host_out = torch.empty(n, dtype=torch.int64 if width == 8 else torch.int16).pin_memory()
-    host_esc = torch.empty((chunks, 16 * cap), dtype=torch.uint8).pin_memory()
-    host_cnt = torch.empty(chunks, dtype=torch.int32).pin_memory()
+    host_esc = torch.empty((chunks, 16 * (cap + 1)), dtype=torch.uint8).pin_memory()   # slots + count per slice
     dcomp = [CompactResults(step, dev, cap, width=2) for _ in range(2)] if width == 2 else None
     streams = [torch.cuda.Stream(dev), torch.cuda.Stream(dev)]
     tail_words = (step + 1) // 2 if narrow else step
@@ -276,8 +275,7 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8, width: int = 2):
                 else:
                     cr = compact(opt, dres[c & 1], m, into=dcomp[c & 1], stream=st.cuda_stream, width=2)
                     host_out[lo:lo + m].copy_(cr.words[:m], non_blocking=True)
-                    host_esc[c].copy_(cr.esc.view(torch.uint8), non_blocking=True)
-                    host_cnt[c:c + 1].copy_(cr.count, non_blocking=True)
+                    host_esc[c].copy_(cr.esc_block.view(torch.uint8), non_blocking=True)
         torch.cuda.synchronize(dev)
 
     run_once()
@@ -294,16 +292,17 @@ def device_pipeline(opt, g, b, reps: int, chunks: int = 8, width: int = 2):
         else:
             words = host_out.numpy().view(np.uint16)
             esc = host_esc.numpy().view(N.ESCAPE_DTYPE)
+            cnt = host_esc.numpy()[:, 16 * cap:16 * cap + 4].copy().view(np.int32)[:, 0]
             got = np.empty(n, np.int64)
             for c, (lo, m, _, _, _) in enumerate(host):
-                k = int(host_cnt[c])
+                k = int(cnt[c])
                 if not 0 <= k <= cap:
                     raise RuntimeError("device pipeline slice %d: %d escapes, %d slots" % (c, k, cap))
                 expand(opt, words[lo:lo + m], esc[c, :k], out=got[lo:lo + m])
             ok = bool(np.array_equal(got, b._bench_ref_results.numpy()))
     kn = sum(h[2] for h in host)
     h2d = sum(h[4].numel() * 8 for h in host)
-    d2h = width * n + (0 if width == 8 else len(host) * (16 * cap + 4))
+    d2h = width * n + (0 if width == 8 else len(host) * 16 * (cap + 1))
     return {"value": round(n / (ms * 1e-3), 1), "unit": "anchor-pairs/s", "ms_per_batch": round(ms, 3),
             "pcie_GBs": round((h2d + d2h) / (ms * 1e-3) / 1e9, 1),
             "h2d_bytes_per_pair": round(h2d / n, 2), "d2h_bytes_per_pair": round(d2h / n, 2),
@@ -509,7 +508,7 @@ def timed_scans(opt, g, b, steps, warmup, ws, dev):
     return t1 - t0, float(np.mean(kms)), out
 
 
-def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, per_rank=4):
+def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, per_rank=4, streams=None):
     """configs[3]: ONE pair stream (the `n` pairs rank 0 scans in the weak run, seed 1337) cut into
     contiguous batches dealt round-robin to the ranks (shard.my_batches).  Rank 0 scans views of its
     own weak batch; every other rank generates only its batches of the stream (stream_share).  Each
@@ -547,12 +546,16 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
         s = b0.sub(lo, hi) if rank == 0 else stream_share(opt, g, cfg_kw, lo, hi)
         subs.append((k, lo, hi, s, torch.empty(hi - lo, dtype=torch.int64, device=dev),
                      {w: CompactResults(hi - lo, dev, cap, width=w) for w in widths}))
-    stream = torch.cuda.current_stream(dev)
-    copier = torch.cuda.Stream(dev)              # D2H of batch k overlaps the scan of batch k+1
+    # scans on one stream, the D2H of batch k on another, overlapping the scan of batch k+1
+    stream, copier = streams if streams is not None else (torch.cuda.current_stream(dev), torch.cuda.Stream(dev))
     done = [torch.cuda.Event() for _ in subs]
+
+    host = {"scan": 0.0, "copy": 0.0, "calls": 0}   # host seconds in the launch calls (FC2_BENCH_HOST_TIMING)
+    clock = time.perf_counter if os.environ.get("FC2_BENCH_HOST_TIMING") else None
 
     def step(mode):                              # mode: None (scans only), 2, 4 (compact widths), 8 (raw)
         for j, (k, lo, hi, s, res, comp) in enumerate(subs):
+            t0 = clock() if clock else 0.0
             scan(opt, g, s, out=ScanOutput(res, None, s.tw, s.stride), stream=stream.cuda_stream)
             if mode is None:
                 continue
@@ -560,14 +563,19 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
                 compact(opt, res, hi - lo, into=comp[mode], stream=stream.cuda_stream)
             done[j].record(stream)
             copier.wait_event(done[j])
+            t1 = clock() if clock else 0.0
             with torch.cuda.stream(copier):
                 if mode != 8:
                     m, c = merged[mode], comp[mode]
                     m.words_t[lo:hi].copy_(c.words[:hi - lo], non_blocking=True)
-                    m.esc_t[k].copy_(c.esc.view(torch.uint8), non_blocking=True)
-                    m.count_t[k:k + 1].copy_(c.count, non_blocking=True)
+                    m.esc_t[k].copy_(c.esc_block.view(torch.uint8), non_blocking=True)   # slots + count
                 else:
                     raw.tensor[lo:hi].copy_(res, non_blocking=True)
+            if clock and mode == 2:
+                t2 = clock()
+                host["scan"] += t1 - t0
+                host["copy"] += t2 - t1
+                host["calls"] += 1
         if mode is not None:                     # the next step's scans overwrite res / comp
             stream.wait_stream(copier)
 
@@ -620,6 +628,9 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
             "merge_8B_words": form(8),
             "pairs_total": n, "batch_pairs": bsz, "n_batches": len(bounds), "ranks": ws,
             "merged_equals_single_rank": equal[2],
+            **({"host_ms_per_batch_2B": {"scan_and_pack_launch": round(host["scan"] / max(1, host["calls"]) * 1e3, 4),
+                                         "copy_calls": round(host["copy"] / max(1, host["calls"]) * 1e3, 4)}}
+               if clock else {}),
             "note": "one %d-pair stream in %d contiguous batches of %d dealt round-robin to %d rank(s), each rank "
                     "holding only its batches; each batch's results packed on the device to 2 B/pair "
                     "(fc2_result_compact_launch, canonical mode, escapes for the rest) and copied into a node-local "

@@ -395,7 +395,10 @@ class ScanOutput:
 class CompactResults:
     """A compact transfer form of a run of results (include/fc2_bp.h "compact results"): device
     words [n] (int32 for width 4, int16 for width 2), escape slots [cap] (``N.ESCAPE_DTYPE`` as
-    16 bytes each) and the escape count."""
+    16 bytes each) and the escape count.  The count lives in the low 4 bytes of one more 16-byte slot
+    after the escape slots, so ``esc_block`` (slots + count) crosses to the host in ONE copy: a
+    separate 4-byte D2H copy per batch made the runtime serialise the copies with the next scan on
+    some stream placements (profiles/r03/strong_small_copies.txt)."""
 
     def __init__(self, n: int, device, cap: int = 0, width: int = 4):
         torch = _torch()
@@ -404,8 +407,9 @@ class CompactResults:
         self.n, self.width = n, width
         self.cap = cap or max(1024, n // 256)
         self.words = torch.empty(max(n, 1), dtype=torch.int16 if width == 2 else torch.int32, device=device)
-        self.esc = torch.empty(2 * self.cap, dtype=torch.int64, device=device)
-        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.esc_block = torch.zeros(2 * (self.cap + 1), dtype=torch.int64, device=device)
+        self.esc = self.esc_block[:2 * self.cap]
+        self.count = self.esc_block[2 * self.cap:2 * self.cap + 1].view(torch.int32)[:1]
 
 
 def compact(options: Options, results, n: int, into: CompactResults = None, stream=None,

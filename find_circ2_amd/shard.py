@@ -140,8 +140,8 @@ class SharedCompactResults(SharedResults):
         self.n, self.bounds, self.cap, self.width = int(n), list(bounds), int(cap), width
         nb = len(self.bounds)
         self._w_bytes = (width * self.n + 63) // 64 * 64
-        self._e_bytes = 16 * self.cap * nb
-        size = max(64, self._w_bytes + self._e_bytes + 8 * nb)
+        self._e_bytes = 16 * (self.cap + 1) * nb    # per batch: cap escape slots, then the count's slot
+        size = max(64, self._w_bytes + self._e_bytes)
         self.creator = create
         self.shm = shared_memory.SharedMemory(name=name, create=create, size=size)
         if not create:
@@ -152,8 +152,12 @@ class SharedCompactResults(SharedResults):
         self.name = self.shm.name
         buf = self.shm.buf
         self.words = np.ndarray((self.n,), np.uint16 if width == 2 else np.uint32, buffer=buf)
-        self.esc = np.ndarray((nb, self.cap), N.ESCAPE_DTYPE, buffer=buf, offset=self._w_bytes)
-        self.esc_count = np.ndarray((nb,), np.int32, buffer=buf, offset=self._w_bytes + self._e_bytes)
+        # batch k's block mirrors the device CompactResults.esc_block: escape slots, then the count in
+        # the low 4 bytes of one more slot; one D2H copy per batch carries both
+        self.esc_blocks = np.ndarray((nb, self.cap + 1), N.ESCAPE_DTYPE, buffer=buf, offset=self._w_bytes)
+        self.esc = self.esc_blocks[:, :self.cap]
+        self.esc_count = np.ndarray((nb,), np.int32, buffer=buf, offset=self._w_bytes + 16 * self.cap,
+                                    strides=(16 * (self.cap + 1),)) if nb else np.zeros(0, np.int32)
         self.array = np.ndarray((size,), np.uint8, buffer=buf)      # the whole segment (pinning, poisoning)
         self._pinned = False
         if pin and size:
@@ -162,8 +166,7 @@ class SharedCompactResults(SharedResults):
         import torch
         self.tensor = torch.from_numpy(self.array)
         self.words_t = torch.from_numpy(self.words.view(np.int16 if width == 2 else np.int32))
-        self.esc_t = torch.from_numpy(self.esc.view(np.uint8).reshape(nb, 16 * self.cap))
-        self.count_t = torch.from_numpy(self.esc_count)
+        self.esc_t = torch.from_numpy(self.esc_blocks.view(np.uint8).reshape(nb, 16 * (self.cap + 1)))
 
     def escapes(self) -> np.ndarray:
         """Every batch's escapes with stream indices; ValueError if a batch overflowed its slots."""
@@ -185,8 +188,8 @@ class SharedCompactResults(SharedResults):
         return expand(options, self.words, self.escapes(), n_threads=n_threads)
 
     def close(self):
-        self.words = self.esc = self.esc_count = None
-        self.words_t = self.esc_t = self.count_t = None
+        self.words = self.esc = self.esc_blocks = self.esc_count = None
+        self.words_t = self.esc_t = None
         super().close()
 
 
