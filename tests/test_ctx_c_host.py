@@ -80,3 +80,62 @@ def test_c_host_equals_python_layer(ctx_host, tmp_path):
         got = np.fromfile(str(tmp_path / "r.bin"), np.int64)
         assert np.array_equal(got, exp), fa
         assert ((got & 0xFFFF) != 0xFFFF).sum() > 100
+
+
+def _build(tmp_path_factory, src, name):
+    exe = str(tmp_path_factory.mktemp("c") / name)
+    r = subprocess.run(["gcc", "-O1", "-Wall", "-Werror", "-std=c11", "-I", os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "tests", "c", src), "-o", exe, "-L", LIBDIR, "-lfc2",
+                        "-Wl,-rpath," + LIBDIR, "-Wl,--allow-shlib-undefined"],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    assert r.returncode == 0, r.stderr.decode()
+    return exe
+
+
+@pytest.fixture(scope="module")
+def findcirc_host(tmp_path_factory):
+    N.build()
+    return _build(tmp_path_factory, "findcirc_host.c", "findcirc_host")
+
+
+def test_c_findcirc_builds_and_fails_cleanly_without_a_gpu(findcirc_host, tmp_path):
+    import ctypes
+    c = ctypes.c_int(0)
+    N.lib().fc2_device_count(ctypes.byref(c))
+    if c.value:
+        pytest.skip("a GPU is visible (the GPU test covers this program)")
+    from test_ingest import _mixed_sam
+    sam = str(tmp_path / "in.sam")
+    fa = _mixed_sam(sam, 50, seed=3)
+    r = subprocess.run([findcirc_host, "-G", fa, "-o", str(tmp_path / "out"), sam], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, timeout=120)
+    assert r.returncode == 2 and b"fc2_ctx_create" in r.stderr, r.stderr
+
+
+@pytest.mark.gpu
+def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path):
+    """The whole read loop and the search driven from C (no Python in the process) write the
+    Python CLI's files: both BED tables, multi_events.tsv and spliced_reads.fastq (decompressed)."""
+    import gzip
+    import sys
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from test_ingest import _mixed_sam
+    sam = str(tmp_path / "in.sam")
+    fa = _mixed_sam(sam, 3000, seed=4711)
+    py_out, c_out = str(tmp_path / "py"), str(tmp_path / "c")
+    r = subprocess.run([sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", py_out, "-n", "cx", "-q", sam],
+                       cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    r = subprocess.run([findcirc_host, "-G", fa, "-o", c_out, "-n", "cx", sam], stdout=subprocess.PIPE,
+                       stderr=subprocess.PIPE, timeout=300)
+    assert r.returncode == 0, r.stderr.decode()
+    for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
+        a, b = open(os.path.join(py_out, f), "rb").read(), open(os.path.join(c_out, f), "rb").read()
+        assert a == b, f
+    circ = open(os.path.join(c_out, "circ_splice_sites.bed")).read().splitlines()
+    assert len(circ) > 10
+    a = gzip.open(os.path.join(py_out, "spliced_reads.fastq.gz")).read()
+    b = gzip.open(os.path.join(c_out, "spliced_reads.fastq.gz")).read()
+    assert a == b and len(a) > 1000
