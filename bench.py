@@ -32,6 +32,7 @@ sys.path.insert(0, ROOT)
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+STRONG_TAIL = 0          # configs[3]: default --strong-tail (shard.round_bounds)
 METRIC = "anchor-pairs/sec (backsplice calls) at 100 bp reads, 1/2/4/8 MI355X"
 
 
@@ -59,6 +60,9 @@ def parse():
     ap.add_argument("--strong-batches", type=int, default=0,
                     help="configs[3]: batches per rank the stream is cut into (shard.round_robin_batch); 0: "
                          "max(2, 8 // ranks)")
+    ap.add_argument("--strong-tail", type=int, default=-1,
+                    help="configs[3]: cut each rank's last batch into t + 1 halving pieces (shard.round_bounds); "
+                         "-1: the default, 0: equal batches")
     ap.add_argument("--config4-pairs", type=int, default=0, help="configs[4] stream length (default 200M; tests)")
     ap.add_argument("--no-cli", action="store_true", help="skip the end-to-end CLI extra (2M reads, BAM on stdin)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
@@ -508,7 +512,7 @@ def timed_scans(opt, g, b, steps, warmup, ws, dev):
     return t1 - t0, float(np.mean(kms)), out
 
 
-def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, per_rank=4, streams=None):
+def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, per_rank=4, streams=None, tail=0):
     """configs[3]: ONE pair stream (the `n` pairs rank 0 scans in the weak run, seed 1337) cut into
     contiguous batches dealt round-robin to the ranks (shard.my_batches).  Rank 0 scans views of its
     own weak batch; every other rank generates only its batches of the stream (stream_share).  Each
@@ -524,11 +528,11 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
     import torch
     from find_circ2_amd import CompactResults, compact, scan
     from find_circ2_amd.hotpath import ScanOutput
-    from find_circ2_amd.shard import (SharedCompactResults, SharedResults, batch_bounds, broadcast_name, my_batches,
+    from find_circ2_amd.shard import (SharedCompactResults, SharedResults, broadcast_name, my_bounds, round_bounds,
                                       round_robin_batch)
     bsz = round_robin_batch(n, ws, per_rank=per_rank)
-    bounds = batch_bounds(n, bsz)
-    mine = my_batches(n, bsz, rank, ws)
+    bounds = round_bounds(n, ws, per_rank=per_rank, tail=tail)
+    mine = my_bounds(bounds, rank, ws)
     cap = max(1024, bsz // 256)
     widths = (2, 4)
     if rank == 0:
@@ -626,12 +630,14 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
             "merge_bytes_per_pair": 2, "escapes": n_esc[2],
             "merge_4B_words": dict(form(4), escapes=n_esc[4], merged_equals_single_rank=equal[4]),
             "merge_8B_words": form(8),
-            "pairs_total": n, "batch_pairs": bsz, "n_batches": len(bounds), "ranks": ws,
+            "pairs_total": n, "batch_pairs": bsz, "n_batches": len(bounds), "ranks": ws, "tail_pieces": tail,
+            "smallest_batch_pairs": min(hi - lo for lo, hi in bounds),
             "merged_equals_single_rank": equal[2],
             **({"host_ms_per_batch_2B": {"scan_and_pack_launch": round(host["scan"] / max(1, host["calls"]) * 1e3, 4),
                                          "copy_calls": round(host["copy"] / max(1, host["calls"]) * 1e3, 4)}}
                if clock else {}),
-            "note": "one %d-pair stream in %d contiguous batches of %d dealt round-robin to %d rank(s), each rank "
+            "note": "one %d-pair stream in %d contiguous batches of up to %d pairs dealt round-robin to %d rank(s) "
+                    "(with tail_pieces = t, each rank's last batch cut into t + 1 halving pieces), each rank "
                     "holding only its batches; each batch's results packed on the device to 2 B/pair "
                     "(fc2_result_compact_launch, canonical mode, escapes for the rest) and copied into a node-local "
                     "pinned shared-memory buffer at their input offsets (host-side ordered merge, no collective on "
@@ -1086,7 +1092,8 @@ def main():
     if not args.no_strong:
         n0, kw0 = workload_cfg(args, 0)
         strong = strong_scaling(opt, g, b if rank == 0 else None, b._bench_ref_results.numpy() if rank == 0 else None,
-                                ws, rank, dev, args.steps, args.warmup, n0, kw0, per_rank=args.strong_batches or max(2, 8 // ws))
+                                ws, rank, dev, args.steps, args.warmup, n0, kw0, per_rank=args.strong_batches or max(2, 8 // ws),
+                                tail=args.strong_tail if args.strong_tail >= 0 else STRONG_TAIL)
         torch.cuda.empty_cache()
     line = {
         "metric": METRIC,

@@ -73,6 +73,38 @@ def round_robin_batch(n: int, world: int, per_rank: int = 4, align: int = 512) -
     return -(-b // align) * align
 
 
+def round_bounds(n: int, world: int, per_rank: int = 4, align: int = 512, tail: int = 0) -> List[Tuple[int, int]]:
+    """Contiguous [start, end) batches covering n pairs, dealt in rounds of `world` equal batches
+    (batch k goes to rank k % world, as in my_batches): `per_rank` rounds of round_robin_batch's
+    size, except that with tail = t > 0 the last round is cut into t + 1 rounds of 1/2, 1/4, ...,
+    1/2^t, 1/2^t of a batch (each rounded up to `align`).  A rank then copies its results off the
+    device in pieces that shrink toward the end of its share: every piece's copy overlaps the scan
+    of the next one, and the copy nobody waits behind is 1/2^t of a batch instead of a whole one.
+    Results never depend on the cut (pairs are independent, find_circ.py:854-974)."""
+    b = round_robin_batch(n, world, per_rank=per_rank, align=align)
+    sizes = [b] * max(0, per_rank - 1)
+    if tail > 0:
+        sizes += [max(align, -(-(b >> j) // align) * align) for j in range(1, tail + 1)]
+        sizes.append(sizes[-1])
+    else:
+        sizes.append(b)
+    out, s, i = [], 0, 0
+    while s < n:
+        size = sizes[min(i, len(sizes) - 1)]
+        for _ in range(max(1, world)):
+            if s >= n:
+                break
+            out.append((s, min(n, s + size)))
+            s += size
+        i += 1
+    return out
+
+
+def my_bounds(bounds: Sequence[Tuple[int, int]], rank: int, world: int) -> List[Tuple[int, int, int]]:
+    """(batch_index, start, end) of the batches of `bounds` rank ``rank`` scans (round-robin)."""
+    return [(k, s, e) for k, (s, e) in enumerate(bounds) if k % world == rank]
+
+
 class SharedResults:
     """Node-local ordered merge of per-pair results: ONE host buffer of n 8-byte ``fc2_result``
     records in /dev/shm that every rank on the node maps.  A rank copies each of its batches'

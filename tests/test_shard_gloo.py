@@ -130,6 +130,23 @@ def test_round_robin_batch_balance():
         assert max(counts) - min(counts) <= b
 
 
+@pytest.mark.parametrize("tail", [0, 1, 3])
+def test_round_bounds_cover_and_shrink(tail):
+    for n, world, per_rank in [(50_000_000, 1, 8), (50_000_000, 8, 2), (1_000_000, 2, 4), (513, 4, 2), (1, 8, 2)]:
+        bounds = shard.round_bounds(n, world, per_rank=per_rank, tail=tail)
+        assert bounds[0][0] == 0 and bounds[-1][1] == n
+        assert all(bounds[k][1] == bounds[k + 1][0] for k in range(len(bounds) - 1))
+        assert all(e > s and s % 512 == 0 for s, e in bounds)
+        b = shard.round_robin_batch(n, world, per_rank=per_rank)
+        counts = [sum(e - s for _, s, e in shard.my_bounds(bounds, r, world)) for r in range(world)]
+        assert sum(counts) == n and max(counts) - min(counts) <= b
+        if tail:
+            # the stream ends on a piece of 1/2^tail of a batch
+            assert bounds[-1][1] - bounds[-1][0] <= max(512, -(-(b >> tail) // 512) * 512)
+        if not tail:
+            assert bounds == shard.batch_bounds(n, b)
+
+
 def _compact_worker(rank, world, port, n, batch, q, width):
     import sys
     import torch.distributed as dist
