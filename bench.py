@@ -966,6 +966,39 @@ def window_carrying(opt, g, b, steps, dev, bpp):
     return out
 
 
+def wave_per_pair(opt, g, b, dev, bpp, reps: int = 3):
+    """North_star's kernel shape on the headline batch: one wavefront per pair (FC2_BATCH_FORM_WAVE,
+    bp_wave_kernel: windows and read staged in LDS, lane = position, ballot prefix sums, wave argmax),
+    timed with HIP events on the scan's stream; every result must equal the shipped form's."""
+    import torch
+    from find_circ2_amd import scan, _native as N
+    ref = scan(opt, g, b).results[:b.n].clone()
+    keep = b.layout
+    b.layout = keep | N.BATCH_FORM_WAVE
+    try:
+        out = scan(opt, g, b)
+        torch.cuda.synchronize(dev)
+        equal = bool(torch.equal(out.results[:b.n], ref))
+        stream = torch.cuda.current_stream(dev)
+        a, z = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(stream)
+        for _ in range(reps):
+            scan(opt, g, b, out=out)
+        z.record(stream)
+        torch.cuda.synchronize(dev)
+        km = a.elapsed_time(z) / reps
+    finally:
+        b.layout = keep
+    del out, ref
+    ach = bpp * b.n / (km * 1e-3) / 1e9
+    return {"value": round(b.n / (km * 1e-3), 1), "unit": "anchor-pairs/s", "kernel_ms": round(km, 4),
+            "frac": round(ach / HBM_PEAK_GBS, 4), "results_equal_shipped_form": equal,
+            "note": "BASELINE north_star's kernel shape (one wavefront per pair, 16 pairs per wave with their loads "
+                    "in flight together, windows + read in LDS, lane t = positions t and t + 64, ballot/popcount "
+                    "prefix sums, shuffle argmax) on the same batch and genome tables; issue-bound (DESIGN.md §4), "
+                    "so the headline keeps one pair per lane"}
+
+
 def _cli_outputs(out):
     import gzip
     files = {}
@@ -1139,6 +1172,7 @@ def main():
             k: v for k, v in device_pipeline(opt, g, b, reps=5, width=8).items() if k != "note"}
         line["extra"]["host_pipeline_from_pair_arrays"] = host_pipeline(opt, g, b)
         line["extra"]["configs[2]_window_carrying_batch"] = window_carrying(opt, g, b, args.steps, dev, bpp)
+        line["extra"]["configs[2]_north_star_wave_per_pair_form"] = wave_per_pair(opt, g, b, dev, bpp)
         # the honest price of locus order for a read-order stream: the device reorder (fc2_reorder_launch,
         # stable counting sort by genome bucket) in front of the scan, both timed; results in input order
         line["extra"]["configs[2]_device_reorder_then_scan"] = reorder_then_scan(opt, g, b, args.steps, dev, bpp)

@@ -90,6 +90,7 @@ BATCH_FORM_UNITS = 0x08
 BATCH_FORM_TWOLANE = 0x10
 BATCH_FORM_TRI = 0x20
 BATCH_FORM_FIVE = 0x40
+BATCH_FORM_WAVE = 0x80     # BASELINE north_star shape: one wavefront per pair (include/fc2_bp.h)
 
 
 class ReorderInfo(ctypes.Structure):

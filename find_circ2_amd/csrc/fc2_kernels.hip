@@ -854,6 +854,10 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         fc2::launch_scan32_win((int)pw, nt, s, *p, *g, *b, out, tiemask, tw);
         return hip_check(hipGetLastError(), "bp_scan32_win_kernel launch");
     }
+    if ((b->layout & FC2_BATCH_FORM_WAVE) && fc2::wave_ok(ml, *g)) {
+        fc2::launch_wave(s, *p, *g, *b, out, tiemask, tw);
+        return hip_check(hipGetLastError(), "bp_wave_kernel launch");
+    }
     if (g_kernel32) {
         const int sw = g_xcd_swizzle == 2 ? ((b->layout & FC2_BATCH_LOCUS_ORDERED) ? 1 : 0) : g_xcd_swizzle;
         fc2_genome_view gv = *g;

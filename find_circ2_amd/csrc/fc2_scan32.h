@@ -33,6 +33,10 @@ void launch_scan32_win(int pw, bool nt, hipStream_t s, const fc2_params &p, cons
                        const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw);
 void launch_gather_windows(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, uint64_t n, uint64_t stride,
                            fc2_pair *pairs, uint64_t *win_words, uint64_t *win_nwords, uint32_t pw);
+// BASELINE north_star's shape (one wavefront per pair, FC2_BATCH_FORM_WAVE); usable when wave_ok().
+bool wave_ok(int ml, const fc2_genome_view &g);
+void launch_wave(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out,
+                 uint64_t *tiemask, uint32_t tw);
 // Measurement kernel: the read-order scan's memory pattern without its arithmetic (needs g.wt).
 int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b,
                          uint64_t *out, int tri);   // tri: the scan's window form, as above

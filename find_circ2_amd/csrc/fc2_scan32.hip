@@ -1495,6 +1495,327 @@ __global__ __launch_bounds__(kBlock) void probe_pattern_kernel(fc2_params p, fc2
     if (live) st_stream<true>(out + i, acc);
 }
 
+// ---------------------------------------------------------------------------------------------
+// bp_wave_kernel: BASELINE.json north_star's kernel shape, run as a per-call form
+// (FC2_BATCH_FORM_WAVE) so that DESIGN.md §4's choice of one pair per lane is measured against it
+// rather than estimated.  ONE wavefront per anchor pair: a wave takes kWavePairs consecutive pairs,
+// loads their records and read rows (round trip 1) and both genome windows of each -- the same
+// 2-bit word pairs of g.wt as the staged form, one 128-B line per window, plus the N words of the
+// windows the super map flags (round trip 2) -- cooperatively into LDS, then evaluates the pairs
+// one after another with lane t on the positions x = t and x = t + 64 (find_circ.py:906-954):
+// per-position mismatches of I against Af and Bf[x+2:], their wavefront prefix sums (a ballot and
+// a popcount below the lane), the GT/AG - CT/AC masks, and a wavefront argmax of the score whose
+// ties keep the stable-sort order (x ascending, '+' before '-', find_circ.py:961-974).  Every
+// comparison uses the staged form's plane bits (low, high, N), so results are identical.
+constexpr int kWavePairs = 16;         // pairs per wave, their loads in flight together
+constexpr int kWaveSlot = 53;          // u32 of LDS per pair
+// record at 0; read rows; read N rows; per window (A, B): lo, hi, n x 5; one pad word (the N-plane
+// funnel's high word); the chromosome's start and size (2 x u64)
+constexpr int kWsRead = 4, kWsReadN = 14, kWsWin = 18, kWsChrom = 49;
+
+struct WaveGeo {
+    uint64_t cstart;
+    int64_t csize, ws[2];
+    int l, W;
+    bool ok, err;
+};
+
+// cstart / csize: the pair's chromosome (0, 0 when unknown), from g.chrom_start / chrom_size
+__device__ __forceinline__ void wave_geo(const fc2_params &p, const fc2_genome_view &g, const fc2_pair &pr,
+                                         uint64_t cstart, int64_t csize, WaveGeo &G) {
+    const int e = p.asize - p.margin;
+    G.l = (int)pr.read_len - 2 * e;
+    G.W = G.l + 2;                             // flank, find_circ.py:900
+    const bool known = pr.chrom < g.n_chrom;
+    G.cstart = known ? cstart : 0ull;
+    G.csize = known ? csize : 0;
+    G.ws[0] = (int64_t)pr.a_pos + e;
+    G.ws[1] = (int64_t)pr.b_aend - e - G.W;
+    const bool bad = (pr.flags & FC2_PAIR_SKIP) || G.l < 0 || G.l > 126 || !known || G.ws[0] > G.csize ||
+                     G.ws[0] + G.W < 0 || G.ws[1] > G.csize || G.ws[1] + G.W < 0;
+    G.ok = !bad;
+    G.err = bad && !(pr.flags & FC2_PAIR_SKIP) && G.l >= 0;   // as scan_pair: ERR_WIN
+}
+
+// may the window [cstart + ws, + W) touch an 'N'? (super map; without one, always load the N words)
+__device__ __forceinline__ bool wave_nflag(const fc2_genome_view &g, uint64_t cstart, int64_t ws, int W) {
+    const int64_t top = (int64_t)(g.n_units * 64) - 1;
+    int64_t lo = (int64_t)cstart + ws, hi = lo + W - 1;
+    lo = lo < 0 ? 0 : lo;
+    hi = hi > top ? top : hi;
+    if (lo > hi) return false;
+    if (!g.nsuper) return true;
+    const uint32_t k0 = (uint32_t)((uint64_t)lo >> g.nsuper_shift), k1 = (uint32_t)((uint64_t)hi >> g.nsuper_shift);
+    return (((g.nsuper[k0 >> 5] >> (k0 & 31u)) | (g.nsuper[k1 >> 5] >> (k1 & 31u))) & 1u) != 0;
+}
+
+__device__ __forceinline__ fc2_pair wave_record(const uint32_t *P) {
+    fc2_pair pr;
+    __builtin_memcpy(&pr, P, sizeof pr);
+    return pr;
+}
+
+__global__ __launch_bounds__(kBlock) void bp_wave_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+                                                         uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
+                                                         uint32_t tw) {
+    __shared__ uint32_t s_w[(kBlock / 64) * kWavePairs * kWaveSlot];
+    const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+    uint32_t *S = s_w + wv * kWavePairs * kWaveSlot;
+    const uint64_t i0 = ((uint64_t)blockIdx.x * (kBlock / 64) + wv) * kWavePairs;
+    if (i0 >= bv.n) return;                    // the whole wave
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void *)g.wt, 0, (int)(uint32_t)g.wt_bytes,
+                                                                         0x00020000);
+    const uint64_t nb = g.n_units * 8;
+    const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc(
+        (void *)g.nplane, 0, (int)(uint32_t)(nb > 0xFFFFFFFFull ? 0xFFFFFFFFull : nb), 0x00020000);
+
+    // round trip 1: records (slots 0 .. kWavePairs-1) and read rows (pair k, row j < 5) into LDS
+    for (int s = lane; s < 6 * kWavePairs; s += 64) {
+        if (s < kWavePairs) {
+            u64x2 v = {0ull, 0ull};
+            if (i0 + s < bv.n) v = ld_pair_raw<false>(bv.pairs + i0 + s);
+            uint32_t *P = S + s * kWaveSlot;
+            P[0] = (uint32_t)v.x; P[1] = (uint32_t)(v.x >> 32); P[2] = (uint32_t)v.y; P[3] = (uint32_t)(v.y >> 32);
+        } else {
+            const int t = s - kWavePairs, k = t / 5, j = t - 5 * k;
+            uint64_t v = 0;
+            if (i0 + k < bv.n && (uint32_t)j < bv.rw) v = bv.read_words[(uint64_t)j * bv.stride + i0 + k];
+            S[k * kWaveSlot + kWsRead + 2 * j] = (uint32_t)v;
+            S[k * kWaveSlot + kWsRead + 2 * j + 1] = (uint32_t)(v >> 32);
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // round trip 2: both windows of every pair (slot: pair s / 10, window (s / 5) & 1, word pair
+    // s % 5) with the N words of flagged windows, then the N rows of READ_N pairs
+    for (int s = lane; s < 10 * kWavePairs; s += 64) {
+        const int k = s / 10, x = (s / 5) & 1, j = s % 5;
+        uint32_t *Q = S + k * kWaveSlot + kWsWin + 15 * x;
+        uint32_t lo = 0, hi = 0, nn = 0;
+        if (i0 + k < bv.n) {
+            const fc2_pair pr = wave_record(S + k * kWaveSlot);
+            const bool known = pr.chrom < g.n_chrom;
+            const uint64_t cstart = known ? g.chrom_start[pr.chrom] : 0ull;
+            const int64_t csize = known ? g.chrom_size[pr.chrom] : 0;
+            if (s % 10 == 0) {                 // kept for the evaluation loop
+                uint32_t *C = S + k * kWaveSlot + kWsChrom;
+                C[0] = (uint32_t)cstart; C[1] = (uint32_t)(cstart >> 32);
+                C[2] = (uint32_t)(uint64_t)csize; C[3] = (uint32_t)((uint64_t)csize >> 32);
+            }
+            WaveGeo G;
+            wave_geo(p, g, pr, cstart, csize, G);
+            if (G.ok && !(pr.flags & FC2_PAIR_BYTEPATH)) {
+                WinW R;
+                window_geom_w(g, G.cstart, G.ws[x], G.W, R);
+                if (j < R.nwd) {
+                    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, R.off + 8u * (uint32_t)j, 0, 0);
+                    lo = v.x;
+                    hi = v.y;
+                    const int32_t w = (int32_t)R.q0 + j;
+                    if (w >= 0 && wave_nflag(g, G.cstart, G.ws[x], G.W))
+                        nn = __builtin_amdgcn_raw_buffer_load_b32(rn, (uint32_t)w * 4u, 0, 0);
+                }
+            }
+        }
+        Q[j] = lo;
+        Q[5 + j] = hi;
+        Q[10 + j] = nn;
+    }
+    for (int s = lane; s < 2 * kWavePairs; s += 64) {
+        const int k = s >> 1, j = s & 1;
+        uint64_t v = 0;
+        if (i0 + k < bv.n) {
+            const fc2_pair pr = wave_record(S + k * kWaveSlot);
+            if ((pr.flags & (FC2_PAIR_READ_N | FC2_PAIR_READ_N1)) == FC2_PAIR_READ_N && bv.read_nwords &&
+                (uint32_t)j < bv.nw)
+                v = bv.read_nwords[(uint64_t)j * bv.stride + i0 + k];
+        }
+        S[k * kWaveSlot + kWsReadN + 2 * j] = (uint32_t)v;
+        S[k * kWaveSlot + kWsReadN + 2 * j + 1] = (uint32_t)(v >> 32);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // evaluation, one pair at a time over the whole wave; lane t holds positions x = t, t + 64
+    const bool want_ties = p.allhits != 0;
+    const uint64_t lt = (1ull << lane) - 1ull;  // lanes below this one
+    uint64_t myres = 0;
+    bool mine = false;
+    for (int k = 0; k < kWavePairs; ++k) {
+        const uint64_t i = i0 + k;
+        if (i >= bv.n) break;
+        const uint32_t *P = S + k * kWaveSlot;
+        // the pair's record and chromosome are the same for every lane: into SGPRs, so the
+        // per-pair geometry runs on the scalar unit
+        auto rfl = [](uint32_t v) -> uint32_t { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); };
+        uint32_t rec[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) rec[j] = rfl(P[j]);
+        fc2_pair pr;
+        __builtin_memcpy(&pr, rec, sizeof pr);
+        if (pr.flags & FC2_PAIR_BYTEPATH) continue;   // left for the byte-exact kernel
+        const uint32_t *C = P + kWsChrom;
+        WaveGeo G;
+        wave_geo(p, g, pr, (uint64_t)rfl(C[0]) | ((uint64_t)rfl(C[1]) << 32),
+                 (int64_t)((uint64_t)rfl(C[2]) | ((uint64_t)rfl(C[3]) << 32)), G);
+        uint64_t res;
+        uint64_t tie[2][2] = {{0ull, 0ull}, {0ull, 0ull}};   // [strand][x / 64]
+        if (!G.ok) {
+            Best32 none;
+            res = pack_result(none, 0, G.err ? FC2_RES_ERR_WIN : 0u);
+        } else {
+            const int l = G.l;
+            const bool n1 = (pr.flags & (FC2_PAIR_READ_N | FC2_PAIR_READ_N1)) == (FC2_PAIR_READ_N | FC2_PAIR_READ_N1);
+            const bool nrow = !n1 && (pr.flags & FC2_PAIR_READ_N);
+            // per window (uniform): bit offset of position 0 in its first word pair, and the window
+            // positions inside the chromosome, [vlo, vhi) (window_finish_w's masking), clamped
+            int sh[2], vlo[2], vhi[2];
+#pragma unroll
+            for (int w = 0; w < 2; ++w) {
+                sh[w] = (int)(((int64_t)G.cstart + G.ws[w]) & 31);
+                const int64_t a = -G.ws[w], z = G.csize - G.ws[w];
+                vlo[w] = (int)(a < -256 ? -256 : (a > 256 ? 256 : a));
+                vhi[w] = (int)(z < -256 ? -256 : (z > 256 ? 256 : z));
+            }
+            // per lane and h: window w's plane bits from position x_h on (bit j = position x_h + j),
+            // positions outside the chromosome as 'N'
+            uint32_t wlo[2][2], whi[2][2], wn[2][2];
+            uint32_t ilo[2], ihi[2], inn[2];       // I[x_h] (bit 0)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int x = lane + 64 * h;
+#pragma unroll
+                for (int w = 0; w < 2; ++w) {
+                    const int t = sh[w] + (x < 127 ? x : 127);
+                    const int kw = t >> 5;
+                    const unsigned sb = (unsigned)(t & 31);
+                    const uint32_t *Q = P + kWsWin + 15 * w;
+                    const uint32_t lo = alignr(Q[kw + 1], Q[kw], sb), hi = alignr(Q[kw + 6], Q[kw + 5], sb),
+                                   nn = alignr(Q[kw + 11], Q[kw + 10], sb);
+                    int v0 = vlo[w] - x, v1 = vhi[w] - x;          // valid j in [v0, v1)
+                    v0 = v0 < 0 ? 0 : (v0 > 3 ? 3 : v0);
+                    v1 = v1 < 0 ? 0 : (v1 > 3 ? 3 : v1);
+                    const uint32_t vm = ((1u << v1) - 1u) & ~((1u << v0) - 1u);
+                    wlo[h][w] = lo & vm;
+                    whi[h][w] = hi & vm;
+                    wn[h][w] = (nn & vm) | (7u & ~vm);
+                }
+                const int y = l + x;
+                ilo[h] = (P[kWsRead + (x >> 5)] >> (x & 31)) & 1u;
+                ihi[h] = (P[kWsRead + ((y >> 5) & 7)] >> (y & 31)) & 1u;
+                inn[h] = n1 ? (x == (int)pr.npos ? 1u : 0u) : (nrow ? (P[kWsReadN + ((x >> 5) & 3)] >> (x & 31)) & 1u : 0u);
+            }
+            auto at = [&](int h, int w, int j) -> unsigned {   // plane bits of window w at position x_h + j
+                return ((wlo[h][w] >> j) & 1u) | (((whi[h][w] >> j) & 1u) << 1) | (((wn[h][w] >> j) & 1u) << 2);
+            };
+            bool mA[2], mB[2], cp[2], cm[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int x = lane + 64 * h;
+                // mismatches: A[x] vs I[x], B[x + 2] vs I[x] on all three planes
+                const uint32_t dA = (wlo[h][0] ^ ilo[h]) | (whi[h][0] ^ ihi[h]) | (wn[h][0] ^ inn[h]);
+                const uint32_t dB = (wlo[h][1] ^ (ilo[h] << 2)) | (whi[h][1] ^ (ihi[h] << 2)) | (wn[h][1] ^ (inn[h] << 2));
+                mA[h] = x < l && (dA & 1u);
+                mB[h] = x < l && (dB & 4u);
+                // the staged form's masks: G = hi & ~lo, C = lo & ~hi, T = hi & lo (N bit ignored), A = no bit
+                const uint32_t aT = whi[h][0] & wlo[h][0];
+                const uint32_t bA = ~(wlo[h][1] | whi[h][1] | wn[h][1]);
+                const uint32_t common = (aT >> 1) & bA;
+                const uint32_t plus = (whi[h][0] & ~wlo[h][0]) & ((whi[h][1] & ~wlo[h][1]) >> 1) & common;
+                const uint32_t minus = (wlo[h][0] & ~whi[h][0]) & ((wlo[h][1] & ~whi[h][1]) >> 1) & common;
+                cp[h] = x <= l && (plus & 1u);
+                cm[h] = x <= l && (minus & 1u);
+            }
+            // wavefront prefix sums of the mismatch flags
+            const uint64_t bA0 = __ballot(mA[0]), bA1 = __ballot(mA[1]);
+            const uint64_t bB0 = __ballot(mB[0]), bB1 = __ballot(mB[1]);
+            const int totB = __popcll(bB0) + __popcll(bB1);
+            int d[2];
+            d[0] = __popcll(bA0 & lt) + totB - __popcll(bB0 & lt);
+            d[1] = __popcll(bA0) + __popcll(bA1 & lt) + totB - __popcll(bB0) - __popcll(bB1 & lt);
+            const int prim_minus = (pr.flags & FC2_PAIR_PRIMARY_REV) ? 1 : 0;
+            const int sp_plus = p.strandpref ? (prim_minus ? 0 : 100) : 0;     // find_circ.py:796-797
+            const int sp_minus = p.strandpref ? (prim_minus ? 100 : 0) : 0;
+            bool hp[2], hm[2];
+            int sp[2], sm[2];
+            int best = INT32_MIN;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int x = lane + 64 * h;
+                const bool q = x <= l && d[h] <= p.maxdist;
+                const int ov = ov_of(x, l, p.margin);
+                if (p.noncanonical) {
+                    hp[h] = hm[h] = q;
+                    sp[h] = 20 * (int)cp[h] - 10 * d[h] - ov + sp_plus;
+                    sm[h] = 20 * (int)cm[h] - 10 * d[h] - ov + sp_minus;
+                } else {
+                    hp[h] = q && cp[h];
+                    hm[h] = q && cm[h];
+                    sp[h] = 20 - 10 * d[h] - ov + sp_plus;
+                    sm[h] = 20 - 10 * d[h] - ov + sp_minus;
+                }
+                if (hp[h] && sp[h] > best) best = sp[h];
+                if (hm[h] && sm[h] > best) best = sm[h];
+            }
+            const uint64_t hb[4] = {__ballot(hp[0]), __ballot(hp[1]), __ballot(hm[0]), __ballot(hm[1])};
+            const int n_hits = __popcll(hb[0]) + __popcll(hb[1]) + __popcll(hb[2]) + __popcll(hb[3]);
+            Best32 B;
+            if (n_hits) {
+                // wavefront argmax of the score
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) {
+                    const int v = __shfl_xor(best, o);
+                    best = v > best ? v : best;
+                }
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    tie[0][h] = __ballot(hp[h] && sp[h] == best);
+                    tie[1][h] = __ballot(hm[h] && sm[h] == best);
+                }
+                // first tie in stable-sort order: lowest x, '+' before '-'
+                const int h = (tie[0][0] | tie[1][0]) ? 0 : 1;
+                const uint64_t any = h ? (tie[0][1] | tie[1][1]) : (tie[0][0] | tie[1][0]);
+                const int xl = __ffsll((unsigned long long)any) - 1;
+                const int x = 64 * h + xl;
+                B.n_hits = n_hits;
+                B.best_score = best;
+                B.best_x = x;
+                B.best_minus = (((h ? tie[0][1] : tie[0][0]) >> xl) & 1ull) ? 0 : 1;
+                B.best_dist = __shfl(h ? d[1] : d[0], xl);
+                B.best_ov = ov_of(x, l, p.margin);
+                B.n_ties = __popcll(tie[0][0]) + __popcll(tie[0][1]) + __popcll(tie[1][0]) + __popcll(tie[1][1]);
+            }
+            unsigned gtag12 = 0;
+            if (B.n_hits) {
+                if (!p.noncanonical) {
+                    constexpr unsigned kGTAG = 2u | (3u << 3) | (0u << 6) | (2u << 9);
+                    constexpr unsigned kCTAC = 1u | (3u << 3) | (0u << 6) | (1u << 9);
+                    gtag12 = B.best_minus ? kCTAC : kGTAG;
+                } else {
+                    // the best x's four bases, from the lane that holds it
+                    const int h = B.best_x >> 6, xl = B.best_x & 63;
+                    auto code = [](unsigned v) -> unsigned { return (v & 4u) ? 4u : (v & 3u); };
+                    const unsigned mine4 = code(at(h, 0, 0)) | (code(at(h, 0, 1)) << 3) | (code(at(h, 1, 0)) << 6) |
+                                           (code(at(h, 1, 1)) << 9);
+                    gtag12 = (unsigned)__shfl((int)mine4, xl);
+                }
+            }
+            res = pack_result(B, gtag12, 0);
+        }
+        if (lane == k) { myres = res; mine = true; }
+        if (want_ties && (uint32_t)lane < tw) {
+            const uint32_t half = tw / 2, j = (uint32_t)lane;
+            const uint32_t s = j < half ? 0u : 1u, w = j < half ? j : j - half;
+            const uint64_t t0 = w ? tie[0][1] : tie[0][0], t1 = w ? tie[1][1] : tie[1][0];
+            tiemask[(uint64_t)j * bv.stride + i] = w < 2 ? (s ? t1 : t0) : 0ull;
+        }
+    }
+    if (mine) out[i0 + lane] = myres;
+}
+
 }  // namespace
 
 namespace fc2 {
@@ -1544,6 +1865,17 @@ void launch_gather_windows(hipStream_t s, const fc2_params &p, const fc2_genome_
         default: hipLaunchKernelGGL(gather_windows_kernel<4>, grid, dim3(kBlock), 0, s, p, g, n, stride, pairs,
                                     win_words, win_nwords); break;
     }
+}
+
+bool wave_ok(int ml, const fc2_genome_view &g) {
+    return ml + 2 <= 128 && !g.dummy && g.wt && g.wt_bytes && g.chrom_start && g.chrom_size && g.nplane;
+}
+
+void launch_wave(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out,
+                 uint64_t *tiemask, uint32_t tw) {
+    constexpr uint64_t per_block = (kBlock / 64) * kWavePairs;
+    hipLaunchKernelGGL(bp_wave_kernel, dim3((unsigned)((b.n + per_block - 1) / per_block)), dim3(kBlock), 0, s, p, g, b,
+                       out, tiemask, tw);
 }
 
 bool stage_bt_ok(int nq, const fc2_genome_view &g) {

@@ -216,6 +216,9 @@ typedef struct fc2_batch_view {
 #define FC2_BATCH_FORM_TWOLANE 0x10u  /* staged word-pair form: two-lane window loads at any length     */
 #define FC2_BATCH_FORM_TRI     0x20u  /* staged word-pair form: three-lane window loads at any length   */
 #define FC2_BATCH_FORM_FIVE    0x40u  /* staged word-pair form: five-lane 8-B window loads at any length */
+#define FC2_BATCH_FORM_WAVE    0x80u  /* BASELINE north_star's shape: one wavefront per pair, windows and read
+                                         staged in LDS, lane = position x, ballot prefix sums, wave argmax
+                                         (needs wt and l + 2 <= 128; otherwise the default form runs) */
 
 /* ---- pairs that need byte-exact evaluation ------------------------------ */
 /* Block for pair k at arena[off[k]]: int32 lenI, lenA, lenB, then

@@ -24,7 +24,7 @@ from find_circ2_amd import _native as N  # noqa: E402
 from test_gpu_parity import genome, oracle_spans, run_spans  # noqa: E402
 
 # per-call form hints (fc2_batch_view.layout, include/fc2_bp.h): one drawn from each group per case
-HINTS = ((0, N.BATCH_FORM_STAGED, N.BATCH_FORM_PLAIN), (0, 0, N.BATCH_FORM_UNITS),
+HINTS = ((0, N.BATCH_FORM_STAGED, N.BATCH_FORM_PLAIN, N.BATCH_FORM_WAVE), (0, 0, N.BATCH_FORM_UNITS),
          (0, N.BATCH_FORM_TWOLANE, N.BATCH_FORM_TRI, N.BATCH_FORM_FIVE), (0, 0, N.BATCH_LOCUS_ORDERED))
 
 

@@ -28,7 +28,8 @@ FORMS = {"default": 0,
          "staged_words_five": N.BATCH_FORM_STAGED | N.BATCH_FORM_FIVE,
          "staged_units": N.BATCH_FORM_STAGED | N.BATCH_FORM_UNITS,
          "plain_words": N.BATCH_FORM_PLAIN,
-         "plain_units": N.BATCH_FORM_PLAIN | N.BATCH_FORM_UNITS}
+         "plain_units": N.BATCH_FORM_PLAIN | N.BATCH_FORM_UNITS,
+         "wave_per_pair": N.BATCH_FORM_WAVE}
 
 
 def _scan_form(opt, g, b, form):
@@ -83,7 +84,7 @@ def test_forms_agree_150bp(hg19):
     b = PairBatch.synthetic(opt, hg19, n, SynthConfig(seed=4242, len_min=120, len_max=150, span_max=20000))
     ref = None
     try:
-        for form in ("default", "staged_words_twolane", "staged_units", "plain_words", "plain_units"):
+        for form in ("default", "staged_words_twolane", "staged_units", "plain_words", "plain_units", "wave_per_pair"):
             out = _scan_form(opt, hg19, b, form)
             torch.cuda.synchronize()
             res = out.results[:n].clone()

@@ -23,11 +23,14 @@ from find_circ2_amd import _native as N  # noqa: E402
 from oracle.bp_oracle import Options as ROptions, RefIndexedFasta, Span, find_breakpoints  # noqa: E402
 
 
-@pytest.fixture(params=[N.BATCH_FORM_STAGED, N.BATCH_FORM_PLAIN], ids=["stage", "nostage"], autouse=True)
+@pytest.fixture(params=[N.BATCH_FORM_STAGED, N.BATCH_FORM_PLAIN, N.BATCH_FORM_WAVE], ids=["stage", "nostage", "wave"],
+                autouse=True)
 def scan_variant(request, monkeypatch):
     """Every parity case runs through both bp_scan32 forms: LDS-staged (chromosome table +
-    super-coarse N map) and unstaged (coarse map from L2), forced per call by the
-    FC2_BATCH_FORM_* hint in the batch view; the default picks per batch."""
+    super-coarse N map) and unstaged (coarse map from L2), and through the one-wavefront-per-pair
+    form of BASELINE's north_star (bp_wave_kernel; batches it cannot take -- no word-pair table,
+    l + 2 > 128 -- run the default form), forced per call by the FC2_BATCH_FORM_* hint in the batch
+    view; the default picks per batch."""
     orig = PairBatch.view
 
     def view(self):
