@@ -516,15 +516,17 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
     """configs[3]: ONE pair stream (the `n` pairs rank 0 scans in the weak run, seed 1337) cut into
     contiguous batches dealt round-robin to the ranks (shard.my_batches).  Rank 0 scans views of its
     own weak batch; every other rank generates only its batches of the stream (stream_share).  Each
-    batch's results are packed on the device into their 2-byte transfer form (fc2_result_compact_launch,
-    canonical mode) and copied to the batch's input offset of ONE node-local pinned host buffer
-    (shard.SharedCompactResults), which rank 0 then holds in input order: the host-side ordered merge
+    batch's scan writes its results in the 2-byte transfer form (canonical mode) straight to the batch's
+    input offset of ONE node-local page-locked host buffer (shard.SharedCompactResults) through the
+    buffer's device address (fc2_bp_scan_compact_launch: the words cross PCIe as the scan's epilogue
+    stores them), so rank 0 then holds every result in input order: the host-side ordered merge
     junction naming needs (find_circ.py:681-690, weights :544/:563/:579).  Timed: scans only; scans +
-    the 2-byte merge (pack, D2H into the shared buffer, a barrier per step, so rank 0 could consume
-    every step's merged results); and, for comparison, the same with the 4-byte form and with the raw
-    8-byte words.  Then checked passes: rank 0 poisons the buffer, every rank scans, packs and copies,
-    and the merged buffer expanded on the host (fc2_result_expand, what fc2_caller_submit_compact does
-    per chunk) must equal rank 0's single-rank scan of the whole stream word for word (both widths)."""
+    that merge (with a barrier per step, so rank 0 could consume every step's merged results); and,
+    for comparison, 8-byte scans whose results are packed to 2 or 4 bytes (fc2_result_compact_launch)
+    or left at 8 bytes and copied D2H on a side stream.  Then checked passes: rank 0 poisons the buffer,
+    every rank scans (and packs and copies), and the merged buffer expanded on the host
+    (fc2_result_expand, what fc2_caller_submit_compact does
+    per chunk) must equal rank 0's single-rank scan of the whole stream word for word (every form)."""
     import torch
     from find_circ2_amd import CompactResults, compact, scan
     from find_circ2_amd.hotpath import ScanOutput
@@ -557,7 +559,21 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
     host = {"scan": 0.0, "copy": 0.0, "calls": 0}   # host seconds in the launch calls (FC2_BENCH_HOST_TIMING)
     clock = time.perf_counter if os.environ.get("FC2_BENCH_HOST_TIMING") else None
 
-    def step(mode):                              # mode: None (scans only), 2, 4 (compact widths), 8 (raw)
+    # zero-copy form: the scan's epilogue writes each pair's 2-byte word straight into the shared
+    # host buffer (fc2_bp_scan_compact_launch through the buffer's device address), escapes into the
+    # batch's slots and the count into its slot: no 8-byte words, no pack launch, no copy
+    from find_circ2_amd.hotpath import host_device_pointer, scan_compact
+    zdev = host_device_pointer(merged[2].array.ctypes.data)
+    zblk = 16 * (cap + 1)
+    zctr = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in subs]
+
+    def step(mode):                              # mode: None (scans only), 2, 4 (compact widths), 8 (raw), "z"
+        if mode == "z":
+            for j, (k, lo, hi, s, res, comp) in enumerate(subs):
+                eb = zdev + merged[2]._w_bytes + k * zblk
+                scan_compact(opt, g, s, zdev + 2 * lo, 2, eb, cap, zctr[j].data_ptr(), eb + 16 * cap,
+                             stream=stream.cuda_stream)
+            return
         for j, (k, lo, hi, s, res, comp) in enumerate(subs):
             t0 = clock() if clock else 0.0
             scan(opt, g, s, out=ScanOutput(res, None, s.tw, s.stride), stream=stream.cuda_stream)
@@ -595,26 +611,27 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
         barrier(ws)
         return max_over_ranks(time.perf_counter() - t0, ws, dev)
 
-    for mode in (2, 4, 8):
+    for mode in (2, 4, 8, "z"):
         for _ in range(max(1, warmup)):
             step(mode)
     torch.cuda.synchronize(dev)
     scan_s = timed(None)
-    t = {mode: timed(mode) for mode in (2, 4, 8)}
-    # checked passes, one per width
+    t = {mode: timed(mode) for mode in (2, 4, 8, "z")}
+    # checked passes, one per width (and the zero-copy form, which lands in the 2-byte buffer)
     equal, n_esc = {}, {}
-    for w in widths:
+    for w in widths + ("z",):
+        m = merged[2 if w == "z" else w]
         if rank == 0:
-            merged[w].words[:] = 0x5A5A
-            merged[w].esc_count[:] = -1
+            m.words[:] = 0x5A5A
+            m.esc_count[:] = -1
         barrier(ws)
         step(w)
         torch.cuda.synchronize(dev)
         barrier(ws)
         if rank == 0:
             try:
-                equal[w] = bool(np.array_equal(merged[w].merged(opt), ref64))
-                n_esc[w] = int(merged[w].esc_count.sum())
+                equal[w] = bool(np.array_equal(m.merged(opt), ref64))
+                n_esc[w] = int(m.esc_count.sum())
             except Exception as ex:              # an overflowed escape area or a bad escape list
                 equal[w], n_esc[w] = repr(ex), None
     out = None
@@ -623,26 +640,34 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
             return {"value": round(n * steps / t[mode], 1), "ms_per_step": round(t[mode] / steps * 1e3, 4),
                     "merge_ms_per_step": round((t[mode] - scan_s) / steps * 1e3, 4)}
         out = {
-            "value": round(n * steps / t[2], 1), "unit": "anchor-pairs/s", "scaling": "strong",
-            "ms_per_step": round(t[2] / steps * 1e3, 4),
-            "scan_only": {"value": round(n * steps / scan_s, 1), "ms_per_step": round(scan_s / steps * 1e3, 4)},
-            "merge_ms_per_step": round((t[2] - scan_s) / steps * 1e3, 4),
-            "merge_bytes_per_pair": 2, "escapes": n_esc[2],
+            "value": round(n * steps / t["z"], 1), "unit": "anchor-pairs/s", "scaling": "strong",
+            "ms_per_step": round(t["z"] / steps * 1e3, 4),
+            "scan_only": {"value": round(n * steps / scan_s, 1), "ms_per_step": round(scan_s / steps * 1e3, 4),
+                          "note": "scans writing 8-byte results to HBM, no merge"},
+            "merge_ms_per_step": round((t["z"] - scan_s) / steps * 1e3, 4),
+            "merge_form": "zero_copy_2B: the scan's epilogue writes each pair's 2-byte word, the escapes and the "
+                          "batch's escape count straight into the shared page-locked buffer through its device "
+                          "address (fc2_bp_scan_compact_launch): no 8-byte results, pack launch or copy; a merge "
+                          "below 0 means that writing 2 B/pair over PCIe costs the scan less than the scans-only "
+                          "baseline's 8 B/pair to HBM",
+            "merge_bytes_per_pair": 2, "escapes": n_esc["z"],
+            "merge_2B_copied": dict(form(2), escapes=n_esc[2], merged_equals_single_rank=equal[2],
+                                    note="8-byte scan, pack launch, D2H copy on a side stream"),
             "merge_4B_words": dict(form(4), escapes=n_esc[4], merged_equals_single_rank=equal[4]),
             "merge_8B_words": form(8),
             "pairs_total": n, "batch_pairs": bsz, "n_batches": len(bounds), "ranks": ws, "tail_pieces": tail,
             "smallest_batch_pairs": min(hi - lo for lo, hi in bounds),
-            "merged_equals_single_rank": equal[2],
+            "merged_equals_single_rank": equal["z"],
             **({"host_ms_per_batch_2B": {"scan_and_pack_launch": round(host["scan"] / max(1, host["calls"]) * 1e3, 4),
                                          "copy_calls": round(host["copy"] / max(1, host["calls"]) * 1e3, 4)}}
                if clock else {}),
             "note": "one %d-pair stream in %d contiguous batches of up to %d pairs dealt round-robin to %d rank(s) "
                     "(with tail_pieces = t, each rank's last batch cut into t + 1 halving pieces), each rank "
-                    "holding only its batches; each batch's results packed on the device to 2 B/pair "
-                    "(fc2_result_compact_launch, canonical mode, escapes for the rest) and copied into a node-local "
-                    "pinned shared-memory buffer at their input offsets (host-side ordered merge, no collective on "
-                    "the data path); value = stream pairs / (scans + pack + merge + per-step barrier), max over "
-                    "ranks; merge_4B_words / merge_8B_words = the same with the 4-byte form / the raw 8-B words"
+                    "holding only its batches; each batch's scan writes its results as 2-byte words (canonical "
+                    "mode, escapes for the rest) straight into ONE node-local page-locked shared-memory buffer at "
+                    "their input offsets (host-side ordered merge, no collective on the data path); value = stream "
+                    "pairs / (scans + merge + per-step barrier), max over ranks; merge_2B_copied / merge_4B_words / "
+                    "merge_8B_words = 8-byte scans whose results are packed (2 or 4 B) or not and copied D2H"
                     % (n, len(bounds), bsz, ws)}
     barrier(ws)
     for m in merged.values():

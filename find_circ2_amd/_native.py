@@ -93,6 +93,11 @@ BATCH_FORM_FIVE = 0x40
 BATCH_FORM_WAVE = 0x80     # BASELINE north_star shape: one wavefront per pair (include/fc2_bp.h)
 
 
+class CompactOut(ctypes.Structure):        # fc2_compact_out
+    _fields_ = [("width", ctypes.c_int32), ("esc_cap", ctypes.c_uint32), ("words", ctypes.c_void_p),
+                ("esc", ctypes.c_void_p), ("esc_count", ctypes.c_void_p), ("count_out", ctypes.c_void_p)]
+
+
 class ReorderInfo(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("workspace_bytes", ctypes.c_uint64), ("shift", ctypes.c_uint32),
                 ("n_buckets", ctypes.c_uint32), ("bucket_bits", ctypes.c_uint32), ("n_chunks", ctypes.c_uint32),
@@ -117,7 +122,7 @@ EXPORTED = [
     "fc2_abi_version", "fc2_last_error", "fc2_device_count", "fc2_host_register", "fc2_host_unregister", "fc2_set_tuning", "fc2_get_tuning", "fc2_max_fast_l",
     "fc2_batch_geometry",
     "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch", "fc2_probe_pattern_launch",
-    "fc2_result_compact_launch", "fc2_result_expand",
+    "fc2_result_compact_launch", "fc2_result_expand", "fc2_bp_scan_compact_launch", "fc2_host_device_pointer",
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill", "fc2_window_geometry", "fc2_pack_windows",
@@ -206,6 +211,8 @@ def lib() -> ctypes.CDLL:
         "fc2_probe_pattern_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp]),
         "fc2_result_compact_launch": (ctypes.c_int, [P(Params), vp, u64, ctypes.c_int, vp, vp, u32, vp, vp]),
         "fc2_result_expand": (ctypes.c_int, [P(Params), vp, ctypes.c_int, u64, vp, u64, vp, ctypes.c_int]),
+        "fc2_bp_scan_compact_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), P(CompactOut), vp]),
+        "fc2_host_device_pointer": (ctypes.c_int, [vp, P(vp)]),
         "fc2_fasta_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(vp)]),
         "fc2_fasta_close": (None, [vp]),
         "fc2_fasta_n_chrom": (ctypes.c_int, [vp]),

@@ -820,12 +820,13 @@ inline int long_window_form(uint32_t layout, int ml) {
 // ===========================================================================
 // C ABI: launches
 // ===========================================================================
-extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
-                                  fc2_result *results, uint64_t *tiemask, uint32_t tw, void *stream) {
-    int rc = fc2::validate_params(p);
-    if (rc) return rc;
-    if (!g || !b || !results) return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: null argument");
-    if (b->n == 0) return FC2_OK;
+namespace {
+// fc2_bp_scan_launch / fc2_bp_scan_compact_launch: argument checks and the choice of kernel form.
+// sv carries the caller's view (and, for the compact launch, where the epilogue writes); out is the
+// 8-byte result array (unused by a compact launch's scan kernels).
+int scan_dispatch(const fc2_params *p, const fc2_genome_view *g, const fc2::ScanView &sv, uint64_t *out,
+                  uint64_t *tiemask, uint32_t tw, void *stream) {
+    const fc2_batch_view *b = &sv;
     if (!b->pairs || !b->read_words || b->stride < b->n || b->rw == 0)
         return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: bad batch view");
     const bool carried = b->win_words != nullptr;   // window-carrying batch: no genome gather
@@ -844,18 +845,17 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: read rows too narrow for max_l");
     hipStream_t s = (hipStream_t)stream;
     const unsigned grid = grid_for(b->n, kBlock);
-    uint64_t *out = reinterpret_cast<uint64_t *>(results);
     const bool nt = stream_nt();
     if (carried) {
         const uint32_t pw = (uint32_t)((ml + 2 + 31) / 32);
         if (ml + 2 > 128) return fc2::fail(FC2_E_RANGE, "fc2_bp_scan_launch: window rows carry l + 2 <= 128 only");
         if (b->ww < 2 * pw || (b->win_nwords && b->wnw < pw) || !b->win_nwords)
             return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: window rows too narrow for max_l");
-        fc2::launch_scan32_win((int)pw, nt, s, *p, *g, *b, out, tiemask, tw);
+        fc2::launch_scan32_win((int)pw, nt, s, *p, *g, sv, out, tiemask, tw);
         return hip_check(hipGetLastError(), "bp_scan32_win_kernel launch");
     }
     if ((b->layout & FC2_BATCH_FORM_WAVE) && fc2::wave_ok(ml, *g)) {
-        fc2::launch_wave(s, *p, *g, *b, out, tiemask, tw);
+        fc2::launch_wave(s, *p, *g, sv, out, tiemask, tw);
         return hip_check(hipGetLastError(), "bp_wave_kernel launch");
     }
     if (g_kernel32) {
@@ -876,20 +876,21 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
         const int opts = sw ? fc2::kOptSwizzle : 0;
         const int nq = (ml + 2 + 31) / 32;
         if (stage && (g_stage_block != 256 || tri) && g_persist == 0 && fc2::stage_bt_ok(nq, gv)) {
-            fc2::launch_scan32_stage_bt(g_stage_block, tri, nt, s, *p, gv, *b, out, tiemask, tw);
+            fc2::launch_scan32_stage_bt(g_stage_block, tri, nt, s, *p, gv, sv, out, tiemask, tw);
             return hip_check(hipGetLastError(), "bp_scan32_stage_bt_kernel launch");
         }
 #if FC2_AB_FORMS
         if (stage && g_persist != 0 && fc2::persist_ok(nq, gv)) {
-            fc2::launch_scan32_persist(nt, s, *p, gv, *b, out, tiemask, tw, g_persist < 0 ? 0 : g_persist);
+            fc2::launch_scan32_persist(nt, s, *p, gv, sv, out, tiemask, tw, g_persist < 0 ? 0 : g_persist);
             return hip_check(hipGetLastError(), "bp_scan32_persist_kernel launch");
         }
 #endif
-        fc2::launch_scan32((ml + 2 + 31) / 32, nt, opts, stage, grid, s, *p, gv, *b, out, tiemask, tw,
+        fc2::launch_scan32((ml + 2 + 31) / 32, nt, opts, stage, grid, s, *p, gv, sv, out, tiemask, tw,
                            (unsigned)g_extra_lds);
         return hip_check(hipGetLastError(), "bp_scan32_kernel launch");
     }
 #if FC2_AB_FORMS
+    if (sv.c_words) return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_compact_launch: not with the 64-bit kernel (FC2_TUNE_KERNEL32 0)");
 #define FC2_LAUNCH(NWV, NTV) \
     hipLaunchKernelGGL((bp_scan_kernel<NWV, NTV>), dim3(grid), dim3(kBlock), 0, s, *p, *g, *b, out, tiemask, tw)
     if (nwords <= 2) { if (nt) FC2_LAUNCH(2, true); else FC2_LAUNCH(2, false); }
@@ -902,6 +903,50 @@ extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g,
     (void)nwords;
     return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: unreachable form");
 #endif
+}
+
+__global__ void compact_count_move_kernel(uint32_t *count, uint32_t *out) {
+    *out = *count;
+    *count = 0u;
+}
+
+}  // namespace
+
+extern "C" int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                                  fc2_result *results, uint64_t *tiemask, uint32_t tw, void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (!g || !b || !results) return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_launch: null argument");
+    if (b->n == 0) return FC2_OK;
+    return scan_dispatch(p, g, fc2::ScanView(*b), reinterpret_cast<uint64_t *>(results), tiemask, tw, stream);
+}
+
+extern "C" int fc2_bp_scan_compact_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                                          const fc2_compact_out *co, void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (!g || !b || !co) return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_compact_launch: null argument");
+    if (p->noncanonical || p->allhits)
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_compact_launch: canonical mode without --all-hits only");
+    if (co->width != 2 && co->width != 4) return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_compact_launch: width is 2 or 4");
+    if (!co->esc_count || (b->n && !co->words) || (co->esc_cap && !co->esc))
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_compact_launch: bad output");
+    if (b->n) {
+        fc2::ScanView sv(*b);
+        sv.c_words = co->words;
+        sv.c_esc = co->esc;
+        sv.c_count = co->esc_count;
+        sv.c_cap = co->esc_cap;
+        sv.c_width = co->width;
+        rc = scan_dispatch(p, g, sv, nullptr, nullptr, 0, stream);
+        if (rc) return rc;
+    }
+    if (co->count_out) {
+        hipLaunchKernelGGL(compact_count_move_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, co->esc_count,
+                           co->count_out);
+        return hip_check(hipGetLastError(), "compact_count_move_kernel launch");
+    }
+    return FC2_OK;
 }
 
 extern "C" int fc2_gather_windows_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
@@ -1153,8 +1198,15 @@ extern "C" int fc2_device_count(int *count) {
 
 extern "C" int fc2_host_register(void *ptr, uint64_t bytes) {
     if (!ptr || !bytes) return fc2::fail(FC2_E_PARAM, "fc2_host_register: empty range");
-    const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterPortable);
+    const hipError_t e = hipHostRegister(ptr, (size_t)bytes, hipHostRegisterPortable | hipHostRegisterMapped);
     if (e != hipSuccess) return fc2::fail(FC2_E_HIP, std::string("hipHostRegister: ") + hipGetErrorString(e));
+    return FC2_OK;
+}
+
+extern "C" int fc2_host_device_pointer(void *host, void **dev) {
+    if (!host || !dev) return fc2::fail(FC2_E_PARAM, "fc2_host_device_pointer: null argument");
+    const hipError_t e = hipHostGetDevicePointer(dev, host, 0);
+    if (e != hipSuccess) return fc2::fail(FC2_E_HIP, std::string("hipHostGetDevicePointer: ") + hipGetErrorString(e));
     return FC2_OK;
 }
 

@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include "fc2_common.h"
+#include "fc2_compact.h"
 #include "fc2_scan32.h"
 
 namespace {
@@ -62,6 +63,27 @@ __device__ __forceinline__ void st_stream(uint64_t *p, uint64_t v) {
     if constexpr (NT) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
+// A pair's result: the 8-byte word to out[i], or (fc2_bp_scan_compact_launch) its compact word to
+// bv.c_words[i] with an escape through the device counter when it does not fit (fc2_compact.h)
+template <bool NT>
+__device__ __forceinline__ void emit(const fc2::ScanView &bv, uint64_t *out, uint64_t i, uint64_t w) {
+    if (bv.c_words) {
+        bool esc;
+        const uint32_t c = fc2::compact_pack(w, bv.c_width, esc);
+        if (esc) {
+            const uint32_t k = atomicAdd(bv.c_count, 1u);
+            if (k < bv.c_cap) {
+                bv.c_esc[k].index = i;
+                __builtin_memcpy(&bv.c_esc[k].result, &w, sizeof w);
+            }
+        }
+        if (bv.c_width == 2) __builtin_nontemporal_store((uint16_t)c, (uint16_t *)bv.c_words + i);
+        else __builtin_nontemporal_store(c, (uint32_t *)bv.c_words + i);
+    } else {
+        st_stream<NT>(out + i, w);
+    }
+}
+
 template <bool NT>
 __device__ __forceinline__ u64x2 ld_pair_raw(const fc2_pair *p) {
     if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
@@ -843,7 +865,7 @@ __device__ __forceinline__ uint64_t xcd_block(uint32_t b, uint32_t nwg) {
 // PW > 0: window-carrying batch (fc2_batch_view.win_words, pw = PW): the windows arrive with the
 // record in round trip 1 and nothing is gathered from the genome (NQ == 4, !COOP, !WL).
 template <int NQ, bool NT, bool COOP, bool WL = false, int PW = 0, int TRI = 0>
-__device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &bv,
+__device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_view &g, const fc2::ScanView &bv,
                                           uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask, uint32_t tw,
                                           uint64_t i, const uint64_t *s_cstart, const int64_t *s_csize, bool lds_tab,
                                           const uint32_t *s_nsuper, ulonglong2 *xchg) {
@@ -903,7 +925,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
         // skipped / empty x-range: no hit; anything else is routed to the byte path by the host
         const bool err = !(pr.flags & FC2_PAIR_SKIP) && l >= 0;
         Best32 none;
-        st_stream<NT>(out + i, pack_result(none, 0, err ? FC2_RES_ERR_WIN : 0u));
+        emit<NT>(bv, out, i, pack_result(none, 0, err ? FC2_RES_ERR_WIN : 0u));
         if (want_ties)
             for (uint32_t k = 0; k < tw; ++k) tiemask[(uint64_t)k * bv.stride + i] = 0;
         if (!COOP) return;
@@ -1154,7 +1176,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
                      (code_at32<NQ>(B, x + 1) << 9);
         }
     }
-    st_stream<NT>(out + i, pack_result(Bst, gtag12, 0));
+    emit<NT>(bv, out, i, pack_result(Bst, gtag12, 0));
 
     if (want_ties) {
         // --all-hits: every tie (find_circ.py:966-974); tie words are 64-bit, x-major
@@ -1207,7 +1229,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
 // which is cheaper when the batch is locus-ordered or the genome is cache-resident (the kernel is
 // then VALU-bound and the staging's registers and barrier cost more than they save).
 template <int NQ, bool NT, bool STAGE>
-__global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+__global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_genome_view g, fc2::ScanView bv,
                                                            uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
                                                            uint32_t tw, int opts) {
     const bool swizzle = opts & fc2::kOptSwizzle;
@@ -1274,7 +1296,7 @@ __global__ __launch_bounds__(kBlock) void bp_scan32_kernel(fc2_params p, fc2_gen
 // the record -- the design BASELINE.json's north_star sketches (windows gathered on the host
 // from the mmap'd FASTA).  No genome gather, no LDS.
 template <int PW, bool NT>
-__global__ __launch_bounds__(kBlock) void bp_scan32_win_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+__global__ __launch_bounds__(kBlock) void bp_scan32_win_kernel(fc2_params p, fc2_genome_view g, fc2::ScanView bv,
                                                                uint64_t *__restrict__ out,
                                                                uint64_t *__restrict__ tiemask, uint32_t tw) {
     const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -1348,7 +1370,7 @@ __global__ __launch_bounds__(kBlock) void gather_windows_kernel(fc2_params p, fc
 // The STAGE + cooperative word-pair form with BT-thread blocks (FC2_TUNE_STAGE_BLOCK): the LDS
 // tables are staged once per BT pairs instead of once per 256 (each staging is ~60 L2 requests).
 template <int BT, bool NT, int TRI>
-__global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+__global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc2_genome_view g, fc2::ScanView bv,
                                                                 uint64_t *__restrict__ out,
                                                                 uint64_t *__restrict__ tiemask, uint32_t tw) {
     __shared__ uint64_t s_cstart[kChromLds];
@@ -1380,7 +1402,7 @@ __global__ __launch_bounds__(BT) void bp_scan32_stage_bt_kernel(fc2_params p, fc
 // barrier before the block's first window request.  The loop bound is uniform per block.
 template <bool NT>
 __global__ __launch_bounds__(kBlock) void bp_scan32_persist_kernel(fc2_params p, fc2_genome_view g,
-                                                                   fc2_batch_view bv, uint64_t *__restrict__ out,
+                                                                   fc2::ScanView bv, uint64_t *__restrict__ out,
                                                                    uint64_t *__restrict__ tiemask, uint32_t tw,
                                                                    uint64_t n_tiles) {
     constexpr int NQ = 4;
@@ -1555,7 +1577,7 @@ __device__ __forceinline__ fc2_pair wave_record(const uint32_t *P) {
     return pr;
 }
 
-__global__ __launch_bounds__(kBlock) void bp_wave_kernel(fc2_params p, fc2_genome_view g, fc2_batch_view bv,
+__global__ __launch_bounds__(kBlock) void bp_wave_kernel(fc2_params p, fc2_genome_view g, fc2::ScanView bv,
                                                          uint64_t *__restrict__ out, uint64_t *__restrict__ tiemask,
                                                          uint32_t tw) {
     __shared__ uint32_t s_w[(kBlock / 64) * kWavePairs * kWaveSlot];
@@ -1813,7 +1835,7 @@ __global__ __launch_bounds__(kBlock) void bp_wave_kernel(fc2_params p, fc2_genom
             tiemask[(uint64_t)j * bv.stride + i] = w < 2 ? (s ? t1 : t0) : 0ull;
         }
     }
-    if (mine) out[i0 + lane] = myres;
+    if (mine) emit<false>(bv, out, i0 + lane, myres);
 }
 
 }  // namespace
@@ -1828,7 +1850,7 @@ int launch_probe_pattern(hipStream_t s, const fc2_params &p, const fc2_genome_vi
 }
 
 void launch_scan32_win(int pw, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
-                       const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
+                       const ScanView &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
     const unsigned grid = (unsigned)((b.n + kBlock - 1) / kBlock);
 #if FC2_AB_FORMS
 #define FC2_LW(PWV)                                                                                          \
@@ -1871,7 +1893,7 @@ bool wave_ok(int ml, const fc2_genome_view &g) {
     return ml + 2 <= 128 && !g.dummy && g.wt && g.wt_bytes && g.chrom_start && g.chrom_size && g.nplane;
 }
 
-void launch_wave(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out,
+void launch_wave(hipStream_t s, const fc2_params &p, const fc2_genome_view &g, const ScanView &b, uint64_t *out,
                  uint64_t *tiemask, uint32_t tw) {
     constexpr uint64_t per_block = (kBlock / 64) * kWavePairs;
     hipLaunchKernelGGL(bp_wave_kernel, dim3((unsigned)((b.n + per_block - 1) / per_block)), dim3(kBlock), 0, s, p, g, b,
@@ -1884,7 +1906,7 @@ bool stage_bt_ok(int nq, const fc2_genome_view &g) {
 }
 
 void launch_scan32_stage_bt(int bt, int tri, bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
-                            const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
+                            const ScanView &b, uint64_t *out, uint64_t *tiemask, uint32_t tw) {
 #if FC2_AB_FORMS
 #define FC2_LBT(BTV, TRV)                                                                                     \
     do {                                                                                                      \
@@ -1928,7 +1950,7 @@ bool persist_ok(int nq, const fc2_genome_view &g) {
 }
 
 void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc2_genome_view &g,
-                           const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw, int blocks_per_cu) {
+                           const ScanView &b, uint64_t *out, uint64_t *tiemask, uint32_t tw, int blocks_per_cu) {
     static int cus = 0, occ[2] = {0, 0};
     if (!cus) {
         int dev = 0;
@@ -1958,7 +1980,7 @@ void launch_scan32_persist(bool nt, hipStream_t s, const fc2_params &p, const fc
 #endif
 
 void launch_scan32(int nq, bool nt, int opts, bool stage, unsigned grid, hipStream_t s, const fc2_params &p,
-                   const fc2_genome_view &g, const fc2_batch_view &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
+                   const fc2_genome_view &g, const ScanView &b, uint64_t *out, uint64_t *tiemask, uint32_t tw,
                    unsigned extra_lds) {
 #define FC2_L32(NQV, NTV, STV)                                                                                   \
     hipLaunchKernelGGL((bp_scan32_kernel<NQV, NTV, STV>), dim3(grid), dim3(kBlock), extra_lds, s, p, g, b, out, tiemask, \

@@ -428,6 +428,33 @@ def compact(options: Options, results, n: int, into: CompactResults = None, stre
     return c
 
 
+def host_device_pointer(host_ptr: int) -> int:
+    """The device address of page-locked host memory (fc2_host_register'ed or pinned)."""
+    d = ctypes.c_void_p()
+    N.check(N.lib().fc2_host_device_pointer(host_ptr, ctypes.byref(d)))
+    return d.value
+
+
+def scan_compact(options: Options, genome: Genome, batch: "PairBatch", words: int, width: int, esc: int, cap: int,
+                 esc_count: int, count_out: int = None, stream=None) -> None:
+    """``find_breakpoints`` for every pair of ``batch`` with the results written by the scan itself in
+    a compact form (``fc2_bp_scan_compact_launch``): ``words`` / ``esc`` are device addresses (device
+    memory, or page-locked host memory through ``host_device_pointer``: the words then cross PCIe as
+    the scan writes them), ``esc_count`` a device int32 that is zero before the launch and is moved to
+    ``count_out`` (and zeroed) after it when that is given.  Canonical mode without --all-hits; a
+    batch with byte-path pairs is refused (their results are 8-byte words from the byte kernel)."""
+    torch = _torch()
+    if batch.m_bytepath:
+        raise ValueError("scan_compact: the batch has %d byte-path pairs" % batch.m_bytepath)
+    s = stream if stream is not None else torch.cuda.current_stream(batch.device).cuda_stream
+    p = options.params()
+    gv = genome.view()
+    bv = batch.view()
+    co = N.CompactOut(width, cap, words, esc, esc_count, count_out)
+    N.check(N.lib().fc2_bp_scan_compact_launch(ctypes.byref(p), ctypes.byref(gv), ctypes.byref(bv), ctypes.byref(co),
+                                               s))
+
+
 def expand(options: Options, words: np.ndarray, esc: np.ndarray, out: np.ndarray = None,
            n_threads: int = 0) -> np.ndarray:
     """Host: the 8-byte result words (int64) back from compact words (a 4-byte dtype: width 4, a

@@ -128,6 +128,9 @@ typedef struct fc2_result_escape {
 } fc2_result_escape;
 int fc2_result_compact_launch(const fc2_params *p, const fc2_result *results, uint64_t n, int width, void *words,
                               fc2_result_escape *esc, uint32_t esc_cap, uint32_t *esc_count, void *stream);
+/* The device address of page-locked host memory registered with fc2_host_register (or allocated
+ * page-locked): what a kernel writes through to reach it. */
+int fc2_host_device_pointer(void *host, void **dev);
 /* Host: the 8-byte results back from words[n] (width 4 or 2) and the n_esc escapes (indices < n),
  * on n_threads threads (<= 0: all cores, at most 64).  FC2_E_FORMAT if the escapes do not match
  * the escaped words one to one. */
@@ -310,6 +313,25 @@ int         fc2_batch_geometry(const fc2_params *p, int32_t max_read_len,
 int fc2_bp_scan_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
                        fc2_result *results, uint64_t *tiemask, uint32_t tw, void *stream);
 
+/* The scan writing its results straight in a compact form (no 8-byte words, no pack launch, no
+ * copy): every pair's word goes to words[i] from the scan's own epilogue, escapes to esc[] through
+ * the device counter *esc_count.  words and esc may be page-locked host memory mapped into the device
+ * (fc2_host_register + fc2_host_device_pointer): the results then cross PCIe as the scan produces
+ * them, which is the ordered merge of a strong-scaled stream without a copy.  *esc_count must be
+ * zero before the launch; with count_out != NULL a one-thread kernel after the scan moves the count
+ * there (host memory allowed) and zeroes *esc_count again, ready for the next launch.  Canonical
+ * mode without --all-hits only, and the batch must hold no FC2_PAIR_BYTEPATH pair (their results
+ * come from fc2_bp_scan_bytes_launch as 8-byte words).  Otherwise as fc2_bp_scan_launch. */
+typedef struct fc2_compact_out {
+    int32_t  width;              /* 2 or 4 */
+    uint32_t esc_cap;
+    void    *words;              /* [n] uint16 / uint32 */
+    fc2_result_escape *esc;      /* [esc_cap] */
+    uint32_t *esc_count;         /* device memory */
+    uint32_t *count_out;         /* or NULL */
+} fc2_compact_out;
+int fc2_bp_scan_compact_launch(const fc2_params *p, const fc2_genome_view *g, const fc2_batch_view *b,
+                               const fc2_compact_out *co, void *stream);
 /* Byte-exact evaluation of the pairs listed in v (any read length, any bytes). */
 int fc2_bp_scan_bytes_launch(const fc2_params *p, const fc2_bytes_view *v, fc2_result *results,
                              uint64_t *tiemask, uint32_t tw, uint64_t stride, void *stream);

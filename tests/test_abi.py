@@ -359,3 +359,25 @@ def test_ctx_arguments_without_a_device(L):
     assert L.fc2_ctx_genome_load(None, None, 0) == N.FC2_E_PARAM
     assert L.fc2_ctx_last_error(None) == b""
     L.fc2_ctx_destroy(None)
+
+
+def test_compact_scan_arguments_without_a_device(L):
+    """fc2_bp_scan_compact_launch / fc2_host_device_pointer check their arguments before any HIP call:
+    the compact forms are canonical-mode only, without --all-hits, width 2 or 4."""
+    gv, bv = N.GenomeView(), N.BatchView()
+    co = N.CompactOut(2, 0, None, None, None, None)
+    assert L.fc2_bp_scan_compact_launch(ctypes.byref(N.Params(15, 2, 2, 0, 0, 0, 0)), None, ctypes.byref(bv),
+                                        ctypes.byref(co), None) == N.FC2_E_PARAM
+    for nc, ah in ((1, 0), (0, 1)):
+        p = N.Params(15, 2, 2, nc, 0, ah, 0)
+        assert L.fc2_bp_scan_compact_launch(ctypes.byref(p), ctypes.byref(gv), ctypes.byref(bv), ctypes.byref(co),
+                                            None) == N.FC2_E_PARAM
+    p = N.Params(15, 2, 2, 0, 0, 0, 0)
+    for width in (0, 3, 8):
+        bad = N.CompactOut(width, 0, None, None, None, None)
+        assert L.fc2_bp_scan_compact_launch(ctypes.byref(p), ctypes.byref(gv), ctypes.byref(bv), ctypes.byref(bad),
+                                            None) == N.FC2_E_PARAM
+    assert L.fc2_bp_scan_compact_launch(ctypes.byref(p), ctypes.byref(gv), ctypes.byref(bv), ctypes.byref(co),
+                                        None) == N.FC2_E_PARAM     # no esc_count
+    d = ctypes.c_void_p()
+    assert L.fc2_host_device_pointer(None, ctypes.byref(d)) == N.FC2_E_PARAM

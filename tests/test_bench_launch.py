@@ -71,6 +71,7 @@ def test_two_ranks_configs3_and_configs4_on_hg19():
         assert line["n_gpus"] == ranks and st["ranks"] == ranks and st["pairs_total"] == 8_000_000
         assert st["merged_equals_single_rank"] is True
         assert st["merge_bytes_per_pair"] == 2 and st["merge_4B_words"]["merged_equals_single_rank"] is True
+        assert st["merge_2B_copied"]["merged_equals_single_rank"] is True
         c4 = line["configs4_200M_150bp"]
         assert c4["ranks"] == ranks and c4["pairs_total"] == 8_000_000
     assert one["configs4_200M_150bp"]["results_checksum"] == two["configs4_200M_150bp"]["results_checksum"]

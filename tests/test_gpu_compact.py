@@ -70,3 +70,85 @@ def test_escape_overflow_is_reported():
     assert cap == 16 and k > cap
     with pytest.raises(Exception):
         expand(Options(), got, esc)
+
+
+# --- the scan writing the compact form itself (fc2_bp_scan_compact_launch) ------------------------
+
+def _compact_scan(opt, g, b, width, cap, host):
+    """Run scan_compact into device memory or into page-locked host memory (through its device
+    address); return words, escapes sorted by index, the moved count, and the device counter after."""
+    import mmap
+    from find_circ2_amd.hotpath import host_device_pointer, scan_compact
+    dev = _dev()
+    n = b.n
+    wbytes = (width * n + 63) // 64 * 64
+    size = wbytes + 16 * (cap + 1)
+    ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+    if host:
+        mm = mmap.mmap(-1, size)
+        buf = np.frombuffer(mm, np.uint8)
+        buf[:] = 0xA5
+        N.check(N.lib().fc2_host_register(buf.ctypes.data, size))
+        base = host_device_pointer(buf.ctypes.data)
+    else:
+        dbuf = torch.full((size,), 0xA5, dtype=torch.uint8, device=dev)
+        base = dbuf.data_ptr()
+    try:
+        scan_compact(opt, g, b, base, width, base + wbytes, cap, ctr.data_ptr(), base + wbytes + 16 * cap)
+        torch.cuda.synchronize(dev)
+        raw = buf.copy() if host else dbuf.cpu().numpy()
+    finally:
+        if host:
+            N.lib().fc2_host_unregister(buf.ctypes.data)
+            del buf
+            mm.close()
+    words = raw[:width * n].view(np.uint16 if width == 2 else np.uint32)
+    k = int(raw[wbytes + 16 * cap:wbytes + 16 * cap + 4].view(np.int32)[0])
+    esc = raw[wbytes:wbytes + 16 * cap].view(N.ESCAPE_DTYPE)[:min(k, cap)]
+    return words, np.sort(esc, order="index"), k, int(ctr.item())
+
+
+@pytest.mark.parametrize("host", [False, True], ids=["device_memory", "host_memory"])
+@pytest.mark.parametrize("width", [2, 4])
+def test_compact_scan_equals_pack_of_the_scan(width, host):
+    """The scan's own compact epilogue writes the words and escapes the packer writes from the
+    8-byte scan (escape-heavy spans: long reads, -d 6), into device memory or straight into
+    page-locked host memory; the count moves to its slot and the device counter is zero again."""
+    path = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    opt = Options(maxdist=6, margin=0)
+    spans = make_spans(load_genome(path), 6000, seed=606, asize=opt.asize, L=(60, 300), p_readN=0.05)
+    g = genome(path)
+    b, out = run_spans(opt, g, spans)
+    assert b.m_bytepath == 0
+    res = out.results[:b.n].cpu().numpy()
+    exp_words, exp_esc, exp_k, _ = _device_form(opt, res, width, cap=b.n)
+    words, esc, k, ctr = _compact_scan(opt, g, b, width, b.n, host)
+    assert ctr == 0
+    assert k == exp_k and (width == 4 or k > 100)
+    assert np.array_equal(words, exp_words.view(words.dtype))
+    assert np.array_equal(esc["index"], exp_esc["index"])
+    assert np.array_equal(esc["result"].view(np.int64), exp_esc["result"].view(np.int64))
+    assert np.array_equal(expand(opt, words, esc), res)
+
+
+def test_compact_scan_hg19_shaped_batch_and_refusals():
+    """A read-order batch on the hg19-shaped genome (the staged headline form): the 2-byte words from
+    the scan equal the packer's, 0 escapes; --non-canonical / --all-hits are refused."""
+    from find_circ2_amd import Genome, PairBatch, SynthConfig, scan, sq_table
+    from find_circ2_amd.hotpath import scan_compact
+    dev = _dev()
+    names, sizes = sq_table(os.path.join(GOLDEN, "test_norm.sam"))
+    g = Genome.synthetic(names, sizes, seed=4711, device=dev)
+    opt = Options()
+    b = PairBatch.synthetic(opt, g, 2_000_000, SynthConfig(seed=77, span_max=20000))
+    res = scan(opt, g, b).results[:b.n]
+    torch.cuda.synchronize(dev)
+    exp_words, exp_esc, exp_k, _ = _device_form(opt, res.cpu().numpy(), 2)
+    words, esc, k, ctr = _compact_scan(opt, g, b, 2, 4096, host=True)
+    assert k == exp_k == 0 and ctr == 0
+    assert np.array_equal(words, exp_words.view(words.dtype))
+    ctr_t = torch.zeros(1, dtype=torch.int32, device=dev)
+    buf = torch.empty(2 * b.n, dtype=torch.uint8, device=dev)
+    for bad in (Options(noncanonical=True), Options(allhits=True)):
+        with pytest.raises(Exception):
+            scan_compact(bad, g, b, buf.data_ptr(), 2, 0, 0, ctr_t.data_ptr())
