@@ -81,3 +81,20 @@ def test_random_options_and_kernel_forms(seed, form_hint):
             assert [(t.start, t.end, t.strand, t.gtag, int(t.dist), t.ov, t.n_hits) for t in ties] == \
                 [(int(x["start"]), int(x["end"]), x["strand"].decode(), x["gtag"].decode(), int(x["dist"]),
                   int(x["ov"]), int(x["n_hits"])) for x in exp], (label, i)
+    if not opt.noncanonical and not opt.allhits and b.m_bytepath == 0:
+        # the same scan writing the compact forms itself (fc2_bp_scan_compact_launch, same form hints):
+        # the words and escapes expand back to the 8-byte results, which equal the oracle's (above)
+        from find_circ2_amd import expand
+        from find_circ2_amd.hotpath import scan_compact
+        res = out.results[:b.n].cpu().numpy()
+        for width in (2, 4):
+            dev = torch.device("cuda", 0)
+            words = torch.empty(width * b.n, dtype=torch.uint8, device=dev)
+            esc = torch.zeros(16 * b.n, dtype=torch.uint8, device=dev)
+            ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+            scan_compact(opt, g, b, words.data_ptr(), width, esc.data_ptr(), b.n, ctr.data_ptr())
+            torch.cuda.synchronize(dev)
+            k = int(ctr.item())
+            w = words.cpu().numpy().view(np.uint16 if width == 2 else np.uint32)
+            e = esc.cpu().numpy().view(N.ESCAPE_DTYPE)[:k]
+            assert np.array_equal(expand(opt, w, e), res), (label, width)
