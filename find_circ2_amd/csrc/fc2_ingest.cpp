@@ -824,8 +824,10 @@ int read_header(fc2_ingest *h) {
 }
 
 // splitter: the input from where the header ended, in newline-aligned numbered blocks
-void sam_split_loop(fc2_ingest *h) {
-    auto &A = *h->ahead;
+// (A is handed over, not read from h->ahead: closing resets h->ahead before ~SamAhead joins, and a
+// thread that only starts running then must still find its object)
+void sam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
+    auto &A = *ap;
     std::string carry(h->buf.data() + h->beg, h->end - h->beg);   // bytes read with the header
     h->beg = h->end;
     bool in_eof = h->eof_in;
@@ -895,8 +897,8 @@ void sam_split_loop(fc2_ingest *h) {
 }
 
 // parser: blocks to record batches (own RNAME cache and CIGAR scratch)
-void sam_parse_loop(fc2_ingest *h) {
-    auto &A = *h->ahead;
+void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
+    auto &A = *ap;
     fc2_ingest::ParseScratch ps;
     for (;;) {
         std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
@@ -1301,9 +1303,10 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
     if (h->need_text) h->need_text = false;     // (written once: the parse thread reads it)
     // plain SAM text: parsed on threads of their own (compressed SAM stays on the sequential reader)
     if (!h->ahead && !h->bam && h->src == fc2_ingest::SRC_RAW && !h->bam_out && !h->finished) {
-        h->ahead.reset(new fc2_ingest::SamAhead());
-        h->ahead->splitter = std::thread(sam_split_loop, h);
-        for (int k = 0; k < fc2_ingest::SamAhead::kParsers; ++k) h->ahead->parsers.emplace_back(sam_parse_loop, h);
+        fc2_ingest::SamAhead *ap = new fc2_ingest::SamAhead();
+        h->ahead.reset(ap);
+        ap->splitter = std::thread(sam_split_loop, h, ap);
+        for (int k = 0; k < fc2_ingest::SamAhead::kParsers; ++k) ap->parsers.emplace_back(sam_parse_loop, h, ap);
     }
     return run_loop(h, p, max_frags, &sink, nullptr, eof);
 }

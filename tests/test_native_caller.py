@@ -556,3 +556,26 @@ def test_native_caller_compact_results_equal_raw(tmp_path, extra, width):
     assert cli.main(["-G", fa, "-o", o2, "-q"] + extra + [sam], evaluator_factory=compact_factory(width)) == 0
     same(o1, o2)
     assert sum(1 for l in open(os.path.join(o2, "circ_splice_sites.bed")) if l[0] != "#") > 10
+
+
+def test_native_caller_close_before_parse_threads_run(tmp_path):
+    """Closing right after the first pull on a tiny SAM input: the parse-ahead threads may only
+    start running once close has begun (which resets the handle's pointer to them before joining);
+    they must not reach the object through that pointer.  Repeated so the window is hit (the bug
+    crashed about 1 run in 200 under load)."""
+    import ctypes
+    from find_circ2_amd import _native as N
+    from find_circ2_amd.caller import CallerOptions
+    from find_circ2_amd.native_caller import NativeCaller
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    for k, body in enumerate(["\n\n", "", "u1\t4\t*\t0\t0\t*\t*\t0\t0\tACGT\t####\n"]):
+        sam = str(tmp_path / ("d%d.sam" % k))
+        open(sam, "w").write("@SQ\tSN:testbed_plus\tLN:720\n" + body)
+        for _ in range(400):
+            nc = NativeCaller(sam, False, CallerOptions(), ["testbed_plus"], write_reads=False,
+                              write_multi=False, genome_dummy=True)
+            nc.open()
+            batch, eof = N.CallerBatch(), ctypes.c_int(0)
+            rc = N.lib().fc2_caller_next(nc.h, ctypes.byref(batch), ctypes.byref(eof))
+            assert rc == (N.FC2_OK if k < 2 else rc)   # one record: the reference's UnboundLocalError
+            nc.close()
