@@ -43,6 +43,16 @@ def algo_bytes_per_pair(L: int, asize: int = 15, margin: int = 2) -> int:
     return -(-l // 4) + 2 * (-(-(l + 2) // 4)) + 16 + 8
 
 
+def mean_algo_bytes(b, asize: int, margin: int) -> float:
+    """B(L) of SURVEY.md 8(d) averaged over a batch's own read_part lengths (variable-length batches:
+    configs[4]'s 120..150 bp reads and its shorter three-segment pairs)."""
+    import torch
+    L = b.pairs[:16 * b.n].view(b.n, 16)[:, 12:14].contiguous().view(torch.int16).to(torch.int64).flatten()
+    l = L - 2 * (asize - margin)
+    by = (l + 3) // 4 + 2 * ((l + 5) // 4) + 24
+    return float(by.double().mean().item())
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -167,14 +177,20 @@ def max_over_ranks(x: float, ws: int, dev) -> float:
     return x if ws == 1 else _mor(x, device=dev)
 
 
+# 10 % three-segment reads (2 pairs each; their weight 0.5 is host-side only)
+CONFIG5_THREE_SEG = 0.1
+
+
 def workload_cfg(args, rank: int):
     """(pairs per GPU, SynthConfig keywords) of the workload: rank r's weak-scaling batch is the stream
     seeded 1337 + 7919 r; rank 0's stream is also configs[3]'s strong-scaling stream."""
     span = (150, 20000) if args.workload == "hg19" else (150, 2500)
     n = args.pairs or (50_000_000 if args.workload == "hg19" else 1_000_000)
+    variable = bool(getattr(args, "read_len_min", None))      # configs[4]'s per-GPU share: config 5's reads
     kw = dict(seed=1337 + 7919 * rank, len_min=getattr(args, "read_len_min", None) or args.read_len,
               len_max=args.read_len, p_backsplice=1.0, p_planted=0.5, mut_rate=0.005, n_rate=0.0005,
-              span_min=span[0], span_max=span[1], locus_ordered=bool(getattr(args, "locus_ordered", False)))
+              span_min=span[0], span_max=span[1], locus_ordered=bool(getattr(args, "locus_ordered", False)),
+              p_three_seg=CONFIG5_THREE_SEG if variable else 0.0)
     return n, kw
 
 
@@ -432,8 +448,9 @@ def configs4(opt, g, ws, rank, dev, steps, warmup, total=200_000_000):
     hi = total * (rank + 1) // ws
     n = hi - lo
     kw = dict(seed=4242, len_min=120, len_max=150, p_backsplice=1.0, p_planted=0.5, mut_rate=0.005, n_rate=0.0005,
-              span_min=150, span_max=20000)
+              span_min=150, span_max=20000, p_three_seg=CONFIG5_THREE_SEG)
     b = stream_share(opt, g, kw, lo, hi)
+    bmean = mean_algo_bytes(b, opt.asize, opt.margin)
     elapsed, kms, out = timed_scans(opt, g, b, steps, warmup, ws, dev)
     elapsed = max_over_ranks(elapsed, ws, dev)
     kms = max_over_ranks(kms, ws, dev)
@@ -447,9 +464,13 @@ def configs4(opt, g, ws, rank, dev, steps, warmup, total=200_000_000):
             "pairs_total": total, "pairs_per_rank": n, "ranks": ws, "rank0_pairs_with_hit": hits,
             "results_checksum": "%016x" % csum,
             "achieved_algo_GBs_per_rank_at_150bp": round(bpp * n / (kms * 1e-3) / 1e9, 1),
-            "note": "configs[4]: one %d-pair stream (seed 4242), read lengths uniform in 120..150 bp, cut into "
+            "algo_bytes_per_pair_mean": round(bmean, 2),
+            "achieved_algo_GBs_per_rank_at_mean": round(bmean * n / (kms * 1e-3) / 1e9, 1),
+            "note": "configs[4]: one %d-pair stream (seed 4242), read lengths uniform in 120..150 bp, 10 %% of "
+                    "pair slots the two anchor pairs of one three-segment read (SURVEY.md 8(d) config 5), cut into "
                     "contiguous shares over the ranks, each generated and scanned on its own rank's GPU; "
-                    "hg19-shaped genome, read order; algorithmic bytes priced at 150 bp (%d B/pair)" % (total, bpp)}
+                    "hg19-shaped genome, read order; algorithmic bytes priced at 150 bp (%d B/pair) and at the "
+                    "stream's mean read_part length" % (total, bpp)}
 
 
 def reorder_then_scan(opt, g, b, steps, dev, bpp):
@@ -1231,14 +1252,18 @@ def main():
         a4 = argparse.Namespace(**vars(args))
         a4.pairs, a4.read_len, a4.read_len_min = 25_000_000, 150, 120
         o4, g4, b4 = build_workload(a4, rank, dev)
+        bm4 = mean_algo_bytes(b4, o4.asize, o4.margin)
         el4, km4, _ = timed_scans(o4, g4, b4, args.steps, args.warmup, 1, dev)
         bpp4 = algo_bytes_per_pair(150, o4.asize, o4.margin)
         line["extra"]["configs[4]_150bp_variable_per_gpu_share"] = {
             "value": round(b4.n * args.steps / el4, 1), "unit": "anchor-pairs/s", "kernel_ms": round(km4, 4),
             "achieved_algo_GBs_at_150bp": round(bpp4 * b4.n / (km4 * 1e-3) / 1e9, 1),
+            "algo_bytes_per_pair_mean": round(bm4, 2),
+            "achieved_algo_GBs_at_mean": round(bm4 * b4.n / (km4 * 1e-3) / 1e9, 1),
             "note": "25M pairs (the per-GPU share of configs[4]'s 200M over 8 GPUs), read lengths uniform in "
-                    "120..150 bp (anchors of varying length, SURVEY.md 8(d) config 5), hg19-shaped genome, read order; algorithmic bytes "
-                    "priced at 150 bp (%d B)" % bpp4}
+                    "120..150 bp (anchors of varying length) and 10 %% of pair slots the two pairs of one three-segment read "
+                    "(SURVEY.md 8(d) config 5), hg19-shaped genome, read order; algorithmic bytes "
+                    "priced at 150 bp (%d B) and at the batch's mean read_part length" % bpp4}
         del b4, g4
         torch.cuda.empty_cache()
         if not args.no_cli:

@@ -114,7 +114,7 @@ class SynthCfg(ctypes.Structure):
                 ("p_planted", ctypes.c_float), ("p_minus_site", ctypes.c_float),
                 ("p_backsplice", ctypes.c_float), ("mut_rate", ctypes.c_float), ("n_rate", ctypes.c_float),
                 ("p_clip", ctypes.c_float), ("span_min", ctypes.c_int32), ("span_max", ctypes.c_int32),
-                ("locus_ordered", ctypes.c_int32), ("_pad", ctypes.c_int32), ("first", ctypes.c_uint64)]
+                ("locus_ordered", ctypes.c_int32), ("p_three_seg", ctypes.c_float), ("first", ctypes.c_uint64)]
 
 
 # every symbol include/fc2_bp.h declares (checked by tests/test_abi.py)

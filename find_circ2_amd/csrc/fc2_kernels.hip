@@ -602,19 +602,77 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
     Rng R{smix(cfg.seed ^ smix(cfg.first + i + 0x51ED2701ull))};
     const int e = p.asize - p.margin;
     const int amin = p.asize;
-    int L = cfg.len_min + (int)R.below(cfg.len_max - cfg.len_min + 1);
-    if (L < 2 * amin) L = 2 * amin;
-    const int kA = amin + (int)R.below(L - 2 * amin + 1);
-    const int kB = L - kA;
-    const bool bs = R.uni() < cfg.p_backsplice;
-    const bool planted = R.uni() < cfg.p_planted;
-    const bool msite = R.uni() < cfg.p_minus_site;
     const int64_t total = chrom_cum[g.n_chrom];
-
+    // three-segment reads: stream pairs 2s and 2s+1 are the two anchor
+    // pairs (s1,s2), (s2,s3) of ONE read from a short circle [start, end) of length c, read =
+    // G[end-k1:end] + G[start:end] + G[start:start+k3]; both pairs draw the slot's geometry from the
+    // slot's own stream, so a share boundary may split a slot (each pair depends on seed + index)
+    const uint64_t gi = cfg.first + i;
+    const uint64_t slot = gi >> 1;
+    bool three = false;
+    if (cfg.p_three_seg > 0.f) {
+        Rng RS{smix(cfg.seed ^ smix(slot * 0x2545F4914F6CDD1Dull + 0x3A5E9ull))};
+        three = RS.uni() < cfg.p_three_seg;
+    }
+    int L, kA, kB;
+    bool bs;
     uint32_t chrom = 0;
     uint64_t cs = 0;
     int64_t sz = 0, A0 = 0, B0 = 0, t0 = 0, t1 = 0;
+    int64_t tg0 = 0;                // read position of read_part[0] (three-segment pair (s2,s3): k1)
     bool ok = false;
+    bool prim_rev;
+    int c0 = 0, c1 = 0;
+    if (three) {
+        Rng R3{smix(cfg.seed ^ smix(slot * 0x9E3779B97F4A7C15ull + 0x7C3E5ull))};
+        int L3 = cfg.len_min + (int)R3.below(cfg.len_max - cfg.len_min + 1);
+        if (L3 < 3 * amin) L3 = 3 * amin;
+        // the read wraps the circle once: k1, k3 <= c (c >= L/3), every segment >= asize
+        const int cmin = (L3 + 2) / 3 > amin ? (L3 + 2) / 3 : amin;
+        const int c = cmin + (int)R3.below(L3 - 2 * amin - cmin + 1);
+        const int klo = L3 - 2 * c > amin ? L3 - 2 * c : amin;
+        const int khi = c < L3 - c - amin ? c : L3 - c - amin;
+        const int k1 = klo + (int)R3.below(khi - klo + 1);
+        const int k3 = L3 - c - k1;
+        const bool planted = R3.uni() < cfg.p_planted;
+        const bool msite = R3.uni() < cfg.p_minus_site;
+        prim_rev = (R3.next() & 1ull) != 0;
+        for (int attempt = 0; attempt < 16 && !ok; ++attempt) {
+            int64_t gp = R3.below(total);
+            uint32_t a = 0, z = g.n_chrom;
+            while (z - a > 1) {
+                const uint32_t m = (a + z) >> 1;
+                if (chrom_cum[m] <= gp) a = m; else z = m;
+            }
+            chrom = a;
+            cs = g.chrom_start[chrom];
+            sz = g.chrom_size[chrom];
+            int64_t end = gp - chrom_cum[chrom];
+            if (planted) {      // donor at end, acceptor before end - c (both ends of the circle)
+                for (int q = 0; q < 512; ++q)
+                    if (dinuc(g, cs, sz, end + q, msite ? cC : cG, cT) &&
+                        dinuc(g, cs, sz, end + q - c - 2, cA, msite ? cC : cG)) { end = end + q; break; }
+            }
+            const int64_t start = end - c;
+            if (start >= 0 && end <= sz && gbase(g, cs, sz, end - 1) < 4u && gbase(g, cs, sz, start) < 4u) {
+                t0 = start; t1 = end; ok = true;
+            }
+        }
+        bs = true;
+        if (!(gi & 1)) { kA = k1; kB = c; A0 = t1 - k1; tg0 = 0; }     // (s1, s2)
+        else           { kA = c; kB = k3; A0 = t0; tg0 = k1; }        // (s2, s3)
+        B0 = t0;
+        if (!ok) A0 = B0 = 0;       // SKIP
+        L = kA + kB;
+    } else {
+    L = cfg.len_min + (int)R.below(cfg.len_max - cfg.len_min + 1);
+    if (L < 2 * amin) L = 2 * amin;
+    kA = amin + (int)R.below(L - 2 * amin + 1);
+    kB = L - kA;
+    bs = R.uni() < cfg.p_backsplice;
+    const bool planted = R.uni() < cfg.p_planted;
+    const bool msite = R.uni() < cfg.p_minus_site;
+
     for (int attempt = 0; attempt < 16 && !ok; ++attempt) {
         int64_t gp;
         if (cfg.locus_ordered) {   // i-th of n strata (redraws stay in the stratum's neighbourhood)
@@ -668,8 +726,9 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
             }
         }
     }
-    int c0 = 0, c1 = 0;
     if (R.uni() < cfg.p_clip) { c0 = (int)R.below(4); c1 = (int)R.below(4); }
+    prim_rev = (R.next() & 1ull) != 0;
+    }
     const int Lp = L - c0 - c1;
     const int l = Lp - 2 * e;
     fc2_pair pr;
@@ -677,7 +736,7 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
     pr.b_aend = (int32_t)(B0 + kB - c1);
     pr.chrom = chrom;
     pr.read_len = (uint16_t)Lp;
-    pr.flags = (uint8_t)((bs ? FC2_PAIR_BACKSPLICE : 0u) | ((R.next() & 1ull) ? FC2_PAIR_PRIMARY_REV : 0u) |
+    pr.flags = (uint8_t)((bs ? FC2_PAIR_BACKSPLICE : 0u) | (prim_rev ? FC2_PAIR_PRIMARY_REV : 0u) |
                          (ok ? 0u : FC2_PAIR_SKIP));
     pr.npos = 0;
     if (truth) { truth[2 * i] = ok ? (int32_t)t0 : -1; truth[2 * i + 1] = ok ? (int32_t)t1 : -1; }
@@ -698,6 +757,8 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
         Rng R2{smix(cfg.seed ^ smix((cfg.first + i) * 0x9E37ull + 0xABCDEFull))};   // same mutation stream both passes
         for (int j = 0; j < lim; ++j) {
             const int t = c0 + e + j;
+            // a three-segment read's two pairs share its bases: mutations keyed by read position
+            if (three) R2.s = smix(cfg.seed ^ smix(slot * 0x100000001B3ull + (uint64_t)(tg0 + t) * 0x9E37ull + 0x55ull));
             unsigned c = t < kA ? gbase(g, cs, sz, A0 + t) : gbase(g, cs, sz, B0 + t - kA);
             if (R2.uni() < cfg.mut_rate) c = (c >= 4u) ? (unsigned)R2.below(4) : ((c + 1u + (unsigned)R2.below(3)) & 3u);
             else (void)R2.next();

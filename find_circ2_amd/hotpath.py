@@ -69,13 +69,14 @@ class SynthConfig:
     span_min: int = 150
     span_max: int = 5000
     locus_ordered: bool = False
+    p_three_seg: float = 0.0  # slots whose two pairs come from one three-segment read (config 5: 0.1)
     first: int = 0          # generate pairs [first, first + n) of the seeded stream
 
     def cfg(self) -> N.SynthCfg:
         return N.SynthCfg(int(self.seed), int(self.len_min), int(self.len_max), float(self.p_planted),
                           float(self.p_minus_site), float(self.p_backsplice), float(self.mut_rate),
                           float(self.n_rate), float(self.p_clip), int(self.span_min), int(self.span_max),
-                          int(bool(self.locus_ordered)), 0, int(self.first))
+                          int(bool(self.locus_ordered)), float(self.p_three_seg), int(self.first))
 
 
 # ---------------------------------------------------------------------------
