@@ -440,7 +440,9 @@ typedef struct fc2_synth_cfg {
     int32_t  locus_ordered;        /* 1: pair i's locus is drawn from the i-th of n equal genome
                                       strata (a batch ordered by position); 0: uniform (read order) */
     float    p_three_seg;          /* of stream slots (pairs 2s, 2s+1): the two anchor pairs of one
-                                      three-segment read wrapping a short circle (config 5: 0.1) */
+                                      three-segment read wrapping a short circle (config 5: 0.1);
+                                      always backsplice, circle length from the read length (span_*,
+                                      p_backsplice, p_clip and locus_ordered do not apply to them) */
     uint64_t first;                /* pair i of the call is pair first + i of the seeded stream
                                       (each pair depends only on seed and its stream index): a
                                       rank generates just its share of a stream */
