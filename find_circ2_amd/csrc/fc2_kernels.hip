@@ -610,7 +610,7 @@ __global__ void synth_pairs_kernel(fc2_params p, fc2_synth_cfg cfg, fc2_genome_v
     const uint64_t gi = cfg.first + i;
     const uint64_t slot = gi >> 1;
     bool three = false;
-    if (cfg.p_three_seg > 0.f) {
+    if (cfg.p_three_seg > 0.f && cfg.len_max >= 3 * amin) {   // (rows are sized for len_max)
         Rng RS{smix(cfg.seed ^ smix(slot * 0x2545F4914F6CDD1Dull + 0x3A5E9ull))};
         three = RS.uni() < cfg.p_three_seg;
     }
