@@ -25,6 +25,7 @@ FC2_E_FORMAT = -3
 FC2_E_RANGE = -4
 FC2_E_IO = -5
 FC2_E_KEY = -6
+FC2_E_OS = -7
 
 MAX_READ_LEN = 32767          # FC2_MAX_READ_LEN: longest read_part (x < 2^15 fits best_x, 2(l+1) ties fit n_ties)
 
@@ -258,7 +259,7 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_close": (None, [vp]),
         "fc2_caller_next": (ctypes.c_int, [vp, P(CallerBatch), P(ctypes.c_int)]),
         "fc2_caller_submit": (ctypes.c_int, [vp, vp, vp, u32, u64]),
-        "fc2_caller_submit_compact": (ctypes.c_int, [vp, vp, ctypes.c_int, vp, u64, vp, u32, u64]),
+        "fc2_caller_submit_compact": (ctypes.c_int, [vp, vp, ctypes.c_int, u64, vp, u64, vp, u32, u64]),
         "fc2_caller_queued": (ctypes.c_int, [vp]),
         "fc2_caller_take": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_set_reads_gz": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, u64]),

@@ -147,11 +147,12 @@ def main(argv=None, evaluator_factory=None) -> int:
                    noncanonical=options.noncanonical, strandpref=options.strandpref, allhits=options.allhits)
     genome = None
     if evaluator_factory is None:
+        from . import _native as N
         from .genome import Genome
         try:
             genome = Genome.from_fasta(options.genome, device=options.device, write_index=True)
-        except Exception as ex:        # GenomeAccessor dummy mode (find_circ.py:340-345)
-            if "cannot open" not in str(ex):
+        except N.Fc2Error as ex:       # GenomeAccessor dummy mode (find_circ.py:338-345): IOError only
+            if ex.code != N.FC2_E_IO:
                 raise
             logging.getLogger("GenomeAccessor").warning(
                 "Could not access '%s'. Switching to dummy mode (only Ns)" % options.genome)

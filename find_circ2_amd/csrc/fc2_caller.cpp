@@ -1667,8 +1667,9 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
     return rc;
 }
 
-extern "C" int fc2_caller_submit_compact(fc2_caller *h, const void *words, int width, const fc2_result_escape *esc,
-                                         uint64_t n_esc, const uint64_t *tiemask, uint32_t tw, uint64_t stride) {
+extern "C" int fc2_caller_submit_compact(fc2_caller *h, const void *words, int width, uint64_t n_words,
+                                         const fc2_result_escape *esc, uint64_t n_esc, const uint64_t *tiemask,
+                                         uint32_t tw, uint64_t stride) {
     if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_compact: null argument");
     size_t n = 0;
     {
@@ -1677,6 +1678,9 @@ extern "C" int fc2_caller_submit_compact(fc2_caller *h, const void *words, int w
             return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_compact: no chunk handed out by fc2_caller_next");
         n = h->queued.front().b_pairs.size();
     }
+    if (n_words != n)
+        return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_compact: " + std::to_string(n_words) +
+                                          " words for a batch of " + std::to_string(n) + " pairs");
     // the chunk's 8-byte results back from the transfer form, into per-thread scratch (a chunk's
     // worth: what record_hits reads next, still in cache)
     static thread_local std::vector<fc2_result> scratch;

@@ -289,10 +289,18 @@ extern "C" int fc2_ctx_scan_async(fc2_ctx *c, const fc2_params *p, uint64_t n, c
     for (uint64_t i = 0; i < n; ++i)
         if (!(hp[i].flags & (FC2_PAIR_BYTEPATH | FC2_PAIR_SKIP))) max_l = std::max(max_l, (int)hp[i].read_len - 2 * e);
     const hipStream_t s = c->stream;
+    // from the first enqueue on, a failure must not return while copies out of the page-locked
+    // staging or the scan are still queued: the next call would rewrite (or HostBuf::reserve free)
+    // memory they read, and fc2_ctx_sync would return at once (pending stays false)
+    auto abandon = [&](int code) {
+        const std::string msg = fc2_last_error();
+        (void)hipStreamSynchronize(s);
+        return keep(c, fc2::fail(code, msg));
+    };
     if ((rc = h2d(c->d_pairs, hp, n * sizeof(fc2_pair), s)) || (rc = h2d(c->d_words, c->h_words.p, (size_t)rw * n * 8, s)) ||
         (rc = h2d(c->d_nwords, c->h_nwords.p, (size_t)nw * n * 8, s)))
-        return keep(c, rc);
-    if (tmw && hipMemsetAsync(c->d_tm.p, 0, tmw * 8, s) != hipSuccess) return keep(c, fc2::fail(FC2_E_HIP, "tie-mask memset"));
+        return abandon(rc);
+    if (tmw && hipMemsetAsync(c->d_tm.p, 0, tmw * 8, s) != hipSuccess) return abandon(fc2::fail(FC2_E_HIP, "tie-mask memset"));
     fc2_batch_view bv{};
     bv.pairs = c->d_pairs.as<const fc2_pair>();
     bv.read_words = c->d_words.as<const uint64_t>();
@@ -304,28 +312,28 @@ extern "C" int fc2_ctx_scan_async(fc2_ctx *c, const fc2_params *p, uint64_t n, c
     bv.max_l = max_l;
     bv.layout = 0;
     uint64_t *dtm = tmw ? c->d_tm.as<uint64_t>() : nullptr;
-    if ((rc = fc2_bp_scan_launch(p, &c->gv, &bv, c->d_res.as<fc2_result>(), dtm, tw, s))) return keep(c, rc);
+    if ((rc = fc2_bp_scan_launch(p, &c->gv, &bv, c->d_res.as<fc2_result>(), dtm, tw, s))) return abandon(rc);
     if (n_bytepath) {                          // pairs whose windows need the FASTA's bytes
         uint64_t m = 0, arena = 0;
-        if ((rc = fc2_bytepath_size(p, n, hp, &m, &arena))) return keep(c, rc);
+        if ((rc = fc2_bytepath_size(p, n, hp, &m, &arena))) return abandon(rc);
         if ((rc = c->h_bidx.reserve(m * 8, "byte-path index")) || (rc = c->h_bpairs.reserve(m * sizeof(fc2_pair), "byte-path pairs")) ||
             (rc = c->h_boff.reserve(m * 8, "byte-path offsets")) || (rc = c->h_arena.reserve(std::max<uint64_t>(arena, 16), "byte-path arena")) ||
             (rc = c->d_bidx.reserve(m * 8, "byte-path index")) || (rc = c->d_bpairs.reserve(m * sizeof(fc2_pair), "byte-path pairs")) ||
             (rc = c->d_boff.reserve(m * 8, "byte-path offsets")) || (rc = c->d_arena.reserve(std::max<uint64_t>(arena, 16), "byte-path arena")))
-            return keep(c, rc);
+            return abandon(rc);
         if ((rc = fc2_bytepath_fill(p, c->fa, n, reads, read_off, hp, c->h_bidx.as<uint64_t>(), c->h_bpairs.as<fc2_pair>(),
                                     c->h_boff.as<uint64_t>(), c->h_arena.as<uint8_t>())))
-            return keep(c, rc);
+            return abandon(rc);
         if ((rc = h2d(c->d_bidx, c->h_bidx.p, m * 8, s)) || (rc = h2d(c->d_bpairs, c->h_bpairs.p, m * sizeof(fc2_pair), s)) ||
             (rc = h2d(c->d_boff, c->h_boff.p, m * 8, s)) || (rc = h2d(c->d_arena, c->h_arena.p, arena, s)))
-            return keep(c, rc);
+            return abandon(rc);
         fc2_bytes_view v{c->d_bidx.as<const uint64_t>(), c->d_bpairs.as<const fc2_pair>(), c->d_arena.as<const uint8_t>(),
                          c->d_boff.as<const uint64_t>(), m};
-        if ((rc = fc2_bp_scan_bytes_launch(p, &v, c->d_res.as<fc2_result>(), dtm, tw, n, s))) return keep(c, rc);
+        if ((rc = fc2_bp_scan_bytes_launch(p, &v, c->d_res.as<fc2_result>(), dtm, tw, n, s))) return abandon(rc);
     }
     hipError_t he = hipMemcpyAsync(c->h_res.p, c->d_res.p, n * 8, hipMemcpyDeviceToHost, s);
     if (he == hipSuccess && tmw) he = hipMemcpyAsync(c->h_tm.p, c->d_tm.p, tmw * 8, hipMemcpyDeviceToHost, s);
-    if (he != hipSuccess) return keep(c, hip_fail(he, "hipMemcpyAsync D2H"));
+    if (he != hipSuccess) return abandon(hip_fail(he, "hipMemcpyAsync D2H"));
     c->pending = true;
     return FC2_OK;
 }

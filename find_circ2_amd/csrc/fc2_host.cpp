@@ -36,10 +36,11 @@ int fail(int code, const std::string &msg) {
 
 int validate_params(const fc2_params *p) {
     if (!p) return fail(FC2_E_PARAM, "null fc2_params");
-    if (p->asize - p->margin <= 0)
-        return fail(FC2_E_PARAM,
-                    "asize - margin <= 0: the reference's read[eff_a:-eff_a] (find_circ.py:895) "
-                    "is empty/garbled and find_breakpoints fails; unsupported");
+    // asize <= margin is legal: eff_a <= 0 turns read[eff_a:-eff_a] (find_circ.py:895) into a short or
+    // empty slice, and fc2_pack_pairs sends every pair to the byte-exact path, which follows the
+    // reference's string / numpy semantics for it
+    if ((int64_t)p->asize - p->margin < -65536)
+        return fail(FC2_E_RANGE, "asize - margin < -65536 is not supported (windows of over 128k bases per pair)");
     if (p->margin > 255) return fail(FC2_E_RANGE, "margin > 255 is not supported (ov is stored in 8 bits)");
     return FC2_OK;
 }
@@ -248,7 +249,8 @@ static bool py2_unescape(const std::string &in, std::string &out) {  // 'string_
 
 static int load_index_file(fc2_fasta *f, const std::string &ipath) {
     FILE *fp = fopen(ipath.c_str(), "r");
-    if (!fp) return fail(FC2_E_IO, "cannot read " + ipath);
+    if (!fp) return fail(FC2_E_IO, "cannot open index: IOError: [Errno " + std::to_string(errno) + "] " +
+                                       strerror(errno) + ": '" + ipath + "'");   // file(ipath), find_circ.py:185
     char *line = nullptr;
     size_t cap = 0;
     ssize_t len;
@@ -287,8 +289,10 @@ static int load_index_file(fc2_fasta *f, const std::string &ipath) {
     return rc;
 }
 
-static void store_index_file(const fc2_fasta *f, const std::string &ipath) {
-    // find_circ.py:157-179: temp file in the same directory, fsync, chmod 0444, rename
+// find_circ.py:157-179: temp file in the index's directory, fsync, chmod 0444, rename.  Every step is
+// an os-level call whose failure raises OSError in Python 2 (tempfile's os.open, os.fsync, os.chmod,
+// os.rename), which GenomeAccessor does not catch (:340 catches IOError only): FC2_E_OS.
+static int store_index_file(const fc2_fasta *f, const std::string &ipath) {
     std::vector<const fc2_chrom_rec *> v;
     for (auto &c : f->chroms) v.push_back(&c);
     std::sort(v.begin(), v.end(), [](const fc2_chrom_rec *a, const fc2_chrom_rec *b) { return a->name < b->name; });
@@ -296,8 +300,12 @@ static void store_index_file(const fc2_fasta *f, const std::string &ipath) {
     std::string tmpl = (dir.empty() ? std::string("./") : dir) + "tmpXXXXXX";
     std::vector<char> buf(tmpl.begin(), tmpl.end());
     buf.push_back(0);
+    auto oserror = [&](int err, const char *what) {
+        return fail(FC2_E_OS, std::string("OSError: [Errno ") + std::to_string(err) + "] " + strerror(err) + ": '" +
+                                  what + "' (writing the FASTA index " + ipath + ")");
+    };
     int fd = mkstemp(buf.data());
-    if (fd < 0) return;  // like the reference, a failure here is not fatal for reading
+    if (fd < 0) return oserror(errno, tmpl.c_str());
     std::string body;
     for (auto *c : v) {
         char num[128];
@@ -308,12 +316,23 @@ static void store_index_file(const fc2_fasta *f, const std::string &ipath) {
         snprintf(num, sizeof num, "\t%lld\n", (long long)c->size);
         body += num;
     }
-    ssize_t w = write(fd, body.data(), body.size());
-    (void)w;
-    fsync(fd);
+    size_t done = 0;
+    while (done < body.size()) {
+        const ssize_t w = write(fd, body.data() + done, body.size() - done);
+        if (w < 0) {
+            if (errno == EINTR) continue;
+            const int err = errno;
+            close(fd);
+            unlink(buf.data());
+            return oserror(err, buf.data());
+        }
+        done += (size_t)w;
+    }
+    if (fsync(fd) != 0) { const int err = errno; close(fd); unlink(buf.data()); return oserror(err, buf.data()); }
     close(fd);
-    chmod(buf.data(), S_IRUSR | S_IRGRP | S_IROTH);
-    if (rename(buf.data(), ipath.c_str()) != 0) unlink(buf.data());
+    if (chmod(buf.data(), S_IRUSR | S_IRGRP | S_IROTH) != 0) { const int err = errno; unlink(buf.data()); return oserror(err, buf.data()); }
+    if (rename(buf.data(), ipath.c_str()) != 0) { const int err = errno; unlink(buf.data()); return oserror(err, buf.data()); }
+    return FC2_OK;
 }
 
 // ---------------------------------------------------------------------------
@@ -333,10 +352,17 @@ static inline int64_t pyclip(int64_t i, int64_t n) {
 // caller only needs to know that a window is longer than that (a window far outside its chromosome
 // is padded with 'N' to its full, possibly huge, length by the reference)
 static int get_upper_impl(const fc2_fasta *f, int ci, int64_t start, int64_t end, std::string &out,
-                          size_t limit = SIZE_MAX) {
+                          size_t limit = SIZE_MAX, int64_t *full_len = nullptr, int tail_char = -1,
+                          int64_t *tail_mis = nullptr) {
+    // full_len: the window's untruncated length; tail_mis: how many of its bytes past `limit` differ
+    // from tail_char (upper-cased) -- a one-base internal part broadcast over the window needs them
     out.clear();
+    if (tail_mis) *tail_mis = 0;
     if (!f) {  // GenomeAccessor.get_dummy (find_circ.py:370-371)
         if (end > start) out.assign(std::min((size_t)(end - start), limit), 'N');
+        const int64_t full = end > start ? end - start : 0;
+        if (full_len) *full_len = full;
+        if (tail_mis && tail_char != 'N' && full > (int64_t)limit) *tail_mis = full - (int64_t)limit;
         return FC2_OK;
     }
     if (ci < 0 || ci >= (int)f->chroms.size()) return fail(FC2_E_KEY, "unknown chromosome index");
@@ -360,6 +386,21 @@ static int get_upper_impl(const fc2_fasta *f, int ci, int64_t start, int64_t end
         ++p;
     }
     out.append(std::min((size_t)pad_end, limit - out.size()), 'N');
+    if (full_len || tail_mis) {   // the slice's bytes after skip_char removal + the pads
+        const int64_t lim = limit == SIZE_MAX ? INT64_MAX : (int64_t)limit;
+        int64_t k = pad_start, mis = 0;
+        const bool n_differs = tail_char != 'N';
+        if (n_differs && pad_start > lim) mis += pad_start - lim;
+        for (int64_t p = os; p < oe;) {
+            if (sl && p + (int64_t)sl <= oe && !memcmp(f->data + p, c.skipchar.data(), sl)) { p += (int64_t)sl; continue; }
+            if (k >= lim && (int)upc(f->data[p]) != tail_char) ++mis;
+            ++k;
+            ++p;
+        }
+        if (n_differs) mis += std::max<int64_t>(0, k + pad_end - std::max(k, lim));
+        if (full_len) *full_len = k + pad_end;
+        if (tail_mis) *tail_mis = mis;
+    }
     return FC2_OK;
 }
 
@@ -389,17 +430,31 @@ extern "C" int fc2_batch_geometry(const fc2_params *p, int32_t max_read_len, uin
 extern "C" int fc2_fasta_open(const char *path, int write_index, fc2_fasta **out) {
     if (!path || !out) return fail(FC2_E_PARAM, "fc2_fasta_open: null argument");
     *out = nullptr;
+    // FC2_E_IO exactly where indexed_fasta() raises IOError (file(fname), find_circ.py:117/124; file(ipath),
+    // :185), which GenomeAccessor turns into its all-N dummy mode (:338-345); a failure the reference does
+    // not catch there (mmap.error, :118) is FC2_E_OS, a malformed index FC2_E_FORMAT.
+    auto ioerror = [&](int err) {
+        return fail(FC2_E_IO, std::string("cannot open FASTA: IOError: [Errno ") + std::to_string(err) + "] " +
+                                  strerror(err) + ": '" + path + "'");
+    };
     int fd = open(path, O_RDONLY);
-    if (fd < 0) return fail(FC2_E_IO, std::string("cannot open FASTA '") + path + "': " + strerror(errno));
+    if (fd < 0) return ioerror(errno);
     struct stat st;
-    if (fstat(fd, &st) != 0) { close(fd); return fail(FC2_E_IO, "fstat failed"); }
+    if (fstat(fd, &st) != 0) { const int err = errno; close(fd); return ioerror(err); }
+    if (S_ISDIR(st.st_mode)) { close(fd); return ioerror(EISDIR); }   // Python 2's file(<directory>)
     fc2_fasta *f = new fc2_fasta();
     f->path = path;
     f->fd = fd;
     f->n = (size_t)st.st_size;
     if (f->n) {
         void *m = mmap(nullptr, f->n, PROT_READ, MAP_SHARED, fd, 0);
-        if (m == MAP_FAILED) { close(fd); delete f; return fail(FC2_E_IO, "mmap failed"); }
+        if (m == MAP_FAILED) {
+            const int err = errno;
+            close(fd);
+            delete f;
+            return fail(FC2_E_OS, std::string("mmap.error: [Errno ") + std::to_string(err) + "] " + strerror(err) +
+                                      " (FASTA '" + path + "')");
+        }
         f->data = (const uint8_t *)m;
         madvise(m, f->n, MADV_WILLNEED);
     }
@@ -409,7 +464,7 @@ extern "C" int fc2_fasta_open(const char *path, int write_index, fc2_fasta **out
         rc = load_index_file(f, ipath);
     } else {
         rc = build_index(f);                       // find_circ.py:114-115
-        if (rc == FC2_OK && write_index) store_index_file(f, ipath);
+        if (rc == FC2_OK && write_index) rc = store_index_file(f, ipath);
     }
     if (rc != FC2_OK) { fc2_fasta_close(f); return rc; }
     *out = f;
@@ -665,6 +720,7 @@ extern "C" int fc2_pack_pairs(const fc2_params *p, const fc2_fasta *f, uint64_t 
                 if (f && (int)pr.chrom >= nch) { int64_t x = -1; bad_chrom.compare_exchange_strong(x, (int64_t)i); break; }
                 if (l < 0) break;  // range(l+1) is empty: no hit, no window use
                 if (maxdist > 255 && l > 255) { int64_t x = -1; bad_dist.compare_exchange_strong(x, (int64_t)i); }
+                if (e <= 0) { bytepath = true; break; }   // read[e:-e] is not the read's middle (fc2_bytepath_fill)
                 if (l > kMaxFastL) { bytepath = true; break; }
                 if ((uint64_t)2 * l > (uint64_t)rw * 64 || (uint64_t)l > (uint64_t)nw * 64) {
                     int64_t x = -1; bad_rows.compare_exchange_strong(x, (int64_t)i); break;
@@ -831,9 +887,9 @@ extern "C" int fc2_pack_windows(const fc2_params *p, const fc2_fasta *f, uint64_
     return FC2_OK;
 }
 
-static inline uint64_t block_bytes(int l) {  // header + I + A + B (windows up to l+3)
+static inline uint64_t block_bytes(int l) {  // 16-B header + I + A + B (window slots of l+3 bytes)
     const uint64_t lc = (uint64_t)std::max(0, l);
-    return (12 + lc + 2 * (lc + 3) + 3) & ~3ull;
+    return (16 + lc + 2 * (lc + 3) + 3) & ~3ull;
 }
 
 extern "C" int fc2_bytepath_size(const fc2_params *p, uint64_t n, const fc2_pair *pairs, uint64_t *m, uint64_t *arena_bytes) {
@@ -864,36 +920,46 @@ extern "C" int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64
         if (!(pr.flags & FC2_PAIR_BYTEPATH)) continue;
         const int L = pr.read_len;
         const int l = L - 2 * e;
-        int32_t lenI = std::max(0, l);
+        // internal = read[e:-e] with Python's slice rules (find_circ.py:895): the read's middle l bases
+        // for e > 0; for e <= 0 read[e:-e] is '' (e == 0) or read[max(L+e, 0) : min(-e, L)]
+        int i0 = e, i1 = L - e;
+        if (e <= 0) { i0 = std::max(L + e, 0); i1 = e == 0 ? 0 : std::min(-e, L); }
+        const int32_t lenI = l < 0 ? 0 : std::max(0, i1 - i0);
+        int64_t fullA = 0, fullB = 0, tailB = 0;
         A.clear(); B.clear();
         if (l >= 0) {
             const int64_t flank = l + 2;
-            // only min(length, l + 3) bytes of a window are kept below
+            // only min(length, l + 3) bytes of a window are stored; the header keeps the full length and,
+            // for a one-base internal part, the mismatches of B's bytes past its slot against that base
+            const int c1 = lenI == 1 ? (int)upc(reads[read_off[i] + i0]) : -1;
             rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + flank, A,
-                                (size_t)flank + 1);
+                                (size_t)flank + 1, &fullA);
             if (rc) return rc;
             rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - flank, (int64_t)pr.b_aend - e, B,
-                                (size_t)flank + 1);
+                                (size_t)flank + 1, &fullB, c1, lenI == 1 ? &tailB : nullptr);
             if (rc) return rc;
         }
-        // a window of unexpected length (outside get_data's defined range) is kept at
-        // l+3 bytes so the kernel sees the length mismatch and reports ERR_WIN
-        const int lc = std::max(0, l);
-        const int32_t lenA = (int32_t)std::min<size_t>(A.size(), (size_t)lc + 3);
-        const int32_t lenB = (int32_t)std::min<size_t>(B.size(), (size_t)lc + 3);
+        // a window of unexpected length (outside get_data's defined range) keeps l+3 stored bytes:
+        // the kernel sees the length mismatch (ERR_WIN) or, where numpy broadcasts a 1-byte operand,
+        // counts the rest of the window as the 'N' padding it is (bp_bytes_kernel)
+        const int32_t lenA = (int32_t)std::min<int64_t>(fullA, INT32_MAX);
+        const int32_t lenB = (int32_t)std::min<int64_t>(fullB, INT32_MAX);
         index[k] = i;
         bpairs[k] = pr;
         off[k] = pos;
         uint8_t *blk = arena + pos;
+        const int32_t tail = (int32_t)std::min<int64_t>(tailB, INT32_MAX);
         memcpy(blk, &lenI, 4);
         memcpy(blk + 4, &lenA, 4);
         memcpy(blk + 8, &lenB, 4);
-        uint8_t *q = blk + 12;
-        for (int j = 0; j < lenI; ++j) q[j] = upc(reads[read_off[i] + e + j]);
+        memcpy(blk + 12, &tail, 4);
+        uint8_t *q = blk + 16;
+        for (int j = 0; j < lenI; ++j) q[j] = upc(reads[read_off[i] + i0 + j]);
         q += lenI;
-        memcpy(q, A.data(), (size_t)std::min<int32_t>(lenA, (int32_t)A.size()));
-        q += lenA;
-        memcpy(q, B.data(), (size_t)std::min<int32_t>(lenB, (int32_t)B.size()));
+        const int lc = std::max(0, l);
+        memcpy(q, A.data(), std::min<size_t>(A.size(), (size_t)lc + 3));
+        q += lc + 3;
+        memcpy(q, B.data(), std::min<size_t>(B.size(), (size_t)lc + 3));
         pos += block_bytes(l);
         ++k;
     }

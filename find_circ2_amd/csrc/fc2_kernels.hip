@@ -437,6 +437,7 @@ __device__ __forceinline__ unsigned code_of(uint8_t c) {
     return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
 }
 
+
 __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_bytes_view v, uint64_t *__restrict__ out,
                                                           uint64_t *__restrict__ tiemask, uint32_t tw, uint64_t stride) {
     const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -445,11 +446,14 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
     const fc2_pair pr = v.pairs[k];
     const uint8_t *blk = v.arena + v.off[k];
     const int lenI = ((const int32_t *)blk)[0], lenA = ((const int32_t *)blk)[1], lenB = ((const int32_t *)blk)[2];
-    const uint8_t *I = blk + 12;
-    const uint8_t *Af = I + lenI;
-    const uint8_t *Bf = Af + lenA;
+    const int tailB = ((const int32_t *)blk)[3];      // lenI == 1: B's bytes past its slot that differ from I[0]
     const int e = p.asize - p.margin;
     const int l = (int)pr.read_len - 2 * e;
+    const int64_t slot = (int64_t)(l < 0 ? 0 : l) + 3;   // stored bytes per window (fc2_bytepath_fill)
+    const uint8_t *I = blk + 16;
+    const uint8_t *Af = I + lenI;
+    const uint8_t *Bf = Af + slot;
+    const int64_t sB = lenB < slot ? lenB : slot;   // A is only read below x + 2 <= l + 2 < slot
     const bool want_ties = p.allhits != 0;
     const uint32_t half = tw / 2;
     if (want_ties)
@@ -457,10 +461,12 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
     if ((pr.flags & FC2_PAIR_SKIP) || l < 0) { out[i] = nohit_result(0); return; }
 
     // Windows normally have l+2 bytes.  Outside get_data's defined range they can
-    // come back shorter or longer (find_circ.py:194-211); then the literal
-    // string form of find_circ.py:907-908 is followed byte by byte, including
-    // the reference's failure when the spliced string's length differs from the
-    // internal part (numpy comparison, :863) -> ERR_WIN.
+    // come back shorter or longer (find_circ.py:194-211), and with asize <= margin the
+    // internal part read[e:-e] (:895) is not l bytes long; then the literal string form
+    // of find_circ.py:907-908 is followed byte by byte: with -d 0, simple_match's `!=`
+    // of unequal strings is True (:865-866, never a hit); otherwise numpy compares the
+    // two byte arrays (:861-863) -- equal lengths elementwise, a 1-byte operand broadcast
+    // against the other, anything else fails (-> ERR_WIN).
     const bool regular = (lenI == l && lenA == l + 2 && lenB == l + 2);
     int totB = 0;
     if (regular)
@@ -476,15 +482,31 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
             if (regular) {
                 if (x > 0) d += (int)(Af[x - 1] != I[x - 1]) - (int)(Bf[x + 1] != I[x - 1]);
             } else {
-                const int n1 = x < lenA ? x : lenA;
-                const int n2 = lenB - (x + 2) > 0 ? lenB - (x + 2) : 0;
-                if (n1 + n2 != lenI) {
-                    if (p.maxdist != 0) { err = FC2_RES_ERR_WIN; break; }
+                const int64_t n1 = x < lenA ? x : lenA;                                // A_flank[:x]
+                const int64_t n2 = (int64_t)lenB - (x + 2) > 0 ? (int64_t)lenB - (x + 2) : 0;   // B_flank[x+2:]
+                const int64_t sl = n1 + n2;
+                int64_t dd = 0;
+                if (sl == lenI) {   // then B[x+2:] lies in its slot: lenB <= lenI + x + 2 <= l + 2
+                    for (int64_t j = 0; j < n1; ++j) dd += Af[j] != I[j];
+                    for (int64_t j = 0; j < n2; ++j) dd += Bf[x + 2 + j] != I[n1 + j];
+                    if (p.maxdist == 0) dd = dd != 0;                                  // the bool a != b
+                } else if (p.maxdist == 0) {
                     continue;  // simple_match: unequal strings never qualify (find_circ.py:865-866)
-                }
-                d = 0;
-                for (int j = 0; j < n1; ++j) d += Af[j] != I[j];
-                for (int j = 0; j < n2; ++j) d += Bf[x + 2 + j] != I[n1 + j];
+                } else if (lenI == 1 && sl > 0) {                                      // I broadcast over spliced
+                    const uint8_t c = I[0];
+                    for (int64_t j = 0; j < n1; ++j) dd += Af[j] != c;
+                    const int64_t b0 = x + 2, b1 = x + 2 + n2;                         // B bytes [b0, b1)
+                    const int64_t st = b1 < sB ? b1 : sB;
+                    for (int64_t j = b0; j < st; ++j) dd += Bf[j] != c;
+                    if (b1 > sB) dd += tailB;                                          // B[slot:], b0 < slot
+                } else if (sl == 1 && lenI > 0) {                                      // spliced[0] broadcast
+                    const uint8_t c = n1 ? Af[0] : Bf[x + 2];                          // x + 2 < slot
+                    for (int j = 0; j < lenI; ++j) dd += I[j] != c;
+                } else if (!((sl == 0 && lenI == 1) || (sl == 1 && lenI == 0))) {
+                    err = FC2_RES_ERR_WIN;  // shapes numpy cannot broadcast
+                    break;
+                }                            // else (0,) against (1,): an empty comparison, dist 0
+                d = dd > 0x7FFFFFFF ? 0x7FFFFFFF : (int)dd;
             }
             if (d > p.maxdist) continue;
             const bool have4 = (x + 1 < lenA) && (x + 1 < lenB);
@@ -493,7 +515,7 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
             if (!(have4 && is_acgtn(g0) && is_acgtn(g1) && is_acgtn(g2) && is_acgtn(g3))) { err = FC2_RES_ERR_KEY; break; }
             const int cp = (g0 == 'G' && g1 == 'T' && g2 == 'A' && g3 == 'G');
             const int cm = (g0 == 'C' && g1 == 'T' && g2 == 'A' && g3 == 'C');
-            const int ov = ov_of(x, l, p.margin);
+    const int ov = ov_of(x, l, p.margin);
             if (p.noncanonical) {
                 const int s1 = 20 * cp - 10 * d - ov + sp_plus, s2 = 20 * cm - 10 * d - ov + sp_minus;
                 if (pass == 0) { add_hit(Bst, x, 0, d, ov, s1); add_hit(Bst, x, 1, d, ov, s2); }

@@ -84,6 +84,14 @@ __device__ __forceinline__ void emit(const fc2::ScanView &bv, uint64_t *out, uin
     }
 }
 
+// A byte-path pair in a compact launch: the escape word without an escape record, so that
+// fc2_result_expand fails (FC2_E_FORMAT: more escaped words than escapes) instead of decoding
+// whatever the word held before -- the compact launch takes no byte-path pairs (fc2_bp.h).
+__device__ __forceinline__ void mark_unscanned(const fc2::ScanView &bv, uint64_t i) {
+    if (bv.c_width == 2) __builtin_nontemporal_store((uint16_t)FC2_R16_ESCAPE, (uint16_t *)bv.c_words + i);
+    else __builtin_nontemporal_store((uint32_t)FC2_R32_ESCAPE, (uint32_t *)bv.c_words + i);
+}
+
 template <bool NT>
 __device__ __forceinline__ u64x2 ld_pair_raw(const fc2_pair *p) {
     if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u64x2 *>(p));
@@ -894,6 +902,7 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     fc2_pair pr;
     __builtin_memcpy(&pr, &prv, sizeof pr);
     bool active = live && !(pr.flags & FC2_PAIR_BYTEPATH);   // BYTEPATH: left for the byte-exact kernel
+    if (live && !active && bv.c_words) mark_unscanned(bv, i);
     if (!COOP && !active) return;
 
     const int e = p.asize - p.margin;
@@ -1678,7 +1687,10 @@ __global__ __launch_bounds__(kBlock) void bp_wave_kernel(fc2_params p, fc2_genom
         for (int j = 0; j < 4; ++j) rec[j] = rfl(P[j]);
         fc2_pair pr;
         __builtin_memcpy(&pr, rec, sizeof pr);
-        if (pr.flags & FC2_PAIR_BYTEPATH) continue;   // left for the byte-exact kernel
+        if (pr.flags & FC2_PAIR_BYTEPATH) {           // left for the byte-exact kernel
+            if (bv.c_words && threadIdx.x % 64 == 0) mark_unscanned(bv, i);
+            continue;
+        }
         const uint32_t *C = P + kWsChrom;
         WaveGeo G;
         wave_geo(p, g, pr, (uint64_t)rfl(C[0]) | ((uint64_t)rfl(C[1]) << 32),

@@ -356,7 +356,8 @@ class NativeCaller:
             words = np.ascontiguousarray(res.words)
             esc = np.ascontiguousarray(res.escapes, dtype=N.ESCAPE_DTYPE)
             return L.fc2_caller_submit_compact(self.h, words.ctypes.data if n else None, words.dtype.itemsize,
-                                               esc.ctypes.data if len(esc) else None, len(esc), tm_ptr, tw, n)
+                                               len(words), esc.ctypes.data if len(esc) else None, len(esc), tm_ptr,
+                                               tw, n)
         res_ptr = None
         if n:
             res = np.ascontiguousarray(res, dtype=np.int64)

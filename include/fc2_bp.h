@@ -42,8 +42,12 @@ extern "C" {
 #define FC2_E_HIP    -2   /* HIP runtime error (message via fc2_last_error)       */
 #define FC2_E_FORMAT -3   /* malformed FASTA / index                               */
 #define FC2_E_RANGE  -4   /* value outside the supported range                     */
-#define FC2_E_IO     -5   /* file could not be opened / mapped                     */
+#define FC2_E_IO     -5   /* IOError class: the file cannot be opened or read (the reference's
+                             file()/open() raises IOError; GenomeAccessor then switches to its
+                             all-N dummy mode, find_circ.py:338-345)                         */
 #define FC2_E_KEY    -6   /* unknown chromosome (reference KeyError, find_circ.py:193) */
+#define FC2_E_OS     -7   /* OS error the reference does not catch (mmap.error, OSError from
+                             writing the .byo_index, find_circ.py:118, 157-179)             */
 
 /* ---- options the hot path reads (find_circ.py:393-404) ----------------- */
 typedef struct fc2_params {
@@ -224,9 +228,13 @@ typedef struct fc2_batch_view {
                                          (needs wt and l + 2 <= 128; otherwise the default form runs) */
 
 /* ---- pairs that need byte-exact evaluation ------------------------------ */
-/* Block for pair k at arena[off[k]]: int32 lenI, lenA, lenB, then
- * I (lenI bytes, uppercased internal read), A window (lenA), B window (lenB),
- * exactly as get_data(...).upper() returns them (find_circ.py:895, 901-902). */
+/* Block for pair k at arena[off[k]]: int32 lenI, lenA, lenB, tailB, then
+ * I (lenI bytes: read[e:-e].upper() with Python's slice rules, find_circ.py:895), then the A and B
+ * windows of get_data(...).upper() (:901-902) in slots of l+3 bytes each (l = read_len - 2e).
+ * lenA / lenB are the windows' full lengths (saturated at INT32_MAX); a window outside get_data's
+ * defined range can be longer than its slot (:194-211), and only a one-base internal part that
+ * numpy broadcasts over the spliced string (:861-863) reads past the slot: tailB = the bytes of
+ * B[l+3:] that differ from I[0] when lenI == 1, else 0. */
 typedef struct fc2_bytes_view {
     const uint64_t *index;       /* device [m] : pair index into results/tiemask */
     const fc2_pair *pairs;       /* device [m] */
@@ -368,7 +376,14 @@ typedef struct fc2_fasta fc2_fasta;
 
 /* Open + mmap a (multi-)FASTA.  If <path>.byo_index is readable it is used
  * (find_circ.py:110-112); otherwise the file is indexed (:120-155) and, when
- * write_index != 0, the index is stored atomically next to it (:157-179). */
+ * write_index != 0, the index is stored atomically next to it (:157-179).
+ * Errors follow the exception the reference's indexed_fasta() raises:
+ *   FC2_E_IO     IOError (missing or unreadable file, a directory -- the -G <folder> form of
+ *                find_circ.py:386 -- or an unreadable index): GenomeAccessor catches it and
+ *                runs in dummy mode (find_circ.py:338-345), so a host passes NULL to
+ *                fc2_ctx_genome_load / fc2_caller_set_genome and goes on;
+ *   FC2_E_OS     mmap.error or an OSError writing the index (not caught by the reference);
+ *   FC2_E_FORMAT a FASTA / index the reference's index()/load_index() fail on. */
 int  fc2_fasta_open(const char *path, int write_index, fc2_fasta **out);
 void fc2_fasta_close(fc2_fasta *f);
 int  fc2_fasta_n_chrom(const fc2_fasta *f);

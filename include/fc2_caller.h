@@ -87,10 +87,11 @@ int fc2_caller_queued(fc2_caller *h);
 int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const uint64_t *tiemask, uint32_t tw,
                       uint64_t stride);
 /* The same with the results in a compact transfer form (include/fc2_bp.h "compact results",
- * canonical mode, width 4 or 2 bytes): words [n] and the n_esc escapes (indices into this batch),
- * expanded here. */
-int fc2_caller_submit_compact(fc2_caller *h, const void *words, int width, const fc2_result_escape *esc,
-                              uint64_t n_esc, const uint64_t *tiemask, uint32_t tw, uint64_t stride);
+ * canonical mode, width 4 or 2 bytes): words [n_words] and the n_esc escapes (indices into this
+ * batch), expanded here.  FC2_E_PARAM unless n_words is the oldest queued batch's pair count. */
+int fc2_caller_submit_compact(fc2_caller *h, const void *words, int width, uint64_t n_words,
+                              const fc2_result_escape *esc, uint64_t n_esc, const uint64_t *tiemask, uint32_t tw,
+                              uint64_t stride);
 
 /* Output text produced since the last call: 0 = spliced_reads.fastq, 1 =
  * multi_events.tsv rows, 2 = test_results.tsv rows. */

@@ -58,6 +58,8 @@ def lib():
         L.orc_fasta_index.restype = vp
         L.orc_fasta_index.argtypes = [vp, ctypes.c_int64]
         L.orc_fasta_free.argtypes = [vp]
+        L.orc_fasta_dummy.restype = vp
+        L.orc_fasta_dummy.argtypes = []
         L.orc_fasta_n_chrom.argtypes = [vp]
         L.orc_fasta_chrom_name.restype = ctypes.c_char_p
         L.orc_fasta_chrom_name.argtypes = [vp, ctypes.c_int]
@@ -85,6 +87,8 @@ def params(asize=15, margin=2, maxdist=2, noncanonical=False, strandpref=False, 
 class OracleFasta:
     """A FASTA indexed with the reference's semantics (find_circ.py:120-155)."""
 
+    dummy = False
+
     def __init__(self, path: str = None, data: bytes = None):
         if data is None:
             with open(path, "rb") as f:
@@ -94,6 +98,26 @@ class OracleFasta:
         n = lib().orc_fasta_n_chrom(self.h)
         self.names = [lib().orc_fasta_chrom_name(self.h, i).decode() for i in range(n)]
         self.sizes = [lib().orc_fasta_chrom_size(self.h, i) for i in range(n)]
+
+    @classmethod
+    def dummy_genome(cls) -> "OracleFasta":
+        """GenomeAccessor's dummy mode (find_circ.py:338-345, 370-371): all-N windows for every
+        chromosome, used when indexed_fasta() raises IOError (e.g. -G <directory>)."""
+        g = cls.__new__(cls)
+        g._buf = None
+        g.h = lib().orc_fasta_dummy()
+        g.names, g.sizes, g.dummy = [], [], True
+        return g
+
+    @classmethod
+    def open_or_dummy(cls, path: str) -> "OracleFasta":
+        """GenomeAccessor.__init__ (find_circ.py:338-345): IOError -> dummy mode.  Python 3's
+        IOError is OSError; the reference's file() raises it for a missing file, a directory or
+        missing permissions."""
+        try:
+            return cls(path)
+        except OSError:
+            return cls.dummy_genome()
 
     def __del__(self):
         try:
@@ -154,7 +178,7 @@ def scan_fasta(p: OrcParams, fasta: OracleFasta, reads, chrom_idx, a_pos, b_aend
     at = ao = None
     cap = 0
     if all_ties:
-        cap = int(2 * (lens.astype(np.int64) + 2).sum()) + 16
+        cap = int(2 * (lens.astype(np.int64) + 2 + 2 * max(0, p.margin - p.asize)).sum()) + 16
         at = np.zeros(cap, dtype=ORC_HIT_DTYPE)
         ao = np.zeros(n, dtype=np.int64)
     lib().orc_scan_fasta(ctypes.byref(p), fasta.h, n, _ptr(buf), _ptr(off), _ptr(lens), _ptr(chrom_idx),
@@ -178,7 +202,7 @@ def scan_windows(p: OrcParams, reads, wins: np.ndarray, win_off: np.ndarray, a_p
     at = ao = None
     cap = 0
     if all_ties:
-        cap = int(2 * (lens.astype(np.int64) + 2).sum()) + 16
+        cap = int(2 * (lens.astype(np.int64) + 2 + 2 * max(0, p.margin - p.asize)).sum()) + 16
         at = np.zeros(cap, dtype=ORC_HIT_DTYPE)
         ao = np.zeros(n, dtype=np.int64)
     lib().orc_scan_windows(ctypes.byref(p), n, _ptr(buf), _ptr(off), _ptr(lens), _ptr(wins), _ptr(win_off),

@@ -71,6 +71,7 @@ typedef struct {
     int64_t n;
     orc_chrom *chroms;
     int n_chrom;
+    int dummy;             /* GenomeAccessor dummy mode (find_circ.py:338-345, 370-371) */
 } orc_fasta;
 
 static int is_space(unsigned char c) { return c == ' ' || c == '\t' || c == '\n' || c == '\r' || c == '\v' || c == '\f'; }
@@ -135,6 +136,14 @@ orc_fasta *orc_fasta_index(const unsigned char *data, int64_t n) {
     return f;
 }
 
+/* GenomeAccessor.get_dummy (find_circ.py:370-371): "N"*int(end-start) for every chromosome, which
+ * is what find_breakpoints sees once indexed_fasta() raised IOError (:338-345). */
+orc_fasta *orc_fasta_dummy(void) {
+    orc_fasta *f = (orc_fasta *)calloc(1, sizeof(orc_fasta));
+    f->dummy = 1;
+    return f;
+}
+
 void orc_fasta_free(orc_fasta *f) { if (f) { free(f->chroms); free(f); } }
 int orc_fasta_n_chrom(const orc_fasta *f) { return f->n_chrom; }
 const char *orc_fasta_chrom_name(const orc_fasta *f, int i) { return f->chroms[i].name; }
@@ -156,6 +165,11 @@ static int64_t floordiv(int64_t a, int64_t b) { int64_t q = a / b; if ((a % b !=
  * Writes up to cap bytes into out, returns the produced length (may differ from end-start
  * outside the reference's well-defined range). */
 int64_t orc_get_upper(const orc_fasta *f, int ci, int64_t start, int64_t end, unsigned char *out, int64_t cap) {
+    if (f->dummy) {
+        int64_t k = end > start ? end - start : 0;
+        for (int64_t q = 0; q < k && q < cap; q++) out[q] = 'N';
+        return k;
+    }
     const orc_chrom *c = &f->chroms[ci];
     int64_t pad_start = 0, pad_end = 0;
     if (start < 0) { pad_start = -start; start = 0; }
@@ -212,12 +226,23 @@ static void push_hit(orc_hit *h, int x, int start, int end, char strand, int dis
     h->score = s; h->n_hits = 1;
 }
 
+/* One byte of a window whose first `stored` bytes are in W: past them lies the 'N' padding that
+ * get_data appends to a window starting past the chromosome end (find_circ.py:194-211). */
+static unsigned char win_byte(const unsigned char *W, int64_t stored, int64_t j) { return j < stored ? W[j] : 'N'; }
+
 /* Literal O(l^2) restatement (find_circ.py:854-974).
- * read: read_part (L bytes, any case); Af/Bf: uppercased windows of lengths la/lb as
- * produced by get_data (normally l+2).  Returns number of ties written (<= max_ties
- * are stored), or -ORC_ERR_*.  hits_tmp: scratch of >= 2*(l+1) entries. */
+ * read: read_part (L bytes, any case); Af/Bf: uppercased windows of true lengths la/lb as
+ * produced by get_data (normally l+2), of which the first sa/sb bytes are stored.  Returns number
+ * of ties written (<= max_ties are stored), or -ORC_ERR_*.  hits_tmp: scratch of >= 2*(l+1) entries.
+ *
+ * mismatches(a, b) = (fromstring(a) != fromstring(b)).sum() (:861-863) with numpy's rules: equal
+ * lengths compare elementwise; a 1-byte operand is broadcast against the other (a 0-byte one
+ * against a 1-byte one gives an empty comparison, sum 0); any other pair of lengths makes `!=` the
+ * scalar True (numpy 1.x) and .sum() raises -> ORC_ERR_SHAPE.  simple_match (-d 0, :865-866) is the
+ * plain string inequality. */
 int orc_find_breakpoints_naive(const orc_params *p, const unsigned char *read, int L,
-                               const unsigned char *Af, int la, const unsigned char *Bf, int lb,
+                               const unsigned char *Af, int64_t la, int64_t sa,
+                               const unsigned char *Bf, int64_t lb, int64_t sb,
                                int32_t a_pos, int32_t b_aend, int is_backsplice, int primary_rev,
                                orc_hit *hits_tmp, orc_hit *ties, int max_ties) {
     int e = p->asize - p->margin;
@@ -229,29 +254,36 @@ int orc_find_breakpoints_naive(const orc_params *p, const unsigned char *read, i
     int ilen = (s1 > s0) ? (int)(s1 - s0) : 0;
     unsigned char *internal = (unsigned char *)malloc((size_t)(ilen + 1));
     for (int i = 0; i < ilen; i++) internal[i] = up(read[s0 + i]);
-    unsigned char *spliced = (unsigned char *)malloc((size_t)(la + lb + 4));
     int nh = 0, err = 0;
     for (int x = 0; x <= l; x++) {
-        int n1 = x < la ? x : la;                 /* A_flank[:x] */
-        int n2 = (x + 2 < lb) ? lb - (x + 2) : 0; /* B_flank[x+2:] */
-        memcpy(spliced, Af, (size_t)n1);
-        if (n2) memcpy(spliced + n1, Bf + x + 2, (size_t)n2);
-        int slen = n1 + n2;
-        int dist;
+        int64_t n1 = x < la ? x : la;                 /* A_flank[:x] */
+        int64_t n2 = (x + 2 < lb) ? lb - (x + 2) : 0; /* B_flank[x+2:] */
+        int64_t slen = n1 + n2;
+        /* byte j of spliced = A_flank[:x] + B_flank[x+2:] */
+#define SPLICED(j) ((j) < n1 ? win_byte(Af, sa, (j)) : win_byte(Bf, sb, x + 2 + (j) - n1))
+        int64_t dist;
         if (p->maxdist == 0) {
             /* simple_match: a != b  (bool) */
-            dist = !(slen == ilen && !memcmp(spliced, internal, (size_t)slen));
-        } else {
-            if (slen != ilen) { err = ORC_ERR_SHAPE; break; }
+            int eq = slen == ilen;
+            for (int64_t j = 0; eq && j < slen; j++) eq = SPLICED(j) == internal[j];
+            dist = !eq;
+        } else if (slen == ilen) {
             dist = 0;
-            for (int i = 0; i < slen; i++) dist += spliced[i] != internal[i];
-        }
+            for (int64_t j = 0; j < slen; j++) dist += SPLICED(j) != internal[j];
+        } else if (ilen == 1) {
+            dist = 0;
+            for (int64_t j = 0; j < slen; j++) dist += SPLICED(j) != internal[0];
+        } else if (slen == 1) {
+            dist = 0;
+            for (int j = 0; j < ilen; j++) dist += SPLICED(0) != internal[j];
+        } else { err = ORC_ERR_SHAPE; break; }
+#undef SPLICED
         if (dist <= p->maxdist) {
             int ov = ov_of(x, l, p->margin);
             char gtag[5] = {0, 0, 0, 0, 0};
             int gl = 0;
-            for (int i = x; i < x + 2 && i < la; i++) gtag[gl++] = (char)Af[i];
-            for (int i = x; i < x + 2 && i < lb; i++) gtag[gl++] = (char)Bf[i];
+            for (int i = x; i < x + 2 && i < la; i++) gtag[gl++] = (char)win_byte(Af, sa, i);
+            for (int i = x; i < x + 2 && i < lb; i++) gtag[gl++] = (char)win_byte(Bf, sb, i);
             if (gl != 4) { err = ORC_ERR_KEY; break; }
             for (int i = 0; i < 4; i++) if (!is_acgtn((unsigned char)gtag[i])) { err = ORC_ERR_KEY; }
             if (err) break;
@@ -261,16 +293,16 @@ int orc_find_breakpoints_naive(const orc_params *p, const unsigned char *read, i
             start = lo; end = hi;
             if (is_backsplice) end -= 1; else start -= 1;
             if (p->noncanonical) {
-                push_hit(&hits_tmp[nh++], x, start, end, '+', dist, ov, gtag, primary_rev, p);
-                push_hit(&hits_tmp[nh++], x, start, end, '-', dist, ov, rc, primary_rev, p);
+                push_hit(&hits_tmp[nh++], x, start, end, '+', (int)dist, ov, gtag, primary_rev, p);
+                push_hit(&hits_tmp[nh++], x, start, end, '-', (int)dist, ov, rc, primary_rev, p);
             } else if (!strcmp(gtag, "GTAG")) {
-                push_hit(&hits_tmp[nh++], x, start, end, '+', dist, ov, gtag, primary_rev, p);
+                push_hit(&hits_tmp[nh++], x, start, end, '+', (int)dist, ov, gtag, primary_rev, p);
             } else if (!strcmp(gtag, "CTAC")) {
-                push_hit(&hits_tmp[nh++], x, start, end, '-', dist, ov, rc, primary_rev, p);
+                push_hit(&hits_tmp[nh++], x, start, end, '-', (int)dist, ov, rc, primary_rev, p);
             }
         }
     }
-    free(internal); free(spliced);
+    free(internal);
     if (err) return -err;
     return finish_hits(hits_tmp, nh, ties, max_ties);
 }
@@ -331,8 +363,8 @@ int64_t orc_scan_fasta(const orc_params *p, const orc_fasta *f, int64_t n,
     (void)n_threads;
     int maxL = 0;
     for (int64_t i = 0; i < n; i++) if (read_len[i] > maxL) maxL = read_len[i];
-    int wcap = maxL + 8;
-    int hcap = 2 * (maxL + 2) + 4;
+    int wcap = maxL + 2 * (e < 0 ? -e : 0) + 8;
+    int hcap = 2 * (maxL + 2 * (e < 0 ? -e : 0) + 2) + 4;
     unsigned char *Af = (unsigned char *)malloc((size_t)wcap * 2 + 64);
     unsigned char *Bf = (unsigned char *)malloc((size_t)wcap * 2 + 64);
     orc_hit *tmp = (orc_hit *)malloc(sizeof(orc_hit) * (size_t)hcap);
@@ -342,24 +374,23 @@ int64_t orc_scan_fasta(const orc_params *p, const orc_fasta *f, int64_t n,
         int l = L - 2 * e;
         int ci = chrom_idx[i];
         if (all_off) all_off[i] = total_all;
-        if (ci < 0 || ci >= f->n_chrom) { n_ties[i] = -ORC_ERR_CHROM; continue; }
+        if (!f->dummy && (ci < 0 || ci >= f->n_chrom)) { n_ties[i] = -ORC_ERR_CHROM; continue; }
         int flank = l + 2;
         int64_t as = (int64_t)a_pos[i] + e, bs = (int64_t)b_aend[i] - e - flank;
         int64_t la = 0, lb = 0;
         if (flank > 0 && flank <= wcap) {
+            /* true lengths; the buffers keep the first wcap * 2 bytes (a longer window is 'N' padding
+             * past that point, win_byte) */
             la = orc_get_upper(f, ci, as, as + flank, Af, wcap * 2);
             lb = orc_get_upper(f, ci, bs, bs + flank, Bf, wcap * 2);
-            /* a window longer than flank + 1 (far outside the chromosome: get_data pads it with 'N') acts
-             * in find_breakpoints exactly as one of flank + 1 bytes: only A[:x], A[x:x+2] (x <= l) and
-             * the length of B[x+2:] are read, and any length > flank gives the same shape mismatch */
-            if (la > flank + 1) la = flank + 1;
-            if (lb > flank + 1) lb = flank + 1;
         }
         int r;
         if (use_fast && e > 0 && la == flank && lb == flank)
             r = orc_find_breakpoints_fast(p, reads + read_off[i], L, Af, Bf, a_pos[i], b_aend[i], is_bs[i], primary_rev[i], tmp, ties, hcap);
         else
-            r = orc_find_breakpoints_naive(p, reads + read_off[i], L, Af, (int)la, Bf, (int)lb, a_pos[i], b_aend[i], is_bs[i], primary_rev[i], tmp, ties, hcap);
+            r = orc_find_breakpoints_naive(p, reads + read_off[i], L, Af, la, la < wcap * 2 ? la : wcap * 2, Bf, lb,
+                                           lb < wcap * 2 ? lb : wcap * 2, a_pos[i], b_aend[i], is_bs[i], primary_rev[i],
+                                           tmp, ties, hcap);
         n_ties[i] = r;
         if (r > 0) {
             first[i] = ties[0];
@@ -383,7 +414,7 @@ int64_t orc_scan_windows(const orc_params *p, int64_t n,
     int e = p->asize - p->margin;
     int maxL = 0;
     for (int64_t i = 0; i < n; i++) if (read_len[i] > maxL) maxL = read_len[i];
-    int hcap = 2 * (maxL + 2) + 4;
+    int hcap = 2 * (maxL + 2 * (e < 0 ? -e : 0) + 2) + 4;
     orc_hit *tmp = (orc_hit *)malloc(sizeof(orc_hit) * (size_t)hcap);
     orc_hit *ties = (orc_hit *)malloc(sizeof(orc_hit) * (size_t)hcap);
     for (int64_t i = 0; i < n; i++) {
@@ -398,7 +429,7 @@ int64_t orc_scan_windows(const orc_params *p, int64_t n,
         if (use_fast && e > 0)
             r = orc_find_breakpoints_fast(p, reads + read_off[i], L, Af, Bf, a_pos[i], b_aend[i], is_bs[i], primary_rev[i], tmp, ties, hcap);
         else
-            r = orc_find_breakpoints_naive(p, reads + read_off[i], L, Af, flank, Bf, flank, a_pos[i], b_aend[i], is_bs[i], primary_rev[i], tmp, ties, hcap);
+            r = orc_find_breakpoints_naive(p, reads + read_off[i], L, Af, flank, flank, Bf, flank, flank, a_pos[i], b_aend[i], is_bs[i], primary_rev[i], tmp, ties, hcap);
         n_ties[i] = r;
         if (r > 0) {
             first[i] = ties[0];

@@ -314,10 +314,12 @@ class Hit:
 
 
 def _mismatches(a: bytes, b: bytes) -> int:
-    """find_circ.py:861-863 -- numpy byte compare + sum."""
-    if len(a) != len(b):
-        # numpy 1.x (Python 2): `!=` of unequal lengths returns the scalar True (DeprecationWarning),
-        # and True.sum() raises AttributeError (find_circ.py:861-863)
+    """find_circ.py:861-863 -- numpy byte compare + sum, with numpy's broadcasting: equal lengths
+    compare elementwise, a 1-byte operand is broadcast against the other (0 against 1 bytes is an
+    empty comparison)."""
+    if len(a) != len(b) and len(a) != 1 and len(b) != 1:
+        # numpy 1.x (Python 2): `!=` of shapes it cannot broadcast returns the scalar True
+        # (DeprecationWarning), and True.sum() raises AttributeError (find_circ.py:861-863)
         raise ReferenceShapeError("'bool' object has no attribute 'sum'")
     return int((np.frombuffer(a, dtype=np.int8) != np.frombuffer(b, dtype=np.int8)).sum())
 

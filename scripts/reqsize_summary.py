@@ -1,4 +1,4 @@
-"""Summarise scripts/gpu_r03_reqsize_policy.sh: per policy_probe variant, L2->fabric read requests per
+"""Summarise the r03 policy_probe runs (scripts/policy_probe.hip): per policy_probe variant, L2->fabric read requests per
 random gather by size (TCC_EA0_RDREQ_32B/64B/128B) and those that went to DRAM.  The probe runs
 3 allocations x 12 variants x 6 launches (one warm-up + five timed), in that order; the 4th launch of
 each variant is the one reported.  Usage: python scripts/reqsize_summary.py gpurun_out/req_policy > summary.json"""

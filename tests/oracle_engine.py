@@ -10,11 +10,13 @@ from find_circ2_amd.hotpath import WINDOW_SHAPE_MESSAGE, BreakpointError, Splice
 
 
 def oracle_evaluator_factory(options, hp):
-    of = oracle.OracleFasta(options.genome)
+    of = oracle.OracleFasta.open_or_dummy(options.genome)     # GenomeAccessor, find_circ.py:338-345
+    if of.dummy:
+        _dummy_warning(options.genome)
     p = oracle.params(hp.asize, hp.margin, hp.maxdist, hp.noncanonical, hp.strandpref, hp.allhits)
 
     def evaluate(spans):
-        idx = [of.names.index(s.chrom) if s.chrom in of.names else -1 for s in spans]
+        idx = [0 if of.dummy else of.names.index(s.chrom) if s.chrom in of.names else -1 for s in spans]
         r = oracle.scan_fasta(p, of, [s.read_part.encode("latin-1") for s in spans], idx,
                               [s.align_A.pos for s in spans], [s.align_B.aend for s in spans],
                               [s.is_backsplice for s in spans], [s.strand == '-' for s in spans],
@@ -52,16 +54,24 @@ def oracle_batch_engine(options, hp):
 
     from find_circ2_amd import _native as N
 
-    of = oracle.OracleFasta(options.genome)
+    of = oracle.OracleFasta.open_or_dummy(options.genome)     # GenomeAccessor, find_circ.py:338-345
     p = oracle.params(hp.asize, hp.margin, hp.maxdist, hp.noncanonical, hp.strandpref, hp.allhits)
     h = ctypes.c_void_p()
-    N.check(N.lib().fc2_fasta_open(options.genome.encode(), 0, ctypes.byref(h)))
+    rc = N.lib().fc2_fasta_open(options.genome.encode(), 0, ctypes.byref(h))
+    assert (rc == N.FC2_E_IO) == of.dummy, (rc, of.dummy)      # the product's test of the same condition
+    if of.dummy:
+        _dummy_warning(options.genome)
+        h = None
+    else:
+        N.check(rc)
     names = []
-    for i in range(N.lib().fc2_fasta_n_chrom(h)):
+    for i in range(N.lib().fc2_fasta_n_chrom(h) if h else 0):
         nm = ctypes.c_char_p()
         N.check(N.lib().fc2_fasta_chrom(h, i, ctypes.byref(nm), None, None, None, None, None))
         names.append(nm.value.decode())
     to_oracle = np.array([of.names.index(nm) for nm in names] or [0], np.int64)   # handle index -> oracle index
+    if of.dummy:
+        to_oracle = np.zeros(1, np.int64)
     code = {c: i for i, c in enumerate("ACGTN")}
     rc = str.maketrans("ACGTN", "TGCAN")
     hpp = hp.params()
@@ -72,6 +82,8 @@ def oracle_batch_engine(options, hp):
         rp = [bytes(reads[int(o):int(o) + int(l)]) for o, l in zip(read_off, lens)]
         skip = (pairs["flags"] & N.PAIR_SKIP) != 0
         idx = np.where(skip, -1, to_oracle[np.minimum(pairs["chrom"].astype(np.int64), len(to_oracle) - 1)])
+        if of.dummy:
+            idx = np.where(skip, -1, 0)
         r = oracle.scan_fasta(p, of, rp, idx, pairs["a_pos"], pairs["b_aend"],
                               (pairs["flags"] & N.PAIR_BACKSPLICE) != 0, (pairs["flags"] & N.PAIR_PRIMARY_REV) != 0,
                               use_fast=False, all_ties=True)
@@ -109,7 +121,12 @@ def oracle_batch_engine(options, hp):
         res["info"] = info.astype(np.uint16)
         return res.view(np.int64), tm
 
-    return evaluate, names, h, False
+    return evaluate, names, h, of.dummy
+
+
+def _dummy_warning(path):
+    import logging
+    logging.getLogger("GenomeAccessor").warning("Could not access '%s'. Switching to dummy mode (only Ns)" % path)
 
 
 oracle_evaluator_factory.batch = oracle_batch_engine

@@ -124,3 +124,53 @@ def make_spans(genome: Dict[str, str], n: int, seed: int, L=(60, 160), asize=15,
 
 def load_genome(path: str) -> Dict[str, str]:
     return read_fasta(path)
+
+
+def make_odd_spans(genome: Dict[str, str], n: int, seed: int, asize=15, margin=2) -> List[SmallSpan]:
+    """Spans at the edges of find_breakpoints' input domain (find_circ.py:854-974): read parts of
+    0..4 bases and of 2e-2 .. 2e+3 bases (e = asize - margin, so the internal part read[e:-e] is
+    empty or one base long), windows that start past a chromosome's end or end before its start
+    (get_data pads them with 'N' to more than the requested length, :194-211), next to ordinary
+    spans.  Reads are genome text around a random junction, so some candidates qualify."""
+    rng = np.random.default_rng(seed)
+    names = list(genome)
+    e = asize - margin
+    out: List[SmallSpan] = []
+    while len(out) < n:
+        ci = int(rng.integers(len(names)))
+        chrom = names[ci]
+        g = genome[chrom]
+        G = len(g)
+        u = rng.random()
+        if u < 0.35:
+            L = int(rng.integers(0, 5))
+        elif u < 0.7:
+            L = int(rng.integers(max(0, 2 * e - 2), max(1, 2 * e + 4)))
+        else:
+            L = int(rng.integers(max(1, 2 * e), max(2, 2 * e + 60)))
+        v = rng.random()
+        if v < 0.2:                                        # windows past the chromosome's end
+            a_pos = G + int(rng.integers(-5, 40))
+            b_aend = G + int(rng.integers(-5, 80))
+        elif v < 0.4:                                      # windows before its start
+            a_pos = int(rng.integers(-40, 8))
+            b_aend = int(rng.integers(-20, 30))
+        else:
+            a_pos = int(rng.integers(0, max(1, G - 1)))
+            b_aend = int(rng.integers(0, max(1, G)))
+        kA = L // 2
+        src = rng.random() < 0.6
+        if src and 0 <= a_pos and a_pos + kA <= G and b_aend - (L - kA) >= 0 and b_aend <= G:
+            read = g[a_pos:a_pos + kA] + g[b_aend - (L - kA):b_aend]
+        else:
+            read = "".join("ACGTN"[int(c)] for c in rng.integers(0, 5, L))
+        bs = rng.random() < 0.5
+        a_aend = a_pos + kA
+        b_pos = b_aend - (L - kA)
+        if bs and b_pos >= a_aend:                         # is_backsplice = b_pos < a_aend (:842)
+            b_pos = a_aend - 1 - int(rng.integers(0, 50))
+        elif not bs and b_pos < a_aend:
+            b_pos = a_aend + int(rng.integers(0, 50))
+        out.append(SmallSpan(chrom, ci, int(a_pos), int(a_aend), int(b_pos), int(b_aend), read.encode(),
+                             bool(rng.random() < 0.5)))
+    return out

@@ -47,8 +47,12 @@ def test_info_calls(L):
     for L_, t in ((26 + 62, 2), (26 + 63, 4), (26 + 127, 6), (26 + 126, 4)):
         assert L.fc2_batch_geometry(ctypes.byref(p), L_, ctypes.byref(rw), ctypes.byref(nw), ctypes.byref(tw)) == 0
         assert tw.value == t, (L_, tw.value)
-    bad = N.Params(2, 2, 2, 0, 0, 0, 0)
-    assert L.fc2_batch_geometry(ctypes.byref(bad), 100, None, None, None) == N.FC2_E_PARAM
+    # asize <= margin is the reference's own (degenerate) search (find_circ.py:895), not an error
+    e0 = N.Params(2, 2, 2, 0, 0, 0, 0)
+    assert L.fc2_batch_geometry(ctypes.byref(e0), 100, ctypes.byref(rw), ctypes.byref(nw), ctypes.byref(tw)) == 0
+    assert tw.value == 2 * ((100 + 2 + 63) // 64)
+    bad = N.Params(2, 70000, 2, 0, 0, 0, 0)
+    assert L.fc2_batch_geometry(ctypes.byref(bad), 100, None, None, None) == N.FC2_E_RANGE
     assert b"asize - margin" in L.fc2_last_error()
 
 
@@ -321,14 +325,17 @@ def test_bytepath_arena_matches_reference_windows(L, tmp_path):
         lenI, lenA, lenB = np.frombuffer(arena[o:o + 12].tobytes(), np.int32)
         l = len(s.read_part) - 2 * e
         assert lenI == max(0, l)
-        I = arena[o + 12:o + 12 + lenI].tobytes()
+        I = arena[o + 16:o + 16 + lenI].tobytes()
         assert I == s.read_part[e:len(s.read_part) - e].upper()
         if l >= 0:
-            A = arena[o + 12 + lenI:o + 12 + lenI + lenA].tobytes()
-            B = arena[o + 12 + lenI + lenA:o + 12 + lenI + lenA + lenB].tobytes()
+            # header: the windows' full lengths; body: l + 3 byte slots holding their first bytes
+            slot = l + 3
+            A = arena[o + 16 + lenI:o + 16 + lenI + min(lenA, slot)].tobytes()
+            B = arena[o + 16 + lenI + slot:o + 16 + lenI + slot + min(lenB, slot)].tobytes()
             ra = ref.get_data(s.chrom, s.a_pos + e, s.a_pos + e + l + 2).upper()
             rb = ref.get_data(s.chrom, s.b_aend - e - l - 2, s.b_aend - e).upper()
-            assert A == ra[:l + 3] and B == rb[:l + 3]
+            assert (lenA, lenB) == (len(ra), len(rb))
+            assert A == ra[:slot] and B == rb[:slot]
     L.fc2_fasta_close(h)
 
 

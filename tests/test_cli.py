@@ -21,7 +21,9 @@ def _reads(path):
     return [(n, seqs[n.split()[0]]) for n in names]
 
 
-def run_cli(tmp_path, fa, reads, extra=(), bam=False, evaluator=oracle_evaluator_factory, tag="out"):
+def run_cli(tmp_path, fa, reads, extra=(), bam=False, evaluator=oracle_evaluator_factory, tag="out", genome_arg=None):
+    """Align `reads` to `fa` (tests/bwa_emul.py) and run the CLI on them; `genome_arg` is what -G
+    gets (default: fa itself)."""
     genome = read_fasta(fa)
     sam = sam_text(genome, reads)
     inp = str(tmp_path / ("in.bam" if bam else "in.sam"))
@@ -30,7 +32,8 @@ def run_cli(tmp_path, fa, reads, extra=(), bam=False, evaluator=oracle_evaluator
     else:
         open(inp, "w").write(sam)
     out = str(tmp_path / tag)
-    rc = cli.main(["-G", fa, "-o", out, "-n", "test", "-q"] + list(extra) + [inp], evaluator_factory=evaluator)
+    rc = cli.main(["-G", genome_arg or fa, "-o", out, "-n", "test", "-q"] + list(extra) + [inp],
+                  evaluator_factory=evaluator)
     return rc, out
 
 

@@ -221,3 +221,45 @@ def test_gpu_cli_bam_on_stdin_equals_oracle_cli(tmp_path, extra):
     feeder.wait()
     assert r.returncode == 0, r.stderr.decode()[-3000:]
     same(o1, o2)
+
+
+@pytest.mark.parametrize("extra", [[], ["--python-caller"], ["--non-canonical", "--all-hits", "-d", "0"]])
+def test_gpu_cli_genome_folder_dummy_mode_equals_oracle(tmp_path, extra):
+    """-G <folder> (find_circ.py:386): file() raises IOError (:117, :124), GenomeAccessor runs in
+    all-N dummy mode (:338-345) -- the GPU CLI writes what the oracle CLI writes, no junctions."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import shutil
+    fa = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    folder = tmp_path / "folder"
+    folder.mkdir()
+    shutil.copy(fa, str(folder / "chr_CDR1as.fa"))
+    rd = _reads(os.path.join(GOLDEN, "cdr1as_reads.fa"))
+    rc1, o1 = run_cli(tmp_path, fa, rd, extra=extra, tag="oracle", genome_arg=str(folder))
+    rc2, o2 = run_cli(tmp_path, fa, rd, extra=extra, evaluator=None, tag="gpu", genome_arg=str(folder))
+    assert rc1 == rc2 == 0
+    _compare(o1, o2)
+    for o in (o1, o2):
+        assert "Switching to dummy mode" in open(os.path.join(o, "run.log")).read()
+        assert [l for l in open(os.path.join(o, "circ_splice_sites.bed")) if not l.startswith("#")] == []
+
+
+@pytest.mark.parametrize("opts", [["-a", "2", "-m", "2", "-d", "0"], ["-a", "10", "-m", "12", "-d", "0"],
+                                  ["-a", "2", "-m", "2", "-d", "2"], ["-a", "3", "-m", "3", "-d", "1",
+                                                                      "--non-canonical"]])
+def test_gpu_cli_asize_le_margin_equals_oracle(tmp_path, opts):
+    """asize <= margin (find_circ.py:882, :895): with -d 0 every span finds no breakpoint and the
+    run completes; with -d > 0 numpy's shape failure (:861-863) ends the run (exit 1) at the first
+    span record_hits evaluates -- the GPU CLI does what the oracle CLI does."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    rd = _reads(os.path.join(GOLDEN, "test_reads.fa"))
+    for extra in (opts, opts + ["--python-caller"]):
+        rc1, o1 = run_cli(tmp_path, fa, rd, extra=extra, tag="oracle")
+        rc2, o2 = run_cli(tmp_path, fa, rd, extra=extra, evaluator=None, tag="gpu")
+        assert rc1 == rc2
+        if "-d" in opts and opts[opts.index("-d") + 1] == "0":
+            assert rc1 == 0
+        if rc1 == 0:
+            _compare(o1, o2)

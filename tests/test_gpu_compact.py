@@ -152,3 +152,83 @@ def test_compact_scan_hg19_shaped_batch_and_refusals():
     for bad in (Options(noncanonical=True), Options(allhits=True)):
         with pytest.raises(Exception):
             scan_compact(bad, g, b, buf.data_ptr(), 2, 0, 0, ctr_t.data_ptr())
+
+
+@pytest.mark.parametrize("width", [2, 4])
+def test_sharded_zero_copy_merge_with_escapes(width):
+    """bench.py's configs[3] merge on escape-heavy pairs (long reads, -d 6): sub-batch views of one
+    batch dealt to 3 "ranks" (shard.round_bounds / my_bounds) each scan straight into ONE page-locked
+    SharedCompactResults through its device address (words at the batch's input offset, escapes into
+    the batch's slots with batch-relative indices, the count into its slot); merged() -- escapes()
+    adding each batch's start back, then fc2_result_expand -- equals the 8-byte scan of the whole
+    batch word for word."""
+    from find_circ2_amd.hotpath import host_device_pointer, scan_compact
+    from find_circ2_amd.shard import SharedCompactResults, my_bounds, round_bounds
+    dev = _dev()
+    path = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    opt = Options(maxdist=6, margin=0)
+    spans = make_spans(load_genome(path), 12000, seed=909, asize=opt.asize, L=(60, 300), p_readN=0.05)
+    g = genome(path)
+    b, out = run_spans(opt, g, spans)
+    assert b.m_bytepath == 0
+    ref = out.results[:b.n].cpu().numpy()
+    ws = 3
+    bounds = round_bounds(b.n, ws, per_rank=2, align=512, tail=2)
+    cap = 4096
+    m = SharedCompactResults(b.n, bounds, cap, create=True, pin=True, width=width)
+    try:
+        m.array[:] = 0x5A                                          # poison: every word must be written
+        zdev = host_device_pointer(m.array.ctypes.data)
+        zblk = 16 * (cap + 1)
+        ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+        n_esc = 0
+        for rank in range(ws):
+            for k, lo, hi in my_bounds(bounds, rank, ws):
+                eb = zdev + m._w_bytes + k * zblk
+                scan_compact(opt, g, b.sub(lo, hi), zdev + width * lo, width, eb, cap, ctr.data_ptr(), eb + 16 * cap)
+        torch.cuda.synchronize(dev)
+        n_esc = int(m.esc_count.sum())
+        assert (m.esc_count <= cap).all()
+        if width == 2:
+            assert n_esc > 100 and (m.esc_count[:len(bounds)] > 0).sum() >= 3
+        assert np.array_equal(m.merged(opt), ref)
+    finally:
+        m.close()
+
+
+@pytest.mark.parametrize("width", [2, 4])
+def test_compact_launch_marks_byte_path_pairs(width):
+    """fc2_bp_scan_compact_launch takes no byte-path pairs (fc2_bp.h); a C host that passes some
+    gets the escape word without an escape record for each of them, so fc2_result_expand fails
+    (FC2_E_FORMAT) instead of decoding whatever the word held before."""
+    import ctypes
+    dev = _dev()
+    path = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    opt = Options()
+    spans = make_spans(load_genome(path), 600, seed=5, asize=opt.asize, L=(60, 120))
+    reads = [s.read_part for s in spans]
+    reads[17] = reads[17][:30] + b"R" + reads[17][31:]           # an IUPAC byte: byte-exact path
+    from find_circ2_amd import PairBatch
+    g = genome(path)
+    flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) for s in spans]
+    b = PairBatch.pack(opt, g, reads, [s.a_pos for s in spans], [s.b_aend for s in spans],
+                       [g.chrom_index_or_missing(s.chrom) for s in spans], flags)
+    assert b.m_bytepath >= 1
+    n = b.n
+    words = torch.full((n * width // 2 + 8,), 0x2A2A, dtype=torch.int16, device=dev)   # stale contents
+    esc = torch.zeros(16 * 64, dtype=torch.uint8, device=dev)
+    ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+    co = N.CompactOut(width, 64, words.data_ptr(), esc.data_ptr(), ctr.data_ptr(), None)
+    p, gv, bv = opt.params(), g.view(), b.view()
+    N.check(N.lib().fc2_bp_scan_compact_launch(ctypes.byref(p), ctypes.byref(gv), ctypes.byref(bv),
+                                               ctypes.byref(co), torch.cuda.current_stream(dev).cuda_stream))
+    torch.cuda.synchronize(dev)
+    k = int(ctr.item())
+    w = words.cpu().numpy().view(np.uint16 if width == 2 else np.uint32)[:n]
+    e = esc.cpu().numpy().view(N.ESCAPE_DTYPE)[:min(k, 64)]
+    bp = np.nonzero(b.host_pairs["flags"] & N.PAIR_BYTEPATH)[0]
+    marker = N.R16_ESCAPE if width == 2 else N.R32_ESCAPE
+    assert (w[bp] == marker).all()
+    with pytest.raises(N.Fc2Error) as ei:
+        expand(opt, w, e)
+    assert ei.value.code == N.FC2_E_FORMAT

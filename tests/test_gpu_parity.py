@@ -13,7 +13,7 @@ import pytest
 import oracle
 from conftest import GOLDEN
 from gpu_helpers import assert_same, gpu_arrays, oracle_arrays
-from synth_small import load_genome, make_spans
+from synth_small import load_genome, make_odd_spans, make_spans
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -130,6 +130,56 @@ def test_word_layout_vs_oracle(fa, oi):
     assert ga["done"].all()
     hits = assert_same(ga, oracle_arrays(r), label=f"word layout {fa} {o}")
     assert hits > 100
+
+
+ODD_OPTS = [
+    dict(asize=2, margin=2, maxdist=0),          # eff_a = 0: read[0:0] == '' (find_circ.py:895)
+    dict(asize=2, margin=2, maxdist=2),
+    dict(asize=10, margin=12, maxdist=0),        # eff_a < 0: read[-2:2]
+    dict(asize=10, margin=12, maxdist=3),
+    dict(asize=3, margin=3, maxdist=1, noncanonical=True, allhits=True),
+    dict(),                                       # one-base internal parts against over-long windows
+    dict(asize=6, margin=2, maxdist=40, noncanonical=True),
+]
+
+
+@pytest.mark.parametrize("dummy", [False, True], ids=["fasta", "dummy"])
+@pytest.mark.parametrize("oi", range(len(ODD_OPTS)))
+def test_degenerate_spans_vs_oracle(oi, dummy):
+    """asize <= margin (every pair takes the byte-exact kernel), read parts of 0..4 bases and of
+    2e +- 3 bases, windows past either chromosome end, on the FASTA and on GenomeAccessor's dummy
+    genome (find_circ.py:338-345): pair by pair against the oracle, incl. numpy's broadcast of a
+    one-byte operand and its shape failure (:861-863)."""
+    o = ODD_OPTS[oi]
+    opt = Options(**o)
+    path = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    g = Genome.dummy_genome(device=_dev()) if dummy else genome(path)
+    spans = make_odd_spans(load_genome(path), 2000, seed=31 + oi, asize=opt.asize, margin=opt.margin)
+    flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.primary_reverse else 0)
+             for s in spans]
+    b = PairBatch.pack(opt, g, [s.read_part for s in spans], [s.a_pos for s in spans], [s.b_aend for s in spans],
+                       [0 if dummy else g.chrom_index_or_missing(s.chrom) for s in spans], flags)
+    if opt.eff_a <= 0:
+        assert b.m_bytepath == len(spans)
+    out = scan(opt, g, b)
+    torch.cuda.synchronize()
+    of = oracle.OracleFasta.dummy_genome() if dummy else oracle.OracleFasta(path)
+    r = oracle.scan_fasta(oracle.params(**o), of, [s.read_part for s in spans],
+                          [0 if dummy else of.names.index(s.chrom) for s in spans], [s.a_pos for s in spans],
+                          [s.b_aend for s in spans], [s.is_backsplice for s in spans],
+                          [s.primary_reverse for s in spans], use_fast=False, all_ties=True)
+    ga = gpu_arrays(opt, b.host_pairs, out.host(b.n))
+    assert ga["done"].all()
+    assert_same(ga, oracle_arrays(r), label=f"odd spans {o} dummy={dummy}")
+    if opt.allhits:
+        got = decode_splices(opt, g, b, out, raise_errors=False)
+        for i, ties in enumerate(got):
+            if r.n_ties[i] < 0:
+                continue
+            exp = r.ties_of(i)
+            assert [(t.start, t.end, t.strand, t.gtag, int(t.dist), t.ov, t.n_hits) for t in ties] == \
+                [(int(e["start"]), int(e["end"]), e["strand"].decode(), e["gtag"].decode(), int(e["dist"]),
+                  int(e["ov"]), int(e["n_hits"])) for e in exp], i
 
 
 @pytest.mark.parametrize("o", [dict(), dict(allhits=True, noncanonical=True, strandpref=True)])

@@ -579,3 +579,36 @@ def test_native_caller_close_before_parse_threads_run(tmp_path):
             rc = N.lib().fc2_caller_next(nc.h, ctypes.byref(batch), ctypes.byref(eof))
             assert rc == (N.FC2_OK if k < 2 else rc)   # one record: the reference's UnboundLocalError
             nc.close()
+
+
+def test_submit_compact_checks_word_count(tmp_path):
+    """fc2_caller_submit_compact takes the words' count and refuses one that is not the queued
+    chunk's pair count (it would read past the words otherwise)."""
+    import ctypes
+
+    import numpy as np
+
+    from find_circ2_amd import _native as N
+    from find_circ2_amd.caller import CallerOptions
+    from find_circ2_amd.native_caller import NativeCaller
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 50, seed=7)
+    from bwa_emul import read_fasta
+    nc = NativeCaller(sam, False, CallerOptions(), list(read_fasta(fa)), write_reads=False, write_multi=False,
+                      genome_dummy=True)
+    nc.open()
+    try:
+        batch, eof = N.CallerBatch(), ctypes.c_int(0)
+        while True:
+            N.check(N.lib().fc2_caller_next(nc.h, ctypes.byref(batch), ctypes.byref(eof)))
+            if batch.n or eof.value:
+                break
+        n = int(batch.n)
+        assert n > 1
+        words = np.zeros(n, np.uint32)
+        L = N.lib()
+        rc = L.fc2_caller_submit_compact(nc.h, words.ctypes.data, 4, n - 1, None, 0, None, 0, n)
+        assert rc == N.FC2_E_PARAM and b"words for a batch of" in L.fc2_last_error()
+        assert L.fc2_caller_submit_compact(nc.h, words.ctypes.data, 4, n, None, 0, None, 0, n) == N.FC2_OK
+    finally:
+        nc.close()
