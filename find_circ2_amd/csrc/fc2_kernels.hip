@@ -276,8 +276,9 @@ __global__ __launch_bounds__(kBlock) void bp_scan_kernel(fc2_params p, fc2_genom
     const int64_t wsA = (int64_t)pr.a_pos + e;
     const int64_t wsB = (int64_t)pr.b_aend - e - W;
     // get_data is only length-preserving for start <= size and end >= 0; the host
-    // routes anything else to the byte kernel -- flag defensively here.
-    if (wsA > csize || wsA + W < 0 || wsB > csize || wsB + W < 0) {
+    // routes anything else to the byte kernel -- flag defensively here.  The dummy
+    // genome's "N"*(end-start) (find_circ.py:370-371) has the requested length anywhere.
+    if (!g.dummy && (wsA > csize || wsA + W < 0 || wsB > csize || wsB + W < 0)) {
         st_stream<NT>(out + i, nohit_result(FC2_RES_ERR_WIN));
         if (want_ties)
             for (uint32_t k = 0; k < tw; ++k) tiemask[(uint64_t)k * bv.stride + i] = 0;

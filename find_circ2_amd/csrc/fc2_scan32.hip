@@ -929,8 +929,9 @@ __device__ __forceinline__ void scan_pair(const fc2_params &p, const fc2_genome_
     }
     const int64_t wsA = (int64_t)pr.a_pos + e;
     const int64_t wsB = (int64_t)pr.b_aend - e - W;
+    // (the dummy genome's "N"*(end-start), find_circ.py:370-371, has the requested length anywhere)
     if (active && ((pr.flags & FC2_PAIR_SKIP) || l < 0 || l > 32 * NQ - 2 || pr.chrom >= g.n_chrom ||
-                   wsA > csize || wsA + W < 0 || wsB > csize || wsB + W < 0)) {
+                   (!g.dummy && (wsA > csize || wsA + W < 0 || wsB > csize || wsB + W < 0)))) {
         // skipped / empty x-range: no hit; anything else is routed to the byte path by the host
         const bool err = !(pr.flags & FC2_PAIR_SKIP) && l >= 0;
         Best32 none;
