@@ -9,13 +9,17 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <deque>
+#include <exception>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
 #include <set>
 #include <stdexcept>
 #include <string>
+#include <thread>
 #include <tuple>
 #include <unordered_map>
 #include <unordered_set>
@@ -426,6 +430,172 @@ class HitVec {
     size_t n_ = 0;
 };
 
+// ---- the recording side, parallel (fc2_caller_submit) --------------------------------------
+// record_hits (:1276-1439) touches three kinds of state: the fragment's own (its spans' results,
+// the coordinates, flags and rows it derives from them), the junction tables (Hit.add of every
+// splice, :526-582, and the flags), and the names, given by first appearance (:684-686).  A chunk
+// is therefore recorded in phases: (A) the fragments, cut into contiguous ranges, on all workers:
+// everything record_hits decides from the fragment alone, including every exception it can raise,
+// with each table update emitted as an event for the shard that owns the junction's coordinate;
+// (B) the shards on all workers, each applying its events in input order -- so every float sum
+// of a junction (:544, :563, :579) and every min / last-value field sees its updates in the
+// sequential order; (C) one thread names the chunk's new junctions by merging the shards' first
+// appearances; (D) the ranges again: the read names and multi_events rows, which need the names,
+// written per range and joined in input order.
+constexpr int kShards = 16;
+
+struct JRef {                                  // a junction: its shard and its index there
+    uint32_t shard = 0, idx = 0;
+};
+
+struct Shard {
+    HitVec hits[2];                            // 0 circ, 1 lin; never relocated
+    CIndex index[2];                           // coordinate -> index in hits
+    Arena strings;                             // the hits' read names, canonical reads, fragment names
+    std::vector<std::pair<uint64_t, uint32_t>> fresh[2];   // this chunk's new junctions: (seq, idx)
+};
+
+inline int shard_of(const CKey &k) { return (int)(CKeyHash()(k) >> 60) & (kShards - 1); }
+
+struct SEv {                                   // one table update of a shard (phase A -> B)
+    uint64_t seq;                              // fragment index << 20 | the fragment's add ordinal
+    CKey key;
+    uint32_t frag;                             // fragment index in the chunk
+    uint32_t slot;                             // the range's slot: written (add) / read (flag)
+    int32_t span;                              // Splice.junc_span (a span of the chunk)
+    int32_t dist, ov, n_hits;
+    uint8_t kind;                              // 0 circ, 1 lin
+    uint8_t op;                                // 0 Hit.add (+ the read), 1 add_flag
+    uint8_t warn;                              // op 1: the flag
+    uint8_t dist_bool;                         // -d 0: dist is simple_match's bool
+    uint8_t mate, gtag_len;
+    char gtag[6];
+};
+
+struct FOut {                                  // a fragment with junctions (phase A -> D)
+    uint32_t frag;
+    uint32_t warns;
+    uint32_t j0, nj;                           // its distinct junctions: RangeOut::jk[j0, j0 + nj)
+    int64_t m0 = -1;                           // multi_events row: parts at RangeOut::mtext[m0, ...)
+    uint32_t m1 = 0, m2 = 0;                   // ... lengths of the text before / after the name
+    uint32_t circ_slot = 0;
+};
+
+struct RangeOut {                              // one range of a chunk's fragments
+    std::vector<SEv> ev[kShards];
+    std::vector<JRef> slots;                   // one per add event, resolved in phase B
+    std::vector<FOut> fouts;
+    std::vector<std::pair<uint8_t, uint32_t>> jk;   // (kind, slot) of FOut junctions
+    std::string mtext, test, out0, out1;
+    std::vector<std::pair<const char *, double>> N;
+    int64_t err_frag = -1;                     // the first fragment that raised (phase A), or -1
+    int err_code = 0;
+    std::string err_msg;
+    void clear() {
+        for (auto &v : ev) v.clear();
+        slots.clear();
+        fouts.clear();
+        jk.clear();
+        mtext.clear();
+        test.clear();
+        out0.clear();
+        out1.clear();
+        N.clear();
+        err_frag = -1;
+        err_code = 0;
+        err_msg.clear();
+    }
+};
+
+// Fork-join workers: run(n, f) calls f(0) .. f(n-1) on the workers and the calling thread and
+// returns when all have returned.  Tasks are claimed from a counter tagged with the run's
+// generation, so a worker still leaving the previous run can never take a task of this one.
+class WorkPool {
+  public:
+    explicit WorkPool(int n_workers) {
+        for (int k = 0; k < n_workers; ++k) th_.emplace_back([this] { loop(); });
+    }
+    ~WorkPool() {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto &t : th_) t.join();
+    }
+    int size() const { return (int)th_.size() + 1; }
+    // as run, with an exception of a task (bad_alloc, a Fatal) handed to the caller after all
+    // tasks returned: the first one, by task index
+    void run_checked(int n, const std::function<void(int)> &f) {
+        std::vector<std::exception_ptr> ex((size_t)std::max(n, 0));
+        run(n, [&](int k) {
+            try {
+                f(k);
+            } catch (...) {
+                ex[(size_t)k] = std::current_exception();
+            }
+        });
+        for (auto &e : ex)
+            if (e) std::rethrow_exception(e);
+    }
+    void run(int n, const std::function<void(int)> &f) {
+        if (n <= 0) return;
+        if (n == 1 || th_.empty()) {
+            for (int k = 0; k < n; ++k) f(k);
+            return;
+        }
+        uint64_t g;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            job_ = &f;
+            n_ = n;
+            done_ = 0;
+            g = ++gen_;
+            next_.store(g << 32);
+        }
+        cv_.notify_all();
+        work(g, &f, n);
+        std::unique_lock<std::mutex> lk(m_);
+        done_cv_.wait(lk, [&] { return done_ == n; });
+    }
+  private:
+    std::vector<std::thread> th_;
+    std::mutex m_;
+    std::condition_variable cv_, done_cv_;
+    const std::function<void(int)> *job_ = nullptr;
+    int n_ = 0, done_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+    std::atomic<uint64_t> next_{0};
+    void work(uint64_t g, const std::function<void(int)> *job, int n) {
+        for (;;) {
+            uint64_t v = next_.load();
+            do {
+                if ((v >> 32) != g || (int)(v & 0xFFFFFFFFu) >= n) return;
+            } while (!next_.compare_exchange_weak(v, v + 1));
+            (*job)((int)(v & 0xFFFFFFFFu));
+            std::lock_guard<std::mutex> lk(m_);
+            if (++done_ == n) done_cv_.notify_all();
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            const std::function<void(int)> *job;
+            int n;
+            {
+                std::unique_lock<std::mutex> lk(m_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+                job = job_;
+                n = n_;
+            }
+            work(seen, job, n);
+        }
+    }
+};
+
 }  // namespace
 
 struct fc2_caller {
@@ -478,14 +648,17 @@ struct fc2_caller {
     // fc2_caller_stats' values, published by fc2_caller_next on the thread that advances the input
     // (a recording thread may ask for them while the reader runs)
     std::atomic<uint64_t> st_reads{0}, st_pairs{0};
-    // aggregation
-    struct Storage {
-        std::string prefix;
-        HitVec hits;                            // insertion (= dict) order; never relocated
-        Arena strings;                          // the hits' read names, canonical reads, fragment names
-        CIndex index;
-        int64_t novel = 0;
-    } st[2];                                    // 0 circ, 1 lin
+    // aggregation: SpliceSiteStorage (:657-730) of circ (0) and linear (1) junctions, its dict cut
+    // into kShards shards by the coordinate's hash (Shard); the dict order -- known sites, then
+    // junctions by first appearance, which also gives the names (:684-686) -- is kept in order[]
+    Shard sh[kShards];
+    std::vector<JRef> order[2];                 // every junction in insertion (= dict) order
+    int64_t novel[2] = {0, 0};                  // junctions named so far (:684-686)
+    std::string prefix[2] = {"circ", "lin"};
+    // the recording side's workers and per-range scratch (fc2_caller_submit)
+    std::unique_ptr<WorkPool> pool;
+    std::vector<RangeOut> ranges;
+    size_t min_range_frags = 2048;              // fragments per range at least (FC2_CALLER_MIN_RANGE)
     std::unordered_map<std::string, uint32_t> ids;    // interned chromosome / strand strings (submit side)
     std::vector<std::string> id_names;                // ... and back
     std::vector<int64_t> tid_cid;                     // reference id -> interned chromosome (submit side)
@@ -582,9 +755,25 @@ void CanonSet::insert(const std::string &read, Arena &a) {
     canon.insert(rc, a);
 }
 
+// Hit.add of a splice from the chunk (:547-582) as phase B applies it: the checks that raise
+// (stranded, :532-533; a non-integer anchor quality, :558-566; rev_comp of the read, :573-582)
+// already passed in phase A (check_add)
+void hit_apply(const fc2_caller *h, Hit &t, const SEv &e) {
+    t.signal.assign(e.gtag, e.gtag_len);
+    t.added = true;
+    t.edits.add(e.dist, e.dist_bool != 0);
+    t.overlaps.add(e.ov, false);
+    t.n_hits.add(e.n_hits, false);
+    const Span &s = h->spans[(size_t)e.span];
+    t.n_spanned += 1;
+    t.n_weighted += s.weight;
+    if (s.qA && s.qB) t.n_uniq_bridges += s.weight;
+    if (!t.has_mq) { t.has_mq = true; t.mq_a = s.qA; t.mq_b = s.qB; }
+    else { t.mq_a = std::max(t.mq_a, s.qA); t.mq_b = std::max(t.mq_b, s.qB); }
+}
+
 // the span-dependent part of Hit.add that needs the fragment's primary
-void hit_add_read(fc2_caller *h, int kind, Hit &t, const Span &s, const Align &prim) {
-    Arena &a = h->st[kind].strings;
+void hit_add_read(Arena &a, Hit &t, const Span &s, const Align &prim) {
     t.readnames.insert(prim.qname, a);
     const std::string &read = prim.seq;
     check_comp(read);                           // rev_comp(read) raises here (:573, :582)
@@ -599,7 +788,7 @@ void hit_name(const fc2_caller *h, int kind, const Hit &t, std::string &out) {
     if (!t.novel) { out += t.known_name; return; }
     out += h->name;                             // name + "_%s_%06d" % (prefix, novel)
     out += '_';
-    out += h->st[kind].prefix;
+    out += h->prefix[kind];
     out += '_';
     char d[24];
     int n = 0;
@@ -608,34 +797,12 @@ void hit_name(const fc2_caller *h, int kind, const Hit &t, std::string &out) {
     while (n) out += d[--n];
 }
 
-std::string hit_name(const fc2_caller *h, int kind, const Hit &t) {
-    std::string r;
-    hit_name(h, kind, t, r);
-    return r;
-}
-
-size_t storage_add(fc2_caller *h, int kind, const Splice &sp, const Align *prim) {
-    auto &S = h->st[kind];
-    const CKey key = coord_key(h, sp);
-    const auto ins = S.index.try_emplace(key, S.hits.size());
-    const size_t k = ins.first;
-    if (ins.second) {                           // a new junction: named by first appearance (:684-686)
-        S.novel += 1;
-        Hit &t = S.hits.emplace_back();
-        t.novel = S.novel;
-        t.key = key;
-        hit_add(h, t, sp);
-    } else {
-        hit_add(h, S.hits[k], sp);
-    }
-    if (sp.span >= 0) hit_add_read(h, kind, S.hits[k], h->spans[sp.span], *prim);
-    return k;
-}
-
-void add_flag(fc2_caller *h, Hit &t, uint32_t w, const std::string &frag) {
+void add_flag(Arena &a, Hit &t, uint32_t w, const std::string &frag) {
     t.flag_n[w] += 1;
-    t.read_flags.add(frag, 1u << w, h->st[0].strings);
+    t.read_flags.add(frag, 1u << w, a);
 }
+
+const Hit &hit_at(const fc2_caller *h, int kind, const JRef &j) { return h->sh[j.shard].hits[kind][j.idx]; }
 
 // categories (:601-654) as literals, into cats[]; returns how many
 int categories(const fc2_caller *h, const Hit &t, const char *cats[8]) {
@@ -703,9 +870,8 @@ void app_pymin(std::string &out, const PyMin &m) {
 
 void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :690-730
     const auto &o = h->o;
-    const HitVec &hits = h->st[kind].hits;
-    for (size_t k = 0; k < hits.size(); ++k) {
-        const Hit &t = hits[k];
+    for (const JRef &j : h->order[kind]) {      // dict order
+        const Hit &t = hit_at(h, kind, j);
         if (!t.n_reads) continue;
         const int64_t qa = t.mq_a, qb = t.mq_b;
         if (o.halfunique) {
@@ -768,7 +934,6 @@ uint64_t load_known(fc2_caller *h, int kind, const std::string &path) {
     if (path.empty()) return 0;
     FILE *f = fopen(path.c_str(), "r");
     if (!f) throw Fatal{FC2_E_IO, "IOError: [Errno 2] No such file or directory: " + py_repr(path)};
-    auto &S = h->st[kind];
     uint64_t n = 0;
     std::string line;
     char buf[65536];
@@ -802,9 +967,12 @@ uint64_t load_known(fc2_caller *h, int kind, const std::string &path) {
         sp.ov = 10;
         sp.gtag = "NNNN";
         const CKey key = coord_key(h, sp);
-        const auto ins = S.index.try_emplace(key, S.hits.size());
+        const int si = shard_of(key);
+        Shard &S = h->sh[si];
+        const auto ins = S.index[kind].try_emplace(key, S.hits[kind].size());
         // a repeated coordinate keeps its first dict position, with the later line's Hit
-        Hit &t = ins.second ? S.hits.emplace_back() : S.hits[ins.first];
+        Hit &t = ins.second ? S.hits[kind].emplace_back() : S.hits[kind][ins.first];
+        if (ins.second) h->order[kind].push_back(JRef{(uint32_t)si, (uint32_t)ins.first});
         t = Hit();
         t.known_name = fl[3];
         t.key = key;
@@ -816,7 +984,7 @@ uint64_t load_known(fc2_caller *h, int kind, const std::string &path) {
 }
 
 // ---- fragments ----------------------------------------------------------------------
-std::string chrom_of(fc2_caller *h, int32_t tid) {               // fast_chrom_lookup (:471-477)
+std::string chrom_of(const fc2_caller *h, int32_t tid) {         // fast_chrom_lookup (:471-477)
     const char *nm = fc2_ingest_ref_name(h->ing, tid);
     if (tid < 0 || !nm) throw Fatal{FC2_E_FORMAT, "ValueError: reference id " + i2s(tid) + " out of range"};
     return nm;
@@ -960,8 +1128,20 @@ int score_of(const fc2_caller *h, const std::string &sig, int64_t dist, int64_t 
     return (int)sc;
 }
 
+// the interned chromosome of every span the chunk evaluates, before the workers read tid_cid
+// (a reference id outside the header stays unresolved: decode raises chrom_of's error for it)
+void resolve_chroms(fc2_caller *h) {
+    for (const Span &s : h->spans) {
+        if (s.eval < 0 || (s.tid >= 0 && (size_t)s.tid < h->tid_cid.size() && h->tid_cid[(size_t)s.tid] >= 0)) continue;
+        const char *nm = s.tid >= 0 ? fc2_ingest_ref_name(h->ing, s.tid) : nullptr;
+        if (!nm) continue;
+        if ((size_t)s.tid >= h->tid_cid.size()) h->tid_cid.resize((size_t)s.tid + 1, -1);
+        h->tid_cid[(size_t)s.tid] = intern(h, nm);
+    }
+}
+
 // fills ev (a reused scratch object: its vectors keep their capacity)
-void decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask, uint32_t tw, uint64_t stride,
+void decode(const fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask, uint32_t tw, uint64_t stride,
             Eval &ev) {
     ev.err = 0;
     ev.msg.clear();
@@ -969,9 +1149,8 @@ void decode(fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask,
     const Span &s = h->spans[si];
     const fc2_pair &pr = h->b_pairs[(size_t)s.eval];
     if (s.tid < 0 || (size_t)s.tid >= h->tid_cid.size() || h->tid_cid[(size_t)s.tid] < 0) {
-        const std::string name = chrom_of(h, s.tid);        // raises for an id outside the header
-        if ((size_t)s.tid >= h->tid_cid.size()) h->tid_cid.resize((size_t)s.tid + 1, -1);
-        h->tid_cid[(size_t)s.tid] = intern(h, name);
+        (void)chrom_of(h, s.tid);                          // raises for an id outside the header
+        throw Fatal{FC2_E_PARAM, "native caller: chromosome of span not resolved"};   // (resolve_chroms)
     }
     const int64_t cid = h->tid_cid[(size_t)s.tid];
     const std::string &chrom = h->id_names[(size_t)cid];    // (nothing below interns a new name)
@@ -1166,7 +1345,7 @@ void parse_truth(const std::string &align_str, bool stranded, std::set<Coord> &l
     }
 }
 
-std::string test_row(fc2_caller *h, const Frag &fr, const std::set<Coord> &lin_coords,
+std::string test_row(const fc2_caller *h, const Frag &fr, const std::set<Coord> &lin_coords,
                      const std::set<Coord> &circ_coords, const std::vector<UCoord> &unspliced,
                      const std::vector<UCoord> &broken) {                     // :1202-1273
     const std::string &name = fr.name;
@@ -1206,13 +1385,15 @@ std::string test_row(fc2_caller *h, const Frag &fr, const std::set<Coord> &lin_c
     return row + "\n";
 }
 
-std::string multi_row(fc2_caller *h, const Frag &fr, const Hit &circ, const std::set<Coord> &lin_cons,
-                      const std::set<Coord> &lin_incons, const std::set<UCoord> &un_cons,
-                      const std::set<UCoord> &un_incons) {                    // :733-763
+// the multi_events row (:733-763) as the text before and after the circ junction's name, which
+// phase D fills in; raises (need_int) exactly where the row itself would
+void multi_row_parts(const fc2_caller *h, const Frag &fr, const CKey &circ, const std::set<Coord> &lin_cons,
+                     const std::set<Coord> &lin_incons, const std::set<UCoord> &un_cons,
+                     const std::set<UCoord> &un_incons, std::string &p1, std::string &p2) {
     const int64_t score = (int64_t)lin_cons.size() - 10 * (int64_t)lin_incons.size() + (int64_t)un_cons.size() -
                           10 * (int64_t)un_incons.size();
-    std::vector<std::string> cols = {key_chrom(h, circ.key), i2s(circ.key.start), i2s(circ.key.end),
-                                     "ME:" + hit_name(h, 0, circ), i2s(score), key_strand(h, circ.key), fr.name};
+    p1 = key_chrom(h, circ) + "\t" + i2s(circ.start) + "\t" + i2s(circ.end) + "\tME:";
+    std::vector<std::string> cols = {i2s(score), key_strand(h, circ), fr.name};
     std::vector<std::string> v;
     for (const Coord &c : lin_cons) v.push_back(i2s(std::get<1>(c)) + "-" + i2s(std::get<2>(c)));
     cols.push_back(v.empty() ? "NO_LIN_CONS" : join(v, ","));
@@ -1226,7 +1407,7 @@ std::string multi_row(fc2_caller *h, const Frag &fr, const Hit &circ, const std:
     v.clear();
     for (const UCoord &c : un_incons) v.push_back("[" + c.chrom + ":" + i2s(need_int(c.pos)) + "-" + i2s(need_int(c.aend)) + "]");
     cols.push_back(v.empty() ? "NO_UNSPLICED_INCONS" : join(v, ","));
-    return join(cols, "\t") + "\n";
+    p2 = "\t" + join(cols, "\t") + "\n";
 }
 
 // the evaluation results of the pending chunk
@@ -1239,19 +1420,25 @@ struct Results {
 
 // record_hits' per-fragment scratch (find_circ.py:1276-1439): reused objects, so recording a
 // fragment allocates nothing beyond what the junction tables keep
+struct KeySlot {                                // a junction of the fragment: kind, coordinate, slot
+    int kind;
+    CKey key;
+    uint32_t slot;
+};
+
 struct FragScratch {
     std::vector<int> ev_si;                     // find_breakpoints' results of this fragment, by span
     std::vector<Eval> evs;
     size_t n_ev = 0;
-    std::vector<size_t> circ_idx, lin_idx;      // distinct circ / linear junctions (their coords)
-    std::vector<std::pair<int, size_t>> junc;   // every junction the fragment's reads support
+    std::vector<KeySlot> circ, lin, junc;       // distinct circ / linear junctions; every junction
     uint32_t warns = 0;                         // Warn bits
     std::vector<std::string> names;             // write_read: the junction names, sorted
     std::string tail;                           // ... and the name part both mates share
-    void reset() { n_ev = 0; circ_idx.clear(); lin_idx.clear(); junc.clear(); warns = 0; }
+    std::string p1, p2;                         // multi_events row parts
+    void reset() { n_ev = 0; circ.clear(); lin.clear(); junc.clear(); warns = 0; }
 };
 
-const std::vector<Splice> &find_breakpoints(fc2_caller *h, int si, const Results &R, FragScratch &F) {
+const std::vector<Splice> &find_breakpoints(const fc2_caller *h, int si, const Results &R, FragScratch &F) {
     size_t k = 0;
     while (k < F.n_ev && F.ev_si[k] != si) ++k;
     if (k == F.n_ev) {                          // first evaluation of this span in the fragment
@@ -1265,78 +1452,129 @@ const std::vector<Splice> &find_breakpoints(fc2_caller *h, int si, const Results
     return ev.ties;
 }
 
-using HitRef = std::pair<int, size_t>;          // (storage, index)
+// the key of a Splice from decode (cid resolved, strand '+' / '-'): coord_key without interning
+CKey splice_key(const Splice &sp) {
+    const uint32_t c = (uint32_t)sp.cid, st = sp.strand == "-" ? 1u : 0u;
+    return sp.start < sp.end ? CKey{sp.start, sp.end, c, st} : CKey{sp.end, sp.start, c, st};
+}
 
-void add_unique(std::vector<size_t> &v, size_t x) {
-    for (size_t y : v)
-        if (y == x) return;
+// add a junction to a fragment's list unless its coordinate is there (one junction per coordinate)
+void add_unique(std::vector<KeySlot> &v, const KeySlot &x) {
+    for (const KeySlot &y : v)
+        if (y.kind == x.kind && y.key == x.key) return;
     v.push_back(x);
 }
 
-void add_unique(std::vector<HitRef> &v, const HitRef &x) {
-    for (const HitRef &y : v)
-        if (y == x) return;
-    v.push_back(x);
-}
-
-void record_hits(fc2_caller *h, Frag &fr, const Results &R, FragScratch &F) {
+// phase A, one fragment: record_hits (:1276-1439) up to the table updates, which become events;
+// raises Fatal exactly where record_hits would, with the same message
+void phase_a_frag(const fc2_caller *h, uint32_t fi, const Frag &fr, const Results &R, FragScratch &F,
+                  RangeOut &ro) {
     const auto &o = h->o;
     F.reset();
-    HitRef circ{-1, 0};
+    uint32_t ord = 0;
+    auto count = [&](const char *k) { incN_into(ro.N, k, 1.); };
+    // Hit.add of one splice (storage_add, :526-582): the raising checks now, the update as an event
+    auto store = [&](int kind, const Splice &sp, const Span &span) -> KeySlot {
+        if (o.stranded)   // Splice has no strandmatch attribute (:532-533)
+            throw Fatal{FC2_E_FORMAT, "AttributeError: 'Splice' object has no attribute 'strandmatch'"};
+        if (!span.q_int)  // a float / string last AS or XS: Python arithmetic (:558-566)
+            throw Fatal{FC2_E_FORMAT, "native caller: the last AS / XS tags of a junction's anchors must be integers "
+                                      "(use --python-caller)"};
+        check_comp(fr.prim[span.mate].seq);     // rev_comp(read) raises here (:573, :582)
+        SEv e;
+        e.key = splice_key(sp);
+        e.seq = ((uint64_t)fi << 20) | ord++;
+        e.frag = fi;
+        e.slot = (uint32_t)ro.slots.size();
+        ro.slots.emplace_back();
+        e.span = sp.span;
+        e.dist = (int32_t)sp.dist;
+        e.ov = (int32_t)sp.ov;
+        e.n_hits = (int32_t)sp.n_hits;
+        e.kind = (uint8_t)kind;
+        e.op = 0;
+        e.warn = 0;
+        e.dist_bool = sp.dist_bool;
+        e.mate = (uint8_t)span.mate;
+        e.gtag_len = (uint8_t)std::min<size_t>(sp.gtag.size(), sizeof e.gtag);
+        memcpy(e.gtag, sp.gtag.data(), e.gtag_len);
+        ro.ev[shard_of(e.key)].push_back(e);
+        return KeySlot{kind, e.key, e.slot};
+    };
+    auto flag = [&](const KeySlot &j, uint32_t w) {
+        SEv e{};
+        e.key = j.key;
+        e.frag = fi;
+        e.slot = j.slot;
+        e.kind = 0;
+        e.op = 1;
+        e.warn = (uint8_t)w;
+        ro.ev[shard_of(j.key)].push_back(e);
+    };
+    auto finish = [&]() {                       // what write_read / the multi row need later
+        if (F.junc.empty()) return;
+        FOut fo;
+        fo.frag = fi;
+        fo.warns = F.warns;
+        fo.j0 = (uint32_t)ro.jk.size();
+        fo.nj = (uint32_t)F.junc.size();
+        for (const KeySlot &j : F.junc) ro.jk.emplace_back((uint8_t)j.kind, j.slot);
+        ro.fouts.push_back(fo);
+    };
+    KeySlot circ{0, CKey{}, 0};
     for (int si : fr.circ) {
         const Span &span = h->spans[si];
-        if (!(span.uniq >= o.min_uniq_qual)) { incN(h, "circ_junc_not_unique"); continue; }
+        if (!(span.uniq >= o.min_uniq_qual)) { count("circ_junc_not_unique"); continue; }
         const std::vector<Splice> &splices = find_breakpoints(h, si, R, F);
         if (splices.empty()) {
-            incN(h, "circ_no_bp");
+            count("circ_no_bp");
             F.warns |= 1u << W_WARN_UNRESOLVED_EXTRA_BACKSPLICE;
             continue;
         }
-        incN(h, "circ_spliced");
+        count("circ_spliced");
         const size_t n = o.allhits ? splices.size() : 1;
         for (size_t k = 0; k < n; ++k) {
-            const size_t idx = storage_add(h, 0, splices[k], &fr.prim[span.mate]);
-            circ = HitRef(0, idx);
-            add_unique(F.circ_idx, idx);        // circ_coords: one coordinate per junction
+            circ = store(0, splices[k], span);
+            add_unique(F.circ, circ);           // circ_coords: one coordinate per junction
             add_unique(F.junc, circ);
         }
     }
-    if (F.circ_idx.size() > 1) {
-        for (size_t idx : F.circ_idx) {
+    if (F.circ.size() > 1) {
+        for (const KeySlot &j : F.circ) {
             F.warns |= 1u << W_WARN_MULTI_BACKSPLICE;
-            add_flag(h, h->st[0].hits[idx], W_WARN_MULTI_BACKSPLICE, fr.name);
-            add_unique(F.junc, HitRef(0, idx));
+            flag(j, W_WARN_MULTI_BACKSPLICE);
         }
+        finish();
         return;
     }
-    if (F.circ_idx.empty() && o.nolinear) return;
+    if (F.circ.empty() && o.nolinear) { finish(); return; }
     int64_t circ_start = 0, circ_end = 0;
     int circ_span = -1;
-    if (!F.circ_idx.empty()) {
-        const CKey &cc = h->st[0].hits[circ.second].key;
-        circ_start = cc.start;
-        circ_end = cc.end;
+    if (!F.circ.empty()) {
+        circ = F.circ[0];
+        circ_start = circ.key.start;
+        circ_end = circ.key.end;
         circ_span = fr.circ[0];
         if (fr.circ.size() > 1) F.warns |= 1u << W_SUPPORT_CLOSURE;
     }
     std::set<Coord> lin_cons, lin_incons;
     for (int si : fr.lin) {
         const Span &span = h->spans[si];
-        if (!(span.uniq >= o.min_uniq_qual)) { incN(h, "lin_junc_not_unique"); continue; }
+        if (!(span.uniq >= o.min_uniq_qual)) { count("lin_junc_not_unique"); continue; }
         const std::vector<Splice> &splices = find_breakpoints(h, si, R, F);
         if (splices.empty()) {
-            incN(h, "lin_no_bp");
+            count("lin_no_bp");
             F.warns |= 1u << W_WARN_UNRESOLVED_LINSPLICE;
             continue;
         }
-        incN(h, "lin_spliced");
+        count("lin_spliced");
         const size_t n = o.allhits ? splices.size() : 1;
         for (size_t k = 0; k < n; ++k) {
             const Splice &sp = splices[k];
-            const size_t idx = storage_add(h, 1, sp, &fr.prim[span.mate]);
-            add_unique(F.junc, HitRef(1, idx));
-            if (o.test) add_unique(F.lin_idx, idx);
-            if (!F.circ_idx.empty()) {
+            const KeySlot j = store(1, sp, span);
+            add_unique(F.junc, j);
+            if (o.test) add_unique(F.lin, j);
+            if (!F.circ.empty()) {
                 if (sp.start <= circ_start || sp.end >= circ_end) {
                     F.warns |= 1u << W_WARN_OUTSIDE_SPLICE_JUNCTION;
                     lin_incons.insert(sp.coord());
@@ -1349,18 +1587,18 @@ void record_hits(fc2_caller *h, Frag &fr, const Results &R, FragScratch &F) {
     }
     if (o.test) {
         auto coords = [&](const APos &a) {
-            const std::string s = o.stranded ? (a.rev ? "-" : "+") : "*";
-            return UCoord{chrom_of(h, a.tid), a.pos, a.aend < 0 ? kNone : a.aend, s};
+            const std::string st = o.stranded ? (a.rev ? "-" : "+") : "*";
+            return UCoord{chrom_of(h, a.tid), a.pos, a.aend < 0 ? kNone : a.aend, st};
         };
         std::vector<UCoord> un, br;
         for (const APos &a : fr.unspliced) un.push_back(coords(a));
         for (const APos &a : fr.broken) br.push_back(coords(a));
         std::set<Coord> lin_coords, circ_coords;
-        for (size_t idx : F.lin_idx) lin_coords.insert(key_coord(h, h->st[1].hits[idx].key));
-        for (size_t idx : F.circ_idx) circ_coords.insert(key_coord(h, h->st[0].hits[idx].key));
-        h->out[2] += test_row(h, fr, lin_coords, circ_coords, un, br);
+        for (const KeySlot &j : F.lin) lin_coords.insert(key_coord(h, j.key));
+        for (const KeySlot &j : F.circ) circ_coords.insert(key_coord(h, j.key));
+        ro.test += test_row(h, fr, lin_coords, circ_coords, un, br);
     }
-    if (!F.circ_idx.empty()) {
+    if (!F.circ.empty()) {
         std::set<UCoord> un_cons, un_incons;
         const int32_t circ_tid = fr.prim[h->spans[circ_span].mate].tid;
         for (const APos &a : fr.unspliced) {
@@ -1377,71 +1615,146 @@ void record_hits(fc2_caller *h, Frag &fr, const Results &R, FragScratch &F) {
             }
         }
         if (!fr.broken.empty()) F.warns |= 1u << W_BROKEN_SEGMENTS;
-        if ((!un_cons.empty() || !un_incons.empty() || !lin_cons.empty() || !lin_incons.empty()) && o.multi_events &&
-            o.write_multi)
-            h->out[1] += multi_row(h, fr, h->st[0].hits[circ.second], lin_cons, lin_incons, un_cons, un_incons);
+        const bool multi = (!un_cons.empty() || !un_incons.empty() || !lin_cons.empty() || !lin_incons.empty()) &&
+                           o.multi_events && o.write_multi;
+        if (multi) multi_row_parts(h, fr, circ.key, lin_cons, lin_incons, un_cons, un_incons, F.p1, F.p2);
         for (uint32_t w = 0; w < kNumWarn; ++w)
-            if (F.warns & (1u << w)) add_flag(h, h->st[0].hits[circ.second], w, fr.name);
+            if (F.warns & (1u << w)) flag(circ, w);
+        finish();
+        if (multi) {
+            FOut &fo = ro.fouts.back();
+            fo.m0 = (int64_t)ro.mtext.size();
+            fo.m1 = (uint32_t)F.p1.size();
+            fo.m2 = (uint32_t)F.p2.size();
+            fo.circ_slot = circ.slot;
+            ro.mtext += F.p1;
+            ro.mtext += F.p2;
+        }
+        return;
     }
+    finish();
 }
 
-// the junction-table slots a fragment's best splices will look up (decode's coordinates, computed
-// early from the raw results): issued a few fragments ahead, they hide the tables' cache misses
-void prefetch_frag(const fc2_caller *h, const Frag &fr, const Results &R) {
-    const int64_t e = h->o.asize - h->o.margin;
-    for (int kind = 0; kind < 2; ++kind) {
-        for (int si : kind ? fr.lin : fr.circ) {
-            const Span &s = h->spans[si];
-            if (s.eval < 0 || (size_t)s.tid >= h->tid_cid.size() || h->tid_cid[(size_t)s.tid] < 0) continue;
-            const fc2_result &r = R.res[s.eval];
-            const fc2_pair &pr = h->b_pairs[(size_t)s.eval];
-            if (r.best_x < 0 || (r.info & (FC2_RES_ERR_KEY | FC2_RES_ERR_WIN)) || (pr.flags & FC2_PAIR_SKIP)) continue;
-            const int64_t l = (int64_t)pr.read_len - 2 * e;
-            const int64_t s0 = pr.b_aend - e - l + r.best_x, e0 = pr.a_pos + e + r.best_x + 1;
-            int64_t st = std::min(s0, e0), en = std::max(s0, e0);
-            if (pr.flags & FC2_PAIR_BACKSPLICE) en -= 1; else st -= 1;
-            const uint32_t c = (uint32_t)h->tid_cid[(size_t)s.tid], strand = (r.info & FC2_RES_MINUS) ? 1u : 0u;
-            h->st[kind].index.prefetch(st < en ? CKey{st, en, c, strand} : CKey{en, st, c, strand});
+// phase A over a range of fragments: stops at the first fragment that raises
+void phase_a(const fc2_caller *h, size_t f0, size_t f1, const Results &R, RangeOut &ro) {
+    static thread_local FragScratch F;
+    ro.clear();
+    for (size_t f = f0; f < f1; ++f) {
+        try {
+            phase_a_frag(h, (uint32_t)f, h->frags[f], R, F, ro);
+        } catch (const Fatal &e) {              // (a test row written before the error stays, :1361)
+            ro.err_frag = (int64_t)f;
+            ro.err_code = e.code;
+            ro.err_msg = e.msg;
+            return;
         }
     }
 }
 
-// ' <sorted junction names> <sorted flags>': the part of the read names both mates share
-void read_name_tail(fc2_caller *h, FragScratch &F) {
-    const size_t nj = F.junc.size();
-    if (F.names.size() < nj) F.names.resize(nj);
-    for (size_t k = 0; k < nj; ++k) {
-        F.names[k].clear();
-        hit_name(h, F.junc[k].first, h->st[F.junc[k].first].hits[F.junc[k].second], F.names[k]);
+// phase B, one shard: its events of every range in input order, up to the failing fragment fe
+void phase_b(fc2_caller *h, int s, size_t n_ranges, uint64_t fe) {
+    Shard &S = h->sh[s];
+    S.fresh[0].clear();
+    S.fresh[1].clear();
+    constexpr size_t kAhead = 8;
+    for (size_t r = 0; r < n_ranges; ++r) {
+        RangeOut &ro = h->ranges[r];
+        const std::vector<SEv> &v = ro.ev[s];
+        for (size_t k = 0; k < v.size(); ++k) {
+            const SEv &e = v[k];
+            if (e.frag >= fe) break;
+            if (k + kAhead < v.size()) S.index[v[k + kAhead].kind].prefetch(v[k + kAhead].key);
+            if (e.op == 0) {
+                HitVec &hv = S.hits[e.kind];
+                const auto ins = S.index[e.kind].try_emplace(e.key, hv.size());
+                if (ins.second) {
+                    Hit &t = hv.emplace_back();
+                    t.key = e.key;
+                    S.fresh[e.kind].emplace_back(e.seq, (uint32_t)ins.first);
+                }
+                Hit &t = hv[ins.first];
+                hit_apply(h, t, e);
+                const Span &span = h->spans[(size_t)e.span];
+                hit_add_read(S.strings, t, span, h->frags[e.frag].prim[e.mate]);
+                ro.slots[e.slot] = JRef{(uint32_t)s, (uint32_t)ins.first};
+            } else {
+                const JRef j = ro.slots[e.slot];
+                add_flag(S.strings, S.hits[0][j.idx], e.warn, h->frags[e.frag].name);
+            }
+        }
     }
-    if (nj > 1) std::sort(F.names.begin(), F.names.begin() + (std::ptrdiff_t)nj);
-    std::string &t = F.tail;
-    t.assign(1, ' ');
-    for (size_t k = 0; k < nj; ++k) {
-        if (k) t += ',';
-        t += F.names[k];
-    }
-    t += ' ';
-    bool first = true;
-    for (uint32_t w = 0; w < kNumWarn; ++w)
-        if (F.warns & (1u << w)) { if (!first) t += ','; t += kWarnName[w]; first = false; }
 }
 
-void write_read(fc2_caller *h, const Align &m, const FragScratch &F) {       // :1442-1447
-    // '@<qname> <sorted junction names> <sorted flags>' , seq, '+' + the same name, qual
-    std::string &o = h->out[0];
-    o += '@';
-    const size_t n0 = o.size();
-    o += m.qname;
-    o += F.tail;
-    const size_t n1 = o.size();
-    o += '\n';
-    o += m.has_seq ? m.seq : std::string("None");
-    o += "\n+";
-    o.append(o, n0, n1 - n0);
-    o += '\n';
-    o += m.has_qual ? m.qual : std::string("None");
-    o += '\n';
+// phase C: the chunk's new junctions named in order of first appearance (:684-686)
+void phase_c(fc2_caller *h) {
+    for (int kind = 0; kind < 2; ++kind) {
+        size_t pos[kShards] = {};
+        for (;;) {                              // merge of the shards' lists (each in seq order)
+            int best = -1;
+            uint64_t bseq = 0;
+            for (int s = 0; s < kShards; ++s) {
+                const auto &fl = h->sh[s].fresh[kind];
+                if (pos[s] < fl.size() && (best < 0 || fl[pos[s]].first < bseq)) { best = s; bseq = fl[pos[s]].first; }
+            }
+            if (best < 0) break;
+            const uint32_t idx = h->sh[best].fresh[kind][pos[best]++].second;
+            h->sh[best].hits[kind][idx].novel = ++h->novel[kind];
+            h->order[kind].push_back(JRef{(uint32_t)best, idx});
+        }
+    }
+}
+
+// phase D over a range: read names (write_read, :1442-1447) and multi_events rows, which need the
+// junction names, for the fragments before fe
+void phase_d(const fc2_caller *h, RangeOut &ro, uint64_t fe) {
+    static thread_local FragScratch F;
+    for (const FOut &fo : ro.fouts) {
+        if (fo.frag >= fe) break;
+        const Frag &fr = h->frags[fo.frag];
+        if (fo.m0 >= 0) {
+            ro.out1.append(ro.mtext, (size_t)fo.m0, fo.m1);
+            hit_name(h, 0, hit_at(h, 0, ro.slots[fo.circ_slot]), ro.out1);
+            ro.out1.append(ro.mtext, (size_t)fo.m0 + fo.m1, fo.m2);
+        }
+        if (!h->o.write_reads) continue;
+        // ' <sorted junction names> <sorted flags>': the part of the read names both mates share
+        const size_t nj = fo.nj;
+        if (F.names.size() < nj) F.names.resize(nj);
+        for (size_t k = 0; k < nj; ++k) {
+            const auto &j = ro.jk[fo.j0 + k];
+            F.names[k].clear();
+            hit_name(h, j.first, hit_at(h, j.first, ro.slots[j.second]), F.names[k]);
+        }
+        if (nj > 1) std::sort(F.names.begin(), F.names.begin() + (std::ptrdiff_t)nj);
+        std::string &t = F.tail;
+        t.assign(1, ' ');
+        for (size_t k = 0; k < nj; ++k) {
+            if (k) t += ',';
+            t += F.names[k];
+        }
+        t += ' ';
+        bool first = true;
+        for (uint32_t w = 0; w < kNumWarn; ++w)
+            if (fo.warns & (1u << w)) { if (!first) t += ','; t += kWarnName[w]; first = false; }
+        for (int m = 0; m < 2; ++m) {
+            if (!fr.has[m]) continue;
+            // '@<qname> <sorted junction names> <sorted flags>' , seq, '+' + the same name, qual
+            const Align &a = fr.prim[m];
+            std::string &o = ro.out0;
+            o += '@';
+            const size_t n0 = o.size();
+            o += a.qname;
+            o += t;
+            const size_t n1 = o.size();
+            o += '\n';
+            o += a.has_seq ? a.seq : std::string("None");
+            o += "\n+";
+            o.append(o, n0, n1 - n0);
+            o += '\n';
+            o += a.has_qual ? a.qual : std::string("None");
+            o += '\n';
+        }
+    }
 }
 
 }  // namespace
@@ -1466,8 +1779,8 @@ extern "C" int fc2_caller_open(const char *path, int is_bam, const fc2_caller_op
     h->ip.asize = opts->asize;
     h->ip.nolinear = opts->nolinear;
     h->ip.noop = opts->noop;
-    h->st[0].prefix = "circ";
-    h->st[1].prefix = "lin";
+    if (const char *env = getenv("FC2_CALLER_MIN_RANGE"))   // fragments per phase-A range at least (tests)
+        if (atoi(env) > 0) h->min_range_frags = (size_t)atoi(env);
     *out = h;
     return FC2_OK;
 }
@@ -1637,18 +1950,40 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
     const Results R{results, tiemask, tw, stride};
     int rc = FC2_OK;
     try {
-        static thread_local FragScratch F;
-        constexpr size_t kAhead = 16;          // sequential profile on the box: 0 / 8 / 16 ahead ->
-                                                // 0.354 / 0.347 / 0.344 s per 2M reads
-        for (size_t f = 0; f < h->nfrags; ++f) {
-            if (f + kAhead < h->nfrags) prefetch_frag(h, h->frags[f + kAhead], R);
-            Frag &fr = h->frags[f];
-            record_hits(h, fr, R, F);
-            if (!F.junc.empty()) {
-                if (h->o.write_reads) read_name_tail(h, F);
-                if (h->o.write_reads && fr.has[0]) write_read(h, fr.prim[0], F);
-                if (h->o.write_reads && fr.has[1]) write_read(h, fr.prim[1], F);
+        resolve_chroms(h);
+        if (!h->pool) {
+            const char *env = getenv("FC2_CALLER_THREADS");
+            int nt = env && atoi(env) > 0 ? atoi(env) : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+            nt = std::max(1, std::min(nt, 64));
+            h->pool.reset(new WorkPool(nt - 1));
+        }
+        // (A) ranges of fragments -> events per shard, text that needs no names
+        const size_t nf = h->nfrags;
+        const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)h->pool->size(), nf / std::max<size_t>(1, h->min_range_frags)));
+        if (h->ranges.size() < T) h->ranges.resize(T);
+        h->pool->run_checked((int)T, [&](int r) { phase_a(h, nf * (size_t)r / T, nf * (size_t)(r + 1) / T, R, h->ranges[(size_t)r]); });
+        uint64_t fe = nf;                       // the first fragment that raised (or none)
+        size_t n_r = T;                         // the ranges that count: up to the one that raised
+        for (size_t r = 0; r < T; ++r)
+            if (h->ranges[r].err_frag >= 0) { fe = (uint64_t)h->ranges[r].err_frag; n_r = r + 1; break; }
+        // (B) the shards apply their events in input order; (C) names; (D) read names, multi rows
+        h->pool->run_checked(kShards, [&](int sidx) { phase_b(h, sidx, n_r, fe); });
+        phase_c(h);
+        h->pool->run_checked((int)n_r, [&](int r) { phase_d(h, h->ranges[(size_t)r], fe); });
+        for (size_t r = 0; r < n_r; ++r) {
+            RangeOut &ro = h->ranges[r];
+            for (const auto &kv : ro.N) incN(h, kv.first, kv.second);
+            if (h->reads_gz.is_open()) {
+                if (!ro.out0.empty()) h->reads_gz.append(ro.out0);
+            } else {
+                h->out[0] += ro.out0;
             }
+            h->out[1] += ro.out1;
+            h->out[2] += ro.test;
+        }
+        if (fe < nf) {
+            const RangeOut &ro = h->ranges[n_r - 1];
+            rc = fc2::fail(ro.err_code, ro.err_msg);
         }
     } catch (const Fatal &f) {
         rc = fc2::fail(f.code, f.msg);

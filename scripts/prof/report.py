@@ -49,7 +49,7 @@ def main():
     names = symbolize(keys)
     for tag in sorted({r[0] for r in rows}):
         sel = [r for r in rows if r[0] == tag]
-        selfc, inlib, inlib_outer, inlib_line = (collections.Counter() for _ in range(4))
+        selfc, inlib, inlib_outer, inlib_line, own_line = (collections.Counter() for _ in range(5))
         for _, pc, sym, callers in sel:
             if lib(pc[0]):
                 fr = names.get(pc, [("?", "?")])
@@ -65,10 +65,12 @@ def main():
             inlib[fr[0][0][:100]] += 1
             inlib_outer[fr[-1][0][:100]] += 1
             inlib_line[fr[0][1]] += 1
+            own = next((f for f in fr if f[1].startswith("fc2_")), None)    # the innermost line of our sources
+            own_line["%s  %s" % (own[1], own[0][:60]) if own else "?"] += 1
         n = len(sel)
         print("== tag %s: %d samples" % (tag, n))
         for title, c in (("self", selfc), ("in-lib (innermost)", inlib), ("in-lib (outermost)", inlib_outer),
-                         ("in-lib line", inlib_line)):
+                         ("in-lib line", inlib_line), ("own source line", own_line)):
             print("-- %s" % title)
             for k, v in c.most_common(top):
                 print("%6.1f%%  %s" % (100.0 * v / n, k))
