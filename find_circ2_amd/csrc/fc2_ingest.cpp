@@ -896,6 +896,73 @@ void sam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
     }
 }
 
+// BAM splitter: the decompressed stream (ensure(): BGZF blocks inflated on their own threads, or
+// any gzip stream) cut into numbered blocks of whole records (block_size + body), ~kBlock bytes
+// each.  Where the stream ends inside a record, or the input fails, the block ends after the last
+// whole record and carries the error parse_bam_record would have reported there.
+void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
+    auto &A = *ap;
+    for (uint64_t seq = 0;; ++seq) {
+        std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
+        {
+            std::unique_lock<std::mutex> lk(A.m);
+            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.kInflight; });
+            if (A.stop) return;
+            ++A.inflight;
+            if (!A.spare.empty()) { b = std::move(A.spare.back()); A.spare.pop_back(); }
+        }
+        if (!b) b.reset(new fc2_ingest::SamAhead::Batch());
+        b->seq = seq;
+        b->n = 0;
+        b->rc = FC2_OK;
+        b->err.clear();
+        b->read_rc = FC2_OK;
+        b->read_err.clear();
+        b->eof = false;
+        std::string &blk = b->block;
+        blk.clear();
+        auto truncated = [&]() {
+            b->read_rc = FC2_E_FORMAT;
+            b->read_err = "truncated BAM record" + (h->z_err.empty() ? "" : " (" + h->z_err + ")");
+            b->eof = true;
+        };
+        while (blk.size() < A.kBlock) {
+            if (!ensure(h, 4)) {                // end of input (clean, or an input error first)
+                if (h->in_rc) { b->read_rc = h->in_rc; b->read_err = h->in_err; }
+                else if (!h->z_err.empty()) { b->read_rc = FC2_E_FORMAT; b->read_err = "BAM input: " + h->z_err; }
+                else if (h->end > h->beg) truncated();
+                b->eof = true;
+                break;
+            }
+            // every whole record in the buffer, in one copy
+            const char *base = h->buf.data();
+            size_t q = h->beg;
+            while (q + 4 <= h->end) {
+                int32_t bs;
+                memcpy(&bs, base + q, 4);
+                if (bs < 32 || q + 4 + (size_t)bs > h->end) break;
+                q += 4 + (size_t)bs;
+                if (blk.size() + (q - h->beg) >= A.kBlock) break;
+            }
+            if (q > h->beg) {
+                blk.append(base + h->beg, q - h->beg);
+                h->beg = q;
+                continue;
+            }
+            int32_t bs;                         // the record at beg is not whole yet
+            memcpy(&bs, base + h->beg, 4);
+            if (bs < 32 || !ensure(h, 4 + (size_t)bs)) { truncated(); break; }
+        }
+        const bool last = b->eof;
+        {
+            std::lock_guard<std::mutex> lk(A.m);
+            A.todo.push_back(std::move(b));
+        }
+        A.cv.notify_all();
+        if (last) return;
+    }
+}
+
 // parser: blocks to record batches (own RNAME cache and CIGAR scratch)
 void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
     auto &A = *ap;
@@ -910,7 +977,16 @@ void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
             A.todo.pop_front();
         }
         const char *p = b->block.data(), *end = p + b->block.size();
-        while (p < end && b->rc == FC2_OK) {
+        while (h->bam && p < end && b->rc == FC2_OK) {     // whole BAM records (bam_split_loop)
+            int32_t bs;
+            memcpy(&bs, p, 4);
+            if (b->n == b->recs.size()) b->recs.emplace_back();
+            const int rc = parse_bam_body(h, (const uint8_t *)p + 4, bs, b->recs[b->n], ps.ops, h->need_text, false);
+            if (rc) { b->rc = rc; b->err = fc2_last_error(); break; }
+            ++b->n;
+            p += 4 + (size_t)bs;
+        }
+        while (!h->bam && p < end && b->rc == FC2_OK) {
             const char *nl = (const char *)memchr(p, '\n', (size_t)(end - p));
             const char *ls = p, *le = nl ? nl : end;
             p = nl ? nl + 1 : end;
@@ -1301,11 +1377,12 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
 int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof) {
     if (!h || !p) return fc2::fail(FC2_E_PARAM, "ingest pull: null argument");
     if (h->need_text) h->need_text = false;     // (written once: the parse thread reads it)
-    // plain SAM text: parsed on threads of their own (compressed SAM stays on the sequential reader)
-    if (!h->ahead && !h->bam && h->src == fc2_ingest::SRC_RAW && !h->bam_out && !h->finished) {
+    // plain SAM text and BAM (any compression): parsed on threads of their own; compressed SAM stays
+    // on the sequential reader, and so does everything when -B writes records while reading
+    if (!h->ahead && (h->bam || h->src == fc2_ingest::SRC_RAW) && !h->bam_out && !h->finished) {
         fc2_ingest::SamAhead *ap = new fc2_ingest::SamAhead();
         h->ahead.reset(ap);
-        ap->splitter = std::thread(sam_split_loop, h, ap);
+        ap->splitter = h->bam ? std::thread(bam_split_loop, h, ap) : std::thread(sam_split_loop, h, ap);
         for (int k = 0; k < fc2_ingest::SamAhead::kParsers; ++k) ap->parsers.emplace_back(sam_parse_loop, h, ap);
     }
     return run_loop(h, p, max_frags, &sink, nullptr, eof);

@@ -1,16 +1,30 @@
 #!/usr/bin/env python
 """Same-box A/B of the whole CLI (two-thread loop, GPU search): libfc2_<NAME>.so against the tree's
 libfc2.so on one generated hg19-sized input, alternating, one process per run (the library is chosen
-at import through FC2_LIB_VARIANT).  usage: ab_cli.py NAME [rounds] [reads]"""
+at import through FC2_LIB_VARIANT), in bench.py's two forms: BGZF BAM piped on stdin and SAM by path.
+Every run's output files must equal the first run's.  One JSON line per run.
+usage: ab_cli.py NAME [rounds] [reads]"""
+import gzip
+import json
 import os
 import re
 import subprocess
 import sys
+import time
 
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "scripts")]
+
+
+def outputs(o):
+    r = {}
+    for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
+        r[f] = open(os.path.join(o, f), "rb").read()
+    with gzip.open(os.path.join(o, "spliced_reads.fastq.gz"), "rb") as fh:
+        r["reads"] = fh.read()
+    return r
 
 
 def main():
@@ -19,30 +33,49 @@ def main():
     reads = int(sys.argv[3]) if len(sys.argv) > 3 else 2_000_000
     from cli_scale_check import make_genome, write_fasta, write_sam
     from find_circ2_amd import sq_table
+    from find_circ2_amd.ingest import sam_to_bam
     d = "/tmp/fc2_abcli"
     os.makedirs(d, exist_ok=True)
-    fa, sam = os.path.join(d, "genome.fa"), os.path.join(d, "reads.sam")
+    fa, sam, bam = os.path.join(d, "genome.fa"), os.path.join(d, "reads.sam"), os.path.join(d, "reads.bam")
     rng = np.random.default_rng(2024)
     names, sizes = sq_table(os.path.join(ROOT, "tests", "golden", "test_norm.sam"))
     seqs = make_genome(fa, names, sizes, rng)
     write_sam(sam, seqs, reads, rng)
     write_fasta(fa, seqs)
     del seqs
+    sam_to_bam(sam, bam)
+    ref = None
     for r in range(rounds + 1):                  # round 0 builds the .byo_index (not reported)
         for v in (name, "cur"):
-            env = dict(os.environ)
-            env.pop("FC2_LIB_VARIANT", None)
-            if v != "cur":
-                env["FC2_LIB_VARIANT"] = v
-            out = os.path.join(d, "out_" + v)
-            subprocess.run([sys.executable, "-c", "import sys; from find_circ2_amd import cli; "
-                            "sys.exit(cli.main(['-G', %r, '-o', %r, '-q', %r]))" % (fa, out, sam)],
-                           env=env, check=True, cwd=ROOT)
-            log = open(os.path.join(out, "run.log")).read()
-            rate = re.search(r"overall ([0-9.]+)k reads/second", log).group(1)
-            st = re.search(r"read loop stages: (.*)", log).group(1)
-            if r:
-                print(v, rate, st, flush=True)
+            for form in ("bam_stdin", "sam_path"):
+                env = dict(os.environ)
+                env.pop("FC2_LIB_VARIANT", None)
+                if v != "cur":
+                    env["FC2_LIB_VARIANT"] = v
+                out = os.path.join(d, "out_%s_%s" % (v, form))
+                cmd = [sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", out, "-q"]
+                t0 = time.time()
+                if form == "bam_stdin":
+                    feeder = subprocess.Popen(["cat", bam], stdout=subprocess.PIPE)
+                    subprocess.run(cmd, env=env, check=True, cwd=ROOT, stdin=feeder.stdout, timeout=600)
+                    feeder.stdout.close()
+                    feeder.wait()
+                else:
+                    subprocess.run(cmd + [sam], env=env, check=True, cwd=ROOT, timeout=600)
+                wall = time.time() - t0
+                log = open(os.path.join(out, "run.log")).read()
+                rate = float(re.search(r"overall ([0-9.]+)k reads/second", log).group(1)) * 1e3
+                st = re.search(r"read loop stages: (.*)", log).group(1)
+                o = outputs(out)
+                if ref is None:
+                    ref = o
+                same = o == ref
+                if r:
+                    print(json.dumps({"variant": v, "form": form, "round": r, "reads_per_s": rate,
+                                      "process_wall_s": round(wall, 2), "stages": st, "outputs_identical": same}),
+                          flush=True)
+                if not same:
+                    raise SystemExit("outputs differ: %s %s" % (v, form))
 
 
 if __name__ == "__main__":

@@ -151,3 +151,38 @@ def test_corrupt_bam_records_are_errors(tmp_path, case):
         _native_all(str(p))
     with pytest.raises(ValueError):
         _python_all(str(p))
+
+
+@pytest.mark.parametrize("form", ["bam_bgzf", "bam_gzip", "bam_raw", "sam"])
+def test_parse_ahead_equals_sequential_reader_on_damage(forms, tmp_path, form):
+    """The native loop's parse-ahead threads (BAM: records cut into blocks from the decompressed
+    stream; SAM: newline-aligned blocks) against the sequential reader the loop uses with -B: the
+    same exit status on every damaged input and, when a run completes, the same files.  The reader
+    must stop exactly where the sequential one reports the damage."""
+    import gzip as gz
+    import os
+    d, fa, data = forms
+    rng = random.Random(2027 + len(form))
+    n_err = 0
+    for k in range(10):
+        p = str(tmp_path / ("in%d" % k))
+        with open(p, "wb") as fh:
+            fh.write(data[form] if k == 0 else _damage(rng, data[form]))
+        rcs, outs = [], []
+        for tag, extra in (("ahead", []), ("seq", ["-B"])):
+            o = str(tmp_path / ("o%d_%s" % (k, tag)))
+            try:
+                rc = cli.main(["-G", fa, "-o", o, "-q"] + extra + [p], evaluator_factory=oracle_evaluator_factory)
+            except (IOError, OSError, ValueError, RuntimeError, EOFError, KeyError, IndexError):
+                rc = 1
+            rcs.append(rc)
+            outs.append(o)
+        assert rcs[0] == rcs[1], (k, rcs)
+        n_err += rcs[0] != 0
+        if rcs[0] == 0:
+            for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
+                assert open(os.path.join(outs[0], f)).read() == open(os.path.join(outs[1], f)).read(), (k, f)
+            with gz.open(os.path.join(outs[0], "spliced_reads.fastq.gz"), "rt") as a, \
+                    gz.open(os.path.join(outs[1], "spliced_reads.fastq.gz"), "rt") as b:
+                assert a.read() == b.read(), k
+    assert n_err > 0
