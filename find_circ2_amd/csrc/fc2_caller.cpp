@@ -34,6 +34,7 @@
 
 using fc2::ing::Mate;
 using fc2::ing::Rec;
+using fc2::ing::RecFields;
 
 namespace {
 
@@ -128,14 +129,41 @@ struct Align : APos {                          // a primary: what record_hits an
     bool has_seq = false, has_qual = false;
 };
 
-APos apos_of(const Rec &r) {
+APos apos_of(const RecFields &r) {
     APos a;
     a.tid = r.tid;
     a.pos = r.pos;
     a.aend = r.aend;
-    a.rev = r.reverse();
+    a.rev = (r.flag & 0x10) != 0;
     return a;
 }
+
+// A chunk's read_part bytes: grows without initialising, as each fragment writes its own region
+class ByteBuf {
+  public:
+    char *data() { return p_.get(); }
+    const char *data() const { return p_.get(); }
+    size_t size() const { return n_; }
+    void clear() { n_ = 0; }
+    void resize(size_t n) {
+        if (n > cap_) {
+            const size_t c = std::max(n, 2 * cap_);
+            std::unique_ptr<char[]> q(new char[c]);
+            if (n_) memcpy(q.get(), p_.get(), n_);
+            p_.swap(q);
+            cap_ = c;
+        }
+        n_ = n;
+    }
+    void swap(ByteBuf &o) noexcept {
+        p_.swap(o.p_);
+        std::swap(n_, o.n_);
+        std::swap(cap_, o.cap_);
+    }
+  private:
+    std::unique_ptr<char[]> p_;
+    size_t n_ = 0, cap_ = 0;
+};
 
 // the primary's strings are swapped in, not copied: the record gets the recycled Align's buffers
 // back (the ingest reads nothing of a handed-over fragment's records, FragSink)
@@ -169,6 +197,14 @@ struct Frag {
     Align prim[2];
     std::vector<int> circ, lin;                // indices into the chunk's spans
     std::vector<APos> unspliced, broken;
+    // the mates' records as process_mate reads them (next side): fields at the chunk's recf[r0,
+    // r0 + nrec), the proper segments' indices at prop[p0, p0 + np)
+    struct MateFields {
+        uint32_t r0 = 0, nrec = 0, p0 = 0, np = 0;
+    } mf[2];
+    uint64_t span0 = 0, span_max = 0;          // its span slots [span0, span0 + span_max) in the chunk
+    uint64_t arena0 = 0;                       // its read_part bytes from here (at most one read per pair)
+    bool dropped = false;                      // no pair record_hits would look at (on_fragment)
 };
 
 using Coord = std::tuple<std::string, int64_t, int64_t, std::string>;   // (chrom, start, end, strand)
@@ -618,7 +654,13 @@ struct fc2_caller {
     std::vector<Frag> bf_frags;                 // the chunk being formed (next): its first bf_nfrags
     size_t bf_nfrags = 0;                       // entries (the rest are recycled objects)
     std::vector<Span> bf_spans;
-    std::string bf_arena;                       // read_part bytes
+    ByteBuf bf_arena;                           // read_part bytes
+    uint64_t bf_nspans = 0, bf_narena = 0;      // span slots / arena bytes reserved so far
+    std::vector<RecFields> bf_recf;             // the chunk's mates' records (Frag::MateFields)
+    std::vector<int32_t> bf_prop;
+    std::unique_ptr<WorkPool> next_pool;        // the next side's workers (process_mate)
+    std::vector<std::vector<std::pair<const char *, double>>> next_N;   // their counters per range
+    std::vector<std::pair<int64_t, Fatal>> next_err_at;                 // their first error per range
     std::vector<uint64_t> bf_off;
     std::vector<fc2_pair> bf_pairs;
     std::vector<int64_t> bf_starts, bf_ends;    // process_mate scratch
@@ -626,7 +668,7 @@ struct fc2_caller {
     std::vector<Frag> frags;                    // the chunk being recorded (submit): first nfrags
     size_t nfrags = 0;
     std::vector<Span> spans;
-    std::string arena;
+    ByteBuf arena;
     std::vector<uint64_t> b_off;
     std::vector<fc2_pair> b_pairs;
     // chunks handed out by fc2_caller_next and not yet submitted, oldest first: the caller may
@@ -635,7 +677,7 @@ struct fc2_caller {
         std::vector<Frag> frags;
         size_t nfrags = 0;
         std::vector<Span> spans;
-        std::string arena;
+        ByteBuf arena;
         std::vector<uint64_t> b_off;
         std::vector<fc2_pair> b_pairs;
     };
@@ -990,7 +1032,7 @@ std::string chrom_of(const fc2_caller *h, int32_t tid) {         // fast_chrom_l
     return nm;
 }
 
-int64_t uniqness(const Rec &a) {                                  // :809-819
+int64_t uniqness(const RecFields &a) {                                  // :809-819
     if (!a.has_as) throw Fatal{FC2_E_KEY, "KeyError: \"tag 'AS' not present\""};
     if (!a.as_int || (a.has_xs && !a.xs_int))
         throw Fatal{FC2_E_FORMAT, "native caller: AS / XS tags must be integers (use --python-caller)"};
@@ -1000,7 +1042,7 @@ int64_t uniqness(const Rec &a) {                                  // :809-819
 // Hit.add's anchor quality (find_circ.py:556-559): dict(tags) keeps the LAST AS / XS of a record.
 // Only Hit.add reads it, so a non-integer last tag matters only for a span that reaches a Hit
 // (hit_add raises there); false when it is not an integer
-bool dict_quality(const Rec &a, int64_t &q) {
+bool dict_quality(const RecFields &a, int64_t &q) {
     q = 0;
     if (!a.as_last_int || (a.has_xs && !a.xs_last_int)) return false;
     q = a.as_last - (a.has_xs ? a.xs_last : 0);
@@ -1009,25 +1051,34 @@ bool dict_quality(const Rec &a, int64_t &q) {
 
 const char *kNoneLen = "TypeError: object of type 'NoneType' has no len()";
 
-// process_mate (:1492-1527) with adjacent_segment_pairs (:1058-1140)
-void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
-    const Rec &prim = m.recs[0];
-    if (m.proper.size() < 2) {
-        incN_in(h, "unspliced_mates");
+// process_mate (:1492-1527) with adjacent_segment_pairs (:1058-1140), on the mate's recorded
+// fields (Frag::MateFields) and its primary's sequence (fr.prim[mi], taken by on_fragment): spans
+// into the fragment's slots of `spans` from *sk on, read parts into `arena` from *ap on
+void process_mate(const fc2_caller *h, const RecFields *recs, size_t nrec, const int32_t *proper, size_t n, int mi,
+                  Frag &fr, Span *spans, uint64_t &sk, char *arena, uint64_t &ap,
+                  std::vector<std::pair<const char *, double>> &N) {
+    const RecFields &prim = recs[0];
+    if (n < 2) {
+        incN_into(N, "unspliced_mates", 1.);
         fr.unspliced.push_back(apos_of(prim));
         return;
     }
     if (!prim.has_seq) throw Fatal{FC2_E_FORMAT, kNoneLen};      // L = len(mate.full_seq)
-    const int64_t L = (int64_t)prim.seq.size();
-    const size_t n = m.proper.size();
+    const std::string &seq = fr.prim[mi].seq;
+    const int64_t L = (int64_t)seq.size();
     const double weight = 1. / ((double)n - 1.);
-    std::vector<int64_t> &starts = h->bf_starts, &ends = h->bf_ends;
-    std::vector<size_t> &order = h->bf_order;
-    starts.resize(n);
-    ends.resize(n);
-    order.resize(n);
+    int64_t st_small[16], en_small[16];
+    size_t ord_small[16];
+    std::vector<int64_t> st_big, en_big;
+    std::vector<size_t> ord_big;
+    int64_t *starts = st_small, *ends = en_small;
+    size_t *order = ord_small;
+    if (n > 16) {
+        st_big.resize(n); en_big.resize(n); ord_big.resize(n);
+        starts = st_big.data(); ends = en_big.data(); order = ord_big.data();
+    }
     for (size_t k = 0; k < n; ++k) {
-        const Rec &s = m.recs[m.proper[k]];
+        const RecFields &s = recs[proper[k]];
         if (s.qlen < 0) throw Fatal{FC2_E_FORMAT, kNoneLen};     // len(s.query)
         starts[k] = s.astart;
         ends[k] = s.astart + s.qlen;
@@ -1043,10 +1094,10 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
     for (size_t k = 0; k + 1 < n; ++k) {
         const size_t a = order[k], b = order[k + 1];
         if (ends[a] - starts[a] < h->o.asize || ends[b] - starts[b] < h->o.asize) {
-            incN_in(h, "seg_too_short_skip");
+            incN_into(N, "seg_too_short_skip", 1.);
             continue;
         }
-        const Rec &A = m.recs[m.proper[a]], &B = m.recs[m.proper[b]];
+        const RecFields &A = recs[proper[a]], &B = recs[proper[b]];
         const int64_t q_start = std::min(starts[a], starts[b]), q_end = std::max(ends[a], ends[b]);
         (void)chrom_of(h, A.tid);
         Span s;
@@ -1064,49 +1115,95 @@ void process_mate(fc2_caller *h, const Mate &m, int mi, Frag &fr) {
         s.q_int = qa_int && qb_int;
         s.qA = s.circ ? qb : qa;
         s.qB = s.circ ? qa : qb;
-        s.a_rev = s.circ ? B.reverse() : A.reverse();
+        s.a_rev = s.circ ? (B.flag & 0x10) != 0 : (A.flag & 0x10) != 0;
         // read_part = primary.seq[q_start:q_end] (Python slice)
         const int64_t lo = std::max<int64_t>(0, std::min(q_start, L)), hi = std::max(lo, std::min(q_end, L));
-        s.read_off = h->bf_arena.size();
+        s.read_off = ap;
         s.read_len = (uint32_t)(hi - lo);
-        h->bf_arena.append(prim.seq, (size_t)lo, (size_t)(hi - lo));
-        h->bf_spans.push_back(s);
-        (s.circ ? fr.circ : fr.lin).push_back((int)h->bf_spans.size() - 1);
+        if (hi > lo) memcpy(arena + ap, seq.data() + lo, (size_t)(hi - lo));
+        ap += (uint64_t)(hi - lo);
+        spans[sk] = s;
+        (s.circ ? fr.circ : fr.lin).push_back((int)sk);
+        ++sk;
         min_s = std::min(min_s, q_start);
         max_e = std::max(max_e, q_end);
     }
     if (max_e < L - h->o.asize || min_s > h->o.asize) {
-        for (size_t k = 1; k < m.recs.size(); ++k)
-            if (m.recs[k].tid != prim.tid) fr.broken.push_back(apos_of(m.recs[k]));
-        for (size_t k = 1; k < m.recs.size(); ++k)
-            if (m.recs[k].tid == prim.tid && m.recs[k].reverse() != prim.reverse())
-                fr.broken.push_back(apos_of(m.recs[k]));
+        const bool prev = (prim.flag & 0x10) != 0;
+        for (size_t k = 1; k < nrec; ++k)
+            if (recs[k].tid != prim.tid) fr.broken.push_back(apos_of(recs[k]));
+        for (size_t k = 1; k < nrec; ++k)
+            if (recs[k].tid == prim.tid && ((recs[k].flag & 0x10) != 0) != prev) fr.broken.push_back(apos_of(recs[k]));
     }
 }
 
-int on_fragment(fc2_caller *h, Mate *m1, Mate *m2) {
-    // the next slot of the chunk; a recycled Frag is reset field by field (capacity kept)
-    if (h->bf_nfrags == h->bf_frags.size()) h->bf_frags.emplace_back();
-    Frag &fr = h->bf_frags[h->bf_nfrags];
-    fr.name.assign(m2->recs[0].qname);          // Fragment(mate2.primary.qname, ...)
+// on_fragment's processing of one recorded fragment (both mates, process_mate) and the reference's
+// filter on the result (Caller._flush): no circ span, or no span at all with --no-linear
+void process_frag(const fc2_caller *h, Frag &fr, const std::vector<RecFields> &recf, const std::vector<int32_t> &prop,
+                  Span *spans, char *arena, std::vector<std::pair<const char *, double>> &N) {
     fr.circ.clear();
     fr.lin.clear();
     fr.unspliced.clear();
     fr.broken.clear();
+    for (uint64_t k = 0; k < fr.span_max; ++k) spans[fr.span0 + k].eval = -1;   // unused slots
+    uint64_t sk = fr.span0, ap = fr.arena0;
+    for (int k = 0; k < 2; ++k) {
+        if (!fr.has[k]) continue;
+        const Frag::MateFields &mf = fr.mf[k];
+        process_mate(h, recf.data() + mf.r0, mf.nrec, prop.data() + mf.p0, mf.np, k, fr, spans, sk, arena, ap, N);
+    }
+    fr.dropped = (fr.circ.empty() && h->o.nolinear) || (fr.circ.empty() && fr.lin.empty());
+}
+
+// The sink of the ingest's pull loop: the fragment's records are recorded (their fields, the
+// primaries' strings) into the chunk's next slot, with room for the spans and read parts it can
+// have.  With `defer` the chunk's fragments are processed afterwards on the next side's workers
+// (fc2_caller_next); otherwise (-B writes records while reading, and the reference stops at a
+// failing fragment) here, raising where process_mate raises.
+int on_fragment(fc2_caller *h, Mate *m1, Mate *m2, bool defer) {
+    // the next slot of the chunk; a recycled Frag is reset field by field (capacity kept)
+    if (h->bf_nfrags == h->bf_frags.size()) h->bf_frags.emplace_back();
+    Frag &fr = h->bf_frags[h->bf_nfrags];
+    fr.name.assign(m2->recs[0].qname);          // Fragment(mate2.primary.qname, ...)
+    fr.dropped = false;
     Mate *ms[2] = {m1, m2};
-    const size_t span0 = h->bf_spans.size(), arena0 = h->bf_arena.size();
+    fr.span0 = h->bf_nspans;
+    fr.arena0 = h->bf_narena;
+    uint64_t smax = 0, amax = 0;
+    const size_t recf0 = h->bf_recf.size(), prop0 = h->bf_prop.size();
     for (int k = 0; k < 2; ++k) {
         fr.has[k] = ms[k] != nullptr;
+        Frag::MateFields &mf = fr.mf[k];
+        mf = Frag::MateFields();
         if (!ms[k]) continue;
-        process_mate(h, *ms[k], k, fr);          // reads the records first
+        const Mate &m = *ms[k];
+        mf.r0 = (uint32_t)h->bf_recf.size();
+        mf.nrec = (uint32_t)m.recs.size();
+        for (const Rec &r : m.recs) h->bf_recf.push_back(static_cast<const RecFields &>(r));
+        mf.p0 = (uint32_t)h->bf_prop.size();
+        mf.np = (uint32_t)m.proper.size();
+        h->bf_prop.insert(h->bf_prop.end(), m.proper.begin(), m.proper.end());
+        if (mf.np >= 2) {
+            smax += mf.np - 1;
+            amax += (uint64_t)(mf.np - 1) * m.recs[0].seq.size();
+        }
         take_align(fr.prim[k], ms[k]->recs[0]);
     }
-    if ((fr.circ.empty() && h->o.nolinear) || (fr.circ.empty() && fr.lin.empty())) {
-        h->bf_spans.resize(span0);                // not pending: its spans are never evaluated
-        h->bf_arena.resize(arena0);
-        return FC2_OK;                            // the slot is reused by the next fragment
-    }
+    fr.span_max = smax;
+    h->bf_nspans += smax;
+    h->bf_narena += amax;
     ++h->bf_nfrags;
+    if (defer) return FC2_OK;
+    if (h->bf_spans.size() < h->bf_nspans) h->bf_spans.resize(h->bf_nspans);
+    if (h->bf_arena.size() < h->bf_narena) h->bf_arena.resize(h->bf_narena);
+    process_frag(h, fr, h->bf_recf, h->bf_prop, h->bf_spans.data(), h->bf_arena.data(), h->N_in);
+    if (fr.dropped) {                           // not pending: its spans are never evaluated
+        --h->bf_nfrags;                         // the slot is reused by the next fragment
+        h->bf_nspans = fr.span0;
+        h->bf_narena = fr.arena0;
+        h->bf_recf.resize(recf0);
+        h->bf_prop.resize(prop0);
+    }
     return FC2_OK;
 }
 
@@ -1843,14 +1940,18 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         return fc2::fail(code, h->next_err_msg);
     }
     h->bf_nfrags = 0;
-    h->bf_spans.clear();
-    h->bf_arena.clear();
+    h->bf_nspans = h->bf_narena = 0;
+    h->bf_recf.clear();
+    h->bf_prop.clear();
     h->bf_off.clear();
     h->bf_pairs.clear();
+    // the chunk's fragments are processed after they are all read, on the next side's workers --
+    // unless -B writes records while reading (the reference's writer stops at a failing fragment)
+    const bool defer = !fc2::ing::writes_records(h->ing);
     Fatal err{0, ""};
     const fc2::ing::FragSink sink = [&](Mate *m1, Mate *m2, bool) -> int {
         try {
-            return on_fragment(h, m1, m2);
+            return on_fragment(h, m1, m2, defer);
         } catch (const Fatal &f) {
             err = f;
             return f.code ? f.code : FC2_E_FORMAT;
@@ -1860,18 +1961,72 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     // instead of waiting for a whole first chunk; chunk boundaries change nothing in the outputs
     const uint64_t limit = std::max<uint64_t>(1, (uint64_t)h->o.chunksize >> (h->n_chunks < 4 ? 4 - h->n_chunks : 0));
     ++h->n_chunks;
+    int in_code = FC2_OK;                      // an error of the input (or, without defer, of a fragment)
+    std::string in_msg;
     while (!h->eof && h->bf_nfrags < limit) {
         int e = 0;
         const int rc = fc2::ing::pull(h->ing, &h->ip, limit, sink, &e);
         if (rc) {
-            const int code = err.code ? err.code : rc;
-            const std::string msg = err.code ? err.msg : std::string(fc2_last_error());
-            if (!h->bf_nfrags) return fc2::fail(code, msg);
-            h->next_err = code;                    // hand out the fragments before it first
-            h->next_err_msg = msg;
+            in_code = err.code ? err.code : rc;
+            in_msg = err.code ? err.msg : std::string(fc2_last_error());
             break;
         }
         h->eof = e != 0;
+    }
+    if (defer) {
+        // process_mate of every fragment on the workers, in ranges; the first fragment that raises
+        // ends the chunk there (an input error after it is never reached)
+        h->bf_spans.resize(h->bf_nspans);
+        h->bf_arena.resize(h->bf_narena);
+        if (!h->next_pool) {
+            const char *env = getenv("FC2_NEXT_THREADS");
+            int nt = env && atoi(env) > 0 ? atoi(env) : (int)std::min(4u, std::max(1u, std::thread::hardware_concurrency()));
+            h->next_pool.reset(new WorkPool(std::max(1, std::min(nt, 64)) - 1));
+        }
+        const size_t nf = h->bf_nfrags;
+        const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)h->next_pool->size(),
+                                                              nf / std::max<size_t>(1, h->min_range_frags)));
+        if (h->next_N.size() < T) h->next_N.resize(T);
+        h->next_err_at.assign(T, std::pair<int64_t, Fatal>(-1, Fatal{0, ""}));
+        Span *spans = h->bf_spans.data();
+        char *arena = h->bf_arena.data();
+        h->next_pool->run_checked((int)T, [&](int r) {
+            auto &N = h->next_N[(size_t)r];
+            N.clear();
+            for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
+                try {
+                    process_frag(h, h->bf_frags[f], h->bf_recf, h->bf_prop, spans, arena, N);
+                } catch (const Fatal &x) {
+                    h->next_err_at[(size_t)r] = {(int64_t)f, x};
+                    return;
+                }
+            }
+        });
+        size_t fe = nf;
+        for (size_t r = 0; r < T; ++r) {
+            for (const auto &kv : h->next_N[r]) incN_in(h, kv.first, kv.second);
+            if (h->next_err_at[r].first >= 0) {
+                fe = (size_t)h->next_err_at[r].first;
+                in_code = h->next_err_at[r].second.code ? h->next_err_at[r].second.code : FC2_E_FORMAT;
+                in_msg = h->next_err_at[r].second.msg;
+                break;
+            }
+        }
+        if (fe < nf) h->bf_spans.resize(h->bf_frags[fe].span0);   // no span of a fragment not processed
+        // drop the fragments with no span record_hits looks at (rare: the ingest hands out only
+        // fragments with pairs), keeping the order
+        size_t k = 0;
+        for (size_t f = 0; f < fe; ++f) {
+            if (h->bf_frags[f].dropped) continue;
+            if (k != f) std::swap(h->bf_frags[k], h->bf_frags[f]);
+            ++k;
+        }
+        h->bf_nfrags = k;
+    }
+    if (in_code) {
+        if (!h->bf_nfrags) return fc2::fail(in_code, in_msg);
+        h->next_err = in_code;                     // hand out the fragments before it first
+        h->next_err_msg = in_msg;
     }
     // the spans record_hits will evaluate, in fragment order (Caller._flush)
     for (size_t f = 0; f < h->bf_nfrags; ++f) {
@@ -1897,12 +2052,14 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             }
         }
     }
+    if (h->bf_spans.size() > h->bf_nspans) h->bf_spans.resize(h->bf_nspans);
     for (const Span &s : h->bf_spans)
         if (s.eval >= 0 && s.read_len > FC2_MAX_READ_LEN)
             return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
                                               " bases (fc2_result.best_x is 16-bit)");
     h->n_pairs += h->bf_pairs.size();
-    h->bf_arena.append(16, '\0');                 // readers of the batch may load whole words past the end
+    h->bf_arena.resize(h->bf_narena + 16);       // readers of the batch may load whole words past the end
+    memset(h->bf_arena.data() + h->bf_narena, 0, 16);
     fc2_caller::Chunk c;
     c.frags.swap(h->bf_frags);
     c.nfrags = h->bf_nfrags;
@@ -1918,7 +2075,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     b->reads = (const uint8_t *)q.arena.data();
     b->read_off = q.b_off.data();
     b->pairs = q.b_pairs.data();
-    if (eof) *eof = h->eof ? 1 : 0;
+    if (eof) *eof = h->eof && !h->next_err ? 1 : 0;   // an error still to report: not the end yet
     return FC2_OK;
 }
 

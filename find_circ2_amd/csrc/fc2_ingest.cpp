@@ -1388,6 +1388,8 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
     return run_loop(h, p, max_frags, &sink, nullptr, eof);
 }
 
+bool fc2::ing::writes_records(const fc2_ingest *h) { return h && h->bam_out != nullptr; }
+
 extern "C" int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags,
                                fc2_ingest_counts *counts, const char **text, uint64_t *text_len, uint64_t *n_handed,
                                int *eof) {

@@ -92,5 +92,9 @@ using FragSink = std::function<int(Mate *m1, Mate *m2, bool must_see)>;
 // stops the loop and is returned.
 int pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof);
 
+// true when the ingest writes records while reading (-B, fc2_ingest_set_bam_out): the reference
+// stops writing at a failing fragment, so the caller must process each fragment as it comes
+bool writes_records(const fc2_ingest *h);
+
 }  // namespace ing
 }  // namespace fc2

@@ -1,6 +1,6 @@
-"""The native recording side on many workers (fc2_caller_submit's phases A-D) against the Python
-loop (find_circ2_amd.caller, a line-by-line restatement of find_circ.py:1276-1439): every output
-file and counter identical whatever the number of workers and of fragment ranges -- junction
+"""The native read loop on many workers -- fc2_caller_next's process_mate over fragment ranges and
+fc2_caller_submit's phases A-D -- against the Python loop (find_circ2_amd.caller, a line-by-line
+restatement of find_circ.py:1276-1439): every output file and counter identical whatever the number of workers and of fragment ranges -- junction
 names by first appearance (:684-686), float weight sums in input order (:544, :563, :579) -- and,
 on a run that fails part-way, the same partial outputs (spliced reads and multi_events rows of
 the fragments before the failing one, its test row when written before the failure)."""
@@ -14,8 +14,9 @@ from oracle_engine import oracle_evaluator_factory, pipelined_factory
 from test_ingest import same
 from test_native_caller import _rich_sam
 
-MODES = [dict(FC2_CALLER_THREADS="1"), dict(FC2_CALLER_THREADS="3", FC2_CALLER_MIN_RANGE="1"),
-         dict(FC2_CALLER_THREADS="8", FC2_CALLER_MIN_RANGE="5"), dict(FC2_CALLER_THREADS="16")]
+MODES = [dict(FC2_CALLER_THREADS="1", FC2_NEXT_THREADS="1"),
+         dict(FC2_CALLER_THREADS="3", FC2_NEXT_THREADS="2", FC2_CALLER_MIN_RANGE="1"),
+         dict(FC2_CALLER_THREADS="8", FC2_NEXT_THREADS="7", FC2_CALLER_MIN_RANGE="5"), dict(FC2_CALLER_THREADS="16")]
 
 
 @pytest.fixture(scope="module")
@@ -60,7 +61,7 @@ def _gz(path):
 
 
 @pytest.mark.parametrize("mode", range(len(MODES)))
-@pytest.mark.parametrize("bad", ["seq", "unspliced_none"])
+@pytest.mark.parametrize("bad", ["seq", "unspliced_none", "no_as"])
 def test_parallel_recording_fails_where_python_loop_fails(tmp_path, monkeypatch, rich, hit_names, mode, bad):
     """A read sequence with a byte outside the IUPAC table (rev_comp's KeyError in Hit.add,
     find_circ.py:573-582), or -- with --test -- a test name that parse_truth cannot read, in a
@@ -76,6 +77,8 @@ def test_parallel_recording_fails_where_python_loop_fails(tmp_path, monkeypatch,
                 f[9] = f[9][:40] + "." + f[9][41:]
             elif bad == "unspliced_none":
                 f[0] = target + "___O:chr1:x:+"          # int('x') in parse_truth (:1148-1200)
+            elif bad == "no_as":                         # uniqness: KeyError in process_mate (:809-819)
+                f = f[:11] + [t for t in f[11:] if not t.startswith("AS:")]
         out.append("\t".join(f))
     p = str(tmp_path / "bad.sam")
     open(p, "w").write("\n".join(out) + "\n")
