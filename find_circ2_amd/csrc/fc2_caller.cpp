@@ -8,6 +8,8 @@
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
+#include <sys/resource.h>
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -1963,6 +1965,12 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     ++h->n_chunks;
     int in_code = FC2_OK;                      // an error of the input (or, without defer, of a fragment)
     std::string in_msg;
+    static const bool timing = getenv("FC2_CALLER_TIMING") != nullptr;   // phase times on stderr
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto ms = [](std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+        return std::chrono::duration<double, std::milli>(b - a).count();
+    };
+    const auto t0 = now();
     while (!h->eof && h->bf_nfrags < limit) {
         int e = 0;
         const int rc = fc2::ing::pull(h->ing, &h->ip, limit, sink, &e);
@@ -1973,6 +1981,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         }
         h->eof = e != 0;
     }
+    const auto t1 = now();
     if (defer) {
         // process_mate of every fragment on the workers, in ranges; the first fragment that raises
         // ends the chunk there (an input error after it is never reached)
@@ -2023,6 +2032,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         }
         h->bf_nfrags = k;
     }
+    const auto t2 = now();
     if (in_code) {
         if (!h->bf_nfrags) return fc2::fail(in_code, in_msg);
         h->next_err = in_code;                     // hand out the fragments before it first
@@ -2058,6 +2068,9 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
                                               " bases (fc2_result.best_x is 16-bit)");
     h->n_pairs += h->bf_pairs.size();
+    if (timing)
+        fprintf(stderr, "next nf=%zu read=%.2f process=%.2f pairs=%.2f ms\n", h->bf_nfrags, ms(t0, t1), ms(t1, t2),
+                ms(t2, now()));
     h->bf_arena.resize(h->bf_narena + 16);       // readers of the batch may load whole words past the end
     memset(h->bf_arena.data() + h->bf_narena, 0, 16);
     fc2_caller::Chunk c;
@@ -2118,15 +2131,33 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
         const size_t nf = h->nfrags;
         const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)h->pool->size(), nf / std::max<size_t>(1, h->min_range_frags)));
         if (h->ranges.size() < T) h->ranges.resize(T);
+        static const bool timing = getenv("FC2_CALLER_TIMING") != nullptr;
+        auto now = [] { return std::chrono::steady_clock::now(); };
+        const auto t0 = now();
+        struct rusage ru0;
+        getrusage(RUSAGE_SELF, &ru0);
         h->pool->run_checked((int)T, [&](int r) { phase_a(h, nf * (size_t)r / T, nf * (size_t)(r + 1) / T, R, h->ranges[(size_t)r]); });
         uint64_t fe = nf;                       // the first fragment that raised (or none)
         size_t n_r = T;                         // the ranges that count: up to the one that raised
         for (size_t r = 0; r < T; ++r)
             if (h->ranges[r].err_frag >= 0) { fe = (uint64_t)h->ranges[r].err_frag; n_r = r + 1; break; }
         // (B) the shards apply their events in input order; (C) names; (D) read names, multi rows
+        const auto t1 = now();
         h->pool->run_checked(kShards, [&](int sidx) { phase_b(h, sidx, n_r, fe); });
+        const auto t2 = now();
         phase_c(h);
+        const auto t3 = now();
         h->pool->run_checked((int)n_r, [&](int r) { phase_d(h, h->ranges[(size_t)r], fe); });
+        const auto t4 = now();
+        if (timing) {
+            auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            struct rusage ru1;
+            getrusage(RUSAGE_SELF, &ru1);
+            fprintf(stderr, "submit nf=%zu T=%zu A=%.2f B=%.2f C=%.2f D=%.2f ms minflt=%ld user=%.1f sys=%.1f ms\n", nf, T,
+                    ms(t0, t1), ms(t1, t2), ms(t2, t3), ms(t3, t4), ru1.ru_minflt - ru0.ru_minflt,
+                    (ru1.ru_utime.tv_sec - ru0.ru_utime.tv_sec) * 1e3 + (ru1.ru_utime.tv_usec - ru0.ru_utime.tv_usec) / 1e3,
+                    (ru1.ru_stime.tv_sec - ru0.ru_stime.tv_sec) * 1e3 + (ru1.ru_stime.tv_usec - ru0.ru_stime.tv_usec) / 1e3);
+        }
         for (size_t r = 0; r < n_r; ++r) {
             RangeOut &ro = h->ranges[r];
             for (const auto &kv : ro.N) incN(h, kv.first, kv.second);
