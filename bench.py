@@ -588,12 +588,18 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
     zblk = 16 * (cap + 1)
     zctr = [torch.zeros(1, dtype=torch.int32, device=dev) for _ in subs]
 
-    def step(mode):                              # mode: None (scans only), 2, 4 (compact widths), 8 (raw), "z"
+    def step(mode):                              # mode: None (scans only), 2, 4 (compact widths), 8 (raw), "z", "zd"
         if mode == "z":
             for j, (k, lo, hi, s, res, comp) in enumerate(subs):
                 eb = zdev + merged[2]._w_bytes + k * zblk
                 scan_compact(opt, g, s, zdev + 2 * lo, 2, eb, cap, zctr[j].data_ptr(), eb + 16 * cap,
                              stream=stream.cuda_stream)
+            return
+        if mode == "zd":                         # the same launches writing into device memory
+            for j, (k, lo, hi, s, res, comp) in enumerate(subs):
+                c = comp[2]
+                scan_compact(opt, g, s, c.words.data_ptr(), 2, c.esc.data_ptr(), cap, zctr[j].data_ptr(),
+                             c.count.data_ptr(), stream=stream.cuda_stream)
             return
         for j, (k, lo, hi, s, res, comp) in enumerate(subs):
             t0 = clock() if clock else 0.0
@@ -632,12 +638,12 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
         barrier(ws)
         return max_over_ranks(time.perf_counter() - t0, ws, dev)
 
-    for mode in (2, 4, 8, "z"):
+    for mode in (2, 4, 8, "z", "zd"):
         for _ in range(max(1, warmup)):
             step(mode)
     torch.cuda.synchronize(dev)
     scan_s = timed(None)
-    t = {mode: timed(mode) for mode in (2, 4, 8, "z")}
+    t = {mode: timed(mode) for mode in (2, 4, 8, "z", "zd")}
     # checked passes, one per width (and the zero-copy form, which lands in the 2-byte buffer)
     equal, n_esc = {}, {}
     for w in widths + ("z",):
@@ -665,12 +671,17 @@ def strong_scaling(opt, g, b0, ref64, ws, rank, dev, steps, warmup, n, cfg_kw, p
             "ms_per_step": round(t["z"] / steps * 1e3, 4),
             "scan_only": {"value": round(n * steps / scan_s, 1), "ms_per_step": round(scan_s / steps * 1e3, 4),
                           "note": "scans writing 8-byte results to HBM, no merge"},
-            "merge_ms_per_step": round((t["z"] - scan_s) / steps * 1e3, 4),
+            "scan_only_compact_device": {"value": round(n * steps / t["zd"], 1),
+                                         "ms_per_step": round(t["zd"] / steps * 1e3, 4),
+                                         "note": "the merge's own launches (fc2_bp_scan_compact_launch, 2-byte words, "
+                                                 "escapes and count) writing into device memory, per-step barrier "
+                                                 "as in the merge: the baseline of merge_ms_per_step"},
+            "merge_ms_per_step": round((t["z"] - t["zd"]) / steps * 1e3, 4),
             "merge_form": "zero_copy_2B: the scan's epilogue writes each pair's 2-byte word, the escapes and the "
                           "batch's escape count straight into the shared page-locked buffer through its device "
-                          "address (fc2_bp_scan_compact_launch): no 8-byte results, pack launch or copy; a merge "
-                          "below 0 means that writing 2 B/pair over PCIe costs the scan less than the scans-only "
-                          "baseline's 8 B/pair to HBM",
+                          "address (fc2_bp_scan_compact_launch): no 8-byte results, pack launch or copy. "
+                          "merge_ms_per_step = that run minus the same launches writing to device memory with the same "
+                          "per-step barrier (scan_only_compact_device): the cost of the host destination alone",
             "merge_bytes_per_pair": 2, "escapes": n_esc["z"],
             "merge_2B_copied": dict(form(2), escapes=n_esc[2], merged_equals_single_rank=equal[2],
                                     note="8-byte scan, pack launch, D2H copy on a side stream"),

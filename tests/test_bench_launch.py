@@ -76,3 +76,26 @@ def test_two_ranks_configs3_and_configs4_on_hg19():
         assert c4["ranks"] == ranks and c4["pairs_total"] == 8_000_000
     assert one["configs4_200M_150bp"]["results_checksum"] == two["configs4_200M_150bp"]["results_checksum"]
     assert two["configs4_200M_150bp"]["pairs_per_rank"] == 4_000_000
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(1200)
+def test_two_ranks_full_size_configs3_and_configs4():
+    """The driver's N = 2 launch at the full sizes, so that the 8-GPU SCALE run exercises nothing
+    untested: configs[3]'s whole 50M-pair stream dealt round-robin to two ranks and merged through
+    the zero-copy 2-byte form equals the single-rank scan word for word (and the 4-byte and copied
+    forms too); configs[4]'s 200M-pair 120-150 bp stream in two shares has the single-rank
+    order-sensitive results checksum.  Per-rank shared-memory and page-locked sizes are those of
+    the N = 8 run."""
+    one = _bench(1, ["--no-cli"])
+    two = _bench(2, ["--no-cli"])
+    for line, ranks in ((one, 1), (two, 2)):
+        st = line["strong_scaling"]
+        assert line["n_gpus"] == ranks and st["ranks"] == ranks and st["pairs_total"] == 50_000_000
+        assert st["merged_equals_single_rank"] is True
+        assert st["merge_4B_words"]["merged_equals_single_rank"] is True
+        assert st["merge_2B_copied"]["merged_equals_single_rank"] is True
+        assert st["merge_ms_per_step"] > -0.5                  # the host destination's cost, not a kernel swap
+        c4 = line["configs4_200M_150bp"]
+        assert c4["ranks"] == ranks and c4["pairs_total"] == 200_000_000
+    assert one["configs4_200M_150bp"]["results_checksum"] == two["configs4_200M_150bp"]["results_checksum"]
