@@ -81,6 +81,10 @@ def main():
         L.fc2_set_tuning(10, 0 if not m else (-1 if m.group(1) == "A" else int(m.group(1))))
 
     junk = torch.empty(b.n, dtype=torch.int64, device=dev)
+    from find_circ2_amd import CompactResults
+    from find_circ2_amd.hotpath import expand, scan_compact
+    cres = {w: CompactResults(b.n, dev, cap=max(1 << 20, b.n // 64), width=w) for w in (2, 4)}
+    cctr = torch.zeros(1, dtype=torch.int32, device=dev)
 
     win = {}
 
@@ -105,6 +109,12 @@ def main():
                                             out.results.data_ptr(), None, b.tw,
                                             torch.cuda.current_stream(dev).cuda_stream))
             return
+        mc = re.match(r"cmp(2|4)", v)
+        if mc:                     # the same scan writing its results in a compact form (fc2_bp_scan_compact_launch)
+            c = cres[int(mc.group(1))]
+            scan_compact(opt, g, b, c.words.data_ptr(), c.width, c.esc.data_ptr(), c.cap, cctr.data_ptr(),
+                         c.count.data_ptr())
+            return
         if v.startswith("probe"):  # the scan's access pattern without its arithmetic (fc2_probe_pattern_launch)
             gv, bv, pv = g.view(), b.view(), opt.params()
             N.check(N.lib().fc2_probe_pattern_launch(ctypes.byref(pv), ctypes.byref(gv), ctypes.byref(bv),
@@ -126,7 +136,15 @@ def main():
             e.record(stream)
             torch.cuda.synchronize()
             times[v].append(s.elapsed_time(e) / a.reps)
-            assert a.no_check or v.startswith("probe") or torch.equal(out.results[:b.n], ref), "variant %s changed results" % v
+            assert a.no_check or v.startswith(("probe", "cmp")) or torch.equal(out.results[:b.n], ref), \
+                "variant %s changed results" % v
+    for w in (2, 4):                               # the compact variants' words expand to the 8-byte results
+        if "cmp%d" % w in variants and not a.no_check:
+            c = cres[w]
+            k = int(c.count.item())
+            assert k <= c.cap
+            esc = c.esc.cpu().numpy().view(N.ESCAPE_DTYPE)[:k]
+            assert np.array_equal(expand(opt, c.words[:b.n].cpu().numpy(), esc), ref.cpu().numpy()), "cmp%d" % w
     for v in variants:
         t = np.array(times[v])
         print(json.dumps({"variant": v, "workload": a.workload + ("-ordered" if a.ordered else ""), "pairs": b.n, "median_ms": round(float(np.median(t)), 4),
