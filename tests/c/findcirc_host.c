@@ -48,7 +48,13 @@ int main(int argc, char **argv) {
     }
     mkdir(outdir, 0755);
     fc2_fasta *fa = NULL;
-    if (fc2_fasta_open(genome, 1, &fa) != FC2_OK) return fail("fc2_fasta_open", fc2_last_error());
+    const int frc = fc2_fasta_open(genome, 1, &fa);
+    if (frc == FC2_E_IO) {   /* the reference's IOError: GenomeAccessor's all-N dummy mode (find_circ.py:338-345) */
+        fprintf(stderr, "Could not access '%s'. Switching to dummy mode (only Ns)\n", genome);
+        fa = NULL;
+    } else if (frc != FC2_OK) {
+        return fail("fc2_fasta_open", fc2_last_error());
+    }
     fc2_ctx *ctx = NULL;
     if (fc2_ctx_create(0, &ctx) != FC2_OK) return fail("fc2_ctx_create", fc2_last_error());
     if (fc2_ctx_genome_load(ctx, fa, 0) != FC2_OK) return fail("fc2_ctx_genome_load", fc2_ctx_last_error(ctx));
@@ -65,7 +71,7 @@ int main(int argc, char **argv) {
     fc2_ingest *ing = fc2_caller_ingest(c);
     const int n_ref = fc2_ingest_n_refs(ing);
     int32_t *t2c = (int32_t *)malloc(sizeof(int32_t) * (n_ref > 0 ? n_ref : 1));
-    for (int t = 0; t < n_ref; ++t) t2c[t] = fc2_fasta_find(fa, fc2_ingest_ref_name(ing, t));
+    for (int t = 0; t < n_ref; ++t) t2c[t] = fa ? fc2_fasta_find(fa, fc2_ingest_ref_name(ing, t)) : 0;
     if (fc2_caller_set_genome(c, t2c, n_ref, fa, NULL, NULL) != FC2_OK) return fail("fc2_caller_set_genome", fc2_last_error());
     char gz[4096];
     snprintf(gz, sizeof gz, "%s/spliced_reads.fastq.gz", outdir);
@@ -108,7 +114,7 @@ int main(int argc, char **argv) {
     }
     fc2_caller_close(c);
     fc2_ctx_destroy(ctx);
-    fc2_fasta_close(fa);
+    if (fa) fc2_fasta_close(fa);
     free(results);
     free(t2c);
     return 0;

@@ -113,9 +113,11 @@ def test_c_findcirc_builds_and_fails_cleanly_without_a_gpu(findcirc_host, tmp_pa
 
 
 @pytest.mark.gpu
-def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path):
+@pytest.mark.parametrize("genome", ["fasta", "folder"])
+def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path, genome):
     """The whole read loop and the search driven from C (no Python in the process) write the
-    Python CLI's files: both BED tables, multi_events.tsv and spliced_reads.fastq (decompressed)."""
+    Python CLI's files: both BED tables, multi_events.tsv and spliced_reads.fastq (decompressed).
+    With -G naming a folder, both run in GenomeAccessor's dummy mode (find_circ.py:338-345)."""
     import gzip
     import sys
     torch = pytest.importorskip("torch")
@@ -124,6 +126,9 @@ def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path):
     from test_ingest import _mixed_sam
     sam = str(tmp_path / "in.sam")
     fa = _mixed_sam(sam, 3000, seed=4711)
+    if genome == "folder":
+        fa = str(tmp_path / "genome_folder")
+        os.makedirs(fa)
     py_out, c_out = str(tmp_path / "py"), str(tmp_path / "c")
     r = subprocess.run([sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", py_out, "-n", "cx", "-q", sam],
                        cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=300)
@@ -135,6 +140,10 @@ def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path):
         a, b = open(os.path.join(py_out, f), "rb").read(), open(os.path.join(c_out, f), "rb").read()
         assert a == b, f
     circ = open(os.path.join(c_out, "circ_splice_sites.bed")).read().splitlines()
+    if genome == "folder":
+        assert b"Switching to dummy mode" in r.stderr
+        assert len(circ) == 1                         # the header: all-N windows never hold a GT/AG signal
+        return
     assert len(circ) > 10
     a = gzip.open(os.path.join(py_out, "spliced_reads.fastq.gz")).read()
     b = gzip.open(os.path.join(c_out, "spliced_reads.fastq.gz")).read()
