@@ -295,7 +295,7 @@ struct fc2_ingest::SamAhead {
         bool eof = false;                       // the last block of the input
     };
     static constexpr size_t kBlock = size_t(4) << 20;
-    static constexpr int kParsers = 2;
+    static constexpr int kParsers = 3;          // default parser threads (FC2_PARSE_THREADS)
     static constexpr size_t kInflight = 8;      // blocks read but not yet consumed
     std::mutex m;
     std::condition_variable cv;
@@ -1383,7 +1383,9 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
         fc2_ingest::SamAhead *ap = new fc2_ingest::SamAhead();
         h->ahead.reset(ap);
         ap->splitter = h->bam ? std::thread(bam_split_loop, h, ap) : std::thread(sam_split_loop, h, ap);
-        for (int k = 0; k < fc2_ingest::SamAhead::kParsers; ++k) ap->parsers.emplace_back(sam_parse_loop, h, ap);
+        const char *env = getenv("FC2_PARSE_THREADS");
+        const int np = env && atoi(env) > 0 ? std::min(atoi(env), 32) : fc2_ingest::SamAhead::kParsers;
+        for (int k = 0; k < np; ++k) ap->parsers.emplace_back(sam_parse_loop, h, ap);
     }
     return run_loop(h, p, max_frags, &sink, nullptr, eof);
 }
