@@ -1980,6 +1980,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     // instead of waiting for a whole first chunk; chunk boundaries change nothing in the outputs
     const uint64_t limit = std::max<uint64_t>(1, (uint64_t)h->o.chunksize >> (h->n_chunks < 4 ? 4 - h->n_chunks : 0));
     ++h->n_chunks;
+    if (h->bf_frags.size() < limit + 1) h->bf_frags.reserve(limit + 1);   // no Frag moved while the chunk forms
     int in_code = FC2_OK;                      // an error of the input (or, without defer, of a fragment)
     std::string in_msg;
     static const bool timing = getenv("FC2_CALLER_TIMING") != nullptr;   // phase times on stderr
@@ -1990,7 +1991,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     const auto t0 = now();
     while (!h->eof && h->bf_nfrags < limit) {
         int e = 0;
-        const int rc = fc2::ing::pull(h->ing, &h->ip, limit, sink, &e);
+        const int rc = fc2::ing::pull(h->ing, &h->ip, limit - h->bf_nfrags, sink, &e);   // at most `limit` per chunk
         if (rc) {
             in_code = err.code ? err.code : rc;
             in_msg = err.code ? err.msg : std::string(fc2_last_error());
@@ -2086,8 +2087,8 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
                                               " bases (fc2_result.best_x is 16-bit)");
     h->n_pairs += h->bf_pairs.size();
     if (timing)
-        fprintf(stderr, "next nf=%zu read=%.2f process=%.2f pairs=%.2f ms\n", h->bf_nfrags, ms(t0, t1), ms(t1, t2),
-                ms(t2, now()));
+        fprintf(stderr, "next nf=%zu read=%.2f (waiting for parsers %.2f) process=%.2f pairs=%.2f ms\n", h->bf_nfrags,
+                ms(t0, t1), fc2::ing::take_wait_ms(h->ing), ms(t1, t2), ms(t2, now()));
     h->bf_arena.resize(h->bf_narena + 16);       // readers of the batch may load whole words past the end
     memset(h->bf_arena.data() + h->bf_narena, 0, 16);
     fc2_caller::Chunk c;

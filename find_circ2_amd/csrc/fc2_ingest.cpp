@@ -26,6 +26,7 @@
 #include <memory>
 #include <mutex>
 #include <string>
+#include <chrono>
 #include <thread>
 #include <unordered_map>
 #include <vector>
@@ -304,6 +305,7 @@ struct fc2_ingest::SamAhead {
     std::vector<std::unique_ptr<Batch>> spare;
     size_t inflight = 0;
     uint64_t next_consume = 0;
+    double wait_ms = 0;                         // the consumer's time waiting for parsed batches
     std::unique_ptr<Batch> cur;                 // the consumer's batch
     size_t pos = 0;
     bool stop = false;
@@ -1016,7 +1018,11 @@ Rec *next_ahead(fc2_ingest *h, int &rc) {
     for (;;) {
         if (!A.cur) {
             std::unique_lock<std::mutex> lk(A.m);
-            A.cv.wait(lk, [&] { return A.done.count(A.next_consume) != 0; });
+            if (!A.done.count(A.next_consume)) {
+                const auto w0 = std::chrono::steady_clock::now();
+                A.cv.wait(lk, [&] { return A.done.count(A.next_consume) != 0; });
+                A.wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
+            }
             auto it = A.done.find(A.next_consume);
             A.cur = std::move(it->second);
             A.done.erase(it);
@@ -1391,6 +1397,13 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
 }
 
 bool fc2::ing::writes_records(const fc2_ingest *h) { return h && h->bam_out != nullptr; }
+
+double fc2::ing::take_wait_ms(fc2_ingest *h) {
+    if (!h || !h->ahead) return 0;
+    const double w = h->ahead->wait_ms;
+    h->ahead->wait_ms = 0;
+    return w;
+}
 
 extern "C" int fc2_ingest_next(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags,
                                fc2_ingest_counts *counts, const char **text, uint64_t *text_len, uint64_t *n_handed,

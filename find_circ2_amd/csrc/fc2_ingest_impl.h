@@ -96,5 +96,8 @@ int pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const Fr
 // stops writing at a failing fragment, so the caller must process each fragment as it comes
 bool writes_records(const fc2_ingest *h);
 
+// the consumer's time spent waiting for parse-ahead batches since the last call (FC2_CALLER_TIMING)
+double take_wait_ms(fc2_ingest *h);
+
 }  // namespace ing
 }  // namespace fc2

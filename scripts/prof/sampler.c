@@ -12,6 +12,9 @@
 #include <string.h>
 #include <time.h>
 #include <ucontext.h>
+#include <stdlib.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 
 #define MAXS (1 << 20)
 #define DEPTH 12
@@ -46,9 +49,15 @@ int sampler_start(int usec) {
     if (sigaction(SIGPROF, &sa, 0)) return -1;
     struct sigevent ev;
     memset(&ev, 0, sizeof ev);
-    ev.sigev_notify = SIGEV_SIGNAL;
     ev.sigev_signo = SIGPROF;
-    if (timer_create(CLOCK_MONOTONIC, &ev, &tid)) return -2;
+    if (getenv("FC2_SAMPLE_THREAD")) {           /* only the calling thread, on its own CPU clock */
+        ev.sigev_notify = SIGEV_THREAD_ID;
+        ev._sigev_un._tid = (pid_t)syscall(SYS_gettid);
+        if (timer_create(CLOCK_THREAD_CPUTIME_ID, &ev, &tid)) return -2;
+    } else {
+        ev.sigev_notify = SIGEV_SIGNAL;
+        if (timer_create(CLOCK_MONOTONIC, &ev, &tid)) return -2;
+    }
     struct itimerspec it;
     it.it_interval.tv_sec = 0;
     it.it_interval.tv_nsec = (long)usec * 1000L;
