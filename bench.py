@@ -33,14 +33,16 @@ sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 STRONG_TAIL = 0          # configs[3]: default --strong-tail (shard.round_bounds)
+HEADLINE_RESULT_BYTES = 2  # the headline scan's result form: 2-byte compact words (fc2_bp_scan_compact_launch)
 METRIC = "anchor-pairs/sec (backsplice calls) at 100 bp reads, 1/2/4/8 MI355X"
 
 
-def algo_bytes_per_pair(L: int, asize: int = 15, margin: int = 2) -> int:
-    """B(L) = ceil(l/4) + 2*ceil((l+2)/4) + 16 + 8 (2-bit read, two 2-bit windows,
-    16 B record, 8 B result); 81 B at L = 100."""
+def algo_bytes_per_pair(L: int, asize: int = 15, margin: int = 2, result_bytes: int = 8) -> int:
+    """B(L) = ceil(l/4) + 2*ceil((l+2)/4) + 16 + R (2-bit read, two 2-bit windows,
+    16 B record, R-byte result); 81 B at L = 100 with the 8-byte fc2_result, 75 B with the 2-byte
+    compact word the headline scan writes (round 4)."""
     l = L - 2 * (asize - margin)
-    return -(-l // 4) + 2 * (-(-(l + 2) // 4)) + 16 + 8
+    return -(-l // 4) + 2 * (-(-(l + 2) // 4)) + 16 + result_bytes
 
 
 def mean_algo_bytes(b, asize: int, margin: int) -> float:
@@ -76,7 +78,7 @@ def parse():
     ap.add_argument("--config4-pairs", type=int, default=0, help="configs[4] stream length (default 200M; tests)")
     ap.add_argument("--no-cli", action="store_true", help="skip the end-to-end CLI extra (2M reads, BAM on stdin)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r03.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r04.json"))
     return ap.parse_args()
 
 
@@ -509,13 +511,28 @@ def reorder_then_scan(opt, g, b, steps, dev, bpp):
                     "events); the headline keeps the read-order scan because this sum is larger"}
 
 
-def timed_scans(opt, g, b, steps, warmup, ws, dev):
-    """Warmup, then exactly `steps` scans bracketed by barrier + synchronize; per-launch HIP events."""
+def timed_scans(opt, g, b, steps, warmup, ws, dev, compact_width=0):
+    """Warmup, then exactly `steps` scans bracketed by barrier + synchronize; per-launch HIP events.
+    compact_width 2 / 4: the scans write their results in that compact form themselves
+    (fc2_bp_scan_compact_launch into device memory, canonical mode), and after the timed region the
+    words, expanded on the host, must equal the 8-byte scan's results word for word."""
     import torch
-    from find_circ2_amd import scan
+    from find_circ2_amd import CompactResults, scan
+    from find_circ2_amd.hotpath import expand, scan_compact
     out = scan(opt, g, b)
+    c = ctr = None
+    if compact_width:
+        c = CompactResults(b.n, dev, cap=max(1 << 16, b.n // 64), width=compact_width)
+        ctr = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def launch(stream=None):
+        if c is None:
+            scan(opt, g, b, out=out, stream=stream)
+        else:
+            scan_compact(opt, g, b, c.words.data_ptr(), c.width, c.esc.data_ptr(), c.cap, ctr.data_ptr(),
+                         c.count.data_ptr(), stream=stream)
     for _ in range(max(0, warmup - 1)):
-        scan(opt, g, b, out=out)
+        launch()
     torch.cuda.synchronize(dev)
     stream = torch.cuda.current_stream(dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
@@ -524,12 +541,21 @@ def timed_scans(opt, g, b, steps, warmup, ws, dev):
     t0 = time.perf_counter()
     for k in range(steps):
         ev[k][0].record(stream)
-        scan(opt, g, b, out=out, stream=stream.cuda_stream)
+        launch(stream.cuda_stream)
         ev[k][1].record(stream)
     torch.cuda.synchronize(dev)
     barrier(ws)
     t1 = time.perf_counter()
     kms = [s.elapsed_time(e) for s, e in ev]
+    if c is not None:                     # the compact words are the 8-byte results, exactly
+        k = int(c.count.item())
+        if k > c.cap:
+            raise RuntimeError("compact headline: %d escapes, %d slots" % (k, c.cap))
+        from find_circ2_amd import _native as N
+        esc = c.esc.cpu().numpy().view(N.ESCAPE_DTYPE)[:k]
+        words = c.words[:b.n].cpu().numpy()
+        if not np.array_equal(expand(opt, words, esc), out.results[:b.n].cpu().numpy()):
+            raise RuntimeError("compact headline: expanded words differ from the 8-byte scan")
     return t1 - t0, float(np.mean(kms)), out
 
 
@@ -1147,12 +1173,16 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     opt, g, b = build_workload(args, rank, dev)
-    elapsed, kernel_ms, out = timed_scans(opt, g, b, args.steps, args.warmup, ws, dev)
+    # the headline scan writes each pair's result as the 2-byte compact word (canonical mode; escapes
+    # for results that do not fit, none on this workload): 2.2 % faster than 8-byte words in a
+    # same-process A/B (profiles/r04/ab_compact_headline.jsonl), checked word for word after timing
+    cw = 0 if (opt.noncanonical or opt.allhits) else HEADLINE_RESULT_BYTES
+    elapsed, kernel_ms, out = timed_scans(opt, g, b, args.steps, args.warmup, ws, dev, compact_width=cw)
     elapsed = max_over_ranks(elapsed, ws, dev)
     kernel_ms = max_over_ranks(kernel_ms, ws, dev)
     total_pairs = b.n * args.steps * ws
     value = total_pairs / elapsed
-    bpp = algo_bytes_per_pair(args.read_len, opt.asize, opt.margin)
+    bpp = algo_bytes_per_pair(args.read_len, opt.asize, opt.margin, result_bytes=cw or 8)
     achieved = bpp * b.n / (kernel_ms * 1e-3) / 1e9
     # HBM bytes per launch from the PMC passes of scripts/profile_round.sh (a --pmc pass cannot run
     # inside this process); used only for the same workload, and stamped with the commit, kernel and
@@ -1196,7 +1226,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "u64",
+        "dtype": "u32",                 # the search's arithmetic: 32-bit integer bit planes
         "data": "synthetic (seeded; genome and anchor pairs generated on device, SURVEY.md 8(d))",
         "config": {
             "workload": ("configs[2]/[3]: hg19-shaped synthetic genome (93 @SQ contigs of test_norm.sam, 3.137 Gbp, "
@@ -1211,7 +1241,9 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "kernel_ms": round(kernel_ms, 4), "algo_bytes_per_pair": bpp,
-                     "kernel": kernel_label(g, args.locus_ordered)},
+                     "result_bytes_per_pair": cw or 8,
+                     "kernel": kernel_label(g, args.locus_ordered) +
+                     ("; each result written as a 2-byte compact word (fc2_bp_scan_compact_launch)" if cw else "")},
         "cpu_baseline": None,
         "strong_scaling": strong,
         "configs4_200M_150bp": c4,

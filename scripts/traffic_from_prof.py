@@ -85,7 +85,8 @@ def main():
     for v in out.values():
         v["commit"] = commit        # the tree the passes ran on (stamped when the JSON is built, locally)
     out["correction"] = ("reads = 2 x FETCH_SIZE x 1024 (gfx950 128-B fills tallied at 64 B), writes = WRITE_SIZE x "
-                         "1024 (exact: 8 B x pairs)")
+                         "1024 (exact: the result bytes x pairs -- 2 B compact words in the round-4 headline, the one "
+                         "8-B reference scan of the run averaged in)")
     out["source"] = ("rocprofv3 --kernel-trace --stats (r03: of the default bench run itself, averaged over the "
                      "dispatches on the whole 50M-pair batch) and separate --pmc passes of bench.py --steps 10 --warmup 2 "
                      "(scripts/profile_round.sh, scripts/profile_r03.sh); PMC averages over the scan-kernel dispatches")
