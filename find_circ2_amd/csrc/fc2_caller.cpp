@@ -1863,11 +1863,13 @@ void phase_d(const fc2_caller *h, RangeOut &ro, uint64_t fe) {
             o += t;
             const size_t n1 = o.size();
             o += '\n';
-            o += a.has_seq ? a.seq : std::string("None");
+            if (a.has_seq) o += a.seq;
+            else o += "None";
             o += "\n+";
             o.append(o, n0, n1 - n0);
             o += '\n';
-            o += a.has_qual ? a.qual : std::string("None");
+            if (a.has_qual) o += a.qual;
+            else o += "None";
             o += '\n';
         }
     }
