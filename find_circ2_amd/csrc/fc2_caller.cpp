@@ -34,7 +34,7 @@
 #include "fc2_gzpieces.h"
 #include "fc2_ingest_impl.h"
 
-using fc2::ing::Mate;
+using fc2::ing::MateRef;
 using fc2::ing::Rec;
 using fc2::ing::RecFields;
 
@@ -1179,13 +1179,13 @@ void process_frag(const fc2_caller *h, Frag &fr, const std::vector<RecFields> &r
 // have.  With `defer` the chunk's fragments are processed afterwards on the next side's workers
 // (fc2_caller_next); otherwise (-B writes records while reading, and the reference stops at a
 // failing fragment) here, raising where process_mate raises.
-int on_fragment(fc2_caller *h, Mate *m1, Mate *m2, bool defer) {
+int on_fragment(fc2_caller *h, MateRef *m1, MateRef *m2, bool defer) {
     // the next slot of the chunk; a recycled Frag is reset field by field (capacity kept)
     if (h->bf_nfrags == h->bf_frags.size()) h->bf_frags.emplace_back();
     Frag &fr = h->bf_frags[h->bf_nfrags];
-    fr.name.assign(m2->recs[0].qname);          // Fragment(mate2.primary.qname, ...)
+    fr.name.assign(m2->rec(0).qname);           // Fragment(mate2.primary.qname, ...)
     fr.dropped = false;
-    Mate *ms[2] = {m1, m2};
+    MateRef *ms[2] = {m1, m2};
     fr.span0 = h->bf_nspans;
     fr.arena0 = h->bf_narena;
     uint64_t smax = 0, amax = 0;
@@ -1195,18 +1195,18 @@ int on_fragment(fc2_caller *h, Mate *m1, Mate *m2, bool defer) {
         Frag::MateFields &mf = fr.mf[k];
         mf = Frag::MateFields();
         if (!ms[k]) continue;
-        const Mate &m = *ms[k];
+        const MateRef &m = *ms[k];
         mf.r0 = (uint32_t)h->bf_recf.size();
-        mf.nrec = (uint32_t)m.recs.size();
-        for (const Rec &r : m.recs) h->bf_recf.push_back(static_cast<const RecFields &>(r));
+        mf.nrec = m.n;
+        for (uint32_t j = 0; j < m.n; ++j) h->bf_recf.push_back(static_cast<const RecFields &>(m.rec(j)));
         mf.p0 = (uint32_t)h->bf_prop.size();
-        mf.np = (uint32_t)m.proper.size();
-        h->bf_prop.insert(h->bf_prop.end(), m.proper.begin(), m.proper.end());
+        mf.np = m.np;
+        h->bf_prop.insert(h->bf_prop.end(), m.proper, m.proper + m.np);
         if (mf.np >= 2) {
             smax += mf.np - 1;
-            amax += (uint64_t)(mf.np - 1) * m.recs[0].seq.size();
+            amax += (uint64_t)(mf.np - 1) * m.rec(0).seq.size();
         }
-        take_align(fr.prim[k], ms[k]->recs[0]);
+        take_align(fr.prim[k], m.rec(0));
     }
     fr.span_max = smax;
     h->bf_nspans += smax;
@@ -1970,7 +1970,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     // unless -B writes records while reading (the reference's writer stops at a failing fragment)
     const bool defer = !fc2::ing::writes_records(h->ing);
     Fatal err{0, ""};
-    const fc2::ing::FragSink sink = [&](Mate *m1, Mate *m2, bool) -> int {
+    const fc2::ing::FragSink sink = [&](MateRef *m1, MateRef *m2, bool) -> int {
         try {
             return on_fragment(h, m1, m2, defer);
         } catch (const Fatal &f) {
@@ -2088,9 +2088,12 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
                                               " bases (fc2_result.best_x is 16-bit)");
     h->n_pairs += h->bf_pairs.size();
-    if (timing)
-        fprintf(stderr, "next nf=%zu read=%.2f (waiting for parsers %.2f) process=%.2f pairs=%.2f ms\n", h->bf_nfrags,
-                ms(t0, t1), fc2::ing::take_wait_ms(h->ing), ms(t1, t2), ms(t2, now()));
+    if (timing) {
+        uint64_t grouped = 0;
+        const double wait = fc2::ing::take_wait_ms(h->ing, &grouped);
+        fprintf(stderr, "next nf=%zu read=%.2f (waiting for parsers %.2f, grouped there %llu) process=%.2f pairs=%.2f ms\n",
+                h->bf_nfrags, ms(t0, t1), wait, (unsigned long long)grouped, ms(t1, t2), ms(t2, now()));
+    }
     h->bf_arena.resize(h->bf_narena + 16);       // readers of the batch may load whole words past the end
     memset(h->bf_arena.data() + h->bf_narena, 0, 16);
     fc2_caller::Chunk c;

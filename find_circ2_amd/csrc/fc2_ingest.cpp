@@ -37,6 +37,7 @@
 #include "fc2_ingest_impl.h"
 
 using fc2::ing::Mate;
+using fc2::ing::MateRef;
 using fc2::ing::Rec;
 
 namespace {
@@ -294,8 +295,22 @@ struct fc2_ingest::SamAhead {
         int read_rc = FC2_OK;                   // read(2) failed after the block's lines: reported
         std::string read_err;                   // once they are parsed (records before an error first)
         bool eof = false;                       // the last block of the input
+        // fragments the parse thread grouped on its own (group_batch): records [gs, gt) form whole
+        // fragments (gs == gt: none); the handed ones are listed with the counts up to them
+        struct GFrag {
+            int32_t r0[2], n[2], p0[2], np[2];  // mate 0 = the other mate (n[0] == 0: none), 1 = current
+            bool must;
+            fc2_ingest_counts cum;              // counts of the region through this fragment
+            uint64_t frags;                     // fragments closed in the region through this one
+        };
+        uint32_t gs = 0, gt = 0;
+        std::vector<GFrag> gfrags;
+        std::vector<int32_t> gidx;              // record positions and proper indices of gfrags' mates
+        fc2_ingest_counts gtotal{};             // counts of the whole region (records [gs, gt))
+        uint64_t gtotal_frags = 0;
     };
     static constexpr size_t kBlock = size_t(4) << 20;
+    size_t block = kBlock;                      // FC2_PARSE_BLOCK (bytes): small blocks in the tests
     static constexpr int kParsers = 3;          // default parser threads (FC2_PARSE_THREADS)
     static constexpr size_t kInflight = 8;      // blocks read but not yet consumed
     std::mutex m;
@@ -308,6 +323,15 @@ struct fc2_ingest::SamAhead {
     double wait_ms = 0;                         // the consumer's time waiting for parsed batches
     std::unique_ptr<Batch> cur;                 // the consumer's batch
     size_t pos = 0;
+    // grouping on the parse threads (pull only: the sink path); the consumer's place in a batch's
+    // region: past its first record's close (in_region), the next handed fragment, counts applied
+    fc2_ingest_params gp{};
+    bool group = false;
+    bool in_region = false;
+    size_t gnext = 0;
+    fc2_ingest_counts gapplied{};
+    uint64_t gapplied_frags = 0;
+    uint64_t grouped = 0;                       // handed fragments grouped on the parse threads
     bool stop = false;
     std::thread splitter;
     std::vector<std::thread> parsers;
@@ -855,7 +879,7 @@ void sam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         carry.clear();
         // read until the block holds kBlock bytes and a newline, or the input ends
         bool has_nl = memchr(blk.data(), '\n', blk.size()) != nullptr;
-        while (!in_eof && (blk.size() < A.kBlock || !has_nl)) {
+        while (!in_eof && (blk.size() < A.block || !has_nl)) {
             if (A.wake[0] >= 0) {
                 pollfd pf[2] = {{h->fd, POLLIN, 0}, {A.wake[0], POLLIN, 0}};
                 int pr;
@@ -863,9 +887,9 @@ void sam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
                 if (pr > 0 && pf[1].revents) return;       // the ingest is closing
             }
             const size_t have = blk.size();
-            blk.resize(have + A.kBlock);
+            blk.resize(have + A.block);
             ssize_t k;
-            do { k = read(h->fd, &blk[have], A.kBlock); } while (k < 0 && errno == EINTR);
+            do { k = read(h->fd, &blk[have], A.block); } while (k < 0 && errno == EINTR);
             if (k < 0) {
                 blk.resize(have);
                 b->read_rc = FC2_E_IO;
@@ -928,7 +952,7 @@ void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
             b->read_err = "truncated BAM record" + (h->z_err.empty() ? "" : " (" + h->z_err + ")");
             b->eof = true;
         };
-        while (blk.size() < A.kBlock) {
+        while (blk.size() < A.block) {
             if (!ensure(h, 4)) {                // end of input (clean, or an input error first)
                 if (h->in_rc) { b->read_rc = h->in_rc; b->read_err = h->in_err; }
                 else if (!h->z_err.empty()) { b->read_rc = FC2_E_FORMAT; b->read_err = "BAM input: " + h->z_err; }
@@ -944,7 +968,7 @@ void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
                 memcpy(&bs, base + q, 4);
                 if (bs < 32 || q + 4 + (size_t)bs > h->end) break;
                 q += 4 + (size_t)bs;
-                if (blk.size() + (q - h->beg) >= A.kBlock) break;
+                if (blk.size() + (q - h->beg) >= A.block) break;
             }
             if (q > h->beg) {
                 blk.append(base + h->beg, q - h->beg);
@@ -964,6 +988,8 @@ void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         if (last) return;
     }
 }
+
+void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b);
 
 // parser: blocks to record batches (own RNAME cache and CIGAR scratch)
 void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
@@ -1002,6 +1028,8 @@ void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
             ++b->n;
         }
         if (b->rc == FC2_OK && b->read_rc) { b->rc = b->read_rc; b->err = b->read_err; }
+        b->gs = b->gt = 0;
+        if (A.group) group_batch(A.gp, *b);
         {
             std::lock_guard<std::mutex> lk(A.m);
             const uint64_t seq = b->seq;
@@ -1090,29 +1118,29 @@ struct MateEval {
     bool python_must_see = false;   // the reference would fail or compute on it: let the caller do it
 };
 
-MateEval eval_mate(const Mate &m, int asize) {
+MateEval eval_mate(const MateRef &m, int asize) {
     MateEval ev;
-    if (m.proper.size() < 2) { ev.unspliced = true; return ev; }
-    const Rec &prim = m.recs[0];
+    if (m.np < 2) { ev.unspliced = true; return ev; }
+    const Rec &prim = m.rec(0);
     if (!prim.has_seq) { ev.python_must_see = true; return ev; }   // len(None) in the reference
-    for (int k : m.proper) {
-        const Rec &s = m.recs[k];
+    for (uint32_t k = 0; k < m.np; ++k) {
+        const Rec &s = m.rec((size_t)m.proper[k]);
         if (s.qlen < 0 || s.aend < 0) { ev.python_must_see = true; return ev; }
     }
     int small[16];
     std::vector<int> big;
     int *segs = small;
-    const size_t n = m.proper.size();
-    if (n > 16) { big.assign(m.proper.begin(), m.proper.end()); segs = big.data(); }
-    else std::copy(m.proper.begin(), m.proper.end(), small);
+    const size_t n = m.np;
+    if (n > 16) { big.assign(m.proper, m.proper + n); segs = big.data(); }
+    else std::copy(m.proper, m.proper + n, small);
     for (size_t i = 1; i < n; ++i) {            // stable insertion sort by query start
         const int v = segs[i];
         size_t j = i;
-        while (j > 0 && m.recs[segs[j - 1]].astart > m.recs[v].astart) { segs[j] = segs[j - 1]; --j; }
+        while (j > 0 && m.rec((size_t)segs[j - 1]).astart > m.rec((size_t)v).astart) { segs[j] = segs[j - 1]; --j; }
         segs[j] = v;
     }
     for (size_t k = 0; k + 1 < n; ++k) {
-        const Rec &a = m.recs[segs[k]], &b = m.recs[segs[k + 1]];
+        const Rec &a = m.rec((size_t)segs[k]), &b = m.rec((size_t)segs[k + 1]);
         if (a.qlen < asize || b.qlen < asize) { ev.too_short++; continue; }
         // JunctionSpan.__init__ raises on these whether or not the span is ever evaluated
         // (uniqness: AS missing or not an integer, :809-819): the caller must see the fragment
@@ -1154,6 +1182,15 @@ int write_anchors(fc2_ingest *h, const Mate &m, int asize) {
     return put(m.recs[segs.back()]);
 }
 
+MateRef ref_of(Mate &m) {
+    MateRef r;
+    r.base = m.recs.begin();
+    r.n = (uint32_t)m.recs.size();
+    r.proper = m.proper.data();
+    r.np = (uint32_t)m.proper.size();
+    return r;
+}
+
 int emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed,
                   const fc2::ing::FragSink *sink) {
     h->counts.n_reads++;
@@ -1165,12 +1202,13 @@ int emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed,
                 if (int rc = write_anchors(h, *m, p->asize)) return rc;
     }
     const Mate *mates[2] = {h->have_other ? &h->other : nullptr, &h->current};
+    MateRef refs[2] = {h->have_other ? ref_of(h->other) : MateRef(), ref_of(h->current)};
     MateEval ev[2];
     int circ = 0, lin = 0;
     bool must = false;
     for (int k = 0; k < 2; ++k) {
         if (!mates[k]) continue;
-        ev[k] = eval_mate(*mates[k], p->asize);
+        ev[k] = eval_mate(refs[k], p->asize);
         circ += ev[k].n_circ;
         lin += ev[k].n_lin;
         must |= ev[k].python_must_see;
@@ -1186,13 +1224,157 @@ int emit_or_count(fc2_ingest *h, const fc2_ingest_params *p, uint64_t &n_handed,
     }
     ++n_handed;
     h->counts.handed_back++;
-    if (sink) return (*sink)(h->have_other ? &h->other : nullptr, &h->current, must);
+    if (sink) return (*sink)(h->have_other ? &refs[0] : nullptr, &refs[1], must);
     for (int k = 0; k < 2; ++k) {
         if (!mates[k]) continue;
         for (const Rec &r : mates[k]->recs) { h->out += r.text; h->out += '\n'; }
     }
     h->out += '\n';
     return FC2_OK;
+}
+
+// ---- grouping on the parse threads ---------------------------------------------------------------
+// The loop above closes a fragment at every mapped record whose qname differs from the current
+// primary's.  In a batch, let P be the qname of its first mapped record: the first mapped record
+// with another qname (gs) closes a fragment whatever came before the batch -- every mapped record
+// before it has qname P, so the primary then has qname P too (a continued mate keeps its primary,
+// whose qname matched; an opened one has qname P).  From gs on the batch is grouped here, on its
+// parse thread, exactly as the loop would: the fragments closed in [gs, gt) with their counts, the
+// handed ones listed for the sink; the consumer closes the fragment before gs, takes the list, and
+// goes on sequentially from gt (whose record opens the fragment still open at the batch's end).
+void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b) {
+    using Batch = fc2_ingest::SamAhead::Batch;
+    b.gs = b.gt = 0;
+    b.gfrags.clear();
+    b.gidx.clear();
+    b.gtotal = fc2_ingest_counts{};
+    b.gtotal_frags = 0;
+    Rec *R = b.recs.data();
+    const size_t n = b.n;
+    size_t i = 0;
+    while (i < n && R[i].unmapped()) ++i;
+    if (i == n) return;
+    size_t s = i + 1;
+    while (s < n && (R[s].unmapped() || R[s].qname == R[i].qname)) ++s;
+    if (s >= n) return;
+    struct LM {                                 // a mate: record positions, proper indices
+        std::vector<int32_t> r, p;
+    };
+    thread_local LM cur, oth;
+    bool have_oth = false;
+    fc2_ingest_counts C{};
+    uint64_t F = 0;
+    fc2_ingest_counts Ct{};
+    uint64_t Ft = 0;
+    size_t t = s;
+    auto open = [&](LM &m, size_t j) {
+        C.total_mates++;
+        m.r.clear();
+        m.p.clear();
+        m.r.push_back((int32_t)j);
+        m.p.push_back(0);
+    };
+    auto ref = [&](LM &m) {
+        MateRef x;
+        x.base = R;
+        x.idx = m.r.data();
+        x.n = (uint32_t)m.r.size();
+        x.proper = m.p.data();
+        x.np = (uint32_t)m.p.size();
+        return x;
+    };
+    // emit_or_count without a -B writer
+    auto close = [&]() {
+        C.n_reads++;
+        ++F;
+        if (p.noop) return;
+        LM *ms[2] = {have_oth ? &oth : nullptr, &cur};
+        MateEval ev[2];
+        int circ = 0, lin = 0;
+        bool must = false;
+        for (int k = 0; k < 2; ++k) {
+            if (!ms[k]) continue;
+            ev[k] = eval_mate(ref(*ms[k]), p.asize);
+            circ += ev[k].n_circ;
+            lin += ev[k].n_lin;
+            must |= ev[k].python_must_see;
+        }
+        const bool hand = must || ((circ || lin) && !(circ == 0 && p.nolinear));
+        if (!hand) {
+            for (int k = 0; k < 2; ++k) {
+                if (!ms[k]) continue;
+                if (ev[k].unspliced) C.unspliced_mates++;
+                C.seg_too_short_skip += (uint64_t)ev[k].too_short;
+            }
+            return;
+        }
+        C.handed_back++;
+        Batch::GFrag g;
+        for (int k = 0; k < 2; ++k) {
+            g.r0[k] = g.n[k] = g.p0[k] = g.np[k] = 0;
+            if (!ms[k]) continue;
+            g.r0[k] = (int32_t)b.gidx.size();
+            g.n[k] = (int32_t)ms[k]->r.size();
+            b.gidx.insert(b.gidx.end(), ms[k]->r.begin(), ms[k]->r.end());
+            g.p0[k] = (int32_t)b.gidx.size();
+            g.np[k] = (int32_t)ms[k]->p.size();
+            b.gidx.insert(b.gidx.end(), ms[k]->p.begin(), ms[k]->p.end());
+        }
+        g.must = must;
+        g.cum = C;
+        g.frags = F;
+        b.gfrags.push_back(g);
+    };
+    C.records++;
+    open(cur, s);
+    for (size_t j = s + 1; j < n; ++j) {
+        const Rec &r = R[j];
+        if (r.unmapped()) {
+            C.records++;
+            C.unmapped_reads++;
+            continue;
+        }
+        const Rec &prim = R[cur.r[0]];
+        const bool same = r.qname == prim.qname;
+        if (same && r.read1() == prim.read1()) {              // add_segment
+            C.records++;
+            const bool proper = r.tid == prim.tid && r.reverse() == prim.reverse();
+            cur.r.push_back((int32_t)j);
+            if (proper) cur.p.push_back((int32_t)cur.r.size() - 1);
+        } else if (same) {                                    // the other mate
+            C.records++;
+            std::swap(oth, cur);
+            have_oth = true;
+            open(cur, j);
+        } else {                                              // r closes the fragment
+            close();
+            Ct = C;                                           // the region ends before r ...
+            Ft = F;
+            t = j;
+            C.records++;                                      // ... if no later record closes one
+            have_oth = false;
+            open(cur, j);
+        }
+    }
+    if (t == s) {                                             // no fragment closed after gs's
+        b.gfrags.clear();
+        b.gidx.clear();
+        return;
+    }
+    b.gs = (uint32_t)s;
+    b.gt = (uint32_t)t;
+    b.gtotal = Ct;
+    b.gtotal_frags = Ft;
+}
+
+void add_counts(fc2_ingest_counts &c, const fc2_ingest_counts &to, const fc2_ingest_counts &from) {
+    c.n_reads += to.n_reads - from.n_reads;
+    c.total_mates += to.total_mates - from.total_mates;
+    c.unmapped_reads += to.unmapped_reads - from.unmapped_reads;
+    c.unspliced_mates += to.unspliced_mates - from.unspliced_mates;
+    c.seg_too_short_skip += to.seg_too_short_skip - from.seg_too_short_skip;
+    c.records += to.records - from.records;
+    c.handed_back += to.handed_back - from.handed_back;
 }
 
 }  // namespace
@@ -1330,6 +1512,57 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
     int rc = FC2_OK;
     bool done = h->finished;
     while (!done && frags < max_frags) {
+        // a batch's region grouped on its parse thread (group_batch): its first record closes the
+        // current fragment; then the region's handed fragments go to the sink, and its last
+        // record opens the fragment the loop goes on with
+        if (h->ahead && sink && h->ahead->cur && h->ahead->cur->gt > h->ahead->cur->gs &&
+            h->ahead->pos == h->ahead->cur->gs) {
+            auto &A = *h->ahead;
+            auto &b = *A.cur;
+            if (!A.in_region) {
+                rc = emit_or_count(h, p, handed, sink);
+                ++frags;
+                h->have_other = false;
+                recycle(h, h->other);
+                A.in_region = true;
+                A.gnext = 0;
+                A.gapplied = fc2_ingest_counts{};
+                A.gapplied_frags = 0;
+                if (rc) return rc;
+                continue;
+            }
+            while (A.gnext < b.gfrags.size() && frags < max_frags) {
+                const auto &g = b.gfrags[A.gnext++];
+                add_counts(h->counts, g.cum, A.gapplied);
+                h->n_records += g.cum.records - A.gapplied.records;
+                frags += g.frags - A.gapplied_frags;
+                A.gapplied = g.cum;
+                A.gapplied_frags = g.frags;
+                ++handed;
+                ++A.grouped;
+                MateRef m[2];
+                for (int k = 0; k < 2; ++k) {
+                    m[k].base = b.recs.data();
+                    m[k].idx = b.gidx.data() + g.r0[k];
+                    m[k].n = (uint32_t)g.n[k];
+                    m[k].proper = b.gidx.data() + g.p0[k];
+                    m[k].np = (uint32_t)g.np[k];
+                }
+                rc = (*sink)(g.n[0] ? &m[0] : nullptr, &m[1], g.must);
+                if (rc) return rc;
+            }
+            if (A.gnext < b.gfrags.size()) continue;          // stopped at max_frags: resumed here
+            add_counts(h->counts, b.gtotal, A.gapplied);
+            h->n_records += b.gtotal.records - A.gapplied.records;
+            frags += b.gtotal_frags - A.gapplied_frags;
+            A.in_region = false;
+            Rec &rt = b.recs[b.gt];                            // opens the next fragment
+            A.pos = (size_t)b.gt + 1;
+            h->n_records++;
+            h->counts.records++;
+            open_mate(h, h->current, rt);
+            continue;
+        }
         // the next record: in its parse batch, or parsed here into the scratch record
         Rec *rp = nullptr;
         rc = FC2_OK;
@@ -1388,9 +1621,15 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
     if (!h->ahead && (h->bam || h->src == fc2_ingest::SRC_RAW) && !h->bam_out && !h->finished) {
         fc2_ingest::SamAhead *ap = new fc2_ingest::SamAhead();
         h->ahead.reset(ap);
+        if (const char *be = getenv("FC2_PARSE_BLOCK"))
+            if (atol(be) > 0) ap->block = (size_t)atol(be);
         ap->splitter = h->bam ? std::thread(bam_split_loop, h, ap) : std::thread(sam_split_loop, h, ap);
         const char *env = getenv("FC2_PARSE_THREADS");
         const int np = env && atoi(env) > 0 ? std::min(atoi(env), 32) : fc2_ingest::SamAhead::kParsers;
+        // fragments grouped on the parse threads (FC2_GROUP_AHEAD=0: on the consumer, as before)
+        const char *ge = getenv("FC2_GROUP_AHEAD");
+        ap->gp = *p;
+        ap->group = !(ge && atoi(ge) == 0);
         for (int k = 0; k < np; ++k) ap->parsers.emplace_back(sam_parse_loop, h, ap);
     }
     return run_loop(h, p, max_frags, &sink, nullptr, eof);
@@ -1398,10 +1637,13 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
 
 bool fc2::ing::writes_records(const fc2_ingest *h) { return h && h->bam_out != nullptr; }
 
-double fc2::ing::take_wait_ms(fc2_ingest *h) {
+double fc2::ing::take_wait_ms(fc2_ingest *h, uint64_t *grouped) {
+    if (grouped) *grouped = 0;
     if (!h || !h->ahead) return 0;
     const double w = h->ahead->wait_ms;
     h->ahead->wait_ms = 0;
+    if (grouped) *grouped = h->ahead->grouped;
+    h->ahead->grouped = 0;
     return w;
 }
 

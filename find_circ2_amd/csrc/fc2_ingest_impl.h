@@ -82,11 +82,24 @@ struct Mate {
     bool valid = false;
 };
 
+// A mate as the sink sees it: its records, the primary first, and the indices of its proper
+// segments among them.  The records sit in the ingest's Mate or -- for a fragment a parse thread
+// grouped on its own (group_batch in fc2_ingest.cpp) -- in place in their parse batch, where `idx`
+// lists their positions.
+struct MateRef {
+    Rec *base = nullptr;
+    const int32_t *idx = nullptr;      // null: the records are base[0, n)
+    uint32_t n = 0;
+    const int32_t *proper = nullptr;   // indices into this mate's records
+    uint32_t np = 0;
+    Rec &rec(size_t k) const { return base[idx ? idx[k] : k]; }
+};
+
 // Fragments that carry anchor pairs (or that the reference would fail on: must_see) are passed
 // to the sink in input order; m1 = the other mate (may be null), m2 = the current mate.
 // The sink may take the mates' strings (swap them out): the loop reads nothing of a fragment's
 // records after handing it over.
-using FragSink = std::function<int(Mate *m1, Mate *m2, bool must_see)>;
+using FragSink = std::function<int(MateRef *m1, MateRef *m2, bool must_see)>;
 
 // The loop of fc2_ingest_next with a sink instead of SAM text; a non-zero return of the sink
 // stops the loop and is returned.
@@ -96,8 +109,9 @@ int pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const Fr
 // stops writing at a failing fragment, so the caller must process each fragment as it comes
 bool writes_records(const fc2_ingest *h);
 
-// the consumer's time spent waiting for parse-ahead batches since the last call (FC2_CALLER_TIMING)
-double take_wait_ms(fc2_ingest *h);
+// the consumer's time spent waiting for parse-ahead batches since the last call, and the handed
+// fragments grouped on the parse threads meanwhile (FC2_CALLER_TIMING)
+double take_wait_ms(fc2_ingest *h, uint64_t *grouped = nullptr);
 
 }  // namespace ing
 }  // namespace fc2

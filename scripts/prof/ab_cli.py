@@ -2,8 +2,9 @@
 """Same-box A/B of the whole CLI (two-thread loop, GPU search): libfc2_<NAME>.so against the tree's
 libfc2.so on one generated hg19-sized input, alternating, one process per run (the library is chosen
 at import through FC2_LIB_VARIANT), in bench.py's two forms: BGZF BAM piped on stdin and SAM by path.
-Every run's output files must equal the first run's.  One JSON line per run.
-usage: ab_cli.py NAME [rounds] [reads]"""
+NAME may also be env:K=V[,K=V...] (the tree's library under those environment settings), and several
+variants joined by '+'.  Every run's output files must equal the first run's.  One JSON line per run.
+usage: ab_cli.py NAME[+NAME...] [rounds] [reads]"""
 import gzip
 import json
 import os
@@ -46,13 +47,17 @@ def main():
     sam_to_bam(sam, bam)
     ref = None
     for r in range(rounds + 1):                  # round 0 builds the .byo_index (not reported)
-        for v in (name, "cur"):
+        for v in name.split("+") + ["cur"]:
             for form in ("bam_stdin", "sam_path"):
                 env = dict(os.environ)
                 env.pop("FC2_LIB_VARIANT", None)
-                if v != "cur":
+                if v.startswith("env:"):
+                    for kv in v[4:].split(","):
+                        k, _, val = kv.partition("=")
+                        env[k] = val
+                elif v != "cur":
                     env["FC2_LIB_VARIANT"] = v
-                out = os.path.join(d, "out_%s_%s" % (v, form))
+                out = os.path.join(d, "out_%s_%s" % (re.sub(r"[^A-Za-z0-9_]", "_", v), form))
                 cmd = [sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", out, "-q"]
                 t0 = time.time()
                 if form == "bam_stdin":

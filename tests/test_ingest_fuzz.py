@@ -153,14 +153,19 @@ def test_corrupt_bam_records_are_errors(tmp_path, case):
         _python_all(str(p))
 
 
+@pytest.mark.parametrize("block", [None, "900"])
 @pytest.mark.parametrize("form", ["bam_bgzf", "bam_gzip", "bam_raw", "sam"])
-def test_parse_ahead_equals_sequential_reader_on_damage(forms, tmp_path, form):
+def test_parse_ahead_equals_sequential_reader_on_damage(forms, tmp_path, monkeypatch, form, block):
     """The native loop's parse-ahead threads (BAM: records cut into blocks from the decompressed
-    stream; SAM: newline-aligned blocks) against the sequential reader the loop uses with -B: the
-    same exit status on every damaged input and, when a run completes, the same files.  The reader
-    must stop exactly where the sequential one reports the damage."""
+    stream; SAM: newline-aligned blocks; fragments grouped on the parse threads from each block's
+    first closing record on) against the sequential reader the loop uses with -B: the same exit
+    status on every damaged input and, when a run completes, the same files.  The reader must stop
+    exactly where the sequential one reports the damage.  block: the parse block size in bytes
+    (FC2_PARSE_BLOCK; default 4 MiB), small enough here for fragments to straddle blocks."""
     import gzip as gz
     import os
+    if block:
+        monkeypatch.setenv("FC2_PARSE_BLOCK", block)
     d, fa, data = forms
     rng = random.Random(2027 + len(form))
     n_err = 0
