@@ -224,6 +224,21 @@ struct Frag {
     uint64_t span0 = 0, span_max = 0;          // its span slots [span0, span0 + span_max) in the chunk
     uint64_t arena0 = 0;                       // its read_part bytes from here (at most one read per pair)
     bool dropped = false;                      // no pair record_hits would look at (on_fragment)
+    // recorded in place (a fragment grouped on a parse thread, its batch pinned until the chunk is
+    // processed): the mates' records are read where they are, name and primaries taken by
+    // process_frag on the workers instead of by on_fragment
+    bool in_batch = false;
+    MateRef ref[2];
+};
+
+// a mate's records as process_mate reads them: recorded fields, or records in their parse batch
+struct RecsView {
+    const RecFields *fields = nullptr;
+    const Rec *recs = nullptr;
+    const int32_t *idx = nullptr;
+    const RecFields &operator[](size_t k) const {
+        return fields ? fields[k] : static_cast<const RecFields &>(recs[idx[k]]);
+    }
 };
 
 using Coord = std::tuple<std::string, int64_t, int64_t, std::string>;   // (chrom, start, end, strand)
@@ -1073,7 +1088,7 @@ const char *kNoneLen = "TypeError: object of type 'NoneType' has no len()";
 // process_mate (:1492-1527) with adjacent_segment_pairs (:1058-1140), on the mate's recorded
 // fields (Frag::MateFields) and its primary's sequence (fr.prim[mi], taken by on_fragment): spans
 // into the fragment's slots of `spans` from *sk on, read parts into `arena` from *ap on
-void process_mate(const fc2_caller *h, const RecFields *recs, size_t nrec, const int32_t *proper, size_t n, int mi,
+void process_mate(const fc2_caller *h, const RecsView &recs, size_t nrec, const int32_t *proper, size_t n, int mi,
                   Frag &fr, Span *spans, uint64_t &sk, char *arena, uint64_t &ap,
                   std::vector<std::pair<const char *, double>> &N) {
     const RecFields &prim = recs[0];
@@ -1165,11 +1180,26 @@ void process_frag(const fc2_caller *h, Frag &fr, const std::vector<RecFields> &r
     fr.unspliced.clear();
     fr.broken.clear();
     for (uint64_t k = 0; k < fr.span_max; ++k) spans[fr.span0 + k].eval = -1;   // unused slots
+    if (fr.in_batch) {                          // what on_fragment takes of a fragment it recorded in place
+        fr.name.assign(fr.ref[1].rec(0).qname);
+        for (int k = 0; k < 2; ++k)
+            if (fr.has[k]) take_align(fr.prim[k], fr.ref[k].rec(0));
+    }
     uint64_t sk = fr.span0, ap = fr.arena0;
     for (int k = 0; k < 2; ++k) {
         if (!fr.has[k]) continue;
-        const Frag::MateFields &mf = fr.mf[k];
-        process_mate(h, recf.data() + mf.r0, mf.nrec, prop.data() + mf.p0, mf.np, k, fr, spans, sk, arena, ap, N);
+        if (fr.in_batch) {
+            const MateRef &m = fr.ref[k];
+            RecsView v;
+            v.recs = m.base;
+            v.idx = m.idx;
+            process_mate(h, v, m.n, m.proper, m.np, k, fr, spans, sk, arena, ap, N);
+        } else {
+            const Frag::MateFields &mf = fr.mf[k];
+            RecsView v;
+            v.fields = recf.data() + mf.r0;
+            process_mate(h, v, mf.nrec, prop.data() + mf.p0, mf.np, k, fr, spans, sk, arena, ap, N);
+        }
     }
     fr.dropped = (fr.circ.empty() && h->o.nolinear) || (fr.circ.empty() && fr.lin.empty());
 }
@@ -1183,7 +1213,8 @@ int on_fragment(fc2_caller *h, MateRef *m1, MateRef *m2, bool defer) {
     // the next slot of the chunk; a recycled Frag is reset field by field (capacity kept)
     if (h->bf_nfrags == h->bf_frags.size()) h->bf_frags.emplace_back();
     Frag &fr = h->bf_frags[h->bf_nfrags];
-    fr.name.assign(m2->rec(0).qname);           // Fragment(mate2.primary.qname, ...)
+    fr.in_batch = defer && m2->stable && (!m1 || m1->stable);
+    if (!fr.in_batch) fr.name.assign(m2->rec(0).qname);   // Fragment(mate2.primary.qname, ...)
     fr.dropped = false;
     MateRef *ms[2] = {m1, m2};
     fr.span0 = h->bf_nspans;
@@ -1196,16 +1227,20 @@ int on_fragment(fc2_caller *h, MateRef *m1, MateRef *m2, bool defer) {
         mf = Frag::MateFields();
         if (!ms[k]) continue;
         const MateRef &m = *ms[k];
+        if (m.np >= 2) {
+            smax += m.np - 1;
+            amax += (uint64_t)(m.np - 1) * m.seq_len;
+        }
+        if (fr.in_batch) {                      // read in place by process_frag
+            fr.ref[k] = m;
+            continue;
+        }
         mf.r0 = (uint32_t)h->bf_recf.size();
         mf.nrec = m.n;
         for (uint32_t j = 0; j < m.n; ++j) h->bf_recf.push_back(static_cast<const RecFields &>(m.rec(j)));
         mf.p0 = (uint32_t)h->bf_prop.size();
         mf.np = m.np;
         h->bf_prop.insert(h->bf_prop.end(), m.proper, m.proper + m.np);
-        if (mf.np >= 2) {
-            smax += mf.np - 1;
-            amax += (uint64_t)(mf.np - 1) * m.rec(0).seq.size();
-        }
         take_align(fr.prim[k], m.rec(0));
     }
     fr.span_max = smax;
@@ -1969,6 +2004,9 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     // the chunk's fragments are processed after they are all read, on the next side's workers --
     // unless -B writes records while reading (the reference's writer stops at a failing fragment)
     const bool defer = !fc2::ing::writes_records(h->ing);
+    // fragments grouped on the parse threads are recorded in place: their batches stay pinned until
+    // this chunk's fragments are processed below
+    fc2::ing::set_pin(h->ing, defer);
     Fatal err{0, ""};
     const fc2::ing::FragSink sink = [&](MateRef *m1, MateRef *m2, bool) -> int {
         try {
@@ -2051,6 +2089,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             ++k;
         }
         h->bf_nfrags = k;
+        fc2::ing::release(h->ing);             // every kept fragment has taken what it needs
     }
     const auto t2 = now();
     if (in_code) {

@@ -259,6 +259,7 @@ struct fc2_ingest {
     fc2_ingest_counts counts{};
     bool finished = false;
     bool need_text = true;       // false once a native caller pulls structured fragments
+    bool pin = false;            // fc2::ing::set_pin (applies to the parse-ahead batches)
     // fc2_ingest_next: an error met after some fragments were formed is returned by the next call,
     // after those fragments (the reference records each fragment before it reads the next)
     int deferred_rc = FC2_OK;
@@ -299,6 +300,7 @@ struct fc2_ingest::SamAhead {
         // fragments (gs == gt: none); the handed ones are listed with the counts up to them
         struct GFrag {
             int32_t r0[2], n[2], p0[2], np[2];  // mate 0 = the other mate (n[0] == 0: none), 1 = current
+            uint32_t seq_len[2];                // len(SEQ) of each mate's primary
             bool must;
             fc2_ingest_counts cum;              // counts of the region through this fragment
             uint64_t frags;                     // fragments closed in the region through this one
@@ -332,6 +334,8 @@ struct fc2_ingest::SamAhead {
     fc2_ingest_counts gapplied{};
     uint64_t gapplied_frags = 0;
     uint64_t grouped = 0;                       // handed fragments grouped on the parse threads
+    bool pin = false;                           // set_pin: consumed batches wait in `pinned` for release()
+    std::vector<std::unique_ptr<Batch>> pinned;
     bool stop = false;
     std::thread splitter;
     std::vector<std::thread> parsers;
@@ -1063,7 +1067,8 @@ Rec *next_ahead(fc2_ingest *h, int &rc) {
         {
             std::lock_guard<std::mutex> lk(A.m);
             --A.inflight;
-            A.spare.push_back(std::move(A.cur));
+            if (A.pin) A.pinned.push_back(std::move(A.cur));
+            else A.spare.push_back(std::move(A.cur));
         }
         A.cv.notify_all();
     }
@@ -1188,6 +1193,7 @@ MateRef ref_of(Mate &m) {
     r.n = (uint32_t)m.recs.size();
     r.proper = m.proper.data();
     r.np = (uint32_t)m.proper.size();
+    r.seq_len = m.recs.empty() ? 0 : (uint32_t)m.recs[0].seq.size();
     return r;
 }
 
@@ -1312,7 +1318,9 @@ void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b) {
         Batch::GFrag g;
         for (int k = 0; k < 2; ++k) {
             g.r0[k] = g.n[k] = g.p0[k] = g.np[k] = 0;
+            g.seq_len[k] = 0;
             if (!ms[k]) continue;
+            g.seq_len[k] = (uint32_t)R[ms[k]->r[0]].seq.size();
             g.r0[k] = (int32_t)b.gidx.size();
             g.n[k] = (int32_t)ms[k]->r.size();
             b.gidx.insert(b.gidx.end(), ms[k]->r.begin(), ms[k]->r.end());
@@ -1547,6 +1555,8 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
                     m[k].n = (uint32_t)g.n[k];
                     m[k].proper = b.gidx.data() + g.p0[k];
                     m[k].np = (uint32_t)g.np[k];
+                    m[k].seq_len = g.seq_len[k];
+                    m[k].stable = A.pin;
                 }
                 rc = (*sink)(g.n[0] ? &m[0] : nullptr, &m[1], g.must);
                 if (rc) return rc;
@@ -1630,12 +1640,31 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
         const char *ge = getenv("FC2_GROUP_AHEAD");
         ap->gp = *p;
         ap->group = !(ge && atoi(ge) == 0);
+        ap->pin = h->pin;
         for (int k = 0; k < np; ++k) ap->parsers.emplace_back(sam_parse_loop, h, ap);
     }
     return run_loop(h, p, max_frags, &sink, nullptr, eof);
 }
 
 bool fc2::ing::writes_records(const fc2_ingest *h) { return h && h->bam_out != nullptr; }
+
+void fc2::ing::set_pin(fc2_ingest *h, bool on) {
+    if (!h) return;
+    h->pin = on;
+    if (h->ahead) h->ahead->pin = on;
+    if (!on) release(h);
+}
+
+void fc2::ing::release(fc2_ingest *h) {
+    if (!h || !h->ahead || h->ahead->pinned.empty()) return;
+    auto &A = *h->ahead;
+    {
+        std::lock_guard<std::mutex> lk(A.m);
+        for (auto &b : A.pinned) A.spare.push_back(std::move(b));
+    }
+    A.pinned.clear();
+    A.cv.notify_all();
+}
 
 double fc2::ing::take_wait_ms(fc2_ingest *h, uint64_t *grouped) {
     if (grouped) *grouped = 0;

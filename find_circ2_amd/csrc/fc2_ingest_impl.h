@@ -92,6 +92,10 @@ struct MateRef {
     uint32_t n = 0;
     const int32_t *proper = nullptr;   // indices into this mate's records
     uint32_t np = 0;
+    uint32_t seq_len = 0;              // len(SEQ) of the primary (rec(0).seq.size())
+    // the records (and idx, proper) stay where they are until release(): the sink may keep the
+    // reference instead of copying what it needs (set_pin; fragments grouped on a parse thread)
+    bool stable = false;
     Rec &rec(size_t k) const { return base[idx ? idx[k] : k]; }
 };
 
@@ -108,6 +112,11 @@ int pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const Fr
 // true when the ingest writes records while reading (-B, fc2_ingest_set_bam_out): the reference
 // stops writing at a failing fragment, so the caller must process each fragment as it comes
 bool writes_records(const fc2_ingest *h);
+
+// pinning: with `on`, parse batches whose fragments were handed over stay untouched (their records
+// are not reused) until release(); the sink then gets stable MateRefs for them
+void set_pin(fc2_ingest *h, bool on);
+void release(fc2_ingest *h);
 
 // the consumer's time spent waiting for parse-ahead batches since the last call, and the handed
 // fragments grouped on the parse threads meanwhile (FC2_CALLER_TIMING)
