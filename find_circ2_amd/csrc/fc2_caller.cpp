@@ -2130,8 +2130,11 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     if (timing) {
         uint64_t grouped = 0;
         const double wait = fc2::ing::take_wait_ms(h->ing, &grouped);
-        fprintf(stderr, "next nf=%zu read=%.2f (waiting for parsers %.2f, grouped there %llu) process=%.2f pairs=%.2f ms\n",
-                h->bf_nfrags, ms(t0, t1), wait, (unsigned long long)grouped, ms(t1, t2), ms(t2, now()));
+        double iw, sb, pi;
+        fc2::ing::take_stage_ms(h->ing, &iw, &sb, &pi);
+        fprintf(stderr, "next nf=%zu read=%.2f (waiting for parsers %.2f, grouped there %llu) process=%.2f pairs=%.2f ms"
+                " | upstream: inflate wait %.2f, splitter blocked %.2f, parsers idle %.2f ms\n",
+                h->bf_nfrags, ms(t0, t1), wait, (unsigned long long)grouped, ms(t1, t2), ms(t2, now()), iw, sb, pi);
     }
     h->bf_arena.resize(h->bf_narena + 16);       // readers of the batch may load whole words past the end
     memset(h->bf_arena.data() + h->bf_narena, 0, 16);

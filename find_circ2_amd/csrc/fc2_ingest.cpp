@@ -125,10 +125,37 @@ size_t bgzf_block_size(const uint8_t *h, size_t avail) {
     return 0;
 }
 
+// a byte vector whose growth leaves the new bytes uninitialised (inflate overwrites them)
+template <class T>
+struct NoInitAlloc : std::allocator<T> {
+    template <class U>
+    struct rebind {
+        using other = NoInitAlloc<U>;
+    };
+    NoInitAlloc() = default;
+    template <class U>
+    NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+    template <class U>
+    void construct(U *p) noexcept {
+        ::new (static_cast<void *>(p)) U;
+    }
+    template <class U, class... Args>
+    void construct(U *p, Args &&...args) {
+        ::new (static_cast<void *>(p)) U(std::forward<Args>(args)...);
+    }
+};
+using CharBuf = std::vector<char, NoInitAlloc<char>>;
+
+// kHead bytes of headroom in front of a batch's inflated bytes: the parse-ahead splitter moves the
+// record cut by the previous batch's end there instead of copying the batch (bgzf_split_loop)
+constexpr size_t kHead = size_t(1) << 16;
+
 struct BgzfBatch {
-    std::vector<char> out;
+    CharBuf out;                 // kHead bytes of headroom, then the inflated bytes
+    size_t n = 0;                // inflated bytes
     bool eof = false;
     std::string err;
+    const char *data() const { return out.data() + kHead; }
 };
 
 int bgzf_threads() {
@@ -180,7 +207,8 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
         const uint8_t *t = raw.data() + boff[i] + bsz[i] - 4;
         ooff[i + 1] = ooff[i] + (size_t)(t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24));
     }
-    B.out.resize(ooff[nb]);
+    B.n = ooff[nb];
+    B.out.resize(kHead + B.n);
     std::atomic<size_t> next{0};
     std::atomic<bool> bad{false};
     auto work = [&]() {
@@ -193,7 +221,7 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
             zs.next_in = (Bytef *)(blk + 12 + xl);
             zs.avail_in = (uInt)(bsz[i] - 12 - xl - 8);
             uint8_t none = 0;                   // an empty block (the EOF marker): zlib wants a real pointer
-            zs.next_out = ooff[i + 1] > ooff[i] ? (Bytef *)(B.out.data() + ooff[i]) : (Bytef *)&none;
+            zs.next_out = ooff[i + 1] > ooff[i] ? (Bytef *)(B.out.data() + kHead + ooff[i]) : (Bytef *)&none;
             zs.avail_out = (uInt)(ooff[i + 1] - ooff[i]);
             const int rc = inflate(&zs, Z_FINISH);
             const uint8_t *t = blk + bsz[i] - 8;
@@ -239,7 +267,9 @@ struct fc2_ingest {
     // BGZF (the BAM case): batches inflated in parallel, one batch ahead of the parser
     bool bgzf = false;
     int bgzf_nt = 1;
+    int bgzf_blocks = 256;       // BGZF blocks per inflated batch (FC2_BGZF_BATCH: small in the tests)
     std::future<BgzfBatch> bgzf_next;
+    std::atomic<int64_t> inflate_wait_ns{0};     // the reader's wait for inflated BGZF batches (timing)
     std::string z_err;
     // header
     std::string header;
@@ -289,6 +319,9 @@ struct fc2_ingest::SamAhead {
     struct Batch {
         uint64_t seq = 0;
         std::string block;                      // the block's bytes (whole lines)
+        // or, BGZF input (bgzf_split_loop): whole records in place in an inflated batch
+        std::shared_ptr<const CharBuf> vbuf;
+        size_t voff = 0, vlen = 0;
         std::vector<Rec> recs;
         size_t n = 0;
         int rc = FC2_OK;
@@ -323,6 +356,9 @@ struct fc2_ingest::SamAhead {
     size_t inflight = 0;
     uint64_t next_consume = 0;
     double wait_ms = 0;                         // the consumer's time waiting for parsed batches
+    // FC2_CALLER_TIMING: the splitter blocked on the consumer (all blocks in flight), the parsers
+    // idle (no block to parse), summed over parser threads
+    std::atomic<int64_t> split_block_ns{0}, parse_idle_ns{0};
     std::unique_ptr<Batch> cur;                 // the consumer's batch
     size_t pos = 0;
     // grouping on the parse threads (pull only: the sink path); the consumer's place in a batch's
@@ -396,14 +432,16 @@ bool ensure(fc2_ingest *h, size_t n) {
             h->end += (size_t)k;
         } else if (h->src == fc2_ingest::SRC_BGZF) {
             if (h->z_done) return false;
-            BgzfBatch b = h->bgzf_next.get();
+            const auto w0 = std::chrono::steady_clock::now();
+            BgzfBatch b = h->bgzf_next.get();   // (bgzf_split_loop reads batches without this copy)
+            h->inflate_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             if (!b.err.empty()) { h->z_err = b.err; h->z_done = true; return false; }
             if (b.eof) h->z_done = true;
-            else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), 256,
+            else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), h->bgzf_blocks,
                                            h->bgzf_nt);
-            if (h->buf.size() < h->end + b.out.size()) h->buf.resize(h->end + b.out.size());
-            if (!b.out.empty()) memcpy(h->buf.data() + h->end, b.out.data(), b.out.size());
-            h->end += b.out.size();
+            if (h->buf.size() < h->end + b.n) h->buf.resize(h->end + b.n);
+            if (b.n) memcpy(h->buf.data() + h->end, b.data(), b.n);
+            h->end += b.n;
         } else {
             if (h->z_done) return false;
             // inflate more
@@ -865,7 +903,9 @@ void sam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
         {
             std::unique_lock<std::mutex> lk(A.m);
+            const auto w0 = std::chrono::steady_clock::now();
             A.cv.wait(lk, [&] { return A.stop || A.inflight < A.kInflight; });
+            A.split_block_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             if (A.stop) return;
             ++A.inflight;
             if (!A.spare.empty()) { b = std::move(A.spare.back()); A.spare.pop_back(); }
@@ -936,7 +976,9 @@ void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
         {
             std::unique_lock<std::mutex> lk(A.m);
+            const auto w0 = std::chrono::steady_clock::now();
             A.cv.wait(lk, [&] { return A.stop || A.inflight < A.kInflight; });
+            A.split_block_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             if (A.stop) return;
             ++A.inflight;
             if (!A.spare.empty()) { b = std::move(A.spare.back()); A.spare.pop_back(); }
@@ -993,6 +1035,109 @@ void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
     }
 }
 
+// BGZF input parsed ahead: the inflated batches are cut into blocks of whole records in place --
+// a block is a view into its batch's buffer, shared with the parse threads, and the record cut by a
+// batch's end moves into the next batch's headroom (kHead) -- so the stream is never copied in bulk
+// on this thread (bam_split_loop copies it twice: into the reader's buffer, then into the block).
+// The errors are bam_split_loop's, at the same records.
+void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
+    auto &A = *ap;
+    std::shared_ptr<CharBuf> cur = std::make_shared<CharBuf>(h->buf.begin() + (ptrdiff_t)h->beg,
+                                                             h->buf.begin() + (ptrdiff_t)h->end);   // inflated with the header
+    size_t beg = 0, end = cur->size();
+    h->beg = h->end;
+    // the next batch behind the bytes not yet cut; false at the end of the input or an input error
+    auto more = [&]() -> bool {
+        if (h->z_done) return false;
+        const auto w0 = std::chrono::steady_clock::now();
+        BgzfBatch b = h->bgzf_next.get();
+        h->inflate_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
+        if (!b.err.empty()) { h->z_err = b.err; h->z_done = true; return false; }
+        if (b.eof) h->z_done = true;
+        else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), h->bgzf_blocks, h->bgzf_nt);
+        const size_t L = end - beg;
+        std::shared_ptr<CharBuf> nb;
+        if (L <= kHead) {
+            if (L) memcpy(b.out.data() + kHead - L, cur->data() + beg, L);
+            nb = std::make_shared<CharBuf>(std::move(b.out));
+            beg = kHead - L;
+        } else {                                // a record longer than the headroom: joined by copy
+            nb = std::make_shared<CharBuf>();
+            nb->reserve(L + b.n);
+            nb->insert(nb->end(), cur->data() + beg, cur->data() + end);
+            nb->insert(nb->end(), b.data(), b.data() + b.n);
+            beg = 0;
+        }
+        end = beg + L + b.n;
+        cur = std::move(nb);
+        return true;
+    };
+    for (uint64_t seq = 0;; ++seq) {
+        std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
+        {
+            std::unique_lock<std::mutex> lk(A.m);
+            const auto w0 = std::chrono::steady_clock::now();
+            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.kInflight; });
+            A.split_block_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
+            if (A.stop) return;
+            ++A.inflight;
+            if (!A.spare.empty()) { b = std::move(A.spare.back()); A.spare.pop_back(); }
+        }
+        if (!b) b.reset(new fc2_ingest::SamAhead::Batch());
+        b->seq = seq;
+        b->n = 0;
+        b->rc = FC2_OK;
+        b->err.clear();
+        b->read_rc = FC2_OK;
+        b->read_err.clear();
+        b->eof = false;
+        b->block.clear();
+        b->vbuf.reset();
+        b->voff = b->vlen = 0;
+        auto truncated = [&]() {
+            b->read_rc = FC2_E_FORMAT;
+            b->read_err = "truncated BAM record" + (h->z_err.empty() ? "" : " (" + h->z_err + ")");
+            b->eof = true;
+        };
+        for (;;) {
+            // every whole record from beg on, up to a block's worth
+            const char *base = cur->data();
+            size_t q = beg;
+            while (q + 4 <= end) {
+                int32_t bs;
+                memcpy(&bs, base + q, 4);
+                if (bs < 32 || q + 4 + (size_t)bs > end) break;
+                q += 4 + (size_t)bs;
+                if (q - beg >= A.block) break;
+            }
+            if (q > beg) {
+                b->vbuf = cur;
+                b->voff = beg;
+                b->vlen = q - beg;
+                beg = q;
+                break;
+            }
+            if (end - beg < 4) {                // no whole record: the input ends here, or more comes
+                if (more()) continue;
+                if (!h->z_err.empty()) { b->read_rc = FC2_E_FORMAT; b->read_err = "BAM input: " + h->z_err; }
+                else if (end > beg) truncated();
+                b->eof = true;
+                break;
+            }
+            int32_t bs;                         // the record at beg is not whole yet
+            memcpy(&bs, base + beg, 4);
+            if (bs < 32 || !more()) { truncated(); break; }
+        }
+        const bool last = b->eof;
+        {
+            std::lock_guard<std::mutex> lk(A.m);
+            A.todo.push_back(std::move(b));
+        }
+        A.cv.notify_all();
+        if (last) return;
+    }
+}
+
 void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b);
 
 // parser: blocks to record batches (own RNAME cache and CIGAR scratch)
@@ -1003,13 +1148,16 @@ void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
         {
             std::unique_lock<std::mutex> lk(A.m);
+            const auto w0 = std::chrono::steady_clock::now();
             A.cv.wait(lk, [&] { return A.stop || !A.todo.empty(); });
+            A.parse_idle_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             if (A.stop) return;
             b = std::move(A.todo.front());
             A.todo.pop_front();
         }
-        const char *p = b->block.data(), *end = p + b->block.size();
-        while (h->bam && p < end && b->rc == FC2_OK) {     // whole BAM records (bam_split_loop)
+        const char *p = b->vbuf ? b->vbuf->data() + b->voff : b->block.data();
+        const char *end = p + (b->vbuf ? b->vlen : b->block.size());
+        while (h->bam && p < end && b->rc == FC2_OK) {     // whole BAM records (bam/bgzf_split_loop)
             int32_t bs;
             memcpy(&bs, p, 4);
             if (b->n == b->recs.size()) b->recs.emplace_back();
@@ -1032,6 +1180,7 @@ void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
             ++b->n;
         }
         if (b->rc == FC2_OK && b->read_rc) { b->rc = b->read_rc; b->err = b->read_err; }
+        b->vbuf.reset();                        // the inflated batch goes once all its blocks are parsed
         b->gs = b->gt = 0;
         if (A.group) group_batch(A.gp, *b);
         {
@@ -1415,7 +1564,10 @@ extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
             h->src = fc2_ingest::SRC_BGZF;
             h->bgzf = true;
             h->bgzf_nt = bgzf_threads();
-            h->bgzf_next = std::async(std::launch::async, bgzf_batch, fd, std::move(pre), 16, h->bgzf_nt);
+            if (const char *e = getenv("FC2_BGZF_BATCH"))
+                if (atoi(e) > 0) h->bgzf_blocks = std::min(atoi(e), 4096);
+            h->bgzf_next = std::async(std::launch::async, bgzf_batch, fd, std::move(pre), std::min(16, h->bgzf_blocks),
+                                      h->bgzf_nt);
         } else {
             // any other gzip stream (gzip -c, concatenated members)
             h->src = fc2_ingest::SRC_GZIP;
@@ -1633,7 +1785,10 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
         h->ahead.reset(ap);
         if (const char *be = getenv("FC2_PARSE_BLOCK"))
             if (atol(be) > 0) ap->block = (size_t)atol(be);
-        ap->splitter = h->bam ? std::thread(bam_split_loop, h, ap) : std::thread(sam_split_loop, h, ap);
+        const char *zc = getenv("FC2_BGZF_INPLACE");     // 0: the copying splitter (A/B)
+        ap->splitter = !h->bam                                   ? std::thread(sam_split_loop, h, ap)
+                       : h->src == fc2_ingest::SRC_BGZF && !(zc && atoi(zc) == 0) ? std::thread(bgzf_split_loop, h, ap)
+                                                                                  : std::thread(bam_split_loop, h, ap);
         const char *env = getenv("FC2_PARSE_THREADS");
         const int np = env && atoi(env) > 0 ? std::min(atoi(env), 32) : fc2_ingest::SamAhead::kParsers;
         // fragments grouped on the parse threads (FC2_GROUP_AHEAD=0: on the consumer, as before)
@@ -1664,6 +1819,15 @@ void fc2::ing::release(fc2_ingest *h) {
     }
     A.pinned.clear();
     A.cv.notify_all();
+}
+
+void fc2::ing::take_stage_ms(fc2_ingest *h, double *inflate_wait, double *split_block, double *parse_idle) {
+    *inflate_wait = *split_block = *parse_idle = 0;
+    if (!h) return;
+    *inflate_wait = (double)h->inflate_wait_ns.exchange(0) * 1e-6;
+    if (!h->ahead) return;
+    *split_block = (double)h->ahead->split_block_ns.exchange(0) * 1e-6;
+    *parse_idle = (double)h->ahead->parse_idle_ns.exchange(0) * 1e-6;
 }
 
 double fc2::ing::take_wait_ms(fc2_ingest *h, uint64_t *grouped) {

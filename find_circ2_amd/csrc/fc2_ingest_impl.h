@@ -122,5 +122,9 @@ void release(fc2_ingest *h);
 // fragments grouped on the parse threads meanwhile (FC2_CALLER_TIMING)
 double take_wait_ms(fc2_ingest *h, uint64_t *grouped = nullptr);
 
+// the stages upstream of the consumer since the last call (FC2_CALLER_TIMING): the reader's wait for
+// inflated BGZF batches, the splitter's wait for a free block slot, the parse threads' idle time
+void take_stage_ms(fc2_ingest *h, double *inflate_wait, double *split_block, double *parse_idle);
+
 }  // namespace ing
 }  // namespace fc2

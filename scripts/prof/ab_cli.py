@@ -4,6 +4,8 @@ libfc2.so on one generated hg19-sized input, alternating, one process per run (t
 at import through FC2_LIB_VARIANT), in bench.py's two forms: BGZF BAM piped on stdin and SAM by path.
 NAME may also be env:K=V[,K=V...] (the tree's library under those environment settings), and several
 variants joined by '+'.  Every run's output files must equal the first run's.  One JSON line per run.
+AB_TIMING=1: each run under FC2_CALLER_TIMING, its per-chunk phase times kept in
+gpurun_out/abcli_timing/<variant>_<form>_<round>.txt.
 usage: ab_cli.py NAME[+NAME...] [rounds] [reads]"""
 import gzip
 import json
@@ -59,14 +61,22 @@ def main():
                     env["FC2_LIB_VARIANT"] = v
                 out = os.path.join(d, "out_%s_%s" % (re.sub(r"[^A-Za-z0-9_]", "_", v), form))
                 cmd = [sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", out, "-q"]
+                err = None
+                if os.environ.get("AB_TIMING") == "1":
+                    env["FC2_CALLER_TIMING"] = "1"
+                    td = os.path.join(ROOT, "gpurun_out", "abcli_timing")
+                    os.makedirs(td, exist_ok=True)
+                    err = open(os.path.join(td, "%s_%s_%d.txt" % (re.sub(r"[^A-Za-z0-9_]", "_", v), form, r)), "w")
                 t0 = time.time()
                 if form == "bam_stdin":
                     feeder = subprocess.Popen(["cat", bam], stdout=subprocess.PIPE)
-                    subprocess.run(cmd, env=env, check=True, cwd=ROOT, stdin=feeder.stdout, timeout=600)
+                    subprocess.run(cmd, env=env, check=True, cwd=ROOT, stdin=feeder.stdout, stderr=err, timeout=600)
                     feeder.stdout.close()
                     feeder.wait()
                 else:
-                    subprocess.run(cmd + [sam], env=env, check=True, cwd=ROOT, timeout=600)
+                    subprocess.run(cmd + [sam], env=env, check=True, cwd=ROOT, stderr=err, timeout=600)
+                if err is not None:
+                    err.close()
                 wall = time.time() - t0
                 log = open(os.path.join(out, "run.log")).read()
                 rate = float(re.search(r"overall ([0-9.]+)k reads/second", log).group(1)) * 1e3

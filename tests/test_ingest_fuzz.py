@@ -191,3 +191,65 @@ def test_parse_ahead_equals_sequential_reader_on_damage(forms, tmp_path, monkeyp
                     gz.open(os.path.join(outs[1], "spliced_reads.fastq.gz"), "rt") as b:
                 assert a.read() == b.read(), k
     assert n_err > 0
+
+
+@pytest.fixture(scope="module")
+def long_bam(tmp_path_factory):
+    """The rich SAM with 80-kb unspliced reads spliced in (records longer than the inflated
+    batches' 64-KiB headroom), as raw BAM bytes."""
+    from test_native_caller import _rich_sam
+    d = tmp_path_factory.mktemp("bgzf_split")
+    sam = str(d / "rich.sam")
+    fa = _rich_sam(sam, 600, seed=5150)
+    lines = open(sam).read().splitlines()
+    rng = random.Random(99)
+    out, k = [], 0
+    for l in lines:
+        out.append(l)
+        if not l.startswith("@") and rng.random() < 0.01:
+            L = 80_000
+            seq = "".join(rng.choice("ACGT") for _ in range(L))
+            out.append("long%d\t0\tchr1\t%d\t60\t%dM\t*\t0\t0\t%s\t%s\tAS:i:%d" % (k, 1001, L, seq, "I" * L, L))
+            k += 1
+    text = "\n".join(out) + "\n"
+    p = str(d / "raw.bam")
+    sam_to_bam(text, p, compress="none")
+    return d, fa, open(p, "rb").read()
+
+
+@pytest.mark.parametrize("bgzf_block,batch,parse_block", [(3000, 2, None), (9000, 5, "20000"), (65280, 1, None)])
+def test_bgzf_inplace_splitter_equals_copying_and_sequential(long_bam, tmp_path, monkeypatch, bgzf_block, batch,
+                                                             parse_block):
+    """The BGZF splitter that cuts parse blocks in place in the inflated batches (bgzf_split_loop:
+    a record cut by a batch's end moved into the next batch's headroom, or joined by copy when it
+    is longer than the headroom) against the copying splitter (FC2_BGZF_INPLACE=0) and the
+    sequential reader (-B): tiny BGZF blocks and batches of 1-5 blocks put batch boundaries inside
+    records of every size; the files are identical, on the whole input and on truncations."""
+    import os
+    d, fa, raw = long_bam
+    monkeypatch.setenv("FC2_BGZF_BATCH", str(batch))
+    if parse_block:
+        monkeypatch.setenv("FC2_PARSE_BLOCK", parse_block)
+    data = bgzf_compress(raw, block=bgzf_block, level=1)
+    rng = random.Random(bgzf_block)
+    cuts = [len(data)] + [rng.randrange(len(data) // 3, len(data)) for _ in range(3)]
+    for k, n in enumerate(cuts):
+        p = str(tmp_path / ("in%d.bam" % k))
+        with open(p, "wb") as fh:
+            fh.write(data[:n])
+        res = []
+        for tag, env, extra in (("inplace", "1", []), ("copying", "0", []), ("seq", "1", ["-B"])):
+            monkeypatch.setenv("FC2_BGZF_INPLACE", env)
+            o = str(tmp_path / ("o%d_%s" % (k, tag)))
+            try:
+                rc = cli.main(["-G", fa, "-o", o, "-q"] + extra + [p], evaluator_factory=oracle_evaluator_factory)
+            except (IOError, OSError, ValueError, RuntimeError, EOFError, KeyError, IndexError):
+                rc = 1
+            files = {}
+            for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
+                fp = os.path.join(o, f)
+                files[f] = open(fp).read() if os.path.exists(fp) else None
+            res.append((rc, files))
+        assert res[0] == res[1] == res[2], (k, n, [r[0] for r in res])
+        if k == 0:
+            assert res[0][0] == 0 and res[0][1]["circ_splice_sites.bed"].count("\n") > 20
