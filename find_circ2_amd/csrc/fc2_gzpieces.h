@@ -7,6 +7,8 @@
 #include <stdio.h>
 #include <zlib.h>
 
+#include "fc2_deflate.h"
+
 #include <algorithm>
 #include <condition_variable>
 #include <deque>
@@ -137,17 +139,7 @@ class GzPieces {
     }
 
     void compress(Job &j) {
-        z_stream zs{};
-        if (deflateInit2(&zs, level_, Z_DEFLATED, 15 + 16, 8, Z_DEFAULT_STRATEGY) != Z_OK) { j.zerr = true; return; }
-        j.out.resize(deflateBound(&zs, (uLong)j.in.size()) + 64);
-        zs.next_in = (Bytef *)j.in.data();
-        zs.avail_in = (uInt)j.in.size();
-        zs.next_out = (Bytef *)&j.out[0];
-        zs.avail_out = (uInt)j.out.size();
-        const int rc = deflate(&zs, Z_FINISH);
-        j.out.resize(zs.total_out);
-        deflateEnd(&zs);
-        if (rc != Z_STREAM_END) j.zerr = true;
+        if (!dfl::gzip_member(j.in, level_, j.out)) j.zerr = true;   // libdeflate, or zlib (fc2_deflate.h)
         std::string().swap(j.in);
     }
 };

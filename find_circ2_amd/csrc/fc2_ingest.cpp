@@ -34,6 +34,7 @@
 #include "../../include/fc2_ingest.h"
 #include "fc2_bamout.h"
 #include "fc2_common.h"
+#include "fc2_deflate.h"
 #include "fc2_ingest_impl.h"
 
 using fc2::ing::Mate;
@@ -212,25 +213,17 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
     std::atomic<size_t> next{0};
     std::atomic<bool> bad{false};
     auto work = [&]() {
-        z_stream zs{};
-        if (inflateInit2(&zs, -15) != Z_OK) { bad = true; return; }
+        fc2::dfl::Inflater inf;                 // libdeflate (zlib without it): fc2_deflate.h
+        if (!inf.ok()) { bad = true; return; }
         for (size_t i; (i = next.fetch_add(1)) < nb && !bad;) {
             const uint8_t *blk = raw.data() + boff[i];
             const size_t xl = blk[10] | (blk[11] << 8);
-            inflateReset(&zs);
-            zs.next_in = (Bytef *)(blk + 12 + xl);
-            zs.avail_in = (uInt)(bsz[i] - 12 - xl - 8);
-            uint8_t none = 0;                   // an empty block (the EOF marker): zlib wants a real pointer
-            zs.next_out = ooff[i + 1] > ooff[i] ? (Bytef *)(B.out.data() + kHead + ooff[i]) : (Bytef *)&none;
-            zs.avail_out = (uInt)(ooff[i + 1] - ooff[i]);
-            const int rc = inflate(&zs, Z_FINISH);
+            char *dst = B.out.data() + kHead + ooff[i];
+            const size_t n = ooff[i + 1] - ooff[i];
             const uint8_t *t = blk + bsz[i] - 8;
             const uint32_t crc = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
-            if (rc != Z_STREAM_END || zs.avail_out != 0 ||
-                crc32(0L, (const Bytef *)zs.next_out - (ooff[i + 1] - ooff[i]), (uInt)(ooff[i + 1] - ooff[i])) != crc)
-                bad = true;
+            if (!inf.exact(blk + 12 + xl, bsz[i] - 12 - xl - 8, dst, n) || fc2::dfl::crc32(dst, n) != crc) bad = true;
         }
-        inflateEnd(&zs);
     };
     const int nt = (int)std::min<size_t>((size_t)n_threads, std::max<size_t>(1, nb));
     std::vector<std::thread> pool;
@@ -347,7 +340,8 @@ struct fc2_ingest::SamAhead {
     static constexpr size_t kBlock = size_t(4) << 20;
     size_t block = kBlock;                      // FC2_PARSE_BLOCK (bytes): small blocks in the tests
     static constexpr int kParsers = 3;          // default parser threads (FC2_PARSE_THREADS)
-    static constexpr size_t kInflight = 8;      // blocks read but not yet consumed
+    static constexpr size_t kInflight = 8;      // blocks read but not yet consumed (FC2_PARSE_INFLIGHT)
+    size_t max_inflight = kInflight;
     std::mutex m;
     std::condition_variable cv;
     std::deque<std::unique_ptr<Batch>> todo;    // read, not yet parsed (block order)
@@ -904,7 +898,7 @@ void sam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         {
             std::unique_lock<std::mutex> lk(A.m);
             const auto w0 = std::chrono::steady_clock::now();
-            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.kInflight; });
+            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.max_inflight; });
             A.split_block_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             if (A.stop) return;
             ++A.inflight;
@@ -977,7 +971,7 @@ void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         {
             std::unique_lock<std::mutex> lk(A.m);
             const auto w0 = std::chrono::steady_clock::now();
-            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.kInflight; });
+            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.max_inflight; });
             A.split_block_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             if (A.stop) return;
             ++A.inflight;
@@ -1077,7 +1071,7 @@ void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         {
             std::unique_lock<std::mutex> lk(A.m);
             const auto w0 = std::chrono::steady_clock::now();
-            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.kInflight; });
+            A.cv.wait(lk, [&] { return A.stop || A.inflight < A.max_inflight; });
             A.split_block_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             if (A.stop) return;
             ++A.inflight;
@@ -1785,6 +1779,8 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
         h->ahead.reset(ap);
         if (const char *be = getenv("FC2_PARSE_BLOCK"))
             if (atol(be) > 0) ap->block = (size_t)atol(be);
+        if (const char *fe = getenv("FC2_PARSE_INFLIGHT"))
+            if (atoi(fe) > 0) ap->max_inflight = (size_t)std::min(atoi(fe), 256);
         const char *zc = getenv("FC2_BGZF_INPLACE");     // 0: the copying splitter (A/B)
         ap->splitter = !h->bam                                   ? std::thread(sam_split_loop, h, ap)
                        : h->src == fc2_ingest::SRC_BGZF && !(zc && atoi(zc) == 0) ? std::thread(bgzf_split_loop, h, ap)

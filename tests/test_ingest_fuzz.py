@@ -253,3 +253,57 @@ def test_bgzf_inplace_splitter_equals_copying_and_sequential(long_bam, tmp_path,
         assert res[0] == res[1] == res[2], (k, n, [r[0] for r in res])
         if k == 0:
             assert res[0][0] == 0 and res[0][1]["circ_splice_sites.bed"].count("\n") > 20
+
+
+_CLI_SCRIPT = """
+import sys
+sys.path[:0] = [%r]
+from oracle_engine import oracle_evaluator_factory
+from find_circ2_amd import cli
+try:
+    rc = cli.main(sys.argv[1:], evaluator_factory=oracle_evaluator_factory)
+except Exception as e:
+    print("RAISED", type(e).__name__, e, file=sys.stderr)
+    rc = 1
+sys.exit(rc)
+"""
+
+
+def test_libdeflate_and_zlib_give_the_same_run(long_bam, tmp_path):
+    """BGZF blocks inflated and CRC-checked by libdeflate (default) or by zlib (FC2_LIBDEFLATE=0,
+    the fallback without the library), spliced_reads.fastq.gz compressed by either: the same exit
+    status and the same text on the whole input and on damaged copies (a flipped byte inside a
+    block is caught by the CRC or the inflater in both)."""
+    import os
+    import subprocess
+    import sys
+    d, fa, raw = long_bam
+    data = bgzf_compress(raw, block=20000, level=1)
+    rng = random.Random(7)
+    inputs = [data]
+    for _ in range(3):
+        b = bytearray(data)
+        i = rng.randrange(100, len(b))
+        b[i] ^= 1 << rng.randrange(8)
+        inputs.append(bytes(b))
+    script = _CLI_SCRIPT % os.path.dirname(os.path.abspath(__file__))
+    for k, blob in enumerate(inputs):
+        p = str(tmp_path / ("in%d.bam" % k))
+        with open(p, "wb") as fh:
+            fh.write(blob)
+        res = []
+        for lib in ("1", "0"):
+            o = str(tmp_path / ("o%d_%s" % (k, lib)))
+            env = dict(os.environ, FC2_LIBDEFLATE=lib, FC2_BGZF_BATCH="3")
+            r = subprocess.run([sys.executable, "-c", script, "-G", fa, "-o", o, "-q", p], env=env,
+                               capture_output=True, text=True, timeout=300)
+            files = {}
+            for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
+                fp = os.path.join(o, f)
+                files[f] = open(fp).read() if os.path.exists(fp) else None
+            fq = os.path.join(o, "spliced_reads.fastq.gz")
+            files["reads"] = gzip.open(fq, "rt").read() if os.path.exists(fq) and r.returncode == 0 else None
+            res.append((r.returncode, files))
+        assert res[0] == res[1], (k, res[0][0], res[1][0])
+        if k == 0:
+            assert res[0][0] == 0 and res[0][1]["reads"].count("\n") > 100
