@@ -340,7 +340,7 @@ struct fc2_ingest::SamAhead {
     static constexpr size_t kBlock = size_t(4) << 20;
     size_t block = kBlock;                      // FC2_PARSE_BLOCK (bytes): small blocks in the tests
     static constexpr int kParsers = 3;          // default parser threads (FC2_PARSE_THREADS)
-    static constexpr size_t kInflight = 8;      // blocks read but not yet consumed (FC2_PARSE_INFLIGHT)
+    static constexpr size_t kInflight = 24;     // blocks read but not yet consumed (FC2_PARSE_INFLIGHT)
     size_t max_inflight = kInflight;
     std::mutex m;
     std::condition_variable cv;

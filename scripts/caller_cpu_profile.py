@@ -6,7 +6,10 @@ scaled hg19-shaped genome, with the CPU oracle behind the batch hook (tests/orac
 time is excluded), and prints the seconds spent in next (ingest, process_mate, pairs) and submit
 (record_hits, junction tables, writers) -- the two halves the CLI overlaps on two threads.
 
-    python scripts/caller_cpu_profile.py [reads] [genome-scale] [--all-hits --non-canonical ...]
+    python scripts/caller_cpu_profile.py [reads] [genome-scale] [--bam] [--all-hits --non-canonical ...]
+
+--bam reads the input as a BGZF BAM.  Under scripts/prof/sampler.c the samples are tagged 1 in
+fc2_caller_next, 2 in fc2_caller_submit, 3 during the search (the parse-ahead threads run on).
 """
 import json
 import os
@@ -23,7 +26,8 @@ from cli_scale_check import make_genome, write_fasta, write_sam  # noqa: E402
 
 def main():
     pos = [a for a in sys.argv[1:] if not a.startswith("-")]
-    extra = [a for a in sys.argv[1:] if a.startswith("-")]
+    bam = "--bam" in sys.argv[1:]
+    extra = [a for a in sys.argv[1:] if a.startswith("-") and a != "--bam"]
     reads = int(pos[0]) if pos else 200_000
     scale = float(pos[1]) if len(pos) > 1 else 0.01
     from find_circ2_amd import cli, sq_table
@@ -39,12 +43,17 @@ def main():
         seqs = make_genome(fa, names, sizes, rng)
         write_sam(sam, seqs, reads, rng)
         write_fasta(fa, seqs)
+    if bam:
+        from find_circ2_amd.ingest import sam_to_bam
+        if not os.path.exists(sam + ".bam"):
+            sam_to_bam(sam, sam + ".bam")
+        sam = sam + ".bam"
     options, _ = cli.build_parser().parse_args(["-G", fa, "-o", os.path.join(d, "out"), "-n", "prof"] + extra + [sam])
     from find_circ2_amd.hotpath import Options as HPOptions
     hp = HPOptions(asize=options.asize, margin=options.margin, maxdist=options.maxdist,
                    noncanonical=options.noncanonical, strandpref=options.strandpref, allhits=options.allhits)
     evaluate, names, fasta, dummy = oracle_batch_engine(options, hp)
-    nc = NativeCaller(sam, False, options, names, fasta, write_reads=True, write_multi=True, genome_dummy=dummy)
+    nc = NativeCaller(sam, bam, options, names, fasta, write_reads=True, write_multi=True, genome_dummy=dummy)
     nc.open()
 
     class Sink:
@@ -90,7 +99,9 @@ def _sampled_loop(nc, evaluate, sampler):
         N.check(rc)
         n = int(b.n)
         t = time.perf_counter()
+        sampler.sampler_phase(3)
         res, tm = evaluate(*nc._host_batch(b, n)) if n else (None, None)
+        sampler.sampler_phase(0)
         prof["eval_s"] += time.perf_counter() - t
         res_ptr = tm_ptr = None
         tw = 0

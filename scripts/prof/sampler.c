@@ -14,6 +14,7 @@
 #include <ucontext.h>
 #include <stdlib.h>
 #include <sys/syscall.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #define MAXS (1 << 20)
@@ -50,6 +51,15 @@ int sampler_start(int usec) {
     struct sigevent ev;
     memset(&ev, 0, sizeof ev);
     ev.sigev_signo = SIGPROF;
+    if (getenv("FC2_SAMPLE_PROCESS")) {          /* every thread, on the process's CPU clock (ITIMER_PROF:
+                                                    the signal goes to the thread that used the CPU) */
+        struct itimerval iv;
+        iv.it_interval.tv_sec = 0;
+        iv.it_interval.tv_usec = usec;
+        iv.it_value = iv.it_interval;
+        tid = 0;
+        return setitimer(ITIMER_PROF, &iv, 0);
+    }
     if (getenv("FC2_SAMPLE_THREAD")) {           /* only the calling thread, on its own CPU clock */
         ev.sigev_notify = SIGEV_THREAD_ID;
         ev._sigev_un._tid = (pid_t)syscall(SYS_gettid);
@@ -69,7 +79,13 @@ void sampler_phase(int tag) { cur_tag = tag; }
 
 int sampler_stop(const char *path) {
     cur_tag = 0;
-    timer_delete(tid);
+    if (getenv("FC2_SAMPLE_PROCESS")) {
+        struct itimerval iv;
+        memset(&iv, 0, sizeof iv);
+        setitimer(ITIMER_PROF, &iv, 0);
+    } else {
+        timer_delete(tid);
+    }
     FILE *f = fopen(path, "w");
     if (!f) return -1;
     const int n = n_samples < MAXS ? n_samples : MAXS;
