@@ -187,6 +187,7 @@ class ByteBuf {
 // the primary's strings are swapped in, not copied: the record gets the recycled Align's buffers
 // back (the ingest reads nothing of a handed-over fragment's records, FragSink)
 void take_align(Align &a, Rec &r) {
+    r.decode();                                 // SEQ / QUAL left in the parse block (fc2::ing::Rec)
     static_cast<APos &>(a) = apos_of(r);
     a.qname.swap(r.qname);
     a.seq.swap(r.seq);

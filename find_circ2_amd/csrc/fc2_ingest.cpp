@@ -97,6 +97,38 @@ void finish_rec(Rec &r, const std::vector<std::pair<int, int>> &ops, int64_t seq
     }
 }
 
+}  // namespace
+
+void fc2::ing::Rec::decode_lazy() {
+    const int32_t n = lz.n_seq;
+    if (lz.bam) {
+        // two bases per byte through a 256-entry table of base pairs
+        static const struct Pairs {
+            char t[256][2];
+            Pairs() {
+                static const char *SEQ = "=ACMGRSVTWYHKDBN";
+                for (int v = 0; v < 256; ++v) { t[v][0] = SEQ[v >> 4]; t[v][1] = SEQ[v & 0xF]; }
+            }
+        } kPairs;
+        const uint8_t *p = (const uint8_t *)lz.seq, *q = (const uint8_t *)lz.qual;
+        if (n == 0) {
+            seq.assign(1, '*');
+        } else {
+            seq.resize((size_t)n);
+            for (int k = 0; k + 1 < n; k += 2) memcpy(&seq[k], kPairs.t[p[k >> 1]], 2);
+            if (n & 1) seq[n - 1] = kPairs.t[p[(n - 1) >> 1]][0];
+        }
+        if (n == 0 || q[0] == 0xFF) qual.assign(1, '*');
+        else { qual.resize((size_t)n); for (int k = 0; k < n; ++k) qual[k] = (char)(q[k] + 33); }
+    } else {
+        seq.assign(lz.seq, (size_t)n);
+        qual.assign(lz.qual, (size_t)lz.n_qual);
+    }
+    lz.n_seq = -1;
+}
+
+namespace {
+
 // ---- parallel BGZF ----------------------------------------------------------------------
 // BAM is a series of BGZF blocks (gzip members of <= 64 KiB with the compressed size in a
 // "BC" extra field), so the blocks can be inflated independently.  A batch of blocks is
@@ -565,7 +597,8 @@ int find_tabs(const char *b, const char *e, const char **t, int maxn) {
     return n;
 }
 
-int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r, fc2_ingest::ParseScratch &ps) {
+int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r, fc2_ingest::ParseScratch &ps,
+                     bool lazy = false) {
     // every tab of the line in one pass: fields 1-11, then the tags
     constexpr int kMaxTabs = 64;
     const char *tabs[kMaxTabs];
@@ -605,16 +638,27 @@ int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r, fc2_
             }
         }
     }
-    r.seq.assign(fb(9), fe(9));
-    r.has_seq = !(r.seq.size() == 1 && r.seq[0] == '*');
-    r.qual.assign(fb(10), fe(10));
-    r.has_qual = !(r.qual.size() == 1 && r.qual[0] == '*');
+    const char *sb = fb(9), *se = fe(9), *qb = fb(10), *qe = fe(10);
+    r.has_seq = !(se - sb == 1 && *sb == '*');
+    r.has_qual = !(qe - qb == 1 && *qb == '*');
+    r.seq_n = (uint32_t)(se - sb);
+    if (lazy) {                                     // decoded if the record is ever needed (Rec::decode)
+        r.lz.seq = sb;
+        r.lz.qual = qb;
+        r.lz.n_seq = (int32_t)(se - sb);
+        r.lz.n_qual = (int32_t)(qe - qb);
+        r.lz.bam = false;
+    } else {
+        r.lz.n_seq = -1;
+        r.seq.assign(sb, se);
+        r.qual.assign(qb, qe);
+    }
     r.has_as = r.has_xs = false;
     r.as_int = r.xs_int = true;
     r.as = r.xs = 0;
     r.as_last_int = r.xs_last_int = true;
     r.as_last = r.xs_last = 0;
-    finish_rec(r, ops, r.has_seq ? (int64_t)r.seq.size() : 0);
+    finish_rec(r, ops, r.has_seq ? (int64_t)r.seq_n : 0);
     if (nf == 12) {                                 // tags: [tabs[k] + 1, next tab or line end), k >= 10
         const int last = nt == kMaxTabs ? nt - 1 : nt;
         for (int k = 10; k < last; ++k) note_tag(r, tabs[k] + 1, k + 1 < nt ? tabs[k + 1] : le);
@@ -737,7 +781,7 @@ bool scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
 // fields do not fit its block, with an unterminated query name or corrupt aux data is an error, as
 // in htslib's bam_read1 / aux parsing.
 int parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
-                   std::vector<std::pair<int, int>> &ops, bool need_text, bool keep_raw) {
+                   std::vector<std::pair<int, int>> &ops, bool need_text, bool keep_raw, bool lazy = false) {
     if (bs < 32) return fc2::fail(FC2_E_FORMAT, "invalid BAM record (block shorter than its fixed fields)");
     const uint8_t *e = b + bs;
     int32_t ref_id, pos, l_seq, nref, npos, tlen;
@@ -761,28 +805,18 @@ int parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
     }
     const uint8_t *cigp = p;
     p += 4 * n_cig;
-    // two bases per byte through a 256-entry table of base pairs
-    static const struct Pairs {
-        char t[256][2];
-        Pairs() {
-            static const char *SEQ = "=ACMGRSVTWYHKDBN";
-            for (int v = 0; v < 256; ++v) { t[v][0] = SEQ[v >> 4]; t[v][1] = SEQ[v & 0xF]; }
-        }
-    } kPairs;
-    std::string &seq = r.seq;
-    seq.resize((size_t)l_seq);
-    for (int k = 0; k + 1 < l_seq; k += 2) memcpy(&seq[k], kPairs.t[p[k >> 1]], 2);
-    if (l_seq & 1) seq[l_seq - 1] = kPairs.t[p[(l_seq - 1) >> 1]][0];
-    p += (l_seq + 1) / 2;
-    std::string &qual = r.qual;
-    if (l_seq == 0 || p[0] == 0xFF) qual.assign(1, '*');
-    else { qual.resize((size_t)l_seq); for (int k = 0; k < l_seq; ++k) qual[k] = (char)(p[k] + 33); }
-    p += l_seq;
+    r.lz.seq = (const char *)p;
+    r.lz.qual = (const char *)p + (l_seq + 1) / 2;
+    r.lz.n_seq = l_seq;
+    r.lz.bam = true;
+    r.has_seq = l_seq > 0;
+    r.has_qual = !(l_seq == 0 || p[(l_seq + 1) / 2] == 0xFF);
+    r.seq_n = r.has_seq ? (uint32_t)l_seq : 1u;
+    if (!lazy) r.decode_lazy();                 // (else when the record is needed: Rec::decode)
+    p += (l_seq + 1) / 2 + l_seq;
     r.flag = flag;
     r.tid = ref_id;
     r.pos = pos;
-    r.has_seq = l_seq > 0;
-    if (!r.has_seq) seq.assign(1, '*');
     finish_rec(r, ops, l_seq);
     r.has_as = r.has_xs = false;
     r.as_int = r.xs_int = true;
@@ -790,8 +824,8 @@ int parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
     r.as_last_int = r.xs_last_int = true;
     r.as_last = r.xs_last = 0;
     if (!scan_bam_tags(r, p, e)) return fc2::fail(FC2_E_FORMAT, "corrupted aux data in a BAM record");
-    r.has_qual = !(qual.size() == 1 && qual[0] == '*');
     if (!need_text) return FC2_OK;
+    const std::string &seq = r.seq, &qual = r.qual;
     std::string cig;
     char tmp[32];
     for (int k = 0; k < n_cig; ++k) {
@@ -1155,7 +1189,8 @@ void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
             int32_t bs;
             memcpy(&bs, p, 4);
             if (b->n == b->recs.size()) b->recs.emplace_back();
-            const int rc = parse_bam_body(h, (const uint8_t *)p + 4, bs, b->recs[b->n], ps.ops, h->need_text, false);
+            const int rc = parse_bam_body(h, (const uint8_t *)p + 4, bs, b->recs[b->n], ps.ops, h->need_text, false,
+                                          !h->need_text);
             if (rc) { b->rc = rc; b->err = fc2_last_error(); break; }
             ++b->n;
             p += 4 + (size_t)bs;
@@ -1169,12 +1204,11 @@ void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
             for (const char *c = ls; c < le; ++c) if (!isspace((unsigned char)*c)) { blank = false; break; }
             if (blank) continue;
             if (b->n == b->recs.size()) b->recs.emplace_back();
-            const int rc = parse_sam_record(h, ls, le, b->recs[b->n], ps);
+            const int rc = parse_sam_record(h, ls, le, b->recs[b->n], ps, !h->need_text);
             if (rc) { b->rc = rc; b->err = fc2_last_error(); break; }
             ++b->n;
         }
         if (b->rc == FC2_OK && b->read_rc) { b->rc = b->read_rc; b->err = b->read_err; }
-        b->vbuf.reset();                        // the inflated batch goes once all its blocks are parsed
         b->gs = b->gt = 0;
         if (A.group) group_batch(A.gp, *b);
         {
@@ -1336,7 +1370,7 @@ MateRef ref_of(Mate &m) {
     r.n = (uint32_t)m.recs.size();
     r.proper = m.proper.data();
     r.np = (uint32_t)m.proper.size();
-    r.seq_len = m.recs.empty() ? 0 : (uint32_t)m.recs[0].seq.size();
+    r.seq_len = m.recs.empty() ? 0 : m.recs[0].seq_n;
     return r;
 }
 
@@ -1463,7 +1497,7 @@ void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b) {
             g.r0[k] = g.n[k] = g.p0[k] = g.np[k] = 0;
             g.seq_len[k] = 0;
             if (!ms[k]) continue;
-            g.seq_len[k] = (uint32_t)R[ms[k]->r[0]].seq.size();
+            g.seq_len[k] = R[ms[k]->r[0]].seq_n;
             g.r0[k] = (int32_t)b.gidx.size();
             g.n[k] = (int32_t)ms[k]->r.size();
             b.gidx.insert(b.gidx.end(), ms[k]->r.begin(), ms[k]->r.end());

@@ -32,14 +32,31 @@ struct RecFields {
     int64_t as_last = 0, xs_last = 0;
 };
 
+// SEQ / QUAL a parse thread left where they are in the record's parse block (which stays until
+// its batch is reused): most records never need them, only the primaries of handed fragments do
+struct LazySeq {
+    const char *seq = nullptr, *qual = nullptr;
+    int32_t n_seq = -1;        // -1: Rec::seq / qual hold the decoded strings
+    int32_t n_qual = 0;        // SAM text: QUAL's length (BAM: n_seq bytes, 0xFF for none)
+    bool bam = false;          // 4-bit BAM bases and binary qualities; else SAM text
+};
+
 struct Rec : RecFields {
     std::string text;      // SAM line (no newline): for the Python hand-back and the -B writer
     std::string raw;       // BAM input with a -B writer: block_size + record bytes
     std::string qname;
-    std::string seq, qual;  // SEQ / QUAL
+    std::string seq, qual;  // SEQ / QUAL (see decode())
+    uint32_t seq_n = 0;    // seq.size() once decoded ("*" counts 1, as the string does)
+    LazySeq lz;
     bool unmapped() const { return flag & 0x4; }
     bool read1() const { return flag & 0x40; }
     bool reverse() const { return flag & 0x10; }
+    // seq / qual from the parse block if a parse thread left them there; a record decodes before
+    // it leaves its batch (RecList::take) or is read (the native caller's take_align)
+    void decode() {
+        if (lz.n_seq >= 0) decode_lazy();
+    }
+    void decode_lazy();
 };
 
 // member-wise: the strings swap their buffers, the plain fields swap as one block (cheaper than
@@ -51,6 +68,8 @@ inline void swap(Rec &a, Rec &b) noexcept {
     a.qname.swap(b.qname);
     a.seq.swap(b.seq);
     a.qual.swap(b.qual);
+    std::swap(a.seq_n, b.seq_n);
+    std::swap(a.lz, b.lz);
 }
 
 // A mate's records.  Slots past size() stay constructed: take() swaps a parsed record into the next
@@ -69,6 +88,7 @@ class RecList {
     void clear() { n_ = 0; }
     void take(Rec &r) {
         if (n_ == v_.size()) v_.emplace_back();
+        r.decode();                     // (its parse block may be reused while the mate is open)
         swap(v_[n_++], r);
     }
   private:

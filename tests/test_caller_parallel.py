@@ -19,7 +19,7 @@ MODES = [dict(FC2_CALLER_THREADS="1", FC2_NEXT_THREADS="1"),
          dict(FC2_CALLER_THREADS="8", FC2_NEXT_THREADS="7", FC2_CALLER_MIN_RANGE="5"), dict(FC2_CALLER_THREADS="16"),
          # fragments grouped on the parse threads across many small parse blocks (a fragment cut
          # by a block boundary, regions of one fragment, none), and grouped on the consumer alone
-         dict(FC2_PARSE_BLOCK="700", FC2_NEXT_THREADS="2", FC2_CALLER_MIN_RANGE="1"),
+         dict(FC2_PARSE_BLOCK="700", FC2_NEXT_THREADS="2", FC2_CALLER_MIN_RANGE="1", FC2_PARSE_INFLIGHT="2"),
          dict(FC2_PARSE_BLOCK="4000", FC2_PARSE_THREADS="5", FC2_CALLER_THREADS="3"),
          dict(FC2_GROUP_AHEAD="0", FC2_PARSE_BLOCK="1500")]
 

@@ -228,6 +228,7 @@ def test_bgzf_inplace_splitter_equals_copying_and_sequential(long_bam, tmp_path,
     import os
     d, fa, raw = long_bam
     monkeypatch.setenv("FC2_BGZF_BATCH", str(batch))
+    monkeypatch.setenv("FC2_PARSE_INFLIGHT", "3")       # parse batches reused soon after they are read
     if parse_block:
         monkeypatch.setenv("FC2_PARSE_BLOCK", parse_block)
     data = bgzf_compress(raw, block=bgzf_block, level=1)
@@ -249,6 +250,8 @@ def test_bgzf_inplace_splitter_equals_copying_and_sequential(long_bam, tmp_path,
             for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
                 fp = os.path.join(o, f)
                 files[f] = open(fp).read() if os.path.exists(fp) else None
+            fq = os.path.join(o, "spliced_reads.fastq.gz")
+            files["reads"] = gzip.open(fq, "rt").read() if rc == 0 else None
             res.append((rc, files))
         assert res[0] == res[1] == res[2], (k, n, [r[0] for r in res])
         if k == 0:
