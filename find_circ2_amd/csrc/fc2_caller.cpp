@@ -1306,9 +1306,15 @@ void decode(const fc2_caller *h, int si, const fc2_result &r, const uint64_t *ti
     }
     const int64_t cid = h->tid_cid[(size_t)s.tid];
     const std::string &chrom = h->id_names[(size_t)cid];    // (nothing below interns a new name)
-    if (pr.flags & FC2_PAIR_SKIP) {            // chromosome missing from the genome (get_data, :193)
-        ev.err = FC2_E_KEY;
-        ev.msg = "KeyError: " + py_repr(chrom);
+    if (pr.flags & FC2_PAIR_SKIP) {
+        const int32_t c = s.tid < (int32_t)h->tid2chrom.size() ? h->tid2chrom[(size_t)s.tid] : -1;
+        if (c < 0) {                            // chromosome missing from the genome (get_data, :193; A's window)
+            ev.err = FC2_E_KEY;
+            ev.msg = "KeyError: " + py_repr(chrom);
+        } else {                                // align_B.aend None: B's window, `B.aend - eff_a` (:902)
+            ev.err = FC2_E_FORMAT;
+            ev.msg = "TypeError: unsupported operand type(s) for -: 'NoneType' and 'int'";
+        }
         return;
     }
     if (r.info & FC2_RES_ERR_KEY) {
@@ -2098,35 +2104,68 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         h->next_err = in_code;                     // hand out the fragments before it first
         h->next_err_msg = in_msg;
     }
-    // the spans record_hits will evaluate, in fragment order (Caller._flush)
-    for (size_t f = 0; f < h->bf_nfrags; ++f) {
-        const Frag &fr = h->bf_frags[f];
-        for (int pass = 0; pass < 2; ++pass) {
-            for (int si : pass ? fr.lin : fr.circ) {
-                Span &s = h->bf_spans[si];
-                if (!(s.uniq >= h->o.min_uniq_qual)) continue;
-                fc2_pair pr{};
-                pr.a_pos = (int32_t)s.a_pos;
-                pr.b_aend = (int32_t)s.b_aend;
-                const int32_t c = (s.tid >= 0 && s.tid < (int32_t)h->tid2chrom.size()) ? h->tid2chrom[s.tid] : -1;
-                pr.chrom = c < 0 ? 0u : (uint32_t)c;
-                pr.read_len = (uint16_t)std::min<uint32_t>(s.read_len, 65535u);
-                if (s.b_aend < 0)               // align_B.aend is None: packing the pair fails (int(None))
-                    return fc2::fail(FC2_E_FORMAT, "TypeError: int() argument must be a string, a bytes-like object "
-                                                   "or a number, not 'NoneType'");
-                pr.flags = (uint8_t)((s.circ ? FC2_PAIR_BACKSPLICE : 0) |
-                                     (fr.prim[s.mate].rev ? FC2_PAIR_PRIMARY_REV : 0) | (c < 0 ? FC2_PAIR_SKIP : 0));
-                s.eval = (int64_t)h->bf_pairs.size();
-                h->bf_pairs.push_back(pr);
-                h->bf_off.push_back(s.read_off);
-            }
+    // the spans record_hits will evaluate, in fragment order (Caller._flush): counted per fragment
+    // range, then written at each range's offset, on the next side's workers
+    {
+        if (!h->next_pool) {
+            const char *env = getenv("FC2_NEXT_THREADS");
+            int nt = env && atoi(env) > 0 ? atoi(env) : (int)std::min(4u, std::max(1u, std::thread::hardware_concurrency()));
+            h->next_pool.reset(new WorkPool(std::max(1, std::min(nt, 64)) - 1));
         }
+        const size_t nf = h->bf_nfrags;
+        const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)h->next_pool->size(),
+                                                              nf / std::max<size_t>(1, h->min_range_frags)));
+        std::vector<uint64_t> cnt(T + 1, 0);
+        std::vector<uint8_t> bad_len(T, 0);
+        const int64_t min_uq = h->o.min_uniq_qual;
+        auto eligible = [&](const Span &sp) { return sp.uniq >= min_uq; };
+        h->next_pool->run((int)T, [&](int r) {
+            uint64_t n = 0;
+            for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
+                const Frag &fr = h->bf_frags[f];
+                for (int si : fr.circ) n += eligible(h->bf_spans[si]);
+                for (int si : fr.lin) n += eligible(h->bf_spans[si]);
+            }
+            cnt[(size_t)r + 1] = n;
+        });
+        for (size_t r = 0; r < T; ++r) cnt[r + 1] += cnt[r];
+        h->bf_pairs.resize(cnt[T]);
+        h->bf_off.resize(cnt[T]);
+        h->next_pool->run((int)T, [&](int r) {
+            uint64_t k = cnt[(size_t)r];
+            for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
+                const Frag &fr = h->bf_frags[f];
+                for (int pass = 0; pass < 2; ++pass) {
+                    for (int si : pass ? fr.lin : fr.circ) {
+                        Span &sp = h->bf_spans[si];
+                        if (!eligible(sp)) continue;
+                        fc2_pair pr{};
+                        pr.a_pos = (int32_t)sp.a_pos;
+                        // align_B.aend None: not scanned; find_breakpoints raises when it reaches B's
+                        // window (decode)
+                        const bool none_aend = sp.b_aend < 0;
+                        pr.b_aend = none_aend ? 0 : (int32_t)sp.b_aend;
+                        const int32_t c = (sp.tid >= 0 && sp.tid < (int32_t)h->tid2chrom.size()) ? h->tid2chrom[sp.tid] : -1;
+                        pr.chrom = c < 0 ? 0u : (uint32_t)c;
+                        pr.read_len = (uint16_t)std::min<uint32_t>(sp.read_len, 65535u);
+                        if (sp.read_len > FC2_MAX_READ_LEN) bad_len[(size_t)r] = 1;
+                        pr.flags = (uint8_t)((sp.circ ? FC2_PAIR_BACKSPLICE : 0) |
+                                             (fr.prim[sp.mate].rev ? FC2_PAIR_PRIMARY_REV : 0) |
+                                             (c < 0 || none_aend ? FC2_PAIR_SKIP : 0));
+                        sp.eval = (int64_t)k;
+                        h->bf_pairs[k] = pr;
+                        h->bf_off[k] = sp.read_off;
+                        ++k;
+                    }
+                }
+            }
+        });
+        for (size_t r = 0; r < T; ++r)
+            if (bad_len[r])
+                return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
+                                                  " bases (fc2_result.best_x is 16-bit)");
     }
     if (h->bf_spans.size() > h->bf_nspans) h->bf_spans.resize(h->bf_nspans);
-    for (const Span &s : h->bf_spans)
-        if (s.eval >= 0 && s.read_len > FC2_MAX_READ_LEN)
-            return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
-                                              " bases (fc2_result.best_x is 16-bit)");
     h->n_pairs += h->bf_pairs.size();
     if (timing) {
         uint64_t grouped = 0;

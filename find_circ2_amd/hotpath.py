@@ -814,6 +814,12 @@ class JunctionSpan:
         return splices_or_raise(JunctionSpan.engine.find_breakpoints_batch([self])[0])
 
 
+def none_aend_error():
+    """find_breakpoints of a span whose align_B.aend is None: B's window, ``B.aend - eff_a``
+    (find_circ.py:902), after A's window has been fetched (a missing chromosome raises first)."""
+    return TypeError("unsupported operand type(s) for -: 'NoneType' and 'int'")
+
+
 def splices_or_raise(r):
     """A ``find_breakpoints_batch`` entry as the reference method returns it: raises the
     per-span exception, else returns the tie list."""
@@ -849,9 +855,10 @@ class BreakpointEngine:
         missing = 0xFFFFFFFF
         chrom = [self.genome.chrom_index_or_missing(s.chrom) for s in spans]
         flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.strand == '-' else 0) |
-                 (N.PAIR_SKIP if c == missing else 0) for s, c in zip(spans, chrom)]
+                 (N.PAIR_SKIP if c == missing or s.align_B.aend is None else 0) for s, c in zip(spans, chrom)]
         b = PairBatch.pack(self.options, self.genome, reads, [s.align_A.pos for s in spans],
-                           [s.align_B.aend for s in spans], [0 if c == missing else c for c in chrom], flags)
+                           [s.align_B.aend or 0 for s in spans], [0 if c == missing else c for c in chrom], flags)
         out = scan(self.options, self.genome, b)
         res = decode_splices(self.options, self.genome, b, out, spans, raise_errors=False)
-        return [KeyError(s.chrom) if c == missing else r for s, r, c in zip(spans, res, chrom)]
+        return [KeyError(s.chrom) if c == missing else none_aend_error() if s.align_B.aend is None else r
+                for s, r, c in zip(spans, res, chrom)]

@@ -6,7 +6,7 @@ without a GPU and (b) on a GPU box the outputs of the GPU evaluator can be
 compared file-for-file with this one.
 """
 import oracle
-from find_circ2_amd.hotpath import WINDOW_SHAPE_MESSAGE, BreakpointError, Splice
+from find_circ2_amd.hotpath import WINDOW_SHAPE_MESSAGE, BreakpointError, Splice, none_aend_error
 
 
 def oracle_evaluator_factory(options, hp):
@@ -17,13 +17,17 @@ def oracle_evaluator_factory(options, hp):
 
     def evaluate(spans):
         idx = [0 if of.dummy else of.names.index(s.chrom) if s.chrom in of.names else -1 for s in spans]
-        r = oracle.scan_fasta(p, of, [s.read_part.encode("latin-1") for s in spans], idx,
-                              [s.align_A.pos for s in spans], [s.align_B.aend for s in spans],
+        none_b = [s.align_B.aend is None for s in spans]
+        r = oracle.scan_fasta(p, of, [s.read_part.encode("latin-1") for s in spans],
+                              [-1 if nb else i for i, nb in zip(idx, none_b)],
+                              [s.align_A.pos for s in spans], [s.align_B.aend or 0 for s in spans],
                               [s.is_backsplice for s in spans], [s.strand == '-' for s in spans],
                               use_fast=False, all_ties=True)
         for i, s in enumerate(spans):
             nt = int(r.n_ties[i])
-            if nt == -oracle.ORC_ERR_KEY:
+            if none_b[i]:                       # A's window first (a missing chromosome), then B.aend - eff_a
+                s.result = KeyError(s.chrom) if idx[i] < 0 else none_aend_error()
+            elif nt == -oracle.ORC_ERR_KEY:
                 s.result = KeyError("gtag")
             elif nt == -oracle.ORC_ERR_CHROM:
                 s.result = KeyError(s.chrom)

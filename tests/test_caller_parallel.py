@@ -66,7 +66,7 @@ def _gz(path):
 
 
 @pytest.mark.parametrize("mode", range(len(MODES)))
-@pytest.mark.parametrize("bad", ["seq", "unspliced_none", "no_as"])
+@pytest.mark.parametrize("bad", ["seq", "unspliced_none", "no_as", "b_no_cigar"])
 def test_parallel_recording_fails_where_python_loop_fails(tmp_path, monkeypatch, rich, hit_names, mode, bad):
     """A read sequence with a byte outside the IUPAC table (rev_comp's KeyError in Hit.add,
     find_circ.py:573-582), or -- with --test -- a test name that parse_truth cannot read, in a
@@ -84,6 +84,10 @@ def test_parallel_recording_fails_where_python_loop_fails(tmp_path, monkeypatch,
                 f[0] = target + "___O:chr1:x:+"          # int('x') in parse_truth (:1148-1200)
             elif bad == "no_as":                         # uniqness: KeyError in process_mate (:809-819)
                 f = f[:11] + [t for t in f[11:] if not t.startswith("AS:")]
+            elif bad == "b_no_cigar" and int(f[1]) & 2048:   # B.aend None: int(None) packing the pair
+                f[5] = "*"
+                if f[9] == "*":
+                    f[9], f[10] = "A" * 60, "I" * 60
         out.append("\t".join(f))
     p = str(tmp_path / "bad.sam")
     open(p, "w").write("\n".join(out) + "\n")
@@ -95,6 +99,9 @@ def test_parallel_recording_fails_where_python_loop_fails(tmp_path, monkeypatch,
     o2 = str(tmp_path / "native")
     rc2 = cli.main(["-G", fa, "-o", o2, "-q"] + extra + [p], evaluator_factory=pipelined_factory(3))
     assert rc1 == rc2 == 1
+    if bad == "b_no_cigar":
+        err = [l for l in open(os.path.join(o2, "run.log")) if "Error" in l]
+        assert err and "NoneType" in err[-1], err
     for f in ("multi_events.tsv", "test_results.tsv"):
         p1, p2 = os.path.join(o1, f), os.path.join(o2, f)
         assert os.path.exists(p1) == os.path.exists(p2)
