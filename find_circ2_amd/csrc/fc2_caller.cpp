@@ -849,11 +849,11 @@ void hit_apply(const fc2_caller *h, Hit &t, const SEv &e) {
     else { t.mq_a = std::max(t.mq_a, s.qA); t.mq_b = std::max(t.mq_b, s.qB); }
 }
 
-// the span-dependent part of Hit.add that needs the fragment's primary
+// the span-dependent part of Hit.add that needs the fragment's primary (its read passed
+// check_comp in phase A's store before the event was made: rev_comp(read), :573, :582)
 void hit_add_read(Arena &a, Hit &t, const Span &s, const Align &prim) {
     t.readnames.insert(prim.qname, a);
     const std::string &read = prim.seq;
-    check_comp(read);                           // rev_comp(read) raises here (:573, :582)
     t.n_reads += 1;
     t.has_tissue = true;
     t.tissue += s.weight;
@@ -1593,7 +1593,8 @@ struct FragScratch {
     std::vector<std::string> names;             // write_read: the junction names, sorted
     std::string tail;                           // ... and the name part both mates share
     std::string p1, p2;                         // multi_events row parts
-    void reset() { n_ev = 0; circ.clear(); lin.clear(); junc.clear(); warns = 0; }
+    bool comp_ok[2] = {false, false};           // the mate's read passed check_comp in this fragment
+    void reset() { n_ev = 0; circ.clear(); lin.clear(); junc.clear(); warns = 0; comp_ok[0] = comp_ok[1] = false; }
 };
 
 const std::vector<Splice> &find_breakpoints(const fc2_caller *h, int si, const Results &R, FragScratch &F) {
@@ -1638,7 +1639,10 @@ void phase_a_frag(const fc2_caller *h, uint32_t fi, const Frag &fr, const Result
         if (!span.q_int)  // a float / string last AS or XS: Python arithmetic (:558-566)
             throw Fatal{FC2_E_FORMAT, "native caller: the last AS / XS tags of a junction's anchors must be integers "
                                       "(use --python-caller)"};
-        check_comp(fr.prim[span.mate].seq);     // rev_comp(read) raises here (:573, :582)
+        if (!F.comp_ok[span.mate]) {            // rev_comp(read) raises here (:573, :582); once per mate
+            check_comp(fr.prim[span.mate].seq);
+            F.comp_ok[span.mate] = true;
+        }
         SEv e;
         e.key = splice_key(sp);
         e.seq = ((uint64_t)fi << 20) | ord++;
