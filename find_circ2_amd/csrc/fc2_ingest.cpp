@@ -1498,6 +1498,7 @@ void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b) {
             g.seq_len[k] = 0;
             if (!ms[k]) continue;
             g.seq_len[k] = R[ms[k]->r[0]].seq_n;
+            R[ms[k]->r[0]].decode();            // the primary's SEQ / QUAL, here rather than on the consumer's side
             g.r0[k] = (int32_t)b.gidx.size();
             g.n[k] = (int32_t)ms[k]->r.size();
             b.gidx.insert(b.gidx.end(), ms[k]->r.begin(), ms[k]->r.end());
