@@ -1973,6 +1973,15 @@ extern "C" void fc2_caller_close(fc2_caller *h) {
     delete h;
 }
 
+// the next side's workers (FC2_NEXT_THREADS, default min(8, cores)): process_mate over fragment
+// ranges, the chunk's pairs
+static void ensure_next_pool(fc2_caller *h) {
+    if (h->next_pool) return;
+    const char *env = getenv("FC2_NEXT_THREADS");
+    const int nt = env && atoi(env) > 0 ? atoi(env) : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+    h->next_pool.reset(new WorkPool(std::max(1, std::min(nt, 64)) - 1));
+}
+
 extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     if (!h || !b) return fc2::fail(FC2_E_PARAM, "fc2_caller_next: null argument");
     struct PublishStats {                          // on every way out of this call
@@ -2056,11 +2065,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         // ends the chunk there (an input error after it is never reached)
         h->bf_spans.resize(h->bf_nspans);
         h->bf_arena.resize(h->bf_narena);
-        if (!h->next_pool) {
-            const char *env = getenv("FC2_NEXT_THREADS");
-            int nt = env && atoi(env) > 0 ? atoi(env) : (int)std::min(4u, std::max(1u, std::thread::hardware_concurrency()));
-            h->next_pool.reset(new WorkPool(std::max(1, std::min(nt, 64)) - 1));
-        }
+        ensure_next_pool(h);
         const size_t nf = h->bf_nfrags;
         const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)h->next_pool->size(),
                                                               nf / std::max<size_t>(1, h->min_range_frags)));
@@ -2111,11 +2116,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     // the spans record_hits will evaluate, in fragment order (Caller._flush): counted per fragment
     // range, then written at each range's offset, on the next side's workers
     {
-        if (!h->next_pool) {
-            const char *env = getenv("FC2_NEXT_THREADS");
-            int nt = env && atoi(env) > 0 ? atoi(env) : (int)std::min(4u, std::max(1u, std::thread::hardware_concurrency()));
-            h->next_pool.reset(new WorkPool(std::max(1, std::min(nt, 64)) - 1));
-        }
+        ensure_next_pool(h);
         const size_t nf = h->bf_nfrags;
         const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)h->next_pool->size(),
                                                               nf / std::max<size_t>(1, h->min_range_frags)));
