@@ -267,34 +267,43 @@ def test_gpu_cli_asize_le_margin_equals_oracle(tmp_path, opts):
 
 @pytest.mark.parametrize("extra", [[], ["--python-caller"]])
 def test_gpu_cli_none_aend_span_raises_where_oracle_does(tmp_path, extra):
-    """A spliced read whose supplementary record has CIGAR '*' (align_B.aend None): the GPU runs
-    (native loop, and the Python loop with the GPU evaluator) fail at that fragment with the
-    reference's TypeError of `B.aend - eff_a` (find_circ.py:902), after recording the fragments
-    before it -- the same partial files as the oracle CLI."""
+    """A spliced read whose supplementary record -- the B segment, after a primary aligned from
+    query position 0 -- has CIGAR '*' (align_B.aend None): the GPU runs (native loop, and the Python
+    loop with the GPU evaluator) fail at that fragment with the reference's TypeError of
+    `B.aend - eff_a` (find_circ.py:902), after recording the fragments before it -- the same
+    partial files as the oracle CLI."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    import re
     from find_circ2_amd import cli
     from oracle_engine import oracle_evaluator_factory
     from test_native_caller import _rich_sam
     sam = str(tmp_path / "rich.sam")
     fa = _rich_sam(sam, 700, seed=77)
     lines = open(sam).read().splitlines()
-    supp = [l.split("\t")[0] for l in lines if not l.startswith("@") and int(l.split("\t")[1]) & 2048]
-    target = supp[len(supp) // 2]
-    out = []
-    for l in lines:
-        f = l.split("\t")
-        if not l.startswith("@") and f[0] == target and int(f[1]) & 2048:
-            f[5] = "*"
-            if f[9] == "*":
-                f[9], f[10] = "A" * 60, "I" * 60
-        out.append("\t".join(f))
-    p = str(tmp_path / "bad.sam")
-    open(p, "w").write("\n".join(out) + "\n")
-    o1, o2 = str(tmp_path / "oracle"), str(tmp_path / "gpu")
-    rc1 = cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", p], evaluator_factory=oracle_evaluator_factory)
-    rc2 = cli.main(["-G", fa, "-o", o2, "-q"] + extra + [p])
-    assert rc1 == rc2 == 1
-    err = [l for l in open(os.path.join(o2, "run.log")) if "Error" in l]
-    assert err and "unsupported operand type(s) for -: 'NoneType' and 'int'" in err[-1], err
-    _compare(o1, o2)
+    recs = [l.split("\t") for l in lines if not l.startswith("@")]
+    supp = {f[0] for f in recs if int(f[1]) & 2048}
+    cands = [f[0] for f in recs if f[0] in supp and not int(f[1]) & 2048 and re.match(r"^\d+M\d+S$", f[5])]
+    msg = "unsupported operand type(s) for -: 'NoneType' and 'int'"
+    for target in cands[len(cands) // 2:][:6]:
+        out = []
+        for l in lines:
+            f = l.split("\t")
+            if not l.startswith("@") and f[0] == target and int(f[1]) & 2048:
+                f[5] = "*"
+                if f[9] == "*":
+                    f[9], f[10] = "A" * 60, "I" * 60
+            out.append("\t".join(f))
+        p = str(tmp_path / "bad.sam")
+        open(p, "w").write("\n".join(out) + "\n")
+        o1, o2 = str(tmp_path / ("oracle_" + target)), str(tmp_path / ("gpu_" + target))
+        rc1 = cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", p], evaluator_factory=oracle_evaluator_factory)
+        if rc1 != 1 or msg not in open(os.path.join(o1, "run.log")).read():
+            continue                             # the span is not evaluated (not unique enough)
+        rc2 = cli.main(["-G", fa, "-o", o2, "-q"] + extra + [p])
+        assert rc2 == 1
+        err = [l for l in open(os.path.join(o2, "run.log")) if "Error" in l]
+        assert err and msg in err[-1], err
+        _compare(o1, o2)
+        return
+    pytest.fail("no fragment whose B segment's span is evaluated")
