@@ -4,9 +4,11 @@ The reference writes the file through one GzipFile at level 9 (find_circ.py:445)
 at genome scale costs more than the whole native read loop.  Here the text is cut into
 ~4 MiB pieces, each compressed as its own gzip member on a thread pool (zlib releases the
 GIL) and written in order; concatenated members are one valid gzip stream (RFC 1952 2.2),
-so every gzip reader returns the same text.  Level 2: on the FASTQ text this file holds it
-compresses 6x faster than level 6 for 13 % more bytes (5.2x instead of 6.0x smaller), which at
-genome scale is the difference between the compression and the read loop setting the pace.  Text is encoded as latin-1, the decoding every
+so every gzip reader returns the same text.  Level 1: on the FASTQ text this file holds, zlib's
+level 2 compresses 6x faster than level 6 for 13 % more bytes (5.2x instead of 6.0x smaller), and
+the native loop's libdeflate (csrc/fc2_deflate.h) at level 1 is another 1.55x faster than at level 2
+for 1 % more bytes -- at genome scale the compression would otherwise set the read loop's pace on
+the box's CPU quota.  Text is encoded as latin-1, the decoding every
 reader of this package uses, so input bytes >= 0x80 (qnames, SEQ/QUAL) are written back as the
 same single bytes, as the Python-2 reference writes its byte strings.
 """
@@ -25,7 +27,7 @@ def _member(data: bytes, level: int) -> bytes:
 
 
 class ParallelGzipWriter(io.TextIOBase):
-    def __init__(self, path: str, level: int = 2, threads: int = 0, piece: int = 4 << 20, encoding: str = "latin-1"):
+    def __init__(self, path: str, level: int = 1, threads: int = 0, piece: int = 4 << 20, encoding: str = "latin-1"):
         self.path = path
         self.level = level
         self.piece = piece
