@@ -31,6 +31,7 @@
 
 #include "../../include/fc2_caller.h"
 #include "fc2_common.h"
+#include "fc2_cpuacct.h"
 #include "fc2_gzpieces.h"
 #include "fc2_ingest_impl.h"
 
@@ -1969,8 +1970,16 @@ extern "C" fc2_ingest *fc2_caller_ingest(fc2_caller *h) { return h ? h->ing : nu
 
 extern "C" void fc2_caller_close(fc2_caller *h) {
     if (!h) return;
-    fc2_ingest_close(h->ing);
+    fc2_ingest_close(h->ing);                   // (joins the parse-ahead threads)
     delete h;
+    if (fc2::cpu::enabled()) {                  // CPU seconds per stage over the run (fc2_cpuacct.h)
+        static const char *const kName[fc2::cpu::kStages] = {"inflate", "split", "parse+group", "consumer",
+                                                              "next pool", "submit pool", "submit serial", "gzip"};
+        std::atomic<int64_t> *t = fc2::cpu::totals();
+        fprintf(stderr, "cpu s:");
+        for (int k = 0; k < fc2::cpu::kStages; ++k) fprintf(stderr, " %s %.3f", kName[k], (double)t[k].exchange(0) * 1e-9);
+        fprintf(stderr, "\n");
+    }
 }
 
 // the next side's workers (FC2_NEXT_THREADS, default min(8, cores)): process_mate over fragment
@@ -2049,6 +2058,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         return std::chrono::duration<double, std::milli>(b - a).count();
     };
     const auto t0 = now();
+    fc2::cpu::Scope acct(fc2::cpu::CONSUME);      // this thread's share of the call (the pools count apart)
     while (!h->eof && h->bf_nfrags < limit) {
         int e = 0;
         const int rc = fc2::ing::pull(h->ing, &h->ip, limit - h->bf_nfrags, sink, &e);   // at most `limit` per chunk
@@ -2074,6 +2084,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         Span *spans = h->bf_spans.data();
         char *arena = h->bf_arena.data();
         h->next_pool->run_checked((int)T, [&](int r) {
+            fc2::cpu::Scope acct(fc2::cpu::NEXT_POOL);
             auto &N = h->next_N[(size_t)r];
             N.clear();
             for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
@@ -2125,6 +2136,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         const int64_t min_uq = h->o.min_uniq_qual;
         auto eligible = [&](const Span &sp) { return sp.uniq >= min_uq; };
         h->next_pool->run((int)T, [&](int r) {
+            fc2::cpu::Scope acct(fc2::cpu::NEXT_POOL);
             uint64_t n = 0;
             for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
                 const Frag &fr = h->bf_frags[f];
@@ -2137,6 +2149,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         h->bf_pairs.resize(cnt[T]);
         h->bf_off.resize(cnt[T]);
         h->next_pool->run((int)T, [&](int r) {
+            fc2::cpu::Scope acct(fc2::cpu::NEXT_POOL);
             uint64_t k = cnt[(size_t)r];
             for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
                 const Frag &fr = h->bf_frags[f];
@@ -2246,18 +2259,30 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
         const auto t0 = now();
         struct rusage ru0;
         getrusage(RUSAGE_SELF, &ru0);
-        h->pool->run_checked((int)T, [&](int r) { phase_a(h, nf * (size_t)r / T, nf * (size_t)(r + 1) / T, R, h->ranges[(size_t)r]); });
+        h->pool->run_checked((int)T, [&](int r) {
+            fc2::cpu::Scope acct(fc2::cpu::SUBMIT_POOL);
+            phase_a(h, nf * (size_t)r / T, nf * (size_t)(r + 1) / T, R, h->ranges[(size_t)r]);
+        });
         uint64_t fe = nf;                       // the first fragment that raised (or none)
         size_t n_r = T;                         // the ranges that count: up to the one that raised
         for (size_t r = 0; r < T; ++r)
             if (h->ranges[r].err_frag >= 0) { fe = (uint64_t)h->ranges[r].err_frag; n_r = r + 1; break; }
         // (B) the shards apply their events in input order; (C) names; (D) read names, multi rows
         const auto t1 = now();
-        h->pool->run_checked(kShards, [&](int sidx) { phase_b(h, sidx, n_r, fe); });
+        h->pool->run_checked(kShards, [&](int sidx) {
+            fc2::cpu::Scope acct(fc2::cpu::SUBMIT_POOL);
+            phase_b(h, sidx, n_r, fe);
+        });
         const auto t2 = now();
-        phase_c(h);
+        {
+            fc2::cpu::Scope acct(fc2::cpu::SUBMIT_SERIAL);
+            phase_c(h);
+        }
         const auto t3 = now();
-        h->pool->run_checked((int)n_r, [&](int r) { phase_d(h, h->ranges[(size_t)r], fe); });
+        h->pool->run_checked((int)n_r, [&](int r) {
+            fc2::cpu::Scope acct(fc2::cpu::SUBMIT_POOL);
+            phase_d(h, h->ranges[(size_t)r], fe);
+        });
         const auto t4 = now();
         if (timing) {
             auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };

@@ -7,6 +7,7 @@
 #include <stdio.h>
 #include <zlib.h>
 
+#include "fc2_cpuacct.h"
 #include "fc2_deflate.h"
 
 #include <algorithm>
@@ -139,6 +140,7 @@ class GzPieces {
     }
 
     void compress(Job &j) {
+        cpu::Scope acct(cpu::GZIP);
         if (!dfl::gzip_member(j.in, level_, j.out)) j.zerr = true;   // libdeflate, or zlib (fc2_deflate.h)
         std::string().swap(j.in);
     }

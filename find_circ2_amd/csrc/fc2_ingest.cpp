@@ -34,6 +34,7 @@
 #include "../../include/fc2_ingest.h"
 #include "fc2_bamout.h"
 #include "fc2_common.h"
+#include "fc2_cpuacct.h"
 #include "fc2_deflate.h"
 #include "fc2_ingest_impl.h"
 
@@ -245,6 +246,7 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
     std::atomic<size_t> next{0};
     std::atomic<bool> bad{false};
     auto work = [&]() {
+        fc2::cpu::Scope acct(fc2::cpu::INFLATE);
         fc2::dfl::Inflater inf;                 // libdeflate (zlib without it): fc2_deflate.h
         if (!inf.ok()) { bad = true; return; }
         for (size_t i; (i = next.fetch_add(1)) < nb && !bad;) {
@@ -923,6 +925,7 @@ int read_header(fc2_ingest *h) {
 // (A is handed over, not read from h->ahead: closing resets h->ahead before ~SamAhead joins, and a
 // thread that only starts running then must still find its object)
 void sam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
+    fc2::cpu::Scope acct(fc2::cpu::SPLIT);
     auto &A = *ap;
     std::string carry(h->buf.data() + h->beg, h->end - h->beg);   // bytes read with the header
     h->beg = h->end;
@@ -999,6 +1002,7 @@ void sam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
 // each.  Where the stream ends inside a record, or the input fails, the block ends after the last
 // whole record and carries the error parse_bam_record would have reported there.
 void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
+    fc2::cpu::Scope acct(fc2::cpu::SPLIT);
     auto &A = *ap;
     for (uint64_t seq = 0;; ++seq) {
         std::unique_ptr<fc2_ingest::SamAhead::Batch> b;
@@ -1069,6 +1073,7 @@ void bam_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
 // on this thread (bam_split_loop copies it twice: into the reader's buffer, then into the block).
 // The errors are bam_split_loop's, at the same records.
 void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
+    fc2::cpu::Scope acct(fc2::cpu::SPLIT);
     auto &A = *ap;
     std::shared_ptr<CharBuf> cur = std::make_shared<CharBuf>(h->buf.begin() + (ptrdiff_t)h->beg,
                                                              h->buf.begin() + (ptrdiff_t)h->end);   // inflated with the header
@@ -1170,6 +1175,7 @@ void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b);
 
 // parser: blocks to record batches (own RNAME cache and CIGAR scratch)
 void sam_parse_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
+    fc2::cpu::Scope acct(fc2::cpu::PARSE);
     auto &A = *ap;
     fc2_ingest::ParseScratch ps;
     for (;;) {
