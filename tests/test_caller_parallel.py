@@ -109,3 +109,58 @@ def test_parallel_recording_fails_where_python_loop_fails(tmp_path, monkeypatch,
             assert open(p1).read() == open(p2).read(), f
     r1, r2 = _gz(os.path.join(o1, "spliced_reads.fastq.gz")), _gz(os.path.join(o2, "spliced_reads.fastq.gz"))
     assert r1 == r2 and r1.count("\n@") > 10
+
+
+def _edge_sam(src, dst, seed, first):
+    """The rich SAM with grouping edge cases spliced in: unmapped records with fresh qnames and with
+    the qname of the record before them, a fragment's records repeated later (its qname seen again
+    after others), and a first record that is unmapped -- with the first mapped qname ("same") or
+    another ("other")."""
+    import random
+    rng = random.Random(seed)
+    lines = open(src).read().splitlines()
+    head = [l for l in lines if l.startswith("@")]
+    body = [l for l in lines if not l.startswith("@")]
+    out = []
+    for k, l in enumerate(body):
+        f = l.split("\t")
+        r = rng.random()
+        if r < 0.03:
+            out.append("\t".join(["unm%d" % k, "4", "*", "0", "0", "*", "*", "0", "0", "ACGTACGTAC", "IIIIIIIIII"]))
+        elif r < 0.06:
+            out.append("\t".join([f[0], str(4 | (int(f[1]) & 0x40)), "*", "0", "0", "*", "*", "0", "0", "ACGT", "IIII"]))
+        out.append(l)
+        if r > 0.985 and k > 10:                         # an earlier fragment's records again
+            q = body[k - 7].split("\t")[0]
+            out.extend(x for x in body[max(0, k - 12):k] if x.split("\t")[0] == q)
+    q0 = out[0].split("\t")[0] if first == "same" else "lead"
+    out.insert(0, "\t".join([q0, "4", "*", "0", "0", "*", "*", "0", "0", "ACGTAC", "IIIIII"]))
+    open(dst, "w").write("\n".join(head + out) + "\n")
+
+
+@pytest.mark.parametrize("first", ["same", "other"])
+@pytest.mark.parametrize("mode", [dict(FC2_PARSE_BLOCK="300", FC2_PARSE_INFLIGHT="2"),
+                                  dict(FC2_PARSE_BLOCK="1100", FC2_NEXT_THREADS="3", FC2_CALLER_MIN_RANGE="1"),
+                                  dict(FC2_GROUP_AHEAD="0", FC2_PARSE_BLOCK="500")])
+@pytest.mark.parametrize("bam", [False, True])
+def test_grouping_edge_cases_equal_python_ingest(tmp_path, monkeypatch, rich, first, mode, bam):
+    """Fragments grouped on the parse threads (group_batch) at tiny parse blocks against the pure
+    Python reader and loop (--python-ingest: samio + caller, find_circ.py:1450-1486): every file
+    and every run.log counter identical, with unmapped records inside and between fragments, a
+    qname seen again after others, and an unmapped first record."""
+    from samgen import sam_to_bam
+    from test_ingest import same as same_files
+    fa, sam = rich
+    p = str(tmp_path / "edge.sam")
+    _edge_sam(sam, p, seed=len(first) + len(mode), first=first)
+    if bam:
+        sam_to_bam(open(p).read(), str(tmp_path / "edge.bam"))
+        p = str(tmp_path / "edge.bam")
+    o1 = str(tmp_path / "py")
+    rc1 = cli.main(["-G", fa, "-o", o1, "-q", "--python-ingest"] + [p], evaluator_factory=oracle_evaluator_factory)
+    for k, v in mode.items():
+        monkeypatch.setenv(k, v)
+    o2 = str(tmp_path / "native")
+    rc2 = cli.main(["-G", fa, "-o", o2, "-q", p], evaluator_factory=pipelined_factory(3))
+    assert rc1 == rc2 == 0
+    same_files(o1, o2)
