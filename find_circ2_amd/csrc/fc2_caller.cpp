@@ -2297,7 +2297,7 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
             RangeOut &ro = h->ranges[r];
             for (const auto &kv : ro.N) incN(h, kv.first, kv.second);
             if (h->reads_gz.is_open()) {
-                if (!ro.out0.empty()) h->reads_gz.append(ro.out0);
+                h->reads_gz.append_owned(ro.out0);   // each range's text is one gzip member, not copied
             } else {
                 h->out[0] += ro.out0;
             }

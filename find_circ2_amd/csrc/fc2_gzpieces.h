@@ -61,6 +61,32 @@ class GzPieces {
         text.clear();
     }
 
+    // takes `text` whole as the next member (after what append() left pending) if it is at most two
+    // pieces long, leaving `text` empty with a recycled buffer's capacity: a chunk's range texts go
+    // out without being copied
+    void append_owned(std::string &text) {
+        if (text.empty()) return;
+        if (text.size() > 2 * piece_) {         // members stay about a piece long
+            append(text);
+            return;
+        }
+        if (!buf_.empty()) {
+            submit(std::move(buf_));
+            buf_.clear();
+        }
+        std::string fresh;
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            if (!spare_.empty()) {
+                fresh.swap(spare_.back());
+                spare_.pop_back();
+            }
+        }
+        fresh.swap(text);                       // text: the recycled buffer, emptied
+        text.clear();
+        submit(std::move(fresh));
+    }
+
     // compresses what is left, writes every member, stops the workers; false on a write error
     bool close(std::string &err) {
         if (!f_) return true;
@@ -96,6 +122,7 @@ class GzPieces {
     std::condition_variable cv_work_, cv_done_;
     std::vector<std::thread> th_;
     bool stop_ = false, werr_ = false, wrote_any_ = false;
+    std::vector<std::string> spare_;           // compressed inputs' buffers, for append_owned
 
     void submit(std::string &&data) {
         auto j = std::make_shared<Job>();
@@ -142,6 +169,9 @@ class GzPieces {
     void compress(Job &j) {
         cpu::Scope acct(cpu::GZIP);
         if (!dfl::gzip_member(j.in, level_, j.out)) j.zerr = true;   // libdeflate, or zlib (fc2_deflate.h)
+        j.in.clear();
+        std::lock_guard<std::mutex> lk(m_);
+        if (spare_.size() < 2 * max_pending_) spare_.push_back(std::move(j.in));
         std::string().swap(j.in);
     }
 };
