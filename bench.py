@@ -33,6 +33,7 @@ sys.path.insert(0, ROOT)
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 STRONG_TAIL = 0          # configs[3]: default --strong-tail (shard.round_bounds)
+CLI_RUNS = 3               # cli_end_to_end: BAM-on-stdin runs, the median reported
 HEADLINE_RESULT_BYTES = 2  # the headline scan's result form: 2-byte compact words (fc2_bp_scan_compact_launch)
 MERGE_ROUNDS = 5           # interleaved zero-copy / device-memory rounds behind merge_ms_per_step
 METRIC = "anchor-pairs/sec (backsplice calls) at 100 bp reads, 1/2/4/8 MI355X"
@@ -1109,10 +1110,11 @@ def cli_end_to_end(reads=2_000_000):
     find_circ -G genome.fa -o out``: scripts/cli_scale_check.py's generator writes an hg19-shaped genome
     FASTA and a bwa-mem-like SAM of `reads` reads, fc2_sam_to_bam turns it into a BGZF BAM, and
     `python -m find_circ2_amd.cli` runs as its own process reading that BAM from a stdin pipe (format
-    detected from the bytes; BGZF blocks inflated on worker threads, C++ read loop on two threads, HIP
-    search through pipeline.ScanPipeline, gzip members on worker threads).  The same reads as SAM text
-    by path run too; both runs must write identical files.  The first run builds the .byo_index; the
-    runs after it are reported: the loop's own reads/s (run.log) and the process wall time."""
+    detected from the bytes; BGZF blocks inflated on worker threads, the C++ read loop on worker pools,
+    HIP search through pipeline.ScanPipeline, gzip members on worker threads).  The same reads as SAM
+    text by path run too; both runs must write identical files.  The first run builds the .byo_index;
+    the runs after it are reported: the loop's own reads/s (run.log) and the process wall time, the
+    BAM form as the median of CLI_RUNS runs (one run moves +-10 % on the box's shared CPU quota)."""
     import re
     import shutil
     import subprocess
@@ -1153,7 +1155,11 @@ def cli_end_to_end(reads=2_000_000):
                          "process_wall_s": round(wall, 2), "stages": st.group(1) if st else None}
 
         run("warm", False)                     # builds genome.fa.byo_index
-        o_bam, res = run("bam_stdin", True)
+        runs = [run("bam_stdin%d" % k, True) for k in range(CLI_RUNS)]
+        vals = [r[1]["value"] for r in runs]
+        k_med = sorted(range(len(runs)), key=lambda k: (vals[k] is None, vals[k] or 0))[len(runs) // 2]
+        o_bam, res = runs[k_med]
+        res = dict(res, runs=vals)
         o_sam, res_sam = run("sam_path", False)
         res["reads"] = reads
         res["bam_bytes"] = os.path.getsize(bam)
@@ -1161,7 +1167,7 @@ def cli_end_to_end(reads=2_000_000):
         res["sam_by_path"] = res_sam
         res["note"] = ("whole CLI, BGZF BAM piped on stdin (cat reads.bam | python -m find_circ2_amd.cli -G genome.fa "
                        "-o out), hg19-shaped genome, .byo_index present: value = the read loop's reads/s from "
-                       "run.log; process_wall_s includes interpreter start, genome load and upload; sam_by_path = "
+                       "run.log, the median of `runs`; process_wall_s includes interpreter start, genome load and upload; sam_by_path = "
                        "the same reads as SAM text by path; outputs of the two runs compared here, and against "
                        "the Python loop in tests and scripts/cli_scale_check.py")
         return res
