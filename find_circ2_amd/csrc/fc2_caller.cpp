@@ -2059,7 +2059,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     };
     const auto t0 = now();
     fc2::cpu::Scope acct(fc2::cpu::CONSUME);      // this thread's share of the call (the pools count apart)
-    while (!h->eof && h->bf_nfrags < limit) {
+    while (!h->eof && h->bf_nfrags < limit && !fc2::ing::pin_full(h->ing)) {
         int e = 0;
         const int rc = fc2::ing::pull(h->ing, &h->ip, limit - h->bf_nfrags, sink, &e);   // at most `limit` per chunk
         if (rc) {

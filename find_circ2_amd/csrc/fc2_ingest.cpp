@@ -400,6 +400,8 @@ struct fc2_ingest::SamAhead {
     uint64_t grouped = 0;                       // handed fragments grouped on the parse threads
     bool pin = false;                           // set_pin: consumed batches wait in `pinned` for release()
     std::vector<std::unique_ptr<Batch>> pinned;
+    size_t max_pinned = 64;                     // pull stops there (FC2_PIN_MAX): few handed fragments
+                                                // must not pin the whole input
     bool stop = false;
     std::thread splitter;
     std::vector<std::thread> parsers;
@@ -1707,6 +1709,8 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
     int rc = FC2_OK;
     bool done = h->finished;
     while (!done && frags < max_frags) {
+        if (sink && h->ahead && h->ahead->pin && h->ahead->pinned.size() >= h->ahead->max_pinned)
+            break;                              // the chunk ends here (fc2::ing::pin_full)
         // a batch's region grouped on its parse thread (group_batch): its first record closes the
         // current fragment; then the region's handed fragments go to the sink, and its last
         // record opens the fragment the loop goes on with
@@ -1820,6 +1824,8 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
         h->ahead.reset(ap);
         if (const char *be = getenv("FC2_PARSE_BLOCK"))
             if (atol(be) > 0) ap->block = (size_t)atol(be);
+        if (const char *pm = getenv("FC2_PIN_MAX"))
+            if (atoi(pm) > 0) ap->max_pinned = (size_t)atoi(pm);
         if (const char *fe = getenv("FC2_PARSE_INFLIGHT"))
             if (atoi(fe) > 0) ap->max_inflight = (size_t)std::min(atoi(fe), 256);
         const char *zc = getenv("FC2_BGZF_INPLACE");     // 0: the copying splitter (A/B)
@@ -1845,6 +1851,10 @@ void fc2::ing::set_pin(fc2_ingest *h, bool on) {
     h->pin = on;
     if (h->ahead) h->ahead->pin = on;
     if (!on) release(h);
+}
+
+bool fc2::ing::pin_full(const fc2_ingest *h) {
+    return h && h->ahead && h->ahead->pin && h->ahead->pinned.size() >= h->ahead->max_pinned;
 }
 
 void fc2::ing::release(fc2_ingest *h) {

@@ -137,6 +137,8 @@ bool writes_records(const fc2_ingest *h);
 // are not reused) until release(); the sink then gets stable MateRefs for them
 void set_pin(fc2_ingest *h, bool on);
 void release(fc2_ingest *h);
+// as many batches pinned as allowed (FC2_PIN_MAX, default 64): pull returns, the chunk ends there
+bool pin_full(const fc2_ingest *h);
 
 // the consumer's time spent waiting for parse-ahead batches since the last call, and the handed
 // fragments grouped on the parse threads meanwhile (FC2_CALLER_TIMING)

@@ -21,7 +21,9 @@ MODES = [dict(FC2_CALLER_THREADS="1", FC2_NEXT_THREADS="1"),
          # by a block boundary, regions of one fragment, none), and grouped on the consumer alone
          dict(FC2_PARSE_BLOCK="700", FC2_NEXT_THREADS="2", FC2_CALLER_MIN_RANGE="1", FC2_PARSE_INFLIGHT="2"),
          dict(FC2_PARSE_BLOCK="4000", FC2_PARSE_THREADS="5", FC2_CALLER_THREADS="3"),
-         dict(FC2_GROUP_AHEAD="0", FC2_PARSE_BLOCK="1500")]
+         dict(FC2_GROUP_AHEAD="0", FC2_PARSE_BLOCK="1500"),
+         # chunks cut short by the pinned-batch cap (one 400-byte block per chunk; some chunks empty)
+         dict(FC2_PARSE_BLOCK="400", FC2_PIN_MAX="1", FC2_PARSE_INFLIGHT="3")]
 
 
 @pytest.fixture(scope="module")
