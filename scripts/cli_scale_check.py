@@ -129,6 +129,7 @@ def main():
     res = {"reads": a.reads, "bases": int(sum(sizes)), "gen_s": round(t_gen, 1)}
     outs = {}
     for tag, extra in (("native", []), ("native_gpus2", ["--gpus", "2"]), ("python_caller", ["--python-caller"]),
+                       ("python_ingest", ["--python-ingest"]),
                        ("native_allhits", ["--all-hits", "--non-canonical"]),
                        ("python_caller_allhits", ["--python-caller", "--all-hits", "--non-canonical"])):
         if a.only and tag not in a.only.split(","):
@@ -147,7 +148,8 @@ def main():
         print(json.dumps(res))
         return 0
     same = True
-    for x, y in (("native", "python_caller"), ("native", "native_gpus2"), ("native_allhits", "python_caller_allhits")):
+    for x, y in (("native", "python_caller"), ("native", "native_gpus2"), ("native", "python_ingest"),
+                 ("native_allhits", "python_caller_allhits")):
         for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
             if open(os.path.join(outs[x], f)).read() != open(os.path.join(outs[y], f)).read():
                 same = False
