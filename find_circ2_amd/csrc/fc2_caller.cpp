@@ -818,18 +818,15 @@ void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
 void CanonSet::insert(const std::string &read, Arena &a) {
     const size_t n = read.size();
     const unsigned char *in = (const unsigned char *)read.data();
-    int cmp = 0;                                // read vs rc(read), bytewise as std::string compares
-    for (size_t k = 0; k < n && !cmp; ++k) {
-        const unsigned char x = in[k], y = (unsigned char)kComp.t[in[n - 1 - k]];
-        cmp = x < y ? -1 : (x > y ? 1 : 0);
-    }
+    static thread_local std::string rc;         // rc(read) in one branch-free pass, then one memcmp
+    rc.resize(n);
+    char *o = &rc[0];
+    for (size_t k = 0; k < n; ++k) o[k] = kComp.t[in[n - 1 - k]];
+    const int cmp = n ? memcmp(read.data(), rc.data(), n) : 0;   // bytewise, as std::string compares
     if (cmp <= 0) {
         if (canon.insert(read, a) && cmp == 0) palindromes += 1;
         return;
     }
-    static thread_local std::string rc;
-    rc.resize(n);
-    for (size_t k = 0; k < n; ++k) rc[k] = kComp.t[in[n - 1 - k]];
     canon.insert(rc, a);
 }
 

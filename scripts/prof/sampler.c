@@ -40,6 +40,59 @@ static void on_prof(int sig, siginfo_t *si, void *ucv) {
     }
 }
 
+/* FC2_SAMPLE_ALL: a CLOCK_MONOTONIC timer per thread (hrtimer resolution, unlike the tick-driven CPU
+   clocks), each signalling its own thread; a monitor thread arms one for every new thread found in
+   /proc/self/task.  Samples of blocked threads land in the blocking call (report.py --drop-waits). */
+#include <dirent.h>
+#include <pthread.h>
+#define MAXT 512
+static int n_armed;
+static pid_t armed[MAXT];
+static timer_t armed_timer[MAXT];
+static volatile int monitor_stop;
+static pthread_t monitor;
+static int sample_usec;
+
+static int arm(pid_t t) {
+    for (int i = 0; i < n_armed; ++i)
+        if (armed[i] == t) return 0;
+    if (n_armed >= MAXT) return -1;
+    struct sigevent ev;
+    memset(&ev, 0, sizeof ev);
+    ev.sigev_signo = SIGPROF;
+    ev.sigev_notify = SIGEV_THREAD_ID;
+    ev._sigev_un._tid = t;
+    timer_t tm;
+    if (timer_create(CLOCK_MONOTONIC, &ev, &tm)) return -1;
+    struct itimerspec it;
+    it.it_interval.tv_sec = 0;
+    it.it_interval.tv_nsec = (long)sample_usec * 1000L;
+    it.it_value = it.it_interval;
+    timer_settime(tm, 0, &it, 0);
+    armed[n_armed] = t;
+    armed_timer[n_armed++] = tm;
+    return 1;
+}
+
+static void *monitor_loop(void *arg) {
+    (void)arg;
+    const pid_t self = (pid_t)syscall(SYS_gettid);
+    while (!monitor_stop) {
+        DIR *d = opendir("/proc/self/task");
+        if (d) {
+            struct dirent *e;
+            while ((e = readdir(d)))
+                if (e->d_name[0] != '.') {
+                    const pid_t t = (pid_t)atoi(e->d_name);
+                    if (t != self) arm(t);
+                }
+            closedir(d);
+        }
+        usleep(2000);
+    }
+    return 0;
+}
+
 int sampler_start(int usec) {
     void *warm[4];
     backtrace(warm, 4);                          // loads the unwinder outside the signal handler
@@ -51,6 +104,11 @@ int sampler_start(int usec) {
     struct sigevent ev;
     memset(&ev, 0, sizeof ev);
     ev.sigev_signo = SIGPROF;
+    if (getenv("FC2_SAMPLE_ALL")) {
+        sample_usec = usec;
+        monitor_stop = 0;
+        return pthread_create(&monitor, 0, monitor_loop, 0);
+    }
     if (getenv("FC2_SAMPLE_PROCESS")) {          /* every thread, on the process's CPU clock (ITIMER_PROF:
                                                     the signal goes to the thread that used the CPU) */
         struct itimerval iv;
@@ -79,6 +137,12 @@ void sampler_phase(int tag) { cur_tag = tag; }
 
 int sampler_stop(const char *path) {
     cur_tag = 0;
+    if (getenv("FC2_SAMPLE_ALL")) {
+        monitor_stop = 1;
+        pthread_join(monitor, 0);
+        for (int i = 0; i < n_armed; ++i) timer_delete(armed_timer[i]);
+        n_armed = 0;
+    } else
     if (getenv("FC2_SAMPLE_PROCESS")) {
         struct itimerval iv;
         memset(&iv, 0, sizeof iv);
