@@ -213,24 +213,26 @@ struct Span {                                  // JunctionSpan (:821-852)
 };
 
 struct Frag {
-    std::string name;
+    // what on_fragment writes, first and together (the chunk's Frags are written in order, and a
+    // Frag is ~600 bytes: the fewer cache lines the consumer touches per fragment the better)
     bool has[2] = {false, false};
-    Align prim[2];
-    std::vector<int> circ, lin;                // indices into the chunk's spans
-    std::vector<APos> unspliced, broken;
-    // the mates' records as process_mate reads them (next side): fields at the chunk's recf[r0,
-    // r0 + nrec), the proper segments' indices at prop[p0, p0 + np)
-    struct MateFields {
-        uint32_t r0 = 0, nrec = 0, p0 = 0, np = 0;
-    } mf[2];
-    uint64_t span0 = 0, span_max = 0;          // its span slots [span0, span0 + span_max) in the chunk
-    uint64_t arena0 = 0;                       // its read_part bytes from here (at most one read per pair)
     bool dropped = false;                      // no pair record_hits would look at (on_fragment)
     // recorded in place (a fragment grouped on a parse thread, its batch pinned until the chunk is
     // processed): the mates' records are read where they are, name and primaries taken by
     // process_frag on the workers instead of by on_fragment
     bool in_batch = false;
+    uint64_t span0 = 0, span_max = 0;          // its span slots [span0, span0 + span_max) in the chunk
+    uint64_t arena0 = 0;                       // its read_part bytes from here (at most one read per pair)
+    // the mates' records as process_mate reads them (next side): fields at the chunk's recf[r0,
+    // r0 + nrec), the proper segments' indices at prop[p0, p0 + np)
+    struct MateFields {
+        uint32_t r0 = 0, nrec = 0, p0 = 0, np = 0;
+    } mf[2];
     MateRef ref[2];
+    std::string name;
+    Align prim[2];
+    std::vector<int> circ, lin;                // indices into the chunk's spans
+    std::vector<APos> unspliced, broken;
 };
 
 // a mate's records as process_mate reads them: recorded fields, or records in their parse batch
