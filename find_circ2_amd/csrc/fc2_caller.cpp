@@ -696,6 +696,14 @@ struct fc2_caller {
     uint64_t bf_nspans = 0, bf_narena = 0;      // span slots / arena bytes reserved so far
     std::vector<RecFields> bf_recf;             // the chunk's mates' records (Frag::MateFields)
     std::vector<int32_t> bf_prop;
+    // runs of fragments a parse thread grouped, recorded whole (the bulk sink): fragments
+    // [f0, f0 + r.n) of the chunk, their spans and read parts from span0 / arena0 on
+    struct Seg {
+        fc2::ing::RegionRef r;
+        size_t f0;
+        uint64_t span0, arena0;
+    };
+    std::vector<Seg> bf_segs;
     std::unique_ptr<WorkPool> next_pool;        // the next side's workers (process_mate)
     std::vector<std::vector<std::pair<const char *, double>>> next_N;   // their counters per range
     std::vector<std::pair<int64_t, Fatal>> next_err_at;                 // their first error per range
@@ -1981,6 +1989,33 @@ extern "C" void fc2_caller_close(fc2_caller *h) {
     }
 }
 
+// a fragment of a bulk-recorded run (fc2_caller::Seg): what on_fragment writes for one recorded in
+// place, from its GFrag
+static void fill_from_seg(const fc2_caller::Seg &sg, size_t f, Frag &fr) {
+    const size_t i = f - sg.f0;
+    const fc2::ing::GFrag &g = sg.r.g[i];
+    const uint64_t sb = i ? sg.r.g[i - 1].span_cum : sg.r.span_before;
+    const uint64_t ab = i ? sg.r.g[i - 1].arena_cum : sg.r.arena_before;
+    fr.in_batch = true;
+    fr.dropped = false;
+    fr.span0 = sg.span0 + (sb - sg.r.span_before);
+    fr.arena0 = sg.arena0 + (ab - sg.r.arena_before);
+    fr.span_max = g.span_cum - sb;
+    for (int k = 0; k < 2; ++k) {
+        fr.has[k] = k == 1 || g.n[0] != 0;
+        fr.mf[k] = Frag::MateFields();
+        if (!fr.has[k]) continue;
+        MateRef &m = fr.ref[k];
+        m.base = sg.r.recs;
+        m.idx = sg.r.gidx + g.r0[k];
+        m.n = (uint32_t)g.n[k];
+        m.proper = sg.r.gidx + g.p0[k];
+        m.np = (uint32_t)g.np[k];
+        m.seq_len = g.seq_len[k];
+        m.stable = true;
+    }
+}
+
 // the next side's workers (FC2_NEXT_THREADS, default min(8, cores)): process_mate over fragment
 // ranges, the chunk's pairs
 static void ensure_next_pool(fc2_caller *h) {
@@ -2025,6 +2060,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     }
     h->bf_nfrags = 0;
     h->bf_nspans = h->bf_narena = 0;
+    h->bf_segs.clear();
     h->bf_recf.clear();
     h->bf_prop.clear();
     h->bf_off.clear();
@@ -2036,6 +2072,17 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     // this chunk's fragments are processed below
     fc2::ing::set_pin(h->ing, defer);
     Fatal err{0, ""};
+    // a run of fragments grouped on a parse thread: recorded whole, each fragment's slot filled by
+    // the workers below (fill_from_seg); its spans and read parts take their room here
+    const fc2::ing::BulkSink bulk = [&](const fc2::ing::RegionRef &r) -> int {
+        h->bf_segs.push_back(fc2_caller::Seg{r, h->bf_nfrags, h->bf_nspans, h->bf_narena});
+        const size_t need = h->bf_nfrags + r.n;
+        if (h->bf_frags.size() < need) h->bf_frags.resize(need);
+        h->bf_nfrags = need;
+        h->bf_nspans += r.g[r.n - 1].span_cum - r.span_before;
+        h->bf_narena += r.g[r.n - 1].arena_cum - r.arena_before;
+        return FC2_OK;
+    };
     const fc2::ing::FragSink sink = [&](MateRef *m1, MateRef *m2, bool) -> int {
         try {
             return on_fragment(h, m1, m2, defer);
@@ -2060,7 +2107,8 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     fc2::cpu::Scope acct(fc2::cpu::CONSUME);      // this thread's share of the call (the pools count apart)
     while (!h->eof && h->bf_nfrags < limit && !fc2::ing::pin_full(h->ing)) {
         int e = 0;
-        const int rc = fc2::ing::pull(h->ing, &h->ip, limit - h->bf_nfrags, sink, &e);   // at most `limit` per chunk
+        const int rc = fc2::ing::pull(h->ing, &h->ip, limit - h->bf_nfrags, sink, &e,   // at most `limit` per chunk
+                                      defer ? &bulk : nullptr);
         if (rc) {
             in_code = err.code ? err.code : rc;
             in_msg = err.code ? err.msg : std::string(fc2_last_error());
@@ -2086,7 +2134,15 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             fc2::cpu::Scope acct(fc2::cpu::NEXT_POOL);
             auto &N = h->next_N[(size_t)r];
             N.clear();
-            for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
+            const size_t fa = nf * (size_t)r / T;
+            // the first run (bulk-recorded) not ending before fa
+            size_t si = (size_t)(std::upper_bound(h->bf_segs.begin(), h->bf_segs.end(), fa,
+                                                  [](size_t f, const fc2_caller::Seg &sg) { return f < sg.f0; }) -
+                                 h->bf_segs.begin());
+            if (si) --si;
+            for (size_t f = fa, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
+                while (si < h->bf_segs.size() && h->bf_segs[si].f0 + h->bf_segs[si].r.n <= f) ++si;
+                if (si < h->bf_segs.size() && h->bf_segs[si].f0 <= f) fill_from_seg(h->bf_segs[si], f, h->bf_frags[f]);
                 try {
                     process_frag(h, h->bf_frags[f], h->bf_recf, h->bf_prop, spans, arena, N);
                 } catch (const Fatal &x) {

@@ -358,13 +358,7 @@ struct fc2_ingest::SamAhead {
         bool eof = false;                       // the last block of the input
         // fragments the parse thread grouped on its own (group_batch): records [gs, gt) form whole
         // fragments (gs == gt: none); the handed ones are listed with the counts up to them
-        struct GFrag {
-            int32_t r0[2], n[2], p0[2], np[2];  // mate 0 = the other mate (n[0] == 0: none), 1 = current
-            uint32_t seq_len[2];                // len(SEQ) of each mate's primary
-            bool must;
-            fc2_ingest_counts cum;              // counts of the region through this fragment
-            uint64_t frags;                     // fragments closed in the region through this one
-        };
+        using GFrag = fc2::ing::GFrag;
         uint32_t gs = 0, gt = 0;
         std::vector<GFrag> gfrags;
         std::vector<int32_t> gidx;              // record positions and proper indices of gfrags' mates
@@ -1457,6 +1451,7 @@ void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b) {
     uint64_t F = 0;
     fc2_ingest_counts Ct{};
     uint64_t Ft = 0;
+    uint64_t span_cum = 0, arena_cum = 0;
     size_t t = s;
     auto open = [&](LM &m, size_t j) {
         C.total_mates++;
@@ -1514,6 +1509,13 @@ void group_batch(const fc2_ingest_params &p, fc2_ingest::SamAhead::Batch &b) {
             g.np[k] = (int32_t)ms[k]->p.size();
             b.gidx.insert(b.gidx.end(), ms[k]->p.begin(), ms[k]->p.end());
         }
+        for (int k = 0; k < 2; ++k)
+            if (g.np[k] >= 2) {
+                span_cum += (uint64_t)(g.np[k] - 1);
+                arena_cum += (uint64_t)(g.np[k] - 1) * g.seq_len[k];
+            }
+        g.span_cum = span_cum;
+        g.arena_cum = arena_cum;
         g.must = must;
         g.cum = C;
         g.frags = F;
@@ -1704,7 +1706,7 @@ extern "C" const char *fc2_ingest_header(const fc2_ingest *h) { return h ? h->he
 
 namespace {
 int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const fc2::ing::FragSink *sink,
-             uint64_t *n_handed, int *eof) {
+             uint64_t *n_handed, int *eof, const fc2::ing::BulkSink *bulk = nullptr) {
     uint64_t handed = 0, frags = 0;
     int rc = FC2_OK;
     bool done = h->finished;
@@ -1729,6 +1731,31 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
                 A.gapplied_frags = 0;
                 if (rc) return rc;
                 continue;
+            }
+            if (bulk && A.pin && A.gnext < b.gfrags.size() && frags < max_frags) {
+                // a run of the listed fragments at once: as many as the loop below would hand
+                // before `frags` reaches max_frags
+                const size_t g0 = A.gnext;
+                size_t k = g0 + 1;
+                while (k < b.gfrags.size() && frags + (b.gfrags[k - 1].frags - A.gapplied_frags) < max_frags) ++k;
+                const auto &g = b.gfrags[k - 1];
+                add_counts(h->counts, g.cum, A.gapplied);
+                h->n_records += g.cum.records - A.gapplied.records;
+                frags += g.frags - A.gapplied_frags;
+                A.gapplied = g.cum;
+                A.gapplied_frags = g.frags;
+                handed += k - g0;
+                A.grouped += k - g0;
+                A.gnext = k;
+                fc2::ing::RegionRef rr;
+                rr.recs = b.recs.data();
+                rr.g = b.gfrags.data() + g0;
+                rr.n = k - g0;
+                rr.gidx = b.gidx.data();
+                rr.span_before = g0 ? b.gfrags[g0 - 1].span_cum : 0;
+                rr.arena_before = g0 ? b.gfrags[g0 - 1].arena_cum : 0;
+                rc = (*bulk)(rr);
+                if (rc) return rc;
             }
             while (A.gnext < b.gfrags.size() && frags < max_frags) {
                 const auto &g = b.gfrags[A.gnext++];
@@ -1814,7 +1841,8 @@ int run_loop(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, cons
 }
 }  // namespace
 
-int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof) {
+int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof,
+                   const BulkSink *bulk) {
     if (!h || !p) return fc2::fail(FC2_E_PARAM, "ingest pull: null argument");
     if (h->need_text) h->need_text = false;     // (written once: the parse thread reads it)
     // plain SAM text and BAM (any compression): parsed on threads of their own; compressed SAM stays
@@ -1841,7 +1869,7 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
         ap->pin = h->pin;
         for (int k = 0; k < np; ++k) ap->parsers.emplace_back(sam_parse_loop, h, ap);
     }
-    return run_loop(h, p, max_frags, &sink, nullptr, eof);
+    return run_loop(h, p, max_frags, &sink, nullptr, eof, bulk);
 }
 
 bool fc2::ing::writes_records(const fc2_ingest *h) { return h && h->bam_out != nullptr; }

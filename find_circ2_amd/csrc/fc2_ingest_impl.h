@@ -119,6 +119,30 @@ struct MateRef {
     Rec &rec(size_t k) const { return base[idx ? idx[k] : k]; }
 };
 
+// A handed fragment a parse thread grouped on its own (group_batch): its mates' records by position
+// in the batch (gidx), the run.log counts and fragments closed up to it in the batch's region, and
+// the cumulative span / read-part room its spans need (for the caller's chunk offsets)
+struct GFrag {
+    int32_t r0[2], n[2], p0[2], np[2];  // mate 0 = the other mate (n[0] == 0: none), 1 = current
+    uint32_t seq_len[2];                // len(SEQ) of each mate's primary
+    bool must;
+    fc2_ingest_counts cum;              // counts of the region through this fragment
+    uint64_t frags;                     // fragments closed in the region through this one
+    uint64_t span_cum, arena_cum;       // sum over the batch's handed fragments through this one of
+                                        // (np - 1) and (np - 1) * seq_len per mate with np >= 2
+};
+
+// Consecutive handed fragments of one batch, stable until release() (set_pin): the bulk sink
+// records them without touching each fragment (the caller's workers read them later)
+struct RegionRef {
+    Rec *recs;
+    const GFrag *g;                     // g[0, n)
+    size_t n;
+    const int32_t *gidx;
+    uint64_t span_before, arena_before; // span_cum / arena_cum of the batch's handed fragment before g[0]
+};
+using BulkSink = std::function<int(const RegionRef &)>;
+
 // Fragments that carry anchor pairs (or that the reference would fail on: must_see) are passed
 // to the sink in input order; m1 = the other mate (may be null), m2 = the current mate.
 // The sink may take the mates' strings (swap them out): the loop reads nothing of a fragment's
@@ -126,8 +150,10 @@ struct MateRef {
 using FragSink = std::function<int(MateRef *m1, MateRef *m2, bool must_see)>;
 
 // The loop of fc2_ingest_next with a sink instead of SAM text; a non-zero return of the sink
-// stops the loop and is returned.
-int pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof);
+// stops the loop and is returned.  With `bulk` and pinning on, the fragments a parse thread grouped
+// go to `bulk` a run at a time, in input order with the sink's.
+int pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags, const FragSink &sink, int *eof,
+         const BulkSink *bulk = nullptr);
 
 // true when the ingest writes records while reading (-B, fc2_ingest_set_bam_out): the reference
 // stops writing at a failing fragment, so the caller must process each fragment as it comes
