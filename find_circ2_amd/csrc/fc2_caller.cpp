@@ -2301,7 +2301,7 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
         resolve_chroms(h);
         if (!h->pool) {
             const char *env = getenv("FC2_CALLER_THREADS");
-            int nt = env && atoi(env) > 0 ? atoi(env) : (int)std::min(8u, std::max(1u, std::thread::hardware_concurrency()));
+            int nt = env && atoi(env) > 0 ? atoi(env) : (int)std::min(12u, std::max(1u, std::thread::hardware_concurrency()));
             nt = std::max(1, std::min(nt, 64));
             h->pool.reset(new WorkPool(nt - 1));
         }
