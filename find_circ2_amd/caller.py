@@ -23,7 +23,7 @@ import time
 from collections import defaultdict
 from typing import Dict, List, Optional, Sequence
 
-from .hotpath import Splice
+from .hotpath import Splice, _py2_min, uniq_ok
 
 _COMP = {'a': 't', 't': 'a', 'c': 'g', 'g': 'c', 'k': 'm', 'm': 'k', 'r': 'y', 'y': 'r', 's': 's', 'w': 'w',
          'b': 'v', 'v': 'b', 'h': 'd', 'd': 'h', 'n': 'n', 'A': 'T', 'T': 'A', 'C': 'G', 'G': 'C', 'K': 'M',
@@ -183,7 +183,7 @@ class Span:
         self.weight = weight
         self.uniq_A = _uniqness(align_A)
         self.uniq_B = _uniqness(align_B)
-        self.uniq = min(self.uniq_A, self.uniq_B)
+        self.uniq = _py2_min(self.uniq_A, self.uniq_B)
         self.strand = '-' if primary.is_reverse else '+'
         self.dist = align_B.pos - align_A.aend
         self.read_part = primary.seq[q_start:q_end]
@@ -203,7 +203,7 @@ class Span:
         return self.result
 
 
-def _uniqness(align) -> int:                 # :809-819
+def _uniqness(align):                        # :809-819 (an int, a float, or a str / array AS as it is)
     u = align.get_tag('AS')
     if align.has_tag('XS'):
         u -= align.get_tag('XS')
@@ -535,7 +535,7 @@ class Caller:
         circ_coords = set()
         circ = None
         for span in frag.circ:
-            if not span.uniq >= o.min_uniq_qual:
+            if not uniq_ok(span.uniq, o.min_uniq_qual):
                 N['circ_junc_not_unique'] += 1
                 continue
             splices = span.find_breakpoints()
@@ -564,7 +564,7 @@ class Caller:
                 warns.add('SUPPORT_CLOSURE')
         lin_cons, lin_incons, lin_coords = set(), set(), set()
         for span in frag.lin:
-            if not span.uniq >= o.min_uniq_qual:
+            if not uniq_ok(span.uniq, o.min_uniq_qual):
                 N['lin_junc_not_unique'] += 1
                 continue
             splices = span.find_breakpoints()
@@ -626,7 +626,7 @@ class Caller:
         # is recorded (the reference stops at the fragment that raises, find_circ.py:1578-1583)
         frags = list(pending)
         pending.clear()
-        spans = [s for f in frags for s in f.circ + f.lin if s.uniq >= self.o.min_uniq_qual]
+        spans = [s for f in frags for s in f.circ + f.lin if uniq_ok(s.uniq, self.o.min_uniq_qual)]
         if spans:
             t0 = time.perf_counter()
             self.evaluate(spans)

@@ -36,6 +36,7 @@
 #include "fc2_ingest_impl.h"
 
 using fc2::ing::MateRef;
+using fc2::ing::PyNum;
 using fc2::ing::Rec;
 using fc2::ing::RecFields;
 
@@ -75,6 +76,29 @@ struct Fatal {                                 // an exception the reference rai
     int code;
     std::string msg;
 };
+
+// ---- Python 2 arithmetic on AS / XS tag values (find_circ.py:809-819, :556-566, :593) -------------
+const char *py_type(PyNum::Kind k) {
+    switch (k) {
+        case PyNum::INT: return "int";
+        case PyNum::FLOAT: return "float";
+        case PyNum::STR: return "str";
+        default: return "array.array";
+    }
+}
+
+// a - b as Python computes it: int - int an int, a float operand a float; false where Python raises
+// TypeError (a str or array operand)
+bool py_sub(const PyNum &a, const PyNum &b, PyNum &out) {
+    if (!a.number() || !b.number()) return false;
+    out = (a.k == PyNum::INT && b.k == PyNum::INT) ? PyNum::of_int(a.i - b.i) : PyNum::of_float(a.value() - b.value());
+    return true;
+}
+
+Fatal sub_error(const char *op, PyNum::Kind a, PyNum::Kind b) {
+    return Fatal{FC2_E_FORMAT, std::string("TypeError: unsupported operand type(s) for ") + op + ": '" + py_type(a) +
+                                   "' and '" + py_type(b) + "'"};
+}
 
 // find_circ.py:54-58 (KeyError outside the IUPAC table)
 char comp(char c) {
@@ -203,14 +227,23 @@ struct Span {                                  // JunctionSpan (:821-852)
     bool circ;                                 // is_backsplice: B.pos - A.aend < 0
     int64_t a_pos, b_aend;
     double weight;
-    int64_t uniq;
-    int64_t qA, qB;                            // Hit.add's anchor qualities (after the backsplice swap)
-    bool q_int;                                // both from integer last AS / XS tags (else Hit.add needs Python)
+    // JunctionSpan.uniq = min(uniq_A, uniq_B) (:829-831): its value when a number; a str / array
+    // (uniq_num false) orders above every number in Python 2, so `uniq >= min_uniq_qual` holds
+    double uniq;
+    bool uniq_num;
+    // Hit.add's anchor qualities (after the backsplice swap), numbers; q_bad: one of Hit.add's
+    // subtractions raises TypeError (a str / array last AS or XS), the first with operands q_bad_l, q_bad_r
+    bool q_bad;
+    PyNum::Kind q_bad_l, q_bad_r;
+    PyNum qA, qB;
     bool a_rev;                                // A.is_reverse after the swap
     uint64_t read_off;
     uint32_t read_len;
     int64_t eval = -1;                         // index in the evaluation batch
 };
+
+// `span.uniq >= options.min_uniq_qual` (:1299, :1351) with Python 2's ordering (nan compares false)
+inline bool uniq_ok(const Span &s, int64_t min_uniq_qual) { return !s.uniq_num || s.uniq >= (double)min_uniq_qual; }
 
 struct Frag {
     // what on_fragment writes, first and together (the chunk's Frags are written in order, and a
@@ -464,7 +497,7 @@ struct Hit {                                   // Hit (:486-654)
     StrSet readnames;
     CanonSet uniq;
     bool has_mq = false;
-    int64_t mq_a = 0, mq_b = 0;                // max of mapquals_A / _B
+    PyNum mq_a, mq_b;                          // sorted(mapquals_A / _B, reverse=True)[0] (:593): the first maximum
     double n_weighted = 0.;
     int64_t n_spanned = 0;
     double n_uniq_bridges = 0.;
@@ -812,17 +845,15 @@ void hit_add(fc2_caller *h, Hit &t, const Splice &sp) {
     t.edits.add(sp.dist, sp.dist_bool);
     t.overlaps.add(sp.ov, false);
     t.n_hits.add(sp.n_hits, false);
-    if (sp.span < 0) return;
-    const Span &s = h->spans[sp.span];
-    if (!s.q_int)        // a float / string last AS or XS: Python arithmetic (:558-566)
-        throw Fatal{FC2_E_FORMAT, "native caller: the last AS / XS tags of a junction's anchors must be integers "
-                                  "(use --python-caller)"};
-    t.n_spanned += 1;
-    t.n_weighted += s.weight;
-    if (s.qA && s.qB) t.n_uniq_bridges += s.weight;
-    if (!t.has_mq) { t.has_mq = true; t.mq_a = s.qA; t.mq_b = s.qB; }
-    else { t.mq_a = std::max(t.mq_a, s.qA); t.mq_b = std::max(t.mq_b, s.qB); }
-    return;
+    // only known sites come here (Splice(None, ...), :676): no junc_span, nothing more to add (:542)
+}
+
+// Hit.add's anchor-quality part (:558-566): qA / qB are numbers (check_add raised otherwise)
+void hit_quals(Hit &t, const Span &s) {
+    if (s.qA.value() != 0 && s.qB.value() != 0) t.n_uniq_bridges += s.weight;   // `if qA and qB` (nan is true)
+    if (!t.has_mq) { t.has_mq = true; t.mq_a = s.qA; t.mq_b = s.qB; return; }
+    if (s.qA.value() > t.mq_a.value()) t.mq_a = s.qA;      // the first of equal maxima stays (stable sort)
+    if (s.qB.value() > t.mq_b.value()) t.mq_b = s.qB;
 }
 
 void CanonSet::insert(const std::string &read, Arena &a) {
@@ -852,9 +883,7 @@ void hit_apply(const fc2_caller *h, Hit &t, const SEv &e) {
     const Span &s = h->spans[(size_t)e.span];
     t.n_spanned += 1;
     t.n_weighted += s.weight;
-    if (s.qA && s.qB) t.n_uniq_bridges += s.weight;
-    if (!t.has_mq) { t.has_mq = true; t.mq_a = s.qA; t.mq_b = s.qB; }
-    else { t.mq_a = std::max(t.mq_a, s.qA); t.mq_b = std::max(t.mq_b, s.qB); }
+    hit_quals(t, s);
 }
 
 // the span-dependent part of Hit.add that needs the fragment's primary (its read passed
@@ -894,7 +923,7 @@ int categories(const fc2_caller *h, const Hit &t, const char *cats[8]) {
     const auto &o = h->o;
     int n = 0;
     if (t.signal != "GTAG") cats[n++] = "NON_CANONICAL";
-    if (t.mq_a == 0 || t.mq_b == 0) cats[n++] = "WARN_NON_UNIQUE_ANCHOR";
+    if (t.mq_a.value() == 0 || t.mq_b.value() == 0) cats[n++] = "WARN_NON_UNIQUE_ANCHOR";
     if (t.n_uniq_bridges == 0) cats[n++] = "WARN_NO_UNIQ_BRIDGES";
     if (t.n_hits.v > 1) cats[n++] = "WARN_AMBIGUOUS_BP";
     const int64_t mov = t.overlaps.v, med = t.edits.v;
@@ -948,6 +977,11 @@ void app_py2_float(std::string &out, double v) {   // py2_float, integral values
     out += py2_float(v);
 }
 
+void app_pynum(std::string &out, const PyNum &v) {  // str() of an anchor quality: int or float
+    if (v.k == PyNum::FLOAT) app_py2_float(out, v.f);
+    else app_int(out, v.i);
+}
+
 void app_pymin(std::string &out, const PyMin &m) {
     if (m.is_bool) out += m.v ? "True" : "False";
     else app_int(out, m.v);
@@ -958,10 +992,10 @@ void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :69
     for (const JRef &j : h->order[kind]) {      // dict order
         const Hit &t = hit_at(h, kind, j);
         if (!t.n_reads) continue;
-        const int64_t qa = t.mq_a, qb = t.mq_b;
+        const double qa = t.mq_a.value(), qb = t.mq_b.value(), mq = (double)o.min_uniq_qual;
         if (o.halfunique) {
-            if (qa < o.min_uniq_qual && qb < o.min_uniq_qual) { incN(h, "anchor_not_uniq"); continue; }
-        } else if (qa < o.min_uniq_qual || qb < o.min_uniq_qual) {
+            if (qa < mq && qb < mq) { incN(h, "anchor_not_uniq"); continue; }
+        } else if (qa < mq || qb < mq) {
             incN(h, "anchor_not_uniq");
             continue;
         }
@@ -978,8 +1012,8 @@ void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :69
         app_int(outs, t.n_spanned); outs += tab;
         app_int(outs, t.uniq.size() / 2); outs += tab;
         app_py2_float(outs, t.n_uniq_bridges); outs += tab;
-        app_int(outs, qa); outs += tab;
-        app_int(outs, qb); outs += tab;
+        app_pynum(outs, t.mq_a); outs += tab;
+        app_pynum(outs, t.mq_b); outs += tab;
         if (t.has_tissue) outs += h->name;
         outs += tab;
         if (t.has_tissue) app_py2_float(outs, t.tissue);
@@ -1075,21 +1109,23 @@ std::string chrom_of(const fc2_caller *h, int32_t tid) {         // fast_chrom_l
     return nm;
 }
 
-int64_t uniqness(const RecFields &a) {                                  // :809-819
+PyNum uniqness(const RecFields &a) {                                    // :809-819
     if (!a.has_as) throw Fatal{FC2_E_KEY, "KeyError: \"tag 'AS' not present\""};
-    if (!a.as_int || (a.has_xs && !a.xs_int))
-        throw Fatal{FC2_E_FORMAT, "native caller: AS / XS tags must be integers (use --python-caller)"};
-    return a.as - (a.has_xs ? a.xs : 0);
+    if (!a.has_xs) return a.as;                                         // a str / array AS stays as it is
+    PyNum u;
+    if (!py_sub(a.as, a.xs, u)) throw sub_error("-=", a.as.k, a.xs.k);  // u -= get_tag('XS')
+    return u;
 }
 
-// Hit.add's anchor quality (find_circ.py:556-559): dict(tags) keeps the LAST AS / XS of a record.
-// Only Hit.add reads it, so a non-integer last tag matters only for a span that reaches a Hit
-// (hit_add raises there); false when it is not an integer
-bool dict_quality(const RecFields &a, int64_t &q) {
-    q = 0;
-    if (!a.as_last_int || (a.has_xs && !a.xs_last_int)) return false;
-    q = a.as_last - (a.has_xs ? a.xs_last : 0);
-    return true;
+// Hit.add's anchor quality (find_circ.py:556-559): dict(tags) keeps the LAST AS / XS of a record,
+// and get('XS', 0) defaults to the int 0.  Only Hit.add reads it, so a non-number matters only for a
+// span that reaches a Hit (check_add raises there); false, with the operands' kinds, when the
+// subtraction raises
+bool dict_quality(const RecFields &a, PyNum &q, PyNum::Kind &l, PyNum::Kind &r) {
+    const PyNum xs = a.has_xs ? a.xs_last : PyNum::of_int(0);
+    l = a.as_last.k;
+    r = xs.k;
+    return py_sub(a.as_last, xs, q);
 }
 
 const char *kNoneLen = "TypeError: object of type 'NoneType' has no len()";
@@ -1146,16 +1182,25 @@ void process_mate(const fc2_caller *h, const RecsView &recs, size_t nrec, const 
         Span s;
         s.mate = mi;
         s.tid = A.tid;
-        const int64_t ua = uniqness(A), ub = uniqness(B);
+        const PyNum ua = uniqness(A), ub = uniqness(B);
         if (A.aend < 0) throw Fatal{FC2_E_FORMAT, "TypeError: unsupported operand type(s) for -: 'int' and 'NoneType'"};
         s.circ = B.pos - A.aend < 0;
         s.a_pos = A.pos;
         s.b_aend = B.aend;
         s.weight = weight;
-        s.uniq = std::min(ua, ub);
-        int64_t qa, qb;
-        const bool qa_int = dict_quality(A, qa), qb_int = dict_quality(B, qb);   // both computed, as both set
-        s.q_int = qa_int && qb_int;
+        // min(uniq_A, uniq_B) in Python 2: numbers by value (ub only if strictly smaller), a number
+        // before a str / array; two non-numbers give a non-number
+        if (ua.number() && ub.number()) s.uniq = ub.value() < ua.value() ? ub.value() : ua.value();
+        else s.uniq = ua.number() ? ua.value() : ub.value();
+        s.uniq_num = ua.number() || ub.number();
+        PyNum qa, qb;
+        PyNum::Kind la, ra, lb, rb;
+        const bool qa_ok = dict_quality(A, qa, la, ra), qb_ok = dict_quality(B, qb, lb, rb);
+        // after Hit.add's swap (backsplice: A, B = B, A) qA comes first: its failure is the one raised
+        const bool first_ok = s.circ ? qb_ok : qa_ok, second_ok = s.circ ? qa_ok : qb_ok;
+        s.q_bad = !(first_ok && second_ok);
+        s.q_bad_l = !first_ok ? (s.circ ? lb : la) : (s.circ ? la : lb);
+        s.q_bad_r = !first_ok ? (s.circ ? rb : ra) : (s.circ ? ra : rb);
         s.qA = s.circ ? qb : qa;
         s.qB = s.circ ? qa : qb;
         s.a_rev = s.circ ? (B.flag & 0x10) != 0 : (A.flag & 0x10) != 0;
@@ -1644,9 +1689,8 @@ void phase_a_frag(const fc2_caller *h, uint32_t fi, const Frag &fr, const Result
     auto store = [&](int kind, const Splice &sp, const Span &span) -> KeySlot {
         if (o.stranded)   // Splice has no strandmatch attribute (:532-533)
             throw Fatal{FC2_E_FORMAT, "AttributeError: 'Splice' object has no attribute 'strandmatch'"};
-        if (!span.q_int)  // a float / string last AS or XS: Python arithmetic (:558-566)
-            throw Fatal{FC2_E_FORMAT, "native caller: the last AS / XS tags of a junction's anchors must be integers "
-                                      "(use --python-caller)"};
+        if (span.q_bad)   // qA / qB = AS - XS of a str / array tag (:558-559)
+            throw sub_error("-", span.q_bad_l, span.q_bad_r);
         if (!F.comp_ok[span.mate]) {            // rev_comp(read) raises here (:573, :582); once per mate
             check_comp(fr.prim[span.mate].seq);
             F.comp_ok[span.mate] = true;
@@ -1694,7 +1738,7 @@ void phase_a_frag(const fc2_caller *h, uint32_t fi, const Frag &fr, const Result
     KeySlot circ{0, CKey{}, 0};
     for (int si : fr.circ) {
         const Span &span = h->spans[si];
-        if (!(span.uniq >= o.min_uniq_qual)) { count("circ_junc_not_unique"); continue; }
+        if (!uniq_ok(span, o.min_uniq_qual)) { count("circ_junc_not_unique"); continue; }
         const std::vector<Splice> &splices = find_breakpoints(h, si, R, F);
         if (splices.empty()) {
             count("circ_no_bp");
@@ -1730,7 +1774,7 @@ void phase_a_frag(const fc2_caller *h, uint32_t fi, const Frag &fr, const Result
     std::set<Coord> lin_cons, lin_incons;
     for (int si : fr.lin) {
         const Span &span = h->spans[si];
-        if (!(span.uniq >= o.min_uniq_qual)) { count("lin_junc_not_unique"); continue; }
+        if (!uniq_ok(span, o.min_uniq_qual)) { count("lin_junc_not_unique"); continue; }
         const std::vector<Splice> &splices = find_breakpoints(h, si, R, F);
         if (splices.empty()) {
             count("lin_no_bp");
@@ -2189,7 +2233,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         std::vector<uint64_t> cnt(T + 1, 0);
         std::vector<uint8_t> bad_len(T, 0);
         const int64_t min_uq = h->o.min_uniq_qual;
-        auto eligible = [&](const Span &sp) { return sp.uniq >= min_uq; };
+        auto eligible = [&](const Span &sp) { return uniq_ok(sp, min_uq); };
         h->next_pool->run((int)T, [&](int r) {
             fc2::cpu::Scope acct(fc2::cpu::NEXT_POOL);
             uint64_t n = 0;

@@ -553,20 +553,26 @@ int64_t to_i64(const char *b, const char *e) {
     return strtoll(std::string(b, e).c_str(), nullptr, 10);
 }
 
+// a SAM text tag value of type ty in [b, e) as pysam returns it: 'i' an int, 'f' the float32 htslib
+// stores (strtod, then narrowed), 'B' an array, anything else a str
+fc2::ing::PyNum tag_num(char ty, const char *b, const char *e) {
+    using fc2::ing::PyNum;
+    if (ty == 'i') return PyNum::of_int(to_i64(b, e));
+    if (ty == 'f') return PyNum::of_float((double)(float)strtod(std::string(b, e).c_str(), nullptr));
+    return PyNum::other(ty == 'B' ? PyNum::ARRAY : PyNum::STR);
+}
+
 // AS / XS of one tag in SAM text form "TG:T:value" (first occurrence wins, like get_tag)
 void note_tag(Rec &r, const char *t, const char *e) {
     if (e - t < 5 || t[2] != ':' || t[4] != ':') return;
     const bool as = t[0] == 'A' && t[1] == 'S', xs = t[0] == 'X' && t[1] == 'S';
     if (!as && !xs) return;
-    const bool isint = t[3] == 'i';
-    const int64_t v = isint ? to_i64(t + 5, e) : 0;
+    const fc2::ing::PyNum v = tag_num(t[3], t + 5, e);
     if (as) {
-        if (!r.has_as) { r.has_as = true; r.as_int = isint; r.as = v; }
-        r.as_last_int = isint;
+        if (!r.has_as) { r.has_as = true; r.as = v; }
         r.as_last = v;
     } else {
-        if (!r.has_xs) { r.has_xs = true; r.xs_int = isint; r.xs = v; }
-        r.xs_last_int = isint;
+        if (!r.has_xs) { r.has_xs = true; r.xs = v; }
         r.xs_last = v;
     }
 }
@@ -652,10 +658,7 @@ int parse_sam_record(fc2_ingest *h, const char *ls, const char *le, Rec &r, fc2_
         r.qual.assign(qb, qe);
     }
     r.has_as = r.has_xs = false;
-    r.as_int = r.xs_int = true;
-    r.as = r.xs = 0;
-    r.as_last_int = r.xs_last_int = true;
-    r.as_last = r.xs_last = 0;
+    r.as = r.xs = r.as_last = r.xs_last = fc2::ing::PyNum();
     finish_rec(r, ops, r.has_seq ? (int64_t)r.seq_n : 0);
     if (nf == 12) {                                 // tags: [tabs[k] + 1, next tab or line end), k >= 10
         const int last = nt == kMaxTabs ? nt - 1 : nt;
@@ -713,7 +716,8 @@ void append_bam_tags(std::string &t, const uint8_t *p, const uint8_t *end) {
             case 'S': { uint16_t v; memcpy(&v, p, 2); ival(v); break; }
             case 'i': { int32_t v; memcpy(&v, p, 4); ival(v); break; }
             case 'I': { uint32_t v; memcpy(&v, p, 4); ival(v); break; }
-            case 'f': { float v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, ":f:%g", v); t += tmp; break; }
+            // nine significant digits: the Python loop parses back the very float32 (samio._tag_value)
+            case 'f': { float v; memcpy(&v, p, 4); snprintf(tmp, sizeof tmp, ":f:%.9g", v); t += tmp; break; }
             case 'A': t += ":A:"; t += (char)*p; break;
             case 'Z': case 'H':
                 t += ':'; t += ty; t += ':';
@@ -744,31 +748,35 @@ void append_bam_tags(std::string &t, const uint8_t *p, const uint8_t *end) {
     }
 }
 
-// AS / XS from binary BAM tags (integer types as ints, anything else marked non-int); false when
-// the aux data is corrupt (aux_value_size) or ends inside a tag
+// AS / XS from binary BAM tags, as pysam's get_tag returns them (fc2::ing::PyNum); false when the
+// aux data is corrupt (aux_value_size) or ends inside a tag
 bool scan_bam_tags(Rec &r, const uint8_t *p, const uint8_t *end) {
+    using fc2::ing::PyNum;
     while (p < end) {
         if (end - p < 3) return false;
         const char t0 = (char)p[0], t1 = (char)p[1], ty = (char)p[2];
         p += 3;
         const ptrdiff_t adv = aux_value_size(ty, p, end);
         if (adv < 0) return false;
-        int64_t v = 0;
-        bool isint = true;
-        switch (ty) {
-            case 'c': v = *(const int8_t *)p; break;
-            case 'C': v = *(const uint8_t *)p; break;
-            case 's': { int16_t x; memcpy(&x, p, 2); v = x; break; }
-            case 'S': { uint16_t x; memcpy(&x, p, 2); v = x; break; }
-            case 'i': { int32_t x; memcpy(&x, p, 4); v = x; break; }
-            case 'I': { uint32_t x; memcpy(&x, p, 4); v = x; break; }
-            default: isint = false; break;
-        }
         const bool as = t0 == 'A' && t1 == 'S', xs = t0 == 'X' && t1 == 'S';
-        if (as && !r.has_as) { r.has_as = true; r.as_int = isint; r.as = v; }
-        if (xs && !r.has_xs) { r.has_xs = true; r.xs_int = isint; r.xs = v; }
-        if (as) { r.as_last_int = isint; r.as_last = v; }
-        if (xs) { r.xs_last_int = isint; r.xs_last = v; }
+        if (as || xs) {
+            PyNum v;
+            switch (ty) {
+                case 'c': v = PyNum::of_int(*(const int8_t *)p); break;
+                case 'C': v = PyNum::of_int(*(const uint8_t *)p); break;
+                case 's': { int16_t x; memcpy(&x, p, 2); v = PyNum::of_int(x); break; }
+                case 'S': { uint16_t x; memcpy(&x, p, 2); v = PyNum::of_int(x); break; }
+                case 'i': { int32_t x; memcpy(&x, p, 4); v = PyNum::of_int(x); break; }
+                case 'I': { uint32_t x; memcpy(&x, p, 4); v = PyNum::of_int(x); break; }
+                case 'f': { float x; memcpy(&x, p, 4); v = PyNum::of_float(x); break; }
+                case 'B': v = PyNum::other(PyNum::ARRAY); break;
+                default: v = PyNum::other(PyNum::STR); break;          // A Z H
+            }
+            if (as && !r.has_as) { r.has_as = true; r.as = v; }
+            if (xs && !r.has_xs) { r.has_xs = true; r.xs = v; }
+            if (as) r.as_last = v;
+            if (xs) r.xs_last = v;
+        }
         p += adv;
     }
     return true;
@@ -817,10 +825,7 @@ int parse_bam_body(const fc2_ingest *h, const uint8_t *b, int32_t bs, Rec &r,
     r.pos = pos;
     finish_rec(r, ops, l_seq);
     r.has_as = r.has_xs = false;
-    r.as_int = r.xs_int = true;
-    r.as = r.xs = 0;
-    r.as_last_int = r.xs_last_int = true;
-    r.as_last = r.xs_last = 0;
+    r.as = r.xs = r.as_last = r.xs_last = fc2::ing::PyNum();
     if (!scan_bam_tags(r, p, e)) return fc2::fail(FC2_E_FORMAT, "corrupted aux data in a BAM record");
     if (!need_text) return FC2_OK;
     const std::string &seq = r.seq, &qual = r.qual;
@@ -1327,9 +1332,10 @@ MateEval eval_mate(const MateRef &m, int asize) {
         const Rec &a = m.rec((size_t)segs[k]), &b = m.rec((size_t)segs[k + 1]);
         if (a.qlen < asize || b.qlen < asize) { ev.too_short++; continue; }
         // JunctionSpan.__init__ raises on these whether or not the span is ever evaluated
-        // (uniqness: AS missing or not an integer, :809-819): the caller must see the fragment
-        // even under --no-linear
-        if (!a.has_as || !b.has_as || !a.as_int || !b.as_int || (a.has_xs && !a.xs_int) || (b.has_xs && !b.xs_int)) {
+        // (uniqness: AS missing, or a str / array AS or XS, :809-819): the caller must see the
+        // fragment even under --no-linear
+        if (!a.has_as || !b.has_as || !a.as.number() || !b.as.number() || (a.has_xs && !a.xs.number()) ||
+            (b.has_xs && !b.xs.number())) {
             ev.python_must_see = true;
             return ev;
         }

@@ -14,6 +14,26 @@
 namespace fc2 {
 namespace ing {
 
+// A tag value as pysam's get_tag returns it and Python 2 computes with it (find_circ.py:809-819,
+// :556-566): an int for the integer types c C s S i I, a float for 'f' (the stored float32, widened
+// to a double as pysam does; SAM text is rounded to float32 as htslib stores it), a str for A Z H,
+// an array for B.  Only numbers take part in arithmetic; the caller raises Python's TypeError where
+// the reference would subtract a non-number.
+struct PyNum {
+    enum Kind : uint8_t { INT = 0, FLOAT = 1, STR = 2, ARRAY = 3 };
+    union {
+        int64_t i;
+        double f;
+    };
+    Kind k;
+    PyNum() : i(0), k(INT) {}
+    static PyNum of_int(int64_t v) { PyNum n; n.i = v; return n; }
+    static PyNum of_float(double v) { PyNum n; n.f = v; n.k = FLOAT; return n; }
+    static PyNum other(Kind kind) { PyNum n; n.k = kind; return n; }
+    bool number() const { return k == INT || k == FLOAT; }
+    double value() const { return k == FLOAT ? f : (double)i; }   // exact for |int| < 2^53 (tag ints are 32-bit)
+};
+
 // the plain fields of a record (swapped as one block, see swap(Rec &, Rec &))
 struct RecFields {
     uint32_t flag = 0;
@@ -24,12 +44,11 @@ struct RecFields {
     int32_t qlen = -1;     // len(query); -1: query is None (SEQ '*')
     bool has_seq = false;  // SEQ / QUAL "*" -> false
     bool has_qual = false;
-    // AS / XS tags as pysam's get_tag returns them: present?, integer-typed?, value
-    bool has_as = false, has_xs = false, as_int = true, xs_int = true;
-    int64_t as = 0, xs = 0;
+    // AS / XS tags as pysam's get_tag returns them (the first occurrence): present?, value
+    bool has_as = false, has_xs = false;
+    PyNum as, xs;
     // the LAST occurrence of each, as dict(read.tags) gives it (Hit.add, find_circ.py:556-557)
-    bool as_last_int = true, xs_last_int = true;
-    int64_t as_last = 0, xs_last = 0;
+    PyNum as_last, xs_last;
 };
 
 // SEQ / QUAL a parse thread left where they are in the record's parse block (which stays until

@@ -759,12 +759,32 @@ def _window_gtag(genome: Genome, hp, i, x, e, l) -> str:
 # ---------------------------------------------------------------------------
 # drop-in mirror of the reference objects
 # ---------------------------------------------------------------------------
-def uniqness(align) -> int:
-    """AS - XS (find_circ.py:809-819)."""
+def uniqness(align):
+    """AS - XS (find_circ.py:809-819): an int, a float, or a str / array AS as it is."""
     u = align.get_tag('AS')
     if align.has_tag('XS'):
         u -= align.get_tag('XS')
     return u
+
+
+def _is_number(v) -> bool:
+    return isinstance(v, (int, float)) and not isinstance(v, bool)
+
+
+def _py2_min(a, b):
+    """min(a, b) with Python 2's ordering of mixed types: numbers by value (b only if strictly
+    smaller, as the builtin), any number before a non-number (a str or array tag value)."""
+    if _is_number(a) and _is_number(b):
+        return b if b < a else a
+    if _is_number(b):
+        return b
+    return a
+
+
+def uniq_ok(uniq, min_uniq_qual: int) -> bool:
+    """``uniq >= options.min_uniq_qual`` (find_circ.py:1299, :1351) under Python 2: a non-number
+    (str / array) orders above every int."""
+    return uniq >= min_uniq_qual if _is_number(uniq) else True
 
 
 class JunctionSpan:
@@ -786,7 +806,7 @@ class JunctionSpan:
         self.weight = weight
         self.uniq_A = uniqness(align_A)
         self.uniq_B = uniqness(align_B)
-        self.uniq = min(self.uniq_A, self.uniq_B)
+        self.uniq = _py2_min(self.uniq_A, self.uniq_B)
         self.strand = '-' if primary.is_reverse else '+'
         self.dist = align_B.pos - align_A.aend
         self.read_part = primary.seq[q_start:q_end]
@@ -795,11 +815,11 @@ class JunctionSpan:
     min_uniq_qual = 2   # options.min_uniq_qual (find_circ.py:393), read by is_uniq like the reference
 
     def is_uniq_for(self, min_uniq_qual: int) -> bool:        # find_circ.py:846-848
-        return self.uniq >= min_uniq_qual
+        return uniq_ok(self.uniq, min_uniq_qual)
 
     @property
     def is_uniq(self) -> bool:                                # find_circ.py:846-848
-        return self.uniq >= self.min_uniq_qual
+        return uniq_ok(self.uniq, self.min_uniq_qual)
 
     @property
     def is_backsplice(self):                                  # find_circ.py:850-852

@@ -13,6 +13,7 @@ exposes it:
 """
 from __future__ import annotations
 
+import array
 import gzip
 import io
 import re
@@ -118,15 +119,28 @@ def parse_sam_line(line: str, tid_of: Dict[str, int]) -> AlignedSegment:
                           None if f[9] == "*" else f[9], None if f[10] == "*" else f[10], tags)
 
 
+def _float32(v: float) -> float:
+    """The float32 htslib stores for a 'f' value (pysam hands it back widened to a double)."""
+    try:
+        return struct.unpack("<f", struct.pack("<f", v))[0]
+    except OverflowError:     # C's narrowing of an out-of-range double
+        return float("inf") if v > 0 else float("-inf")
+
+
+_B_CODES = {"c": "b", "C": "B", "s": "h", "S": "H", "i": "i", "I": "I", "f": "f"}
+
+
 def _tag_value(typ: str, val: str):
+    """A SAM text tag value as pysam's get_tag returns it: 'i' an int, 'f' a float (rounded to the
+    float32 htslib keeps), 'B' an array.array, anything else (A, Z, H) a str."""
     if typ == "i":
         return int(val)
     if typ == "f":
-        return float(val)
+        return _float32(float(val))
     if typ == "B":
         parts = val.split(",")
         conv = float if parts[0] == "f" else int
-        return [conv(x) for x in parts[1:]]
+        return array.array(_B_CODES.get(parts[0], "i"), [conv(x) for x in parts[1:]])
     return val            # Z, A, H
 
 
@@ -342,8 +356,8 @@ class AlignmentFile:
             elif typ == "B":
                 sub = chr(buf[o])
                 cnt, = struct.unpack_from("<i", buf, o + 1)
-                fmt = {"c": "b", "C": "B", "s": "h", "S": "H", "i": "i", "I": "I", "f": "f"}[sub]
-                v = list(struct.unpack_from("<%d%s" % (cnt, fmt), buf, o + 5))
+                fmt = _B_CODES[sub]
+                v = array.array(fmt, struct.unpack_from("<%d%s" % (cnt, fmt), buf, o + 5))
                 o += 5 + cnt * struct.calcsize(fmt)
             else:
                 raise ValueError("bad BAM tag type %r" % typ)
@@ -392,7 +406,10 @@ def sam_line(rec: AlignedSegment, references: List[str]) -> str:
         if isinstance(v, int):
             tags.append("%s:i:%d" % (t, v))
         elif isinstance(v, float):
-            tags.append("%s:f:%g" % (t, v))
+            tags.append("%s:f:%.9g" % (t, v))
+        elif isinstance(v, array.array):
+            sub = {c: k for k, c in _B_CODES.items()}[v.typecode]
+            tags.append("%s:B:%s" % (t, ",".join([sub] + ["%.9g" % x if sub == "f" else "%d" % x for x in v])))
         else:
             tags.append("%s:Z:%s" % (t, v))
     return "\t".join([rec.qname, str(rec.flag), references[rec.tid] if rec.tid >= 0 else "*", str(rec.pos + 1),

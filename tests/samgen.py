@@ -107,6 +107,15 @@ def sam_to_bam(sam: str, path: str, bgzf: bool = True, compress: str = ""):
             tg, typ, val = t.split(":", 2)
             if typ == "i":
                 aux += tg.encode() + b"i" + struct.pack("<i", int(val))
+            elif typ == "f":                                # float32, as htslib stores a SAM 'f' value
+                aux += tg.encode() + b"f" + struct.pack("<f", float(val))
+            elif typ == "A":
+                aux += tg.encode() + b"A" + val.encode()[:1]
+            elif typ == "B":
+                sub, *vals = val.split(",")
+                fmt = {"c": "b", "C": "B", "s": "h", "S": "H", "i": "i", "I": "I", "f": "f"}[sub]
+                aux += tg.encode() + b"B" + sub.encode() + struct.pack("<i%d%s" % (len(vals), fmt), len(vals),
+                                                                      *[(float if sub == "f" else int)(v) for v in vals])
             else:
                 aux += tg.encode() + b"Z" + val.encode() + b"\0"
         body = struct.pack("<iiBBHHHiiii", tid.get(f[2], -1), int(f[3]) - 1, len(qn), int(f[4]), 0, len(cig),

@@ -18,7 +18,8 @@ import pytest
 from conftest import GOLDEN
 from find_circ2_amd import cli
 from oracle_engine import oracle_evaluator_factory
-from samgen import sam_to_bam
+from bwa_emul import read_fasta
+from samgen import sam_text, sam_to_bam
 from test_cli import _reads, run_cli
 from test_ingest import _mixed_sam, counters, same
 
@@ -504,43 +505,123 @@ def test_native_reads_gz_unwritable_path(tmp_path):
         nc.close()
 
 
-def test_native_caller_float_last_as_only_matters_in_hit_add(tmp_path):
-    """A non-integer LAST AS tag (after an integer first one) is read only by Hit.add
-    (dict(tags), find_circ.py:556-559): on spans that never reach a Hit the native loop completes
-    with the Python loop's files; on a span that does, it stops with a pointer to --python-caller
-    (the float arithmetic of best_qual_* is left to the Python loop)."""
-    import gzip
-    sam0 = str(tmp_path / "base.sam")
-    fa = _rich_sam(sam0, 300, seed=5150)
-    o0 = str(tmp_path / "base_out")
-    assert cli.main(["-G", fa, "-o", o0, "-q", "--python-caller", sam0], evaluator_factory=oracle_evaluator_factory) == 0
-    with gzip.open(os.path.join(o0, "spliced_reads.fastq.gz"), "rt") as fh:
-        hit_reads = {l[1:].split()[0] for l in fh.read().splitlines()[::4]}
-    lines = open(sam0).read().splitlines()
-    qnames = [l.split("\t")[0] for l in lines if not l.startswith("@")]
-    spliced = {q for q in qnames if qnames.count(q) > 1} - hit_reads
-    assert hit_reads and spliced
-
-    def with_float_as(targets):
-        out = []
-        for l in lines:
-            f = l.split("\t")
-            if not l.startswith("@") and f[0] in targets and any(t.startswith("AS:i:") for t in f[11:]):
-                l += "\tAS:f:7.5"
+def _retag(lines, rng, rewrite):
+    """The SAM lines with each record's tag fields (after the 11 mandatory ones) passed through
+    rewrite(tags, rng) -> tags."""
+    out = []
+    for l in lines:
+        if l.startswith("@"):
             out.append(l)
-        p = str(tmp_path / ("f%d.sam" % len(targets)))
-        open(p, "w").write("\n".join(out) + "\n")
-        return p
+            continue
+        f = l.split("\t")
+        out.append("\t".join(f[:11] + rewrite(f[11:], rng)))
+    return out
 
-    sam = with_float_as(spliced)
-    o1, o2 = str(tmp_path / "py"), str(tmp_path / "nat")
-    assert cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory) == 0
-    assert cli.main(["-G", fa, "-o", o2, "-q", sam], evaluator_factory=oracle_evaluator_factory) == 0
-    same(o1, o2)
-    sam = with_float_as({sorted(hit_reads)[0]})
-    o3 = str(tmp_path / "nat_hit")
-    assert cli.main(["-G", fa, "-o", o3, "-q", sam], evaluator_factory=oracle_evaluator_factory) == 1
-    assert "--python-caller" in open(os.path.join(o3, "run.log")).read()
+
+def _float_tags(tags, rng):
+    """AS / XS of one record as floats in the ways an aligner may write them: an integral float, a
+    value float32 cannot hold exactly (pysam hands back the float32), an extra float XS, an integer
+    AS with a float XS, and a later float AS that only dict(tags) sees (find_circ.py:556-559)."""
+    r = rng.random()
+    asv = [t for t in tags if t.startswith("AS:i:")]
+    if not asv:
+        return tags
+    a = int(asv[0][5:])
+    if r < 0.2:
+        return [("AS:f:%d.0" % a) if t.startswith("AS:i:") else t for t in tags]
+    if r < 0.4:
+        return [("AS:f:%.1f" % (a - 0.9)) if t.startswith("AS:i:") else t for t in tags]
+    if r < 0.55:
+        return [t for t in tags if not t.startswith("XS:")] + ["XS:f:%.2f" % (a - 2.5 + rng.random())]
+    if r < 0.65:
+        return tags + ["AS:f:%.3f" % (rng.random() * 3)]
+    if r < 0.75:
+        return [("XS:f:%.1f" % (float(t[5:]) + 0.5)) if t.startswith("XS:i:") else t for t in tags]
+    return tags
+
+
+@pytest.mark.parametrize("extra", [[], ["--half-unique", "--min-uniq-qual", "1"], ["--all-hits", "--non-canonical"]],
+                         ids=["default", "half-unique", "all-hits"])
+def test_native_caller_float_as_xs(tmp_path, extra):
+    """Float AS / XS tags (type 'f'): JunctionSpan.uniq (:809-831), Hit.add's qA / qB, the uniqueness
+    of bridges and best_qual_left/right (:556-566, :593, :704-713) follow Python's mixed int / float
+    arithmetic and Python 2's str(float) in all three read loops, from SAM and from BAM."""
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, 800, seed=5150)
+    rng = np.random.default_rng(77)
+    sam = str(tmp_path / "float.sam")
+    open(sam, "w").write("\n".join(_retag(open(sam0).read().splitlines(), rng, _float_tags)) + "\n")
+    bam = str(tmp_path / "float.bam")
+    sam_to_bam(open(sam).read(), bam)
+    rcs, outs = _three(tmp_path, fa, sam, extra)
+    assert rcs == [0, 0, 0]
+    same(outs[0], outs[1])
+    same(outs[0], outs[2])
+    rows = open(os.path.join(outs[2], "circ_splice_sites.bed")).read().splitlines()[1:]
+    quals = [c for r in rows for c in r.split("\t")[10:12]]
+    assert any("." in q for q in quals) and any(q.endswith(".0") for q in quals), quals[:20]
+    o_bam = str(tmp_path / "nat_bam")
+    assert cli.main(["-G", fa, "-o", o_bam, "-n", "mix", "-q"] + extra + [bam], evaluator_factory=oracle_evaluator_factory) == 0
+    same(outs[0], o_bam)
+
+
+def test_float32_rounding_of_sam_tags(tmp_path):
+    """A SAM 'f' value is kept as the float32 htslib stores (pysam returns it widened): AS:f:30.1
+    prints as Python 2's str() of float32(30.1) = 30.1000003815 in best_qual_left."""
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    rd = _reads(os.path.join(GOLDEN, "test_reads.fa"))
+    _, o0 = run_cli(tmp_path, fa, rd, extra=[], tag="base")
+    base = open(os.path.join(o0, "circ_splice_sites.bed")).read().splitlines()
+    assert len(base) > 1
+    lines = sam_text(read_fasta(fa), rd).splitlines()        # the SAM run_cli feeds the CLI
+    sam = str(tmp_path / "f.sam")
+    open(sam, "w").write("\n".join(_retag(lines, None, lambda t, _: [("AS:f:30.1" if x.startswith("AS:") else x)
+                                                                      for x in t])) + "\n")
+    outs = []
+    for tag, mode in (("py", ["--python-ingest"]), ("nat", [])):
+        o = str(tmp_path / tag)
+        assert cli.main(["-G", fa, "-o", o, "-q"] + mode + [sam], evaluator_factory=oracle_evaluator_factory) == 0
+        outs.append(o)
+    same(*outs)
+    rows = open(os.path.join(outs[1], "circ_splice_sites.bed")).read().splitlines()[1:]
+    assert rows and all(r.split("\t")[10] == "30.1000003815" for r in rows), rows
+
+
+@pytest.mark.parametrize("case", ["str_as_with_xs", "str_last_as_in_hit", "str_as_no_xs", "array_xs"])
+def test_native_caller_non_numeric_as_xs(tmp_path, case):
+    """A str (A / Z / H) or array (B) AS / XS: Python raises TypeError where it subtracts one
+    (uniqness, :816-817; Hit.add, :558-559) and orders a non-number above every int (min() at :831
+    and `uniq >= min_uniq_qual` at :1299, :1351) -- the three read loops agree on the outcome."""
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, 300, seed=5151)
+    rng = np.random.default_rng(3)
+
+    def rewrite(tags, rng):
+        if case == "str_as_with_xs":       # AS:Z - XS -> TypeError in JunctionSpan.__init__
+            return [("AS:Z:x%s" % t[5:]) if t.startswith("AS:i:") and any(u.startswith("XS:") for u in tags)
+                    and rng.random() < 0.02 else t for t in tags]
+        if case == "str_last_as_in_hit":   # a later AS:Z: only dict(tags) in Hit.add sees it
+            return tags + ["AS:Z:late"] if rng.random() < 0.02 else tags
+        if case == "str_as_no_xs":         # AS:A without XS: uniq is a str, which passes uniqueness
+            return [("AS:A:q" if t.startswith("AS:i:") else t) for t in tags if not t.startswith("XS:")] \
+                if rng.random() < 0.3 else tags
+        return [("XS:B:i,1,2" if t.startswith("XS:i:") else t) for t in tags] if rng.random() < 0.02 else tags
+
+    sam = str(tmp_path / "t.sam")
+    open(sam, "w").write("\n".join(_retag(open(sam0).read().splitlines(), rng, rewrite)) + "\n")
+    rcs, outs = _three(tmp_path, fa, sam, [])
+    assert rcs[0] == rcs[1] == rcs[2], rcs
+    if case == "str_as_no_xs":
+        assert rcs[2] in (0, 1)
+    else:
+        assert rcs[2] == 1
+    if rcs[2] == 0:
+        same(outs[0], outs[1])
+        same(outs[0], outs[2])
+    else:
+        logs = [open(os.path.join(o, "run.log")).read() for o in outs]
+        assert all("TypeError: unsupported operand type(s) for -" in g for g in logs), logs[2][-500:]
+        assert logs[1].splitlines()[-1].split("\t")[-1] == logs[2].splitlines()[-1].split("\t")[-1]
 
 
 @pytest.mark.parametrize("width", [4, 2])
