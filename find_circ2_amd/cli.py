@@ -169,15 +169,21 @@ def main(argv=None, evaluator_factory=None) -> int:
     logger.info('reading from {0}'.format(args[0]) if args else 'reading from stdin')
     if not (options.python_ingest or options.python_caller):
         return _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path)
-    if options.python_ingest:
-        sam = AlignmentFile(path, "rb" if is_bam else "r")
-        run = lambda: caller.run(sam)                              # noqa: E731
-    else:
-        from .ingest import NativeIngest
-        sam = NativeIngest(path, is_bam)
-        if bam_path:
-            sam.set_bam_out(bam_path)
-        run = lambda: caller.run_native(sam)                       # noqa: E731
+    try:
+        if options.python_ingest:
+            sam = AlignmentFile(path, "rb" if is_bam else "r")
+            fmt = sam.format
+            run = lambda: caller.run(sam)                          # noqa: E731
+        else:
+            from .ingest import NativeIngest
+            sam = NativeIngest(path, is_bam)
+            fmt = sam.format()[0]
+            if bam_path:
+                sam.set_bam_out(bam_path)
+            run = lambda: caller.run_native(sam)                   # noqa: E731
+    except Exception:
+        return _open_failed(out)
+    _warn_format(logger, path, is_bam, fmt)
 
     cache = {}
 
@@ -224,6 +230,28 @@ def main(argv=None, evaluator_factory=None) -> int:
         if fh is not None and fh is not sys.stdout:
             fh.close()
     return 0
+
+
+def _open_failed(out) -> int:
+    """The input could not be opened: the reference's pysam.Samfile raises at module level
+    (find_circ.py:461-469), an uncaught exception -- traceback, exit status 1."""
+    logging.error("Unhandled exception raised while opening the input")
+    exc = traceback.format_exc()
+    logging.error(exc)
+    sys.stderr.write(exc)
+    for fh in out.values():
+        if fh is not None and fh is not sys.stdout:
+            fh.close()
+    return 1
+
+
+def _warn_format(logger, path, is_bam, fmt):
+    """A BAM-named input (the reference opens it with mode 'rb', find_circ.py:463-466) that holds SAM
+    text is read as SAM, as htslib detects the format from the bytes; noted in run.log, since an
+    older pysam would have refused it."""
+    if is_bam and fmt == "sam":
+        logger.warning("'{0}' is not named *sam but holds SAM text: read as SAM (format detected from the "
+                       "bytes, as htslib does for pysam.Samfile(path, 'rb'))".format(path))
 
 
 def _finish(options, seconds, n_reads, logger, counters, n_spans, eval_seconds):
@@ -275,7 +303,11 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
                       known_circ=options.known_circ, known_lin=options.known_lin, bam_out=bam_path,
                       reads_gz=reads_gz)
     try:
-        n_kc, n_kl = nc.open()
+        try:
+            n_kc, n_kl = nc.open()
+        except Exception:
+            return _open_failed(out)
+        _warn_format(logger, path, is_bam, nc.format)
         for n, p in ((n_kc, options.known_circ), (n_kl, options.known_lin)):
             if p:
                 logger.info("loaded {0} known splice sites from '{1}'".format(n, p))

@@ -1583,8 +1583,8 @@ void add_counts(fc2_ingest_counts &c, const fc2_ingest_counts &to, const fc2_ing
 
 extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
     // is_bam is the reference's mode hint ('rb' unless the name ends in "sam", find_circ.py:463-466);
-    // like htslib's hts_open, reading never trusts it: the format comes from the bytes
-    (void)is_bam;
+    // like htslib's hts_open, reading never trusts it: the format comes from the bytes (the CLI logs a
+    // warning when a BAM-named input holds SAM text)
     if (!path || !out) return fc2::fail(FC2_E_PARAM, "fc2_ingest_open: null argument");
     *out = nullptr;
     int fd = strcmp(path, "-") == 0 ? dup(0) : open(path, O_RDONLY);
@@ -1638,6 +1638,13 @@ extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
                                      "it to BAM or SAM)");
     else if (h->in_rc || !h->z_err.empty()) rc = input_rc(h);
     if (!rc) rc = read_header(h);
+    // pysam's Samfile(path, mode) checks the header (check_sq, on by default): an input that declares
+    // no reference sequence -- an empty file, e.g. what a crashed aligner leaves as x.bam, or SAM text
+    // without @SQ lines -- raises ValueError before the first record (find_circ.py:463-469)
+    if (!rc && h->refs.empty())
+        rc = fc2::fail(FC2_E_FORMAT, std::string("ValueError: file has no sequences defined (mode='") +
+                                         (is_bam ? "rb" : "r") + "') - is it SAM/BAM format? Consider opening with "
+                                         "check_sq=False");
     if (rc) { fc2_ingest_close(h); return rc; }
     *out = h;
     return FC2_OK;

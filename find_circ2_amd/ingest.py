@@ -13,7 +13,8 @@ class NativeIngest:
 
     def __init__(self, path: str, is_bam: bool):
         self.h = ctypes.c_void_p()
-        N.check(N.lib().fc2_ingest_open(path.encode(), int(is_bam), ctypes.byref(self.h)))
+        from .native_caller import _check          # the reference's exception types (ValueError, IOError)
+        _check(N.lib().fc2_ingest_open(path.encode(), int(is_bam), ctypes.byref(self.h)))
         L = N.lib()
         self.references = [L.fc2_ingest_ref_name(self.h, i).decode("latin-1")
                            for i in range(L.fc2_ingest_n_refs(self.h))]

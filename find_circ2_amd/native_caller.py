@@ -90,6 +90,7 @@ class NativeCaller:
         self.bam_out = bam_out
         self.reads_gz = reads_gz     # (path, level, threads, piece): spliced_reads.fastq.gz written natively
         self.opened = False
+        self.format = None           # "sam" | "bam", detected from the bytes (open)
         self.loop_profile = {}       # seconds per stage of the last run (two-thread loop)
 
     def open(self):
@@ -97,10 +98,11 @@ class NativeCaller:
 
         Returns (#known circ sites, #known linear sites)."""
         L = N.lib()
-        N.check(L.fc2_caller_open(self._path.encode(), 1 if self._is_bam else 0, ctypes.byref(self.opts),
-                                  ctypes.byref(self.h)))
+        _check(L.fc2_caller_open(self._path.encode(), 1 if self._is_bam else 0, ctypes.byref(self.opts),
+                                 ctypes.byref(self.h)))
         self.opened = True
         ing = L.fc2_caller_ingest(self.h)
+        self.format = "bam" if L.fc2_ingest_format(ing, None) == 1 else "sam"      # FC2_INGEST_BAM
         if self.bam_out:
             N.check(L.fc2_ingest_set_bam_out(ing, self.bam_out.encode()))
         if self.reads_gz:

@@ -249,6 +249,10 @@ class AlignmentFile:
             self._fh = io.TextIOWrapper(stream, encoding="latin-1", newline="\n")
             self._pending = None
             self._read_sam_header()
+        if not self.references:       # pysam's check_sq (on by default): no @SQ -> ValueError
+            self.close()
+            raise ValueError("file has no sequences defined (mode='%s') - is it SAM/BAM format? Consider "
+                             "opening with check_sq=False" % mode)
 
     # ------------------------------------------------------------------ SAM
     def _read_sam_header(self):

@@ -218,8 +218,11 @@ def test_edge_forms_read_like_the_plain_sam(inputs, tmp_path):
 
 @pytest.mark.parametrize("form", ["empty", "sam_header_only", "bam_header_only", "bgzf_eof_only"])
 def test_inputs_without_records(tmp_path, form):
-    """No alignment records at all: both loops finish with empty tables (no UnboundLocalError, which
-    the reference raises only for exactly one record, find_circ.py:1486)."""
+    """No alignment records at all.  With a header that declares the references both loops finish
+    with empty tables (no UnboundLocalError, which the reference raises only for exactly one record,
+    find_circ.py:1486).  Without one -- an empty stream, an empty BGZF file -- pysam.Samfile's header
+    check (check_sq) raises ValueError when the reference opens the input (find_circ.py:461-469):
+    both loops exit with status 1 and that error, and write no table rows."""
     fa = os.path.join(GOLDEN, "test_ref.fa")
     hdr = "@SQ\tSN:testbed_plus\tLN:720\n@SQ\tSN:testbed_minus\tLN:720\n"
     if form == "empty":
@@ -236,8 +239,37 @@ def test_inputs_without_records(tmp_path, form):
     for loop, ing in (("native", []), ("py", ["--python-ingest"])):
         out = str(tmp_path / loop)
         r = _pipe(["-G", fa, "-o", out, "-q"] + ing, blob)
-        assert r.returncode == 0, (form, loop, r.stderr.decode()[-2000:])
         outs.append(out)
         rows = [l for l in open(os.path.join(out, "circ_splice_sites.bed")) if not l.startswith("#")]
         assert rows == []
-    same(outs[0], outs[1])
+        if form in ("empty", "bgzf_eof_only"):
+            assert r.returncode == 1, (form, loop)
+            assert "ValueError: file has no sequences defined (mode='r')" in r.stderr.decode(), r.stderr.decode()
+            continue
+        assert r.returncode == 0, (form, loop, r.stderr.decode()[-2000:])
+    if form not in ("empty", "bgzf_eof_only"):
+        same(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("body", ["", "sam_no_sq", "sam_text"])
+def test_bam_named_inputs(tmp_path, body):
+    """A path not ending in 'sam' is opened with mode 'rb' by the reference (find_circ.py:463-466).
+    An empty x.bam (what a crashed aligner leaves behind) or one holding SAM text without @SQ fails
+    pysam's header check with ValueError; SAM text with a header is read as SAM (htslib detects the
+    format from the bytes), with a warning in run.log.  All three read loops agree."""
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    rec = "r1\t0\ttestbed_plus\t10\t60\t20M\t*\t0\t0\t%s\t*\tAS:i:20\n" % ("A" * 20)
+    text = {"": "", "sam_no_sq": rec + rec.replace("r1", "r2"),
+            "sam_text": "@SQ\tSN:testbed_plus\tLN:720\n" + rec + rec.replace("r1", "r2")}[body]
+    p = str(tmp_path / "aln.bam")
+    open(p, "w").write(text)
+    for loop, mode in (("native", []), ("pyc", ["--python-caller"]), ("py", ["--python-ingest"])):
+        out = str(tmp_path / loop)
+        rc = cli.main(["-G", fa, "-o", out, "-q"] + mode + [p], evaluator_factory=oracle_evaluator_factory)
+        log = open(os.path.join(out, "run.log")).read()
+        if body == "sam_text":
+            assert rc == 0, (loop, log[-1000:])
+            assert "holds SAM text: read as SAM" in log
+        else:
+            assert rc == 1, loop
+            assert "ValueError: file has no sequences defined (mode='rb')" in log, log[-1000:]
