@@ -565,7 +565,7 @@ struct Shard {
 inline int shard_of(const CKey &k) { return (int)(CKeyHash()(k) >> 60) & (kShards - 1); }
 
 struct SEv {                                   // one table update of a shard (phase A -> B)
-    uint64_t seq;                              // fragment index << 20 | the fragment's add ordinal
+    uint64_t seq;                              // fragment index << 32 | the fragment's add ordinal
     CKey key;
     uint32_t frag;                             // fragment index in the chunk
     uint32_t slot;                             // the range's slot: written (add) / read (flag)
@@ -1697,7 +1697,10 @@ void phase_a_frag(const fc2_caller *h, uint32_t fi, const Frag &fr, const Result
         }
         SEv e;
         e.key = splice_key(sp);
-        e.seq = ((uint64_t)fi << 20) | ord++;
+        // input order of the table updates: the fragment's index in the chunk, then its add ordinal
+        // (32 bits each: --all-hits ties of long reads can number far beyond 2^20 in one fragment)
+        if (ord == UINT32_MAX) throw Fatal{FC2_E_RANGE, "native caller: more than 2^32 - 1 junction updates in one fragment"};
+        e.seq = ((uint64_t)fi << 32) | ord++;
         e.frag = fi;
         e.slot = (uint32_t)ro.slots.size();
         ro.slots.emplace_back();

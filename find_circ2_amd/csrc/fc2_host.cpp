@@ -887,9 +887,12 @@ extern "C" int fc2_pack_windows(const fc2_params *p, const fc2_fasta *f, uint64_
     return FC2_OK;
 }
 
-static inline uint64_t block_bytes(int l) {  // 16-B header + I + A + B (window slots of l+3 bytes)
+// 16-B header + I + A's slot of l+3 bytes + B's slot of 2l+3 bytes (fc2_bytes_view): an irregular
+// window pair -- A cut short past the chromosome's end, B padded long before its start -- compares
+// B[x+2 : x+2+lenI-lenA] (find_circ.py:907-908), which reaches byte 2l+2 of B
+static inline uint64_t block_bytes(int l) {
     const uint64_t lc = (uint64_t)std::max(0, l);
-    return (16 + lc + 2 * (lc + 3) + 3) & ~3ull;
+    return (16 + lc + (lc + 3) + (2 * lc + 3) + 3) & ~3ull;
 }
 
 extern "C" int fc2_bytepath_size(const fc2_params *p, uint64_t n, const fc2_pair *pairs, uint64_t *m, uint64_t *arena_bytes) {
@@ -929,19 +932,21 @@ extern "C" int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64
         A.clear(); B.clear();
         if (l >= 0) {
             const int64_t flank = l + 2;
-            // only min(length, l + 3) bytes of a window are stored; the header keeps the full length and,
-            // for a one-base internal part, the mismatches of B's bytes past its slot against that base
+            // only min(length, slot) bytes of a window are stored (slots of l + 3 and 2l + 3 bytes); the
+            // header keeps the full length and, for a one-base internal part, the mismatches of B's bytes
+            // past its slot against that base
             const int c1 = lenI == 1 ? (int)upc(reads[read_off[i] + i0]) : -1;
             rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + flank, A,
                                 (size_t)flank + 1, &fullA);
             if (rc) return rc;
             rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - flank, (int64_t)pr.b_aend - e, B,
-                                (size_t)flank + 1, &fullB, c1, lenI == 1 ? &tailB : nullptr);
+                                (size_t)(2 * flank - 1), &fullB, c1, lenI == 1 ? &tailB : nullptr);
             if (rc) return rc;
         }
-        // a window of unexpected length (outside get_data's defined range) keeps l+3 stored bytes:
-        // the kernel sees the length mismatch (ERR_WIN) or, where numpy broadcasts a 1-byte operand,
-        // counts the rest of the window as the 'N' padding it is (bp_bytes_kernel)
+        // a window of unexpected length (outside get_data's defined range) keeps its slot's bytes: the
+        // kernel compares what the reference's string form reads of them (at most B[:2l+3] when the
+        // lengths add up), sees a length mismatch numpy cannot broadcast (ERR_WIN) or, where numpy
+        // broadcasts a 1-byte operand, counts B's bytes past the slot through tailB (bp_bytes_kernel)
         const int32_t lenA = (int32_t)std::min<int64_t>(fullA, INT32_MAX);
         const int32_t lenB = (int32_t)std::min<int64_t>(fullB, INT32_MAX);
         index[k] = i;
@@ -959,7 +964,7 @@ extern "C" int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64
         const int lc = std::max(0, l);
         memcpy(q, A.data(), std::min<size_t>(A.size(), (size_t)lc + 3));
         q += lc + 3;
-        memcpy(q, B.data(), std::min<size_t>(B.size(), (size_t)lc + 3));
+        memcpy(q, B.data(), std::min<size_t>(B.size(), 2 * (size_t)lc + 3));
         pos += block_bytes(l);
         ++k;
     }

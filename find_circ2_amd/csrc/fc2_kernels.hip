@@ -438,7 +438,6 @@ __device__ __forceinline__ unsigned code_of(uint8_t c) {
     return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
 }
 
-
 __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_bytes_view v, uint64_t *__restrict__ out,
                                                           uint64_t *__restrict__ tiemask, uint32_t tw, uint64_t stride) {
     const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
@@ -450,11 +449,12 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
     const int tailB = ((const int32_t *)blk)[3];      // lenI == 1: B's bytes past its slot that differ from I[0]
     const int e = p.asize - p.margin;
     const int l = (int)pr.read_len - 2 * e;
-    const int64_t slot = (int64_t)(l < 0 ? 0 : l) + 3;   // stored bytes per window (fc2_bytepath_fill)
+    const int64_t lc = l < 0 ? 0 : l;
+    const int64_t slotA = lc + 3, slotB = 2 * lc + 3;   // stored bytes per window (fc2_bytepath_fill)
     const uint8_t *I = blk + 16;
     const uint8_t *Af = I + lenI;
-    const uint8_t *Bf = Af + slot;
-    const int64_t sB = lenB < slot ? lenB : slot;   // A is only read below x + 2 <= l + 2 < slot
+    const uint8_t *Bf = Af + slotA;
+    const int64_t sB = lenB < slotB ? lenB : slotB;     // A is only read below x + 2 <= l + 2 < slotA
     const bool want_ties = p.allhits != 0;
     const uint32_t half = tw / 2;
     if (want_ties)
@@ -487,7 +487,7 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
                 const int64_t n2 = (int64_t)lenB - (x + 2) > 0 ? (int64_t)lenB - (x + 2) : 0;   // B_flank[x+2:]
                 const int64_t sl = n1 + n2;
                 int64_t dd = 0;
-                if (sl == lenI) {   // then B[x+2:] lies in its slot: lenB <= lenI + x + 2 <= l + 2
+                if (sl == lenI) {   // B[x+2 : x+2+n2] lies in its slot: x + 2 + n2 <= l + 2 + lenI <= 2l + 2
                     for (int64_t j = 0; j < n1; ++j) dd += Af[j] != I[j];
                     for (int64_t j = 0; j < n2; ++j) dd += Bf[x + 2 + j] != I[n1 + j];
                     if (p.maxdist == 0) dd = dd != 0;                                  // the bool a != b
@@ -499,9 +499,9 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
                     const int64_t b0 = x + 2, b1 = x + 2 + n2;                         // B bytes [b0, b1)
                     const int64_t st = b1 < sB ? b1 : sB;
                     for (int64_t j = b0; j < st; ++j) dd += Bf[j] != c;
-                    if (b1 > sB) dd += tailB;                                          // B[slot:], b0 < slot
+                    if (b1 > sB) dd += tailB;                                          // B[slotB:], b0 < slotB
                 } else if (sl == 1 && lenI > 0) {                                      // spliced[0] broadcast
-                    const uint8_t c = n1 ? Af[0] : Bf[x + 2];                          // x + 2 < slot
+                    const uint8_t c = n1 ? Af[0] : Bf[x + 2];                          // x + 2 < slotB
                     for (int j = 0; j < lenI; ++j) dd += I[j] != c;
                 } else if (!((sl == 0 && lenI == 1) || (sl == 1 && lenI == 0))) {
                     err = FC2_RES_ERR_WIN;  // shapes numpy cannot broadcast
@@ -516,7 +516,7 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
             if (!(have4 && is_acgtn(g0) && is_acgtn(g1) && is_acgtn(g2) && is_acgtn(g3))) { err = FC2_RES_ERR_KEY; break; }
             const int cp = (g0 == 'G' && g1 == 'T' && g2 == 'A' && g3 == 'G');
             const int cm = (g0 == 'C' && g1 == 'T' && g2 == 'A' && g3 == 'C');
-    const int ov = ov_of(x, l, p.margin);
+            const int ov = ov_of(x, l, p.margin);
             if (p.noncanonical) {
                 const int s1 = 20 * cp - 10 * d - ov + sp_plus, s2 = 20 * cm - 10 * d - ov + sp_minus;
                 if (pass == 0) { add_hit(Bst, x, 0, d, ov, s1); add_hit(Bst, x, 1, d, ov, s2); }

@@ -230,11 +230,13 @@ typedef struct fc2_batch_view {
 /* ---- pairs that need byte-exact evaluation ------------------------------ */
 /* Block for pair k at arena[off[k]]: int32 lenI, lenA, lenB, tailB, then
  * I (lenI bytes: read[e:-e].upper() with Python's slice rules, find_circ.py:895), then the A and B
- * windows of get_data(...).upper() (:901-902) in slots of l+3 bytes each (l = read_len - 2e).
+ * windows of get_data(...).upper() (:901-902) in slots of l+3 and 2l+3 bytes (l = read_len - 2e).
  * lenA / lenB are the windows' full lengths (saturated at INT32_MAX); a window outside get_data's
- * defined range can be longer than its slot (:194-211), and only a one-base internal part that
- * numpy broadcasts over the spliced string (:861-863) reads past the slot: tailB = the bytes of
- * B[l+3:] that differ from I[0] when lenI == 1, else 0. */
+ * defined range can be longer than its slot (:194-211).  The string form of :907-908 reads at most
+ * B[:2l+3] when A_flank[:x] + B_flank[x+2:] has the internal part's length (A cut short past the
+ * chromosome's end, B padded long before its start); only a one-base internal part that numpy
+ * broadcasts over the spliced string (:861-863) reads past B's slot: tailB = the bytes of
+ * B[2l+3:] that differ from I[0] when lenI == 1, else 0. */
 typedef struct fc2_bytes_view {
     const uint64_t *index;       /* device [m] : pair index into results/tiemask */
     const fc2_pair *pairs;       /* device [m] */

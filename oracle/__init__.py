@@ -95,9 +95,34 @@ class OracleFasta:
                 data = f.read()
         self._buf = np.frombuffer(data, dtype=np.uint8).copy()
         self.h = lib().orc_fasta_index(self._buf.ctypes.data, len(self._buf))
+        if path is not None and os.access(path + ".byo_index", os.R_OK):
+            self._load_index(path + ".byo_index")     # find_circ.py:110-112
         n = lib().orc_fasta_n_chrom(self.h)
         self.names = [lib().orc_fasta_chrom_name(self.h, i).decode() for i in range(n)]
         self.sizes = [lib().orc_fasta_chrom_size(self.h, i) for i in range(n)]
+
+    def _load_index(self, ipath: str):
+        """load_index (find_circ.py:182-187): one line per chromosome, the skip characters as a
+        Python-2 repr (string_escape)."""
+        import codecs
+        rows = []
+        with open(ipath, "rb") as f:
+            for line in f:
+                chrom, ofs, ldata, skip, skipchar, size = line.rstrip().split(b"\t")
+                rows.append((chrom, int(ofs), int(ldata), int(skip), codecs.escape_decode(skipchar[1:-1])[0],
+                             int(size)))
+        n = len(rows)
+        L = lib()
+        if not hasattr(L, "_set_chroms_sig"):
+            vp, i64p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)
+            L.orc_fasta_set_chroms.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), i64p, i64p, i64p,
+                                               ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_int32), i64p]
+            L._set_chroms_sig = True
+        col = lambda k: (ctypes.c_int64 * max(n, 1))(*[r[k] for r in rows])       # noqa: E731
+        names = (ctypes.c_char_p * max(n, 1))(*[r[0] for r in rows])
+        skipc = (ctypes.c_char_p * max(n, 1))(*[r[4] for r in rows])
+        skipl = (ctypes.c_int32 * max(n, 1))(*[len(r[4]) for r in rows])
+        L.orc_fasta_set_chroms(self.h, n, names, col(1), col(2), col(3), skipc, skipl, col(5))
 
     @classmethod
     def dummy_genome(cls) -> "OracleFasta":

@@ -144,6 +144,28 @@ orc_fasta *orc_fasta_dummy(void) {
     return f;
 }
 
+/* load_index (find_circ.py:182-187): the chromosome table of an existing .byo_index replaces the one
+ * index() built, since the reference reads that file instead of indexing (:110-112).  Entry k:
+ * name, ofs, ldata, skip, skipchar (skiplen bytes, escapes already decoded), size. */
+void orc_fasta_set_chroms(orc_fasta *f, int n, const char *const *names, const int64_t *ofs, const int64_t *ldata,
+                          const int64_t *skip, const char *const *skipchar, const int32_t *skiplen,
+                          const int64_t *size) {
+    free(f->chroms);
+    f->chroms = (orc_chrom *)calloc((size_t)(n > 0 ? n : 1), sizeof(orc_chrom));
+    f->n_chrom = n;
+    for (int k = 0; k < n; k++) {
+        orc_chrom *c = &f->chroms[k];
+        strncpy(c->name, names[k], sizeof c->name - 1);
+        c->ofs = ofs[k];
+        c->ldata = ldata[k];
+        c->skip = skip[k];
+        c->size = size[k];
+        int sl = skiplen[k] < 0 ? 0 : skiplen[k] > 7 ? 7 : skiplen[k];
+        memcpy(c->skipchar, skipchar[k], (size_t)sl);
+        c->skiplen = sl;
+    }
+}
+
 void orc_fasta_free(orc_fasta *f) { if (f) { free(f->chroms); free(f); } }
 int orc_fasta_n_chrom(const orc_fasta *f) { return f->n_chrom; }
 const char *orc_fasta_chrom_name(const orc_fasta *f, int i) { return f->chroms[i].name; }

@@ -148,15 +148,20 @@ def make_odd_spans(genome: Dict[str, str], n: int, seed: int, asize=15, margin=2
             L = int(rng.integers(max(0, 2 * e - 2), max(1, 2 * e + 4)))
         else:
             L = int(rng.integers(max(1, 2 * e), max(2, 2 * e + 60)))
-        v = rng.random()
-        if v < 0.2:                                        # windows past the chromosome's end
+        # each window from its own bucket, so a short window (past the end) meets a long one (before
+        # the start) as often as two of a kind: the byte kernel's slots must hold either
+        v, w = rng.random(), rng.random()
+        if v < 0.25:                                       # A's window past the chromosome's end
             a_pos = G + int(rng.integers(-5, 40))
-            b_aend = G + int(rng.integers(-5, 80))
-        elif v < 0.4:                                      # windows before its start
+        elif v < 0.5:                                      # ... or before its start
             a_pos = int(rng.integers(-40, 8))
-            b_aend = int(rng.integers(-20, 30))
         else:
             a_pos = int(rng.integers(0, max(1, G - 1)))
+        if w < 0.25:                                       # B's window past the end
+            b_aend = G + int(rng.integers(-5, 80))
+        elif w < 0.5:                                      # ... or before the start
+            b_aend = int(rng.integers(-20, 30))
+        else:
             b_aend = int(rng.integers(0, max(1, G)))
         kA = L // 2
         src = rng.random() < 0.6
@@ -174,3 +179,29 @@ def make_odd_spans(genome: Dict[str, str], n: int, seed: int, asize=15, margin=2
         out.append(SmallSpan(chrom, ci, int(a_pos), int(a_aend), int(b_pos), int(b_aend), read.encode(),
                              bool(rng.random() < 0.5)))
     return out
+
+
+def truncated_fasta(tmp_path):
+    """A FASTA cut short after it was indexed: its .byo_index (which the reference reads instead of
+    indexing, find_circ.py:110-112) claims 60 more bases for the last chromosome than the file holds,
+    so get_data returns windows shorter than asked near that end and padded longer before the start
+    (:194-211).  Returns (path, {chrom: text})."""
+    rng = np.random.default_rng(8)
+    seqs = {c: bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), n).tobytes()) for c, n in (("u1", 300), ("u2", 240))}
+    for c in seqs:                                   # splice signals to qualify some breakpoints
+        b = bytearray(seqs[c])
+        for k in range(5, len(b) - 5, 37):
+            b[k:k + 2] = b"GT" if k % 2 else b"AG"
+        seqs[c] = bytes(b)
+    path = str(tmp_path / "trunc.fa")
+    body, idx, ofs = b"", [], 0
+    for c, sq in seqs.items():
+        head = b">" + c.encode() + b"\n"
+        ofs += len(head)
+        lines = b"".join(sq[k:k + 60] + b"\n" for k in range(0, len(sq), 60))
+        idx.append("%s\t%d\t60\t1\t'\\n'\t%d\n" % (c, ofs, len(sq) + (60 if c == "u2" else 0)))
+        body += head + lines
+        ofs += len(lines)
+    open(path, "wb").write(body)
+    open(path + ".byo_index", "w").write("".join(idx))
+    return path, {c: sq.decode() for c, sq in seqs.items()}

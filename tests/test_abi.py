@@ -306,6 +306,10 @@ def test_bytepath_arena_matches_reference_windows(L, tmp_path):
             b = int(rng.integers(0, size + 3))
             spans.append(SmallSpan(name, ci, a, a + 5, b - 5, b, bytes(rng.choice(list(b"ACGTNR"), L_)), False))
             cidx.append(ci)
+        # both windows outside the chromosome: A's past its end, B's before its start (padded long)
+        L_ = int(rng.integers(10, 20))
+        spans.append(SmallSpan(name, ci, size + 2, size + 7, -40, -35, bytes(rng.choice(list(b"ACGT"), L_)), True))
+        cidx.append(ci)
     rc, hp, words, nwords, stride, nbp, buf, off = _pack_pairs(L, p, h, spans, cidx)
     assert rc == 0, L.fc2_last_error()
     m, nb = ctypes.c_uint64(), ctypes.c_uint64()
@@ -328,14 +332,67 @@ def test_bytepath_arena_matches_reference_windows(L, tmp_path):
         I = arena[o + 16:o + 16 + lenI].tobytes()
         assert I == s.read_part[e:len(s.read_part) - e].upper()
         if l >= 0:
-            # header: the windows' full lengths; body: l + 3 byte slots holding their first bytes
-            slot = l + 3
-            A = arena[o + 16 + lenI:o + 16 + lenI + min(lenA, slot)].tobytes()
-            B = arena[o + 16 + lenI + slot:o + 16 + lenI + slot + min(lenB, slot)].tobytes()
+            # header: the windows' full lengths; body: slots of l + 3 (A) and 2l + 3 (B) bytes holding
+            # their first bytes
+            sa, sb = l + 3, 2 * l + 3
+            A = arena[o + 16 + lenI:o + 16 + lenI + min(lenA, sa)].tobytes()
+            B = arena[o + 16 + lenI + sa:o + 16 + lenI + sa + min(lenB, sb)].tobytes()
             ra = ref.get_data(s.chrom, s.a_pos + e, s.a_pos + e + l + 2).upper()
             rb = ref.get_data(s.chrom, s.b_aend - e - l - 2, s.b_aend - e).upper()
             assert (lenA, lenB) == (len(ra), len(rb))
-            assert A == ra[:slot] and B == rb[:slot]
+            assert A == ra[:sa] and B == rb[:sb]
+    L.fc2_fasta_close(h)
+
+
+def test_bytepath_arena_truncated_fasta(L, tmp_path):
+    """A FASTA cut short after indexing (its .byo_index claims more bases, find_circ.py:110-112):
+    windows near that end come back shorter than l + 2, windows before the start longer.  The arena's
+    slots hold what the reference's string form can read (A[:l+3], B[:2l+3]), against the Python
+    restatement reading the same index, and the C oracle honours the index as well."""
+    from synth_small import SmallSpan, truncated_fasta
+    path, gen = truncated_fasta(tmp_path)
+    rc, h = _open(path)
+    assert rc == 0
+    _pack(h)
+    ref = RefIndexedFasta(path, use_existing_index=True)
+    of = oracle.OracleFasta(path)
+    assert of.sizes == [len(gen["u1"]), len(gen["u2"]) + 60]
+    p = N.Params(6, 1, 2, 0, 0, 0, 0)
+    e = 5
+    rng = np.random.default_rng(5)
+    spans, cidx = [], []
+    for _ in range(200):
+        L_ = int(rng.integers(2 * e, 2 * e + 30))
+        a = int(rng.integers(len(gen["u2"]) - 30, len(gen["u2"]) + 70)) - e
+        b = int(rng.integers(-40, 20)) + e
+        spans.append(SmallSpan("u2", 1, a, a + 3, b - 3, b, bytes(rng.choice(list(b"ACGT"), L_)), False))
+        cidx.append(1)
+    rc, hp, words, nwords, stride, nbp, buf, off = _pack_pairs(L, p, h, spans, cidx)
+    assert rc == 0, L.fc2_last_error()
+    m, nb = ctypes.c_uint64(), ctypes.c_uint64()
+    assert L.fc2_bytepath_size(ctypes.byref(p), len(spans), hp.ctypes.data, ctypes.byref(m), ctypes.byref(nb)) == 0
+    assert m.value == len(spans)
+    idx = np.zeros(m.value, np.uint64)
+    bp = np.zeros(m.value, N.PAIR_DTYPE)
+    offs = np.zeros(m.value, np.uint64)
+    arena = np.zeros(nb.value, np.uint8)
+    assert L.fc2_bytepath_fill(ctypes.byref(p), h, len(spans), buf.ctypes.data, off.ctypes.data, hp.ctypes.data,
+                               idx.ctypes.data, bp.ctypes.data, offs.ctypes.data, arena.ctypes.data) == 0
+    n_short = 0
+    for k in range(m.value):
+        s = spans[int(idx[k])]
+        o = int(offs[k])
+        lenI, lenA, lenB = np.frombuffer(arena[o:o + 12].tobytes(), np.int32)
+        l = len(s.read_part) - 2 * e
+        sa, sb = l + 3, 2 * l + 3
+        ra = ref.get_data("u2", s.a_pos + e, s.a_pos + e + l + 2).upper()
+        rb = ref.get_data("u2", s.b_aend - e - l - 2, s.b_aend - e).upper()
+        assert ra == of.get_upper(1, s.a_pos + e, s.a_pos + e + l + 2)
+        assert (lenA, lenB) == (len(ra), len(rb))
+        assert arena[o + 16 + lenI:o + 16 + lenI + min(lenA, sa)].tobytes() == ra[:sa]
+        assert arena[o + 16 + lenI + sa:o + 16 + lenI + sa + min(lenB, sb)].tobytes() == rb[:sb]
+        n_short += len(ra) < l + 2 < len(rb)
+    assert n_short > 20
     L.fc2_fasta_close(h)
 
 

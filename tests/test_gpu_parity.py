@@ -13,7 +13,7 @@ import pytest
 import oracle
 from conftest import GOLDEN
 from gpu_helpers import assert_same, gpu_arrays, oracle_arrays
-from synth_small import load_genome, make_odd_spans, make_spans
+from synth_small import load_genome, make_odd_spans, make_spans, truncated_fasta
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -256,6 +256,47 @@ def test_byte_path_exotic_and_irregular(tmp_path):
         assert_same(ga, oracle_arrays(r), label=str(o))
         if o.get("noncanonical"):
             assert (r.n_ties == -oracle.ORC_ERR_KEY).any(), "expected some reference KeyErrors"
+
+
+def test_byte_path_truncated_fasta(tmp_path):
+    """Windows of every length mix: A cut short at the truncated end against B padded long
+    before the chromosome's start, and the other way round.  The string form of find_circ.py:907-908
+    then reads B up to byte 2l+2, which the byte kernel's B slot holds.  Pair by pair vs the oracle,
+    which reads the same .byo_index."""
+    path, gen = truncated_fasta(tmp_path)
+    g = Genome.from_fasta(path, device=_dev())
+    rng = np.random.default_rng(12)
+    from synth_small import SmallSpan
+    n_mixed = 0
+    for o in (dict(asize=6, margin=1, maxdist=60), dict(asize=6, margin=1, maxdist=60, noncanonical=True, allhits=True),
+              dict(asize=8, margin=2, maxdist=0), dict(asize=6, margin=1, maxdist=3)):
+        opt = Options(**o)
+        e = opt.eff_a
+        spans = []
+        for _ in range(3000):
+            c = "u2" if rng.random() < 0.8 else "u1"
+            size = len(gen[c])
+            L = int(rng.integers(2 * e, 2 * e + 40))
+            l = L - 2 * e
+            a_pos = int(rng.integers(size - 30, size + 70)) - e         # A around the real / claimed end
+            b_aend = int(rng.integers(-l - 10, 30)) + e                  # B around the start
+            if rng.random() < 0.3:
+                a_pos, b_aend = int(rng.integers(-l - 10, 20)) - e, int(rng.integers(size - 20, size + 70)) + e
+            src = gen[c][max(0, size - L):] + gen[c][:L]
+            read = src[:L].encode() if rng.random() < 0.5 else bytes(rng.choice(np.frombuffer(b"ACGTN", np.uint8), L))
+            bs = rng.random() < 0.5
+            spans.append(SmallSpan(c, 0, a_pos, a_pos + L // 2, (a_pos - 5) if bs else (a_pos + L), b_aend, read,
+                                   bool(rng.random() < 0.5)))
+            la = len(oracle.OracleFasta(path).get_upper(0 if c == "u1" else 1, a_pos + e, a_pos + e + l + 2)) \
+                if len(spans) <= 60 else l + 2
+            n_mixed += la < l + 2
+        b, out = run_spans(opt, g, spans)
+        assert b.m_bytepath > 0
+        r = oracle_spans(opt, path, spans, g.names)
+        ga = gpu_arrays(opt, b.host_pairs, out.host(b.n))
+        assert ga["done"].all()
+        assert_same(ga, oracle_arrays(r), label="truncated %s" % o)
+    assert n_mixed > 0
 
 
 def test_edge_lengths_and_long_reads():
