@@ -49,6 +49,12 @@ PAIR_DTYPE = np.dtype([("a_pos", "<i4"), ("b_aend", "<i4"), ("chrom", "<u4"), ("
 RESULT_DTYPE = np.dtype([("best_x", "<i2"), ("dist", "u1"), ("ov", "u1"), ("n_ties", "<u2"), ("info", "<u2")])
 assert PAIR_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 8
 ESCAPE_DTYPE = np.dtype([("index", "<u8"), ("result", RESULT_DTYPE)])     # fc2_result_escape
+# pairs with read parts over MAX_READ_LEN and their results (fc2_long_pair / fc2_long_result)
+LONG_PAIR_DTYPE = np.dtype([("read_off", "<u8"), ("read_len", "<u4"), ("chrom", "<u4"), ("a_pos", "<i4"),
+                            ("b_aend", "<i4"), ("flags", "u1"), ("_pad", "u1", (7,))])
+LONG_RESULT_DTYPE = np.dtype([("best_x", "<i4"), ("n_ties", "<u4"), ("dist", "u1"), ("ov", "u1"), ("info", "<u2"),
+                              ("_pad", "<u4")])
+assert LONG_PAIR_DTYPE.itemsize == 32 and LONG_RESULT_DTYPE.itemsize == 16
 R32_ESCAPE = 0x80000000
 R16_ESCAPE = 0x007F
 
@@ -127,7 +133,7 @@ EXPORTED = [
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
     "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill", "fc2_window_geometry", "fc2_pack_windows",
-    "fc2_gather_windows_launch",
+    "fc2_gather_windows_launch", "fc2_long_geometry", "fc2_long_fill", "fc2_bp_scan_long_launch",
     "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_twin_launch", "fc2_wtab_geometry", "fc2_wtab_launch",
     "fc2_nsuper_geometry", "fc2_nsuper_launch", "fc2_synth_pairs_launch",
     "fc2_reorder_plan", "fc2_reorder_launch",
@@ -137,11 +143,11 @@ EXPORTED = [
     "fc2_ingest_format", "fc2_sam_to_bam",
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
-    "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
+    "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_submit_long", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
     "fc2_caller_set_reads_gz", "fc2_caller_close_reads",
     # include/fc2_ctx.h
     "fc2_ctx_create", "fc2_ctx_destroy", "fc2_ctx_genome_load", "fc2_ctx_genome_view", "fc2_ctx_scan_async",
-    "fc2_ctx_sync", "fc2_ctx_stream", "fc2_ctx_last_error",
+    "fc2_ctx_sync", "fc2_ctx_scan_long", "fc2_ctx_stream", "fc2_ctx_last_error",
 ]
 
 
@@ -168,7 +174,7 @@ class CallerOpts(ctypes.Structure):
 
 class CallerBatch(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("reads", ctypes.c_void_p), ("read_off", ctypes.c_void_p),
-                ("pairs", ctypes.c_void_p)]
+                ("pairs", ctypes.c_void_p), ("n_long", ctypes.c_uint64), ("long_pairs", ctypes.c_void_p)]
 
 
 _lib = None
@@ -230,6 +236,9 @@ def lib() -> ctypes.CDLL:
         "fc2_pack_windows": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, u32, u64, ctypes.c_int]),
         "fc2_gather_windows_launch": (ctypes.c_int, [P(Params), P(GenomeView), P(BatchView), vp, vp, vp, u32, vp]),
         "fc2_bytepath_fill": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, vp, vp, vp, vp]),
+        "fc2_long_geometry": (ctypes.c_int, [P(Params), u64, vp, P(ctypes.c_uint64), vp]),
+        "fc2_long_fill": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, vp]),
+        "fc2_bp_scan_long_launch": (ctypes.c_int, [P(Params), u64, vp, vp, vp, vp, vp, vp, vp]),
         "fc2_synth_genome_launch": (ctypes.c_int, [u64, vp, vp, vp, u64, vp, vp, u32, vp]),
         "fc2_coarse_launch": (ctypes.c_int, [vp, vp, u64, vp]),
         "fc2_twin_launch": (ctypes.c_int, [vp, u64, vp, vp]),
@@ -260,6 +269,7 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_next": (ctypes.c_int, [vp, P(CallerBatch), P(ctypes.c_int)]),
         "fc2_caller_submit": (ctypes.c_int, [vp, vp, vp, u32, u64]),
         "fc2_caller_submit_compact": (ctypes.c_int, [vp, vp, ctypes.c_int, u64, vp, u64, vp, u32, u64]),
+        "fc2_caller_submit_long": (ctypes.c_int, [vp, vp, u64, vp, u64]),
         "fc2_caller_queued": (ctypes.c_int, [vp]),
         "fc2_caller_take": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_set_reads_gz": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, u64]),
@@ -273,6 +283,7 @@ def lib() -> ctypes.CDLL:
         "fc2_ctx_genome_view": (ctypes.c_int, [vp, P(GenomeView)]),
         "fc2_ctx_scan_async": (ctypes.c_int, [vp, P(Params), u64, vp, vp, vp, vp, vp, u32, ctypes.c_int]),
         "fc2_ctx_sync": (ctypes.c_int, [vp]),
+        "fc2_ctx_scan_long": (ctypes.c_int, [vp, P(Params), u64, vp, vp, vp, vp]),
         "fc2_ctx_stream": (vp, [vp]),
         "fc2_ctx_last_error": (ctypes.c_char_p, [vp]),
     }

@@ -78,23 +78,14 @@ def build_parser() -> optparse.OptionParser:
 
 
 def gpu_evaluator(genome, hp_options):
-    """evaluate(spans): one batched GPU scan; per-span results or the reference's exception."""
-    from . import _native as N
-    from .hotpath import PairBatch, decode_splices, none_aend_error, scan
-    missing = 0xFFFFFFFF
+    """evaluate(spans): one batched GPU scan (read parts over MAX_READ_LEN on the long path); per-span
+    results or the reference's exception (BreakpointEngine.find_breakpoints_batch)."""
+    from .hotpath import BreakpointEngine
+    engine = BreakpointEngine(genome, hp_options)
 
     def evaluate(spans):
-        idx = [genome.chrom_index_or_missing(s.chrom) for s in spans]
-        flags = [((N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.strand == '-' else 0) |
-                  (N.PAIR_SKIP if c == missing or s.align_B.aend is None else 0)) for s, c in zip(spans, idx)]
-        b = PairBatch.pack(hp_options, genome, [s.read_part for s in spans], [s.align_A.pos for s in spans],
-                           [s.align_B.aend or 0 for s in spans], [0 if c == missing else c for c in idx], flags,
-                           locus_order=True)
-        out = scan(hp_options, genome, b)
-        res = decode_splices(hp_options, genome, b, out, spans, raise_errors=False)
-        for s, r, c in zip(spans, res, idx):
-            # indexed_fasta.get_data (find_circ.py:193) for A's window, then B.aend - eff_a (:902)
-            s.result = KeyError(s.chrom) if c == missing else none_aend_error() if s.align_B.aend is None else r
+        for s, r in zip(spans, engine.find_breakpoints_batch(spans, locus_order=True)):
+            s.result = r
     return evaluate
 
 

@@ -239,8 +239,10 @@ struct Span {                                  // JunctionSpan (:821-852)
     bool a_rev;                                // A.is_reverse after the swap
     uint64_t read_off;
     uint32_t read_len;
-    int64_t eval = -1;                         // index in the evaluation batch
+    int64_t eval = -1;                         // index in the evaluation batch (kLongEval | index: in its long list)
 };
+
+constexpr int64_t kLongEval = int64_t(1) << 62;
 
 // `span.uniq >= options.min_uniq_qual` (:1299, :1351) with Python 2's ordering (nan compares false)
 inline bool uniq_ok(const Span &s, int64_t min_uniq_qual) { return !s.uniq_num || s.uniq >= (double)min_uniq_qual; }
@@ -742,6 +744,7 @@ struct fc2_caller {
     std::vector<std::pair<int64_t, Fatal>> next_err_at;                 // their first error per range
     std::vector<uint64_t> bf_off;
     std::vector<fc2_pair> bf_pairs;
+    std::vector<fc2_long_pair> bf_long;         // pairs with read parts over FC2_MAX_READ_LEN
     std::vector<int64_t> bf_starts, bf_ends;    // process_mate scratch
     std::vector<size_t> bf_order;
     std::vector<Frag> frags;                    // the chunk being recorded (submit): first nfrags
@@ -750,6 +753,12 @@ struct fc2_caller {
     ByteBuf arena;
     std::vector<uint64_t> b_off;
     std::vector<fc2_pair> b_pairs;
+    std::vector<fc2_long_pair> b_long;
+    // the oldest queued chunk's long-pair results (fc2_caller_submit_long): results, tie words and
+    // each pair's first tie word (fc2_long_geometry)
+    std::vector<fc2_long_result> l_res;
+    std::vector<uint64_t> l_ties, l_tie_off;
+    bool l_staged = false;
     // chunks handed out by fc2_caller_next and not yet submitted, oldest first: the caller may
     // read ahead (form chunk k+1 while chunk k is on the GPU or being recorded)
     struct Chunk {
@@ -759,6 +768,7 @@ struct fc2_caller {
         ByteBuf arena;
         std::vector<uint64_t> b_off;
         std::vector<fc2_pair> b_pairs;
+        std::vector<fc2_long_pair> b_long;
     };
     std::deque<Chunk> queued;
     // recorded chunks handed back to the next side: their fragments' strings and vectors keep their
@@ -1345,14 +1355,55 @@ void resolve_chroms(fc2_caller *h) {
     }
 }
 
+// the evaluation results of the pending chunk: the batch's (fc2_caller_submit) and its long pairs'
+// (fc2_caller_submit_long)
+struct Results {
+    const fc2_result *res;
+    const uint64_t *tiemask;
+    uint32_t tw;
+    uint64_t stride;
+    const fc2_long_result *lres;
+    const uint64_t *lties, *ltie_off;
+};
+
 // fills ev (a reused scratch object: its vectors keep their capacity)
-void decode(const fc2_caller *h, int si, const fc2_result &r, const uint64_t *tiemask, uint32_t tw, uint64_t stride,
-            Eval &ev) {
+void decode(const fc2_caller *h, int si, const Results &R, Eval &ev) {
     ev.err = 0;
     ev.msg.clear();
     ev.ties.clear();
     const Span &s = h->spans[si];
-    const fc2_pair &pr = h->b_pairs[(size_t)s.eval];
+    // the pair and its result, from the batch or the long list (the same fields, wider)
+    struct {
+        int64_t a_pos, b_aend, L;
+        uint32_t chrom;
+        uint8_t flags;
+    } pr;
+    struct {
+        int64_t best_x, dist, ov;
+        uint64_t n_ties;
+        uint16_t info;
+    } r;
+    const bool is_long = (s.eval & kLongEval) != 0;
+    const uint64_t ei = (uint64_t)(s.eval & ~kLongEval);
+    if (is_long) {
+        const fc2_long_pair &p = h->b_long[ei];
+        const fc2_long_result &q = R.lres[ei];
+        pr = {p.a_pos, p.b_aend, (int64_t)p.read_len, p.chrom, p.flags};
+        r = {q.best_x, q.dist, q.ov, q.n_ties, q.info};
+    } else {
+        const fc2_pair &p = h->b_pairs[ei];
+        const fc2_result &q = R.res[ei];
+        pr = {p.a_pos, p.b_aend, (int64_t)p.read_len, p.chrom, p.flags};
+        r = {q.best_x, q.dist, q.ov, q.n_ties, q.info};
+    }
+    // tie bit (strand, x): the batch's tie rows, or the pair's own tie words
+    const uint64_t lhalf = is_long ? (R.ltie_off[ei + 1] - R.ltie_off[ei]) / 2 : 0;
+    auto tie_bit = [&](int strand, int64_t xx) -> bool {
+        const uint64_t k = (uint64_t)(xx >> 6), b = (uint64_t)(xx & 63);
+        if (is_long) return (R.lties[R.ltie_off[ei] + (strand ? lhalf : 0) + k] >> b) & 1ull;
+        const uint64_t row = strand ? R.tw / 2 + k : k;
+        return (R.tiemask[row * R.stride + ei] >> b) & 1ull;
+    };
     if (s.tid < 0 || (size_t)s.tid >= h->tid_cid.size() || h->tid_cid[(size_t)s.tid] < 0) {
         (void)chrom_of(h, s.tid);                          // raises for an id outside the header
         throw Fatal{FC2_E_PARAM, "native caller: chromosome of span not resolved"};   // (resolve_chroms)
@@ -1383,7 +1434,7 @@ void decode(const fc2_caller *h, int si, const fc2_result &r, const uint64_t *ti
     }
     if (r.best_x < 0) return;
     const int64_t e = h->o.asize - h->o.margin;
-    const int64_t L = pr.read_len, l = L - 2 * e, x = r.best_x;
+    const int64_t L = pr.L, l = L - 2 * e, x = r.best_x;
     const bool bs = pr.flags & FC2_PAIR_BACKSPLICE, prim_rev = pr.flags & FC2_PAIR_PRIMARY_REV;
     auto coords = [&](int64_t xx, int64_t &st, int64_t &en) {
         const int64_t s0 = pr.b_aend - e - l + xx, e0 = pr.a_pos + e + xx + 1;
@@ -1411,12 +1462,11 @@ void decode(const fc2_caller *h, int si, const fc2_result &r, const uint64_t *ti
         return;
     }
     // all ties in (x asc, '+' before '-') order from the tie mask (hotpath._expand_ties)
-    const uint32_t half = tw / 2;
+    bool have_win = false;
+    std::string winA, winB;
     for (int64_t xx = 0; xx <= l; ++xx) {
-        const uint32_t k = (uint32_t)(xx >> 6), b = (uint32_t)(xx & 63);
         for (int strand = 0; strand < 2; ++strand) {
-            const uint32_t row = strand ? half + k : k;
-            if (!((tiemask[(uint64_t)row * stride + (uint64_t)s.eval] >> b) & 1ull)) continue;
+            if (!tie_bit(strand, xx)) continue;
             Splice t;
             t.span = si;
             t.chrom = chrom;
@@ -1435,27 +1485,31 @@ void decode(const fc2_caller *h, int si, const fc2_result &r, const uint64_t *ti
                 if (!h->fasta) {
                     wg = "NNNN";
                 } else {
-                    const int64_t a0 = pr.a_pos + e, b1 = pr.b_aend - e;
-                    auto window = [&](int64_t lo, int64_t hi) {
-                        std::string w((size_t)std::max<int64_t>(0, hi - lo) + 16, '\0');
-                        int64_t len = 0;
-                        int rc = fc2_fasta_get_upper(h->fasta, (int)pr.chrom, lo, hi, (uint8_t *)&w[0],
-                                                     (int64_t)w.size(), &len);
-                        if (rc == FC2_OK && len > (int64_t)w.size()) {
-                            w.assign((size_t)len, '\0');
-                            rc = fc2_fasta_get_upper(h->fasta, (int)pr.chrom, lo, hi, (uint8_t *)&w[0],
-                                                     (int64_t)w.size(), &len);
-                        }
-                        if (rc != FC2_OK) throw Fatal{rc, fc2_last_error()};
-                        w.resize((size_t)len);
-                        return w;
-                    };
-                    const std::string A = window(a0, a0 + l + 2), B = window(b1 - l - 2, b1);
+                    if (!have_win) {                // the windows once per pair (:900-902)
+                        const int64_t a0 = pr.a_pos + e, b1 = pr.b_aend - e;
+                        auto window = [&](int64_t lo, int64_t hi) {
+                            std::string w((size_t)std::max<int64_t>(0, hi - lo) + 16, '\0');
+                            int64_t len = 0;
+                            int rc = fc2_fasta_get_upper(h->fasta, (int)pr.chrom, lo, hi, (uint8_t *)&w[0],
+                                                         (int64_t)w.size(), &len);
+                            if (rc == FC2_OK && len > (int64_t)w.size()) {
+                                w.assign((size_t)len, '\0');
+                                rc = fc2_fasta_get_upper(h->fasta, (int)pr.chrom, lo, hi, (uint8_t *)&w[0],
+                                                         (int64_t)w.size(), &len);
+                            }
+                            if (rc != FC2_OK) throw Fatal{rc, fc2_last_error()};
+                            w.resize((size_t)len);
+                            return w;
+                        };
+                        winA = window(a0, a0 + l + 2);
+                        winB = window(b1 - l - 2, b1);
+                        have_win = true;
+                    }
                     auto sl = [](const std::string &w, int64_t p) {   // w[p:p+2]
                         if (p >= (int64_t)w.size()) return std::string();
                         return w.substr((size_t)p, 2);
                     };
-                    wg = sl(A, xx) + sl(B, xx);
+                    wg = sl(winA, xx) + sl(winB, xx);
                 }
                 sig = strand ? rev_comp4(wg) : wg;
             } else {
@@ -1621,13 +1675,6 @@ void multi_row_parts(const fc2_caller *h, const Frag &fr, const CKey &circ, cons
     p2 = "\t" + join(cols, "\t") + "\n";
 }
 
-// the evaluation results of the pending chunk
-struct Results {
-    const fc2_result *res;
-    const uint64_t *tiemask;
-    uint32_t tw;
-    uint64_t stride;
-};
 
 // record_hits' per-fragment scratch (find_circ.py:1276-1439): reused objects, so recording a
 // fragment allocates nothing beyond what the junction tables keep
@@ -1656,7 +1703,7 @@ const std::vector<Splice> &find_breakpoints(const fc2_caller *h, int si, const R
     if (k == F.n_ev) {                          // first evaluation of this span in the fragment
         if (F.n_ev == F.evs.size()) { F.evs.emplace_back(); F.ev_si.push_back(0); }
         F.ev_si[k] = si;
-        decode(h, si, R.res[h->spans[si].eval], R.tiemask, R.tw, R.stride, F.evs[k]);
+        decode(h, si, R, F.evs[k]);
         ++F.n_ev;
     }
     const Eval &ev = F.evs[k];
@@ -2097,6 +2144,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
             h->bf_arena.swap(c.arena);
             h->bf_off.swap(c.b_off);
             h->bf_pairs.swap(c.b_pairs);
+            h->bf_long.swap(c.b_long);
             h->spare.pop_back();
         }
     }
@@ -2112,6 +2160,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     h->bf_prop.clear();
     h->bf_off.clear();
     h->bf_pairs.clear();
+    h->bf_long.clear();
     // the chunk's fragments are processed after they are all read, on the next side's workers --
     // unless -B writes records while reading (the reference's writer stops at a failing fragment)
     const bool defer = !fc2::ing::writes_records(h->ing);
@@ -2233,45 +2282,66 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         const size_t nf = h->bf_nfrags;
         const size_t T = std::max<size_t>(1, std::min<size_t>((size_t)h->next_pool->size(),
                                                               nf / std::max<size_t>(1, h->min_range_frags)));
-        std::vector<uint64_t> cnt(T + 1, 0);
-        std::vector<uint8_t> bad_len(T, 0);
+        // (pairs with read parts over FC2_MAX_READ_LEN go to the long list: counted apart)
+        std::vector<uint64_t> cnt(T + 1, 0), cnt_long(T + 1, 0);
         const int64_t min_uq = h->o.min_uniq_qual;
         auto eligible = [&](const Span &sp) { return uniq_ok(sp, min_uq); };
         h->next_pool->run((int)T, [&](int r) {
             fc2::cpu::Scope acct(fc2::cpu::NEXT_POOL);
-            uint64_t n = 0;
+            uint64_t n = 0, nl = 0;
             for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
                 const Frag &fr = h->bf_frags[f];
-                for (int si : fr.circ) n += eligible(h->bf_spans[si]);
-                for (int si : fr.lin) n += eligible(h->bf_spans[si]);
+                for (int pass = 0; pass < 2; ++pass)
+                    for (int si : pass ? fr.lin : fr.circ) {
+                        const Span &sp = h->bf_spans[si];
+                        if (!eligible(sp)) continue;
+                        if (sp.read_len > FC2_MAX_READ_LEN) ++nl; else ++n;
+                    }
             }
             cnt[(size_t)r + 1] = n;
+            cnt_long[(size_t)r + 1] = nl;
         });
-        for (size_t r = 0; r < T; ++r) cnt[r + 1] += cnt[r];
+        for (size_t r = 0; r < T; ++r) {
+            cnt[r + 1] += cnt[r];
+            cnt_long[r + 1] += cnt_long[r];
+        }
         h->bf_pairs.resize(cnt[T]);
         h->bf_off.resize(cnt[T]);
+        h->bf_long.resize(cnt_long[T]);
         h->next_pool->run((int)T, [&](int r) {
             fc2::cpu::Scope acct(fc2::cpu::NEXT_POOL);
-            uint64_t k = cnt[(size_t)r];
+            uint64_t k = cnt[(size_t)r], kl = cnt_long[(size_t)r];
             for (size_t f = nf * (size_t)r / T, f1 = nf * (size_t)(r + 1) / T; f < f1; ++f) {
                 const Frag &fr = h->bf_frags[f];
                 for (int pass = 0; pass < 2; ++pass) {
                     for (int si : pass ? fr.lin : fr.circ) {
                         Span &sp = h->bf_spans[si];
                         if (!eligible(sp)) continue;
-                        fc2_pair pr{};
-                        pr.a_pos = (int32_t)sp.a_pos;
                         // align_B.aend None: not scanned; find_breakpoints raises when it reaches B's
                         // window (decode)
                         const bool none_aend = sp.b_aend < 0;
-                        pr.b_aend = none_aend ? 0 : (int32_t)sp.b_aend;
                         const int32_t c = (sp.tid >= 0 && sp.tid < (int32_t)h->tid2chrom.size()) ? h->tid2chrom[sp.tid] : -1;
+                        const uint8_t flags = (uint8_t)((sp.circ ? FC2_PAIR_BACKSPLICE : 0) |
+                                                        (fr.prim[sp.mate].rev ? FC2_PAIR_PRIMARY_REV : 0) |
+                                                        (c < 0 || none_aend ? FC2_PAIR_SKIP : 0));
+                        if (sp.read_len > FC2_MAX_READ_LEN) {
+                            fc2_long_pair lp{};
+                            lp.read_off = sp.read_off;
+                            lp.read_len = sp.read_len;
+                            lp.chrom = c < 0 ? 0u : (uint32_t)c;
+                            lp.a_pos = (int32_t)sp.a_pos;
+                            lp.b_aend = none_aend ? 0 : (int32_t)sp.b_aend;
+                            lp.flags = flags;
+                            sp.eval = kLongEval | (int64_t)kl;
+                            h->bf_long[kl++] = lp;
+                            continue;
+                        }
+                        fc2_pair pr{};
+                        pr.a_pos = (int32_t)sp.a_pos;
+                        pr.b_aend = none_aend ? 0 : (int32_t)sp.b_aend;
                         pr.chrom = c < 0 ? 0u : (uint32_t)c;
-                        pr.read_len = (uint16_t)std::min<uint32_t>(sp.read_len, 65535u);
-                        if (sp.read_len > FC2_MAX_READ_LEN) bad_len[(size_t)r] = 1;
-                        pr.flags = (uint8_t)((sp.circ ? FC2_PAIR_BACKSPLICE : 0) |
-                                             (fr.prim[sp.mate].rev ? FC2_PAIR_PRIMARY_REV : 0) |
-                                             (c < 0 || none_aend ? FC2_PAIR_SKIP : 0));
+                        pr.read_len = (uint16_t)sp.read_len;
+                        pr.flags = flags;
                         sp.eval = (int64_t)k;
                         h->bf_pairs[k] = pr;
                         h->bf_off[k] = sp.read_off;
@@ -2280,13 +2350,9 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
                 }
             }
         });
-        for (size_t r = 0; r < T; ++r)
-            if (bad_len[r])
-                return fc2::fail(FC2_E_RANGE, "read_part longer than " + std::to_string(FC2_MAX_READ_LEN) +
-                                                  " bases (fc2_result.best_x is 16-bit)");
     }
     if (h->bf_spans.size() > h->bf_nspans) h->bf_spans.resize(h->bf_nspans);
-    h->n_pairs += h->bf_pairs.size();
+    h->n_pairs += h->bf_pairs.size() + h->bf_long.size();
     if (timing) {
         uint64_t grouped = 0;
         const double wait = fc2::ing::take_wait_ms(h->ing, &grouped);
@@ -2306,6 +2372,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     c.arena.swap(h->bf_arena);
     c.b_off.swap(h->bf_off);
     c.b_pairs.swap(h->bf_pairs);
+    c.b_long.swap(h->bf_long);
     std::lock_guard<std::mutex> lk(h->qmu);
     h->queued.push_back(std::move(c));           // moved vectors keep their buffers: *b stays valid
     const fc2_caller::Chunk &q = h->queued.back();
@@ -2313,6 +2380,8 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
     b->reads = (const uint8_t *)q.arena.data();
     b->read_off = q.b_off.data();
     b->pairs = q.b_pairs.data();
+    b->n_long = q.b_long.size();
+    b->long_pairs = q.b_long.data();
     if (eof) *eof = h->eof && !h->next_err ? 1 : 0;   // an error still to report: not the end yet
     return FC2_OK;
 }
@@ -2331,18 +2400,23 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
         if (h->queued.empty())
             return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: no chunk handed out by fc2_caller_next");
         fc2_caller::Chunk &c = h->queued.front();
+        if (!c.b_long.empty() && !h->l_staged)   // (the chunk stays queued: they may still be staged)
+            return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: the chunk's long pairs have no results "
+                                          "(fc2_caller_submit_long)");
         h->frags.swap(c.frags);
         h->nfrags = c.nfrags;
         h->spans.swap(c.spans);
         h->arena.swap(c.arena);
         h->b_off.swap(c.b_off);
         h->b_pairs.swap(c.b_pairs);
+        h->b_long.swap(c.b_long);
         h->queued.pop_front();
+        h->l_staged = false;                     // (l_res / l_ties stay for this chunk's record_hits)
     }
     if (!h->b_pairs.empty() && !results) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: results missing");
     if (h->o.allhits && !h->b_pairs.empty() && (!tiemask || tw < 2 || stride < h->b_pairs.size()))
         return fc2::fail(FC2_E_PARAM, "fc2_caller_submit: --all-hits needs the tie mask");
-    const Results R{results, tiemask, tw, stride};
+    const Results R{results, tiemask, tw, stride, h->l_res.data(), h->l_ties.data(), h->l_tie_off.data()};
     int rc = FC2_OK;
     try {
         resolve_chroms(h);
@@ -2421,10 +2495,42 @@ extern "C" int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const
     c.arena.swap(h->arena);
     c.b_off.swap(h->b_off);
     c.b_pairs.swap(h->b_pairs);
+    c.b_long.swap(h->b_long);
     h->nfrags = 0;
     std::lock_guard<std::mutex> lk(h->qmu);
     if (h->spare.size() < 4) h->spare.push_back(std::move(c));
     return rc;
+}
+
+extern "C" int fc2_caller_submit_long(fc2_caller *h, const fc2_long_result *results, uint64_t n_long,
+                                      const uint64_t *ties, uint64_t n_tie_words) {
+    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_long: null argument");
+    std::lock_guard<std::mutex> lk(h->qmu);
+    if (h->queued.empty()) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_long: no chunk handed out by fc2_caller_next");
+    const std::vector<fc2_long_pair> &lp = h->queued.front().b_long;
+    if (n_long != lp.size())
+        return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_long: " + std::to_string(n_long) + " results for " +
+                                          std::to_string(lp.size()) + " long pairs");
+    if (n_long && !results) return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_long: results missing");
+    fc2_params p{};
+    p.asize = h->o.asize;
+    p.margin = h->o.margin;
+    p.maxdist = h->o.maxdist;
+    p.noncanonical = h->o.noncanonical;
+    p.allhits = h->o.allhits;
+    h->l_tie_off.resize(n_long + 1);
+    if (int rc = fc2_long_geometry(&p, n_long, lp.data(), nullptr, h->l_tie_off.data())) return rc;
+    if (h->o.allhits) {
+        if (n_tie_words != h->l_tie_off[n_long] || (n_tie_words && !ties))
+            return fc2::fail(FC2_E_PARAM, "fc2_caller_submit_long: --all-hits needs " +
+                                              std::to_string(h->l_tie_off[n_long]) + " tie words");
+        h->l_ties.assign(ties, ties + n_tie_words);
+    } else {
+        h->l_ties.clear();
+    }
+    h->l_res.assign(results, results + n_long);
+    h->l_staged = true;
+    return FC2_OK;
 }
 
 extern "C" int fc2_caller_submit_compact(fc2_caller *h, const void *words, int width, uint64_t n_words,

@@ -354,6 +354,54 @@ extern "C" int fc2_ctx_sync(fc2_ctx *c) {
     return FC2_OK;
 }
 
+extern "C" int fc2_ctx_scan_long(fc2_ctx *c, const fc2_params *p, uint64_t n, const uint8_t *reads,
+                                 const fc2_long_pair *pairs, fc2_long_result *results, uint64_t *ties) {
+    if (!c) return fc2::fail(FC2_E_PARAM, "fc2_ctx_scan_long: null context");
+    c->err.clear();
+    int rc = fc2::validate_params(p);
+    if (rc) return keep(c, rc);
+    if (c->pending) return keep(c, fc2::fail(FC2_E_PARAM, "fc2_ctx_scan_long: a batch is queued (fc2_ctx_sync)"));
+    if (!c->have_genome)
+        return keep(c, fc2::fail(FC2_E_PARAM, "fc2_ctx_scan_long: no genome (fc2_ctx_genome_load; NULL = dummy genome)"));
+    if (n == 0) return FC2_OK;
+    if (!reads || !pairs || !results || (p->allhits && !ties))
+        return keep(c, fc2::fail(FC2_E_PARAM, "fc2_ctx_scan_long: null argument"));
+    if ((rc = use_device(c))) return keep(c, rc);
+    uint64_t arena = 0;
+    std::vector<uint64_t> tie_off(n + 1), off(n);
+    if ((rc = fc2_long_geometry(p, n, pairs, &arena, tie_off.data()))) return keep(c, rc);
+    std::vector<uint8_t> h_arena((size_t)std::max<uint64_t>(arena, 16));
+    if ((rc = fc2_long_fill(p, c->fa, n, reads, pairs, off.data(), h_arena.data()))) return keep(c, rc);
+    const uint64_t nt = p->allhits ? tie_off[n] : 0;
+    // device buffers of this call only (long pairs are rare): pairs, offsets, arena, tie offsets,
+    // results, ties
+    DevBuf d_lp, d_off, d_arena, d_toff, d_res, d_ties;
+    auto cleanup = [&] { for (DevBuf *b : {&d_lp, &d_off, &d_arena, &d_toff, &d_res, &d_ties}) b->release(); };
+    const hipStream_t s = c->stream;
+    if ((rc = d_lp.reserve(n * sizeof(fc2_long_pair), "long pairs", false)) || (rc = d_off.reserve(n * 8, "long offsets", false)) ||
+        (rc = d_arena.reserve(h_arena.size(), "long arena", false)) || (rc = d_toff.reserve((n + 1) * 8, "long tie offsets", false)) ||
+        (rc = d_res.reserve(n * sizeof(fc2_long_result), "long results", false)) ||
+        (nt && (rc = d_ties.reserve(nt * 8, "long ties", false)))) {
+        cleanup();
+        return keep(c, rc);
+    }
+    if ((rc = h2d(d_lp, pairs, n * sizeof(fc2_long_pair), s)) || (rc = h2d(d_off, off.data(), n * 8, s)) ||
+        (rc = h2d(d_arena, h_arena.data(), h_arena.size(), s)) || (rc = h2d(d_toff, tie_off.data(), (n + 1) * 8, s)) ||
+        (rc = fc2_bp_scan_long_launch(p, n, d_lp.as<fc2_long_pair>(), d_off.as<uint64_t>(), d_arena.as<uint8_t>(),
+                                      d_toff.as<uint64_t>(), d_res.as<fc2_long_result>(), nt ? d_ties.as<uint64_t>() : nullptr, s))) {
+        (void)hipStreamSynchronize(s);      // the host vectors must outlive the queued copies
+        cleanup();
+        return keep(c, rc);
+    }
+    hipError_t he = hipMemcpyAsync(results, d_res.p, n * sizeof(fc2_long_result), hipMemcpyDeviceToHost, s);
+    if (he == hipSuccess && nt) he = hipMemcpyAsync(ties, d_ties.p, nt * 8, hipMemcpyDeviceToHost, s);
+    const hipError_t se = hipStreamSynchronize(s);
+    cleanup();
+    if (he != hipSuccess) return keep(c, hip_fail(he, "fc2_ctx_scan_long D2H"));
+    if (se != hipSuccess) return keep(c, hip_fail(se, "fc2_ctx_scan_long"));
+    return FC2_OK;
+}
+
 extern "C" void *fc2_ctx_stream(const fc2_ctx *c) { return c ? (void *)c->stream : nullptr; }
 
 extern "C" const char *fc2_ctx_last_error(const fc2_ctx *c) { return c ? c->err.c_str() : ""; }

@@ -890,9 +890,54 @@ extern "C" int fc2_pack_windows(const fc2_params *p, const fc2_fasta *f, uint64_
 // 16-B header + I + A's slot of l+3 bytes + B's slot of 2l+3 bytes (fc2_bytes_view): an irregular
 // window pair -- A cut short past the chromosome's end, B padded long before its start -- compares
 // B[x+2 : x+2+lenI-lenA] (find_circ.py:907-908), which reaches byte 2l+2 of B
-static inline uint64_t block_bytes(int l) {
-    const uint64_t lc = (uint64_t)std::max(0, l);
+static inline uint64_t block_bytes(int64_t l) {
+    const uint64_t lc = (uint64_t)std::max<int64_t>(0, l);
     return (16 + lc + (lc + 3) + (2 * lc + 3) + 3) & ~3ull;
+}
+
+// One pair's block of the byte arena at blk: the read part's internal bytes and both windows
+// (A, B: scratch strings).  L = len(read_part), e = the effective anchor.
+static int fill_block(const fc2_fasta *f, int e, int64_t L, uint32_t chrom, int64_t a_pos, int64_t b_aend,
+                      const uint8_t *read, uint8_t *blk, std::string &A, std::string &B) {
+    const int64_t l = L - 2 * (int64_t)e;
+    // internal = read[e:-e] with Python's slice rules (find_circ.py:895): the read's middle l bases
+    // for e > 0; for e <= 0 read[e:-e] is '' (e == 0) or read[max(L+e, 0) : min(-e, L)]
+    int64_t i0 = e, i1 = L - e;
+    if (e <= 0) { i0 = std::max<int64_t>(L + e, 0); i1 = e == 0 ? 0 : std::min<int64_t>(-e, L); }
+    const int32_t lenI = l < 0 ? 0 : (int32_t)std::max<int64_t>(0, i1 - i0);
+    int64_t fullA = 0, fullB = 0, tailB = 0;
+    A.clear(); B.clear();
+    if (l >= 0) {
+        const int64_t flank = l + 2;
+        // only min(length, slot) bytes of a window are stored (slots of l + 3 and 2l + 3 bytes); the
+        // header keeps the full length and, for a one-base internal part, the mismatches of B's bytes
+        // past its slot against that base
+        const int c1 = lenI == 1 ? (int)upc(read[i0]) : -1;
+        int rc = get_upper_impl(f, (int)chrom, a_pos + e, a_pos + e + flank, A, (size_t)flank + 1, &fullA);
+        if (rc) return rc;
+        rc = get_upper_impl(f, (int)chrom, b_aend - e - flank, b_aend - e, B, (size_t)(2 * flank - 1), &fullB, c1,
+                            lenI == 1 ? &tailB : nullptr);
+        if (rc) return rc;
+    }
+    // a window of unexpected length (outside get_data's defined range) keeps its slot's bytes: the
+    // kernel compares what the reference's string form reads of them (at most B[:2l+3] when the
+    // lengths add up), sees a length mismatch numpy cannot broadcast (ERR_WIN) or, where numpy
+    // broadcasts a 1-byte operand, counts B's bytes past the slot through tailB (bp_bytes_kernel)
+    const int32_t lenA = (int32_t)std::min<int64_t>(fullA, INT32_MAX);
+    const int32_t lenB = (int32_t)std::min<int64_t>(fullB, INT32_MAX);
+    const int32_t tail = (int32_t)std::min<int64_t>(tailB, INT32_MAX);
+    memcpy(blk, &lenI, 4);
+    memcpy(blk + 4, &lenA, 4);
+    memcpy(blk + 8, &lenB, 4);
+    memcpy(blk + 12, &tail, 4);
+    uint8_t *q = blk + 16;
+    for (int64_t j = 0; j < lenI; ++j) q[j] = upc(read[i0 + j]);
+    q += lenI;
+    const uint64_t lc = (uint64_t)std::max<int64_t>(0, l);
+    memcpy(q, A.data(), std::min<size_t>(A.size(), lc + 3));
+    q += lc + 3;
+    memcpy(q, B.data(), std::min<size_t>(B.size(), 2 * lc + 3));
+    return FC2_OK;
 }
 
 extern "C" int fc2_bytepath_size(const fc2_params *p, uint64_t n, const fc2_pair *pairs, uint64_t *m, uint64_t *arena_bytes) {
@@ -902,7 +947,7 @@ extern "C" int fc2_bytepath_size(const fc2_params *p, uint64_t n, const fc2_pair
     uint64_t mm = 0, bytes = 0;
     for (uint64_t i = 0; i < n; ++i) {
         if (!(pairs[i].flags & FC2_PAIR_BYTEPATH)) continue;
-        bytes += block_bytes((int)pairs[i].read_len - 2 * e);
+        bytes += block_bytes((int64_t)pairs[i].read_len - 2 * e);
         ++mm;
     }
     if (m) *m = mm;
@@ -921,52 +966,60 @@ extern "C" int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64
     for (uint64_t i = 0; i < n; ++i) {
         const fc2_pair &pr = pairs[i];
         if (!(pr.flags & FC2_PAIR_BYTEPATH)) continue;
-        const int L = pr.read_len;
-        const int l = L - 2 * e;
-        // internal = read[e:-e] with Python's slice rules (find_circ.py:895): the read's middle l bases
-        // for e > 0; for e <= 0 read[e:-e] is '' (e == 0) or read[max(L+e, 0) : min(-e, L)]
-        int i0 = e, i1 = L - e;
-        if (e <= 0) { i0 = std::max(L + e, 0); i1 = e == 0 ? 0 : std::min(-e, L); }
-        const int32_t lenI = l < 0 ? 0 : std::max(0, i1 - i0);
-        int64_t fullA = 0, fullB = 0, tailB = 0;
-        A.clear(); B.clear();
-        if (l >= 0) {
-            const int64_t flank = l + 2;
-            // only min(length, slot) bytes of a window are stored (slots of l + 3 and 2l + 3 bytes); the
-            // header keeps the full length and, for a one-base internal part, the mismatches of B's bytes
-            // past its slot against that base
-            const int c1 = lenI == 1 ? (int)upc(reads[read_off[i] + i0]) : -1;
-            rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.a_pos + e, (int64_t)pr.a_pos + e + flank, A,
-                                (size_t)flank + 1, &fullA);
-            if (rc) return rc;
-            rc = get_upper_impl(f, (int)pr.chrom, (int64_t)pr.b_aend - e - flank, (int64_t)pr.b_aend - e, B,
-                                (size_t)(2 * flank - 1), &fullB, c1, lenI == 1 ? &tailB : nullptr);
-            if (rc) return rc;
-        }
-        // a window of unexpected length (outside get_data's defined range) keeps its slot's bytes: the
-        // kernel compares what the reference's string form reads of them (at most B[:2l+3] when the
-        // lengths add up), sees a length mismatch numpy cannot broadcast (ERR_WIN) or, where numpy
-        // broadcasts a 1-byte operand, counts B's bytes past the slot through tailB (bp_bytes_kernel)
-        const int32_t lenA = (int32_t)std::min<int64_t>(fullA, INT32_MAX);
-        const int32_t lenB = (int32_t)std::min<int64_t>(fullB, INT32_MAX);
+        if ((rc = fill_block(f, e, pr.read_len, pr.chrom, pr.a_pos, pr.b_aend, reads + read_off[i], arena + pos, A, B)))
+            return rc;
         index[k] = i;
         bpairs[k] = pr;
         off[k] = pos;
-        uint8_t *blk = arena + pos;
-        const int32_t tail = (int32_t)std::min<int64_t>(tailB, INT32_MAX);
-        memcpy(blk, &lenI, 4);
-        memcpy(blk + 4, &lenA, 4);
-        memcpy(blk + 8, &lenB, 4);
-        memcpy(blk + 12, &tail, 4);
-        uint8_t *q = blk + 16;
-        for (int j = 0; j < lenI; ++j) q[j] = upc(reads[read_off[i] + i0 + j]);
-        q += lenI;
-        const int lc = std::max(0, l);
-        memcpy(q, A.data(), std::min<size_t>(A.size(), (size_t)lc + 3));
-        q += lc + 3;
-        memcpy(q, B.data(), std::min<size_t>(B.size(), 2 * (size_t)lc + 3));
-        pos += block_bytes(l);
+        pos += block_bytes((int64_t)pr.read_len - 2 * e);
         ++k;
+    }
+    return FC2_OK;
+}
+
+// ---- long pairs (include/fc2_bp.h fc2_long_pair) ------------------------------------------------
+extern "C" int fc2_long_geometry(const fc2_params *p, uint64_t n, const fc2_long_pair *pairs, uint64_t *arena_bytes,
+                                 uint64_t *tie_off) {
+    int rc = validate_params(p);
+    if (rc) return rc;
+    if (n && !pairs) return fail(FC2_E_PARAM, "fc2_long_geometry: null pairs");
+    const int e = eff_anchor(p);
+    uint64_t bytes = 0, words = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const int64_t l = (int64_t)pairs[i].read_len - 2 * e;
+        bytes += block_bytes(l);
+        if (tie_off) tie_off[i] = words;
+        words += 2 * (uint64_t)((std::max<int64_t>(l, 0) + 2 + 63) / 64);   // x in [0, l] per strand
+    }
+    if (tie_off) tie_off[n] = words;
+    if (arena_bytes) *arena_bytes = bytes;
+    return FC2_OK;
+}
+
+extern "C" int fc2_long_fill(const fc2_params *p, const fc2_fasta *f, uint64_t n, const uint8_t *reads,
+                             const fc2_long_pair *pairs, uint64_t *off, uint8_t *arena) {
+    int rc = validate_params(p);
+    if (rc) return rc;
+    if (n && (!reads || !pairs || !off || !arena)) return fail(FC2_E_PARAM, "fc2_long_fill: null argument");
+    const int e = eff_anchor(p);
+    const int nch = f ? (int)f->chroms.size() : 0;
+    uint64_t pos = 0;
+    std::string A, B;
+    for (uint64_t i = 0; i < n; ++i) {
+        const fc2_long_pair &pr = pairs[i];
+        if (pr.read_len > (uint32_t)INT32_MAX) return fail(FC2_E_RANGE, "fc2_long_fill: read part of 2^31 bases or more");
+        off[i] = pos;
+        const int64_t l = (int64_t)pr.read_len - 2 * e;
+        if (!(pr.flags & FC2_PAIR_SKIP)) {
+            if (f && (int)pr.chrom >= nch)
+                return fail(FC2_E_KEY, "long pair " + std::to_string(i) +
+                                           ": chromosome not in the genome index (reference KeyError, find_circ.py:193)");
+            if ((rc = fill_block(f, e, pr.read_len, pr.chrom, pr.a_pos, pr.b_aend, reads + pr.read_off, arena + pos, A, B)))
+                return rc;
+        } else {
+            memset(arena + pos, 0, 16);
+        }
+        pos += block_bytes(l);
     }
     return FC2_OK;
 }

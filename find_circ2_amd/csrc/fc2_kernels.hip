@@ -438,28 +438,27 @@ __device__ __forceinline__ unsigned code_of(uint8_t c) {
     return c == 'A' ? 0u : c == 'C' ? 1u : c == 'G' ? 2u : c == 'T' ? 3u : 4u;
 }
 
-__global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_bytes_view v, uint64_t *__restrict__ out,
-                                                          uint64_t *__restrict__ tiemask, uint32_t tw, uint64_t stride) {
-    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-    if (k >= v.m) return;
-    const uint64_t i = v.index[k];
-    const fc2_pair pr = v.pairs[k];
-    const uint8_t *blk = v.arena + v.off[k];
+// find_breakpoints (find_circ.py:854-974) of one pair on the bytes of its arena block (fc2_bytes_view
+// layout): the best hit and its tie count into Bst, a reference error into err, the best hit's
+// 4-mer into gtag12; with --all-hits every tie of the best score goes to tie(strand, x) in a second
+// pass (x ascending, as the stable sort keeps them).  L = len(read_part) (< 2^31).
+template <class Tie>
+__device__ __forceinline__ void bytes_eval(const fc2_params &p, int L, uint8_t flags, const uint8_t *blk, Best &Bst,
+                                           unsigned &err, unsigned &gtag12, Tie tie) {
+    err = 0;
+    gtag12 = 0;
+    const int e = p.asize - p.margin;
+    const int l = L - 2 * e;
+    if ((flags & FC2_PAIR_SKIP) || l < 0) return;
     const int lenI = ((const int32_t *)blk)[0], lenA = ((const int32_t *)blk)[1], lenB = ((const int32_t *)blk)[2];
     const int tailB = ((const int32_t *)blk)[3];      // lenI == 1: B's bytes past its slot that differ from I[0]
-    const int e = p.asize - p.margin;
-    const int l = (int)pr.read_len - 2 * e;
-    const int64_t lc = l < 0 ? 0 : l;
+    const int64_t lc = l;
     const int64_t slotA = lc + 3, slotB = 2 * lc + 3;   // stored bytes per window (fc2_bytepath_fill)
     const uint8_t *I = blk + 16;
     const uint8_t *Af = I + lenI;
     const uint8_t *Bf = Af + slotA;
     const int64_t sB = lenB < slotB ? lenB : slotB;     // A is only read below x + 2 <= l + 2 < slotA
     const bool want_ties = p.allhits != 0;
-    const uint32_t half = tw / 2;
-    if (want_ties)
-        for (uint32_t w = 0; w < tw; ++w) tiemask[(uint64_t)w * stride + i] = 0;
-    if ((pr.flags & FC2_PAIR_SKIP) || l < 0) { out[i] = nohit_result(0); return; }
 
     // Windows normally have l+2 bytes.  Outside get_data's defined range they can
     // come back shorter or longer (find_circ.py:194-211), and with asize <= margin the
@@ -472,11 +471,9 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
     int totB = 0;
     if (regular)
         for (int j = 0; j < l; ++j) totB += Bf[j + 2] != I[j];
-    const int prim_minus = (pr.flags & FC2_PAIR_PRIMARY_REV) ? 1 : 0;
+    const int prim_minus = (flags & FC2_PAIR_PRIMARY_REV) ? 1 : 0;
     const int sp_plus = p.strandpref ? (prim_minus ? 0 : 100) : 0;
     const int sp_minus = p.strandpref ? (prim_minus ? 100 : 0) : 0;
-    Best Bst;
-    unsigned err = 0;
     for (int pass = 0; pass < (want_ties ? 2 : 1); ++pass) {
         int d = totB;
         for (int x = 0; x <= l; ++x) {
@@ -521,25 +518,78 @@ __global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_byte
                 const int s1 = 20 * cp - 10 * d - ov + sp_plus, s2 = 20 * cm - 10 * d - ov + sp_minus;
                 if (pass == 0) { add_hit(Bst, x, 0, d, ov, s1); add_hit(Bst, x, 1, d, ov, s2); }
                 else {
-                    if (s1 == Bst.best_score) tiemask[(uint64_t)(x >> 6) * stride + i] |= 1ull << (x & 63);
-                    if (s2 == Bst.best_score) tiemask[(uint64_t)(half + (x >> 6)) * stride + i] |= 1ull << (x & 63);
+                    if (s1 == Bst.best_score) tie(0, x);
+                    if (s2 == Bst.best_score) tie(1, x);
                 }
             } else if (cp || cm) {
                 const int s = 20 - 10 * d - ov + (cm ? sp_minus : sp_plus);
                 if (pass == 0) add_hit(Bst, x, cm, d, ov, s);
-                else if (s == Bst.best_score)
-                    tiemask[(uint64_t)((cm ? half : 0) + (x >> 6)) * stride + i] |= 1ull << (x & 63);
+                else if (s == Bst.best_score) tie(cm, x);
             }
         }
         if (err || !Bst.n_hits) break;
     }
-    if (err) { out[i] = nohit_result(err); return; }
-    unsigned gtag12 = 0;
-    if (Bst.n_hits) {
+    if (!err && Bst.n_hits) {
         const int x = Bst.best_x;
         gtag12 = code_of(Af[x]) | (code_of(Af[x + 1]) << 3) | (code_of(Bf[x]) << 6) | (code_of(Bf[x + 1]) << 9);
     }
-    out[i] = pack_result(Bst, gtag12, 0);
+}
+
+__global__ __launch_bounds__(kBlock) void bp_bytes_kernel(fc2_params p, fc2_bytes_view v, uint64_t *__restrict__ out,
+                                                          uint64_t *__restrict__ tiemask, uint32_t tw, uint64_t stride) {
+    const uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (k >= v.m) return;
+    const uint64_t i = v.index[k];
+    const fc2_pair pr = v.pairs[k];
+    const uint32_t half = tw / 2;
+    if (p.allhits)
+        for (uint32_t w = 0; w < tw; ++w) tiemask[(uint64_t)w * stride + i] = 0;
+    Best Bst;
+    unsigned err, gtag12;
+    bytes_eval(p, (int)pr.read_len, pr.flags, v.arena + v.off[k], Bst, err, gtag12, [&](int minus, int x) {
+        tiemask[(uint64_t)((minus ? half : 0) + (uint32_t)(x >> 6)) * stride + i] |= 1ull << (x & 63);
+    });
+    out[i] = err ? nohit_result(err) : pack_result(Bst, gtag12, 0);
+}
+
+// Long pairs (fc2_long_pair): the same evaluation with 32-bit results; pair j's ties at
+// ties[tie_off[j] ...] ('+' half, then '-' half)
+__global__ __launch_bounds__(kBlock) void bp_long_kernel(fc2_params p, uint64_t n, const fc2_long_pair *__restrict__ pairs,
+                                                         const uint64_t *__restrict__ off, const uint8_t *__restrict__ arena,
+                                                         const uint64_t *__restrict__ tie_off,
+                                                         fc2_long_result *__restrict__ out, uint64_t *__restrict__ ties) {
+    const uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (j >= n) return;
+    const fc2_long_pair pr = pairs[j];
+    uint64_t *tj = nullptr;
+    uint64_t half = 0;
+    if (p.allhits) {
+        tj = ties + tie_off[j];
+        half = (tie_off[j + 1] - tie_off[j]) / 2;
+        for (uint64_t w = 0; w < 2 * half; ++w) tj[w] = 0;
+    }
+    Best Bst;
+    unsigned err, gtag12;
+    bytes_eval(p, (int)pr.read_len, pr.flags, arena + off[j], Bst, err, gtag12, [&](int minus, int x) {
+        tj[(minus ? half : 0) + (uint64_t)(x >> 6)] |= 1ull << (x & 63);
+    });
+    fc2_long_result r;
+    r._pad = 0;
+    if (err || !Bst.n_hits) {
+        r.best_x = -1;
+        r.n_ties = 0;
+        r.dist = 0;
+        r.ov = 0;
+        r.info = (uint16_t)(FC2_RES_DONE | err);
+    } else {
+        r.best_x = Bst.best_x;
+        r.n_ties = Bst.n_hits >= 2 ? (uint32_t)Bst.n_ties : 1u;                   // find_circ.py:961-972
+        r.dist = (uint8_t)(Bst.best_dist > 255 ? 255 : Bst.best_dist);
+        r.ov = (uint8_t)Bst.best_ov;
+        r.info = (uint16_t)(FC2_RES_DONE | (Bst.best_minus ? FC2_RES_MINUS : 0u) |
+                            ((gtag12 << FC2_RES_GTAG_SHIFT) & FC2_RES_GTAG_MASK));
+    }
+    out[j] = r;
 }
 
 // ---------------------------------------------------------------------------
@@ -1074,6 +1124,20 @@ extern "C" int fc2_bp_scan_bytes_launch(const fc2_params *p, const fc2_bytes_vie
     hipLaunchKernelGGL(bp_bytes_kernel, dim3(grid_for(v->m, kBlock)), dim3(kBlock), 0, s, *p, *v,
                        reinterpret_cast<uint64_t *>(results), tiemask, tw, stride);
     return hip_check(hipGetLastError(), "bp_bytes_kernel launch");
+}
+
+extern "C" int fc2_bp_scan_long_launch(const fc2_params *p, uint64_t n, const fc2_long_pair *pairs, const uint64_t *off,
+                                       const uint8_t *arena, const uint64_t *tie_off, fc2_long_result *results,
+                                       uint64_t *ties, void *stream) {
+    int rc = fc2::validate_params(p);
+    if (rc) return rc;
+    if (n == 0) return FC2_OK;
+    if (!pairs || !off || !arena || !results) return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_long_launch: null argument");
+    if (p->allhits && (!ties || !tie_off))
+        return fc2::fail(FC2_E_PARAM, "fc2_bp_scan_long_launch: --all-hits needs the tie words and their offsets");
+    hipLaunchKernelGGL(bp_long_kernel, dim3(grid_for(n, kBlock)), dim3(kBlock), 0, (hipStream_t)stream, *p, n, pairs,
+                       off, arena, tie_off, results, ties);
+    return hip_check(hipGetLastError(), "bp_long_kernel launch");
 }
 
 extern "C" int fc2_synth_genome_launch(uint64_t seed, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,

@@ -666,31 +666,82 @@ def decode_splices(options: Options, genome: Genome, batch: PairBatch, out: Scan
     tm = None
     if options.allhits:
         tm = out.tiemask[:batch.tw * batch.stride].cpu().numpy().view(np.uint64).reshape(batch.tw, batch.stride)
-    result: List[List[Splice]] = []
-    for i in range(batch.n):
-        span = spans[i] if spans is not None else None
-        if evaluated[i] and (a["err_key"][i] or a["err_win"][i]):
-            result.append(KeyError("splice signal with a byte outside ACGTN (find_circ.py:927)") if a["err_key"][i]
-                          else BreakpointError(WINDOW_SHAPE_MESSAGE))
-            continue
-        if not a["hit"][i] or not evaluated[i]:
-            result.append([])
-            continue
-        chrom = genome.names[hp["chrom"][i]] if not genome.dummy else (span.chrom if span is not None else "")
-        g = gtag_str(int(a["gtag12"][i]))
-        strand = '-' if a["minus"][i] else '+'
-        sig = rev_comp4(g) if strand == '-' else g
-        dist = int(a["dist"][i])
-        dist_v = False if options.maxdist == 0 else dist     # simple_match returns a bool (find_circ.py:865-871)
-        s = Splice(span, chrom, int(a["start"][i]), int(a["end"][i]), strand, dist_v, int(a["ov"][i]), sig)
-        nt = int(a["n_ties"][i])
-        s.n_hits = nt
-        s._score = _score(options, sig, dist, s.ov, strand, hp["flags"][i])
-        ties = [s]
-        if options.allhits and nt > 1:
-            ties = _expand_ties(options, genome, hp, i, tm[:, int(slot[i])], s, span, chrom)
-        result.append(ties)
-    return result
+    return [_splices_of(options, genome, hp, a, evaluated, i, spans[i] if spans is not None else None,
+                        lambda i=i: tm[:, int(slot[i])]) for i in range(batch.n)]
+
+
+def _splices_of(options: Options, genome: Genome, hp, a, evaluated, i: int, span, tie_words):
+    """Pair i's find_breakpoints result from its decoded first tie (``a``, first_tie_arrays) and,
+    with --all-hits, its tie words (``tie_words()``: '+' half then '-' half): the tie list, or the
+    exception the reference raises."""
+    if evaluated[i] and (a["err_key"][i] or a["err_win"][i]):
+        return (KeyError("splice signal with a byte outside ACGTN (find_circ.py:927)") if a["err_key"][i]
+                else BreakpointError(WINDOW_SHAPE_MESSAGE))
+    if not a["hit"][i] or not evaluated[i]:
+        return []
+    chrom = genome.names[hp["chrom"][i]] if not genome.dummy else (span.chrom if span is not None else "")
+    g = gtag_str(int(a["gtag12"][i]))
+    strand = '-' if a["minus"][i] else '+'
+    sig = rev_comp4(g) if strand == '-' else g
+    dist = int(a["dist"][i])
+    dist_v = False if options.maxdist == 0 else dist     # simple_match returns a bool (find_circ.py:865-871)
+    s = Splice(span, chrom, int(a["start"][i]), int(a["end"][i]), strand, dist_v, int(a["ov"][i]), sig)
+    nt = int(a["n_ties"][i])
+    s.n_hits = nt
+    s._score = _score(options, sig, dist, s.ov, strand, hp["flags"][i])
+    if options.allhits and nt > 1:
+        return _expand_ties(options, genome, hp, i, tie_words(), s, span, chrom)
+    return [s]
+
+
+def scan_long(options: Options, genome: Genome, reads, long_pairs: np.ndarray, device=None):
+    """find_breakpoints of anchor pairs whose read parts exceed MAX_READ_LEN (fc2_long_pair records,
+    include/fc2_bp.h; the reference's x-loop has no length limit, find_circ.py:873, :904-906): the
+    read parts and windows are laid out on the host (fc2_long_fill, windows from the mmap'd FASTA
+    with get_data's semantics), the byte-exact long kernel runs on ``device`` (default: the genome's),
+    and the call waits for it.  ``reads``: the buffer the records' read_off index (a uint8 array or an
+    address).  Returns (results LONG_RESULT_DTYPE [n], tie words uint64 or None, tie_off [n+1])."""
+    torch = _torch()
+    dev = torch.device(device) if device is not None else genome.device
+    lp = np.ascontiguousarray(long_pairs, N.LONG_PAIR_DTYPE)
+    n = len(lp)
+    p = options.params()
+    nbytes = ctypes.c_uint64()
+    tie_off = np.zeros(n + 1, np.uint64)
+    N.check(N.lib().fc2_long_geometry(ctypes.byref(p), n, lp.ctypes.data, ctypes.byref(nbytes), tie_off.ctypes.data))
+    res = np.zeros(n, N.LONG_RESULT_DTYPE)
+    if n == 0:
+        return res, (np.zeros(0, np.uint64) if options.allhits else None), tie_off
+    off = np.zeros(n, np.uint64)
+    arena = np.zeros(max(16, int(nbytes.value)), np.uint8)
+    rptr = reads if isinstance(reads, int) else np.ascontiguousarray(reads, np.uint8).ctypes.data
+    N.check(N.lib().fc2_long_fill(ctypes.byref(p), genome.fasta if not genome.dummy else None, n, rptr, lp.ctypes.data,
+                                  off.ctypes.data, arena.ctypes.data))
+    d_pairs = torch.from_numpy(lp.view(np.uint8)).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_arena = torch.from_numpy(arena).to(dev)
+    d_res = torch.empty(n * N.LONG_RESULT_DTYPE.itemsize, dtype=torch.uint8, device=dev)
+    d_toff = d_ties = None
+    if options.allhits:
+        d_toff = torch.from_numpy(tie_off.view(np.int64)).to(dev)
+        d_ties = torch.empty(max(1, int(tie_off[n])), dtype=torch.int64, device=dev)
+    s = torch.cuda.current_stream(dev)
+    N.check(N.lib().fc2_bp_scan_long_launch(ctypes.byref(p), n, d_pairs.data_ptr(), d_off.data_ptr(),
+                                            d_arena.data_ptr(), d_toff.data_ptr() if d_toff is not None else None,
+                                            d_res.data_ptr(), d_ties.data_ptr() if d_ties is not None else None,
+                                            s.cuda_stream))
+    res = d_res.cpu().numpy().view(N.LONG_RESULT_DTYPE).copy()
+    ties = d_ties.cpu().numpy().view(np.uint64)[:int(tie_off[n])].copy() if d_ties is not None else None
+    return res, ties, tie_off
+
+
+def decode_long_splices(options: Options, genome: Genome, long_pairs: np.ndarray, res: np.ndarray, ties, tie_off,
+                        spans: Sequence = None) -> List:
+    """decode_splices for the results of scan_long (pairs' tie words at ties[tie_off[j]:tie_off[j+1]])."""
+    a = first_tie_arrays(options, long_pairs, res)
+    evaluated = (long_pairs["flags"] & N.PAIR_SKIP) == 0
+    return [_splices_of(options, genome, long_pairs, a, evaluated, j, spans[j] if spans is not None else None,
+                        lambda j=j: ties[int(tie_off[j]):int(tie_off[j + 1])]) for j in range(len(long_pairs))]
 
 
 def _score(options, sig, dist, ov, strand, flags):
@@ -859,7 +910,7 @@ class BreakpointEngine:
         JunctionSpan.engine = self
         return self
 
-    def find_breakpoints_batch(self, spans: Sequence[JunctionSpan]) -> List:
+    def find_breakpoints_batch(self, spans: Sequence[JunctionSpan], locus_order: bool = False) -> List:
         """``find_breakpoints()`` of every span in ONE launch.  Entry i is span i's tie list, or
         -- where the reference method would raise -- the exception instance, so a caller that
         evaluates spans speculatively raises it only when ``record_hits`` reaches that span
@@ -876,9 +927,31 @@ class BreakpointEngine:
         chrom = [self.genome.chrom_index_or_missing(s.chrom) for s in spans]
         flags = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) | (N.PAIR_PRIMARY_REV if s.strand == '-' else 0) |
                  (N.PAIR_SKIP if c == missing or s.align_B.aend is None else 0) for s, c in zip(spans, chrom)]
-        b = PairBatch.pack(self.options, self.genome, reads, [s.align_A.pos for s in spans],
-                           [s.align_B.aend or 0 for s in spans], [0 if c == missing else c for c in chrom], flags)
-        out = scan(self.options, self.genome, b)
-        res = decode_splices(self.options, self.genome, b, out, spans, raise_errors=False)
+        # read parts over MAX_READ_LEN take the long path (fc2_long_pair); the rest one batch
+        longs = [k for k, r in enumerate(reads) if len(r) > N.MAX_READ_LEN]
+        short = [k for k, r in enumerate(reads) if len(r) <= N.MAX_READ_LEN] if longs else range(len(spans))
+        res: List = [None] * len(spans)
+        if len(short):
+            sub = [spans[k] for k in short]
+            b = PairBatch.pack(self.options, self.genome, [reads[k] for k in short], [s.align_A.pos for s in sub],
+                               [s.align_B.aend or 0 for s in sub], [0 if chrom[k] == missing else chrom[k] for k in short],
+                               [flags[k] for k in short], locus_order=locus_order)
+            out = scan(self.options, self.genome, b)
+            for k, r in zip(short, decode_splices(self.options, self.genome, b, out, sub, raise_errors=False)):
+                res[k] = r
+        if longs:
+            buf = b"".join(reads[k] for k in longs) + b"\0" * 16
+            lp = np.zeros(len(longs), N.LONG_PAIR_DTYPE)
+            lens = np.array([len(reads[k]) for k in longs], np.uint64)
+            lp["read_off"][1:] = np.cumsum(lens[:-1])
+            lp["read_len"] = lens
+            lp["chrom"] = [0 if chrom[k] == missing else chrom[k] for k in longs]
+            lp["a_pos"] = [spans[k].align_A.pos for k in longs]
+            lp["b_aend"] = [spans[k].align_B.aend or 0 for k in longs]
+            lp["flags"] = [flags[k] for k in longs]
+            lr, ties, toff = scan_long(self.options, self.genome, np.frombuffer(buf, np.uint8), lp)
+            for k, r in zip(longs, decode_long_splices(self.options, self.genome, lp, lr, ties, toff,
+                                                       [spans[k] for k in longs])):
+                res[k] = r
         return [KeyError(s.chrom) if c == missing else none_aend_error() if s.align_B.aend is None else r
                 for s, r, c in zip(spans, res, chrom)]

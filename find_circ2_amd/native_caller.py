@@ -193,7 +193,7 @@ class NativeCaller:
                         try:
                             _raise_native(rc)           # fc2_last_error is per thread: read it here
                         except Exception as ex:
-                            q.put(("err", ex, 0))
+                            q.put(("err", ex, 0, None))
                         return
                     n = int(batch.n)
                     te = time.perf_counter()
@@ -207,13 +207,14 @@ class NativeCaller:
                         item = evaluate.submit(batch.reads, off, pairs)
                     else:
                         item = evaluate(*self._host_batch(batch, n))
+                    litem = self._eval_long(evaluate, batch)
                     eval_s[0] += time.perf_counter() - te
-                    q.put(("chunk", item, n))
+                    q.put(("chunk", item, n, litem))
                     if eof_c.value:
-                        q.put(("eof", None, 0))
+                        q.put(("eof", None, 0, None))
                         return
             except BaseException as ex:         # noqa: BLE001 -- handed to the recording thread
-                q.put(("err", ex, 0))
+                q.put(("err", ex, 0, None))
 
         self.loop_profile = {"next_s": 0.0, "queue_wait_s": 0.0, "submit_s": 0.0, "write_s": 0.0}
         th = threading.Thread(target=reader, name="fc2-reader", daemon=True)
@@ -222,7 +223,7 @@ class NativeCaller:
         try:
             while True:
                 tq = time.perf_counter()
-                kind, item, n = q.get()
+                kind, item, n, litem = q.get()
                 self.loop_profile["queue_wait_s"] += time.perf_counter() - tq
                 if kind == "err":
                     raise item
@@ -234,7 +235,9 @@ class NativeCaller:
                     res, tm = evaluate.result(item, copy=False) if pipelined else item
                     eval_s[1] += time.perf_counter() - te
                 ts = time.perf_counter()
-                rc = self._submit(L, res, tm, n)
+                rc = self._submit_long(L, litem)
+                if rc == N.FC2_OK:
+                    rc = self._submit(L, res, tm, n)
                 tw_ = time.perf_counter()
                 self._write_outputs(outputs)
                 self.loop_profile["submit_s"] += tw_ - ts
@@ -309,18 +312,21 @@ class NativeCaller:
                     item = evaluate.submit(batch.reads, off, pairs)
                 else:
                     item = evaluate(*self._host_batch(batch, n))
+                litem = self._eval_long(evaluate, batch)
                 eval_s += time.perf_counter() - te
-                queue.append((item, n))
+                queue.append((item, n, litem))
             if not queue:
                 break
-            item, n = queue.popleft()
+            item, n, litem = queue.popleft()
             res = tm = None
             if n:
                 te = time.perf_counter()
                 res, tm = evaluate.result(item, copy=False) if pipelined else item   # consumed by submit below
                 eval_s += time.perf_counter() - te
             ts = time.perf_counter()
-            rc = self._submit(L, res, tm, n)
+            rc = self._submit_long(L, litem)
+            if rc == N.FC2_OK:
+                rc = self._submit(L, res, tm, n)
             tw_ = time.perf_counter()
             self._write_outputs(outputs)        # what record_hits wrote before any failure
             prof["submit_s"] += tw_ - ts
@@ -345,6 +351,32 @@ class NativeCaller:
         nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()
         L.fc2_caller_stats(self.h, ctypes.byref(nr), ctypes.byref(npairs))
         return time.time() - t0, int(nr.value), int(npairs.value), eval_s
+
+    @staticmethod
+    def _eval_long(evaluate, batch):
+        """The chunk's pairs with read parts over MAX_READ_LEN (fc2_caller_batch.long_pairs), evaluated
+        at once by the evaluator's long path: (results LONG_RESULT_DTYPE, tie words or None), or None."""
+        n_long = int(batch.n_long)
+        if not n_long:
+            return None
+        ev = getattr(evaluate, "evaluate_long", None)
+        if ev is None:
+            raise RuntimeError("the evaluator has no long path for read parts over %d bases" % N.MAX_READ_LEN)
+        lp = np.ctypeslib.as_array(ctypes.cast(batch.long_pairs, ctypes.POINTER(ctypes.c_uint8)),
+                                   (N.LONG_PAIR_DTYPE.itemsize * n_long,)).view(N.LONG_PAIR_DTYPE).copy()
+        return ev(batch.reads, lp)
+
+    def _submit_long(self, L, litem):
+        """fc2_caller_submit_long of a chunk's long-pair results (before its fc2_caller_submit)."""
+        if litem is None:
+            return N.FC2_OK
+        res, ties = litem
+        res = np.ascontiguousarray(res, N.LONG_RESULT_DTYPE)
+        t_ptr, nt = None, 0
+        if ties is not None:
+            ties = np.ascontiguousarray(ties, np.uint64)
+            t_ptr, nt = (ties.ctypes.data if len(ties) else None), len(ties)
+        return L.fc2_caller_submit_long(self.h, res.ctypes.data, len(res), t_ptr, nt)
 
     def _submit(self, L, res, tm, n):
         """fc2_caller_submit of one chunk's results: raw 8-byte words, or a CompactChunk (a compact

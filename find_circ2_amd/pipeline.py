@@ -28,7 +28,7 @@ import numpy as np
 
 from . import _native as N
 from .genome import Genome, _torch
-from .hotpath import Options, PairBatch, ScanOutput, scan
+from .hotpath import Options, PairBatch, ScanOutput, scan, scan_long
 
 
 class _Slot:
@@ -249,6 +249,13 @@ class ScanPipeline:
 
     def result(self, t: Ticket, copy: bool = True):
         return t.scanner.result(t, copy)
+
+    def evaluate_long(self, reads_ptr: int, long_pairs: np.ndarray):
+        """The chunk's pairs with read parts over MAX_READ_LEN (fc2_caller_batch.long_pairs), on the first
+        scanner's device and synchronously -- they are rare (hotpath.scan_long): (results, tie words)."""
+        sc = self.scanners[0]
+        res, ties, _ = scan_long(self.options, sc.genome, int(reads_ptr), long_pairs)
+        return res, ties
 
     def __call__(self, reads, read_off, pairs):
         """Synchronous form (evaluate(reads, read_off, pairs) of native_caller)."""

@@ -80,9 +80,10 @@ typedef struct fc2_pair {
     uint8_t  npos;      /* FC2_PAIR_READ_N1: position of the read part's single 'N'; else 0 */
 } fc2_pair;
 
-/* Longest read_part the library accepts (fc2_pack_pairs / fc2_caller_next fail with FC2_E_RANGE
- * above it): every breakpoint index x <= l < 2^15 fits fc2_result.best_x, and the at most
- * 2(l+1) ties of --non-canonical fit n_ties. */
+/* Longest read_part of a batch pair (fc2_pack_pairs fails with FC2_E_RANGE above it): every
+ * breakpoint index x <= l < 2^15 fits fc2_result.best_x, and the at most 2(l+1) ties of
+ * --non-canonical fit n_ties.  Longer read parts -- the reference's x-loop has no limit
+ * (find_circ.py:873, :904-906) -- travel as fc2_long_pair records, below. */
 #define FC2_MAX_READ_LEN 32767
 
 /* ---- per-pair result, 8 bytes ------------------------------------------- */
@@ -244,6 +245,29 @@ typedef struct fc2_bytes_view {
     const uint64_t *off;         /* device [m] */
     uint64_t m;
 } fc2_bytes_view;
+
+/* ---- anchor pairs with read parts longer than FC2_MAX_READ_LEN ---------- */
+/* fc2_pair's 16-bit read_len and fc2_result's 16-bit best_x / n_ties cannot carry them, so they go
+ * in a list of their own with 32-bit fields and are evaluated byte-exactly (fc2_bp_scan_long_launch),
+ * one thread per pair, with results of the same meaning as fc2_result's.  Any read length BAM allows
+ * (< 2^31) is accepted. */
+typedef struct fc2_long_pair {
+    uint64_t read_off;  /* the read part: read_len bytes at reads + read_off      */
+    uint32_t read_len;  /* L = len(read_part)                                     */
+    uint32_t chrom;     /* as fc2_pair.chrom                                      */
+    int32_t  a_pos;     /* align_A.pos                                            */
+    int32_t  b_aend;    /* align_B.aend                                           */
+    uint8_t  flags;     /* FC2_PAIR_BACKSPLICE | FC2_PAIR_PRIMARY_REV | FC2_PAIR_SKIP */
+    uint8_t  _pad[7];
+} fc2_long_pair;        /* 32 bytes */
+
+typedef struct fc2_long_result {
+    int32_t  best_x;    /* as in fc2_result; -1: find_breakpoints returned []    */
+    uint32_t n_ties;
+    uint8_t  dist, ov;  /* dist saturates at 255 (only with maxdist > 255)       */
+    uint16_t info;      /* FC2_RES_*                                              */
+    uint32_t _pad;
+} fc2_long_result;      /* 16 bytes */
 
 /* ======================================================================== */
 /* library info                                                              */
@@ -440,6 +464,22 @@ int fc2_bytepath_size(const fc2_params *p, uint64_t n, const fc2_pair *pairs, ui
 int fc2_bytepath_fill(const fc2_params *p, const fc2_fasta *f, uint64_t n,
                       const uint8_t *reads, const uint64_t *read_off, const fc2_pair *pairs,
                       uint64_t *index, fc2_pair *bpairs, uint64_t *off, uint8_t *arena);
+
+/* Long pairs (fc2_long_pair), host side: the byte arena of n long pairs (*arena_bytes) and, for --all-hits, the tie words:
+ * pair j's ties are words [tie_off[j], tie_off[j+1]) of a tie array, the first half '+' ties and the
+ * second half '-' ties, bit x of word k of a half = breakpoint index 64k + x (tie_off may be NULL;
+ * tie_off[n] = the array's length in words). */
+int fc2_long_geometry(const fc2_params *p, uint64_t n, const fc2_long_pair *pairs, uint64_t *arena_bytes,
+                      uint64_t *tie_off);
+/* Fill off [n] and the arena (blocks of fc2_bytes_view's layout) with the read parts and the
+ * windows of get_data(...).upper() from f (dummy genome: f == NULL). */
+int fc2_long_fill(const fc2_params *p, const fc2_fasta *f, uint64_t n, const uint8_t *reads, const fc2_long_pair *pairs,
+                  uint64_t *off, uint8_t *arena);
+/* Device: find_breakpoints of every long pair (pairs, off, arena, tie_off and the outputs in device
+ * memory); ties (zeroed by the kernel) and tie_off only with p->allhits, else NULL. */
+int fc2_bp_scan_long_launch(const fc2_params *p, uint64_t n, const fc2_long_pair *pairs, const uint64_t *off,
+                            const uint8_t *arena, const uint64_t *tie_off, fc2_long_result *results, uint64_t *ties,
+                            void *stream);
 
 /* ======================================================================== */
 /* synthetic workloads (cf. simulate_reads.py)              */

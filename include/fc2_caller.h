@@ -49,12 +49,16 @@ typedef struct fc2_caller_opts {     /* find_circ.py:383-413 */
 /* Anchor pairs to evaluate (host memory, valid until the next call). pairs[i].chrom
  * is the genome chromosome index (tid_to_chrom of fc2_caller_open); pairs whose
  * chromosome is missing from the genome carry FC2_PAIR_SKIP and fail when
- * record_hits evaluates them. */
+ * record_hits evaluates them.  Pairs whose read part is longer than FC2_MAX_READ_LEN
+ * come in long_pairs instead (their read parts in the same `reads` buffer); their
+ * results go back with fc2_caller_submit_long before the chunk's fc2_caller_submit. */
 typedef struct fc2_caller_batch {
     uint64_t n;
     const uint8_t *reads;            /* read_part bytes (JunctionSpan.read_part, :844) */
     const uint64_t *read_off;        /* [n]; lengths are pairs[i].read_len */
     const fc2_pair *pairs;           /* [n] */
+    uint64_t n_long;
+    const fc2_long_pair *long_pairs; /* [n_long] */
 } fc2_caller_batch;
 
 /* path / is_bam as fc2_ingest_open.  tid_to_chrom [n_tid]: genome chromosome index
@@ -86,6 +90,11 @@ int fc2_caller_queued(fc2_caller *h);
  * the tie mask [tw][stride] (x-major 64-bit words, '+' rows then '-' rows). */
 int fc2_caller_submit(fc2_caller *h, const fc2_result *results, const uint64_t *tiemask, uint32_t tw,
                       uint64_t stride);
+/* Results of the OLDEST queued batch's long pairs (fc2_bp_scan_long_launch), in their order:
+ * results [n_long] and, with --all-hits, the tie words [tie words of fc2_long_geometry] (copied;
+ * NULL without --all-hits).  Required before fc2_caller_submit(_compact) of a batch with long pairs. */
+int fc2_caller_submit_long(fc2_caller *h, const fc2_long_result *results, uint64_t n_long, const uint64_t *ties,
+                           uint64_t n_tie_words);
 /* The same with the results in a compact transfer form (include/fc2_bp.h "compact results",
  * canonical mode, width 4 or 2 bytes): words [n_words] and the n_esc escapes (indices into this
  * batch), expanded here.  FC2_E_PARAM unless n_words is the oldest queued batch's pair count. */

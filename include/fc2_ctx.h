@@ -56,6 +56,12 @@ int  fc2_ctx_scan_async(fc2_ctx *ctx, const fc2_params *p, uint64_t n, const uin
 /* Wait for the queued batch and write its results; FC2_OK when nothing is queued. */
 int  fc2_ctx_sync(fc2_ctx *ctx);
 
+/* The breakpoint search of n long pairs (read parts over FC2_MAX_READ_LEN, fc2_caller_batch.long_pairs;
+ * read parts at reads + pairs[i].read_off), synchronously: results [n] and, with p->allhits, the tie
+ * words (fc2_long_geometry's layout and length).  FC2_E_PARAM while a batch is queued. */
+int  fc2_ctx_scan_long(fc2_ctx *ctx, const fc2_params *p, uint64_t n, const uint8_t *reads, const fc2_long_pair *pairs,
+                       fc2_long_result *results, uint64_t *ties);
+
 /* The context's hipStream_t (to order other work after or before its scans). */
 void *fc2_ctx_stream(const fc2_ctx *ctx);
 /* The last error a call on this context reported ("" if none); stays valid until the next call. */

@@ -94,6 +94,13 @@ int main(int argc, char **argv) {
         if (b.n && (fc2_ctx_scan_async(ctx, &params, b.n, b.reads, b.read_off, b.pairs, results, NULL, 0, 0) != FC2_OK ||
                     fc2_ctx_sync(ctx) != FC2_OK))
             return fail("fc2_ctx_scan", fc2_ctx_last_error(ctx));
+        if (b.n_long) {                        /* read parts over FC2_MAX_READ_LEN: the long path */
+            fc2_long_result *lr = (fc2_long_result *)malloc(sizeof(fc2_long_result) * b.n_long);
+            if (fc2_ctx_scan_long(ctx, &params, b.n_long, b.reads, b.long_pairs, lr, NULL) != FC2_OK)
+                return fail("fc2_ctx_scan_long", fc2_ctx_last_error(ctx));
+            if (fc2_caller_submit_long(c, lr, b.n_long, NULL, 0) != FC2_OK) return fail("fc2_caller_submit_long", fc2_last_error());
+            free(lr);
+        }
         if (fc2_caller_submit(c, b.n ? results : NULL, NULL, 0, b.n) != FC2_OK) return fail("fc2_caller_submit", fc2_last_error());
         const char *t;
         uint64_t len;

@@ -125,6 +125,50 @@ def oracle_batch_engine(options, hp):
         res["info"] = info.astype(np.uint16)
         return res.view(np.int64), tm
 
+    def evaluate_long(reads_ptr, lp):
+        """The long path (fc2_long_pair records, include/fc2_bp.h) from the same oracle: LONG_RESULT_DTYPE
+        results and the tie words laid out by fc2_long_geometry."""
+        n = len(lp)
+        total = int((lp["read_off"] + lp["read_len"]).max())
+        buf = np.ctypeslib.as_array(ctypes.cast(reads_ptr, ctypes.POINTER(ctypes.c_uint8)), (total,))
+        rp = [bytes(buf[int(o):int(o) + int(l)]) for o, l in zip(lp["read_off"], lp["read_len"])]
+        skip = (lp["flags"] & N.PAIR_SKIP) != 0
+        idx = np.where(skip, -1, 0 if of.dummy else to_oracle[np.minimum(lp["chrom"].astype(np.int64),
+                                                                         len(to_oracle) - 1)])
+        r = oracle.scan_fasta(p, of, rp, idx, lp["a_pos"], lp["b_aend"], (lp["flags"] & N.PAIR_BACKSPLICE) != 0,
+                              (lp["flags"] & N.PAIR_PRIMARY_REV) != 0, use_fast=True, all_ties=True)
+        toff = np.zeros(n + 1, np.uint64)
+        N.check(N.lib().fc2_long_geometry(ctypes.byref(hpp), n, lp.ctypes.data, None, toff.ctypes.data))
+        ties = np.zeros(int(toff[n]), np.uint64) if hp.allhits else None
+        res = np.zeros(n, N.LONG_RESULT_DTYPE)
+        res["best_x"] = -1
+        res["info"] = N.RES_DONE
+        for i in range(n):
+            nt = int(r.n_ties[i])
+            if nt == -oracle.ORC_ERR_KEY:
+                res["info"][i] |= N.RES_ERR_KEY
+            elif nt == -oracle.ORC_ERR_SHAPE:
+                res["info"][i] |= N.RES_ERR_WIN
+            elif nt > 0:
+                f = r.first[i]
+                sig = f["gtag"].decode()
+                minus = f["strand"] == b"-"
+                raw = sig[::-1].translate(rc) if minus else sig
+                res["best_x"][i] = int(f["x"])
+                res["dist"][i] = max(0, int(f["dist"]))
+                res["ov"][i] = int(f["ov"])
+                res["n_ties"][i] = nt
+                res["info"][i] |= (N.RES_MINUS if minus else 0) | \
+                    (sum(code[c] << (3 * k) for k, c in enumerate(raw)) << N.RES_GTAG_SHIFT)
+                if ties is not None:
+                    half = int(toff[i + 1] - toff[i]) // 2
+                    for t in r.ties_of(i):
+                        x = int(t["x"])
+                        ties[int(toff[i]) + (half if t["strand"] == b"-" else 0) + (x >> 6)] |= \
+                            np.uint64(1) << np.uint64(x & 63)
+        return res, ties
+
+    evaluate.evaluate_long = evaluate_long
     return evaluate, names, h, of.dummy
 
 
@@ -165,6 +209,9 @@ class DeferredEvaluator:
         self._in_flight -= 1
         return self.evaluate(*ticket)
 
+    def evaluate_long(self, reads_ptr, long_pairs):
+        return self.evaluate.evaluate_long(reads_ptr, long_pairs)
+
 
 def pipelined_factory(depth):
     """oracle_evaluator_factory whose native-caller batch hook reads `depth` chunks ahead."""
@@ -204,6 +251,7 @@ def compact_factory(width=4):
                 return res, tm
             words, esc = pack(res.view(np.int64) if hasattr(res, "view") else res, width)
             return CompactChunk(words, esc), tm
+        ev.evaluate_long = evaluate.evaluate_long
         return ev, names, h, dummy
 
     import numpy as np

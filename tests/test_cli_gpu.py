@@ -307,3 +307,71 @@ def test_gpu_cli_none_aend_span_raises_where_oracle_does(tmp_path, extra):
         _compare(o1, o2)
         return
     pytest.fail("no fragment whose B segment's span is evaluated")
+
+
+@pytest.mark.parametrize("extra", [[], ["--all-hits", "--non-canonical", "-d", "3"], ["--gpus", "2"]],
+                         ids=["default", "all-hits", "gpus2"])
+@pytest.mark.parametrize("mode", [[], ["--python-caller"]], ids=["native", "python-caller"])
+def test_gpu_cli_long_reads_equal_oracle(tmp_path, extra, mode):
+    """Read parts over FC2_MAX_READ_LEN (33-36 kb) go through the GPU long path (fc2_bp_scan_long_launch;
+    the reference's x-loop has no length limit, find_circ.py:873, :904-906): the GPU CLI, native or
+    Python read loop, writes the files of the Python loop with the CPU oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd import cli
+    from oracle_engine import oracle_evaluator_factory
+    from test_ingest import same
+    from test_read_limits import _long_read_genome, _long_reads, _sam_of
+    L = 36000
+    g = _long_read_genome(L)
+    reads = _long_reads(g, L)
+    fa = str(tmp_path / "g.fa")
+    with open(fa, "w") as f:
+        for c, sq in g.items():
+            t = sq.decode()
+            f.write(">%s\n" % c + "".join(t[i:i + 60] + "\n" for i in range(0, len(t), 60)))
+    sam = str(tmp_path / "in.sam")
+    open(sam, "w").write(_sam_of(g, reads))
+    o1, o2 = str(tmp_path / "oracle_py"), str(tmp_path / "gpu")
+    rc1 = cli.main(["-G", fa, "-o", o1, "-n", "lr", "-q", "--python-caller"] + [e for e in extra if e != "--gpus"
+                   and e != "2"] + [sam], evaluator_factory=oracle_evaluator_factory)
+    rc2 = cli.main(["-G", fa, "-o", o2, "-n", "lr", "-q"] + mode + extra + [sam])
+    assert rc1 == rc2 == 0
+    same(o1, o2)
+    assert "g2\t2000\t%d\t" % (2000 + (L - 2000) + 8000) in open(os.path.join(o2, "circ_splice_sites.bed")).read()
+
+
+def test_gpu_cli_float_as_xs_equals_oracle(tmp_path):
+    """Float AS / XS tags through the GPU CLI: the native loop's Python-2 arithmetic and formatting of
+    best_qual_left/right (find_circ.py:556-566, :593) equal the Python loop with the CPU oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import numpy as np
+    from find_circ2_amd import cli
+    from oracle_engine import oracle_evaluator_factory
+    from test_ingest import same
+    from test_native_caller import _float_tags, _retag, _rich_sam
+    sam0 = str(tmp_path / "base.sam")
+    fa = _rich_sam(sam0, 800, seed=5150)
+    sam = str(tmp_path / "float.sam")
+    open(sam, "w").write("\n".join(_retag(open(sam0).read().splitlines(), np.random.default_rng(77), _float_tags))
+                         + "\n")
+    o1, o2 = str(tmp_path / "oracle_py"), str(tmp_path / "gpu")
+    rc1 = cli.main(["-G", fa, "-o", o1, "-n", "mix", "-q", "--python-caller", sam],
+                   evaluator_factory=oracle_evaluator_factory)
+    rc2 = cli.main(["-G", fa, "-o", o2, "-n", "mix", "-q", sam])
+    assert rc1 == rc2 == 0
+    same(o1, o2)
+
+
+def test_gpu_cli_empty_bam_named_input_fails(tmp_path):
+    """An empty x.bam (a crashed aligner's leftover): pysam's header check raises ValueError where
+    the reference opens it (find_circ.py:463-466) -- the GPU CLI exits 1 with that error."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd import cli
+    p = str(tmp_path / "x.bam")
+    open(p, "wb").close()
+    o = str(tmp_path / "o")
+    assert cli.main(["-G", os.path.join(GOLDEN, "test_ref.fa"), "-o", o, "-q", p]) == 1
+    assert "ValueError: file has no sequences defined (mode='rb')" in open(os.path.join(o, "run.log")).read()
