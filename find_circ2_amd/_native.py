@@ -146,7 +146,7 @@ EXPORTED = [
     "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_submit_long", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
     "fc2_caller_set_reads_gz", "fc2_caller_close_reads",
     # include/fc2_ctx.h
-    "fc2_ctx_create", "fc2_ctx_destroy", "fc2_ctx_genome_load", "fc2_ctx_genome_view", "fc2_ctx_scan_async",
+    "fc2_ctx_create", "fc2_ctx_create_sibling", "fc2_ctx_destroy", "fc2_ctx_genome_load", "fc2_ctx_genome_view", "fc2_ctx_scan_async",
     "fc2_ctx_sync", "fc2_ctx_scan_long", "fc2_ctx_stream", "fc2_ctx_last_error",
 ]
 
@@ -278,6 +278,7 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_counter": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(ctypes.c_double)]),
         "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_ctx_create": (ctypes.c_int, [ctypes.c_int, P(vp)]),
+        "fc2_ctx_create_sibling": (ctypes.c_int, [vp, P(vp)]),
         "fc2_ctx_destroy": (None, [vp]),
         "fc2_ctx_genome_load": (ctypes.c_int, [vp, vp, ctypes.c_int]),
         "fc2_ctx_genome_view": (ctypes.c_int, [vp, P(GenomeView)]),

@@ -18,6 +18,7 @@ import logging
 import optparse
 import os
 import sys
+import time
 import traceback
 
 __version__ = "1.99"
@@ -89,7 +90,21 @@ def gpu_evaluator(genome, hp_options):
     return evaluate
 
 
+def process_age() -> float:
+    """Seconds since this process started (/proc/self/stat starttime, clock-tick resolution): what
+    interpreter start-up and imports cost before main() runs."""
+    try:
+        with open("/proc/self/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        with open("/proc/uptime") as f:
+            uptime = float(f.read().split()[0])
+        return max(0.0, uptime - int(fields[19]) / os.sysconf("SC_CLK_TCK"))
+    except (OSError, ValueError, IndexError):
+        return float("nan")
+
+
 def main(argv=None, evaluator_factory=None) -> int:
+    startup = {"before_main_s": process_age()}
     parser = build_parser()
     options, args = parser.parse_args(argv)
     if options.version:
@@ -138,7 +153,10 @@ def main(argv=None, evaluator_factory=None) -> int:
     hp = HPOptions(asize=options.asize, margin=options.margin, maxdist=options.maxdist,
                    noncanonical=options.noncanonical, strandpref=options.strandpref, allhits=options.allhits)
     genome = None
-    if evaluator_factory is None:
+    dummy_warning = lambda: logging.getLogger("GenomeAccessor").warning(        # noqa: E731
+        "Could not access '%s'. Switching to dummy mode (only Ns)" % options.genome)
+    python_loop = options.python_ingest or options.python_caller
+    if evaluator_factory is None and python_loop:
         from . import _native as N
         from .genome import Genome
         try:
@@ -146,11 +164,20 @@ def main(argv=None, evaluator_factory=None) -> int:
         except N.Fc2Error as ex:       # GenomeAccessor dummy mode (find_circ.py:338-345): IOError only
             if ex.code != N.FC2_E_IO:
                 raise
-            logging.getLogger("GenomeAccessor").warning(
-                "Could not access '%s'. Switching to dummy mode (only Ns)" % options.genome)
+            dummy_warning()
             genome = Genome.dummy_genome(device=options.device)
         evaluate = gpu_evaluator(genome, hp)
-    elif options.python_ingest or options.python_caller:
+    elif evaluator_factory is None:
+        # the native read loop's search over the torch-free C ABI (ctxpipe): the genome is indexed
+        # (.byo_index read or written, find_circ.py:110-115) and made resident on each device here
+        from .ctxpipe import CtxPipeline, FastaGenome
+        t = time.time()
+        genome = FastaGenome.open_or_dummy(options.genome, dummy_warning)
+        startup["genome_index_s"] = time.time() - t
+        t = time.time()
+        evaluate = CtxPipeline(genome, hp, devices=_devices(options))
+        startup["device_genome_s"] = time.time() - t
+    elif python_loop:
         evaluate = evaluator_factory(options, hp)
 
     path = args[0] if args else "-"
@@ -159,7 +186,8 @@ def main(argv=None, evaluator_factory=None) -> int:
     is_bam = bool(args) and not args[0].endswith("sam")
     logger.info('reading from {0}'.format(args[0]) if args else 'reading from stdin')
     if not (options.python_ingest or options.python_caller):
-        return _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path)
+        return _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path,
+                                  genome_eval=evaluate if evaluator_factory is None else None, startup=startup)
     try:
         if options.python_ingest:
             sam = AlignmentFile(path, "rb" if is_bam else "r")
@@ -262,23 +290,23 @@ def _finish(options, seconds, n_reads, logger, counters, n_spans, eval_seconds):
 
 def _devices(options):
     """--gpus N devices starting at --device (cuda:k, cuda:k+1, ...), wrapping round the devices
-    present (a 1-GPU box runs N scanners on cuda:0)."""
-    import torch
+    present (a 1-GPU box runs N scanners on cuda:0); the HIP runtime's count, no torch import."""
+    from .ctxpipe import device_count, device_index
     if options.gpus <= 1:
         return [options.device]
-    base = torch.device(options.device)
-    ndev = max(1, torch.cuda.device_count())
-    first = base.index or 0
+    ndev = max(1, device_count())
+    first = device_index(options.device)
     return ["cuda:%d" % ((first + k) % ndev) for k in range(options.gpus)]
 
 
-def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path="") -> int:
+def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path="",
+                       genome_eval=None, startup=None) -> int:
     """The read loop in C++ (include/fc2_caller.h); only the breakpoint search is called from here."""
     from .caller import BED_HEADER, MULTI_HEADER
     from .gzout import ParallelGzipWriter
-    from .native_caller import NativeCaller, gpu_batch_evaluator
+    from .native_caller import NativeCaller
     if evaluator_factory is None:
-        evaluate = gpu_batch_evaluator(genome, hp, devices=_devices(options))
+        evaluate = genome_eval
         names, fasta, dummy = genome.names, genome.fasta, genome.dummy
     else:
         engine = getattr(evaluator_factory, "batch", None)
@@ -327,9 +355,15 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
         _finish(options, seconds, n_reads, logger, nc.counters(), n_pairs, eval_s)
         if nc.loop_profile:
             logger.info("read loop stages: " + ", ".join("%s=%.3f" % kv for kv in sorted(nc.loop_profile.items())))
+        t_rows = time.time()
         for kind, key in ((0, "circs"), (1, "lins")):
             out[key].write(BED_HEADER)
             out[key].write(nc.rows(kind))
+        if startup is not None:
+            # the process's phases: what runs before the first record and after the last
+            startup.update(read_loop_s=seconds, tables_s=time.time() - t_rows)
+            logger.info("process phases: " + ", ".join("%s=%.3f" % kv for kv in startup.items()) +
+                        ", process_age_s=%.3f" % process_age())
     finally:
         try:
             nc.finish_reads()

@@ -73,8 +73,9 @@ struct fc2_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::string err;
-    // genome
+    // genome (borrowed: another context's tables, fc2_ctx_create_sibling)
     bool have_genome = false;
+    bool borrowed = false;
     const fc2_fasta *fa = nullptr;
     fc2_genome_view gv{};
     DevBuf units, nplane, ncoarse, cstart, csize, twin, nsuper, wt;
@@ -89,7 +90,9 @@ struct fc2_ctx {
     uint64_t *out_tm = nullptr;
 
     void free_genome() {
-        for (DevBuf *b : {&units, &nplane, &ncoarse, &cstart, &csize, &twin, &nsuper, &wt}) b->release();
+        if (!borrowed)
+            for (DevBuf *b : {&units, &nplane, &ncoarse, &cstart, &csize, &twin, &nsuper, &wt}) b->release();
+        borrowed = false;
         gv = fc2_genome_view{};
         have_genome = false;
         fa = nullptr;
@@ -141,6 +144,20 @@ extern "C" int fc2_ctx_create(int device, fc2_ctx **out) {
         delete c;
         return rc;
     }
+    *out = c;
+    return FC2_OK;
+}
+
+extern "C" int fc2_ctx_create_sibling(const fc2_ctx *src, fc2_ctx **out) {
+    if (!src || !out) return fc2::fail(FC2_E_PARAM, "fc2_ctx_create_sibling: null argument");
+    *out = nullptr;
+    if (!src->have_genome) return fc2::fail(FC2_E_PARAM, "fc2_ctx_create_sibling: the source context has no genome");
+    fc2_ctx *c = nullptr;
+    if (int rc = fc2_ctx_create(src->device, &c)) return rc;
+    c->gv = src->gv;                           // read-only tables: shared, never freed by the sibling
+    c->fa = src->fa;
+    c->have_genome = true;
+    c->borrowed = true;
     *out = c;
     return FC2_OK;
 }

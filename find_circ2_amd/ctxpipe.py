@@ -1,0 +1,223 @@
+"""The read loop's breakpoint search over the torch-free C ABI (include/fc2_ctx.h).
+
+``python -m find_circ2_amd.cli`` (the native read loop) hands every chunk of anchor pairs to this
+evaluator: per device one ``fc2_ctx`` holding the resident genome (2-bit planes, N maps, word-pair
+table, built on the host from the mmap'd FASTA and uploaded once), and sibling contexts
+(``fc2_ctx_create_sibling``) that scan against the same tables with their own HIP stream and
+page-locked staging.  A chunk goes to the next context round-robin: host packing (``fc2_pack_pairs``
+on C++ threads, the byte path's windows from the FASTA), H2D, the scan and the D2H of the 8-byte
+results are queued on that context's stream, and ``result`` waits for them only.  With two contexts
+per device one chunk is on the GPU while the host packs the next; results come back in submission
+order, so junctions are named by first appearance and weights summed in input order
+(find_circ.py:681-690, :544, :563, :579).
+
+This module imports neither PyTorch nor the torch-based Genome: the process pays for the HIP
+runtime only, not for ``import torch`` (DESIGN.md §0a start-up).  ``pipeline.ScanPipeline`` is the
+same evaluator on torch streams (the Python read loop's and bench.py's form).
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import _native as N
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    N.check(N.lib().fc2_device_count(ctypes.byref(n)))
+    return int(n.value)
+
+
+def device_index(device) -> int:
+    """'cuda:k' / 'hip:k' / k -> k."""
+    if isinstance(device, int):
+        return device
+    s = str(device)
+    return int(s.split(":", 1)[1]) if ":" in s else 0
+
+
+class FastaGenome:
+    """The genome FASTA as the native read loop needs it: the fc2_fasta handle (mmap'd, .byo_index
+    read or written as find_circ.py:110-115 does) and its chromosome names; ``fasta`` None for
+    GenomeAccessor's dummy mode (find_circ.py:338-345)."""
+
+    def __init__(self, path: Optional[str], write_index: bool = True):
+        self.fasta = None
+        self.names: List[str] = []
+        self.dummy = path is None
+        if path is None:
+            return
+        h = ctypes.c_void_p()
+        rc = N.lib().fc2_fasta_open(path.encode(), int(write_index), ctypes.byref(h))
+        N.check(rc)
+        self.fasta = h
+        for i in range(N.lib().fc2_fasta_n_chrom(h)):
+            nm = ctypes.c_char_p()
+            N.check(N.lib().fc2_fasta_chrom(h, i, ctypes.byref(nm), None, None, None, None, None))
+            self.names.append(nm.value.decode("latin-1"))
+
+    @classmethod
+    def open_or_dummy(cls, path: str, on_dummy=None) -> "FastaGenome":
+        """fc2_fasta_open, or the dummy genome where the reference's indexed_fasta() raises IOError."""
+        try:
+            return cls(path)
+        except N.Fc2Error as ex:
+            if ex.code != N.FC2_E_IO:
+                raise
+            if on_dummy is not None:
+                on_dummy()
+            return cls(None)
+
+    def close(self):
+        if self.fasta is not None:
+            N.lib().fc2_fasta_close(self.fasta)
+            self.fasta = None
+
+
+class _Ctx:
+    def __init__(self, handle, device: int):
+        self.h = handle
+        self.device = device
+        self.lock = threading.Lock()
+        self.pending = None            # the ticket whose results the context still holds
+        self.primary = False           # owns the device's genome tables (siblings read them)
+
+    def check(self, rc: int):
+        if rc != N.FC2_OK:
+            msg = N.lib().fc2_ctx_last_error(self.h)
+            raise N.Fc2Error(rc, msg.decode("utf-8", "replace") if msg else "")
+
+
+class CtxTicket:
+    __slots__ = ("ctx", "n", "res", "tm", "done")
+
+    def __init__(self, ctx, n, res, tm):
+        self.ctx, self.n, self.res, self.tm, self.done = ctx, n, res, tm, False
+
+
+class CtxPipeline:
+    """Chunks dealt round-robin over ``per_device`` contexts on each of ``devices`` (one genome copy
+    per device, siblings share it); ``depth`` = chunks the caller may hold in flight."""
+
+    def __init__(self, genome: FastaGenome, options, devices: Sequence = (0,), per_device: int = 2,
+                 n_threads: int = 0):
+        self.options = options
+        self.params = options.params()
+        self.n_threads = int(n_threads)
+        self.ctxs: List[_Ctx] = []
+        L = N.lib()
+        primary = {}
+        try:
+            for d in devices:
+                dev = device_index(d)
+                if dev not in primary:
+                    h = ctypes.c_void_p()
+                    N.check(L.fc2_ctx_create(dev, ctypes.byref(h)))
+                    c = _Ctx(h, dev)
+                    c.primary = True
+                    self.ctxs.append(c)
+                    c.check(L.fc2_ctx_genome_load(h, genome.fasta, self.n_threads))
+                    primary[dev] = c
+                    k0 = 1
+                else:
+                    k0 = 0                 # a device listed twice: more contexts on it (--gpus N > devices)
+                for _ in range(k0, per_device):
+                    h = ctypes.c_void_p()
+                    N.check(L.fc2_ctx_create_sibling(primary[dev].h, ctypes.byref(h)))
+                    self.ctxs.append(_Ctx(h, dev))
+        except BaseException:
+            self.close()
+            raise
+        self.k = 0
+        self.depth = len(self.ctxs)
+
+    def close(self):
+        """Siblings before the contexts whose genome they read."""
+        L = N.lib()
+        for primary_pass in (False, True):
+            for c in self.ctxs:
+                if c.h and c.primary == primary_pass:
+                    L.fc2_ctx_destroy(c.h)
+                    c.h = None
+        self.ctxs = []
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def _sync(c: _Ctx):
+        t = c.pending
+        if t is not None:
+            c.pending = None
+            c.check(N.lib().fc2_ctx_sync(c.h))
+            t.done = True
+
+    def submit(self, reads_ptr: int, read_off: np.ndarray, pairs: np.ndarray) -> CtxTicket:
+        """Pack, upload, scan and download one chunk on the next context; returns at once after the
+        device work is queued.  reads_ptr / read_off / pairs: the chunk as fc2_caller_next hands it out."""
+        c = self.ctxs[self.k % len(self.ctxs)]
+        self.k += 1
+        n = len(pairs)
+        p = self.params
+        res = np.empty(n, np.int64)
+        tm, tw = None, 0
+        if n and self.options.allhits:
+            rw, nw, tw_ = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
+            N.check(N.lib().fc2_batch_geometry(ctypes.byref(p), int(pairs["read_len"].max()), ctypes.byref(rw),
+                                               ctypes.byref(nw), ctypes.byref(tw_)))
+            tw = tw_.value
+            tm = np.empty((tw, n), np.uint64)
+        t = CtxTicket(c, n, res, tm)
+        pairs = np.ascontiguousarray(pairs, N.PAIR_DTYPE)
+        off = np.ascontiguousarray(read_off, np.uint64)
+        with c.lock:
+            self._sync(c)                  # the context's previous chunk: its results into its ticket
+            if n == 0:
+                t.done = True
+                return t
+            c.check(N.lib().fc2_ctx_scan_async(c.h, ctypes.byref(p), n, reads_ptr, off.ctypes.data, pairs.ctypes.data,
+                                               res.ctypes.data, tm.ctypes.data if tm is not None else None, tw,
+                                               self.n_threads))
+            c.pending = t
+        return t
+
+    def result(self, t: CtxTicket, copy: bool = True):
+        """(results int64 [n] = raw fc2_result words, tie mask uint64 [tw, n] or None) of a chunk."""
+        if not t.done:
+            with t.ctx.lock:
+                if t.ctx.pending is t:
+                    self._sync(t.ctx)
+        return t.res, t.tm
+
+    def evaluate_long(self, reads_ptr: int, long_pairs: np.ndarray):
+        """The chunk's pairs with read parts over MAX_READ_LEN (fc2_caller_batch.long_pairs), on the first
+        context, synchronously (fc2_ctx_scan_long): (results LONG_RESULT_DTYPE, tie words or None)."""
+        lp = np.ascontiguousarray(long_pairs, N.LONG_PAIR_DTYPE)
+        n = len(lp)
+        res = np.zeros(n, N.LONG_RESULT_DTYPE)
+        ties = None
+        p = self.params
+        if self.options.allhits:
+            toff = np.zeros(n + 1, np.uint64)
+            N.check(N.lib().fc2_long_geometry(ctypes.byref(p), n, lp.ctypes.data, None, toff.ctypes.data))
+            ties = np.zeros(max(1, int(toff[n])), np.uint64)
+        c = self.ctxs[0]
+        with c.lock:
+            self._sync(c)
+            c.check(N.lib().fc2_ctx_scan_long(c.h, ctypes.byref(p), n, reads_ptr, lp.ctypes.data, res.ctypes.data,
+                                              ties.ctypes.data if ties is not None else None))
+        if ties is not None:
+            ties = ties[:int(toff[n])]
+        return res, ties
+
+    def __call__(self, reads, read_off, pairs):
+        """Synchronous form (evaluate(reads, read_off, pairs) of native_caller)."""
+        reads = np.ascontiguousarray(reads, np.uint8)
+        return self.result(self.submit(reads.ctypes.data, read_off, pairs))

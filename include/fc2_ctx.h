@@ -30,6 +30,10 @@ typedef struct fc2_ctx fc2_ctx;
 /* A context on HIP device `device` (>= 0): its own non-blocking stream.  FC2_E_PARAM for a negative
  * device, FC2_E_HIP when the device cannot be used. */
 int  fc2_ctx_create(int device, fc2_ctx **out);
+/* A second context on src's device with its own stream and staging that scans against src's resident
+ * genome (shared, not copied): two contexts per device keep one batch on the GPU while the host packs
+ * the next.  src must outlive it and keep its genome (no fc2_ctx_genome_load on src meanwhile). */
+int  fc2_ctx_create_sibling(const fc2_ctx *src, fc2_ctx **out);
 /* Waits for the context's work, frees its device and pinned memory (the FASTA stays the caller's). */
 void fc2_ctx_destroy(fc2_ctx *ctx);
 
