@@ -1111,7 +1111,7 @@ def cli_end_to_end(reads=2_000_000):
     FASTA and a bwa-mem-like SAM of `reads` reads, fc2_sam_to_bam turns it into a BGZF BAM, and
     `python -m find_circ2_amd.cli` runs as its own process reading that BAM from a stdin pipe (format
     detected from the bytes; BGZF blocks inflated on worker threads, the C++ read loop on worker pools,
-    HIP search through pipeline.ScanPipeline, gzip members on worker threads).  The same reads as SAM
+    HIP search through ctxpipe.CtxPipeline (the torch-free fc2_ctx ABI), gzip members on worker threads).  The same reads as SAM
     text by path run too; both runs must write identical files.  The first run builds the .byo_index;
     the runs after it are reported: the loop's own reads/s (run.log) and the process wall time, the
     BAM form as the median of CLI_RUNS runs (one run moves +-10 % on the box's shared CPU quota)."""
@@ -1151,8 +1151,12 @@ def cli_end_to_end(reads=2_000_000):
             log = open(os.path.join(out, "run.log")).read()
             m = re.search(r"overall ([0-9.]+)k reads/second", log)
             st = re.search(r"read loop stages: (.*)", log)
+            ph = re.search(r"process phases: (.*)", log)
+            phases = {k: float(v) for k, v in re.findall(r"(\w+)=([0-9.naN]+)", ph.group(1))} if ph else None
             return out, {"value": round(float(m.group(1)) * 1e3, 1) if m else None, "unit": "reads/s",
-                         "process_wall_s": round(wall, 2), "stages": st.group(1) if st else None}
+                         "process_wall_s": round(wall, 2),
+                         "reads_per_process_wall_s": round(reads / wall, 1),
+                         "phases_s": phases, "stages": st.group(1) if st else None}
 
         run("warm", False)                     # builds genome.fa.byo_index
         runs = [run("bam_stdin%d" % k, True) for k in range(CLI_RUNS)]
@@ -1167,7 +1171,10 @@ def cli_end_to_end(reads=2_000_000):
         res["sam_by_path"] = res_sam
         res["note"] = ("whole CLI, BGZF BAM piped on stdin (cat reads.bam | python -m find_circ2_amd.cli -G genome.fa "
                        "-o out), hg19-shaped genome, .byo_index present: value = the read loop's reads/s from "
-                       "run.log, the median of `runs`; process_wall_s includes interpreter start, genome load and upload; sam_by_path = "
+                       "run.log, the median of `runs`; process_wall_s includes interpreter start, genome load and upload "
+                       "(reads_per_process_wall_s = reads / process_wall_s; phases_s = run.log's process phases: "
+                       "before_main_s interpreter + imports, genome_index_s, device_genome_s HIP init + 2-bit pack + "
+                       "upload + tables, read_loop_s, tables_s); sam_by_path = "
                        "the same reads as SAM text by path; outputs of the two runs compared here, and against "
                        "the Python loop in tests and scripts/cli_scale_check.py")
         return res
