@@ -1153,6 +1153,9 @@ def cli_end_to_end(reads=2_000_000):
             st = re.search(r"read loop stages: (.*)", log)
             ph = re.search(r"process phases: (.*)", log)
             phases = {k: float(v) for k, v in re.findall(r"(\w+)=([0-9.naN]+)", ph.group(1))} if ph else None
+            sd = re.search(r"process shutdown: (.*)", log)
+            if phases is not None and sd:
+                phases.update({"shutdown_" + k: float(v) for k, v in re.findall(r"(\w+)=([0-9.naN]+)", sd.group(1))})
             return out, {"value": round(float(m.group(1)) * 1e3, 1) if m else None, "unit": "reads/s",
                          "process_wall_s": round(wall, 2),
                          "reads_per_process_wall_s": round(reads / wall, 1),

@@ -174,9 +174,9 @@ def main(argv=None, evaluator_factory=None) -> int:
         t = time.time()
         genome = FastaGenome.open_or_dummy(options.genome, dummy_warning)
         startup["genome_index_s"] = time.time() - t
-        t = time.time()
-        evaluate = CtxPipeline(genome, hp, devices=_devices(options))
-        startup["device_genome_s"] = time.time() - t
+        # the device genome is built on a thread of its own while the input is opened and its first
+        # chunks are read (the first search waits for it); its time is logged with the phases
+        evaluate = CtxPipeline(genome, hp, devices=_devices(options), background=True)
     elif python_loop:
         evaluate = evaluator_factory(options, hp)
 
@@ -361,10 +361,13 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             out[key].write(nc.rows(kind))
         if startup is not None:
             # the process's phases: what runs before the first record and after the last
-            startup.update(read_loop_s=seconds, tables_s=time.time() - t_rows)
+            # (device_genome_s overlaps the start of the read loop)
+            startup.update(device_genome_s=getattr(evaluate, "load_s", None) or 0.0, read_loop_s=seconds,
+                           tables_s=time.time() - t_rows)
             logger.info("process phases: " + ", ".join("%s=%.3f" % kv for kv in startup.items()) +
                         ", process_age_s=%.3f" % process_age())
     finally:
+        t_close = time.time()
         try:
             nc.finish_reads()
         finally:
@@ -372,6 +375,13 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
         for k, fh in out.items():
             if fh is not None and fh is not sys.stdout:
                 fh.close()
+        t_ctx = time.time()
+        if genome_eval is not None:            # the contexts (device memory, streams), then the FASTA
+            genome_eval.close()
+            genome.close()
+        if startup is not None and "read_loop_s" in startup:
+            logger.info("process shutdown: outputs_close_s=%.3f, device_release_s=%.3f, process_age_s=%.3f"
+                        % (t_ctx - t_close, time.time() - t_ctx, process_age()))
     return 0
 
 

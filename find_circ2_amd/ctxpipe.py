@@ -104,11 +104,44 @@ class CtxPipeline:
     per device, siblings share it); ``depth`` = chunks the caller may hold in flight."""
 
     def __init__(self, genome: FastaGenome, options, devices: Sequence = (0,), per_device: int = 2,
-                 n_threads: int = 0):
+                 n_threads: int = 0, background: bool = False):
+        """``background``: create the contexts and make the genome resident on a thread of their own,
+        so the caller can open its input and read the first chunks meanwhile (the reference, too,
+        touches the genome only when the first span is evaluated, find_circ.py:435-436); the first
+        submit waits for it and raises its error."""
         self.options = options
         self.params = options.params()
         self.n_threads = int(n_threads)
         self.ctxs: List[_Ctx] = []
+        self.k = 0
+        self.depth = len(devices) * per_device      # per listing of a device: per_device contexts
+        self._ready = None
+        self._error = None
+        self.load_s = None
+        if background:
+            self._ready = threading.Thread(target=self._build_guarded, args=(genome, devices, per_device),
+                                           name="fc2-genome-load", daemon=True)
+            self._ready.start()
+        else:
+            self._build(genome, devices, per_device)
+
+    def _build_guarded(self, genome, devices, per_device):
+        try:
+            self._build(genome, devices, per_device)
+        except BaseException as ex:     # noqa: BLE001 -- raised at the first submit
+            self._error = ex
+
+    def wait_ready(self):
+        """The contexts and resident genome are built (raises what building them raised)."""
+        if self._ready is not None:
+            self._ready.join()
+            self._ready = None
+        if self._error is not None:
+            raise self._error
+
+    def _build(self, genome, devices, per_device):
+        import time
+        t0 = time.time()
         L = N.lib()
         primary = {}
         try:
@@ -132,11 +165,14 @@ class CtxPipeline:
         except BaseException:
             self.close()
             raise
-        self.k = 0
-        self.depth = len(self.ctxs)
+        assert len(self.ctxs) == self.depth, (len(self.ctxs), self.depth)
+        self.load_s = time.time() - t0
 
     def close(self):
         """Siblings before the contexts whose genome they read."""
+        if self._ready is not None:
+            self._ready.join()
+            self._ready = None
         L = N.lib()
         for primary_pass in (False, True):
             for c in self.ctxs:
@@ -162,6 +198,7 @@ class CtxPipeline:
     def submit(self, reads_ptr: int, read_off: np.ndarray, pairs: np.ndarray) -> CtxTicket:
         """Pack, upload, scan and download one chunk on the next context; returns at once after the
         device work is queued.  reads_ptr / read_off / pairs: the chunk as fc2_caller_next hands it out."""
+        self.wait_ready()
         c = self.ctxs[self.k % len(self.ctxs)]
         self.k += 1
         n = len(pairs)
@@ -199,6 +236,7 @@ class CtxPipeline:
     def evaluate_long(self, reads_ptr: int, long_pairs: np.ndarray):
         """The chunk's pairs with read parts over MAX_READ_LEN (fc2_caller_batch.long_pairs), on the first
         context, synchronously (fc2_ctx_scan_long): (results LONG_RESULT_DTYPE, tie words or None)."""
+        self.wait_ready()
         lp = np.ascontiguousarray(long_pairs, N.LONG_PAIR_DTYPE)
         n = len(lp)
         res = np.zeros(n, N.LONG_RESULT_DTYPE)
