@@ -177,6 +177,10 @@ def main(argv=None, evaluator_factory=None) -> int:
         # the device genome is built on a thread of its own while the input is opened and its first
         # chunks are read (the first search waits for it); its time is logged with the phases
         evaluate = CtxPipeline(genome, hp, devices=_devices(options), background=True)
+        if options.gpus > 1:
+            logger.info("--gpus %d: chunks dealt round-robin over %s; the search is a few percent of the read "
+                        "loop, which is bound by the host's cores (DESIGN.md §6), so more GPUs add little here"
+                        % (options.gpus, ",".join(_devices(options))))
     elif python_loop:
         evaluate = evaluator_factory(options, hp)
 

@@ -997,19 +997,22 @@ void app_pymin(std::string &out, const PyMin &m) {
     else app_int(out, m.v);
 }
 
-void storage_rows(fc2_caller *h, int kind, std::string &outs) {           // :690-730
+// store_list (:690-730) for the junctions [b, e) of the dict order: their rows appended to outs, the
+// counters of the ones skipped into N (reads the tables only: ranges run on the workers at once)
+void storage_rows(const fc2_caller *h, int kind, size_t b, size_t e, std::string &outs,
+                  std::vector<std::pair<const char *, double>> &N) {
     const auto &o = h->o;
-    for (const JRef &j : h->order[kind]) {      // dict order
-        const Hit &t = hit_at(h, kind, j);
+    for (size_t k = b; k < e; ++k) {             // dict order
+        const Hit &t = hit_at(h, kind, h->order[kind][k]);
         if (!t.n_reads) continue;
         const double qa = t.mq_a.value(), qb = t.mq_b.value(), mq = (double)o.min_uniq_qual;
         if (o.halfunique) {
-            if (qa < mq && qb < mq) { incN(h, "anchor_not_uniq"); continue; }
+            if (qa < mq && qb < mq) { incN_into(N, "anchor_not_uniq", 1.); continue; }
         } else if (qa < mq || qb < mq) {
-            incN(h, "anchor_not_uniq");
+            incN_into(N, "anchor_not_uniq", 1.);
             continue;
         }
-        if (t.n_uniq_bridges == 0 && !o.report_nobridges) { incN(h, "no_uniq_bridges"); continue; }
+        if (t.n_uniq_bridges == 0 && !o.report_nobridges) { incN_into(N, "no_uniq_bridges", 1.); continue; }
         // the 22 columns of find_circ.py:712-730, appended in place
         const char tab = '\t';
         outs += key_chrom(h, t.key); outs += tab;
@@ -2593,7 +2596,25 @@ extern "C" int fc2_caller_close_reads(fc2_caller *h) {
 extern "C" int fc2_caller_rows(fc2_caller *h, int kind, const char **text, uint64_t *len) {
     if (!h || kind < 0 || kind > 1 || !text || !len) return fc2::fail(FC2_E_PARAM, "fc2_caller_rows: bad arguments");
     h->rows_text.clear();
-    storage_rows(h, kind, h->rows_text);
+    // the rows of ranges of the dict order formatted on the workers, joined in order
+    const size_t nj = h->order[kind].size();
+    const size_t T = std::max<size_t>(1, std::min<size_t>(h->pool ? (size_t)h->pool->size() : 1, nj / 4096));
+    std::vector<std::string> parts(T);
+    std::vector<std::vector<std::pair<const char *, double>>> Ns(T);
+    auto range = [&](int r) { storage_rows(h, kind, nj * (size_t)r / T, nj * (size_t)(r + 1) / T, parts[(size_t)r], Ns[(size_t)r]); };
+    try {
+        if (T > 1) h->pool->run_checked((int)T, range);
+        else range(0);
+    } catch (const std::bad_alloc &) {
+        return fc2::fail(FC2_E_PARAM, "fc2_caller_rows: out of memory");
+    }
+    size_t total = 0;
+    for (const std::string &p : parts) total += p.size();
+    h->rows_text.reserve(total);
+    for (size_t r = 0; r < T; ++r) {
+        h->rows_text += parts[r];
+        for (const auto &kv : Ns[r]) incN(h, kv.first, kv.second);
+    }
     *text = h->rows_text.c_str();
     *len = h->rows_text.size();
     return FC2_OK;

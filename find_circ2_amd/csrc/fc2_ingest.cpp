@@ -1869,16 +1869,16 @@ int fc2::ing::pull(fc2_ingest *h, const fc2_ingest_params *p, uint64_t max_frags
             if (atoi(pm) > 0) ap->max_pinned = (size_t)atoi(pm);
         if (const char *fe = getenv("FC2_PARSE_INFLIGHT"))
             if (atoi(fe) > 0) ap->max_inflight = (size_t)std::min(atoi(fe), 256);
-        const char *zc = getenv("FC2_BGZF_INPLACE");     // 0: the copying splitter (A/B)
-        ap->splitter = !h->bam                                   ? std::thread(sam_split_loop, h, ap)
-                       : h->src == fc2_ingest::SRC_BGZF && !(zc && atoi(zc) == 0) ? std::thread(bgzf_split_loop, h, ap)
-                                                                                  : std::thread(bam_split_loop, h, ap);
+        // BGZF BAM is cut into parse blocks in place in the inflated batches; plain and other gzip BAM
+        // through the copying splitter
+        ap->splitter = !h->bam                          ? std::thread(sam_split_loop, h, ap)
+                       : h->src == fc2_ingest::SRC_BGZF ? std::thread(bgzf_split_loop, h, ap)
+                                                        : std::thread(bam_split_loop, h, ap);
         const char *env = getenv("FC2_PARSE_THREADS");
         const int np = env && atoi(env) > 0 ? std::min(atoi(env), 32) : fc2_ingest::SamAhead::kParsers;
-        // fragments grouped on the parse threads (FC2_GROUP_AHEAD=0: on the consumer, as before)
-        const char *ge = getenv("FC2_GROUP_AHEAD");
+        // fragments grouped on the parse threads (the consumer groups those a parse block cuts)
         ap->gp = *p;
-        ap->group = !(ge && atoi(ge) == 0);
+        ap->group = true;
         ap->pin = h->pin;
         for (int k = 0; k < np; ++k) ap->parsers.emplace_back(sam_parse_loop, h, ap);
     }

@@ -93,10 +93,11 @@ class _Ctx:
 
 
 class CtxTicket:
-    __slots__ = ("ctx", "n", "res", "tm", "done")
+    __slots__ = ("ctx", "n", "res", "tm", "tw", "done", "deferred")
 
-    def __init__(self, ctx, n, res, tm):
-        self.ctx, self.n, self.res, self.tm, self.done = ctx, n, res, tm, False
+    def __init__(self, ctx, n, res, tm, tw=0):
+        self.ctx, self.n, self.res, self.tm, self.tw, self.done = ctx, n, res, tm, tw, False
+        self.deferred = None           # (reads_ptr, read_off, pairs) while the genome is being built
 
 
 class CtxPipeline:
@@ -114,7 +115,12 @@ class CtxPipeline:
         self.n_threads = int(n_threads)
         self.ctxs: List[_Ctx] = []
         self.k = 0
-        self.depth = len(devices) * per_device      # per listing of a device: per_device contexts
+        self.n_ctx = len(devices) * per_device      # per listing of a device: per_device contexts
+        # chunks the caller may hold: tickets own their result buffers, so more than the contexts --
+        # while the genome is being built the read loop reads this many chunks ahead
+        self.depth = 4 * self.n_ctx
+        self._slock = threading.Lock()              # dispatch order (reader thread + recorder thread)
+        self._deferred: List[CtxTicket] = []
         self._ready = None
         self._error = None
         self.load_s = None
@@ -165,7 +171,7 @@ class CtxPipeline:
         except BaseException:
             self.close()
             raise
-        assert len(self.ctxs) == self.depth, (len(self.ctxs), self.depth)
+        assert len(self.ctxs) == self.n_ctx, (len(self.ctxs), self.n_ctx)
         self.load_s = time.time() - t0
 
     def close(self):
@@ -197,36 +203,60 @@ class CtxPipeline:
 
     def submit(self, reads_ptr: int, read_off: np.ndarray, pairs: np.ndarray) -> CtxTicket:
         """Pack, upload, scan and download one chunk on the next context; returns at once after the
-        device work is queued.  reads_ptr / read_off / pairs: the chunk as fc2_caller_next hands it out."""
-        self.wait_ready()
-        c = self.ctxs[self.k % len(self.ctxs)]
-        self.k += 1
+        device work is queued.  reads_ptr / read_off / pairs: the chunk as fc2_caller_next hands it out
+        (its memory stays valid while the chunk is queued).  While the genome is still being built the
+        chunk is only noted, and dispatched in order once it is ready."""
         n = len(pairs)
-        p = self.params
         res = np.empty(n, np.int64)
         tm, tw = None, 0
         if n and self.options.allhits:
             rw, nw, tw_ = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
-            N.check(N.lib().fc2_batch_geometry(ctypes.byref(p), int(pairs["read_len"].max()), ctypes.byref(rw),
-                                               ctypes.byref(nw), ctypes.byref(tw_)))
+            N.check(N.lib().fc2_batch_geometry(ctypes.byref(self.params), int(pairs["read_len"].max()),
+                                               ctypes.byref(rw), ctypes.byref(nw), ctypes.byref(tw_)))
             tw = tw_.value
             tm = np.empty((tw, n), np.uint64)
-        t = CtxTicket(c, n, res, tm)
+        t = CtxTicket(None, n, res, tm, tw)
         pairs = np.ascontiguousarray(pairs, N.PAIR_DTYPE)
         off = np.ascontiguousarray(read_off, np.uint64)
+        with self._slock:
+            if self._ready is not None and self._ready.is_alive():
+                t.deferred = (reads_ptr, off.copy(), pairs.copy())
+                self._deferred.append(t)
+                return t
+            self.wait_ready()
+            self._flush()
+            self._dispatch(t, reads_ptr, off, pairs)
+        return t
+
+    def _flush(self):
+        """Dispatch the chunks noted while the genome was being built (caller holds _slock)."""
+        while self._deferred:
+            t = self._deferred.pop(0)
+            reads_ptr, off, pairs = t.deferred
+            t.deferred = None
+            self._dispatch(t, reads_ptr, off, pairs)
+
+    def _dispatch(self, t: CtxTicket, reads_ptr, off, pairs):
+        c = self.ctxs[self.k % len(self.ctxs)]
+        self.k += 1
+        t.ctx = c
         with c.lock:
             self._sync(c)                  # the context's previous chunk: its results into its ticket
-            if n == 0:
+            if t.n == 0:
                 t.done = True
-                return t
-            c.check(N.lib().fc2_ctx_scan_async(c.h, ctypes.byref(p), n, reads_ptr, off.ctypes.data, pairs.ctypes.data,
-                                               res.ctypes.data, tm.ctypes.data if tm is not None else None, tw,
+                return
+            c.check(N.lib().fc2_ctx_scan_async(c.h, ctypes.byref(self.params), t.n, reads_ptr, off.ctypes.data,
+                                               pairs.ctypes.data, t.res.ctypes.data,
+                                               t.tm.ctypes.data if t.tm is not None else None, t.tw,
                                                self.n_threads))
             c.pending = t
-        return t
 
     def result(self, t: CtxTicket, copy: bool = True):
         """(results int64 [n] = raw fc2_result words, tie mask uint64 [tw, n] or None) of a chunk."""
+        if t.ctx is None and not t.done:
+            with self._slock:
+                self.wait_ready()
+                self._flush()
         if not t.done:
             with t.ctx.lock:
                 if t.ctx.pending is t:
@@ -246,6 +276,8 @@ class CtxPipeline:
             toff = np.zeros(n + 1, np.uint64)
             N.check(N.lib().fc2_long_geometry(ctypes.byref(p), n, lp.ctypes.data, None, toff.ctypes.data))
             ties = np.zeros(max(1, int(toff[n])), np.uint64)
+        with self._slock:
+            self._flush()
         c = self.ctxs[0]
         with c.lock:
             self._sync(c)

@@ -18,10 +18,10 @@ MODES = [dict(FC2_CALLER_THREADS="1", FC2_NEXT_THREADS="1"),
          dict(FC2_CALLER_THREADS="3", FC2_NEXT_THREADS="2", FC2_CALLER_MIN_RANGE="1"),
          dict(FC2_CALLER_THREADS="8", FC2_NEXT_THREADS="7", FC2_CALLER_MIN_RANGE="5"), dict(FC2_CALLER_THREADS="16"),
          # fragments grouped on the parse threads across many small parse blocks (a fragment cut
-         # by a block boundary, regions of one fragment, none), and grouped on the consumer alone
+         # by a block boundary, regions of one fragment, none), on one parse thread
          dict(FC2_PARSE_BLOCK="700", FC2_NEXT_THREADS="2", FC2_CALLER_MIN_RANGE="1", FC2_PARSE_INFLIGHT="2"),
          dict(FC2_PARSE_BLOCK="4000", FC2_PARSE_THREADS="5", FC2_CALLER_THREADS="3"),
-         dict(FC2_GROUP_AHEAD="0", FC2_PARSE_BLOCK="1500"),
+         dict(FC2_PARSE_THREADS="1", FC2_PARSE_BLOCK="1500"),
          # chunks cut short by the pinned-batch cap (one 400-byte block per chunk; some chunks empty)
          dict(FC2_PARSE_BLOCK="400", FC2_PIN_MAX="1", FC2_PARSE_INFLIGHT="3")]
 
@@ -143,7 +143,7 @@ def _edge_sam(src, dst, seed, first):
 @pytest.mark.parametrize("first", ["same", "other"])
 @pytest.mark.parametrize("mode", [dict(FC2_PARSE_BLOCK="300", FC2_PARSE_INFLIGHT="2"),
                                   dict(FC2_PARSE_BLOCK="1100", FC2_NEXT_THREADS="3", FC2_CALLER_MIN_RANGE="1"),
-                                  dict(FC2_GROUP_AHEAD="0", FC2_PARSE_BLOCK="500")])
+                                  dict(FC2_PARSE_THREADS="1", FC2_PARSE_BLOCK="500")])
 @pytest.mark.parametrize("bam", [False, True])
 def test_grouping_edge_cases_equal_python_ingest(tmp_path, monkeypatch, rich, first, mode, bam):
     """Fragments grouped on the parse threads (group_batch) at tiny parse blocks against the pure

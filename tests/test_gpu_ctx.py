@@ -167,3 +167,48 @@ def test_ctx_refuses_a_second_batch_before_sync():
         assert L.fc2_ctx_stream(ctx.c)
     finally:
         ctx.close()
+
+
+@pytest.mark.parametrize("o", [dict(), dict(allhits=True, noncanonical=True)])
+@pytest.mark.parametrize("background", [False, True])
+def test_ctxpipe_round_robin_equals_python_path(o, background):
+    """ctxpipe.CtxPipeline (the CLI's evaluator: a context + sibling contexts sharing its resident
+    genome, chunks dealt round-robin, results in submission order; with background=True chunks
+    submitted while the genome is still being built are dispatched in order once it is ready):
+    every chunk's words and tie masks equal the Python layer's scan of the same pairs."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd.ctxpipe import CtxPipeline, FastaGenome
+    opt = Options(**o)
+    path = os.path.join(GOLDEN, "CDR1as_locus.fa")
+    g = genome(path)
+    fg = FastaGenome(path, write_index=False)
+    pipe = CtxPipeline(fg, opt, devices=["cuda:0", "cuda:0"], per_device=2, background=background)
+    try:
+        assert pipe.n_ctx == 4 and pipe.depth == 16
+        chunks, tickets = [], []
+        for k in range(11):
+            spans = make_spans(load_genome(path), 300 + 37 * k, seed=900 + k, L=(40, 700), p_readN=0.05)
+            reads = [s.read_part for s in spans]
+            off = np.zeros(len(reads), np.uint64)
+            off[1:] = np.cumsum([len(r) for r in reads[:-1]])
+            buf = np.frombuffer(b"".join(reads) + b"\0" * 16, np.uint8)
+            pairs = np.zeros(len(reads), N.PAIR_DTYPE)
+            pairs["a_pos"] = [s.a_pos for s in spans]
+            pairs["b_aend"] = [s.b_aend for s in spans]
+            pairs["chrom"] = [g.chrom_index(s.chrom) for s in spans]
+            pairs["read_len"] = [len(r) for r in reads]
+            pairs["flags"] = [(N.PAIR_BACKSPLICE if s.is_backsplice else 0) |
+                              (N.PAIR_PRIMARY_REV if s.primary_reverse else 0) for s in spans]
+            chunks.append((spans, buf))
+            tickets.append(pipe.submit(buf.ctypes.data, off, pairs))
+        for (spans, buf), t in zip(chunks, tickets):
+            res, tm = pipe.result(t)
+            b, out = run_spans(opt, g, spans)
+            assert np.array_equal(res, out.host(b.n).view(np.int64)), "words"
+            if opt.allhits:
+                ref = out.tiemask[:b.tw * b.stride].cpu().numpy().view(np.uint64).reshape(b.tw, b.stride)
+                assert np.array_equal(tm, ref[:tm.shape[0], :b.n]), "tie mask"
+    finally:
+        pipe.close()
+        fg.close()
