@@ -346,6 +346,8 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             else:
                 seconds, n_reads, n_pairs, eval_s = nc.run(evaluate, out, sys.stderr, options.throughput,
                                                            options.chunksize)
+            if genome_eval is not None:
+                genome_eval.wait_ready()       # no GPU, no run: fails loudly even if no span was searched
         except KeyboardInterrupt:
             logging.warning("KeyboardInterrupt by user while processing input")
             (n_reads, n_pairs), seconds, eval_s = nc.stats(), 0.0, 0.0
@@ -366,7 +368,8 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
         if startup is not None:
             # the process's phases: what runs before the first record and after the last
             # (device_genome_s overlaps the start of the read loop)
-            startup.update(device_genome_s=getattr(evaluate, "load_s", None) or 0.0, read_loop_s=seconds,
+            startup.update(device_genome_s=getattr(evaluate, "load_s", None) or 0.0,
+                           hip_init_s=getattr(evaluate, "hip_init_s", None) or 0.0, read_loop_s=seconds,
                            tables_s=time.time() - t_rows)
             logger.info("process phases: " + ", ".join("%s=%.3f" % kv for kv in startup.items()) +
                         ", process_age_s=%.3f" % process_age())

@@ -4,9 +4,12 @@
 // staging, H2D, fc2_bp_scan_launch + fc2_bp_scan_bytes_launch, D2H -- on the context's own stream.
 // It replaces the Python host layer for hosts that bind the C ABI directly.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -190,7 +193,11 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
         c->have_genome = true;
         return FC2_OK;
     }
-    // index + 2-bit planes on the host (find_circ.py:110-155 semantics, fc2_host.cpp)
+    // index + 2-bit planes on the host (find_circ.py:110-155 semantics, fc2_host.cpp); phase times on
+    // stderr with FC2_CALLER_TIMING
+    static const bool timing = getenv("FC2_CALLER_TIMING") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     const int nch = fc2_fasta_n_chrom(fa);
     std::vector<int64_t> sizes((size_t)std::max(nch, 1), 0);
     for (int i = 0; i < nch; ++i)
@@ -201,7 +208,9 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
     std::vector<uint64_t> units(2 * nu), nplane(nu);
     std::vector<uint32_t> ncoarse((size_t)std::max<uint64_t>(ncw, 1), 0);
     uint64_t n_exotic = 0;
+    const double t_alloc = ms();
     if ((rc = fc2_fasta_pack(fa, units.data(), nplane.data(), ncoarse.data(), &n_exotic, n_threads))) return keep(c, rc);
+    const double t_pack = ms();
     // device tables (genome.py _upload / _upload_tables)
     const hipStream_t s = c->stream;
     if ((rc = c->units.reserve(units.size() * 8, "genome units", false)) || (rc = c->nplane.reserve(nplane.size() * 8, "genome N plane", false)) ||
@@ -227,6 +236,9 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
     }
     const hipError_t e = hipStreamSynchronize(s);          // the host vectors go out of scope here
     if (e != hipSuccess) return keep(c, hip_fail(e, "genome upload"));
+    if (timing)
+        fprintf(stderr, "genome load: host vectors %.1f ms, 2-bit pack %.1f ms, device alloc + upload + tables %.1f ms "
+                        "(%llu units)\n", t_alloc, t_pack - t_alloc, ms() - t_pack, (unsigned long long)nu);
     fc2_genome_view &g = c->gv;
     g.units = c->units.as<const uint64_t>();
     g.nplane = c->nplane.as<const uint64_t>();

@@ -123,7 +123,7 @@ class CtxPipeline:
         self._deferred: List[CtxTicket] = []
         self._ready = None
         self._error = None
-        self.load_s = None
+        self.load_s = self.hip_init_s = None
         if background:
             self._ready = threading.Thread(target=self._build_guarded, args=(genome, devices, per_device),
                                            name="fc2-genome-load", daemon=True)
@@ -156,6 +156,8 @@ class CtxPipeline:
                 if dev not in primary:
                     h = ctypes.c_void_p()
                     N.check(L.fc2_ctx_create(dev, ctypes.byref(h)))
+                    if self.hip_init_s is None:         # the first HIP call of the process
+                        self.hip_init_s = time.time() - t0
                     c = _Ctx(h, dev)
                     c.primary = True
                     self.ctxs.append(c)

@@ -166,3 +166,19 @@ def test_non_ascii_bytes_written_back_unchanged(tmp_path, mode):
     assert b"r\xe9ad" in raw and b"r\xc3\xa9ad" not in raw
     bed = open(os.path.join(out, "circ_splice_sites.bed"), "rb").read()
     assert b"\xc3\xa9" not in bed
+
+
+def test_default_cli_fails_loudly_without_a_gpu(tmp_path):
+    """The shipped search has no CPU fallback: with no HIP device the default CLI (native read loop,
+    ctxpipe) exits 1 with the device error -- also for an input in which no span is searched."""
+    from find_circ2_amd.ctxpipe import device_count
+    try:
+        if device_count() > 0:
+            pytest.skip("a GPU is present")
+    except Exception:
+        pass                                    # no HIP runtime at all: the same failure is expected
+    fa = os.path.join(GOLDEN, "test_ref.fa")
+    for reads in (_reads(os.path.join(GOLDEN, "test_reads.fa")), []):
+        rc, out = run_cli(tmp_path, fa, reads, evaluator=None, tag="default%d" % len(reads))
+        assert rc == 1
+        assert "fc2_ctx_create" in open(os.path.join(out, "run.log")).read()
