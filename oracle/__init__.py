@@ -111,8 +111,13 @@ class OracleFasta:
                 chrom, ofs, ldata, skip, skipchar, size = line.rstrip().split(b"\t")
                 rows.append((chrom, int(ofs), int(ldata), int(skip), codecs.escape_decode(skipchar[1:-1])[0],
                              int(size)))
-        n = len(rows)
+        # the chromosomes keep the positions index() gave them (callers index them in FASTA order, the
+        # reference looks them up by name); names only the index file holds come after them
         L = lib()
+        first = [L.orc_fasta_chrom_name(self.h, i) for i in range(L.orc_fasta_n_chrom(self.h))]
+        rank = {nm: k for k, nm in enumerate(first)}
+        rows.sort(key=lambda r: rank.get(r[0], len(first)))
+        n = len(rows)
         if not hasattr(L, "_set_chroms_sig"):
             vp, i64p = ctypes.c_void_p, ctypes.POINTER(ctypes.c_int64)
             L.orc_fasta_set_chroms.argtypes = [vp, ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), i64p, i64p, i64p,

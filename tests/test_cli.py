@@ -177,7 +177,9 @@ def test_default_cli_fails_loudly_without_a_gpu(tmp_path):
             pytest.skip("a GPU is present")
     except Exception:
         pass                                    # no HIP runtime at all: the same failure is expected
-    fa = os.path.join(GOLDEN, "test_ref.fa")
+    import shutil
+    fa = str(tmp_path / "test_ref.fa")               # (the default CLI writes the .byo_index next to it)
+    shutil.copy(os.path.join(GOLDEN, "test_ref.fa"), fa)
     for reads in (_reads(os.path.join(GOLDEN, "test_reads.fa")), []):
         rc, out = run_cli(tmp_path, fa, reads, evaluator=None, tag="default%d" % len(reads))
         assert rc == 1
