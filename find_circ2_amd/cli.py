@@ -255,6 +255,16 @@ def main(argv=None, evaluator_factory=None) -> int:
     return 0
 
 
+def _write_bytes(fh, data: bytes):
+    """Bytes to a latin-1 text file (or stdout) without decoding and encoding them again."""
+    buf = getattr(fh, "buffer", None)
+    if buf is None:
+        fh.write(data.decode("latin-1"))
+        return
+    fh.flush()
+    buf.write(data)
+
+
 def _open_failed(out) -> int:
     """The input could not be opened: the reference's pysam.Samfile raises at module level
     (find_circ.py:461-469), an uncaught exception -- traceback, exit status 1."""
@@ -364,7 +374,7 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
         t_rows = time.time()
         for kind, key in ((0, "circs"), (1, "lins")):
             out[key].write(BED_HEADER)
-            out[key].write(nc.rows(kind))
+            _write_bytes(out[key], nc.rows_bytes(kind))
         if startup is not None:
             # the process's phases: what runs before the first record and after the last
             # (device_genome_s overlaps the start of the read loop)
@@ -378,7 +388,9 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
         try:
             nc.finish_reads()
         finally:
+            t_fin = time.time()
             nc.close()
+        t_files = time.time()
         for k, fh in out.items():
             if fh is not None and fh is not sys.stdout:
                 fh.close()
@@ -387,10 +399,17 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             genome_eval.close()
             genome.close()
         if startup is not None and "read_loop_s" in startup:
-            logger.info("process shutdown: outputs_close_s=%.3f, device_release_s=%.3f, process_age_s=%.3f"
-                        % (t_ctx - t_close, time.time() - t_ctx, process_age()))
+            logger.info("process shutdown: reads_gz_finish_s=%.3f, caller_close_s=%.3f, files_close_s=%.3f, "
+                        "device_release_s=%.3f, process_age_s=%.3f"
+                        % (t_fin - t_close, t_files - t_fin, t_ctx - t_files, time.time() - t_ctx, process_age()))
     return 0
 
 
 if __name__ == "__main__":
-    sys.exit(main())
+    rc = main()
+    # every output is closed and flushed by now: leave without the interpreter's and the HIP runtime's
+    # teardown (freeing what the process's exit releases anyway)
+    logging.shutdown()
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(rc)

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -205,7 +206,15 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
     uint64_t nu = 0, ncw = 0;
     std::vector<uint64_t> cs((size_t)std::max(nch, 1), 0);
     if ((rc = fc2_fasta_layout(fa, &nu, &ncw, cs.data()))) return keep(c, rc);
-    std::vector<uint64_t> units(2 * nu), nplane(nu);
+    // left uninitialised: fc2_fasta_pack writes every word (padding units included) on its threads, so
+    // the pages are first touched there in parallel instead of being zeroed here on one thread
+    struct HostWords {
+        std::unique_ptr<uint64_t[]> p;
+        size_t n;
+        explicit HostWords(size_t k) : p(new uint64_t[k]), n(k) {}
+        uint64_t *data() { return p.get(); }
+        size_t size() const { return n; }
+    } units(2 * nu), nplane(nu);
     std::vector<uint32_t> ncoarse((size_t)std::max<uint64_t>(ncw, 1), 0);
     uint64_t n_exotic = 0;
     const double t_alloc = ms();

@@ -600,10 +600,12 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
         const uint64_t cu = ((uint64_t)std::max<int64_t>(r.size, 0) + 63) / 64;
         for (uint64_t u = 0; u < cu; u += 16384) items.push_back({c, u, std::min(cu, u + 16384)});
     }
-    // padding units (between chromosomes / tail) stay all-N
-    parallel_for(nu, T, [&](uint64_t b, uint64_t e) {
-        for (uint64_t u = b; u < e; ++u) { units[2 * u] = 0; units[2 * u + 1] = 0; nplane[u] = ~0ull; }
-    });
+    // every unit belongs to one chromosome (they are laid out back to back, compute_layout) and is
+    // written once below -- a regular chromosome's from the FASTA, an irregular one's as all-N; only
+    // the single unit of a genome without bases is padding
+    uint64_t covered = 0;
+    for (const fc2_chrom_rec &r : f->chroms) covered += ((uint64_t)std::max<int64_t>(r.size, 0) + 63) / 64;
+    for (uint64_t u = covered; u < nu; ++u) { units[2 * u] = 0; units[2 * u + 1] = 0; nplane[u] = ~0ull; }
     std::vector<std::vector<uint64_t>> exo(items.size());
     std::atomic<size_t> next{0};
     std::vector<std::thread> pool;
@@ -613,7 +615,14 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
                 const Item it = items[k];
                 const fc2_chrom_rec &r = f->chroms[it.c];
                 const uint64_t gu0 = r.gstart / 64;
-                if (r.regular != 1) continue;  // stays N; pairs on it take the byte path
+                if (r.regular != 1) {           // all N; pairs on it take the byte path
+                    for (uint64_t u = it.u0; u < it.u1; ++u) {
+                        units[2 * (gu0 + u)] = 0;
+                        units[2 * (gu0 + u) + 1] = 0;
+                        nplane[gu0 + u] = ~0ull;
+                    }
+                    continue;
+                }
                 for (uint64_t u = it.u0; u < it.u1; ++u) {
                     uint64_t lo = 0, hi = 0, nn = 0;
                     const int64_t p0 = (int64_t)u * 64;

@@ -421,6 +421,10 @@ class NativeCaller:
         return out
 
     def rows(self, kind: int) -> str:
+        return self.rows_bytes(kind).decode("latin-1")
+
+    def rows_bytes(self, kind: int) -> bytes:
+        """The BED rows as the bytes written (the input's bytes: latin-1 both ways)."""
         t, n = ctypes.c_void_p(), ctypes.c_uint64()
         N.check(N.lib().fc2_caller_rows(self.h, kind, ctypes.byref(t), ctypes.byref(n)))
-        return ctypes.string_at(t.value, n.value).decode("latin-1") if n.value else ""
+        return ctypes.string_at(t.value, n.value) if n.value else b""
