@@ -90,6 +90,11 @@ def gpu_evaluator(genome, hp_options):
     return evaluate
 
 
+# set by `python -m find_circ2_amd.cli`: the process ends right after main() returns, so what only
+# frees memory (the junction tables, the device contexts) is left to its exit
+EXIT_AFTER_MAIN = False
+
+
 def process_age() -> float:
     """Seconds since this process started (/proc/self/stat starttime, clock-tick resolution): what
     interpreter start-up and imports cost before main() runs."""
@@ -380,7 +385,7 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             # (device_genome_s overlaps the start of the read loop)
             startup.update(device_genome_s=getattr(evaluate, "load_s", None) or 0.0,
                            hip_init_s=getattr(evaluate, "hip_init_s", None) or 0.0, read_loop_s=seconds,
-                           tables_s=time.time() - t_rows)
+                           genome_wait_s=getattr(evaluate, "wait_s", 0.0), tables_s=time.time() - t_rows)
             logger.info("process phases: " + ", ".join("%s=%.3f" % kv for kv in startup.items()) +
                         ", process_age_s=%.3f" % process_age())
     finally:
@@ -389,13 +394,14 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             nc.finish_reads()
         finally:
             t_fin = time.time()
-            nc.close()
+            if not EXIT_AFTER_MAIN:             # (the junction tables: freed by the process's exit)
+                nc.close()
         t_files = time.time()
         for k, fh in out.items():
             if fh is not None and fh is not sys.stdout:
                 fh.close()
         t_ctx = time.time()
-        if genome_eval is not None:            # the contexts (device memory, streams), then the FASTA
+        if genome_eval is not None and not EXIT_AFTER_MAIN:   # the contexts, then the FASTA
             genome_eval.close()
             genome.close()
         if startup is not None and "read_loop_s" in startup:
@@ -406,6 +412,7 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
 
 
 if __name__ == "__main__":
+    EXIT_AFTER_MAIN = True
     rc = main()
     # every output is closed and flushed by now: leave without the interpreter's and the HIP runtime's
     # teardown (freeing what the process's exit releases anyway)

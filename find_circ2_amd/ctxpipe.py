@@ -124,6 +124,7 @@ class CtxPipeline:
         self._ready = None
         self._error = None
         self.load_s = self.hip_init_s = None
+        self.wait_s = 0.0
         if background:
             self._ready = threading.Thread(target=self._build_guarded, args=(genome, devices, per_device),
                                            name="fc2-genome-load", daemon=True)
@@ -138,10 +139,14 @@ class CtxPipeline:
             self._error = ex
 
     def wait_ready(self):
-        """The contexts and resident genome are built (raises what building them raised)."""
+        """The contexts and resident genome are built (raises what building them raised); the time
+        spent waiting for them is added up in ``wait_s``."""
         if self._ready is not None:
+            import time
+            t = time.time()
             self._ready.join()
             self._ready = None
+            self.wait_s += time.time() - t
         if self._error is not None:
             raise self._error
 

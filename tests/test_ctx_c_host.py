@@ -113,11 +113,13 @@ def test_c_findcirc_builds_and_fails_cleanly_without_a_gpu(findcirc_host, tmp_pa
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("genome", ["fasta", "folder"])
+@pytest.mark.parametrize("genome", ["fasta", "folder", "long_reads"])
 def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path, genome):
     """The whole read loop and the search driven from C (no Python in the process) write the
     Python CLI's files: both BED tables, multi_events.tsv and spliced_reads.fastq (decompressed).
-    With -G naming a folder, both run in GenomeAccessor's dummy mode (find_circ.py:338-345)."""
+    With -G naming a folder, both run in GenomeAccessor's dummy mode (find_circ.py:338-345); with
+    read parts over 32767 bases the C host evaluates the long pairs (fc2_ctx_scan_long,
+    fc2_caller_submit_long)."""
     import gzip
     import sys
     torch = pytest.importorskip("torch")
@@ -125,7 +127,17 @@ def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path, genome):
         pytest.skip("no GPU")
     from test_ingest import _mixed_sam
     sam = str(tmp_path / "in.sam")
-    fa = _mixed_sam(sam, 3000, seed=4711)
+    if genome == "long_reads":
+        from test_read_limits import _long_read_genome, _long_reads, _sam_of
+        g = _long_read_genome(36000)
+        fa = str(tmp_path / "g.fa")
+        with open(fa, "w") as f:
+            for c, sq in g.items():
+                t = sq.decode()
+                f.write(">%s\n" % c + "".join(t[i:i + 60] + "\n" for i in range(0, len(t), 60)))
+        open(sam, "w").write(_sam_of(g, _long_reads(g, 36000)))
+    else:
+        fa = _mixed_sam(sam, 3000, seed=4711)
     if genome == "folder":
         fa = str(tmp_path / "genome_folder")
         os.makedirs(fa)
@@ -144,7 +156,7 @@ def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path, genome):
         assert b"Switching to dummy mode" in r.stderr
         assert len(circ) == 1                         # the header: all-N windows never hold a GT/AG signal
         return
-    assert len(circ) > 10
+    assert len(circ) > (2 if genome == "long_reads" else 10)
     a = gzip.open(os.path.join(py_out, "spliced_reads.fastq.gz")).read()
     b = gzip.open(os.path.join(c_out, "spliced_reads.fastq.gz")).read()
     assert a == b and len(a) > 1000
