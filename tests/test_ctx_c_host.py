@@ -130,12 +130,13 @@ def test_c_findcirc_equals_the_python_cli(findcirc_host, tmp_path, genome):
     if genome == "long_reads":
         from test_read_limits import _long_read_genome, _long_reads, _sam_of
         g = _long_read_genome(36000)
+        reads = _long_reads(g, 36000)                 # (plants the splice signals into g)
         fa = str(tmp_path / "g.fa")
         with open(fa, "w") as f:
             for c, sq in g.items():
                 t = sq.decode()
                 f.write(">%s\n" % c + "".join(t[i:i + 60] + "\n" for i in range(0, len(t), 60)))
-        open(sam, "w").write(_sam_of(g, _long_reads(g, 36000)))
+        open(sam, "w").write(_sam_of(g, reads))
     else:
         fa = _mixed_sam(sam, 3000, seed=4711)
     if genome == "folder":
