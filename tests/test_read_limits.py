@@ -283,3 +283,89 @@ def test_long_path_vs_oracle(tmp_path, o):
               int(e["n_hits"])) for e in (exp if opt.allhits else exp[:1])], i
     assert n_hit >= 5 if opt.maxdist else n_hit >= 4
     assert int(r.first[0]["x"]) > 55000
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("seed", [21, 22])
+def test_long_path_fuzz_vs_oracle(tmp_path, seed):
+    """The long path over random 32768-36000-base read parts whose windows are drawn independently
+    from three buckets each -- past the chromosome's end, before its start, inside (get_data's 'N'
+    padding, find_circ.py:194-211) -- on a genome with tandem repeats (many ties) and N runs, reads
+    cut around a random junction or random bases with N, both strands, --all-hits with -d 2 and
+    --non-canonical: every pair's first tie, tie count and tie list equal the oracle's."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd import Genome, Options
+    from find_circ2_amd.hotpath import decode_long_splices, scan_long
+    rng = np.random.default_rng(seed)
+    G = 90000
+    g = bytearray(rng.choice(np.frombuffer(b"ACGT", np.uint8), G).tobytes())
+    for _ in range(12):                                   # tandem repeats: runs of equal-scoring x
+        p = int(rng.integers(0, G - 3000))
+        unit = bytes(rng.choice(np.frombuffer(b"ACGT", np.uint8), int(rng.integers(1, 4))).tobytes())
+        g[p:p + 2000] = (unit * 2000)[:2000]
+    for _ in range(4):                                    # N runs
+        p, n = int(rng.integers(0, G - 500)), int(rng.integers(1, 400))
+        g[p:p + n] = b"N" * n
+    for _ in range(40):                                   # GT / AG signals
+        p = int(rng.integers(2, G - 2))
+        g[p:p + 2] = b"GT" if rng.random() < 0.5 else b"AG"
+    opt = Options(allhits=True, noncanonical=bool(seed % 2), maxdist=2)
+    spec, a_pos, b_aend, flags = [], [], [], []
+    for i in range(24):
+        L = int(rng.integers(32768, 36001))
+        kA = int(rng.integers(20, L - 20))
+        v, w = rng.random(), rng.random()
+        if v < 0.25:
+            ap = G + int(rng.integers(-L, 2 * L))
+        elif v < 0.5:
+            ap = int(rng.integers(-2 * L, 100))
+        else:
+            ap = int(rng.integers(0, G - L))
+        if w < 0.25:
+            be = G + int(rng.integers(-L, 2 * L))
+        elif w < 0.5:
+            be = int(rng.integers(-L, L))
+        else:
+            be = int(rng.integers(L, G))
+        cut = 0 <= ap and ap + kA <= G - 2 and be - (L - kA) >= 2 and be <= G and rng.random() < 0.8
+        if cut and rng.random() < 0.7:                     # a donor / acceptor signal at the junction
+            g[ap + kA:ap + kA + 2] = b"GT"
+            g[be - (L - kA) - 2:be - (L - kA)] = b"AG"
+        spec.append((cut, L, kA, ap, be))
+        a_pos.append(ap)
+        b_aend.append(be)
+        flags.append(N.PAIR_PRIMARY_REV if rng.random() < 0.5 else 0)
+    seq = g.decode()
+    reads = [(seq[ap:ap + kA] + seq[be - (L - kA):be] if cut else
+              "".join("ACGTN"[int(c)] for c in rng.integers(0, 5, L))).encode() for cut, L, kA, ap, be in spec]
+    path = _fasta(tmp_path, seq)
+    gen = Genome.from_fasta(path, device="cuda:0")
+    buf = b"".join(reads) + b"\0" * 16
+    lp = np.zeros(len(reads), N.LONG_PAIR_DTYPE)
+    ln = np.array([len(r) for r in reads], np.uint64)
+    lp["read_off"][1:] = np.cumsum(ln[:-1])
+    lp["read_len"], lp["a_pos"], lp["b_aend"], lp["flags"] = ln, a_pos, b_aend, flags
+    res, ties, toff = scan_long(opt, gen, np.frombuffer(buf, np.uint8), lp)
+    assert ((res["info"] & N.RES_DONE) != 0).all()
+    of = oracle.OracleFasta(path)
+    r = oracle.scan_fasta(oracle.params(opt.asize, opt.margin, opt.maxdist, opt.noncanonical, opt.strandpref,
+                                        opt.allhits), of, reads, [0] * len(reads), a_pos, b_aend,
+                          [False] * len(reads), [bool(f & N.PAIR_PRIMARY_REV) for f in flags],
+                          use_fast=True, all_ties=True)
+    got = decode_long_splices(opt, gen, lp, res, ties, toff)
+    n_hit = n_multi = 0
+    for i in range(len(reads)):
+        nt = int(r.n_ties[i])
+        if nt <= 0:
+            assert got[i] == [] or isinstance(got[i], BaseException), (i, nt, got[i])
+            assert int(res["best_x"][i]) == -1, i
+            continue
+        n_hit += 1
+        n_multi += nt > 1
+        assert int(res["best_x"][i]) == int(r.first[i]["x"]) and int(res["n_ties"][i]) == nt, i
+        assert [(t.start, t.end, t.strand, t.gtag, int(t.dist), t.ov, t.n_hits) for t in got[i]] == \
+            [(int(e["start"]), int(e["end"]), e["strand"].decode(), e["gtag"].decode(), int(e["dist"]), int(e["ov"]),
+              int(e["n_hits"])) for e in r.ties_of(i)], i
+    assert n_hit >= 3, n_hit
