@@ -1,0 +1,65 @@
+"""Where the CLI's process wall goes after main() returns (DESIGN.md §5 start-up): the CLI as its own
+process on bench.cli_end_to_end's 2M-read input, main() run either as `python -m` does (memory left
+to the exit) or releasing the junction tables, contexts and FASTA first; each child writes its clock
+and /proc/self/status memory lines just before os._exit, the parent notes when wait() returns.
+One JSON line per run on stdout."""
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+CHILD = r"""
+import os, sys, time
+sys.argv = ["find_circ2_amd.cli"] + %r
+import find_circ2_amd.cli as c
+c.EXIT_AFTER_MAIN = %r
+rc = c.main()
+mem = {l.split(":")[0]: l.split(":")[1].strip() for l in open("/proc/self/status") if l.startswith(("VmRSS", "VmHWM", "RssAnon", "RssFile", "VmPin", "VmLck"))}
+open(%r, "w").write(repr((time.time(), c.process_age(), mem)))
+sys.stdout.flush(); sys.stderr.flush()
+os._exit(rc)
+"""
+
+
+def main():
+    import numpy as np
+    from cli_scale_check import make_genome, write_fasta, write_sam
+    from find_circ2_amd import sq_table
+    from find_circ2_amd.ingest import sam_to_bam
+    reads = int(sys.argv[1]) if len(sys.argv) > 1 else 2_000_000
+    d = tempfile.mkdtemp(prefix="fc2_exit_", dir="/tmp")
+    fa, sam, bam = (os.path.join(d, x) for x in ("genome.fa", "reads.sam", "reads.bam"))
+    rng = np.random.default_rng(2024)
+    names, sizes = sq_table(os.path.join(ROOT, "tests", "golden", "test_norm.sam"))
+    seqs = make_genome(fa, names, sizes, rng)
+    write_sam(sam, seqs, reads, rng)
+    write_fasta(fa, seqs)
+    del seqs
+    sam_to_bam(sam, bam)
+    print(json.dumps({"prepared": d}), flush=True)
+    for rep in range(4):
+        for exit_after in (True, False):
+            out = os.path.join(d, "o%d%d" % (rep, exit_after))
+            marker = os.path.join(d, "m")
+            args = ["-G", fa, "-o", out, "-q", sam]
+            t0 = time.time()
+            rc = subprocess.run([sys.executable, "-c", CHILD % (args, exit_after, marker)], cwd=ROOT,
+                                timeout=600).returncode
+            t1 = time.time()
+            t_mark, age, mem = eval(open(marker).read())
+            log = open(os.path.join(out, "run.log")).read()
+            sd = [l for l in log.splitlines() if "process shutdown" in l]
+            print(json.dumps({"rep": rep, "exit_after_main": exit_after, "rc": rc, "wall_s": round(t1 - t0, 3),
+                              "age_at_exit_s": round(age, 3), "exit_gap_s": round(t1 - t_mark, 3),
+                              "before_exit_s": round(t_mark - t0, 3), "mem": mem,
+                              "shutdown": sd[0].split("process shutdown: ")[1] if sd else None}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
