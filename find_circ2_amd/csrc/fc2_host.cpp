@@ -12,6 +12,7 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <immintrin.h>
 
 #include <algorithm>
 #include <atomic>
@@ -99,6 +100,48 @@ struct PackTable {
 };
 static const PackTable kPackTable;
 static inline uint32_t pack_code(uint8_t c) { return kPackTable.t[c]; }
+
+// The bases of up to 64 FASTA bytes as bit masks (bit j = byte j): a/c/g/t/n = the byte upper-cased
+// is that letter (the reference's .upper(), find_circ.py:901-902, on the 2-bit pack's classes).
+struct BaseMasks {
+    uint64_t a, c, g, t, n;
+};
+
+static inline BaseMasks base_masks_scalar(const uint8_t *s, int len) {
+    BaseMasks m{0, 0, 0, 0, 0};
+    for (int j = 0; j < len; ++j) {
+        const uint64_t bit = 1ull << j;
+        switch (s[j] & 0xDF) {
+            case 'A': m.a |= bit; break;
+            case 'C': m.c |= bit; break;
+            case 'G': m.g |= bit; break;
+            case 'T': m.t |= bit; break;
+            case 'N': m.n |= bit; break;
+            default: break;
+        }
+    }
+    return m;
+}
+
+// 64 bytes at s (all readable): one compare per letter per 32 bytes.  (b & 0xDF) == 'A' holds for
+// 'A' and 'a' only, as upc() + bclass() classify.
+__attribute__((target("avx2"))) static BaseMasks base_masks_avx2(const uint8_t *s) {
+    const __m256i up = _mm256_set1_epi8((char)0xDF);
+    const __m256i v0 = _mm256_and_si256(_mm256_loadu_si256((const __m256i *)s), up);
+    const __m256i v1 = _mm256_and_si256(_mm256_loadu_si256((const __m256i *)(s + 32)), up);
+#define FC2_MASK64(ch)                                                                                     \
+    ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v0, _mm256_set1_epi8(ch))) |                 \
+     (uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v1, _mm256_set1_epi8(ch))) << 32)
+    const BaseMasks m{FC2_MASK64('A'), FC2_MASK64('C'), FC2_MASK64('G'), FC2_MASK64('T'), FC2_MASK64('N')};
+#undef FC2_MASK64
+    return m;
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+static const bool kHaveAvx2 = false;           // (hipcc's device pass over this host-only file)
+#else
+static const bool kHaveAvx2 = (__builtin_cpu_init(), __builtin_cpu_supports("avx2"));
+#endif
 
 // every byte of u (already upper-cased with & 0xDF) is one of 'A' 'C' 'G' 'T' (exact zero-byte tests)
 static inline bool acgt8(uint64_t u) {
@@ -623,41 +666,41 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
                     }
                     continue;
                 }
-                for (uint64_t u = it.u0; u < it.u1; ++u) {
-                    uint64_t lo = 0, hi = 0, nn = 0;
-                    const int64_t p0 = (int64_t)u * 64;
-                    const int64_t p1 = std::min<int64_t>(p0 + 64, r.size);
-                    int64_t col = p0 % r.ldata;
-                    const uint8_t *src = f->data + r.ofs + (p0 / r.ldata) * (r.ldata + r.skip) + col;
-                    uint32_t exotic = 0;
-                    // line segments of the unit: table lookups, no branches per base
-                    for (int b = 0; b < (int)(p1 - p0);) {
-                        const int seg = (int)std::min<int64_t>(r.ldata - col, (p1 - p0) - b);
-                        for (int j = 0; j < seg; ++j) {
-                            const uint32_t c = pack_code(src[j]);
-                            lo |= (uint64_t)(c & 1u) << (b + j);
-                            hi |= (uint64_t)((c >> 1) & 1u) << (b + j);
-                            nn |= (uint64_t)((c >> 2) & 1u) << (b + j);
-                            exotic |= c >> 3;
-                        }
-                        b += seg;
-                        src += seg;
-                        col += seg;
-                        if (col == r.ldata) { col = 0; src += r.skip; }
+                // the item's bases in segments that stay inside one line and one unit: each segment's
+                // class masks (64-byte vector compares where 64 bytes are mapped, else byte by byte)
+                // shifted into the unit's planes; a unit is written once, when full or at the end
+                const int64_t ld = r.ldata;
+                int64_t p = (int64_t)it.u0 * 64;
+                const int64_t pend = std::min<int64_t>((int64_t)it.u1 * 64, r.size);
+                int64_t col = p % ld;
+                const uint8_t *src = f->data + r.ofs + (p / ld) * (ld + r.skip) + col;
+                const uint8_t *const fend = f->data + f->n;
+                uint64_t u = gu0 + it.u0, lo = 0, hi = 0, nn = 0;
+                int b = 0;
+                while (p < pend) {
+                    const int seg = (int)std::min<int64_t>(std::min<int64_t>(ld - col, pend - p), 64 - b);
+                    const BaseMasks m = (kHaveAvx2 && fend - src >= 64) ? base_masks_avx2(src) : base_masks_scalar(src, seg);
+                    const uint64_t keep = seg == 64 ? ~0ull : (1ull << seg) - 1;
+                    const uint64_t acgt = m.a | m.c | m.g | m.t;
+                    lo |= ((m.c | m.t) & keep) << b;
+                    hi |= ((m.g | m.t) & keep) << b;
+                    nn |= (~acgt & keep) << b;
+                    for (uint64_t ex = ~(acgt | m.n) & keep; ex; ex &= ex - 1)   // rare: not ACGTN
+                        exo[k].push_back(r.gstart + (uint64_t)p + (uint64_t)__builtin_ctzll(ex));
+                    b += seg;
+                    p += seg;
+                    src += seg;
+                    col += seg;
+                    if (col == ld) { col = 0; src += r.skip; }
+                    if (b == 64 || p == pend) {
+                        if (b < 64) nn |= ~0ull << b;      // past the chromosome's end
+                        units[2 * u] = lo;
+                        units[2 * u + 1] = hi;
+                        nplane[u] = nn;
+                        ++u;
+                        lo = hi = nn = 0;
+                        b = 0;
                     }
-                    if (exotic) {                 // rare: record the exotic positions
-                        int64_t off = r.ofs + (p0 / r.ldata) * (r.ldata + r.skip) + p0 % r.ldata;
-                        int64_t cl2 = p0 % r.ldata;
-                        for (int64_t p = p0; p < p1; ++p) {
-                            if (bclass(f->data[off]) == 5) exo[k].push_back(r.gstart + (uint64_t)p);
-                            ++off;
-                            if (++cl2 == r.ldata) { cl2 = 0; off += r.skip; }
-                        }
-                    }
-                    for (int b = (int)(p1 - p0); b < 64; ++b) nn |= 1ull << b;
-                    units[2 * (gu0 + u)] = lo;
-                    units[2 * (gu0 + u) + 1] = hi;
-                    nplane[gu0 + u] = nn;
                 }
             }
         });

@@ -43,14 +43,17 @@ def main():
     del seqs
     sam_to_bam(sam, bam)
     print(json.dumps({"prepared": d}), flush=True)
-    for rep in range(4):
+    for rep in range(2):
         for exit_after in (True, False):
             out = os.path.join(d, "o%d%d" % (rep, exit_after))
             marker = os.path.join(d, "m")
             args = ["-G", fa, "-o", out, "-q", sam]
             t0 = time.time()
-            rc = subprocess.run([sys.executable, "-c", CHILD % (args, exit_after, marker)], cwd=ROOT,
-                                timeout=600).returncode
+            env = dict(os.environ, FC2_CALLER_TIMING="1")
+            pr = subprocess.run([sys.executable, "-c", CHILD % (args, exit_after, marker)], cwd=ROOT, env=env,
+                                timeout=600, stderr=subprocess.PIPE, text=True)
+            rc = pr.returncode
+            gl = [l for l in pr.stderr.splitlines() if l.startswith("genome load")]
             t1 = time.time()
             t_mark, age, mem = eval(open(marker).read())
             log = open(os.path.join(out, "run.log")).read()
@@ -58,7 +61,29 @@ def main():
             print(json.dumps({"rep": rep, "exit_after_main": exit_after, "rc": rc, "wall_s": round(t1 - t0, 3),
                               "age_at_exit_s": round(age, 3), "exit_gap_s": round(t1 - t_mark, 3),
                               "before_exit_s": round(t_mark - t0, 3), "mem": mem,
-                              "shutdown": sd[0].split("process shutdown: ")[1] if sd else None}), flush=True)
+                              "shutdown": sd[0].split("process shutdown: ")[1] if sd else None,
+                              "genome_load": gl[0] if gl else None}), flush=True)
+    # bare processes: the interpreter alone, HIP initialised, one context with the genome resident
+    for what, code in (("bare", "pass"),
+                       ("hip_ctx", "from find_circ2_amd import ctxpipe as C, _native as N\n"
+                                   "import ctypes\nh = ctypes.c_void_p()\nN.check(N.lib().fc2_ctx_create(0, ctypes.byref(h)))"),
+                       ("hip_ctx_genome", "from find_circ2_amd import ctxpipe as C, _native as N\n"
+                                          "import ctypes\nh = ctypes.c_void_p()\nN.check(N.lib().fc2_ctx_create(0, ctypes.byref(h)))\n"
+                                          "g = C.FastaGenome(%r)\nN.check(N.lib().fc2_ctx_genome_load(h, g.fasta, 0))" % fa),
+                       ("hip_ctx_genome_released", "from find_circ2_amd import ctxpipe as C, _native as N\n"
+                                          "import ctypes\nh = ctypes.c_void_p()\nN.check(N.lib().fc2_ctx_create(0, ctypes.byref(h)))\n"
+                                          "g = C.FastaGenome(%r)\nN.check(N.lib().fc2_ctx_genome_load(h, g.fasta, 0))\n"
+                                          "N.lib().fc2_ctx_destroy(h)\ng.close()" % fa)):
+        for rep in range(2):
+            marker = os.path.join(d, "m")
+            src = ("import os, sys, time\nsys.path.insert(0, %r)\n" % ROOT + code +
+                   "\nopen(%r, 'w').write(repr(time.time()))\nos._exit(0)\n" % marker)
+            t0 = time.time()
+            rc = subprocess.run([sys.executable, "-c", src], cwd=ROOT, timeout=300).returncode
+            t1 = time.time()
+            t_mark = eval(open(marker).read())
+            print(json.dumps({"what": what, "rep": rep, "rc": rc, "wall_s": round(t1 - t0, 3),
+                              "exit_gap_s": round(t1 - t_mark, 3)}), flush=True)
 
 
 if __name__ == "__main__":
