@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <functional>
 #include <string>
 #include <thread>
@@ -624,6 +625,9 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
     if (!compute_layout(f, &nu))
         return fail(FC2_E_RANGE, "fc2_fasta_pack: chromosome sizes add up to more than 2^40 bases (a damaged index?)");
     const int T = n_workers(n_threads);
+    static const bool timing = getenv("FC2_CALLER_TIMING") != nullptr;      // phase times on stderr
+    const auto t0 = std::chrono::steady_clock::now();
+    auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     // regularity per chromosome
     {
         std::atomic<size_t> next{0};
@@ -635,6 +639,7 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
             });
         for (auto &th : pool) th.join();
     }
+    const double t_regular = ms();
     // work items: (chrom, unit range) of <= 2^14 units
     struct Item { int c; uint64_t u0, u1; };
     std::vector<Item> items;
@@ -705,6 +710,7 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
             }
         });
     for (auto &th : pool) th.join();
+    const double t_planes = ms();
     f->exotic.clear();
     for (auto &v : exo) f->exotic.insert(f->exotic.end(), v.begin(), v.end());
     // irregular chromosomes: every base is "exotic" for routing purposes (handled by chrom flag)
@@ -726,6 +732,9 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
         }
     });
     if (n_exotic) *n_exotic = f->exotic.size();
+    if (timing)
+        fprintf(stderr, "fasta pack: line check %.1f ms, planes %.1f ms, coarse N map %.1f ms (%d threads)\n", t_regular,
+                t_planes - t_regular, ms() - t_planes, T);
     f->packed = true;
     return FC2_OK;
 }

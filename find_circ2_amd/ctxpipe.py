@@ -124,6 +124,8 @@ class CtxPipeline:
         self._ready = None
         self._error = None
         self.load_s = self.hip_init_s = None
+        self.genome_load_s = 0.0                    # fc2_ctx_genome_load calls (pack + upload + tables)
+        self.siblings_s = 0.0                       # fc2_ctx_create_sibling calls
         self.wait_s = 0.0
         if background:
             self._ready = threading.Thread(target=self._build_guarded, args=(genome, devices, per_device),
@@ -166,15 +168,19 @@ class CtxPipeline:
                     c = _Ctx(h, dev)
                     c.primary = True
                     self.ctxs.append(c)
+                    tg = time.time()
                     c.check(L.fc2_ctx_genome_load(h, genome.fasta, self.n_threads))
+                    self.genome_load_s += time.time() - tg
                     primary[dev] = c
                     k0 = 1
                 else:
                     k0 = 0                 # a device listed twice: more contexts on it (--gpus N > devices)
                 for _ in range(k0, per_device):
+                    ts = time.time()
                     h = ctypes.c_void_p()
                     N.check(L.fc2_ctx_create_sibling(primary[dev].h, ctypes.byref(h)))
                     self.ctxs.append(_Ctx(h, dev))
+                    self.siblings_s += time.time() - ts
         except BaseException:
             self.close()
             raise
