@@ -4,11 +4,21 @@ One hot path of find_circ2 (find_circ.py 1.99), ``JunctionSpan.find_breakpoints`
 plus its genome window fetch, as hand-written HIP kernels for gfx950 behind a
 C ABI (include/fc2_bp.h, libfc2.so).  See DESIGN.md.
 """
-from . import _native
-from .genome import Genome, sq_table, synthetic_n_intervals
-from .hotpath import (BreakpointEngine, BreakpointError, CompactResults, JunctionSpan, Options, PairBatch, ScanOutput,
-                      Splice, SynthConfig, compact, decode_splices, expand, first_tie_arrays, gtag_str, reorder, scan,
-                      splices_or_raise)
+import os as _os
+import sys as _sys
+
+# `python -m find_circ2_amd.<module>` (the CLI): nothing of this package calls BLAS, and OpenBLAS's
+# thread pool, started when numpy is first imported (one thread per OMP_NUM_THREADS), costs the
+# process ~0.1 s of start-up.  While -m locates the module, sys.argv[0] is "-m"; an explicit
+# OPENBLAS_NUM_THREADS stays as given, and a library import leaves the environment alone.
+if _sys.argv[:1] == ["-m"] and "numpy" not in _sys.modules:
+    _os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+
+from . import _native  # noqa: E402
+from .genome import Genome, sq_table, synthetic_n_intervals  # noqa: E402
+from .hotpath import (BreakpointEngine, BreakpointError, CompactResults, JunctionSpan, Options,  # noqa: E402
+                      PairBatch, ScanOutput, Splice, SynthConfig, compact, decode_splices, expand,
+                      first_tie_arrays, gtag_str, reorder, scan, splices_or_raise)
 
 __version__ = "0.1.0"
 

@@ -7,11 +7,13 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <sys/mman.h>
 
 #include <algorithm>
 #include <chrono>
 #include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/fc2_bp.h"
@@ -206,15 +208,29 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
     uint64_t nu = 0, ncw = 0;
     std::vector<uint64_t> cs((size_t)std::max(nch, 1), 0);
     if ((rc = fc2_fasta_layout(fa, &nu, &ncw, cs.data()))) return keep(c, rc);
-    // left uninitialised: fc2_fasta_pack writes every word (padding units included) on its threads, so
-    // the pages are first touched there in parallel instead of being zeroed here on one thread
+    // anonymous mappings left untouched: fc2_fasta_pack writes every word (padding units included) on
+    // its threads, so the pages are first touched there in parallel; huge pages where the kernel gives
+    // them (fewer faults); unmapped on a thread of their own once uploaded, so the ~1 GB of an hg19
+    // genome is not released on the caller's time (the read loop waits for this call)
     struct HostWords {
-        std::unique_ptr<uint64_t[]> p;
-        size_t n;
-        explicit HostWords(size_t k) : p(new uint64_t[k]), n(k) {}
-        uint64_t *data() { return p.get(); }
+        uint64_t *p = nullptr;
+        size_t n, bytes;
+        explicit HostWords(size_t k) : n(k), bytes(std::max<size_t>(k, 1) * 8) {
+            void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+            if (m == MAP_FAILED) return;
+            (void)madvise(m, bytes, MADV_HUGEPAGE);
+            p = (uint64_t *)m;
+        }
+        ~HostWords() {
+            if (!p) return;
+            void *m = p;
+            const size_t b = bytes;
+            std::thread([m, b] { munmap(m, b); }).detach();
+        }
+        uint64_t *data() { return p; }
         size_t size() const { return n; }
     } units(2 * nu), nplane(nu);
+    if (!units.p || !nplane.p) return keep(c, fc2::fail(FC2_E_OS, "fc2_ctx_genome_load: cannot map host memory for the 2-bit genome"));
     std::vector<uint32_t> ncoarse((size_t)std::max<uint64_t>(ncw, 1), 0);
     uint64_t n_exotic = 0;
     const double t_alloc = ms();

@@ -18,6 +18,7 @@
 #include <atomic>
 #include <chrono>
 #include <functional>
+#include <memory>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -105,13 +106,14 @@ static inline uint32_t pack_code(uint8_t c) { return kPackTable.t[c]; }
 // The bases of up to 64 FASTA bytes as bit masks (bit j = byte j): a/c/g/t/n = the byte upper-cased
 // is that letter (the reference's .upper(), find_circ.py:901-902, on the 2-bit pack's classes).
 struct BaseMasks {
-    uint64_t a, c, g, t, n;
+    uint64_t a, c, g, t, n, nl;                 // nl: '\n' (a line break inside a row: irregular layout)
 };
 
 static inline BaseMasks base_masks_scalar(const uint8_t *s, int len) {
-    BaseMasks m{0, 0, 0, 0, 0};
+    BaseMasks m{0, 0, 0, 0, 0, 0};
     for (int j = 0; j < len; ++j) {
         const uint64_t bit = 1ull << j;
+        if (s[j] == '\n') m.nl |= bit;
         switch (s[j] & 0xDF) {
             case 'A': m.a |= bit; break;
             case 'C': m.c |= bit; break;
@@ -128,12 +130,13 @@ static inline BaseMasks base_masks_scalar(const uint8_t *s, int len) {
 // 'A' and 'a' only, as upc() + bclass() classify.
 __attribute__((target("avx2"))) static BaseMasks base_masks_avx2(const uint8_t *s) {
     const __m256i up = _mm256_set1_epi8((char)0xDF);
-    const __m256i v0 = _mm256_and_si256(_mm256_loadu_si256((const __m256i *)s), up);
-    const __m256i v1 = _mm256_and_si256(_mm256_loadu_si256((const __m256i *)(s + 32)), up);
-#define FC2_MASK64(ch)                                                                                     \
-    ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v0, _mm256_set1_epi8(ch))) |                 \
-     (uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v1, _mm256_set1_epi8(ch))) << 32)
-    const BaseMasks m{FC2_MASK64('A'), FC2_MASK64('C'), FC2_MASK64('G'), FC2_MASK64('T'), FC2_MASK64('N')};
+    const __m256i r0 = _mm256_loadu_si256((const __m256i *)s), r1 = _mm256_loadu_si256((const __m256i *)(s + 32));
+    const __m256i v0 = _mm256_and_si256(r0, up), v1 = _mm256_and_si256(r1, up);
+#define FC2_MASK64(x0, x1, ch)                                                                             \
+    ((uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(x0, _mm256_set1_epi8(ch))) |                 \
+     (uint64_t)(uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(x1, _mm256_set1_epi8(ch))) << 32)
+    const BaseMasks m{FC2_MASK64(v0, v1, 'A'), FC2_MASK64(v0, v1, 'C'), FC2_MASK64(v0, v1, 'G'),
+                      FC2_MASK64(v0, v1, 'T'), FC2_MASK64(v0, v1, 'N'), FC2_MASK64(r0, r1, '\n')};
 #undef FC2_MASK64
     return m;
 }
@@ -583,38 +586,28 @@ extern "C" int fc2_fasta_layout(const fc2_fasta *cf, uint64_t *n_units, uint64_t
 
 // Is the chromosome laid out exactly as the index arithmetic assumes?  Then
 // get_data's slice-and-strip yields base p at file offset ofs + (p//ldata)*skip + p.
-static bool chrom_regular(const fc2_fasta *f, const fc2_chrom_rec &c) {
+// The layout checks of a chromosome that need no pass over its bases: its rows (ldata bytes each, then
+// the separator skipchar, find_circ.py:204-209) lie inside the file and the separator is whitespace.
+// The per-row part -- no '\n' inside a row, the separator present after each full row -- is checked
+// by the pack's pass itself (fc2_fasta_pack); a chromosome failing either is irregular: stored as N,
+// its pairs restated on the byte path (get_data's string slicing).
+static bool chrom_rows_in_file(const fc2_fasta *f, const fc2_chrom_rec &c) {
     if (c.size <= 0) return true;
     if (c.ldata <= 0) return false;
     if ((int64_t)c.skipchar.size() != c.skip) return false;
     // an index entry (.byo_index) that points outside the file: get_data's Python slices clip or wrap
-    // there, which only the byte path restates; the loop below then never leaves [0, n]
+    // there, which only the byte path restates; the pack's pass then never leaves [0, n]
     const int64_t n = (int64_t)f->n;
     if (c.ofs < 0 || c.ofs > n || c.ldata > n || c.size > n) return false;
     for (char ch : c.skipchar)
         if (!py_isspace((uint8_t)ch)) return false;
     const int64_t nfull = c.size / c.ldata, rem = c.size % c.ldata;
-    const int64_t stride = c.ldata + c.skip;
-    for (int64_t k = 0; k < nfull; ++k) {
-        const int64_t st = c.ofs + k * stride;
-        if (st + c.ldata > (int64_t)f->n) return false;
-        if (memchr(f->data + st, '\n', (size_t)c.ldata)) return false;
-        const int64_t te = st + c.ldata;
-        const bool last = (k == nfull - 1) && rem == 0;
-        if (te + c.skip <= (int64_t)f->n) {
-            if (memcmp(f->data + te, c.skipchar.data(), (size_t)c.skip) != 0) {
-                if (!(last && te == (int64_t)f->n)) return false;
-            }
-        } else if (!(last && te == (int64_t)f->n)) {
-            return false;
-        }
-    }
-    if (rem) {
-        const int64_t st = c.ofs + nfull * stride;
-        if (st + rem > (int64_t)f->n) return false;
-        if (memchr(f->data + st, '\n', (size_t)rem)) return false;
-    }
-    return true;
+    int64_t stride, last;                        // the end of the last row
+    if (__builtin_add_overflow(c.ldata, c.skip, &stride) ||
+        __builtin_mul_overflow(rem ? nfull : nfull - 1, stride, &last) ||
+        __builtin_add_overflow(last, c.ofs + (rem ? rem : c.ldata), &last))
+        return false;
+    return last <= n;
 }
 
 extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,
@@ -628,17 +621,10 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
     static const bool timing = getenv("FC2_CALLER_TIMING") != nullptr;      // phase times on stderr
     const auto t0 = std::chrono::steady_clock::now();
     auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
-    // regularity per chromosome
-    {
-        std::atomic<size_t> next{0};
-        std::vector<std::thread> pool;
-        for (int t = 0; t < std::min<int>(T, (int)f->chroms.size()); ++t)
-            pool.emplace_back([&] {
-                for (size_t k; (k = next.fetch_add(1)) < f->chroms.size();)
-                    f->chroms[k].regular = chrom_regular(f, f->chroms[k]) ? 1 : 0;
-            });
-        for (auto &th : pool) th.join();
-    }
+    // the layout checks that need no pass over the bases; the rest is checked while packing
+    for (fc2_chrom_rec &r : f->chroms) r.regular = chrom_rows_in_file(f, r) ? 1 : 0;
+    std::unique_ptr<std::atomic<uint8_t>[]> broken(new std::atomic<uint8_t>[std::max<size_t>(1, f->chroms.size())]);
+    for (size_t c = 0; c < f->chroms.size(); ++c) broken[c].store(0, std::memory_order_relaxed);
     const double t_regular = ms();
     // work items: (chrom, unit range) of <= 2^14 units
     struct Item { int c; uint64_t u0, u1; };
@@ -682,10 +668,12 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
                 const uint8_t *const fend = f->data + f->n;
                 uint64_t u = gu0 + it.u0, lo = 0, hi = 0, nn = 0;
                 int b = 0;
+                bool bad = false;
                 while (p < pend) {
                     const int seg = (int)std::min<int64_t>(std::min<int64_t>(ld - col, pend - p), 64 - b);
                     const BaseMasks m = (kHaveAvx2 && fend - src >= 64) ? base_masks_avx2(src) : base_masks_scalar(src, seg);
                     const uint64_t keep = seg == 64 ? ~0ull : (1ull << seg) - 1;
+                    bad |= (m.nl & keep) != 0;
                     const uint64_t acgt = m.a | m.c | m.g | m.t;
                     lo |= ((m.c | m.t) & keep) << b;
                     hi |= ((m.g | m.t) & keep) << b;
@@ -696,7 +684,15 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
                     p += seg;
                     src += seg;
                     col += seg;
-                    if (col == ld) { col = 0; src += r.skip; }
+                    if (col == ld) {
+                        // the separator after a full row; the last row may end the file without it
+                        const int64_t te = src - f->data;
+                        const bool sep = te + r.skip <= (int64_t)f->n &&
+                                         memcmp(src, r.skipchar.data(), (size_t)r.skip) == 0;
+                        bad |= !(sep || (p == r.size && te == (int64_t)f->n));
+                        col = 0;
+                        src += r.skip;
+                    }
                     if (b == 64 || p == pend) {
                         if (b < 64) nn |= ~0ull << b;      // past the chromosome's end
                         units[2 * u] = lo;
@@ -707,9 +703,23 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
                         b = 0;
                     }
                 }
+                if (bad) broken[it.c].store(1, std::memory_order_relaxed);
             }
         });
     for (auto &th : pool) th.join();
+    // chromosomes whose rows turned out irregular: all N, no exotic positions (as if known up front)
+    for (size_t k = 0; k < items.size(); ++k) {
+        const Item it = items[k];
+        if (!broken[it.c].load(std::memory_order_relaxed)) continue;
+        f->chroms[it.c].regular = 0;
+        const uint64_t gu0 = f->chroms[it.c].gstart / 64;
+        for (uint64_t u = it.u0; u < it.u1; ++u) {
+            units[2 * (gu0 + u)] = 0;
+            units[2 * (gu0 + u) + 1] = 0;
+            nplane[gu0 + u] = ~0ull;
+        }
+        exo[k].clear();
+    }
     const double t_planes = ms();
     f->exotic.clear();
     for (auto &v : exo) f->exotic.insert(f->exotic.end(), v.begin(), v.end());
@@ -733,7 +743,7 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
     });
     if (n_exotic) *n_exotic = f->exotic.size();
     if (timing)
-        fprintf(stderr, "fasta pack: line check %.1f ms, planes %.1f ms, coarse N map %.1f ms (%d threads)\n", t_regular,
+        fprintf(stderr, "fasta pack: layout check %.1f ms, planes + row check %.1f ms, coarse N map %.1f ms (%d threads)\n", t_regular,
                 t_planes - t_regular, ms() - t_planes, T);
     f->packed = true;
     return FC2_OK;

@@ -124,3 +124,33 @@ def test_pack_irregular_chromosome_is_all_n(tmp_path):
     for a, b in zip(got[:3], exp[:3]):
         assert np.array_equal(a, b)
     assert got[3] == exp[3]
+
+
+@pytest.mark.parametrize("damage", ["long_row", "short_row", "lf_in_crlf", "last_row_long"])
+def test_pack_row_damage_deep_inside_is_all_n(tmp_path, damage):
+    """A row of the wrong length (or a missing '\\r') past the first work item of a 2.2-Mbase
+    chromosome: the row check of the planes pass makes the whole chromosome irregular (all N, no
+    exotic bases counted), its neighbours unchanged."""
+    rng = np.random.default_rng(17)
+    s0, s1, s2 = _seq(rng, 5000), _seq(rng, 2_200_000), _seq(rng, 3333)
+    eol = b"\r\n" if damage == "lf_in_crlf" else b"\n"
+    rows = [s1[i:i + 50] for i in range(0, len(s1), 50)]
+    k = 1_600_000 // 50 if damage != "last_row_long" else len(rows) - 2
+    if damage in ("long_row", "last_row_long"):
+        rows[k], rows[k + 1] = rows[k] + rows[k + 1][:1], rows[k + 1][1:]
+    elif damage == "short_row":
+        rows[k], rows[k + 1] = rows[k][:-1], rows[k][-1:] + rows[k + 1]
+    body1 = eol.join(rows) + eol
+    if damage == "lf_in_crlf":
+        body1 = body1.replace(rows[k] + b"\r\n", rows[k] + b"\n", 1)
+    path = str(tmp_path / "g.fa")
+    with open(path, "wb") as f:
+        f.write(b">a" + eol + eol.join(s0[i:i + 60] for i in range(0, len(s0), 60)) + eol)
+        f.write(b">b" + eol + body1)
+        f.write(b">c" + eol + eol.join(s2[i:i + 70] for i in range(0, len(s2), 70)) + eol)
+    exp = _expected([s0, s1, s2], [True, False, True])
+    for threads in (1, 8):
+        got = _pack(path, threads)
+        for a, b in zip(got[:3], exp[:3]):
+            assert np.array_equal(a, b)
+        assert got[3] == exp[3]
