@@ -13,7 +13,6 @@
 #include <chrono>
 #include <memory>
 #include <string>
-#include <thread>
 #include <vector>
 
 #include "../../include/fc2_bp.h"
@@ -75,6 +74,39 @@ struct HostBuf {
 
 }  // namespace
 
+// Host words in an anonymous mapping (MADV_HUGEPAGE), unmapped by the owner
+class MappedWords {
+  public:
+    MappedWords() = default;
+    explicit MappedWords(size_t k) : n_(k), bytes_(std::max<size_t>(k, 1) * 8) {
+        void *m = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (m == MAP_FAILED) return;
+        (void)madvise(m, bytes_, MADV_HUGEPAGE);
+        p_ = (uint64_t *)m;
+    }
+    MappedWords(const MappedWords &) = delete;
+    MappedWords &operator=(const MappedWords &) = delete;
+    MappedWords &operator=(MappedWords &&o) noexcept {
+        if (this != &o) {
+            release();
+            p_ = o.p_, n_ = o.n_, bytes_ = o.bytes_;
+            o.p_ = nullptr, o.n_ = o.bytes_ = 0;
+        }
+        return *this;
+    }
+    ~MappedWords() { release(); }
+    void release() {
+        if (p_) munmap(p_, bytes_);
+        p_ = nullptr, n_ = bytes_ = 0;
+    }
+    uint64_t *data() { return p_; }
+    size_t size() const { return n_; }
+    bool ok() const { return p_ != nullptr; }
+  private:
+    uint64_t *p_ = nullptr;
+    size_t n_ = 0, bytes_ = 0;
+};
+
 struct fc2_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -85,6 +117,7 @@ struct fc2_ctx {
     const fc2_fasta *fa = nullptr;
     fc2_genome_view gv{};
     DevBuf units, nplane, ncoarse, cstart, csize, twin, nsuper, wt;
+    MappedWords h_units, h_nplane;             // the host planes the device tables were uploaded from
     // batch
     HostBuf h_pairs, h_words, h_nwords, h_res, h_tm, h_bidx, h_bpairs, h_boff, h_arena;
     DevBuf d_pairs, d_words, d_nwords, d_res, d_tm, d_bidx, d_bpairs, d_boff, d_arena;
@@ -98,6 +131,8 @@ struct fc2_ctx {
     void free_genome() {
         if (!borrowed)
             for (DevBuf *b : {&units, &nplane, &ncoarse, &cstart, &csize, &twin, &nsuper, &wt}) b->release();
+        h_units.release();
+        h_nplane.release();
         borrowed = false;
         gv = fc2_genome_view{};
         have_genome = false;
@@ -210,27 +245,13 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
     if ((rc = fc2_fasta_layout(fa, &nu, &ncw, cs.data()))) return keep(c, rc);
     // anonymous mappings left untouched: fc2_fasta_pack writes every word (padding units included) on
     // its threads, so the pages are first touched there in parallel; huge pages where the kernel gives
-    // them (fewer faults); unmapped on a thread of their own once uploaded, so the ~1 GB of an hg19
-    // genome is not released on the caller's time (the read loop waits for this call)
-    struct HostWords {
-        uint64_t *p = nullptr;
-        size_t n, bytes;
-        explicit HostWords(size_t k) : n(k), bytes(std::max<size_t>(k, 1) * 8) {
-            void *m = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-            if (m == MAP_FAILED) return;
-            (void)madvise(m, bytes, MADV_HUGEPAGE);
-            p = (uint64_t *)m;
-        }
-        ~HostWords() {
-            if (!p) return;
-            void *m = p;
-            const size_t b = bytes;
-            std::thread([m, b] { munmap(m, b); }).detach();
-        }
-        uint64_t *data() { return p; }
-        size_t size() const { return n; }
-    } units(2 * nu), nplane(nu);
-    if (!units.p || !nplane.p) return keep(c, fc2::fail(FC2_E_OS, "fc2_ctx_genome_load: cannot map host memory for the 2-bit genome"));
+    // them (fewer faults, a cheap unmap).  Kept by the context until its genome is freed: unmapping
+    // ~1 GB here would hold the process's memory map while the caller (the read loop, the sibling
+    // contexts' HIP queues) waits for this call.
+    c->h_units = MappedWords(2 * nu);
+    c->h_nplane = MappedWords(nu);
+    MappedWords &units = c->h_units, &nplane = c->h_nplane;
+    if (!units.ok() || !nplane.ok()) return keep(c, fc2::fail(FC2_E_OS, "fc2_ctx_genome_load: cannot map host memory for the 2-bit genome"));
     std::vector<uint32_t> ncoarse((size_t)std::max<uint64_t>(ncw, 1), 0);
     uint64_t n_exotic = 0;
     const double t_alloc = ms();
@@ -259,7 +280,7 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
         if ((rc = c->wt.reserve(wt_bytes, "word-pair table", false))) return keep(c, rc);
         if ((rc = fc2_wtab_launch(c->units.as<uint64_t>(), nu, c->wt.as<uint32_t>(), s))) return keep(c, rc);
     }
-    const hipError_t e = hipStreamSynchronize(s);          // the host vectors go out of scope here
+    const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return keep(c, hip_fail(e, "genome upload"));
     if (timing)
         fprintf(stderr, "genome load: host vectors %.1f ms, 2-bit pack %.1f ms, device alloc + upload + tables %.1f ms "

@@ -41,7 +41,9 @@ void fc2_ctx_destroy(fc2_ctx *ctx);
  * context's device with every table of fc2_genome_view.  fa must stay open while the context scans
  * (pairs on irregular FASTA layout or exotic bytes read their windows from it).  fa == NULL selects
  * the reference's dummy genome (no -G: every window all 'N', find_circ.py:340-345, 370-371).
- * Replaces a previously loaded genome. */
+ * Replaces a previously loaded genome.  The context keeps the host copy of the 2-bit planes it
+ * uploaded (24 bytes per 64 bases, ~1.2 GB for hg19) until its genome is replaced or it is destroyed:
+ * releasing them inside this call would hold the process's memory map while the caller waits. */
 int  fc2_ctx_genome_load(fc2_ctx *ctx, const fc2_fasta *fa, int n_threads);
 /* The resident genome as fc2_bp_scan_launch takes it (device pointers owned by the context). */
 int  fc2_ctx_genome_view(const fc2_ctx *ctx, fc2_genome_view *out);
