@@ -1,6 +1,6 @@
 """Where the CLI's process wall goes after main() returns (DESIGN.md §5 start-up): the CLI as its own
-process on bench.cli_end_to_end's 2M-read input, main() run either as `python -m` does (memory left
-to the exit) or releasing the junction tables, contexts and FASTA first; each child writes its clock
+process on bench.cli_end_to_end's 2M-read input, main() run as `python -m` does (memory left
+to the exit), then optionally the FASTA mapping dropped and the freed heap trimmed, each timed; each child writes its clock
 and /proc/self/status memory lines just before os._exit, the parent notes when wait() returns.
 One JSON line per run on stdout."""
 import json
@@ -15,13 +15,26 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 CHILD = r"""
-import os, sys, time
+import ctypes, os, sys, time
 sys.argv = ["find_circ2_amd.cli"] + %r
 import find_circ2_amd.cli as c
-c.EXIT_AFTER_MAIN = %r
+c.EXIT_AFTER_MAIN = True
 rc = c.main()
-mem = {l.split(":")[0]: l.split(":")[1].strip() for l in open("/proc/self/status") if l.startswith(("VmRSS", "VmHWM", "RssAnon", "RssFile", "VmPin", "VmLck"))}
-open(%r, "w").write(repr((time.time(), c.process_age(), mem)))
+variant = %r
+libc = ctypes.CDLL("libc.so.6", use_errno=True)
+t0 = time.time()
+if "fasta" in variant:             # drop the FASTA mapping's page-table entries (the pages stay cached)
+    libc.munmap.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+    for l in open("/proc/self/maps"):
+        if l.rstrip().endswith("genome.fa"):
+            a, b = (int(x, 16) for x in l.split()[0].split("-"))
+            libc.munmap(a, b - a)
+t1 = time.time()
+if "trim" in variant:              # hand freed heap back to the kernel
+    libc.malloc_trim(0)
+t2 = time.time()
+mem = {l.split(":")[0]: l.split(":")[1].strip() for l in open("/proc/self/status") if l.startswith(("VmRSS", "RssAnon", "RssFile"))}
+open(%r, "w").write(repr((time.time(), c.process_age(), mem, t1 - t0, t2 - t1)))
 sys.stdout.flush(); sys.stderr.flush()
 os._exit(rc)
 """
@@ -44,25 +57,20 @@ def main():
     sam_to_bam(sam, bam)
     print(json.dumps({"prepared": d}), flush=True)
     for rep in range(2):
-        for exit_after in (True, False):
-            out = os.path.join(d, "o%d%d" % (rep, exit_after))
+        for variant in ("none", "fasta", "fasta+trim"):
+            out = os.path.join(d, "o%d%s" % (rep, variant))
             marker = os.path.join(d, "m")
             args = ["-G", fa, "-o", out, "-q", sam]
             t0 = time.time()
             env = dict(os.environ, FC2_CALLER_TIMING="1")
-            pr = subprocess.run([sys.executable, "-c", CHILD % (args, exit_after, marker)], cwd=ROOT, env=env,
+            pr = subprocess.run([sys.executable, "-c", CHILD % (args, variant, marker)], cwd=ROOT, env=env,
                                 timeout=600, stderr=subprocess.PIPE, text=True)
-            rc = pr.returncode
-            gl = [l for l in pr.stderr.splitlines() if l.startswith("genome load")]
             t1 = time.time()
-            t_mark, age, mem = eval(open(marker).read())
-            log = open(os.path.join(out, "run.log")).read()
-            sd = [l for l in log.splitlines() if "process shutdown" in l]
-            print(json.dumps({"rep": rep, "exit_after_main": exit_after, "rc": rc, "wall_s": round(t1 - t0, 3),
+            t_mark, age, mem, t_fasta, t_trim = eval(open(marker).read())
+            print(json.dumps({"rep": rep, "variant": variant, "rc": pr.returncode, "wall_s": round(t1 - t0, 3),
                               "age_at_exit_s": round(age, 3), "exit_gap_s": round(t1 - t_mark, 3),
-                              "before_exit_s": round(t_mark - t0, 3), "mem": mem,
-                              "shutdown": sd[0].split("process shutdown: ")[1] if sd else None,
-                              "genome_load": gl[0] if gl else None}), flush=True)
+                              "unmap_fasta_s": round(t_fasta, 3), "malloc_trim_s": round(t_trim, 3),
+                              "mem": mem}), flush=True)
     # bare processes: the interpreter alone, HIP initialised, one context with the genome resident
     for what, code in (("bare", "pass"),
                        ("hip_ctx", "from find_circ2_amd import ctxpipe as C, _native as N\n"
