@@ -13,6 +13,11 @@ import sys as _sys
 # OPENBLAS_NUM_THREADS stays as given, and a library import leaves the environment alone.
 if _sys.argv[:1] == ["-m"] and "numpy" not in _sys.modules:
     _os.environ.setdefault("OPENBLAS_NUM_THREADS", "1")
+# `python -m find_circ2_amd.cli`: the device genome is started now, before the imports below (prestart.py)
+_orig = getattr(_sys, "orig_argv", [])
+if _sys.argv[:1] == ["-m"] and "-m" in _orig and _orig[_orig.index("-m") + 1:][:1] == ["find_circ2_amd.cli"]:
+    from . import prestart as _prestart
+    _prestart.start(_sys.argv[1:])
 
 from . import _native  # noqa: E402
 from .genome import Genome, sq_table, synthetic_n_intervals  # noqa: E402

@@ -12,11 +12,7 @@ import subprocess
 
 import numpy as np
 
-_HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libfc2.so")
-# A/B measurements only (scripts/ab_build.sh): load another in-tree build of the library instead
-if os.environ.get("FC2_LIB_VARIANT"):
-    LIB_PATH = os.path.join(_HERE, "libfc2_%s.so" % os.environ["FC2_LIB_VARIANT"])
+from ._libpath import LIB_PATH, _HERE
 
 FC2_OK = 0
 FC2_E_PARAM = -1

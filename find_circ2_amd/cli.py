@@ -15,67 +15,14 @@ from __future__ import annotations
 
 import io
 import logging
-import optparse
 import os
 import sys
 import time
 import traceback
 
+from .cliopts import USAGE, build_parser  # noqa: F401  (cli.build_parser: the tests' entry)
+
 __version__ = "1.99"
-
-USAGE = """
-   bwa mem -t<threads> [-p] -A2 -B10 -k 15 -T 1 $GENOME_INDEX reads.fastq.gz | %prog [options]
-
-   OR:
-
-   %prog [options] <bwa_mem_genome_alignments.bam>
-"""
-
-
-def build_parser() -> optparse.OptionParser:
-    p = optparse.OptionParser(usage=USAGE)
-    a = p.add_option
-    a("-v", "--version", dest="version", action="store_true", default=False, help="get version information")
-    a("-S", "--system", dest="system", type=str, default="", help="model system database (needs byo; unsupported)")
-    a("-G", "--genome", dest="genome", type=str, default="", help="path to genome (one multichromosome FASTA file)")
-    a("", "--known-circ", dest="known_circ", type=str, default="", help="file with known circRNA junctions (BED6)")
-    a("", "--known-lin", dest="known_lin", type=str, default="", help="file with known linear splice junctions (BED6)")
-    a("-o", "--output", dest="output", default="find_circ_run", help="where to store output")
-    a("-q", "--silent", dest="silent", default=False, action="store_true", help="suppress normal output to stdout")
-    a("", "--stdout", dest="stdout", default=None, choices=['circs', 'lins', 'reads', 'multi', 'test'],
-      help="direct chosen type of output (circs, lins, reads, multi) to stdout instead of file")
-    a("-n", "--name", dest="name", default="unknown", help="tissue/sample name to use (default='unknown')")
-    a("", "--min-uniq-qual", dest="min_uniq_qual", type=int, default=2, help="minimal uniqness for anchor alignments")
-    a("-a", "--anchor", dest="asize", type=int, default=15, help="anchor size (default=15)")
-    a("-m", "--margin", dest="margin", type=int, default=2, help="maximum nts the BP may reside within a segment")
-    a("-d", "--max-mismatch", dest="maxdist", type=int, default=2, help="maximum mismatches in segment extensions")
-    a("", "--short-threshold", dest="short_threshold", type=int, default=100, help="span below which a circ is SHORT")
-    a("", "--huge-threshold", dest="huge_threshold", type=int, default=100000, help="span above which it is HUGE")
-    a("", "--debug", dest="debug", default=False, action="store_true", help="debug output (not implemented)")
-    a("", "--profile", dest="profile", default=False, action="store_true", help="run under cProfile")
-    a("", "--non-canonical", dest="noncanonical", default=False, action="store_true", help="relax GU/AG")
-    a("", "--all-hits", dest="allhits", default=False, action="store_true", help="report each tied hit")
-    a("", "--stranded", dest="stranded", default=False, action="store_true", help="reads are stranded")
-    a("", "--strand-pref", dest="strandpref", default=False, action="store_true", help="prefer matching strand")
-    a("", "--half-unique", dest="halfunique", default=False, action="store_true", help="one unique anchor suffices")
-    a("", "--report-nobridges", dest="report_nobridges", default=False, action="store_true",
-      help="also report junctions lacking a uniquely bridged read")
-    a("-B", "--bam", dest="bam", default=False, action="store_true", help="store anchor alignments in spliced_alignments.bam")
-    a("-t", "--throughput", dest="throughput", default=False, action="store_true", help="print throughput to stderr")
-    a("", "--chunk-size", dest="chunksize", type=int, default=100000, help="reads per chunk (default=100000)")
-    a("", "--noop", dest="noop", default=False, action="store_true", help="only process the alignment stream")
-    a("", "--test", dest="test", default=False, action="store_true", help="compare to splicing encoded in read names")
-    a("", "--no-linear", dest="nolinear", default=False, action="store_true", help="skip linear junctions")
-    a("", "--no-multi", dest="multi_events", default=True, action="store_false", help="do not record multi-events")
-    a("", "--device", dest="device", default="cuda:0", help="HIP device (find_circ2_amd extension)")
-    a("", "--gpus", dest="gpus", type=int, default=1,
-      help="spread the breakpoint search over this many GPUs from --device on (chunks dealt round-robin, "
-           "results merged in input order; more GPUs than present share devices round-robin)")
-    a("", "--python-ingest", dest="python_ingest", default=False, action="store_true",
-      help="parse and group alignments in Python instead of the native ingest (implies --python-caller)")
-    a("", "--python-caller", dest="python_caller", default=False, action="store_true",
-      help="run record_hits and the junction tables in Python (find_circ2_amd.caller) instead of the native caller")
-    return p
 
 
 def gpu_evaluator(genome, hp_options):
@@ -175,13 +122,23 @@ def main(argv=None, evaluator_factory=None) -> int:
     elif evaluator_factory is None:
         # the native read loop's search over the torch-free C ABI (ctxpipe): the genome is indexed
         # (.byo_index read or written, find_circ.py:110-115) and made resident on each device here
+        from . import prestart
         from .ctxpipe import CtxPipeline, FastaGenome
-        t = time.time()
-        genome = FastaGenome.open_or_dummy(options.genome, dummy_warning)
-        startup["genome_index_s"] = time.time() - t
-        # the device genome is built on a thread of its own while the input is opened and its first
-        # chunks are read (the first search waits for it); its time is logged with the phases
-        evaluate = CtxPipeline(genome, hp, devices=_devices(options), background=True)
+        pre = prestart.take(options)
+        if pre is not None:
+            # `python -m`: the FASTA opened and the contexts being built since before the imports
+            # (prestart.py) -- adopted here, their errors raised here as below
+            genome = FastaGenome.adopt(pre, dummy_warning)
+            startup["genome_index_s"] = pre.genome_index_s
+            # (only the number of devices matters here: the prestart resolved them as _devices does)
+            evaluate = CtxPipeline(genome, hp, devices=[options.device] * max(1, options.gpus), prestart=pre)
+        else:
+            t = time.time()
+            genome = FastaGenome.open_or_dummy(options.genome, dummy_warning)
+            startup["genome_index_s"] = time.time() - t
+            # the device genome is built on a thread of its own while the input is opened and its first
+            # chunks are read (the first search waits for it); its time is logged with the phases
+            evaluate = CtxPipeline(genome, hp, devices=_devices(options), background=True)
         if options.gpus > 1:
             logger.info("--gpus %d: chunks dealt round-robin over %s; the search is a few percent of the read "
                         "loop, which is bound by the host's cores (DESIGN.md §6), so more GPUs add little here"
@@ -415,7 +372,11 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
 
 if __name__ == "__main__":
     EXIT_AFTER_MAIN = True
-    rc = main()
+    try:
+        rc = main()
+    except Exception:                   # as the interpreter reports it (traceback, status 1), but without
+        traceback.print_exc()           # a finalisation that the HIP runtime could meet mid-call on the
+        rc = 1                          # genome thread
     # every output is closed and flushed by now: leave without the interpreter's and the HIP runtime's
     # teardown (freeing what the process's exit releases anyway)
     logging.shutdown()

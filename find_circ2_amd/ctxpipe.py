@@ -72,6 +72,26 @@ class FastaGenome:
                 on_dummy()
             return cls(None)
 
+    @classmethod
+    def adopt(cls, pre, on_dummy=None) -> "FastaGenome":
+        """The FASTA the prestart opened (prestart.Prestart): open_or_dummy's outcome, raised or warned
+        here as open_or_dummy does."""
+        pre.fasta_ready.wait()
+        if pre.fasta_error is not None:
+            raise N.Fc2Error(*pre.fasta_error)
+        g = cls(None)
+        if pre.dummy:
+            if on_dummy is not None:
+                on_dummy()
+            return g
+        g.dummy = False
+        g.fasta = ctypes.c_void_p(pre.fasta)
+        for i in range(N.lib().fc2_fasta_n_chrom(g.fasta)):
+            nm = ctypes.c_char_p()
+            N.check(N.lib().fc2_fasta_chrom(g.fasta, i, ctypes.byref(nm), None, None, None, None, None))
+            g.names.append(nm.value.decode("latin-1"))
+        return g
+
     def close(self):
         if self.fasta is not None:
             N.lib().fc2_fasta_close(self.fasta)
@@ -105,11 +125,12 @@ class CtxPipeline:
     per device, siblings share it); ``depth`` = chunks the caller may hold in flight."""
 
     def __init__(self, genome: FastaGenome, options, devices: Sequence = (0,), per_device: int = 2,
-                 n_threads: int = 0, background: bool = False):
+                 n_threads: int = 0, background: bool = False, prestart=None):
         """``background``: create the contexts and make the genome resident on a thread of their own,
         so the caller can open its input and read the first chunks meanwhile (the reference, too,
         touches the genome only when the first span is evaluated, find_circ.py:435-436); the first
-        submit waits for it and raises its error."""
+        submit waits for it and raises its error.  ``prestart``: the contexts prestart.Prestart is
+        building for these devices (the CLI; implies background)."""
         self.options = options
         self.params = options.params()
         self.n_threads = int(n_threads)
@@ -127,7 +148,11 @@ class CtxPipeline:
         self.genome_load_s = 0.0                    # fc2_ctx_genome_load calls (pack + upload + tables)
         self.siblings_s = 0.0                       # fc2_ctx_create_sibling calls
         self.wait_s = 0.0
-        if background:
+        if prestart is not None:
+            self._ready = threading.Thread(target=self._adopt_guarded, args=(prestart,),
+                                           name="fc2-genome-adopt", daemon=True)
+            self._ready.start()
+        elif background:
             self._ready = threading.Thread(target=self._build_guarded, args=(genome, devices, per_device),
                                            name="fc2-genome-load", daemon=True)
             self._ready.start()
@@ -139,6 +164,21 @@ class CtxPipeline:
             self._build(genome, devices, per_device)
         except BaseException as ex:     # noqa: BLE001 -- raised at the first submit
             self._error = ex
+
+    def _adopt_guarded(self, pre):
+        pre.thread.join()
+        if pre.error is not None:
+            self._error = N.Fc2Error(*pre.error)
+            return
+        if len(pre.ctxs) != self.n_ctx:
+            self._error = RuntimeError("genome prestart built %d contexts for %d" % (len(pre.ctxs), self.n_ctx))
+            return
+        for h, dev, primary in pre.ctxs:
+            c = _Ctx(ctypes.c_void_p(h), dev)
+            c.primary = primary
+            self.ctxs.append(c)
+        self.hip_init_s, self.genome_load_s, self.siblings_s = pre.hip_init_s, pre.genome_load_s, pre.siblings_s
+        self.load_s = pre.load_s
 
     def wait_ready(self):
         """The contexts and resident genome are built (raises what building them raised); the time
@@ -189,8 +229,8 @@ class CtxPipeline:
 
     def close(self):
         """Siblings before the contexts whose genome they read."""
-        if self._ready is not None:
-            self._ready.join()
+        if self._ready is not None and self._ready is not threading.current_thread():
+            self._ready.join()          # (from _build's error path on that thread itself: nothing to wait for)
             self._ready = None
         L = N.lib()
         for primary_pass in (False, True):
