@@ -12,6 +12,7 @@ restores the input order.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Iterable, List, Sequence, Tuple
 
 import numpy as np
@@ -105,9 +106,76 @@ def my_bounds(bounds: Sequence[Tuple[int, int]], rank: int, world: int) -> List[
     return [(k, s, e) for k, (s, e) in enumerate(bounds) if k % world == rank]
 
 
+SHM_DIR = "/dev/shm"
+SHM_HEADROOM = 64 << 20
+
+
+def _free_bytes(path: str) -> int:
+    try:
+        st = os.statvfs(path)
+        return st.f_bavail * st.f_frsize
+    except OSError:
+        return 0
+
+
+class _FileSegment:
+    """A MAP_SHARED mapping of a file outside /dev/shm, for a node whose /dev/shm cannot hold the
+    merge buffer (a container's 64 MB default against the ~0.7 GB of configs[3]'s three forms):
+    every rank on the node maps the same file, which page-locks like the tmpfs segment.  Named
+    ``file:<path>`` so the attaching ranks know the kind."""
+    PREFIX = "file:"
+
+    def __init__(self, name: str = None, create: bool = False, size: int = 0):
+        import mmap
+        import tempfile
+        if create:
+            d = tempfile.gettempdir()
+            if _free_bytes(d) < size + SHM_HEADROOM:
+                raise OSError("no room for a %d-byte merge buffer in %s or %s" % (size, SHM_DIR, d))
+            fd, path = tempfile.mkstemp(prefix="fc2_merge_", dir=d)
+            os.ftruncate(fd, size)
+        else:
+            path = name[len(self.PREFIX):]
+            fd = os.open(path, os.O_RDWR)
+            size = os.fstat(fd).st_size
+        try:
+            self._mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        finally:
+            os.close(fd)
+        self.buf = memoryview(self._mm)
+        self.name = self.PREFIX + path
+        self._path = path
+
+    def close(self):
+        self.buf.release()
+        self._mm.close()
+
+    def unlink(self):
+        os.unlink(self._path)
+
+
+def _segment(name: str = None, create: bool = False, size: int = 0):
+    """The node-local segment behind a merge buffer: POSIX shared memory (/dev/shm) when it has room,
+    else a shared file mapping (_FileSegment); attaching ranks follow the creator's choice by name."""
+    if (create and _free_bytes(SHM_DIR) < size + SHM_HEADROOM) or \
+            (not create and name.startswith(_FileSegment.PREFIX)):
+        return _FileSegment(name, create, size)
+    from multiprocessing import resource_tracker, shared_memory
+    shm = shared_memory.SharedMemory(name=name, create=create, size=size)
+    if not create:
+        # the attaching process must not unlink the segment when it exits (Python < 3.13 tracks
+        # every attach as if it owned the segment)
+        try:
+            resource_tracker.unregister(shm._name, "shared_memory")
+        except Exception:
+            pass
+    return shm
+
+
 class SharedResults:
     """Node-local ordered merge of per-pair results: ONE host buffer of n 8-byte ``fc2_result``
-    records in /dev/shm that every rank on the node maps.  A rank copies each of its batches'
+    records in /dev/shm (or a shared file mapping when /dev/shm is too small, _segment) that every
+    rank on the node maps.  A rank copies each of its batches'
     results (D2H, on its own stream) straight to the batch's input offset, so after a barrier rank
     0 holds every result in input order without gathering or reordering anything -- the order
     ``SpliceSiteStorage`` naming (find_circ.py:681-690) and the float weight sums (:544, :563,
@@ -118,17 +186,9 @@ class SharedResults:
     ``close()`` on every rank, rank 0 last (it unlinks)."""
 
     def __init__(self, n: int, name: str = None, create: bool = False, pin: bool = False):
-        from multiprocessing import resource_tracker, shared_memory
         self.n = int(n)
         self.creator = create
-        self.shm = shared_memory.SharedMemory(name=name, create=create, size=max(8, 8 * self.n))
-        if not create:
-            # the attaching process must not unlink the segment when it exits (Python < 3.13 tracks
-            # every attach as if it owned the segment)
-            try:
-                resource_tracker.unregister(self.shm._name, "shared_memory")
-            except Exception:
-                pass
+        self.shm = _segment(name, create, max(8, 8 * self.n))
         self.name = self.shm.name
         self.array = np.ndarray((self.n,), np.int64, buffer=self.shm.buf)
         self._pinned = False
@@ -165,7 +225,6 @@ class SharedCompactResults(SharedResults):
 
     def __init__(self, n: int, bounds: Sequence[Tuple[int, int]], cap: int, name: str = None, create: bool = False,
                  pin: bool = False, width: int = 4):
-        from multiprocessing import resource_tracker, shared_memory
         from . import _native as N
         if width not in (2, 4):
             raise ValueError("width is 2 or 4")
@@ -175,12 +234,7 @@ class SharedCompactResults(SharedResults):
         self._e_bytes = 16 * (self.cap + 1) * nb    # per batch: cap escape slots, then the count's slot
         size = max(64, self._w_bytes + self._e_bytes)
         self.creator = create
-        self.shm = shared_memory.SharedMemory(name=name, create=create, size=size)
-        if not create:
-            try:
-                resource_tracker.unregister(self.shm._name, "shared_memory")
-            except Exception:
-                pass
+        self.shm = _segment(name, create, size)
         self.name = self.shm.name
         buf = self.shm.buf
         self.words = np.ndarray((self.n,), np.uint16 if width == 2 else np.uint32, buffer=buf)

@@ -154,16 +154,21 @@ def test_compact_scan_hg19_shaped_batch_and_refusals():
             scan_compact(bad, g, b, buf.data_ptr(), 2, 0, 0, ctr_t.data_ptr())
 
 
+@pytest.mark.parametrize("file_seg", [False, True], ids=["shm", "file"])
 @pytest.mark.parametrize("width", [2, 4])
-def test_sharded_zero_copy_merge_with_escapes(width):
+def test_sharded_zero_copy_merge_with_escapes(width, file_seg, monkeypatch):
     """bench.py's configs[3] merge on escape-heavy pairs (long reads, -d 6): sub-batch views of one
     batch dealt to 3 "ranks" (shard.round_bounds / my_bounds) each scan straight into ONE page-locked
     SharedCompactResults through its device address (words at the batch's input offset, escapes into
     the batch's slots with batch-relative indices, the count into its slot); merged() -- escapes()
     adding each batch's start back, then fc2_result_expand -- equals the 8-byte scan of the whole
-    batch word for word."""
+    batch word for word.  file_seg: the buffer in a shared file mapping (a node whose /dev/shm has no
+    room, shard._segment), page-locked and written by the GPU the same way."""
+    from find_circ2_amd import shard
     from find_circ2_amd.hotpath import host_device_pointer, scan_compact
     from find_circ2_amd.shard import SharedCompactResults, my_bounds, round_bounds
+    if file_seg:
+        monkeypatch.setattr(shard, "SHM_DIR", "/nonexistent")
     dev = _dev()
     path = os.path.join(GOLDEN, "CDR1as_locus.fa")
     opt = Options(maxdist=6, margin=0)
@@ -176,6 +181,7 @@ def test_sharded_zero_copy_merge_with_escapes(width):
     bounds = round_bounds(b.n, ws, per_rank=2, align=512, tail=2)
     cap = 4096
     m = SharedCompactResults(b.n, bounds, cap, create=True, pin=True, width=width)
+    assert m.name.startswith("file:") == file_seg
     try:
         m.array[:] = 0x5A                                          # poison: every word must be written
         zdev = host_device_pointer(m.array.ctypes.data)

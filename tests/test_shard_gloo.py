@@ -78,14 +78,17 @@ def test_batches_cover_and_partition():
         shard.ordered_merge([[(0, np.zeros(1))]], 2)
 
 
-def _shm_worker(rank, world, port, n, batch, q):
+def _shm_worker(rank, world, port, n, batch, q, file_seg=False):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
+    if file_seg:                                 # a node whose /dev/shm has no room: the file fallback
+        shard.SHM_DIR = "/nonexistent"
     pairs = np.arange(n, dtype=np.int64) * 31 + 7
     merged = shard.SharedResults(n, create=True) if rank == 0 else None
     name = shard.broadcast_name(merged.name if rank == 0 else None)
+    assert name.startswith("file:") == file_seg
     if rank != 0:
         merged = shard.SharedResults(n, name=name)
     dist.barrier()
@@ -102,16 +105,18 @@ def _shm_worker(rank, world, port, n, batch, q):
     dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("file_seg", [False, True], ids=["shm", "file"])
 @pytest.mark.parametrize("n", [1000, 1, 0])
-def test_gloo_two_ranks_shared_memory_merge(n):
+def test_gloo_two_ranks_shared_memory_merge(n, file_seg):
     """bench.py's configs[3] merge (shard.SharedResults): ranks write their round-robin batches'
-    results into one node-local buffer at input offsets; rank 0 reads them in input order."""
+    results into one node-local buffer at input offsets; rank 0 reads them in input order -- in
+    /dev/shm, or in a shared file mapping when /dev/shm has no room (shard._segment)."""
     world = 2
     batch = shard.round_robin_batch(n, world, per_rank=3, align=64)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_shm_worker, args=(r, world, port, n, batch, q)) for r in range(world)]
+    procs = [ctx.Process(target=_shm_worker, args=(r, world, port, n, batch, q, file_seg)) for r in range(world)]
     for p in procs:
         p.start()
     merged = q.get(timeout=120)
