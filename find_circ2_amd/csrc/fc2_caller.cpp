@@ -17,6 +17,7 @@
 #include <functional>
 #include <map>
 #include <memory>
+#include <malloc.h>
 #include <mutex>
 #include <set>
 #include <stdexcept>
@@ -775,6 +776,7 @@ struct fc2_caller {
     // capacity, so forming a chunk allocates nothing in steady state, and nothing allocated on one
     // thread is freed on the other
     std::vector<Chunk> spare;
+    bool read_side_released = false;            // release_read_side ran (after the last chunk)
     std::mutex qmu;                             // guards queued and spare
     // fc2_caller_stats' values, published by fc2_caller_next on the thread that advances the input
     // (a recording thread may ask for them while the reader runs)
@@ -2593,8 +2595,46 @@ extern "C" int fc2_caller_close_reads(fc2_caller *h) {
     return FC2_OK;
 }
 
+// Once the input is read and every chunk recorded, the read side's buffers -- the recycled chunks,
+// the fragments, spans and read parts of both sides, ~1 GB at 2M reads when the loop read ahead while
+// the genome loaded -- are only memory: they are destroyed on a thread of their own while the rows are
+// formatted, and the freed heap is handed back (malloc_trim), so neither the rows nor the process's
+// exit pay for their pages.  Nothing reads them again (fc2_caller_next reports the end from `eof`).
+static void release_read_side(fc2_caller *h) {
+    if (h->read_side_released || !h->eof || h->next_err) return;
+    {
+        std::lock_guard<std::mutex> g(h->qmu);
+        if (!h->queued.empty()) return;
+    }
+    h->read_side_released = true;
+    struct Bag {
+        std::vector<fc2_caller::Chunk> spare;
+        std::vector<Frag> f[2];
+        std::vector<Span> s[2];
+        ByteBuf a[2];
+        std::vector<RecFields> recf;
+        std::vector<fc2_caller::Seg> segs;
+    };
+    std::unique_ptr<Bag> b(new Bag);
+    b->spare.swap(h->spare);
+    b->f[0].swap(h->bf_frags), b->f[1].swap(h->frags);
+    b->s[0].swap(h->bf_spans), b->s[1].swap(h->spans);
+    b->a[0].swap(h->bf_arena), b->a[1].swap(h->arena);
+    b->recf.swap(h->bf_recf);
+    b->segs.swap(h->bf_segs);
+    h->bf_nfrags = h->nfrags = 0;
+    try {
+        std::thread([bag = std::move(b)]() mutable {
+            bag.reset();
+            malloc_trim(0);
+        }).detach();
+    } catch (const std::system_error &) {       // no thread: freed at close instead
+    }
+}
+
 extern "C" int fc2_caller_rows(fc2_caller *h, int kind, const char **text, uint64_t *len) {
     if (!h || kind < 0 || kind > 1 || !text || !len) return fc2::fail(FC2_E_PARAM, "fc2_caller_rows: bad arguments");
+    release_read_side(h);
     h->rows_text.clear();
     // the rows of ranges of the dict order formatted on the workers, joined in order
     const size_t nj = h->order[kind].size();

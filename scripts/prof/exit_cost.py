@@ -34,6 +34,13 @@ if "trim" in variant:              # hand freed heap back to the kernel
     libc.malloc_trim(0)
 t2 = time.time()
 mem = {l.split(":")[0]: l.split(":")[1].strip() for l in open("/proc/self/status") if l.startswith(("VmRSS", "RssAnon", "RssFile"))}
+class MI(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_size_t) for k in ("arena", "ordblks", "smblks", "hblks", "hblkhd", "usmblks", "fsmblks",
+                                                "uordblks", "fordblks", "keepcost")]
+libc.mallinfo2.restype = MI
+mi = libc.mallinfo2()
+mem.update(malloc_heap_mb=mi.arena >> 20, malloc_inuse_mb=mi.uordblks >> 20, malloc_free_mb=mi.fordblks >> 20,
+           malloc_mmapped_mb=mi.hblkhd >> 20, malloc_mmapped_n=mi.hblks)
 open(%r, "w").write(repr((time.time(), c.process_age(), mem, t1 - t0, t2 - t1)))
 sys.stdout.flush(); sys.stderr.flush()
 os._exit(rc)
