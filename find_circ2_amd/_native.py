@@ -127,7 +127,7 @@ EXPORTED = [
     "fc2_bp_scan_launch", "fc2_bp_scan_bytes_launch", "fc2_probe_pattern_launch",
     "fc2_result_compact_launch", "fc2_result_expand", "fc2_bp_scan_compact_launch", "fc2_host_device_pointer",
     "fc2_fasta_open", "fc2_fasta_close", "fc2_fasta_n_chrom", "fc2_fasta_chrom", "fc2_fasta_find",
-    "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack",
+    "fc2_fasta_get_upper", "fc2_fasta_layout", "fc2_fasta_pack", "fc2_fasta_prepack",
     "fc2_pack_pairs", "fc2_bytepath_size", "fc2_bytepath_fill", "fc2_window_geometry", "fc2_pack_windows",
     "fc2_gather_windows_launch", "fc2_long_geometry", "fc2_long_fill", "fc2_bp_scan_long_launch",
     "fc2_synth_genome_launch", "fc2_coarse_launch", "fc2_twin_launch", "fc2_wtab_geometry", "fc2_wtab_launch",
@@ -180,9 +180,10 @@ def build(force: bool = False) -> str:
     srcdir = os.path.join(_HERE, "csrc")
     srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_reorder.hip", "fc2_scan32.h",
                                               "fc2_host.cpp", "fc2_ingest.cpp", "fc2_ingest_impl.h", "fc2_caller.cpp",
-                                              "fc2_bamout.cpp", "fc2_bamout.h",
+                                              "fc2_bamout.cpp", "fc2_bamout.h", "fc2_ctx.cpp", "fc2_hostmem.h",
                                               "fc2_common.h", "Makefile")]
-    srcs += [os.path.join(os.path.dirname(_HERE), "include", h) for h in ("fc2_bp.h", "fc2_ingest.h", "fc2_caller.h")]
+    srcs += [os.path.join(os.path.dirname(_HERE), "include", h)
+             for h in ("fc2_bp.h", "fc2_ingest.h", "fc2_caller.h", "fc2_ctx.h")]
     newest = max(os.path.getmtime(s) for s in srcs)
     if force or not os.path.exists(LIB_PATH) or os.path.getmtime(LIB_PATH) < newest:
         subprocess.check_call(["make", "-s", "-C", srcdir])
@@ -225,6 +226,7 @@ def lib() -> ctypes.CDLL:
         "fc2_fasta_get_upper": (ctypes.c_int, [vp, ctypes.c_int, i64, i64, vp, i64, P(i64)]),
         "fc2_fasta_layout": (ctypes.c_int, [vp, P(u64), P(u64), vp]),
         "fc2_fasta_pack": (ctypes.c_int, [vp, vp, vp, vp, P(u64), ctypes.c_int]),
+        "fc2_fasta_prepack": (ctypes.c_int, [vp, ctypes.c_int]),
         "fc2_pack_pairs": (ctypes.c_int, [P(Params), vp, u64, vp, vp, vp, vp, u32, vp, u32, u64, P(u64),
                                           ctypes.c_int]),
         "fc2_bytepath_size": (ctypes.c_int, [P(Params), u64, vp, P(u64), P(u64)]),

@@ -342,6 +342,7 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             # (device_genome_s overlaps the start of the read loop)
             startup.update(device_genome_s=getattr(evaluate, "load_s", None) or 0.0,
                            hip_init_s=getattr(evaluate, "hip_init_s", None) or 0.0,
+                           prepack_s=getattr(evaluate, "prepack_s", 0.0),
                            genome_load_s=getattr(evaluate, "genome_load_s", 0.0),
                            siblings_s=getattr(evaluate, "siblings_s", 0.0), read_loop_s=seconds,
                            genome_wait_s=getattr(evaluate, "wait_s", 0.0), tables_s=time.time() - t_rows)

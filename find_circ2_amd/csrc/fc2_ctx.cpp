@@ -18,6 +18,7 @@
 #include "../../include/fc2_bp.h"
 #include "../../include/fc2_ctx.h"
 #include "fc2_common.h"
+#include "fc2_hostmem.h"
 
 namespace {
 
@@ -74,39 +75,6 @@ struct HostBuf {
 
 }  // namespace
 
-// Host words in an anonymous mapping (MADV_HUGEPAGE), unmapped by the owner
-class MappedWords {
-  public:
-    MappedWords() = default;
-    explicit MappedWords(size_t k) : n_(k), bytes_(std::max<size_t>(k, 1) * 8) {
-        void *m = mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
-        if (m == MAP_FAILED) return;
-        (void)madvise(m, bytes_, MADV_HUGEPAGE);
-        p_ = (uint64_t *)m;
-    }
-    MappedWords(const MappedWords &) = delete;
-    MappedWords &operator=(const MappedWords &) = delete;
-    MappedWords &operator=(MappedWords &&o) noexcept {
-        if (this != &o) {
-            release();
-            p_ = o.p_, n_ = o.n_, bytes_ = o.bytes_;
-            o.p_ = nullptr, o.n_ = o.bytes_ = 0;
-        }
-        return *this;
-    }
-    ~MappedWords() { release(); }
-    void release() {
-        if (p_) munmap(p_, bytes_);
-        p_ = nullptr, n_ = bytes_ = 0;
-    }
-    uint64_t *data() { return p_; }
-    size_t size() const { return n_; }
-    bool ok() const { return p_ != nullptr; }
-  private:
-    uint64_t *p_ = nullptr;
-    size_t n_ = 0, bytes_ = 0;
-};
-
 struct fc2_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -117,7 +85,7 @@ struct fc2_ctx {
     const fc2_fasta *fa = nullptr;
     fc2_genome_view gv{};
     DevBuf units, nplane, ncoarse, cstart, csize, twin, nsuper, wt;
-    MappedWords h_units, h_nplane;             // the host planes the device tables were uploaded from
+    fc2::MappedWords h_units, h_nplane;             // the host planes the device tables were uploaded from
     // batch
     HostBuf h_pairs, h_words, h_nwords, h_res, h_tm, h_bidx, h_bpairs, h_boff, h_arena;
     DevBuf d_pairs, d_words, d_nwords, d_res, d_tm, d_bidx, d_bpairs, d_boff, d_arena;
@@ -248,14 +216,21 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
     // them (fewer faults, a cheap unmap).  Kept by the context until its genome is freed: unmapping
     // ~1 GB here would hold the process's memory map while the caller (the read loop, the sibling
     // contexts' HIP queues) waits for this call.
-    c->h_units = MappedWords(2 * nu);
-    c->h_nplane = MappedWords(nu);
-    MappedWords &units = c->h_units, &nplane = c->h_nplane;
-    if (!units.ok() || !nplane.ok()) return keep(c, fc2::fail(FC2_E_OS, "fc2_ctx_genome_load: cannot map host memory for the 2-bit genome"));
-    std::vector<uint32_t> ncoarse((size_t)std::max<uint64_t>(ncw, 1), 0);
+    fc2::MappedWords &units = c->h_units, &nplane = c->h_nplane;
+    std::vector<uint32_t> ncoarse;
     uint64_t n_exotic = 0;
+    // planes fc2_fasta_prepack made already (while this context's HIP initialisation ran): upload only
+    const bool prepacked = fc2::take_prepacked(fa, nu, units, nplane, ncoarse);
+    if (!prepacked) {
+        units = fc2::MappedWords(2 * nu);
+        nplane = fc2::MappedWords(nu);
+    }
+    if (!units.ok() || !nplane.ok()) return keep(c, fc2::fail(FC2_E_OS, "fc2_ctx_genome_load: cannot map host memory for the 2-bit genome"));
     const double t_alloc = ms();
-    if ((rc = fc2_fasta_pack(fa, units.data(), nplane.data(), ncoarse.data(), &n_exotic, n_threads))) return keep(c, rc);
+    if (!prepacked) {
+        ncoarse.assign((size_t)std::max<uint64_t>(ncw, 1), 0);
+        if ((rc = fc2_fasta_pack(fa, units.data(), nplane.data(), ncoarse.data(), &n_exotic, n_threads))) return keep(c, rc);
+    }
     const double t_pack = ms();
     // device tables (genome.py _upload / _upload_tables)
     const hipStream_t s = c->stream;
@@ -283,8 +258,9 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return keep(c, hip_fail(e, "genome upload"));
     if (timing)
-        fprintf(stderr, "genome load: host vectors %.1f ms, 2-bit pack %.1f ms, device alloc + upload + tables %.1f ms "
-                        "(%llu units)\n", t_alloc, t_pack - t_alloc, ms() - t_pack, (unsigned long long)nu);
+        fprintf(stderr, "genome load: host vectors %.1f ms, 2-bit pack %.1f ms%s, device alloc + upload + tables %.1f ms "
+                        "(%llu units)\n", t_alloc, t_pack - t_alloc, prepacked ? " (prepacked)" : "", ms() - t_pack,
+                (unsigned long long)nu);
     fc2_genome_view &g = c->gv;
     g.units = c->units.as<const uint64_t>();
     g.nplane = c->nplane.as<const uint64_t>();

@@ -26,6 +26,7 @@
 
 #include "fc2_common.h"
 #include "fc2_compact.h"
+#include "fc2_hostmem.h"
 
 namespace fc2 {
 
@@ -181,6 +182,13 @@ struct fc2_fasta {
     std::unordered_map<std::string, int> by_name;
     std::vector<uint64_t> exotic;  // sorted global positions of non-ACGTN bases
     bool packed = false;
+    // the planes fc2_fasta_prepack made, until a context's fc2_ctx_genome_load takes them
+    struct Prepacked {
+        fc2::MappedWords units, nplane;
+        std::vector<uint32_t> ncoarse;
+        uint64_t n_units = 0;
+    };
+    std::unique_ptr<Prepacked> prepacked;
 };
 
 // ---------------------------------------------------------------------------
@@ -747,6 +755,34 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
                 t_planes - t_regular, ms() - t_planes, T);
     f->packed = true;
     return FC2_OK;
+}
+
+extern "C" int fc2_fasta_prepack(fc2_fasta *f, int n_threads) {
+    if (!f) return fail(FC2_E_PARAM, "fc2_fasta_prepack: null");
+    uint64_t nu = 0, ncw = 0;
+    if (int rc = fc2_fasta_layout(f, &nu, &ncw, nullptr)) return rc;
+    std::unique_ptr<fc2_fasta::Prepacked> pp(new fc2_fasta::Prepacked);
+    pp->units = fc2::MappedWords(2 * nu);
+    pp->nplane = fc2::MappedWords(nu);
+    if (!pp->units.ok() || !pp->nplane.ok())
+        return fail(FC2_E_OS, "fc2_fasta_prepack: cannot map host memory for the 2-bit genome");
+    pp->ncoarse.assign((size_t)std::max<uint64_t>(ncw, 1), 0);
+    uint64_t n_exotic = 0;
+    if (int rc = fc2_fasta_pack(f, pp->units.data(), pp->nplane.data(), pp->ncoarse.data(), &n_exotic, n_threads)) return rc;
+    pp->n_units = nu;
+    f->prepacked = std::move(pp);
+    return FC2_OK;
+}
+
+bool fc2::take_prepacked(const fc2_fasta *cf, uint64_t n_units, MappedWords &units, MappedWords &nplane,
+                         std::vector<uint32_t> &ncoarse) {
+    fc2_fasta *f = const_cast<fc2_fasta *>(cf);
+    if (!f || !f->prepacked || f->prepacked->n_units != n_units) return false;
+    units = std::move(f->prepacked->units);
+    nplane = std::move(f->prepacked->nplane);
+    ncoarse.swap(f->prepacked->ncoarse);
+    f->prepacked.reset();
+    return true;
 }
 
 // ---------------------------------------------------------------------------

@@ -147,6 +147,7 @@ class CtxPipeline:
         self.load_s = self.hip_init_s = None
         self.genome_load_s = 0.0                    # fc2_ctx_genome_load calls (pack + upload + tables)
         self.siblings_s = 0.0                       # fc2_ctx_create_sibling calls
+        self.prepack_s = 0.0                        # fc2_fasta_prepack beside HIP init (prestart only)
         self.wait_s = 0.0
         if prestart is not None:
             self._ready = threading.Thread(target=self._adopt_guarded, args=(prestart,),
@@ -178,6 +179,7 @@ class CtxPipeline:
             c.primary = primary
             self.ctxs.append(c)
         self.hip_init_s, self.genome_load_s, self.siblings_s = pre.hip_init_s, pre.genome_load_s, pre.siblings_s
+        self.prepack_s = pre.prepack_s
         self.load_s = pre.load_s
 
     def wait_ready(self):

@@ -69,7 +69,7 @@ class Prestart:
         self.ctxs = []                  # (fc2_ctx* int, device, primary) in CtxPipeline's order
         self.n_ctx = 0
         self.genome_index_s = self.hip_init_s = self.load_s = None
-        self.genome_load_s = self.siblings_s = 0.0
+        self.genome_load_s = self.siblings_s = self.prepack_s = 0.0
         self.fasta_ready = threading.Event()
         self.taken = False
         self.thread = threading.Thread(target=self._run, name="fc2-genome-prestart", daemon=True)
@@ -89,6 +89,7 @@ class Prestart:
         vp, P = ctypes.c_void_p, ctypes.POINTER
         for name, res, args in (("fc2_last_error", ctypes.c_char_p, []),
                                 ("fc2_fasta_open", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, P(vp)]),
+                                ("fc2_fasta_prepack", ctypes.c_int, [vp, ctypes.c_int]),
                                 ("fc2_device_count", ctypes.c_int, [P(ctypes.c_int)]),
                                 ("fc2_ctx_create", ctypes.c_int, [ctypes.c_int, P(vp)]),
                                 ("fc2_ctx_create_sibling", ctypes.c_int, [vp, P(vp)]),
@@ -116,7 +117,11 @@ class Prestart:
         self.fasta_ready.set()
         t0 = time.time()
         made = []
-        try:
+        first_ctx = {}
+
+        def first_context():
+            """HIP initialisation (the device count for --gpus N, the first context) on a thread of its
+            own while this one packs the FASTA's 2-bit planes (fc2_fasta_prepack)."""
             # cli._devices: --gpus N devices from --device on, wrapping round the devices present
             first = device_index(device)
             if gpus <= 1:
@@ -125,20 +130,43 @@ class Prestart:
                 n = ctypes.c_int(0)
                 rc = L.fc2_device_count(ctypes.byref(n))
                 if rc != FC2_OK:
-                    self.error = (rc, last(L.fc2_last_error()))
+                    first_ctx["error"] = (rc, last(L.fc2_last_error()))
                     return
                 devs = [(first + k) % max(1, n.value) for k in range(gpus)]
+            first_ctx["devs"] = devs
+            c = vp()
+            rc = L.fc2_ctx_create(devs[0], ctypes.byref(c))
+            if rc != FC2_OK:
+                first_ctx["error"] = (rc, last(L.fc2_last_error()))
+                return
+            first_ctx["ctx"] = c.value
+            first_ctx["hip_init_s"] = time.time() - t0
+
+        th = threading.Thread(target=first_context, name="fc2-hip-init", daemon=True)
+        th.start()
+        if self.fasta is not None:
+            tp = time.time()
+            L.fc2_fasta_prepack(self.fasta, 0)          # (a failure shows again in the genome load)
+            self.prepack_s = time.time() - tp
+        th.join()
+        try:
+            if "error" in first_ctx:
+                self.error = first_ctx["error"]
+                return
+            devs = first_ctx["devs"]
+            self.hip_init_s = first_ctx["hip_init_s"]
             self.n_ctx = len(devs) * PER_DEVICE
             primary = {}
             for dev in devs:                       # CtxPipeline._build, call for call
                 if dev not in primary:
                     c = vp()
-                    rc = L.fc2_ctx_create(dev, ctypes.byref(c))
-                    if rc != FC2_OK:
-                        self.error = (rc, last(L.fc2_last_error()))
-                        return
-                    if self.hip_init_s is None:
-                        self.hip_init_s = time.time() - t0
+                    if not made:
+                        c.value = first_ctx["ctx"]
+                    else:
+                        rc = L.fc2_ctx_create(dev, ctypes.byref(c))
+                        if rc != FC2_OK:
+                            self.error = (rc, last(L.fc2_last_error()))
+                            return
                     made.append((c.value, dev, True))
                     tg = time.time()
                     rc = L.fc2_ctx_genome_load(c, self.fasta, 0)

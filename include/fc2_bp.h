@@ -430,6 +430,10 @@ int  fc2_fasta_layout(const fc2_fasta *f, uint64_t *n_units, uint64_t *n_coarse_
  * pairs touching them take the byte path).  n_threads <= 0: all cores. */
 int  fc2_fasta_pack(const fc2_fasta *f, uint64_t *units, uint64_t *nplane, uint32_t *ncoarse,
                     uint64_t *n_exotic, int n_threads);
+/* fc2_fasta_pack into host memory f keeps until the next fc2_ctx_genome_load of f takes it over (that
+ * call then only uploads): a host may pack on one thread while another initialises HIP
+ * (fc2_ctx_create), as the CLI's start-up does.  Freed with f if no context takes it. */
+int  fc2_fasta_prepack(fc2_fasta *f, int n_threads);
 
 /* ======================================================================== */
 /* host side: pair packing                                                   */

@@ -154,3 +154,34 @@ def test_pack_row_damage_deep_inside_is_all_n(tmp_path, damage):
         for a, b in zip(got[:3], exp[:3]):
             assert np.array_equal(a, b)
         assert got[3] == exp[3]
+
+
+def test_prepack_then_pack_and_close(tmp_path):
+    """fc2_fasta_prepack (the CLI's start-up packs beside HIP init; fc2_ctx_genome_load takes the planes
+    over): the FASTA handle is packed as by fc2_fasta_pack (a later pack gives the same planes), a
+    second prepack replaces the first, and planes no context took are freed with the handle."""
+    rng = np.random.default_rng(23)
+    chroms = [(b"c%d" % i, _seq(rng, n), w) for i, (n, w) in enumerate(((70_000, 60), (5, 50), (3000, 61)))]
+    path = str(tmp_path / "g.fa")
+    _write(path, chroms)
+    exp = _expected([s for _, s, _ in chroms], [True] * 3)
+    L = N.lib()
+    for k in range(2):
+        h = ctypes.c_void_p()
+        N.check(L.fc2_fasta_open(path.encode(), 0, ctypes.byref(h)))
+        try:
+            N.check(L.fc2_fasta_prepack(h, 4))
+            if k:
+                N.check(L.fc2_fasta_prepack(h, 1))
+            nu, ncw = ctypes.c_uint64(), ctypes.c_uint64()
+            N.check(L.fc2_fasta_layout(h, ctypes.byref(nu), ctypes.byref(ncw), None))
+            units, nplane = np.zeros(2 * nu.value, np.uint64), np.zeros(nu.value, np.uint64)
+            ncoarse, exo = np.zeros(max(1, ncw.value), np.uint32), ctypes.c_uint64()
+            N.check(L.fc2_fasta_pack(h, units.ctypes.data, nplane.ctypes.data, ncoarse.ctypes.data,
+                                     ctypes.byref(exo), 2))
+            for a, b in zip((units, nplane, ncoarse[:ncw.value]), exp[:3]):
+                assert np.array_equal(a, b)
+            assert exo.value == exp[3]
+        finally:
+            L.fc2_fasta_close(h)
+    assert L.fc2_fasta_prepack(None, 0) == N.FC2_E_PARAM

@@ -22,15 +22,17 @@ from test_gpu_parity import OPTS, WEIRD, genome, oracle_spans, run_spans  # noqa
 
 
 class Ctx:
-    def __init__(self, path=None):
+    def __init__(self, path=None, prepack=False):
         if not torch.cuda.is_available():
             pytest.skip("no GPU")
         self.L = N.lib()
         self.c = ctypes.c_void_p()
-        N.check(self.L.fc2_ctx_create(0, ctypes.byref(self.c)))
         self.fa = ctypes.c_void_p()
         if path:
             N.check(self.L.fc2_fasta_open(path.encode(), 0, ctypes.byref(self.fa)))
+            if prepack:                 # the CLI's start-up: planes packed before (beside) HIP init
+                N.check(self.L.fc2_fasta_prepack(self.fa, 0))
+        N.check(self.L.fc2_ctx_create(0, ctypes.byref(self.c)))
         self.check(self.L.fc2_ctx_genome_load(self.c, self.fa if path else None, 0))
 
     def check(self, rc):
@@ -82,11 +84,12 @@ def _compare(opt, path, g, spans, ctx, label):
     return 0
 
 
+@pytest.mark.parametrize("prepack", [False, True], ids=["pack", "prepacked"])
 @pytest.mark.parametrize("fa", ["CDR1as_locus.fa", "test_ref.fa"])
-def test_ctx_equals_python_path_and_oracle(fa):
+def test_ctx_equals_python_path_and_oracle(fa, prepack):
     path = os.path.join(GOLDEN, fa)
     g = genome(path)
-    ctx = Ctx(path)
+    ctx = Ctx(path, prepack=prepack)
     try:
         gen = load_genome(path)
         for oi in (0, 1, 3, 5, 6, 8):
@@ -99,11 +102,12 @@ def test_ctx_equals_python_path_and_oracle(fa):
         ctx.close()
 
 
-def test_ctx_byte_path_and_long_reads(tmp_path):
+@pytest.mark.parametrize("prepack", [False, True], ids=["pack", "prepacked"])
+def test_ctx_byte_path_and_long_reads(tmp_path, prepack):
     path = str(tmp_path / "weird.fa")
     open(path, "wb").write(b"".join(WEIRD.replace(b">c", b">r%dc" % k) for k in range(3)))
     g = Genome.from_fasta(path, device="cuda:0")
-    ctx = Ctx(path)
+    ctx = Ctx(path, prepack=prepack)
     try:
         gen = load_genome(path)
         for o in (dict(asize=6, margin=1, maxdist=3), dict(asize=6, margin=2, maxdist=2, allhits=True, noncanonical=True)):
