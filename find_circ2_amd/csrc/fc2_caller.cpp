@@ -776,7 +776,8 @@ struct fc2_caller {
     // capacity, so forming a chunk allocates nothing in steady state, and nothing allocated on one
     // thread is freed on the other
     std::vector<Chunk> spare;
-    bool read_side_released = false;            // release_read_side ran (after the last chunk)
+    bool read_side_released = false;            // release_read_side ran (after the last chunk): the
+    fc2_ingest_counts ing_final{};              // input is closed then, its final counts kept here
     std::mutex qmu;                             // guards queued and spare
     // fc2_caller_stats' values, published by fc2_caller_next on the thread that advances the input
     // (a recording thread may ask for them while the reader runs)
@@ -2074,6 +2075,12 @@ extern "C" int fc2_caller_set_genome(fc2_caller *h, const int32_t *tid_to_chrom,
 
 extern "C" fc2_ingest *fc2_caller_ingest(fc2_caller *h) { return h ? h->ing : nullptr; }
 
+// the input's counts: live, or as they were when the input was released (release_read_side)
+static void ingest_counts(const fc2_caller *h, fc2_ingest_counts *c) {
+    if (h->read_side_released) *c = h->ing_final;
+    else fc2_ingest_counts_get(h->ing, c);
+}
+
 extern "C" void fc2_caller_close(fc2_caller *h) {
     if (!h) return;
     fc2_ingest_close(h->ing);                   // (joins the parse-ahead threads)
@@ -2130,7 +2137,7 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         fc2_caller *h;
         ~PublishStats() {
             fc2_ingest_counts c{};
-            fc2_ingest_counts_get(h->ing, &c);
+            ingest_counts(h, &c);
             h->st_reads.store(c.n_reads, std::memory_order_relaxed);
             h->st_pairs.store(h->n_pairs, std::memory_order_relaxed);
         }
@@ -2139,6 +2146,11 @@ extern "C" int fc2_caller_next(fc2_caller *h, fc2_caller_batch *b, int *eof) {
         std::lock_guard<std::mutex> lk(h->qmu);
         if (h->queued.size() >= FC2_CALLER_MAX_QUEUED)
             return fc2::fail(FC2_E_PARAM, "fc2_caller_next: too many chunks not submitted");
+    }
+    if (h->read_side_released) {                   // the input was read to its end and closed
+        memset((void *)b, 0, sizeof(*b));
+        if (eof) *eof = 1;
+        return FC2_OK;
     }
     {
         std::lock_guard<std::mutex> lk(h->qmu);
@@ -2595,17 +2607,17 @@ extern "C" int fc2_caller_close_reads(fc2_caller *h) {
     return FC2_OK;
 }
 
-// Once the input is read and every chunk recorded, the read side's buffers -- the recycled chunks,
-// the fragments, spans and read parts of both sides, ~1 GB at 2M reads when the loop read ahead while
-// the genome loaded -- are only memory: they are destroyed on a thread of their own while the rows are
-// formatted, and the freed heap is handed back (malloc_trim), so neither the rows nor the process's
-// exit pay for their pages.  Nothing reads them again (fc2_caller_next reports the end from `eof`).
+// Once the input is read and every chunk recorded, the read side -- the recycled chunks, the
+// fragments, spans and read parts of both sides, and the input itself with its parse blocks -- is
+// only memory: it is destroyed on a thread of their own while the rows are formatted, and the freed
+// heap is handed back (malloc_trim), so neither the rows nor the process's exit pay for its pages.
 static void release_read_side(fc2_caller *h) {
     if (h->read_side_released || !h->eof || h->next_err) return;
     {
         std::lock_guard<std::mutex> g(h->qmu);
         if (!h->queued.empty()) return;
     }
+    fc2_ingest_counts_get(h->ing, &h->ing_final);
     h->read_side_released = true;
     struct Bag {
         std::vector<fc2_caller::Chunk> spare;
@@ -2623,12 +2635,18 @@ static void release_read_side(fc2_caller *h) {
     b->recf.swap(h->bf_recf);
     b->segs.swap(h->bf_segs);
     h->bf_nfrags = h->nfrags = 0;
+    // the input too: its parse blocks and records (~0.75 GB at 2M reads) -- fc2_caller_ingest returns
+    // NULL from here on, fc2_caller_next reports the end, the counters come from ing_final
+    fc2_ingest *ing = h->ing;
+    h->ing = nullptr;
     try {
-        std::thread([bag = std::move(b)]() mutable {
+        std::thread([bag = std::move(b), ing]() mutable {
+            fc2_ingest_close(ing);
             bag.reset();
             malloc_trim(0);
         }).detach();
-    } catch (const std::system_error &) {       // no thread: freed at close instead
+    } catch (const std::system_error &) {       // no thread: here, then
+        fc2_ingest_close(ing);
     }
 }
 
@@ -2669,7 +2687,7 @@ extern "C" int fc2_caller_counter(fc2_caller *h, int i, const char **name, doubl
         for (const auto &kv : h->N) m[kv.first] += kv.second;
         for (const auto &kv : h->N_in) m[kv.first] += kv.second;
         fc2_ingest_counts c{};
-        fc2_ingest_counts_get(h->ing, &c);
+        ingest_counts(h, &c);
         const std::pair<const char *, uint64_t> ing[4] = {{"total_mates", c.total_mates},
                                                            {"unmapped_reads", c.unmapped_reads},
                                                            {"unspliced_mates", c.unspliced_mates},

@@ -68,7 +68,7 @@ typedef struct fc2_caller_batch {
 int  fc2_caller_open(const char *path, int is_bam, const fc2_caller_opts *opts, fc2_caller **out);
 int  fc2_caller_set_genome(fc2_caller *h, const int32_t *tid_to_chrom, int32_t n_tid, const fc2_fasta *fasta,
                            uint64_t *n_known_circ, uint64_t *n_known_lin);
-fc2_ingest *fc2_caller_ingest(fc2_caller *h);    /* reference names, header */
+fc2_ingest *fc2_caller_ingest(fc2_caller *h);    /* reference names, header (NULL after the rows, below) */
 void fc2_caller_close(fc2_caller *h);
 
 /* Read on until `chunksize` fragments carry pairs (or the input ends); *b = the pairs
@@ -114,7 +114,10 @@ int fc2_caller_set_reads_gz(fc2_caller *h, const char *path, int level, int thre
  * fc2_caller_close); FC2_E_IO if a write failed. */
 int fc2_caller_close_reads(fc2_caller *h);
 /* The BED rows (no header) of 0 = circ_splice_sites.bed, 1 = lin_splice_sites.bed
- * (call once, at the end). */
+ * (call once, at the end).  Once the input was read to its end and every chunk submitted, the first
+ * call releases the read side -- the input (so finish -B output with fc2_ingest_close_bam_out
+ * before), its parse blocks, the chunk buffers -- on a thread of its own: fc2_caller_ingest returns
+ * NULL from then on, fc2_caller_next reports the end, the counters keep their final values. */
 int fc2_caller_rows(fc2_caller *h, int kind, const char **text, uint64_t *len);
 /* The reference's N[...] counters in sorted key order: i-th name and value;
  * FC2_E_RANGE past the end. */

@@ -692,3 +692,47 @@ def test_submit_compact_checks_word_count(tmp_path):
         assert L.fc2_caller_submit_compact(nc.h, words.ctypes.data, 4, n, None, 0, None, 0, n) == N.FC2_OK
     finally:
         nc.close()
+
+
+def test_rows_release_the_read_side(tmp_path):
+    """fc2_caller_rows, once the input is read and every chunk recorded, hands the read side (the
+    input, its parse blocks, the chunk buffers) to a thread that frees it: fc2_caller_ingest is NULL
+    after, fc2_caller_next keeps reporting the end, and the counters and the second table's rows are
+    those of a run without the release (the Python loop's)."""
+    import ctypes
+    from find_circ2_amd import _native as N
+    from find_circ2_amd.native_caller import NativeCaller
+    from oracle_engine import oracle_batch_engine
+    from find_circ2_amd.hotpath import Options as HPOptions
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 300, seed=17)
+    options, _ = cli.build_parser().parse_args(["-G", fa, "-o", str(tmp_path / "o"), sam])
+    hp = HPOptions(asize=options.asize, margin=options.margin, maxdist=options.maxdist)
+    ev, names, fasta, dummy = oracle_batch_engine(options, hp)
+    nc = NativeCaller(sam, False, options, names, fasta, genome_dummy=dummy, write_reads=False)
+    L = N.lib()
+    try:
+        nc.open()
+        nc.run(ev, {}, threads=True)
+        before = nc.counters()
+        assert L.fc2_caller_ingest(nc.h)
+        circ = nc.rows_bytes(0)
+        assert not L.fc2_caller_ingest(nc.h)
+        lin = nc.rows_bytes(1)
+        assert nc.counters() == before
+        b, eof = N.CallerBatch(), ctypes.c_int(0)
+        assert L.fc2_caller_next(nc.h, ctypes.byref(b), ctypes.byref(eof)) == N.FC2_OK
+        assert eof.value == 1 and b.n == 0 and b.n_long == 0
+        assert circ.count(b"\n") > 5 and lin.count(b"\n") > 5
+    finally:
+        nc.close()
+    # the same tables from the Python loop
+    o1, o2 = str(tmp_path / "py"), str(tmp_path / "nat")
+    from oracle_engine import oracle_evaluator_factory
+    assert cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    assert cli.main(["-G", fa, "-o", o2, "-q", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    for f in ("circ_splice_sites.bed", "lin_splice_sites.bed"):
+        rows = lambda o: [l for l in open(os.path.join(o, f), "rb") if not l.startswith(b"#")]   # noqa: E731
+        assert sorted(rows(o1)) == sorted(rows(o2))
+    nat = [l for l in open(os.path.join(o2, "circ_splice_sites.bed"), "rb") if not l.startswith(b"#")]
+    assert sorted(circ.splitlines(True)) == sorted(nat)
