@@ -1171,7 +1171,8 @@ def cli_end_to_end(reads=2_000_000):
         vals = [r[1]["value"] for r in runs]
         k_med = sorted(range(len(runs)), key=lambda k: (vals[k] is None, vals[k] or 0))[len(runs) // 2]
         o_bam, res = runs[k_med]
-        res = dict(res, runs=vals)
+        walls = [r[1]["process_wall_s"] for r in runs]
+        res = dict(res, runs=vals, process_wall_runs=walls, process_wall_median_s=sorted(walls)[len(walls) // 2])
         o_sam, res_sam = run("sam_path", False)
         res["reads"] = reads
         res["bam_bytes"] = os.path.getsize(bam)
@@ -1179,7 +1180,7 @@ def cli_end_to_end(reads=2_000_000):
         res["sam_by_path"] = res_sam
         res["note"] = ("whole CLI, BGZF BAM piped on stdin (cat reads.bam | python -m find_circ2_amd.cli -G genome.fa "
                        "-o out), hg19-shaped genome, .byo_index present: value = the read loop's reads/s from "
-                       "run.log, the median of `runs`; process_wall_s includes interpreter start, genome load and upload "
+                       "run.log, the median of `runs` (process_wall_runs: every run's wall); process_wall_s includes interpreter start, genome load and upload "
                        "(reads_per_process_wall_s = reads / process_wall_s; phases_s = run.log's process phases: "
                        "before_main_s interpreter + imports, genome_index_s, device_genome_s HIP init + 2-bit pack + "
                        "upload + tables -- built on a thread while the loop starts reading, genome_wait_s the "
