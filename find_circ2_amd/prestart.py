@@ -145,8 +145,11 @@ class Prestart:
         th = threading.Thread(target=first_context, name="fc2-hip-init", daemon=True)
         th.start()
         if self.fasta is not None:
+            # two cores fewer than the pack would take (fc2_host.cpp n_workers): HIP's initialisation
+            # and the interpreter's imports run meanwhile, and they are the longer path
+            cores = int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count() or 1
             tp = time.time()
-            L.fc2_fasta_prepack(self.fasta, 0)          # (a failure shows again in the genome load)
+            L.fc2_fasta_prepack(self.fasta, max(1, min(cores, 64) - 2))   # (a failure shows again below)
             self.prepack_s = time.time() - tp
         th.join()
         try:
