@@ -111,6 +111,11 @@ def main():
     ap.add_argument("--out", default="/tmp/fc2_scale")
     ap.add_argument("--only", default="", help="comma list of run tags (timing only; the identity check needs all)")
     a = ap.parse_args()
+    # the runs share this process: the torch-based ones (--python-caller / --python-ingest, the Python
+    # loop's Genome) and the default CLI's torch-free contexts must use one HIP runtime, so torch's is
+    # brought up first (its libamdhip64 then serves libfc2.so too, as in the GPU tests)
+    import torch
+    torch.cuda.init()
     from find_circ2_amd import cli, sq_table
     rng = np.random.default_rng(2024)
     names, sizes = sq_table(os.path.join(ROOT, "tests", "golden", "test_norm.sam"))
