@@ -18,3 +18,16 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def golden():
     return GOLDEN
+
+
+@pytest.fixture(autouse=True)
+def _torch_hip_runtime_first(request):
+    """One HIP runtime per process: before a GPU test can reach the C ABI, torch's
+    runtime is brought up, so that the torch-based tests after a torch-free one still see the device."""
+    if request.node.get_closest_marker("gpu") is not None:
+        try:
+            import torch
+            torch.cuda.is_available()
+        except Exception:
+            pass
+    yield
