@@ -2612,6 +2612,9 @@ extern "C" int fc2_caller_close_reads(fc2_caller *h) {
 // only memory: it is destroyed on a thread of their own while the rows are formatted, and the freed
 // heap is handed back (malloc_trim), so neither the rows nor the process's exit pay for its pages.
 static void release_read_side(fc2_caller *h) {
+#ifdef FC2_AB_NO_RELEASE                        // A/B build only (scripts/prof/ab_cli.py): keep it all
+    return;
+#endif
     if (h->read_side_released || !h->eof || h->next_err) return;
     {
         std::lock_guard<std::mutex> g(h->qmu);
