@@ -1105,6 +1105,19 @@ def _cli_outputs(out):
     return files
 
 
+def _wait_blocking(proc, timeout):
+    """proc's exit status, waited for in one blocking waitpid (a watchdog kills it after `timeout` s):
+    subprocess's wait(timeout) polls with sleeps of up to 50 ms, which would add that much to a
+    sub-second process wall."""
+    import threading
+    dog = threading.Timer(timeout, proc.kill)
+    dog.start()
+    try:
+        return proc.wait()
+    finally:
+        dog.cancel()
+
+
 def cli_end_to_end(reads=2_000_000):
     """The product end to end (an extra, never `value`), in north_star's form ``samtools view -b ... |
     find_circ -G genome.fa -o out``: scripts/cli_scale_check.py's generator writes an hg19-shaped genome
@@ -1140,12 +1153,13 @@ def cli_end_to_end(reads=2_000_000):
             t0 = time.time()
             if stdin_bam:                      # a real pipe, as from samtools / an aligner
                 feeder = subprocess.Popen(["cat", bam], stdout=subprocess.PIPE)
-                rc = subprocess.run(cmd, cwd=ROOT, stdin=feeder.stdout, timeout=600).returncode
+                rc = _wait_blocking(subprocess.Popen(cmd, cwd=ROOT, stdin=feeder.stdout), 600)
+                wall = time.time() - t0
                 feeder.stdout.close()
                 feeder.wait()
             else:
-                rc = subprocess.run(cmd + [sam], cwd=ROOT, timeout=600).returncode
-            wall = time.time() - t0
+                rc = _wait_blocking(subprocess.Popen(cmd + [sam], cwd=ROOT), 600)
+                wall = time.time() - t0
             if rc != 0:
                 raise RuntimeError("cli exit status %d (%s)" % (rc, tag))
             log = open(os.path.join(out, "run.log")).read()
