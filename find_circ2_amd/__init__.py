@@ -19,11 +19,24 @@ if _sys.argv[:1] == ["-m"] and "-m" in _orig and _orig[_orig.index("-m") + 1:][:
     from . import prestart as _prestart
     _prestart.start(_sys.argv[1:])
 
-from . import _native  # noqa: E402
-from .genome import Genome, sq_table, synthetic_n_intervals  # noqa: E402
-from .hotpath import (BreakpointEngine, BreakpointError, CompactResults, JunctionSpan, Options,  # noqa: E402
-                      PairBatch, ScanOutput, Splice, SynthConfig, compact, decode_splices, expand,
-                      first_tie_arrays, gtag_str, reorder, scan, splices_or_raise)
+# the package's names are imported on first use (PEP 562): `python -m find_circ2_amd.cli` then loads
+# only what the CLI needs -- neither numpy nor torch for the default loop
+_EXPORTS = {"Genome": "genome", "sq_table": "genome", "synthetic_n_intervals": "genome",
+            **{k: "hotpath" for k in ("BreakpointEngine", "BreakpointError", "CompactResults", "JunctionSpan",
+                                      "Options", "PairBatch", "ScanOutput", "Splice", "SynthConfig", "compact",
+                                      "decode_splices", "expand", "first_tie_arrays", "gtag_str", "reorder", "scan",
+                                      "splices_or_raise")}}
+
+
+def __getattr__(name):
+    mod = _EXPORTS.get(name)
+    if mod is None:
+        raise AttributeError("module 'find_circ2_amd' has no attribute %r" % (name,))
+    import importlib
+    value = getattr(importlib.import_module("." + mod, __name__), name)
+    globals()[name] = value
+    return value
+
 
 __version__ = "0.1.0"
 

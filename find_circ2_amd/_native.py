@@ -10,9 +10,10 @@ import ctypes
 import os
 import subprocess
 
-import numpy as np
-
+from ._lazy import LazyModule
 from ._libpath import LIB_PATH, _HERE
+
+np = LazyModule("numpy", globals(), "np")
 
 FC2_OK = 0
 FC2_E_PARAM = -1
@@ -40,17 +41,32 @@ RES_ERR_KEY = 0x2000
 RES_ERR_WIN = 0x4000
 RES_DONE = 0x8000
 
-PAIR_DTYPE = np.dtype([("a_pos", "<i4"), ("b_aend", "<i4"), ("chrom", "<u4"), ("read_len", "<u2"),
-                       ("flags", "u1"), ("npos", "u1")])
-RESULT_DTYPE = np.dtype([("best_x", "<i2"), ("dist", "u1"), ("ov", "u1"), ("n_ties", "<u2"), ("info", "<u2")])
-assert PAIR_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 8
-ESCAPE_DTYPE = np.dtype([("index", "<u8"), ("result", RESULT_DTYPE)])     # fc2_result_escape
-# pairs with read parts over MAX_READ_LEN and their results (fc2_long_pair / fc2_long_result)
-LONG_PAIR_DTYPE = np.dtype([("read_off", "<u8"), ("read_len", "<u4"), ("chrom", "<u4"), ("a_pos", "<i4"),
-                            ("b_aend", "<i4"), ("flags", "u1"), ("_pad", "u1", (7,))])
-LONG_RESULT_DTYPE = np.dtype([("best_x", "<i4"), ("n_ties", "<u4"), ("dist", "u1"), ("ov", "u1"), ("info", "<u2"),
-                              ("_pad", "<u4")])
-assert LONG_PAIR_DTYPE.itemsize == 32 and LONG_RESULT_DTYPE.itemsize == 16
+_DTYPE_NAMES = ("PAIR_DTYPE", "RESULT_DTYPE", "ESCAPE_DTYPE", "LONG_PAIR_DTYPE", "LONG_RESULT_DTYPE")
+
+
+def _dtypes():
+    """The numpy record types of the C structs, made (and numpy imported) on first use."""
+    PAIR_DTYPE = np.dtype([("a_pos", "<i4"), ("b_aend", "<i4"), ("chrom", "<u4"), ("read_len", "<u2"),
+                           ("flags", "u1"), ("npos", "u1")])
+    RESULT_DTYPE = np.dtype([("best_x", "<i2"), ("dist", "u1"), ("ov", "u1"), ("n_ties", "<u2"), ("info", "<u2")])
+    assert PAIR_DTYPE.itemsize == 16 and RESULT_DTYPE.itemsize == 8
+    ESCAPE_DTYPE = np.dtype([("index", "<u8"), ("result", RESULT_DTYPE)])     # fc2_result_escape
+    # pairs with read parts over MAX_READ_LEN and their results (fc2_long_pair / fc2_long_result)
+    LONG_PAIR_DTYPE = np.dtype([("read_off", "<u8"), ("read_len", "<u4"), ("chrom", "<u4"), ("a_pos", "<i4"),
+                                ("b_aend", "<i4"), ("flags", "u1"), ("_pad", "u1", (7,))])
+    LONG_RESULT_DTYPE = np.dtype([("best_x", "<i4"), ("n_ties", "<u4"), ("dist", "u1"), ("ov", "u1"), ("info", "<u2"),
+                                  ("_pad", "<u4")])
+    assert LONG_PAIR_DTYPE.itemsize == 32 and LONG_RESULT_DTYPE.itemsize == 16
+    g = globals()
+    for k in _DTYPE_NAMES:
+        g[k] = locals()[k]
+
+
+def __getattr__(name):
+    if name in _DTYPE_NAMES:
+        _dtypes()
+        return globals()[name]
+    raise AttributeError("module %r has no attribute %r" % (__name__, name))
 R32_ESCAPE = 0x80000000
 R16_ESCAPE = 0x007F
 

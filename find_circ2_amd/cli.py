@@ -347,7 +347,8 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
                            siblings_s=getattr(evaluate, "siblings_s", 0.0), read_loop_s=seconds,
                            genome_wait_s=getattr(evaluate, "wait_s", 0.0), tables_s=time.time() - t_rows)
             logger.info("process phases: " + ", ".join("%s=%.3f" % kv for kv in startup.items()) +
-                        ", process_age_s=%.3f" % process_age())
+                        ", process_age_s=%.3f, numpy_loaded=%d, torch_loaded=%d"
+                        % (process_age(), "numpy" in sys.modules, "torch" in sys.modules))
     finally:
         t_close = time.time()
         try:

@@ -21,7 +21,9 @@ import ctypes
 import threading
 from typing import List, Optional, Sequence
 
-import numpy as np
+from ._lazy import LazyModule
+
+np = LazyModule("numpy", globals(), "np")
 
 from . import _native as N
 
@@ -113,11 +115,12 @@ class _Ctx:
 
 
 class CtxTicket:
-    __slots__ = ("ctx", "n", "res", "tm", "tw", "done", "deferred")
+    __slots__ = ("ctx", "n", "res", "tm", "tw", "done", "deferred", "keep")
 
     def __init__(self, ctx, n, res, tm, tw=0):
         self.ctx, self.n, self.res, self.tm, self.tw, self.done = ctx, n, res, tm, tw, False
-        self.deferred = None           # (reads_ptr, read_off, pairs) while the genome is being built
+        self.deferred = None           # (reads_ptr, off_ptr, pairs_ptr) while the genome is being built
+        self.keep = None               # submit(): the arrays those pointers point into
 
 
 class CtxPipeline:
@@ -261,8 +264,9 @@ class CtxPipeline:
         device work is queued.  reads_ptr / read_off / pairs: the chunk as fc2_caller_next hands it out
         (its memory stays valid while the chunk is queued).  While the genome is still being built the
         chunk is only noted, and dispatched in order once it is ready."""
+        pairs = np.ascontiguousarray(pairs, N.PAIR_DTYPE)
+        off = np.ascontiguousarray(read_off, np.uint64)
         n = len(pairs)
-        res = np.empty(n, np.int64)
         tm, tw = None, 0
         if n and self.options.allhits:
             rw, nw, tw_ = ctypes.c_uint32(), ctypes.c_uint32(), ctypes.c_uint32()
@@ -270,28 +274,53 @@ class CtxPipeline:
                                                ctypes.byref(rw), ctypes.byref(nw), ctypes.byref(tw_)))
             tw = tw_.value
             tm = np.empty((tw, n), np.uint64)
-        t = CtxTicket(None, n, res, tm, tw)
-        pairs = np.ascontiguousarray(pairs, N.PAIR_DTYPE)
-        off = np.ascontiguousarray(read_off, np.uint64)
+        t = CtxTicket(None, n, np.empty(n, np.int64), tm, tw)
+        if self._ready is not None and self._ready.is_alive():
+            off, pairs = off.copy(), pairs.copy()      # noted for later: the caller may reuse its arrays
+        t.keep = (off, pairs)
+        self._queue(t, reads_ptr, off.ctypes.data, pairs.ctypes.data)
+        return t
+
+    def submit_ptr(self, reads_ptr: int, off_ptr: int, pairs_ptr: int, n: int) -> CtxTicket:
+        """submit() of a chunk given as fc2_caller_batch's pointers (the native read loop): the results
+        land in a ctypes buffer and nothing here needs numpy -- the default CLI never imports it.  The
+        chunk's memory stays valid until its fc2_caller_submit, which follows result(), so a chunk
+        noted while the genome is built is not copied.  --all-hits (the tie mask's geometry needs the
+        longest read part) goes through submit()."""
+        if n and self.options.allhits:
+            pairs = np.ctypeslib.as_array(ctypes.cast(pairs_ptr, ctypes.POINTER(ctypes.c_uint8)),
+                                          (16 * n,)).view(N.PAIR_DTYPE)
+            off = np.ctypeslib.as_array(ctypes.cast(off_ptr, ctypes.POINTER(ctypes.c_uint64)), (n,))
+            return self.submit(reads_ptr, off, pairs)
+        t = CtxTicket(None, n, (ctypes.c_int64 * max(1, n))(), None, 0)
+        self._queue(t, reads_ptr, off_ptr, pairs_ptr)
+        return t
+
+    def _queue(self, t: CtxTicket, reads_ptr, off_ptr, pairs_ptr):
         with self._slock:
             if self._ready is not None and self._ready.is_alive():
-                t.deferred = (reads_ptr, off.copy(), pairs.copy())
+                t.deferred = (reads_ptr, off_ptr, pairs_ptr)
                 self._deferred.append(t)
-                return t
+                return
             self.wait_ready()
             self._flush()
-            self._dispatch(t, reads_ptr, off, pairs)
-        return t
+            self._dispatch(t, reads_ptr, off_ptr, pairs_ptr)
 
     def _flush(self):
         """Dispatch the chunks noted while the genome was being built (caller holds _slock)."""
         while self._deferred:
             t = self._deferred.pop(0)
-            reads_ptr, off, pairs = t.deferred
+            reads_ptr, off_ptr, pairs_ptr = t.deferred
             t.deferred = None
-            self._dispatch(t, reads_ptr, off, pairs)
+            self._dispatch(t, reads_ptr, off_ptr, pairs_ptr)
 
-    def _dispatch(self, t: CtxTicket, reads_ptr, off, pairs):
+    @staticmethod
+    def _addr(a):
+        if a is None:
+            return None
+        return ctypes.addressof(a) if isinstance(a, ctypes.Array) else a.ctypes.data
+
+    def _dispatch(self, t: CtxTicket, reads_ptr, off_ptr, pairs_ptr):
         c = self.ctxs[self.k % len(self.ctxs)]
         self.k += 1
         t.ctx = c
@@ -300,10 +329,8 @@ class CtxPipeline:
             if t.n == 0:
                 t.done = True
                 return
-            c.check(N.lib().fc2_ctx_scan_async(c.h, ctypes.byref(self.params), t.n, reads_ptr, off.ctypes.data,
-                                               pairs.ctypes.data, t.res.ctypes.data,
-                                               t.tm.ctypes.data if t.tm is not None else None, t.tw,
-                                               self.n_threads))
+            c.check(N.lib().fc2_ctx_scan_async(c.h, ctypes.byref(self.params), t.n, reads_ptr, off_ptr, pairs_ptr,
+                                               self._addr(t.res), self._addr(t.tm), t.tw, self.n_threads))
             c.pending = t
 
     def result(self, t: CtxTicket, copy: bool = True):

@@ -20,7 +20,9 @@ from __future__ import annotations
 import ctypes
 from typing import List, Optional, Sequence
 
-import numpy as np
+from ._lazy import LazyModule
+
+np = LazyModule("numpy", globals(), "np")
 
 from . import _native as N
 

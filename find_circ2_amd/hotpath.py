@@ -20,7 +20,9 @@ import ctypes
 from dataclasses import dataclass, field
 from typing import Iterable, List, Optional, Sequence, Tuple
 
-import numpy as np
+from ._lazy import LazyModule
+
+np = LazyModule("numpy", globals(), "np")
 
 from . import _native as N
 from .genome import Genome, _require_gpu, _torch

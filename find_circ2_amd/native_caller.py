@@ -22,7 +22,9 @@ import threading
 from collections import deque
 from typing import Callable, Dict, NamedTuple, Optional
 
-import numpy as np
+from ._lazy import LazyModule
+
+np = LazyModule("numpy", globals(), "np")
 
 from . import _native as N
 from .hotpath import BreakpointError
@@ -112,12 +114,13 @@ class NativeCaller:
         self.refs = [L.fc2_ingest_ref_name(ing, t).decode("latin-1") for t in range(n_ref)]
         index = {nm: k for k, nm in enumerate(self.genome_names)}
         if self.genome_dummy:             # every window is all 'N'; no chromosome is missing
-            t2c = np.zeros(max(1, n_ref), np.int32)
+            vals = [0] * max(1, n_ref)
         else:
-            t2c = np.array([index.get(nm, -1) for nm in self.refs] or [-1], np.int32)
+            vals = [index.get(nm, -1) for nm in self.refs] or [-1]
+        t2c = (ctypes.c_int32 * len(vals))(*vals)
         self._t2c = t2c
         nkc, nkl = ctypes.c_uint64(), ctypes.c_uint64()
-        _check(L.fc2_caller_set_genome(self.h, t2c.ctypes.data, n_ref, self.fasta_handle, ctypes.byref(nkc),
+        _check(L.fc2_caller_set_genome(self.h, ctypes.addressof(t2c), n_ref, self.fasta_handle, ctypes.byref(nkc),
                                        ctypes.byref(nkl)))
         return int(nkc.value), int(nkl.value)
 
@@ -170,6 +173,7 @@ class NativeCaller:
         L = N.lib()
         t0 = time.time()
         pipelined = hasattr(evaluate, "submit") and hasattr(evaluate, "result")
+        pointers = pipelined and hasattr(evaluate, "submit_ptr")
         depth = max(2, int(getattr(evaluate, "depth", 2)))
         q: "queue.Queue" = queue.Queue()
         # at most `depth` chunks between being handed out and being recorded: a ScanPipeline slot is
@@ -199,6 +203,8 @@ class NativeCaller:
                     te = time.perf_counter()
                     if not n:
                         item = None
+                    elif pointers:          # (ctxpipe: the chunk's own memory, no numpy in the process)
+                        item = evaluate.submit_ptr(batch.reads, batch.read_off, batch.pairs, n)
                     elif pipelined:
                         pairs = np.ctypeslib.as_array(ctypes.cast(batch.pairs, ctypes.POINTER(ctypes.c_uint8)),
                                                       (16 * n,)).view(N.PAIR_DTYPE)
@@ -305,6 +311,8 @@ class NativeCaller:
                 te = time.perf_counter()
                 if not n:
                     item = (None, None)
+                elif pipelined and hasattr(evaluate, "submit_ptr"):
+                    item = evaluate.submit_ptr(batch.reads, batch.read_off, batch.pairs, n)
                 elif pipelined:
                     pairs = np.ctypeslib.as_array(ctypes.cast(batch.pairs, ctypes.POINTER(ctypes.c_uint8)),
                                                   (16 * n,)).view(N.PAIR_DTYPE)
@@ -382,6 +390,8 @@ class NativeCaller:
         """fc2_caller_submit of one chunk's results: raw 8-byte words, or a CompactChunk (a compact
         transfer form, fc2_caller_submit_compact); tm = the --all-hits tie mask [tw, n] or None."""
         tm_ptr, tw = None, 0
+        if isinstance(res, ctypes.Array):           # ctxpipe.submit_ptr: words in a ctypes buffer
+            return L.fc2_caller_submit(self.h, ctypes.addressof(res) if n else None, None, 0, n)
         if tm is not None:
             tm = np.ascontiguousarray(tm, dtype=np.uint64)
             tw = tm.shape[0]

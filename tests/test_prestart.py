@@ -147,4 +147,6 @@ def test_gpu_m_cli_equals_oracle_cli(tmp_path, extra, folder):
     _compare(o1, str(tmp_path / "m"))
     log = open(str(tmp_path / "m" / "run.log")).read()
     assert ("Switching to dummy mode" in log) == folder
-    assert "process phases" in log
+    assert "process phases" in log and "torch_loaded=0" in log
+    if not extra:                               # the default loop never imports numpy (_lazy.py)
+        assert "numpy_loaded=0" in log
