@@ -29,11 +29,14 @@ _EXPORTS = {"Genome": "genome", "sq_table": "genome", "synthetic_n_intervals": "
 
 
 def __getattr__(name):
-    mod = _EXPORTS.get(name)
-    if mod is None:
-        raise AttributeError("module 'find_circ2_amd' has no attribute %r" % (name,))
     import importlib
-    value = getattr(importlib.import_module("." + mod, __name__), name)
+    mod = _EXPORTS.get(name)
+    if mod is not None:
+        value = getattr(importlib.import_module("." + mod, __name__), name)
+    elif not name.startswith("__") and _os.path.exists(_os.path.join(_os.path.dirname(__file__), name + ".py")):
+        value = importlib.import_module("." + name, __name__)     # find_circ2_amd.<submodule>
+    else:
+        raise AttributeError("module 'find_circ2_amd' has no attribute %r" % (name,))
     globals()[name] = value
     return value
 

@@ -150,3 +150,19 @@ def test_gpu_m_cli_equals_oracle_cli(tmp_path, extra, folder):
     assert "process phases" in log and "torch_loaded=0" in log
     if not extra:                               # the default loop never imports numpy (_lazy.py)
         assert "numpy_loaded=0" in log
+
+
+def test_package_names_and_submodules_resolve_lazily():
+    """find_circ2_amd imports its names on first use (PEP 562): every exported name and every submodule
+    reached as an attribute (``find_circ2_amd._native``, as __graft_entry__.build does) resolves, in a
+    fresh interpreter where nothing was imported before; an unknown name raises AttributeError."""
+    code = ("import find_circ2_amd as f, sys\n"
+            "assert 'numpy' not in sys.modules\n"
+            "assert f._native.FC2_OK == 0 and f.hotpath.Options is f.Options and f.ctxpipe.CtxPipeline\n"
+            "for n in f.__all__: getattr(f, n)\n"
+            "try:\n    f.no_such_name\nexcept AttributeError:\n    pass\nelse:\n    raise SystemExit(1)\n"
+            "import __graft_entry__ as g\n"
+            "print('ok')\n")
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                       timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == b"ok", r.stderr.decode()[-2000:]
