@@ -381,8 +381,8 @@ def host_read_arrays(opt, b, chunk: int = 4_000_000):
 
 
 def host_pipeline(opt, g, b, chunk: int = 4_000_000, reps: int = 3):
-    """The product transfer path (find_circ2_amd.pipeline.ScanPipeline, what the CLI's read loop
-    drives) from host pair arrays: per chunk the C++ packer writes records + read rows into
+    """The product transfer path (find_circ2_amd.pipeline.ScanPipeline -- the Python loop's evaluator;
+    the default CLI runs the same sequence inside libfc2.so, fc2_ctx_scan_async) from host pair arrays: per chunk the C++ packer writes records + read rows into
     page-locked staging, then async H2D, scan and D2H of the 8-B results on the scanner's side
     stream, two chunks in flight.  Timed from the host arrays to every raw result word in host
     memory in input order (what fc2_caller_submit consumes); must equal the device-resident scan."""
@@ -417,7 +417,7 @@ def host_pipeline(opt, g, b, chunk: int = 4_000_000, reps: int = 3):
             "pack_threads": int(_os.environ.get("OMP_NUM_THREADS", "0") or 0) or "all cores (<= 64)",
             "note": "host pair arrays (read_part bytes + 16-B records, as fc2_caller_next hands them out) -> "
                     "C++ pack into pinned staging -> H2D -> scan -> D2H raw results, chunks of %d pairs, two per "
-                    "side stream in flight (find_circ2_amd.pipeline, the CLI's evaluator); median of %d passes "
+                    "side stream in flight (find_circ2_amd.pipeline; the CLI's fc2_ctx_scan_async does the same); median of %d passes "
                     "over %d pairs" % (chunk, reps, n)}
 
 
