@@ -778,6 +778,7 @@ struct fc2_caller {
     std::vector<Chunk> spare;
     bool read_side_released = false;            // release_read_side ran (after the last chunk): the
     fc2_ingest_counts ing_final{};              // input is closed then, its final counts kept here
+    std::thread release_thr;                    // ... on this thread (joined by fc2_caller_close)
     std::mutex qmu;                             // guards queued and spare
     // fc2_caller_stats' values, published by fc2_caller_next on the thread that advances the input
     // (a recording thread may ask for them while the reader runs)
@@ -2083,6 +2084,7 @@ static void ingest_counts(const fc2_caller *h, fc2_ingest_counts *c) {
 
 extern "C" void fc2_caller_close(fc2_caller *h) {
     if (!h) return;
+    if (h->release_thr.joinable()) h->release_thr.join();   // the read side's release (fc2_caller_rows)
     fc2_ingest_close(h->ing);                   // (joins the parse-ahead threads)
     delete h;
     if (fc2::cpu::enabled()) {                  // CPU seconds per stage over the run (fc2_cpuacct.h)
@@ -2643,11 +2645,11 @@ static void release_read_side(fc2_caller *h) {
     fc2_ingest *ing = h->ing;
     h->ing = nullptr;
     try {
-        std::thread([bag = std::move(b), ing]() mutable {
+        h->release_thr = std::thread([bag = std::move(b), ing]() mutable {
             fc2_ingest_close(ing);
             bag.reset();
             malloc_trim(0);
-        }).detach();
+        });
     } catch (const std::system_error &) {       // no thread: here, then
         fc2_ingest_close(ing);
     }
