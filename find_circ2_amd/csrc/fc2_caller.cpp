@@ -18,6 +18,7 @@
 #include <map>
 #include <memory>
 #include <malloc.h>
+#include <sys/mman.h>
 #include <mutex>
 #include <set>
 #include <stdexcept>
@@ -302,12 +303,35 @@ struct CKeyHash {
 
 // Memory for the large per-run tables, cache-line aligned.  (Marking it for transparent huge pages
 // cut the recording side's TLB misses but stalled the other thread's allocations behind the
-// compaction it triggered: slower overall on the GPU box, so not done.)
+// compaction it triggered: slower overall on the GPU box, so not done -- FC2_AB_TABLE_THP builds
+// the form again for a same-box A/B.)
+#ifdef FC2_AB_TABLE_THP
+constexpr size_t kHugeTable = size_t(2) << 20;
+inline size_t table_bytes(size_t bytes) { return (bytes + kHugeTable - 1) & ~(kHugeTable - 1); }
+void *table_alloc(size_t bytes) {
+    const size_t len = table_bytes(bytes);
+    void *m = mmap(nullptr, len + kHugeTable, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m == MAP_FAILED) throw std::bad_alloc();
+    const uintptr_t a = ((uintptr_t)m + kHugeTable - 1) & ~(uintptr_t)(kHugeTable - 1);
+    if (a > (uintptr_t)m) munmap(m, a - (uintptr_t)m);
+    const uintptr_t end = (uintptr_t)m + len + kHugeTable;
+    if (end > a + len) munmap((void *)(a + len), end - (a + len));
+    (void)madvise((void *)a, len, MADV_HUGEPAGE);
+    return (void *)a;
+}
+void table_free(void *p, size_t bytes) {
+    if (p) munmap(p, table_bytes(bytes));
+}
+constexpr size_t kArenaBlock = kHugeTable;
+#else
 void *table_alloc(size_t bytes) {
     void *p = aligned_alloc(64, (bytes + 63) / 64 * 64);
     if (!p) throw std::bad_alloc();
     return p;
 }
+void table_free(void *p, size_t) { free(p); }
+constexpr size_t kArenaBlock = size_t(1) << 20;
+#endif
 
 // Open-addressing CKey -> index table (linear probing, power-of-two capacity, load <= 1/2): one flat
 // array of 32-byte slots (two per cache line) instead of a node per junction
@@ -316,7 +340,7 @@ class CIndex {
     CIndex() = default;
     CIndex(const CIndex &) = delete;
     CIndex &operator=(const CIndex &) = delete;
-    ~CIndex() { free(slots_); }
+    ~CIndex() { table_free(slots_, cap_ * sizeof(Slot)); }
     // the index of k, inserting v for a new key; second = inserted
     std::pair<size_t, bool> try_emplace(const CKey &k, size_t v) {
         if (2 * (n_ + 1) > cap_) grow();
@@ -356,7 +380,7 @@ class CIndex {
         n_ = 0;
         for (size_t j = 0; j < old_cap; ++j)
             if (old[j].v1) try_emplace(old[j].k, (size_t)old[j].v1 - 1);
-        free(old);
+        table_free(old, old_cap * sizeof(Slot));
     }
 };
 
@@ -389,20 +413,26 @@ struct PyMin {
 // they are until the caller is closed, as the tables themselves do.
 class Arena {
   public:
+    Arena() = default;
+    Arena(const Arena &) = delete;
+    Arena &operator=(const Arena &) = delete;
+    ~Arena() {
+        for (const auto &b : blocks_) table_free(b.first, b.second);
+    }
     std::string_view put(const char *p, size_t n) {
         if (blocks_.empty() || used_ + n > cap_) {
-            cap_ = std::max<size_t>(n, size_t(1) << 20);
-            blocks_.emplace_back(new char[cap_]);
+            cap_ = std::max<size_t>(n, kArenaBlock);
+            blocks_.emplace_back((char *)table_alloc(cap_), cap_);
             used_ = 0;
         }
-        char *d = blocks_.back().get() + used_;
+        char *d = blocks_.back().first + used_;
         if (n) memcpy(d, p, n);
         used_ += n;
         return std::string_view(d, n);
     }
     std::string_view put(std::string_view v) { return put(v.data(), v.size()); }
   private:
-    std::vector<std::unique_ptr<char[]>> blocks_;
+    std::vector<std::pair<char *, size_t>> blocks_;
     size_t used_ = 0, cap_ = 0;
 };
 
@@ -522,7 +552,7 @@ class HitVec {
     HitVec &operator=(const HitVec &) = delete;
     ~HitVec() {
         for (size_t k = 0; k < n_; ++k) (*this)[k].~Hit();
-        for (Hit *b : blocks_) free(b);
+        for (Hit *b : blocks_) table_free(b, kBlock * sizeof(Hit));
     }
     size_t size() const { return n_; }
     Hit &operator[](size_t k) { return blocks_[k >> kShift][k & (kBlock - 1)]; }
