@@ -12,12 +12,25 @@ import sys
 SYM = "/opt/rocm/lib/llvm/bin/llvm-symbolizer"
 
 
+def local_path(o):
+    """A library of this repository named by its path on the GPU box (gpurun's scratch copy): the
+    same file in this checkout, so samples taken there symbolize here."""
+    import os
+    i = o.find("/find_circ2_amd/")
+    if i >= 0 and not os.path.exists(o):
+        cand = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                            o[i + 1:])
+        if os.path.exists(cand):
+            return cand
+    return o
+
+
 def symbolize(keys):
     """{(obj, off): [(function, file:line), ...innermost first]}"""
     keys = sorted(keys)
     if not keys:
         return {}
-    inp = "".join("%s 0x%x\n" % (o, off) for o, off in keys)
+    inp = "".join("%s 0x%x\n" % (local_path(o), off) for o, off in keys)
     out = subprocess.run([SYM, "--inlining", "--demangle", "--functions=linkage"], input=inp,
                          capture_output=True, text=True).stdout
     blocks = out.strip("\n").split("\n\n")
