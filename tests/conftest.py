@@ -20,6 +20,17 @@ def golden():
     return GOLDEN
 
 
+def pytest_collection_finish(session):
+    """The same ordering for module- and session-scoped fixtures, which run before any function-scoped
+    one: if a GPU test is selected, torch's HIP runtime comes up before a fixture can load libfc2.so."""
+    if any(it.get_closest_marker("gpu") is not None for it in session.items):
+        try:
+            import torch
+            torch.cuda.is_available()
+        except Exception:
+            pass
+
+
 @pytest.fixture(autouse=True)
 def _torch_hip_runtime_first(request):
     """One HIP runtime per process: before a GPU test can reach the C ABI, torch's
