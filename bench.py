@@ -1299,8 +1299,18 @@ def main():
         "strong_scaling": strong,
         "configs4_200M_150bp": c4,
     }
+    if traffic:
+        # HBM bytes moved per algorithmic byte (the random 19-B windows each cost whole 128-B lines)
+        line["roofline"]["traffic_ratio"] = round(traffic / (bpp * b.n), 3)
     if args.workload == "hg19" and not args.locus_ordered and b.n == 50_000_000:
-        line["roofline"]["access_pattern_ceiling"] = pattern_ceiling(opt, g, b, dev)
+        pc = pattern_ceiling(opt, g, b, dev)
+        line["roofline"]["access_pattern_ceiling"] = pc
+        if pc:
+            # flat copies (the driver's record keeps a line's scalar fields only): the frac this read-order
+            # layout can reach at all -- the algorithmic bytes over the duration of a launch that makes
+            # only the scan's memory accesses -- and how close the scan runs to it
+            line["roofline"]["ceiling_frac"] = round(bpp * b.n / (pc["probe_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            line["roofline"]["scan_frac_of_ceiling"] = pc["scan_frac_of_ceiling"]
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cb = cpu_baselines(opt, g, b, args.cpu_seconds)
         line["cpu_baseline"] = cb["main"]

@@ -16,6 +16,7 @@ from ._libpath import LIB_PATH, _HERE
 np = LazyModule("numpy", globals(), "np")
 
 FC2_OK = 0
+CALLER_MAX_QUEUED = 64      # FC2_CALLER_MAX_QUEUED (include/fc2_caller.h): chunks fc2_caller_next keeps queued
 FC2_E_PARAM = -1
 FC2_E_HIP = -2
 FC2_E_FORMAT = -3

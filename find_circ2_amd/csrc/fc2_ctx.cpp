@@ -215,7 +215,9 @@ extern "C" int fc2_ctx_genome_load(fc2_ctx *c, const fc2_fasta *fa, int n_thread
     // its threads, so the pages are first touched there in parallel; huge pages where the kernel gives
     // them (fewer faults, a cheap unmap).  Kept by the context until its genome is freed: unmapping
     // ~1 GB here would hold the process's memory map while the caller (the read loop, the sibling
-    // contexts' HIP queues) waits for this call.
+    // contexts' HIP queues) waits for this call.  Host cost: every primary context keeps its own copy
+    // (2-bit planes + N plane, ~1.2 GB for hg19): only the first load of an fc2_fasta takes the prepacked
+    // planes, so a run over N devices (CLI --gpus N, N > 1) holds N such copies until its contexts close.
     fc2::MappedWords &units = c->h_units, &nplane = c->h_nplane;
     std::vector<uint32_t> ncoarse;
     uint64_t n_exotic = 0;

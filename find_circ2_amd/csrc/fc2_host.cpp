@@ -630,7 +630,10 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
     const auto t0 = std::chrono::steady_clock::now();
     auto ms = [&] { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     // the layout checks that need no pass over the bases; the rest is checked while packing
-    for (fc2_chrom_rec &r : f->chroms) r.regular = chrom_rows_in_file(f, r) ? 1 : 0;
+    // (into a local array, published once at the end: a repack -- every device after the first --
+    // never shows a row-broken chromosome as regular to a concurrent fc2_pack_pairs, even briefly)
+    std::vector<uint8_t> regular(f->chroms.size());
+    for (size_t c = 0; c < f->chroms.size(); ++c) regular[c] = chrom_rows_in_file(f, f->chroms[c]) ? 1 : 0;
     std::unique_ptr<std::atomic<uint8_t>[]> broken(new std::atomic<uint8_t>[std::max<size_t>(1, f->chroms.size())]);
     for (size_t c = 0; c < f->chroms.size(); ++c) broken[c].store(0, std::memory_order_relaxed);
     const double t_regular = ms();
@@ -657,7 +660,7 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
                 const Item it = items[k];
                 const fc2_chrom_rec &r = f->chroms[it.c];
                 const uint64_t gu0 = r.gstart / 64;
-                if (r.regular != 1) {           // all N; pairs on it take the byte path
+                if (regular[(size_t)it.c] != 1) {   // all N; pairs on it take the byte path
                     for (uint64_t u = it.u0; u < it.u1; ++u) {
                         units[2 * (gu0 + u)] = 0;
                         units[2 * (gu0 + u) + 1] = 0;
@@ -719,7 +722,7 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
     for (size_t k = 0; k < items.size(); ++k) {
         const Item it = items[k];
         if (!broken[it.c].load(std::memory_order_relaxed)) continue;
-        f->chroms[it.c].regular = 0;
+        regular[(size_t)it.c] = 0;
         const uint64_t gu0 = f->chroms[it.c].gstart / 64;
         for (uint64_t u = it.u0; u < it.u1; ++u) {
             units[2 * (gu0 + u)] = 0;
@@ -728,6 +731,7 @@ extern "C" int fc2_fasta_pack(const fc2_fasta *cf, uint64_t *units, uint64_t *np
         }
         exo[k].clear();
     }
+    for (size_t c = 0; c < f->chroms.size(); ++c) f->chroms[c].regular = regular[c];
     const double t_planes = ms();
     f->exotic.clear();
     for (auto &v : exo) f->exotic.insert(f->exotic.end(), v.begin(), v.end());

@@ -141,9 +141,12 @@ class CtxPipeline:
         self.k = 0
         self.n_ctx = len(devices) * per_device      # per listing of a device: per_device contexts
         # chunks the caller may hold: tickets own their result buffers, so more than the contexts --
-        # while the genome is being built the read loop reads this many chunks ahead
-        self.depth = 4 * self.n_ctx
+        # while the genome is being built the read loop reads this many chunks ahead; never more than
+        # fc2_caller_next queues (FC2_CALLER_MAX_QUEUED, include/fc2_caller.h), or a run with many
+        # --gpus entries would stop on 'too many chunks not submitted'
+        self.depth = min(4 * self.n_ctx, N.CALLER_MAX_QUEUED)
         self._slock = threading.Lock()              # dispatch order (reader thread + recorder thread)
+        self._wlock = threading.Lock()              # wait_ready's bookkeeping
         self._deferred: List[CtxTicket] = []
         self._ready = None
         self._error = None
@@ -188,12 +191,15 @@ class CtxPipeline:
     def wait_ready(self):
         """The contexts and resident genome are built (raises what building them raised); the time
         spent waiting for them is added up in ``wait_s``."""
-        if self._ready is not None:
+        ready = self._ready             # read once: another thread may clear it (evaluate_long runs on the
+        if ready is not None:           # reader thread, result() on the recorder thread)
             import time
             t = time.time()
-            self._ready.join()
-            self._ready = None
-            self.wait_s += time.time() - t
+            ready.join()
+            with self._wlock:
+                if self._ready is ready:
+                    self._ready = None
+                self.wait_s += time.time() - t
         if self._error is not None:
             raise self._error
 

@@ -831,7 +831,13 @@ def _py2_min(a, b):
         return b if b < a else a
     if _is_number(b):
         return b
-    return a
+    if _is_number(a):
+        return a
+    # two non-numbers: Python 2 compares values of one type by value (str lexicographically, arrays
+    # element-wise) and values of different types by type name ('array' < 'str')
+    if type(a) is type(b):
+        return b if b < a else a
+    return b if type(b).__name__ < type(a).__name__ else a
 
 
 def uniq_ok(uniq, min_uniq_qual: int) -> bool:

@@ -174,7 +174,7 @@ class NativeCaller:
         t0 = time.time()
         pipelined = hasattr(evaluate, "submit") and hasattr(evaluate, "result")
         pointers = pipelined and hasattr(evaluate, "submit_ptr")
-        depth = max(2, int(getattr(evaluate, "depth", 2)))
+        depth = min(max(2, int(getattr(evaluate, "depth", 2))), N.CALLER_MAX_QUEUED)
         q: "queue.Queue" = queue.Queue()
         # at most `depth` chunks between being handed out and being recorded: a ScanPipeline slot is
         # only reused once its chunk's results were taken
@@ -288,7 +288,7 @@ class NativeCaller:
         t_last, last_reads = t0, 0
         eval_s = 0.
         pipelined = hasattr(evaluate, "submit") and hasattr(evaluate, "result")
-        depth = max(1, int(getattr(evaluate, "depth", 1))) if pipelined and not self.bam_out else 1
+        depth = min(max(1, int(getattr(evaluate, "depth", 1))), N.CALLER_MAX_QUEUED) if pipelined and not self.bam_out else 1
         queue = deque()                      # (ticket or (results, tiemask), n) in input order
         eof = False
         deferred = None                      # an error of fc2_caller_next, raised after the queued chunks

@@ -133,6 +133,25 @@ def test_gpu_cli_two_gpus_equals_one(tmp_path, extra):
     same(o, outs["g2"])
 
 
+@pytest.mark.parametrize("gpus", ["9", "20"])
+def test_gpu_cli_many_gpu_entries_read_ahead_within_the_queue_limit(tmp_path, gpus):
+    """--gpus 9 / 20 on a one-GPU box (entries wrap round the devices present: 9 or 20 scanners): the
+    read-ahead depth stays within the chunks fc2_caller_next keeps queued (FC2_CALLER_MAX_QUEUED), so
+    tiny chunks read ahead while the genome loads do not stop the run, and the files equal
+    --gpus 1's."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd import cli
+    from test_ingest import same
+    from test_native_caller import _rich_sam
+    sam = str(tmp_path / "rich.sam")
+    fa = _rich_sam(sam, 3000, seed=4321)
+    o1, o2 = str(tmp_path / "g1"), str(tmp_path / ("g" + gpus))
+    assert cli.main(["-G", fa, "-o", o1, "-q", "--chunk-size", "5", "--gpus", "1", sam]) == 0
+    assert cli.main(["-G", fa, "-o", o2, "-q", "--chunk-size", "5", "--gpus", gpus, sam]) == 0
+    same(o1, o2)
+
+
 def test_gpu_pipeline_readahead_many_chunks(tmp_path):
     """ScanPipeline through the native loop with tiny chunks (hundreds of chunks, two in flight
     per scanner, staging slots reused) on the golden reads: the same files as the oracle CLI."""
