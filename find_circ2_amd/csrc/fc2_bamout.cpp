@@ -8,6 +8,8 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 
 namespace fc2 {
 namespace bam {
@@ -47,32 +49,40 @@ int cigar_op(char c) {
 template <class T> void put(std::string &s, T v) { s.append((const char *)&v, sizeof v); }
 }  // namespace
 
+// one BGZF block of n (<= kBlockIn) input bytes into out (kBlockMax bytes); its size, 0 on failure
+size_t deflate_block(z_stream &zs, const char *in, size_t n, uint8_t *out) {
+    deflateReset(&zs);
+    zs.next_in = (Bytef *)in;
+    zs.avail_in = (uInt)n;
+    zs.next_out = out + 18;
+    zs.avail_out = (uInt)(kBlockMax - 18 - 8);
+    if (deflate(&zs, Z_FINISH) != Z_STREAM_END) return 0;
+    const size_t clen = kBlockMax - 18 - 8 - zs.avail_out;
+    const size_t bsize = 18 + clen + 8;
+    static const uint8_t hdr[16] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0};
+    memcpy(out, hdr, 16);
+    out[16] = (uint8_t)((bsize - 1) & 0xff);
+    out[17] = (uint8_t)((bsize - 1) >> 8);
+    const uint32_t crc = (uint32_t)crc32(0L, (const Bytef *)in, (uInt)n);
+    const uint32_t isize = (uint32_t)n;
+    memcpy(out + 18 + clen, &crc, 4);
+    memcpy(out + 18 + clen + 4, &isize, 4);
+    return bsize;
+}
+
 struct Writer {
     FILE *fp = nullptr;
     std::string buf;                       // uncompressed bytes of the current block
     z_stream zs{};
+    int level = 6;
     bool ok = true;
     std::vector<uint8_t> out;
 
     bool flush_block() {
         if (buf.empty()) return ok;
         out.resize(kBlockMax);
-        deflateReset(&zs);
-        zs.next_in = (Bytef *)buf.data();
-        zs.avail_in = (uInt)buf.size();
-        zs.next_out = out.data() + 18;
-        zs.avail_out = (uInt)(kBlockMax - 18 - 8);
-        if (deflate(&zs, Z_FINISH) != Z_STREAM_END) return ok = false;
-        const size_t clen = kBlockMax - 18 - 8 - zs.avail_out;
-        const size_t bsize = 18 + clen + 8;
-        static const uint8_t hdr[16] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 'B', 'C', 2, 0};
-        memcpy(out.data(), hdr, 16);
-        out[16] = (uint8_t)((bsize - 1) & 0xff);
-        out[17] = (uint8_t)((bsize - 1) >> 8);
-        const uint32_t crc = (uint32_t)crc32(0L, (const Bytef *)buf.data(), (uInt)buf.size());
-        const uint32_t isize = (uint32_t)buf.size();
-        memcpy(out.data() + 18 + clen, &crc, 4);
-        memcpy(out.data() + 18 + clen + 4, &isize, 4);
+        const size_t bsize = deflate_block(zs, buf.data(), buf.size(), out.data());
+        if (!bsize) return ok = false;
         if (fwrite(out.data(), 1, bsize, fp) != bsize) ok = false;
         buf.clear();
         return ok;
@@ -98,6 +108,7 @@ Writer *open_writer(const std::string &path, const std::string &text, const std:
     }
     Writer *w = new Writer();
     w->fp = fp;
+    w->level = level;
     if (deflateInit2(&w->zs, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) {
         fclose(fp);
         delete w;
@@ -121,8 +132,49 @@ Writer *open_writer(const std::string &path, const std::string &text, const std:
 
 bool write_raw(Writer *w, const uint8_t *rec, size_t n) { return w->add((const char *)rec, n); }
 
+bool write_bulk(Writer *w, const char *p, size_t n, int threads) {
+    if (!w->ok) return false;
+    // the current block first (the bytes complete it or stay in it)
+    const size_t head = std::min(n, kBlockIn - w->buf.size());
+    w->buf.append(p, head);
+    p += head;
+    n -= head;
+    if (w->buf.size() < kBlockIn) return true;
+    if (!w->flush_block()) return false;
+    const size_t nb = n / kBlockIn;           // whole blocks; the rest starts the next current block
+    if (nb) {
+        const int T = (int)std::max<size_t>(1, std::min<size_t>((size_t)std::max(threads, 1), nb));
+        std::vector<uint8_t> outb(nb * kBlockMax);
+        std::vector<size_t> sz(nb, 0);
+        std::atomic<size_t> next{0};
+        auto work = [&] {
+            z_stream zs{};
+            if (deflateInit2(&zs, w->level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY) != Z_OK) return;
+            for (size_t b; (b = next.fetch_add(1)) < nb;)
+                sz[b] = deflate_block(zs, p + b * kBlockIn, kBlockIn, outb.data() + b * kBlockMax);
+            deflateEnd(&zs);
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < T; ++t) pool.emplace_back(work);
+        work();
+        for (auto &th : pool) th.join();
+        for (size_t b = 0; b < nb && w->ok; ++b)
+            if (!sz[b] || fwrite(outb.data() + b * kBlockMax, 1, sz[b], w->fp) != sz[b]) w->ok = false;
+        p += nb * kBlockIn;
+        n -= nb * kBlockIn;
+    }
+    w->buf.assign(p, n);
+    return w->ok;
+}
+
 bool write_sam(Writer *w, const char *line, const char *end, const std::unordered_map<std::string, int> &tid_of,
                std::string &err) {
+    std::string rec;
+    return encode_sam(line, end, tid_of, rec, err) && w->add(rec.data(), rec.size());
+}
+
+bool encode_sam(const char *line, const char *end, const std::unordered_map<std::string, int> &tid_of,
+                std::string &rec, std::string &err) {
     std::vector<std::pair<const char *, const char *>> f;
     for (const char *p = line;;) {
         const char *t = (const char *)memchr(p, '\t', (size_t)(end - p));
@@ -238,10 +290,9 @@ bool write_sam(Writer *w, const char *line, const char *end, const std::unordere
             default: err = "ValueError: bad SAM tag type"; return false;
         }
     }
-    std::string rec;
     put<int32_t>(rec, (int32_t)b.size());
     rec += b;
-    return w->add(rec.data(), rec.size());
+    return true;
 }
 
 bool close_writer(Writer *w, std::string &err) {

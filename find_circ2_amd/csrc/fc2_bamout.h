@@ -24,6 +24,13 @@ bool write_raw(Writer *w, const uint8_t *rec, size_t n);
 // one SAM text line (no newline); tid_of maps RNAME/RNEXT to reference ids
 bool write_sam(Writer *w, const char *line, const char *end, const std::unordered_map<std::string, int> &tid_of,
                std::string &err);
+// one SAM text line encoded as write_sam does, appended to rec (block_size + body)
+bool encode_sam(const char *line, const char *end, const std::unordered_map<std::string, int> &tid_of,
+                std::string &rec, std::string &err);
+// record bytes in bulk (BAM records, back to back): the full blocks they complete are deflated on
+// `threads` threads and written in order; the blocks are cut where the record-by-record calls would
+// cut them, so the file is byte for byte what those calls write
+bool write_bulk(Writer *w, const char *p, size_t n, int threads);
 // flush, EOF block, close; false on an I/O error
 bool close_writer(Writer *w, std::string &err);
 

@@ -1698,13 +1698,55 @@ extern "C" int fc2_sam_to_bam(const char *sam_path, const char *bam_path) {
     std::string err;
     fc2::bam::Writer *w = rc ? nullptr : fc2::bam::open_writer(bam_path, h->header, h->refs, h->ref_len, err, 1);
     if (!rc && !w) rc = fc2::fail(FC2_E_IO, err);
+    // lines gathered into batches of ~32 MiB of text, each batch encoded on T threads (contiguous line
+    // ranges) and its records written with fc2::bam::write_bulk (blocks deflated on T threads): the file
+    // is byte for byte what encoding and writing record by record gives
+    int T = (int)std::thread::hardware_concurrency();
+    if (const char *env = getenv("OMP_NUM_THREADS")) if (atoi(env) > 0) T = atoi(env);
+    T = std::max(1, std::min(T, 32));
+    std::string text;
+    std::vector<std::pair<size_t, size_t>> lines;        // (offset, length) in text
+    auto process = [&]() -> int {
+        const size_t nl = lines.size();
+        if (!nl) return FC2_OK;
+        const int P = (int)std::max<size_t>(1, std::min<size_t>((size_t)T, nl / 1024));
+        std::vector<std::string> part((size_t)P), perr((size_t)P);
+        std::vector<char> bad((size_t)P, 0);
+        std::vector<std::thread> pool;
+        auto enc = [&](int r) {
+            for (size_t i = nl * (size_t)r / (size_t)P, e = nl * (size_t)(r + 1) / (size_t)P; i < e; ++i) {
+                const char *a = text.data() + lines[i].first;
+                if (!fc2::bam::encode_sam(a, a + lines[i].second, h->tid_of, part[(size_t)r], perr[(size_t)r])) {
+                    bad[(size_t)r] = 1;
+                    return;
+                }
+            }
+        };
+        for (int r = 1; r < P; ++r) pool.emplace_back(enc, r);
+        enc(0);
+        for (auto &th : pool) th.join();
+        std::string all;                                 // records up to the first failing line
+        int r = 0;
+        for (; r < P; ++r) {
+            all += part[(size_t)r];
+            if (bad[(size_t)r]) break;
+        }
+        if (!fc2::bam::write_bulk(w, all.data(), all.size(), T)) return fc2::fail(FC2_E_IO, "fc2_sam_to_bam: write failed");
+        if (r < P) return fc2::fail(FC2_E_FORMAT, perr[(size_t)r]);
+        text.clear();
+        lines.clear();
+        return FC2_OK;
+    };
     const char *ls, *le;
     while (!rc && next_line_view(h, ls, le)) {
         bool blank = true;
         for (const char *c = ls; c < le; ++c) if (!isspace((unsigned char)*c)) { blank = false; break; }
         if (blank) continue;
-        if (!fc2::bam::write_sam(w, ls, le, h->tid_of, err)) rc = fc2::fail(FC2_E_FORMAT, err);
+        lines.emplace_back(text.size(), (size_t)(le - ls));
+        text.append(ls, le);
+        if (text.size() >= ((size_t)32 << 20)) rc = process();
     }
+    if (!rc) rc = process();
     if (!rc) rc = input_rc(h);
     if (w && !fc2::bam::close_writer(w, err) && !rc) rc = fc2::fail(FC2_E_IO, err);
     fc2_ingest_close(h);
