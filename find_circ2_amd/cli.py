@@ -355,7 +355,9 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             nc.finish_reads()
         finally:
             t_fin = time.time()
-            if not EXIT_AFTER_MAIN:             # (the junction tables: freed by the process's exit)
+            # (the junction tables: freed by the process's exit; closed with FC2_CALLER_TIMING, whose
+            # per-stage CPU totals fc2_caller_close prints)
+            if not EXIT_AFTER_MAIN or os.environ.get("FC2_CALLER_TIMING"):
                 nc.close()
         t_files = time.time()
         for k, fh in out.items():
