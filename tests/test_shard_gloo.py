@@ -1,4 +1,4 @@
-"""world_size-2 gloo tests (CPU) of the multi-GPU sharding logic (find_circ2_amd/shard.py).
+"""gloo tests (CPU, world sizes 2, 4 and 8) of the multi-GPU sharding logic (find_circ2_amd/shard.py).
 
 Each rank "scans" its round-robin batches with a deterministic stand-in for the
 kernel (per-pair results are a pure function of the pair, as find_breakpoints
@@ -46,9 +46,11 @@ def _worker(rank, world, port, n, batch, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,batch", [(1000, 64), (10, 100), (999, 1), (0, 8)])
-def test_gloo_two_ranks_ordered_merge(n, batch):
-    world = 2
+# world 2 over every edge case; 4 and 8 (the node's GPU count) over the cases where some ranks get no
+# batch (n < world batches) and where every rank gets several
+@pytest.mark.parametrize("world,n,batch", [(2, 1000, 64), (2, 10, 100), (2, 999, 1), (2, 0, 8),
+                                           (4, 1000, 64), (4, 10, 4), (8, 1000, 64), (8, 999, 1), (8, 10, 4)])
+def test_gloo_ranks_ordered_merge(world, n, batch):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -61,7 +63,7 @@ def test_gloo_two_ranks_ordered_merge(n, batch):
         assert p.exitcode == 0
     expect = fake_scan(np.arange(n, dtype=np.int64) * 31 + 7)
     assert np.array_equal(merged, expect)
-    assert t == 2.0
+    assert t == float(world)
 
 
 def test_batches_cover_and_partition():
@@ -106,12 +108,11 @@ def _shm_worker(rank, world, port, n, batch, q, file_seg=False):
 
 
 @pytest.mark.parametrize("file_seg", [False, True], ids=["shm", "file"])
-@pytest.mark.parametrize("n", [1000, 1, 0])
-def test_gloo_two_ranks_shared_memory_merge(n, file_seg):
+@pytest.mark.parametrize("world,n", [(2, 1000), (2, 1), (2, 0), (4, 1000), (8, 5000), (8, 1)])
+def test_gloo_ranks_shared_memory_merge(world, n, file_seg):
     """bench.py's configs[3] merge (shard.SharedResults): ranks write their round-robin batches'
     results into one node-local buffer at input offsets; rank 0 reads them in input order -- in
     /dev/shm, or in a shared file mapping when /dev/shm has no room (shard._segment)."""
-    world = 2
     batch = shard.round_robin_batch(n, world, per_rank=3, align=64)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -152,7 +153,7 @@ def test_round_bounds_cover_and_shrink(tail):
             assert bounds == shard.batch_bounds(n, b)
 
 
-def _compact_worker(rank, world, port, n, batch, q, width):
+def _compact_worker(rank, world, port, n, batch, q, width, tail=-1):
     import sys
     import torch.distributed as dist
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -161,8 +162,10 @@ def _compact_worker(rank, world, port, n, batch, q, width):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     words8 = sample_words(n, 77)                 # the stream's 8-byte results (every rank can derive them)
-    bounds = shard.batch_bounds(n, batch)
-    cap = max(1, batch)
+    # tail >= 0: the strong-scaling stream's rounds (shard.round_bounds, as bench.strong_scaling deals them)
+    bounds = shard.batch_bounds(n, batch) if tail < 0 else (shard.round_bounds(n, world, per_rank=3, align=64, tail=tail)
+                                                           if n else [])
+    cap = max([1, batch] + [e - s for s, e in bounds])
     merged = shard.SharedCompactResults(n, bounds, cap, create=True, width=width) if rank == 0 else None
     name = shard.broadcast_name(merged.name if rank == 0 else None)
     if rank != 0:
@@ -172,7 +175,7 @@ def _compact_worker(rank, world, port, n, batch, q, width):
         merged.words[:] = 0x5A5A
         merged.esc_count[:] = -1
     dist.barrier()
-    for k, s, e in shard.my_batches(n, batch, rank, world):
+    for k, s, e in shard.my_bounds(bounds, rank, world):
         c, esc = pack(words8[s:e], width)       # what fc2_result_compact_launch writes for the batch
         merged.words[s:e] = c
         merged.esc[k, :len(esc)] = esc          # batch-relative indices, as the device writes them
@@ -188,21 +191,23 @@ def _compact_worker(rank, world, port, n, batch, q, width):
 
 
 @pytest.mark.parametrize("width", [4, 2])
-@pytest.mark.parametrize("n", [5000, 700, 0])
-def test_gloo_two_ranks_compact_merge(n, width):
+@pytest.mark.parametrize("world,n,tail", [(2, 5000, -1), (2, 700, -1), (2, 0, -1), (4, 5000, -1), (8, 5000, -1),
+                                          (8, 700, -1), (2, 5000, 3), (4, 5000, 3), (8, 20000, 3), (8, 700, 1)])
+def test_gloo_ranks_compact_merge(world, n, tail, width):
     """bench.py's configs[3] merge in a compact transfer form (shard.SharedCompactResults, 4 and 2 bytes):
-    words at input offsets, escapes per batch; rank 0's expansion equals the stream's 8-byte results."""
-    world = 2
+    words at input offsets, escapes per batch; rank 0's expansion equals the stream's 8-byte results.
+    tail >= 0: the strong-scaling layout (shard.round_bounds with shrinking tail rounds)."""
     batch = shard.round_robin_batch(n, world, per_rank=3, align=64)
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_compact_worker, args=(r, world, port, n, batch, q, width)) for r in range(world)]
+    procs = [ctx.Process(target=_compact_worker, args=(r, world, port, n, batch, q, width, tail))
+             for r in range(world)]
     for p in procs:
         p.start()
-    merged, words8, csum = q.get(timeout=120)
+    merged, words8, csum = q.get(timeout=240)
     for p in procs:
-        p.join(timeout=120)
+        p.join(timeout=240)
         assert p.exitcode == 0
     assert np.array_equal(merged, words8)
-    assert csum == 21
+    assert csum == sum(r + 10 for r in range(world))
