@@ -901,6 +901,43 @@ def cpu_baselines(opt, g, b, budget_s):
             if time.perf_counter() - t0 > budget_s:
                 break
         py_rate = done / (time.perf_counter() - t0)
+        # (1b) the same literal path on the host's cores: one spawned process per core of the GPU's CPU
+        # share (each loads the FASTA through its own mmap + .byo_index, as separate reference processes
+        # would), disjoint slices of the sample, every first tie checked against the GPU
+        share = cpu_share()
+        items = [k for k in range(len(reads)) if not skip[k]]
+        spans = [(g.names[int(hp["chrom"][k])], int(hp["a_pos"][k]), *((1, 0) if bs[k] else (0, 1)),
+                  int(hp["b_aend"][k]), reads[k], bool(rev[k])) for k in items]
+        pool_res = None
+        try:
+            import multiprocessing as mp
+            from oracle.bp_oracle import literal_rate
+            P = share
+            sl = [spans[len(spans) * i // P:len(spans) * (i + 1) // P] for i in range(P)]
+            t_pool = time.perf_counter()
+            with mp.get_context("spawn").Pool(P) as pool:
+                outs = pool.starmap(literal_rate, [(fa, x, budget_s) for x in sl])
+            wall_pool = time.perf_counter() - t_pool
+            n_done = sum(o[0] for o in outs)
+            pool_agree = pool_raised = 0
+            for i, (nd, _, ties) in enumerate(outs):
+                base = len(spans) * i // P
+                for j, t in enumerate(ties):
+                    k = items[base + j]
+                    gw = int(gpu[k]) if gpu is not None else 0
+                    if t is None:
+                        pool_raised += 1
+                        pool_agree += int((gw >> 48) & 0x6000 != 0)
+                    else:
+                        gx = gw & 0xFFFF
+                        gx = gx - 65536 if gx >= 32768 else gx
+                        pool_agree += int(gx == t[0] and ((gw >> 32) & 0xFFFF) == t[1])
+            pool_res = {"value": round(n_done / max(o[1] for o in outs), 1), "unit": "anchor-pairs/s",
+                        "cores": P, "kind": "port", "pairs": n_done, "first_ties_agree_with_gpu": pool_agree,
+                        "raised": pool_raised, "wall_s_incl_spawn": round(wall_pool, 1),
+                        "per_process_pairs_per_s": round(n_done / P / max(o[1] for o in outs), 1)}
+        except Exception as ex:         # an extra must not cost the bench line
+            pool_res = {"error": repr(ex)}
     finally:
         shutil.rmtree(d, ignore_errors=True)
 
@@ -919,8 +956,7 @@ def cpu_baselines(opt, g, b, budget_s):
         k += chunk
     naive_rate = min(k, len(reads)) / (time.perf_counter() - t0)
     visible = len(os.sched_getaffinity(0))
-    # the GPU box grants 16 CPUs per GPU; sched_getaffinity lists the whole machine's CPUs there
-    cores = min(visible, 16)
+    cores = share
     t0 = time.perf_counter()
     done_fast = 0
     rounds = 0
@@ -940,15 +976,24 @@ def cpu_baselines(opt, g, b, budget_s):
         model = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
     except Exception:
         model = "unknown"
+    one_core = {"value": round(py_rate, 1), "unit": "anchor-pairs/s", "cores": 1, "kind": "port",
+                "sample": "%d pairs, one process; first ties agree with the GPU on %d of %d (%d raised, as the "
+                          "GPU flagged)" % (done, agree, done, errors)}
+    sample = ("literal Python restatement of find_circ.py:854-974 (per-x string concat + numpy byte compare, "
+              "oracle/bp_oracle.py) with both windows per pair fetched through Track.get -> "
+              "GenomeAccessor.get_data -> indexed_fasta.get_data + .upper() (find_circ.py:900-902) from an "
+              "mmap'd FASTA of the bench genome (%s, its 3 largest chromosomes; written with its .byo_index in "
+              "%.1f s, untimed), on a sample of this batch's pairs there" % (",".join(g.names[c] for c in subset), fa_s))
+    if pool_res and "value" in pool_res:
+        main = dict(pool_res, sample="%d processes (one per core of the GPU's CPU share; %s) x %.0f s: %s; "
+                                     "first ties agree with the GPU on %d of %d pairs (%d raised, as the GPU "
+                                     "flagged); the 1-process rate: cpu_baseline_extra.python_1core"
+                                     % (pool_res["cores"], cpu_model_note(visible), budget_s, sample,
+                                        pool_res["first_ties_agree_with_gpu"], pool_res["pairs"], pool_res["raised"]))
+    else:
+        main = dict(one_core, sample=one_core["sample"] + "; " + sample)
     return dict(
-        main={"value": round(py_rate, 1), "unit": "anchor-pairs/s", "cores": 1, "kind": "port",
-              "sample": "%d pairs of this batch on %s (its 3 largest chromosomes), literal Python restatement "
-                        "of find_circ.py:854-974 (per-x string concat + numpy byte compare, oracle/bp_oracle.py) "
-                        "with both windows per pair fetched through Track.get -> GenomeAccessor.get_data -> "
-                        "indexed_fasta.get_data + .upper() (find_circ.py:900-902) from an mmap'd FASTA of the "
-                        "bench genome with its .byo_index (written in %.1f s, untimed); first ties agree with the "
-                        "GPU on %d of %d pairs (%d raised, as the GPU flagged)"
-                        % (done, ",".join(g.names[c] for c in subset), fa_s, agree, done, errors)},
+        main=main, python_1core=one_core, python_pool=pool_res,
         c_naive={"value": round(naive_rate, 1), "unit": "anchor-pairs/s", "cores": 1, "kind": "port",
                  "sample": "C literal O(l^2) restatement (oracle/bp_oracle.c) on the same sample, windows "
                            "pre-decoded"},
@@ -957,6 +1002,27 @@ def cpu_baselines(opt, g, b, budget_s):
                           "sched_getaffinity lists %d), %d pairs x %d rounds, windows pre-decoded" % (
                               cores, visible, len(reads), rounds)},
         cpu_model=model)
+
+
+def cpu_share() -> int:
+    """CPUs this process may use: the cgroup quota (cpu.max) when one is set, else the affinity set, at
+    most 16 -- the GPU box grants 16 CPUs per GPU while sched_getaffinity lists the whole machine's."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return max(1, min(n, 16))
+
+
+def cpu_model_note(visible: int) -> str:
+    try:
+        model = [l for l in open("/proc/cpuinfo") if l.startswith("model name")][0].split(":", 1)[1].strip()
+    except Exception:
+        model = "unknown"
+    return "%s, sched_getaffinity lists %d" % (model, visible)
 
 
 def kernel_label(g, ordered: bool) -> str:
@@ -1314,7 +1380,8 @@ def main():
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cb = cpu_baselines(opt, g, b, args.cpu_seconds)
         line["cpu_baseline"] = cb["main"]
-        line["cpu_baseline_extra"] = {"c_naive_1core": cb["c_naive"], "c_fast_allcores": cb["c_fast"],
+        line["cpu_baseline_extra"] = {"python_1core": cb["python_1core"], "python_pool": cb["python_pool"],
+                                      "c_naive_1core": cb["c_naive"], "c_fast_allcores": cb["c_fast"],
                                       "cpu_model": cb["cpu_model"]}
     if rank == 0 and ws == 1 and not args.no_extra and args.workload == "hg19":
         line["extra"] = {"device_pipeline_pcie": device_pipeline(opt, g, b, reps=5)}

@@ -20,6 +20,7 @@ search) and every output file must be byte-identical.  One JSON line on stdout; 
 
 usage: python scripts/cli_steady.py [--sizes 2000000,20000000] [--threads 4,8,16,32] [--reps 1]
                                     [--check] [--out DIR] [--keep]
+Each run's record is printed as its own JSON line as soon as it is done; the summary comes last.
 """
 import argparse
 import gzip
@@ -67,8 +68,10 @@ def quota():
         return None
 
 
-def run_cli(fa, bam, out, threads, extra=(), timeout=900):
-    env = dict(os.environ, FC2_CALLER_TIMING="1")
+def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False):
+    env = dict(os.environ)
+    if timing:
+        env["FC2_CALLER_TIMING"] = "1"
     if threads:
         for k in ("FC2_PARSE_THREADS", "FC2_INGEST_THREADS", "FC2_NEXT_THREADS", "FC2_CALLER_THREADS",
                   "OMP_NUM_THREADS"):
@@ -81,7 +84,15 @@ def run_cli(fa, bam, out, threads, extra=(), timeout=900):
     p = subprocess.Popen(cmd, cwd=ROOT, stdin=feeder.stdout, stderr=err, env=env,
                          preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None)
     feeder.stdout.close()
-    rc = p.wait(timeout=timeout)
+    while True:                             # a heartbeat on stderr (a long run is not a hung one)
+        try:
+            rc = p.wait(timeout=30)
+            break
+        except subprocess.TimeoutExpired:
+            if time.time() - t0 > timeout:
+                p.kill()
+                raise
+            log("  ... %s running %.0f s" % (os.path.basename(out), time.time() - t0))
     wall = time.time() - t0
     feeder.wait()
     err.close()
@@ -105,6 +116,18 @@ def run_cli(fa, bam, out, threads, extra=(), timeout=900):
     loop_s = phases.get("read_loop_s")
     net = loop_s - phases.get("genome_wait_s", 0.0) if loop_s else None
     subs = [l for l in errt.splitlines() if l.startswith("submit nf=")]
+    sub_ms = {}
+    for l in subs:
+        for k, v in re.findall(r" ([A-D])=([0-9.]+)", l):
+            sub_ms[k] = sub_ms.get(k, 0.0) + float(v)
+    nxt = {}
+    for l in errt.splitlines():
+        if l.startswith("next nf="):
+            for k, v in re.findall(r"(read|process|pairs)=([0-9.]+)", l):
+                nxt[k] = nxt.get(k, 0.0) + float(v)
+    sd = re.search(r"process shutdown: (.*)", text)
+    if sd:
+        phases.update({"shutdown_" + k: float(v) for k, v in re.findall(r"(\w+)=([0-9.naN]+)", sd.group(1))})
     return {
         "threads": threads, "cpus": len(cpus) if cpus else None, "process_wall_s": round(wall, 3),
         "reads": reads, "spans": spans,
@@ -113,7 +136,9 @@ def run_cli(fa, bam, out, threads, extra=(), timeout=900):
         "loop_spans_per_s": round(spans / loop_s, 1) if loop_s else None,
         "loop_spans_per_s_after_genome": round(spans / net, 1) if net and net > 0 else None,
         "wall_reads_per_s": round(reads / wall, 1), "wall_spans_per_s": round(spans / wall, 1) if spans else None,
-        "stages_s": stages, "cpu_s_per_stage": cpu_s, "phases_s": phases, "n_chunks": len(subs),
+        "stages_s": stages, "cpu_s_per_stage": cpu_s, "phases_s": phases, "n_chunks": len(subs) or None,
+        "submit_phase_ms": {k: round(v, 1) for k, v in sub_ms.items()} or None,
+        "next_phase_ms": {k: round(v, 1) for k, v in nxt.items()} or None,
     }
 
 
@@ -136,7 +161,7 @@ def main():
     ap.add_argument("--keep", action="store_true")
     a = ap.parse_args()
     sizes = [int(x) for x in a.sizes.split(",")]
-    threads = [int(x) for x in a.threads.split(",")]
+    threads = [int(x) for x in a.threads.split(",") if x.strip() and x != "none"]
     import tempfile
     d = a.out or tempfile.mkdtemp(prefix="fc2_steady_", dir="/tmp")
     os.makedirs(d, exist_ok=True)
@@ -174,14 +199,17 @@ def main():
         runs = []
         for n in sorted(sizes):
             for t in [0] + threads:
-                for r in range(a.reps):
-                    out = os.path.join(d, "o_%d_%d_%d" % (n, t, r))
-                    x = run_cli(fa, bams[n], out, t)
+                # the clean runs (what a user gets), then one with FC2_CALLER_TIMING's per-stage CPU
+                # accounting (it also closes the caller at exit to print the totals)
+                for r in list(range(a.reps)) + ["timing"]:
+                    out = os.path.join(d, "o_%d_%d_%s" % (n, t, r))
+                    x = run_cli(fa, bams[n], out, t, timing=(r == "timing"))
                     x["size"] = n
                     x["rep"] = r
                     runs.append(x)
-                    log("size %d threads %s: loop %.3f s, %.3g spans/s loop, %.3g spans/s wall, cpu %s" % (
-                        n, t or "default", x["loop_s"], x["loop_spans_per_s"] or 0, x["wall_spans_per_s"] or 0,
+                    print(json.dumps(x), flush=True)
+                    log("size %d threads %s rep %s: loop %.3f s, %.3g spans/s loop, %.3g spans/s wall, cpu %s" % (
+                        n, t or "default", r, x["loop_s"], x["loop_spans_per_s"] or 0, x["wall_spans_per_s"] or 0,
                         x["cpu_s_per_stage"]))
                     if not a.keep and not (a.check and n == max(sizes) and t == 0 and r == 0):
                         shutil.rmtree(out, ignore_errors=True)
@@ -190,7 +218,7 @@ def main():
             n = max(sizes)
             o_py = os.path.join(d, "python_caller")
             t0 = time.time()
-            x = run_cli(fa, bams[n], o_py, 0, extra=["--python-caller"], timeout=1800)
+            x = run_cli(fa, bams[n], o_py, 0, extra=["--python-caller"], timeout=1500)
             res["python_caller_%d" % n] = {k: x[k] for k in ("process_wall_s", "loop_s", "loop_spans_per_s")}
             same = outputs(os.path.join(d, "o_%d_0_0" % n)) == outputs(o_py)
             res["identical_to_python_loop_at_%d" % n] = same

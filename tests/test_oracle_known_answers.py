@@ -131,3 +131,25 @@ def test_ref_track_chain_equals_indexed_fasta(tmp_path):
             assert [(t.x, t.coord) for t in h1] == [(t.x, t.coord) for t in h2]
             n += bool(h1)
     assert n >= 3
+
+
+def test_literal_rate_pool_matches_direct_calls(tmp_path):
+    """bench.py's multi-process literal CPU baseline (oracle.bp_oracle.literal_rate on spawned workers,
+    disjoint slices): every span's first tie equals a direct find_breakpoints call on the same span."""
+    import multiprocessing as mp
+    import shutil
+    from oracle.bp_oracle import literal_rate
+    fa = str(tmp_path / "CDR1as_locus.fa")
+    shutil.copy(os.path.join(GOLDEN, "CDR1as_locus.fa"), fa)
+    calls = _calls(fa, os.path.join(GOLDEN, "cdr1as_reads.fa")) + \
+        _calls(fa, os.path.join(GOLDEN, "cdr1as_reads.fa"), shift=2)
+    spans = [(sp.chrom, sp.a_pos, sp.a_aend, sp.b_pos, sp.b_aend, sp.read_part, sp.primary_reverse)
+             for _, sp, _ in calls]
+    want = [(h[0].x, h[0].n_hits) if h else (-1, 0) for _, _, h in calls]
+    P = 2
+    sl = [spans[len(spans) * i // P:len(spans) * (i + 1) // P] for i in range(P)]
+    with mp.get_context("spawn").Pool(P) as pool:
+        outs = pool.starmap(literal_rate, [(fa, x, 60.0) for x in sl])
+    assert sum(o[0] for o in outs) == len(spans)
+    assert [t for o in outs for t in o[2]] == want
+    assert (39, 1) in want
