@@ -13,8 +13,13 @@ evaluation per pair, genome window gather included.  Pairs are independent, so
 ranks process their own shards with no collective on the data path (weak
 scaling); the only collectives are the timing barrier and the max-over-ranks.
 
-Also reported (``extra``): configs[1] (1M pairs on CDR1as_locus.fa), and the
-CPU baselines (literal Python restatement, C naive O(l^2), C O(l) on all cores).
+Also reported: ``roofline`` (the kernel's HBM fraction, its PMC traffic, and the ceiling of its
+access pattern), ``cpu_baseline`` (the reference's path restated literally in Python, over a
+process pool of the GPU's CPU share; 1-process and C legs in ``cpu_baseline_extra``),
+``strong_scaling`` (configs[3]) and ``configs4_200M_150bp``; ``extra``: configs[1] (1M pairs on
+CDR1as_locus.fa), the configs[4] per-GPU share, and the whole CLI in anchor pairs/s at 2M and 20M
+reads (BAM on stdin).  ``--research`` adds the forms DESIGN.md §5 compares (pipelines, window-carrying,
+wave-per-pair, reorder-then-scan, locus-ordered).
 """
 from __future__ import annotations
 
@@ -68,7 +73,11 @@ def parse():
     ap.add_argument("--locus-ordered", dest="locus_ordered", action="store_true",
                     help="lay the batch out by A-window locus (PairBatch.pack(locus_order=True)); default read order")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the configs[1] side measurement")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="skip the extras (configs[1], the configs[4] 150-bp share, the CLI end to end)")
+    ap.add_argument("--research", action="store_true",
+                    help="also run the research legs DESIGN.md §5 cites: device / host pipelines, window-carrying, "
+                         "wave-per-pair and reorder-then-scan forms, the locus-ordered batch")
     ap.add_argument("--no-strong", action="store_true", help="skip the configs[3] strong-scaling / ordered-merge run")
     ap.add_argument("--no-config4", action="store_true", help="skip the configs[4] 200M x 120-150 bp run")
     ap.add_argument("--strong-batches", type=int, default=0,
@@ -916,7 +925,7 @@ def cpu_baselines(opt, g, b, budget_s):
             sl = [spans[len(spans) * i // P:len(spans) * (i + 1) // P] for i in range(P)]
             t_pool = time.perf_counter()
             with mp.get_context("spawn").Pool(P) as pool:
-                outs = pool.starmap(literal_rate, [(fa, x, budget_s) for x in sl])
+                outs = pool.starmap(literal_rate, [(fa, x, budget_s, True) for x in sl])
             wall_pool = time.perf_counter() - t_pool
             n_done = sum(o[0] for o in outs)
             pool_agree = pool_raised = 0
@@ -932,8 +941,10 @@ def cpu_baselines(opt, g, b, budget_s):
                         gx = gw & 0xFFFF
                         gx = gx - 65536 if gx >= 32768 else gx
                         pool_agree += int(gx == t[0] and ((gw >> 32) & 0xFFFF) == t[1])
+            n_checked = sum(len(o[2]) for o in outs)
             pool_res = {"value": round(n_done / max(o[1] for o in outs), 1), "unit": "anchor-pairs/s",
-                        "cores": P, "kind": "port", "pairs": n_done, "first_ties_agree_with_gpu": pool_agree,
+                        "cores": P, "kind": "port", "pairs": n_done, "pairs_checked": n_checked,
+                        "first_ties_agree_with_gpu": pool_agree,
                         "raised": pool_raised, "wall_s_incl_spawn": round(wall_pool, 1),
                         "per_process_pairs_per_s": round(n_done / P / max(o[1] for o in outs), 1)}
         except Exception as ex:         # an extra must not cost the bench line
@@ -985,11 +996,13 @@ def cpu_baselines(opt, g, b, budget_s):
               "mmap'd FASTA of the bench genome (%s, its 3 largest chromosomes; written with its .byo_index in "
               "%.1f s, untimed), on a sample of this batch's pairs there" % (",".join(g.names[c] for c in subset), fa_s))
     if pool_res and "value" in pool_res:
-        main = dict(pool_res, sample="%d processes (one per core of the GPU's CPU share; %s) x %.0f s: %s; "
-                                     "first ties agree with the GPU on %d of %d pairs (%d raised, as the GPU "
-                                     "flagged); the 1-process rate: cpu_baseline_extra.python_1core"
+        main = dict(pool_res, sample="%d processes (one per core of the GPU's CPU share; %s) x %.0f s, each "
+                                     "cycling over its slice: %s; first ties agree with the GPU on %d of %d distinct "
+                                     "pairs (%d raised, as the GPU flagged); the 1-process rate: "
+                                     "cpu_baseline_extra.python_1core"
                                      % (pool_res["cores"], cpu_model_note(visible), budget_s, sample,
-                                        pool_res["first_ties_agree_with_gpu"], pool_res["pairs"], pool_res["raised"]))
+                                        pool_res["first_ties_agree_with_gpu"], pool_res["pairs_checked"],
+                                        pool_res["raised"]))
     else:
         main = dict(one_core, sample=one_core["sample"] + "; " + sample)
     return dict(
@@ -1161,115 +1174,50 @@ def wave_per_pair(opt, g, b, dev, bpp, reps: int = 3):
                     "so the headline keeps one pair per lane"}
 
 
-def _cli_outputs(out):
-    import gzip
-    files = {}
-    for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
-        files[f] = open(os.path.join(out, f), "rb").read()
-    with gzip.open(os.path.join(out, "spliced_reads.fastq.gz")) as fh:
-        files["spliced_reads.fastq"] = fh.read()
-    return files
-
-
-def _wait_blocking(proc, timeout):
-    """proc's exit status, waited for in one blocking waitpid (a watchdog kills it after `timeout` s):
-    subprocess's wait(timeout) polls with sleeps of up to 50 ms, which would add that much to a
-    sub-second process wall."""
-    import threading
-    dog = threading.Timer(timeout, proc.kill)
-    dog.start()
-    try:
-        return proc.wait()
-    finally:
-        dog.cancel()
-
-
-def cli_end_to_end(reads=2_000_000):
+def cli_end_to_end(sizes=(2_000_000, 20_000_000)):
     """The product end to end (an extra, never `value`), in north_star's form ``samtools view -b ... |
-    find_circ -G genome.fa -o out``: scripts/cli_scale_check.py's generator writes an hg19-shaped genome
-    FASTA and a bwa-mem-like SAM of `reads` reads, fc2_sam_to_bam turns it into a BGZF BAM, and
-    `python -m find_circ2_amd.cli` runs as its own process reading that BAM from a stdin pipe (format
-    detected from the bytes; BGZF blocks inflated on worker threads, the C++ read loop on worker pools,
-    HIP search through ctxpipe.CtxPipeline (the torch-free fc2_ctx ABI), gzip members on worker threads).  The same reads as SAM
-    text by path run too; both runs must write identical files.  The first run builds the .byo_index;
-    the runs after it are reported: the loop's own reads/s (run.log) and the process wall time, the
-    BAM form as the median of CLI_RUNS runs (one run moves +-10 % on the box's shared CPU quota)."""
-    import re
+    find_circ -G genome.fa -o out`` and in the metric's unit: scripts/gen_reads writes an hg19-shaped
+    genome FASTA and a bwa-mem-like SAM (scripts/cli_steady.py: 60 % unspliced, 40 % spliced reads),
+    fc2_sam_to_bam turns it into a BGZF BAM, and `python -m find_circ2_amd.cli` runs as its own process
+    reading that BAM from a stdin pipe.  Reported per size: anchor pairs (JunctionSpans searched) per
+    second of the read loop and of the process wall, and reads/s; 2M reads as the median of CLI_RUNS
+    runs plus the same reads as SAM by path (files must be identical), 20M reads (steady state: the
+    fixed start-up and the tables amortised) once.  The first run builds the .byo_index."""
     import shutil
-    import subprocess
     import tempfile
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
-    from cli_scale_check import make_genome, write_fasta, write_sam
-    from find_circ2_amd import sq_table
-    from find_circ2_amd.ingest import sam_to_bam
+    from cli_steady import outputs, prepare, quota, run_cli
     d = tempfile.mkdtemp(prefix="fc2_bench_cli_", dir="/tmp")
+    keys = ("loop_spans_per_s", "wall_spans_per_s", "loop_reads_per_s", "wall_reads_per_s", "spans", "reads",
+            "loop_s", "process_wall_s", "genome_wait_s")
     try:
-        fa, sam, bam = os.path.join(d, "genome.fa"), os.path.join(d, "reads.sam"), os.path.join(d, "reads.bam")
-        rng = np.random.default_rng(2024)
-        names, sizes = sq_table(os.path.join(ROOT, "tests", "golden", "test_norm.sam"))
-        seqs = make_genome(fa, names, sizes, rng)
-        write_sam(sam, seqs, reads, rng)
-        write_fasta(fa, seqs)
-        del seqs
-        sam_to_bam(sam, bam)
-
-        def run(tag, stdin_bam):
-            out = os.path.join(d, tag)
-            cmd = [sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", out, "-q"]
-            t0 = time.time()
-            if stdin_bam:                      # a real pipe, as from samtools / an aligner
-                feeder = subprocess.Popen(["cat", bam], stdout=subprocess.PIPE)
-                rc = _wait_blocking(subprocess.Popen(cmd, cwd=ROOT, stdin=feeder.stdout), 600)
-                wall = time.time() - t0
-                feeder.stdout.close()
-                feeder.wait()
-            else:
-                rc = _wait_blocking(subprocess.Popen(cmd + [sam], cwd=ROOT), 600)
-                wall = time.time() - t0
-            if rc != 0:
-                raise RuntimeError("cli exit status %d (%s)" % (rc, tag))
-            log = open(os.path.join(out, "run.log")).read()
-            m = re.search(r"overall ([0-9.]+)k reads/second", log)
-            st = re.search(r"read loop stages: (.*)", log)
-            ph = re.search(r"process phases: (.*)", log)
-            phases = {k: float(v) for k, v in re.findall(r"(\w+)=([0-9.naN]+)", ph.group(1))} if ph else None
-            sd = re.search(r"process shutdown: (.*)", log)
-            if phases is not None and sd:
-                phases.update({"shutdown_" + k: float(v) for k, v in re.findall(r"(\w+)=([0-9.naN]+)", sd.group(1))})
-            after = None
-            if phases and phases.get("read_loop_s"):
-                loop_net = phases["read_loop_s"] - phases.get("genome_wait_s", 0.0)
-                after = round(reads / loop_net, 1) if loop_net > 0 else None
-            return out, {"value": round(float(m.group(1)) * 1e3, 1) if m else None, "unit": "reads/s",
-                         "process_wall_s": round(wall, 2),
-                         "reads_per_process_wall_s": round(reads / wall, 1),
-                         "loop_reads_per_s_after_genome": after,
-                         "phases_s": phases, "stages": st.group(1) if st else None}
-
-        run("warm", False)                     # builds genome.fa.byo_index
-        runs = [run("bam_stdin%d" % k, True) for k in range(CLI_RUNS)]
-        vals = [r[1]["value"] for r in runs]
-        k_med = sorted(range(len(runs)), key=lambda k: (vals[k] is None, vals[k] or 0))[len(runs) // 2]
-        o_bam, res = runs[k_med]
-        walls = [r[1]["process_wall_s"] for r in runs]
-        res = dict(res, runs=vals, process_wall_runs=walls, process_wall_median_s=sorted(walls)[len(walls) // 2])
-        o_sam, res_sam = run("sam_path", False)
-        res["reads"] = reads
-        res["bam_bytes"] = os.path.getsize(bam)
-        res["outputs_identical_to_sam_path_run"] = _cli_outputs(o_bam) == _cli_outputs(o_sam)
-        res["sam_by_path"] = res_sam
-        res["note"] = ("whole CLI, BGZF BAM piped on stdin (cat reads.bam | python -m find_circ2_amd.cli -G genome.fa "
-                       "-o out), hg19-shaped genome, .byo_index present: value = the read loop's reads/s from "
-                       "run.log, the median of `runs` (process_wall_runs: every run's wall); process_wall_s includes interpreter start, genome load and upload "
-                       "(reads_per_process_wall_s = reads / process_wall_s; phases_s = run.log's process phases: "
-                       "before_main_s interpreter + imports, genome_index_s, device_genome_s HIP init + 2-bit pack + "
-                       "upload + tables -- built on a thread while the loop starts reading, genome_wait_s the "
-                       "loop's wait for it, read_loop_s (the loop's reads/s, `value`, includes that wait, as the "
-                       "reference's lazily loaded genome is inside its loop; loop_reads_per_s_after_genome leaves it "
-                       "out, the round-4 form), tables_s, shutdown_*); sam_by_path = "
-                       "the same reads as SAM text by path; outputs of the two runs compared here, and against "
-                       "the Python loop in tests and scripts/cli_scale_check.py")
-        return res
+        small, big = min(sizes), max(sizes)
+        fa, bams, sams, info = prepare(d, sizes, keep_sam_sizes=(small,))
+        run_cli(fa, bams[small], os.path.join(d, "warm"), 0)
+        runs = [run_cli(fa, bams[small], os.path.join(d, "bam%d" % k), 0) for k in range(CLI_RUNS)]
+        order = sorted(range(len(runs)), key=lambda k: runs[k]["loop_spans_per_s"] or 0)
+        med = order[len(order) // 2]
+        res_small = {k: runs[med][k] for k in keys}
+        res_small.update(runs_loop_spans_per_s=[r["loop_spans_per_s"] for r in runs],
+                         runs_process_wall_s=[r["process_wall_s"] for r in runs], phases_s=runs[med]["phases_s"],
+                         stages_s=runs[med]["stages_s"])
+        by_path = run_cli(fa, sams[small], os.path.join(d, "sam_path"), 0, by_path=True)
+        res_small["sam_by_path"] = {k: by_path[k] for k in keys}
+        res_small["outputs_identical_bam_stdin_vs_sam_path"] = (
+            outputs(os.path.join(d, "bam%d" % med)) == outputs(os.path.join(d, "sam_path")))
+        r_big = run_cli(fa, bams[big], os.path.join(d, "big"), 0)
+        res_big = {k: r_big[k] for k in keys}
+        res_big.update(phases_s=r_big["phases_s"], stages_s=r_big["stages_s"])
+        return {"value": res_big["loop_spans_per_s"], "unit": "anchor-pairs/s",
+                "value_process_wall": res_big["wall_spans_per_s"], "reads": big,
+                "at_%dM_reads" % (small // 10**6): res_small, "at_%dM_reads" % (big // 10**6): res_big,
+                "input": info, "cgroup_cpu_quota": quota(), "cpus_visible": len(os.sched_getaffinity(0)),
+                "note": "whole CLI (C++ read loop + HIP search through the C context ABI), BGZF BAM piped on stdin "
+                        "(cat reads.bam | python -m find_circ2_amd.cli -G genome.fa -o out), hg19-shaped genome, "
+                        ".byo_index present; value = anchor pairs searched per second of the read loop at %dM reads "
+                        "(value_process_wall: per second of the whole process, start-up, genome upload, BED tables "
+                        "and exit included); host-bound: the loop uses the box's whole CPU share (DESIGN.md §0, "
+                        "scripts/cli_steady.py for the thread curve)" % (big // 10**6)}
     except Exception as e:          # an extra must not cost the bench line
         return {"error": repr(e)}
     finally:
@@ -1374,8 +1322,10 @@ def main():
         if pc:
             # flat copies (the driver's record keeps a line's scalar fields only): the frac this read-order
             # layout can reach at all -- the algorithmic bytes over the duration of a launch that makes
-            # only the scan's memory accesses -- and how close the scan runs to it
-            line["roofline"]["ceiling_frac"] = round(bpp * b.n / (pc["probe_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+            # only the scan's memory accesses (the probe stores 8-B results, so priced with 8-B results) --
+            # and how close the scan (its 8-B form, in the same run) comes to it
+            bpp8 = algo_bytes_per_pair(args.read_len, opt.asize, opt.margin, result_bytes=8)
+            line["roofline"]["ceiling_frac"] = round(bpp8 * b.n / (pc["probe_ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
             line["roofline"]["scan_frac_of_ceiling"] = pc["scan_frac_of_ceiling"]
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cb = cpu_baselines(opt, g, b, args.cpu_seconds)
@@ -1384,15 +1334,18 @@ def main():
                                       "c_naive_1core": cb["c_naive"], "c_fast_allcores": cb["c_fast"],
                                       "cpu_model": cb["cpu_model"]}
     if rank == 0 and ws == 1 and not args.no_extra and args.workload == "hg19":
-        line["extra"] = {"device_pipeline_pcie": device_pipeline(opt, g, b, reps=5)}
-        line["extra"]["device_pipeline_pcie"]["d2h_8B_words"] = {
-            k: v for k, v in device_pipeline(opt, g, b, reps=5, width=8).items() if k != "note"}
-        line["extra"]["host_pipeline_from_pair_arrays"] = host_pipeline(opt, g, b)
-        line["extra"]["configs[2]_window_carrying_batch"] = window_carrying(opt, g, b, args.steps, dev, bpp)
-        line["extra"]["configs[2]_north_star_wave_per_pair_form"] = wave_per_pair(opt, g, b, dev, bpp)
-        # the honest price of locus order for a read-order stream: the device reorder (fc2_reorder_launch,
-        # stable counting sort by genome bucket) in front of the scan, both timed; results in input order
-        line["extra"]["configs[2]_device_reorder_then_scan"] = reorder_then_scan(opt, g, b, args.steps, dev, bpp)
+        line["extra"] = {}
+        if args.research:
+            # the forms and pipelines DESIGN.md §5 compares the headline with (opt-in: --research)
+            line["extra"]["device_pipeline_pcie"] = device_pipeline(opt, g, b, reps=5)
+            line["extra"]["device_pipeline_pcie"]["d2h_8B_words"] = {
+                k: v for k, v in device_pipeline(opt, g, b, reps=5, width=8).items() if k != "note"}
+            line["extra"]["host_pipeline_from_pair_arrays"] = host_pipeline(opt, g, b)
+            line["extra"]["configs[2]_window_carrying_batch"] = window_carrying(opt, g, b, args.steps, dev, bpp)
+            line["extra"]["configs[2]_north_star_wave_per_pair_form"] = wave_per_pair(opt, g, b, dev, bpp)
+            # the honest price of locus order for a read-order stream: the device reorder (fc2_reorder_launch,
+            # stable counting sort by genome bucket) in front of the scan, both timed; results in input order
+            line["extra"]["configs[2]_device_reorder_then_scan"] = reorder_then_scan(opt, g, b, args.steps, dev, bpp)
         del b, out
         torch.cuda.empty_cache()
         a2 = argparse.Namespace(**vars(args))
@@ -1405,20 +1358,21 @@ def main():
             "achieved_algo_GBs": round(bpp * b2.n / (km2 * 1e-3) / 1e9, 1)}
         del b2, g2
         torch.cuda.empty_cache()
-        # the same configs[2] workload laid out in genome order of the A window, as
-        # PairBatch.pack(locus_order=True) does on the host (results come back in input order)
-        a3 = argparse.Namespace(**vars(args))
-        a3.locus_ordered = True
-        o3, g3, b3 = build_workload(a3, rank, dev)
-        el3, km3, _ = timed_scans(o3, g3, b3, args.steps, args.warmup, 1, dev)
-        ach3 = bpp * b3.n / (km3 * 1e-3) / 1e9
-        line["extra"]["configs[2]_locus_ordered_batch"] = {
-            "value": round(b3.n * args.steps / el3, 1), "unit": "anchor-pairs/s", "kernel_ms": round(km3, 4),
-            "achieved_algo_GBs": round(ach3, 1), "frac": round(ach3 / HBM_PEAK_GBS, 4),
-            "note": "same 50M-pair hg19-shaped workload, batch laid out by A-window locus (host packer option "
-                    "locus_order=True); the headline keeps read order"}
-        del b3, g3
-        torch.cuda.empty_cache()
+        if args.research:
+            # the same configs[2] workload laid out in genome order of the A window, as
+            # PairBatch.pack(locus_order=True) does on the host (results come back in input order)
+            a3 = argparse.Namespace(**vars(args))
+            a3.locus_ordered = True
+            o3, g3, b3 = build_workload(a3, rank, dev)
+            el3, km3, _ = timed_scans(o3, g3, b3, args.steps, args.warmup, 1, dev)
+            ach3 = bpp * b3.n / (km3 * 1e-3) / 1e9
+            line["extra"]["configs[2]_locus_ordered_batch"] = {
+                "value": round(b3.n * args.steps / el3, 1), "unit": "anchor-pairs/s", "kernel_ms": round(km3, 4),
+                "achieved_algo_GBs": round(ach3, 1), "frac": round(ach3 / HBM_PEAK_GBS, 4),
+                "note": "same 50M-pair hg19-shaped workload, batch laid out by A-window locus (host packer option "
+                        "locus_order=True); the headline keeps read order"}
+            del b3, g3
+            torch.cuda.empty_cache()
         # configs[4]: 200M 150 bp pairs with variable anchor lengths over 8 GPUs -> this GPU's 25M share
         a4 = argparse.Namespace(**vars(args))
         a4.pairs, a4.read_len, a4.read_len_min = 25_000_000, 150, 120
@@ -1438,7 +1392,7 @@ def main():
         del b4, g4
         torch.cuda.empty_cache()
         if not args.no_cli:
-            line["extra"]["cli_end_to_end_2M_reads_bam_stdin"] = cli_end_to_end()
+            line["extra"]["cli_end_to_end"] = cli_end_to_end()
     if rank == 0:
         print(json.dumps(line), flush=True)
     if ws > 1:

@@ -406,23 +406,31 @@ def first_tie(hits: List[Hit], opt: Options) -> List[Hit]:
     return list(hits) if opt.allhits else [hits[0]]
 
 
-def literal_rate(fasta_path: str, spans: List[tuple], budget_s: float):
+def literal_rate(fasta_path: str, spans: List[tuple], budget_s: float, cycle: bool = False):
     """The literal path timed on one core, for the bench's CPU baseline run over a process pool: per
     span (chrom, a_pos, a_aend, b_pos, b_aend, read_part, primary_reverse) both windows through the
     Track.get chain of the mmap'd FASTA (its .byo_index loaded) and find_breakpoints with the default
-    options, until `budget_s` seconds have passed.  Returns (spans done, seconds, first ties) with
-    a first tie = (x, n_hits), (-1, 0) for no hit, None where the reference raises."""
+    options, until `budget_s` seconds have passed (cycle: over the spans again until then).  Returns
+    (spans done, seconds, first ties of the first pass) with a first tie = (x, n_hits), (-1, 0) for no
+    hit, None where the reference raises."""
     import time
     track = RefGenomeTrack(RefIndexedFasta(fasta_path, use_existing_index=True, use_mmap=True))
     opt = Options()
     out = []
+    done = 0
     t0 = time.perf_counter()
-    for t in spans:
-        try:
-            ties = find_breakpoints(Span(*t), track, opt)
-            out.append((ties[0].x, ties[0].n_hits) if ties else (-1, 0))
-        except Exception:
-            out.append(None)
-        if time.perf_counter() - t0 > budget_s:
+    while spans:
+        for t in spans:
+            try:
+                ties = find_breakpoints(Span(*t), track, opt)
+                r = (ties[0].x, ties[0].n_hits) if ties else (-1, 0)
+            except Exception:
+                r = None
+            if len(out) < len(spans):
+                out.append(r)
+            done += 1
+            if time.perf_counter() - t0 > budget_s:
+                return done, time.perf_counter() - t0, out
+        if not cycle:
             break
-    return len(out), time.perf_counter() - t0, out
+    return done, time.perf_counter() - t0, out

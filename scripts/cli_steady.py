@@ -68,7 +68,8 @@ def quota():
         return None
 
 
-def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False):
+def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False, by_path=False):
+    """One CLI process on `bam` (piped on stdin; by_path: given as the input path) -> its record."""
     env = dict(os.environ)
     if timing:
         env["FC2_CALLER_TIMING"] = "1"
@@ -80,10 +81,11 @@ def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False):
     cmd = [sys.executable, "-m", "find_circ2_amd.cli", "-G", fa, "-o", out, "-q"] + list(extra)
     err = open(out + ".stderr", "wb")
     t0 = time.time()
-    feeder = subprocess.Popen(["cat", bam], stdout=subprocess.PIPE)
-    p = subprocess.Popen(cmd, cwd=ROOT, stdin=feeder.stdout, stderr=err, env=env,
-                         preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None)
-    feeder.stdout.close()
+    feeder = None if by_path else subprocess.Popen(["cat", bam], stdout=subprocess.PIPE)
+    p = subprocess.Popen(cmd + ([bam] if by_path else []), cwd=ROOT, stdin=feeder.stdout if feeder else None,
+                         stderr=err, env=env, preexec_fn=(lambda: os.sched_setaffinity(0, cpus)) if cpus else None)
+    if feeder:
+        feeder.stdout.close()
     while True:                             # a heartbeat on stderr (a long run is not a hung one)
         try:
             rc = p.wait(timeout=30)
@@ -94,7 +96,8 @@ def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False):
                 raise
             log("  ... %s running %.0f s" % (os.path.basename(out), time.time() - t0))
     wall = time.time() - t0
-    feeder.wait()
+    if feeder:
+        feeder.wait()
     err.close()
     if rc != 0:
         raise RuntimeError("cli exit status %d: %s" % (rc, open(out + ".stderr").read()[-2000:]))
@@ -142,6 +145,44 @@ def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False):
     }
 
 
+def prepare(d, sizes, keep_sam=False, keep_sam_sizes=()):
+    """genome.fa + reads_<n>.bam for every size in d (scripts/gen_reads for the largest, the smaller
+    ones its first reads); returns (fasta, {n: bam}, {n: sam kept}, timings).  SAM files are deleted
+    after conversion unless keep_sam (the largest) or n in keep_sam_sizes."""
+    from find_circ2_amd import sq_table
+    from find_circ2_amd.ingest import sam_to_bam
+    gen = os.path.join(ROOT, "scripts", "gen_reads")
+    if not os.path.exists(gen):
+        subprocess.check_call(["gcc", "-O2", "-o", gen, gen + ".c"])
+    info = {}
+    names, lens = sq_table(os.path.join(ROOT, "tests", "golden", "test_norm.sam"))
+    sq = os.path.join(d, "sq.tsv")
+    open(sq, "w").write("".join("%s\t%d\n" % x for x in zip(names, lens)))
+    fa, big = os.path.join(d, "genome.fa"), os.path.join(d, "reads_%d.sam" % max(sizes))
+    t0 = time.time()
+    subprocess.check_call([gen, sq, str(max(sizes)), "2024", fa, big])
+    info["gen_s"] = round(time.time() - t0, 1)
+    log("generated", max(sizes), "reads in", info["gen_s"], "s")
+    bams, sams = {}, {}
+    for n in sorted(sizes):
+        sam = big if n == max(sizes) else os.path.join(d, "reads_%d.sam" % n)
+        if sam != big:
+            cut_sam(big, sam, n)
+        bam = os.path.join(d, "reads_%d.bam" % n)
+        t0 = time.time()
+        sam_to_bam(sam, bam)
+        info["bam_%d" % n] = {"bytes": os.path.getsize(bam), "convert_s": round(time.time() - t0, 1)}
+        if (sam == big and keep_sam) or n in keep_sam_sizes:
+            sams[n] = sam
+        elif sam != big:
+            os.remove(sam)
+        bams[n] = bam
+        log("bam", n, info["bam_%d" % n])
+    if max(sizes) not in sams:
+        os.remove(big)
+    return fa, bams, sams, info
+
+
 def outputs(out):
     files = {}
     for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
@@ -165,36 +206,12 @@ def main():
     import tempfile
     d = a.out or tempfile.mkdtemp(prefix="fc2_steady_", dir="/tmp")
     os.makedirs(d, exist_ok=True)
-    gen = os.path.join(ROOT, "scripts", "gen_reads")
-    if not os.path.exists(gen):
-        subprocess.check_call(["gcc", "-O2", "-o", gen, gen + ".c"])
-    from find_circ2_amd import sq_table
-    from find_circ2_amd.ingest import sam_to_bam
     res = {"cpus_visible": len(os.sched_getaffinity(0)), "cgroup_cpu_quota": quota(), "sizes": sizes,
            "cpu_model": next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")),
                              None)}
     try:
-        names, lens = sq_table(os.path.join(ROOT, "tests", "golden", "test_norm.sam"))
-        sq = os.path.join(d, "sq.tsv")
-        open(sq, "w").write("".join("%s\t%d\n" % x for x in zip(names, lens)))
-        fa, big = os.path.join(d, "genome.fa"), os.path.join(d, "reads_%d.sam" % max(sizes))
-        t0 = time.time()
-        subprocess.check_call([gen, sq, str(max(sizes)), "2024", fa, big])
-        res["gen_s"] = round(time.time() - t0, 1)
-        log("generated", max(sizes), "reads in", res["gen_s"], "s")
-        bams = {}
-        for n in sorted(sizes):
-            sam = big if n == max(sizes) else os.path.join(d, "reads_%d.sam" % n)
-            if sam != big:
-                cut_sam(big, sam, n)
-            bam = os.path.join(d, "reads_%d.bam" % n)
-            t0 = time.time()
-            sam_to_bam(sam, bam)
-            res["bam_%d" % n] = {"bytes": os.path.getsize(bam), "convert_s": round(time.time() - t0, 1)}
-            if sam != big or not a.check:
-                os.remove(sam)
-            bams[n] = bam
-            log("bam", n, res["bam_%d" % n])
+        fa, bams, _, info = prepare(d, sizes, keep_sam=a.check)
+        res.update(info)
         run_cli(fa, bams[min(sizes)], os.path.join(d, "warm"), 0)       # builds genome.fa.byo_index
         runs = []
         for n in sorted(sizes):
