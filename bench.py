@@ -1237,7 +1237,15 @@ def main():
         print("warning: --gpus %d but WORLD_SIZE %d" % (args.gpus, ws), file=sys.stderr)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    # wall seconds per leg of this rank (DESIGN.md §6 bounds the driver's N = 8 run from them)
+    legs, t_leg = {}, [time.time()]
+
+    def mark(name):
+        now = time.time()
+        legs[name] = round(now - t_leg[0], 2)
+        t_leg[0] = now
     opt, g, b = build_workload(args, rank, dev)
+    mark("workload")
     # the headline scan writes each pair's result as the 2-byte compact word (canonical mode; escapes
     # for results that do not fit, none on this workload): 2.2 % faster than 8-byte words in a
     # same-process A/B (profiles/r04/ab_compact_headline.jsonl), checked word for word after timing
@@ -1245,6 +1253,7 @@ def main():
     elapsed, kernel_ms, out = timed_scans(opt, g, b, args.steps, args.warmup, ws, dev, compact_width=cw)
     elapsed = max_over_ranks(elapsed, ws, dev)
     kernel_ms = max_over_ranks(kernel_ms, ws, dev)
+    mark("timed_scans")
     total_pairs = b.n * args.steps * ws
     value = total_pairs / elapsed
     bpp = algo_bytes_per_pair(args.read_len, opt.asize, opt.margin, result_bytes=cw or 8)
@@ -1272,6 +1281,7 @@ def main():
     c4 = None
     if args.workload == "hg19" and not args.no_config4 and (args.config4_pairs or not args.pairs):
         c4 = configs4(opt, g, ws, rank, dev, args.steps, args.warmup, total=args.config4_pairs or 200_000_000)
+        mark("configs4")
     # configs[3]: rank 0's stream strong-scaled over the ranks with the host-side ordered merge
     strong = None
     if not args.no_strong:
@@ -1280,6 +1290,7 @@ def main():
                                 ws, rank, dev, args.steps, args.warmup, n0, kw0, per_rank=args.strong_batches or max(2, 8 // ws),
                                 tail=args.strong_tail if args.strong_tail >= 0 else STRONG_TAIL)
         torch.cuda.empty_cache()
+        mark("strong_scaling")
     line = {
         "metric": METRIC,
         "value": round(value, 1),
@@ -1318,6 +1329,7 @@ def main():
         line["roofline"]["traffic_ratio"] = round(traffic / (bpp * b.n), 3)
     if args.workload == "hg19" and not args.locus_ordered and b.n == 50_000_000:
         pc = pattern_ceiling(opt, g, b, dev)
+        mark("pattern_ceiling")
         line["roofline"]["access_pattern_ceiling"] = pc
         if pc:
             # flat copies (the driver's record keeps a line's scalar fields only): the frac this read-order
@@ -1329,6 +1341,7 @@ def main():
             line["roofline"]["scan_frac_of_ceiling"] = pc["scan_frac_of_ceiling"]
     if rank == 0 and ws == 1 and not args.no_cpu_baseline:
         cb = cpu_baselines(opt, g, b, args.cpu_seconds)
+        mark("cpu_baselines")
         line["cpu_baseline"] = cb["main"]
         line["cpu_baseline_extra"] = {"python_1core": cb["python_1core"], "python_pool": cb["python_pool"],
                                       "c_naive_1core": cb["c_naive"], "c_fast_allcores": cb["c_fast"],
@@ -1391,9 +1404,12 @@ def main():
                     "priced at 150 bp (%d B) and at the batch's mean read_part length" % bpp4}
         del b4, g4
         torch.cuda.empty_cache()
+        mark("extras")
         if not args.no_cli:
             line["extra"]["cli_end_to_end"] = cli_end_to_end()
+            mark("cli")
     if rank == 0:
+        line["legs_s"] = legs
         print(json.dumps(line), flush=True)
     if ws > 1:
         import torch.distributed as dist
