@@ -20,7 +20,7 @@ import sys
 import time
 import traceback
 
-from .cliopts import USAGE, build_parser  # noqa: F401  (cli.build_parser: the tests' entry)
+from .cliopts import USAGE, apply_threads, build_parser  # noqa: F401  (cli.build_parser: the tests' entry)
 
 __version__ = "1.99"
 
@@ -59,6 +59,7 @@ def main(argv=None, evaluator_factory=None) -> int:
     startup = {"before_main_s": process_age()}
     parser = build_parser()
     options, args = parser.parse_args(argv)
+    apply_threads(options)
     if options.version:
         print("find_circ.py version {0}\n\n(c) Marvin Jens 2012-2016.\nCheck http://www.circbase.org for more "
               "information.\n(MI355X breakpoint search: find_circ2_amd)".format(__version__))
@@ -92,7 +93,8 @@ def main(argv=None, evaluator_factory=None) -> int:
     # as the Python-2 reference writes them
     out = {"circs": open(os.path.join(options.output, "circ_splice_sites.bed"), "w", encoding="latin-1"),
            "lins": open(os.path.join(options.output, "lin_splice_sites.bed"), "w", encoding="latin-1"),
-           "reads": ParallelGzipWriter(os.path.join(options.output, "spliced_reads.fastq.gz")),
+           "reads": ParallelGzipWriter(os.path.join(options.output, "spliced_reads.fastq.gz"),
+                                       threads=min(8, options.threads) if options.threads > 0 else 0),
            "multi": open(os.path.join(options.output, "multi_events.tsv"), "w", encoding="latin-1"),
            "test": open(os.path.join(options.output, "test_results.tsv"), "w", encoding="latin-1")
            if options.test else None}

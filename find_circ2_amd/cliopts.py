@@ -50,8 +50,24 @@ def build_parser(parser_class=optparse.OptionParser) -> optparse.OptionParser:
     a("", "--gpus", dest="gpus", type=int, default=1,
       help="spread the breakpoint search over this many GPUs from --device on (chunks dealt round-robin, "
            "results merged in input order; more GPUs than present share devices round-robin)")
+    a("", "--threads", dest="threads", type=int, default=0,
+      help="host worker threads of each native stage (BGZF inflate (at most 8), SAM/BAM parse, pair formation, "
+           "recording, gzip of the reads file, genome pack); 0: sized from the machine (find_circ2_amd extension)")
     a("", "--python-ingest", dest="python_ingest", default=False, action="store_true",
       help="parse and group alignments in Python instead of the native ingest (implies --python-caller)")
     a("", "--python-caller", dest="python_caller", default=False, action="store_true",
       help="run record_hits and the junction tables in Python (find_circ2_amd.caller) instead of the native caller")
     return p
+
+
+THREAD_ENV = ("FC2_PARSE_THREADS", "FC2_INGEST_THREADS", "FC2_NEXT_THREADS", "FC2_CALLER_THREADS", "OMP_NUM_THREADS")
+
+
+def apply_threads(options) -> None:
+    """--threads N: every native pool sized N, through the variables the library reads when a pool is
+    first built -- so before any native call of the process."""
+    import os
+    n = int(getattr(options, "threads", 0) or 0)
+    if n > 0:
+        for k in THREAD_ENV:
+            os.environ[k] = str(n)

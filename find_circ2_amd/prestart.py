@@ -19,7 +19,7 @@ import threading
 import time
 
 from ._libpath import LIB_PATH
-from .cliopts import build_parser
+from .cliopts import apply_threads, build_parser
 
 FC2_OK = 0
 FC2_E_IO = -5
@@ -227,6 +227,7 @@ def start(argv) -> None:
     if (options.version or options.system or not options.genome or options.python_ingest
             or options.python_caller):
         return
+    apply_threads(options)
     try:
         device_index(options.device)
     except ValueError:

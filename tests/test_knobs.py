@@ -108,3 +108,14 @@ def test_stress_corner_equals_python_loop(bam_input, tmp_path, extra):
     o2 = str(tmp_path / "stress")
     _run(fa, bam, o2, STRESS, extra)
     same(o1, o2)
+
+
+def test_threads_option_sizes_the_pools(bam_input, default_out, tmp_path):
+    """--threads N (cliopts.apply_threads) sizes every native pool through the knobs above: the recording
+    side's phase A runs on at most N ranges, and the files are the default run's."""
+    fa, sam, bam = bam_input
+    o = str(tmp_path / "o")
+    r = _run(fa, bam, o, {"FC2_CALLER_TIMING": "1"}, extra=["--threads", "3"])
+    same(default_out, o)
+    ts = [int(x) for x in re.findall(rb"submit nf=\d+ T=(\d+)", r.stderr)]
+    assert ts and max(ts) <= 3
