@@ -19,7 +19,9 @@ With --check the largest size also runs through the Python read loop (--python-c
 search) and every output file must be byte-identical.  One JSON line on stdout; progress on stderr.
 
 usage: python scripts/cli_steady.py [--sizes 2000000,20000000] [--threads 4,8,16,32] [--reps 1]
-                                    [--check] [--out DIR] [--keep]
+                                    [--check] [--out DIR] [--keep] [--sites K]
+--sites K: the spliced reads cross K planted junctions (many reads per junction, as in a real
+library) instead of one junction each (the junction tables then stay small).
 Each run's record is printed as its own JSON line as soon as it is done; the summary comes last.
 """
 import argparse
@@ -145,7 +147,7 @@ def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False, by_path=
     }
 
 
-def prepare(d, sizes, keep_sam=False, keep_sam_sizes=()):
+def prepare(d, sizes, keep_sam=False, keep_sam_sizes=(), sites=0):
     """genome.fa + reads_<n>.bam for every size in d (scripts/gen_reads for the largest, the smaller
     ones its first reads); returns (fasta, {n: bam}, {n: sam kept}, timings).  SAM files are deleted
     after conversion unless keep_sam (the largest) or n in keep_sam_sizes."""
@@ -160,7 +162,7 @@ def prepare(d, sizes, keep_sam=False, keep_sam_sizes=()):
     open(sq, "w").write("".join("%s\t%d\n" % x for x in zip(names, lens)))
     fa, big = os.path.join(d, "genome.fa"), os.path.join(d, "reads_%d.sam" % max(sizes))
     t0 = time.time()
-    subprocess.check_call([gen, sq, str(max(sizes)), "2024", fa, big])
+    subprocess.check_call([gen, sq, str(max(sizes)), "2024", fa, big] + ([str(sites)] if sites else []))
     info["gen_s"] = round(time.time() - t0, 1)
     log("generated", max(sizes), "reads in", info["gen_s"], "s")
     bams, sams = {}, {}
@@ -200,6 +202,8 @@ def main():
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--out", default="")
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--sites", type=int, default=0,
+                    help="junction sites the spliced reads cross (scripts/gen_reads.c); 0: one per read")
     a = ap.parse_args()
     sizes = [int(x) for x in a.sizes.split(",")]
     threads = [int(x) for x in a.threads.split(",") if x.strip() and x != "none"]
@@ -210,7 +214,8 @@ def main():
            "cpu_model": next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")),
                              None)}
     try:
-        fa, bams, _, info = prepare(d, sizes, keep_sam=a.check)
+        fa, bams, _, info = prepare(d, sizes, keep_sam=a.check, sites=a.sites)
+        res["sites"] = a.sites
         res.update(info)
         run_cli(fa, bams[min(sizes)], os.path.join(d, "warm"), 0)       # builds genome.fa.byo_index
         runs = []

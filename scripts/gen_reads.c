@@ -10,8 +10,12 @@
  * plus a hard-clipped supplementary ((kA)H(L-kA)M).  Seeded (splitmix64): the same arguments give the
  * same files.  Test/measurement infrastructure, not part of the product.
  *
- * usage: gen_reads SQ_TABLE N_READS SEED OUT.fa OUT.sam
+ * usage: gen_reads SQ_TABLE N_READS SEED OUT.fa OUT.sam [SITES]
  *        SQ_TABLE: one "name<TAB>length" line per chromosome
+ *        SITES: 0 (default) plants a junction of its own for every spliced read (every junction is
+ *        supported by one read: the junction tables grow with the input); K > 0 plants K junctions
+ *        (half backsplice, half linear) and every spliced read crosses one of them, drawn uniformly,
+ *        with its own anchor length (junctions supported by many reads, as in real libraries)
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -56,10 +60,11 @@ static void putu(uint64_t v) {
 }
 
 int main(int argc, char **argv) {
-    if (argc != 6) {
-        fprintf(stderr, "usage: %s SQ_TABLE N_READS SEED OUT.fa OUT.sam\n", argv[0]);
+    if (argc != 6 && argc != 7) {
+        fprintf(stderr, "usage: %s SQ_TABLE N_READS SEED OUT.fa OUT.sam [SITES]\n", argv[0]);
         return 2;
     }
+    const uint64_t n_sites = argc == 7 ? strtoull(argv[6], NULL, 10) : 0;
     FILE *t = fopen(argv[1], "r");
     if (!t) { perror(argv[1]); return 1; }
     int nc = 0;
@@ -109,6 +114,36 @@ int main(int argc, char **argv) {
         putc_('\n');
     }
     enum { L = 100 };
+    /* SITES > 0: the junction sites, planted up front (anchor lengths are drawn per read) */
+    typedef struct { int c, back, minus; int64_t lo, hi; } Site;   /* back: E = hi, S = lo; linear: D = lo, D + span = hi */
+    Site *sites = NULL;
+    if (n_sites) {
+        sites = (Site *)malloc(sizeof(Site) * n_sites);
+        for (uint64_t k = 0; k < n_sites; ++k) {
+            const double x = unif() * tot;
+            int lo = 0, hi = nb - 1;
+            while (lo < hi) { const int m = (lo + hi) / 2; if (cum[m] <= x) lo = m + 1; else hi = m; }
+            Site st;
+            st.c = big[lo];
+            unsigned char *g = seq[st.c];
+            const int64_t G = lens[st.c];
+            const int64_t span = range(200, 20000);
+            st.back = k % 2 == 0;
+            st.minus = unif() < 0.5;
+            if (st.back) {                      /* reads take A = G[E-kA:E], B = G[S:S+kB], kA, kB < L */
+                st.hi = range(span + L + 10, G - L - 10);
+                st.lo = st.hi - span;
+                memcpy(g + st.hi, st.minus ? "CT" : "GT", 2);
+                memcpy(g + st.lo - 2, st.minus ? "AC" : "AG", 2);
+            } else {                            /* A = G[D-kA:D], B = G[D+span:D+span+kB] */
+                st.lo = range(L + 10, G - span - L - 10);
+                st.hi = st.lo + span;
+                memcpy(g + st.lo, st.minus ? "CT" : "GT", 2);
+                memcpy(g + st.hi - 2, st.minus ? "AC" : "AG", 2);
+            }
+            sites[k] = st;
+        }
+    }
     char qual[L + 1];
     memset(qual, 'I', L);
     qual[L] = 0;
@@ -132,6 +167,18 @@ int main(int argc, char **argv) {
         const int64_t span = range(200, 20000);
         const int minus = unif() < 0.5;
         int64_t a_pos, b_pos;
+        int cr = c;                             /* the read's chromosome */
+        if (n_sites) {                          /* a read across one of the planted junctions */
+            const Site *st = &sites[below(n_sites)];
+            cr = st->c;
+            g = seq[cr];
+            if (st->back) { a_pos = st->hi - kA; b_pos = st->lo; }
+            else { a_pos = st->lo - kA; b_pos = st->hi; }
+            memcpy(read, g + a_pos, (size_t)kA);
+            memcpy(read + kA, g + b_pos, (size_t)(L - kA));
+            (void)span; (void)minus;
+            goto emit;
+        }
         if (kind < 0.8) {                       /* backsplice: A = G[E-kA:E], B = G[S:S+kB] */
             const int64_t E = range(span + kA + 10, G - 10);
             const int64_t Sx = E - span;
@@ -148,17 +195,18 @@ int main(int argc, char **argv) {
         }
         memcpy(read, g + a_pos, (size_t)kA);
         memcpy(read + kA, g + b_pos, (size_t)(L - kA));
+    emit:
         if (unif() < 0.3) {
             const int k = (int)below(L);
             const char *q = memchr("ACGT", read[k], 4);
             if (q) read[k] = acgt[(q - "ACGT" + 1) % 4];
         }
         const uint64_t xs = below(12);
-        putc_('s'); putu(i); puts_("\t0\t"); puts_(names[c]); putc_('\t'); putu((uint64_t)a_pos + 1);
+        putc_('s'); putu(i); puts_("\t0\t"); puts_(names[cr]); putc_('\t'); putu((uint64_t)a_pos + 1);
         puts_("\t60\t"); putu((uint64_t)kA); putc_('M'); putu((uint64_t)(L - kA)); puts_("S\t*\t0\t0\t");
         put(read, L); putc_('\t'); puts_(qual); puts_("\tAS:i:"); putu((uint64_t)kA); puts_("\tXS:i:"); putu(xs);
         putc_('\n');
-        putc_('s'); putu(i); puts_("\t2048\t"); puts_(names[c]); putc_('\t'); putu((uint64_t)b_pos + 1);
+        putc_('s'); putu(i); puts_("\t2048\t"); puts_(names[cr]); putc_('\t'); putu((uint64_t)b_pos + 1);
         puts_("\t60\t"); putu((uint64_t)kA); putc_('H'); putu((uint64_t)(L - kA)); puts_("M\t*\t0\t0\t");
         put(read + kA, (size_t)(L - kA)); puts_("\t*\tAS:i:"); putu((uint64_t)(L - kA)); putc_('\n');
     }
