@@ -11,6 +11,8 @@
 #   bash scripts/gpu_run.sh rocprof [NAME]        rocprofv3 --kernel-trace --stats of the headline bench
 #   bash scripts/gpu_run.sh pmc                   the HBM PMC passes of scripts/profile_round.sh
 #   bash scripts/gpu_run.sh py SCRIPT [ARGS...]   any probe script under scripts/ (one process)
+#   bash scripts/gpu_run.sh steady [ARGS...]      scripts/cli_steady.py (the CLI in anchor pairs/s, thread curve)
+#   bash scripts/gpu_run.sh cliprof [N] [SITES]   rocprofv3 --kernel-trace --stats of the CLI on N reads
 # Outputs land in gpurun_out/ (copy what should be kept into profiles/<round>/).  Every GPU step has
 # its own time limit and the steps are chained with &&: a failure ends the call.
 set -o pipefail
@@ -57,6 +59,12 @@ case $cmd in
     timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_kt/$NAME -o kt --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-extra --no-strong --no-config4 > $R/gpurun_out/prof_kt/$NAME.out 2>&1 && echo PROF_OK ;;
   pmc)
     bash scripts/profile_round.sh ;;
+  steady)
+    timeout -k 10 1000 python -u scripts/cli_steady.py "$@" > gpurun_out/steady.jsonl 2> gpurun_out/steady.err && echo STEADY_OK ;;
+  cliprof)
+    N=${1:-20000000}; S=${2:-0}
+    mkdir -p gpurun_out/prof_cli && export TMPDIR=/tmp && cd /tmp &&
+    timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_cli/cli_$N -o kt --output-format csv -- python3 $R/scripts/prof/cli_kernels.py $N $S > $R/gpurun_out/prof_cli/cli_$N.out 2>&1 && echo CLIPROF_OK ;;
   py)
     s=$1; shift
     timeout -k 10 900 python -u "$s" "$@" > gpurun_out/py_$(basename $s .py).out 2>&1 && echo PY_OK ;;
