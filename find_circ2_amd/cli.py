@@ -370,9 +370,11 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
             genome_eval.close()
             genome.close()
         if startup is not None and "read_loop_s" in startup:
+            import resource
             logger.info("process shutdown: reads_gz_finish_s=%.3f, caller_close_s=%.3f, files_close_s=%.3f, "
-                        "device_release_s=%.3f, process_age_s=%.3f"
-                        % (t_fin - t_close, t_files - t_fin, t_ctx - t_files, time.time() - t_ctx, process_age()))
+                        "device_release_s=%.3f, process_age_s=%.3f, max_rss_gb=%.2f"
+                        % (t_fin - t_close, t_files - t_fin, t_ctx - t_files, time.time() - t_ctx, process_age(),
+                           resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1048576.))
     return 0
 
 
