@@ -89,7 +89,7 @@ def parse():
     ap.add_argument("--config4-pairs", type=int, default=0, help="configs[4] stream length (default 200M; tests)")
     ap.add_argument("--no-cli", action="store_true", help="skip the end-to-end CLI extra (2M reads, BAM on stdin)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget per CPU baseline leg")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r05.json"))
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_r06.json"))
     return ap.parse_args()
 
 

@@ -78,6 +78,19 @@ def kstats(prof, name, kernel=None):
     return None, 0, None
 
 
+def compact_ns(prof, name, keep):
+    """Mean duration of the scan dispatches with the given ordinals (the 2-B compact launches) in the
+    kernel trace: the launches the bench line's kernel_ms times, without the 8-B reference scans."""
+    t = os.path.join(prof, name, "kt_kernel_trace.csv")
+    if not keep or not os.path.exists(t):
+        return None
+    rows = sorted((r for r in csv.DictReader(open(t)) if KERN in r["Kernel_Name"] and int(r["Grid_Size_X"]) >= N_PAIRS),
+                  key=lambda r: int(r["Dispatch_Id"]))
+    ns = [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rows]
+    sel = [ns[i] for i in keep if i < len(ns)]
+    return sum(sel) / len(sel) if sel else None
+
+
 def main():
     rnd = sys.argv[1] if len(sys.argv) > 1 else "r01"
     prof = os.path.join(ROOT, "gpurun_out", "prof")
@@ -94,6 +107,7 @@ def main():
         hbm = 2 * f["FETCH_SIZE"] * 1024 + wr.get("WRITE_SIZE", 0) * 1024
         out[key] = {"pairs_per_launch": N_PAIRS, "kernel": kname,
                     "avg_kernel_ns_rocprof": ns,
+                    "avg_kernel_ns_rocprof_compact_launches": compact_ns(prof, "kt_" + w, COMPACT.get(w)),
                     "FETCH_SIZE_kB_raw": f["FETCH_SIZE"], "WRITE_SIZE_kB": wr.get("WRITE_SIZE"),
                     "TCC_HIT_sum": h.get("TCC_HIT_sum"), "TCC_MISS_sum": h.get("TCC_MISS_sum"),
                     "TCC_EA0_RDREQ_sum": rq.get("TCC_EA0_RDREQ_sum"), "TCC_REQ_sum": rq.get("TCC_REQ_sum"),
