@@ -439,27 +439,73 @@ class Arena {
 // A set of strings of which only the size is read (Hit.readnames / Hit.uniq): the first member
 // inline, a short vector up to 16, a hash set past that; members live in the Arena.
 struct StrSet {
-    std::string_view first;
+    // up to 16 members in `first` + `more`, past that an open-addressing table; every member is kept
+    // with its hash, so a lookup compares the strings themselves (in the Arena: a cache miss each) only
+    // where the hashes agree.  The table is linear-probed and at most 3/4 full: no allocation per
+    // member -- a junction that many reads support (a real library: tens to thousands of reads per
+    // junction) grows its table log2(n) times instead of allocating a node per read
+    struct Slot {
+        uint64_t h;                            // 0: empty (hashes are forced odd)
+        std::string_view s;
+    };
+    Slot first{0, {}};
     size_t n = 0;
-    std::vector<std::string_view> more;
-    std::unique_ptr<std::unordered_set<std::string_view>> big;
-    bool contains(std::string_view s) const {
-        if (big) return big->count(s) != 0;
-        if (n && first == s) return true;
-        for (const std::string_view &x : more)
-            if (x == s) return true;
+    std::vector<Slot> more;
+    std::unique_ptr<Slot[]> tab;
+    uint32_t cap = 0;                          // slots in tab, a power of two (0: no table yet)
+    static uint64_t hash(std::string_view s) { return (uint64_t)std::hash<std::string_view>()(s) | 1u; }
+    bool find(std::string_view s, uint64_t h, size_t &at) const {
+        for (size_t i = (size_t)(h >> 7) & (cap - 1);; i = (i + 1) & (cap - 1)) {
+            if (!tab[i].h) { at = i; return false; }
+            if (tab[i].h == h && tab[i].s == s) { at = i; return true; }
+        }
+    }
+    void place(const Slot &x) {
+        size_t at;
+        find(x.s, x.h, at);
+        tab[at] = x;
+    }
+    void grow(uint32_t to) {
+        std::unique_ptr<Slot[]> old(std::move(tab));
+        const uint32_t oc = cap;
+        tab.reset(new Slot[to]());
+        cap = to;
+        for (uint32_t k = 0; k < oc; ++k)
+            if (old[k].h) place(old[k]);
+    }
+    bool contains(std::string_view s, uint64_t h) const {
+        if (cap) {
+            size_t at;
+            return find(s, h, at);
+        }
+        if (n && first.h == h && first.s == s) return true;
+        for (const Slot &x : more)
+            if (x.h == h && x.s == s) return true;
         return false;
     }
+    bool contains(std::string_view s) const { return contains(s, hash(s)); }
     // true if s was new
     bool insert(std::string_view s, Arena &a) {
-        if (contains(s)) return false;
-        const std::string_view v = a.put(s);
-        if (big) { big->insert(v); ++n; return true; }
+        const uint64_t h = hash(s);
+        if (cap) {
+            size_t at;
+            if (find(s, h, at)) return false;
+            if (4 * (n + 1) > 3 * (size_t)cap) {
+                grow(2 * cap);
+                find(s, h, at);
+            }
+            tab[at] = Slot{h, a.put(s)};
+            ++n;
+            return true;
+        }
+        if (contains(s, h)) return false;
+        const Slot v{h, a.put(s)};
         if (!n) first = v;
         else more.push_back(v);
-        if (++n > 16) {
-            big.reset(new std::unordered_set<std::string_view>(more.begin(), more.end()));
-            big->insert(first);
+        if (++n > 16) {                         // to the table: 17 members in 64 slots
+            grow(64);
+            place(first);
+            for (const Slot &x : more) place(x);
             more.clear();
             more.shrink_to_fit();
         }

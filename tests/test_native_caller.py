@@ -15,7 +15,7 @@ import os
 import numpy as np
 import pytest
 
-from conftest import GOLDEN
+from conftest import GOLDEN, ROOT
 from find_circ2_amd import cli
 from oracle_engine import oracle_evaluator_factory
 from bwa_emul import read_fasta
@@ -736,3 +736,25 @@ def test_rows_release_the_read_side(tmp_path):
         assert sorted(rows(o1)) == sorted(rows(o2))
     nat = [l for l in open(os.path.join(o2, "circ_splice_sites.bed"), "rb") if not l.startswith(b"#")]
     assert sorted(circ.splitlines(True)) == sorted(nat)
+
+
+def test_native_caller_many_reads_per_junction(tmp_path):
+    """Junctions supported by hundreds of reads (scripts/gen_reads with a junction-site pool: 20 sites,
+    20k reads, repeated read sequences among a junction's reads): the per-junction read-name and
+    uniq-read sets (fc2_caller.cpp StrSet, past 16 members an open-addressing table) give n_frags and
+    n_uniq -- the files equal the Python loop's."""
+    import subprocess
+    gen = os.path.join(ROOT, "scripts", "gen_reads")
+    if not os.path.exists(gen):
+        subprocess.check_call(["gcc", "-O2", "-o", gen, gen + ".c"])
+    sq = tmp_path / "sq.tsv"
+    sq.write_text("chrA\t300000\nchrB\t450000\nchrC\t250000\n")
+    fa, sam = str(tmp_path / "g.fa"), str(tmp_path / "r.sam")
+    subprocess.check_call([gen, str(sq), "20000", "7", fa, sam, "20"])
+    o1, o2 = str(tmp_path / "py"), str(tmp_path / "nat")
+    assert cli.main(["-G", fa, "-o", o1, "-q", "--python-caller", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    assert cli.main(["-G", fa, "-o", o2, "-q", sam], evaluator_factory=oracle_evaluator_factory) == 0
+    same(o1, o2)
+    rows = [l.split("\t") for l in open(os.path.join(o2, "circ_splice_sites.bed")) if l[0] != "#"]
+    assert rows and max(int(r[4]) for r in rows) > 100          # n_frags: hundreds of reads per junction
+    assert any(int(r[8]) < int(r[4]) for r in rows)             # n_uniq < n_frags: repeated read sequences
