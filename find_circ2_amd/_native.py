@@ -153,9 +153,10 @@ EXPORTED = [
     # include/fc2_ingest.h
     "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
     "fc2_ingest_next", "fc2_ingest_counts_get", "fc2_ingest_set_bam_out", "fc2_ingest_close_bam_out",
-    "fc2_ingest_format", "fc2_sam_to_bam",
+    "fc2_ingest_format", "fc2_sam_to_bam", "fc2_bgzf_inflate_launch",
+    "fc2_ingest_set_gpu_inflate", "fc2_ingest_inflate_counts",
     # include/fc2_caller.h
-    "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
+    "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_inflate_counts", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
     "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_submit_long", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
     "fc2_caller_set_reads_gz", "fc2_caller_close_reads",
     # include/fc2_ctx.h
@@ -195,7 +196,8 @@ _lib = None
 
 def build(force: bool = False) -> str:
     srcdir = os.path.join(_HERE, "csrc")
-    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_reorder.hip", "fc2_scan32.h",
+    srcs = [os.path.join(srcdir, f) for f in ("fc2_kernels.hip", "fc2_scan32.hip", "fc2_reorder.hip", "fc2_inflate.hip",
+                                              "fc2_scan32.h",
                                               "fc2_host.cpp", "fc2_ingest.cpp", "fc2_ingest_impl.h", "fc2_caller.cpp",
                                               "fc2_bamout.cpp", "fc2_bamout.h", "fc2_ctx.cpp", "fc2_hostmem.h",
                                               "fc2_common.h", "Makefile")]
@@ -292,6 +294,10 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_rows": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
         "fc2_caller_counter": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(ctypes.c_double)]),
         "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),
+        "fc2_bgzf_inflate_launch": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
+        "fc2_ingest_set_gpu_inflate": (ctypes.c_int, [vp, ctypes.c_int]),
+        "fc2_ingest_inflate_counts": (ctypes.c_int, [vp, P(u64), P(u64)]),
+        "fc2_caller_inflate_counts": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_ctx_create": (ctypes.c_int, [ctypes.c_int, P(vp)]),
         "fc2_ctx_create_sibling": (ctypes.c_int, [vp, P(vp)]),
         "fc2_ctx_destroy": (None, [vp]),

@@ -277,6 +277,12 @@ def _devices(options):
     return ["cuda:%d" % ((first + k) % ndev) for k in range(options.gpus)]
 
 
+def _inflate_device(options):
+    """The GPU that inflates a BAM input's BGZF blocks: the first of the run's devices."""
+    from .ctxpipe import device_index
+    return device_index(options.device)
+
+
 def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path="",
                        genome_eval=None, startup=None) -> int:
     """The read loop in C++ (include/fc2_caller.h); only the breakpoint search is called from here."""
@@ -298,7 +304,8 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
     nc = NativeCaller(path, is_bam, options, names, fasta, write_reads=out.get("reads") is not None,
                       write_multi=out.get("multi") is not None, genome_dummy=dummy,
                       known_circ=options.known_circ, known_lin=options.known_lin, bam_out=bam_path,
-                      reads_gz=reads_gz)
+                      reads_gz=reads_gz,
+                      inflate_device=_inflate_device(options) if genome_eval is not None else None)
     try:
         try:
             n_kc, n_kl = nc.open()
@@ -348,6 +355,7 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
                            genome_load_s=getattr(evaluate, "genome_load_s", 0.0),
                            siblings_s=getattr(evaluate, "siblings_s", 0.0), read_loop_s=seconds,
                            genome_wait_s=getattr(evaluate, "wait_s", 0.0), tables_s=time.time() - t_rows)
+            startup.update(zip(("inflate_gpu_blocks", "inflate_cpu_blocks"), nc.inflate_counts()))
             logger.info("process phases: " + ", ".join("%s=%.3f" % kv for kv in startup.items()) +
                         ", process_age_s=%.3f, numpy_loaded=%d, torch_loaded=%d"
                         % (process_age(), "numpy" in sys.modules, "torch" in sys.modules))

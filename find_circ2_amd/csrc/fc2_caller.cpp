@@ -854,6 +854,7 @@ struct fc2_caller {
     std::vector<Chunk> spare;
     bool read_side_released = false;            // release_read_side ran (after the last chunk): the
     fc2_ingest_counts ing_final{};              // input is closed then, its final counts kept here
+    uint64_t inflate_final[2] = {0, 0};         // (and its GPU / CPU inflate counts)
     std::thread release_thr;                    // ... on this thread (joined by fc2_caller_close)
     std::mutex qmu;                             // guards queued and spare
     // fc2_caller_stats' values, published by fc2_caller_next on the thread that advances the input
@@ -2152,6 +2153,14 @@ extern "C" int fc2_caller_set_genome(fc2_caller *h, const int32_t *tid_to_chrom,
 
 extern "C" fc2_ingest *fc2_caller_ingest(fc2_caller *h) { return h ? h->ing : nullptr; }
 
+extern "C" int fc2_caller_inflate_counts(const fc2_caller *h, uint64_t *gpu_blocks, uint64_t *cpu_blocks) {
+    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_caller_inflate_counts: null argument");
+    if (!h->read_side_released) return fc2_ingest_inflate_counts(h->ing, gpu_blocks, cpu_blocks);
+    if (gpu_blocks) *gpu_blocks = h->inflate_final[0];
+    if (cpu_blocks) *cpu_blocks = h->inflate_final[1];
+    return FC2_OK;
+}
+
 // the input's counts: live, or as they were when the input was released (release_read_side)
 static void ingest_counts(const fc2_caller *h, fc2_ingest_counts *c) {
     if (h->read_side_released) *c = h->ing_final;
@@ -2699,6 +2708,7 @@ static void release_read_side(fc2_caller *h) {
         if (!h->queued.empty()) return;
     }
     fc2_ingest_counts_get(h->ing, &h->ing_final);
+    fc2_ingest_inflate_counts(h->ing, &h->inflate_final[0], &h->inflate_final[1]);
     h->read_side_released = true;
     struct Bag {
         std::vector<fc2_caller::Chunk> spare;

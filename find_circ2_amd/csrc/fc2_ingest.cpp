@@ -36,6 +36,7 @@
 #include "fc2_common.h"
 #include "fc2_cpuacct.h"
 #include "fc2_deflate.h"
+#include "fc2_inflate.h"
 #include "fc2_ingest_impl.h"
 
 using fc2::ing::Mate;
@@ -169,6 +170,18 @@ struct NoInitAlloc : std::allocator<T> {
     NoInitAlloc() = default;
     template <class U>
     NoInitAlloc(const NoInitAlloc<U> &) noexcept {}
+    // a GPU-inflated batch's buffer comes from the pinned pool (fc2_inflate.h), so the inflated bytes
+    // are downloaded straight into it; every other buffer, and any when the pool has none, from the heap
+    static constexpr size_t kPinnedMin = size_t(8) << 20;
+    T *allocate(size_t n) {
+        if (n * sizeof(T) >= kPinnedMin)
+            if (void *p = fc2::inf::pinned_take(n * sizeof(T))) return static_cast<T *>(p);
+        return std::allocator<T>::allocate(n);
+    }
+    void deallocate(T *p, size_t n) {
+        if (n * sizeof(T) >= kPinnedMin && fc2::inf::pinned_give(p)) return;
+        std::allocator<T>::deallocate(p, n);
+    }
     template <class U>
     void construct(U *p) noexcept {
         ::new (static_cast<void *>(p)) U;
@@ -198,21 +211,76 @@ int bgzf_threads() {
     return std::max(1, std::min(n, 8));
 }
 
+// BGZF blocks inflated on a GPU (fc2_ingest_set_gpu_inflate; fc2_inflate.hip): the device's stream
+// and buffers, made by the first batch that uses them (on the batch reader's thread, one batch at a
+// time); a block the GPU refused or whose CRC-32 does not match is inflated on the CPU as before
+struct GpuInflate {
+    int device = -1;
+    uint32_t max_blocks = 0;
+    fc2::inf::Gpu *g = nullptr;
+    bool failed = false;                       // the device could not be had or failed: CPU from then on
+    std::string err;
+    std::atomic<uint64_t> gpu_blocks{0}, cpu_blocks{0};
+    // FC2_CALLER_TIMING: the batch reader's time reading, submitting chunks, waiting for the device,
+    // inflating refused blocks; batches whose buffer was pinned (downloaded into directly)
+    int64_t read_ns = 0, add_ns = 0, wait_ns = 0, cpu_ns = 0;
+    int batches = 0, pinned = 0;
+    ~GpuInflate() {
+        if (getenv("FC2_CALLER_TIMING") && batches)
+            fprintf(stderr, "gpu inflate: %d batches (%d pinned), %llu blocks on the GPU, %llu on the CPU; reader s: "
+                    "read %.3f submit %.3f wait %.3f cpu %.3f\n", batches, pinned, (unsigned long long)gpu_blocks.load(),
+                    (unsigned long long)cpu_blocks.load(), (read_ns - add_ns) * 1e-9, add_ns * 1e-9, wait_ns * 1e-9,
+                    cpu_ns * 1e-9);
+        fc2::inf::gpu_close(g);
+    }
+};
+
+static int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+constexpr size_t kGpuChunk = 256;              // blocks per GPU chunk (16 MiB inflated)
+
 // reads up to `max_blocks` blocks (the first `pre` bytes of the first header are in `pre`)
-BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_threads) {
+BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_threads, std::shared_ptr<GpuInflate> gi) {
     BgzfBatch B;
     std::vector<uint8_t> raw;
     std::vector<size_t> boff, bsz;
     raw.swap(pre);
+    // the GPU inflates the batch in chunks as they are read (fc2_inflate.h), into the batch buffer
+    // itself -- a pinned one from the pool, made max_blocks * 64 KiB long up front
+    bool gpu = gi && !gi->failed && max_blocks <= (int)gi->max_blocks;
+    if (gpu && !gi->g) {                       // the device's buffers and the pinned pool, on first use
+        fc2::cpu::Scope acct(fc2::cpu::INFLATE);
+        gi->g = fc2::inf::gpu_open(gi->device, gi->max_blocks, kHead + (size_t)gi->max_blocks * 65536, gi->err);
+        if (!gi->g) gi->failed = true, gpu = false;
+    }
+    size_t submitted = 0;
+    auto submit = [&](bool last) {             // blocks read so far, in chunks of kGpuChunk
+        if (!gpu) return;
+        if (boff.size() - submitted < kGpuChunk && !(last && boff.size() > submitted)) return;
+        fc2::cpu::Scope acct(fc2::cpu::INFLATE);
+        const int64_t a0 = now_ns();
+        fc2::inf::gpu_add(gi->g, raw.data(), boff.data(), bsz.data(), submitted, boff.size());
+        gi->add_ns += now_ns() - a0;
+        submitted = boff.size();
+    };
+    const int64_t t0 = now_ns();
+    if (gpu) {
+        B.out.resize(kHead + (size_t)max_blocks * 65536);
+        fc2::inf::gpu_begin(gi->g, B.out.data() + kHead);
+        gi->batches += 1;
+        gi->pinned += fc2::inf::pinned_owns(B.out.data());
+    }
     size_t pos = 0;
     while ((int)boff.size() < max_blocks) {
         size_t got;
         if (raw.size() - pos < 18) {           // header
             const size_t have = raw.size() - pos;
             raw.resize(pos + 18);
-            if (!read_full(fd, raw.data() + pos + have, 18 - have, got)) { B.err = "read error"; return B; }
+            if (!read_full(fd, raw.data() + pos + have, 18 - have, got)) { B.err = "read error"; break; }
             if (have + got == 0) { raw.resize(pos); B.eof = true; break; }
-            if (have + got < 18) { B.err = "truncated BGZF block header"; return B; }
+            if (have + got < 18) { B.err = "truncated BGZF block header"; break; }
         }
         const size_t xlen = raw[pos + 10] | (raw[pos + 11] << 8);
         if (raw.size() - pos < 12 + xlen) {
@@ -220,21 +288,35 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
             raw.resize(pos + 12 + xlen);
             if (!read_full(fd, raw.data() + pos + have, 12 + xlen - have, got) || got < 12 + xlen - have) {
                 B.err = "truncated BGZF block header";
-                return B;
+                break;
             }
         }
         const size_t bs = bgzf_block_size(raw.data() + pos, raw.size() - pos);
-        if (bs < 12 + xlen + 8) { B.err = "not a BGZF block"; return B; }
+        if (bs < 12 + xlen + 8) { B.err = "not a BGZF block"; break; }
         const size_t have = raw.size() - pos;
         raw.resize(pos + bs);
         if (!read_full(fd, raw.data() + pos + have, bs - have, got) || got < bs - have) {
             B.err = "truncated BGZF block";
-            return B;
+            break;
         }
         boff.push_back(pos);
         bsz.push_back(bs);
         pos += bs;
+        submit(false);
     }
+    bool on_gpu = false;
+    int64_t t2 = 0;
+    if (gpu) {                                 // (after an error too: the device must be done with B.out)
+        submit(true);
+        const int64_t t1 = now_ns();
+        gi->read_ns += t1 - t0;
+        fc2::cpu::Scope acct(fc2::cpu::INFLATE);
+        on_gpu = fc2::inf::gpu_finish(gi->g, gi->err);
+        if (!on_gpu) gi->failed = true;        // (the CPU inflates every block of this batch and the next)
+        t2 = now_ns();
+        gi->wait_ns += t2 - t1;
+    }
+    if (!B.err.empty()) return B;
     const size_t nb = boff.size();
     std::vector<size_t> ooff(nb + 1, 0);
     for (size_t i = 0; i < nb; ++i) {
@@ -243,13 +325,19 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
     }
     B.n = ooff[nb];
     B.out.resize(kHead + B.n);
+    // the blocks the CPU inflates: all of them, or those the GPU refused
+    std::vector<uint32_t> todo;
+    todo.reserve(on_gpu ? 16 : nb);
+    for (size_t i = 0; i < nb; ++i)
+        if (!on_gpu || fc2::inf::gpu_status(gi->g, i) != 0) todo.push_back((uint32_t)i);
     std::atomic<size_t> next{0};
     std::atomic<bool> bad{false};
     auto work = [&]() {
         fc2::cpu::Scope acct(fc2::cpu::INFLATE);
         fc2::dfl::Inflater inf;                 // libdeflate (zlib without it): fc2_deflate.h
         if (!inf.ok()) { bad = true; return; }
-        for (size_t i; (i = next.fetch_add(1)) < nb && !bad;) {
+        for (size_t k; (k = next.fetch_add(1)) < todo.size() && !bad;) {
+            const size_t i = todo[k];
             const uint8_t *blk = raw.data() + boff[i];
             const size_t xl = blk[10] | (blk[11] << 8);
             char *dst = B.out.data() + kHead + ooff[i];
@@ -259,12 +347,17 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
             if (!inf.exact(blk + 12 + xl, bsz[i] - 12 - xl - 8, dst, n) || fc2::dfl::crc32(dst, n) != crc) bad = true;
         }
     };
-    const int nt = (int)std::min<size_t>((size_t)n_threads, std::max<size_t>(1, nb));
+    const int nt = (int)std::min<size_t>((size_t)n_threads, todo.size());
     std::vector<std::thread> pool;
     for (int t = 1; t < nt; ++t) pool.emplace_back(work);
-    work();
+    if (nt > 0) work();
     for (auto &t : pool) t.join();
     if (bad) B.err = "corrupt BGZF block";
+    if (gi) {
+        gi->gpu_blocks += nb - todo.size();
+        gi->cpu_blocks += todo.size();
+        if (gpu) gi->cpu_ns += now_ns() - t2;
+    }
     return B;
 }
 
@@ -296,6 +389,7 @@ struct fc2_ingest {
     int bgzf_nt = 1;
     int bgzf_blocks = 256;       // BGZF blocks per inflated batch (FC2_BGZF_BATCH: small in the tests)
     std::future<BgzfBatch> bgzf_next;
+    std::shared_ptr<GpuInflate> gpu_inflate;     // fc2_ingest_set_gpu_inflate (null: the CPU inflates)
     std::atomic<int64_t> inflate_wait_ns{0};     // the reader's wait for inflated BGZF batches (timing)
     std::string z_err;
     // header
@@ -462,7 +556,7 @@ bool ensure(fc2_ingest *h, size_t n) {
             if (!b.err.empty()) { h->z_err = b.err; h->z_done = true; return false; }
             if (b.eof) h->z_done = true;
             else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), h->bgzf_blocks,
-                                           h->bgzf_nt);
+                                           h->bgzf_nt, h->gpu_inflate);
             if (h->buf.size() < h->end + b.n) h->buf.resize(h->end + b.n);
             if (b.n) memcpy(h->buf.data() + h->end, b.data(), b.n);
             h->end += b.n;
@@ -1088,7 +1182,8 @@ void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         h->inflate_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
         if (!b.err.empty()) { h->z_err = b.err; h->z_done = true; return false; }
         if (b.eof) h->z_done = true;
-        else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), h->bgzf_blocks, h->bgzf_nt);
+        else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), h->bgzf_blocks, h->bgzf_nt,
+                                       h->gpu_inflate);
         const size_t L = end - beg;
         std::shared_ptr<CharBuf> nb;
         if (L <= kHead) {
@@ -1612,7 +1707,7 @@ extern "C" int fc2_ingest_open(const char *path, int is_bam, fc2_ingest **out) {
             if (const char *e = getenv("FC2_BGZF_BATCH"))
                 if (atoi(e) > 0) h->bgzf_blocks = std::min(atoi(e), 4096);
             h->bgzf_next = std::async(std::launch::async, bgzf_batch, fd, std::move(pre), std::min(16, h->bgzf_blocks),
-                                      h->bgzf_nt);
+                                      h->bgzf_nt, nullptr);
         } else {
             // any other gzip stream (gzip -c, concatenated members)
             h->src = fc2_ingest::SRC_GZIP;
@@ -1656,6 +1751,32 @@ extern "C" int fc2_ingest_format(const fc2_ingest *h, int *compression) {
         *compression = h->src == fc2_ingest::SRC_BGZF ? FC2_INGEST_BGZF
                      : h->src == fc2_ingest::SRC_GZIP ? FC2_INGEST_GZIP : FC2_INGEST_PLAIN;
     return h->bam ? FC2_INGEST_BAM : FC2_INGEST_SAM;
+}
+
+extern "C" int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device) {
+    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_gpu_inflate: null argument");
+    if (h->n_records) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_gpu_inflate: call before reading");
+    const char *e = getenv("FC2_GPU_INFLATE");
+    if (device < 0 || !h->bgzf || (e && atoi(e) == 0)) {
+        h->gpu_inflate.reset();
+        return FC2_OK;
+    }
+    auto gi = std::make_shared<GpuInflate>();
+    gi->device = device;
+    // batches of 1024 blocks (64 MiB inflated, four chunks of 256; fc2_inflate.hip); FC2_BGZF_BATCH
+    // still rules
+    if (!getenv("FC2_BGZF_BATCH")) h->bgzf_blocks = 1024;
+    gi->max_blocks = (uint32_t)h->bgzf_blocks;
+    h->gpu_inflate = gi;
+    return FC2_OK;
+}
+
+extern "C" int fc2_ingest_inflate_counts(const fc2_ingest *h, uint64_t *gpu_blocks, uint64_t *cpu_blocks) {
+    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_ingest_inflate_counts: null argument");
+    const GpuInflate *gi = h->gpu_inflate.get();
+    if (gpu_blocks) *gpu_blocks = gi ? gi->gpu_blocks.load() : 0;
+    if (cpu_blocks) *cpu_blocks = gi ? gi->cpu_blocks.load() : 0;
+    return FC2_OK;
 }
 
 extern "C" int fc2_ingest_set_bam_out(fc2_ingest *h, const char *path) {

@@ -53,6 +53,16 @@ class NativeIngest:
         """-B/--bam: anchor alignments to ``path`` (include/fc2_ingest.h)."""
         N.check(N.lib().fc2_ingest_set_bam_out(self.h, path.encode()))
 
+    def set_gpu_inflate(self, device: int):
+        """A BGZF input's blocks inflated on GPU ``device`` from the next batch on (include/fc2_ingest.h)."""
+        N.check(N.lib().fc2_ingest_set_gpu_inflate(self.h, int(device)))
+
+    def inflate_counts(self) -> Tuple[int, int]:
+        """(blocks inflated on the GPU, on the CPU) since set_gpu_inflate."""
+        g, c = ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(N.lib().fc2_ingest_inflate_counts(self.h, ctypes.byref(g), ctypes.byref(c)))
+        return int(g.value), int(c.value)
+
     def close_bam_out(self):
         N.check(N.lib().fc2_ingest_close_bam_out(self.h))
 

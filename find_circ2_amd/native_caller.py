@@ -72,7 +72,7 @@ class NativeCaller:
 
     def __init__(self, path: str, is_bam: bool, copts, genome_names, fasta_handle=None, write_reads=True,
                  write_multi=True, genome_dummy=False, known_circ: str = "", known_lin: str = "",
-                 bam_out: str = "", reads_gz=None):
+                 bam_out: str = "", reads_gz=None, inflate_device=None):
         o = copts
         # the strings must outlive the handle's open call (fc2_caller_open copies them)
         self._keep = [o.name.encode(), known_circ.encode() if known_circ else None,
@@ -91,6 +91,7 @@ class NativeCaller:
         self._is_bam = is_bam
         self.bam_out = bam_out
         self.reads_gz = reads_gz     # (path, level, threads, piece): spliced_reads.fastq.gz written natively
+        self.inflate_device = inflate_device   # a BGZF input's blocks inflated on this GPU (None: the CPU)
         self.opened = False
         self.format = None           # "sam" | "bam", detected from the bytes (open)
         self.loop_profile = {}       # seconds per stage of the last run (two-thread loop)
@@ -107,6 +108,8 @@ class NativeCaller:
         self.format = "bam" if L.fc2_ingest_format(ing, None) == 1 else "sam"      # FC2_INGEST_BAM
         if self.bam_out:
             N.check(L.fc2_ingest_set_bam_out(ing, self.bam_out.encode()))
+        if self.inflate_device is not None:
+            N.check(L.fc2_ingest_set_gpu_inflate(ing, int(self.inflate_device)))
         if self.reads_gz:
             path, level, threads, piece = self.reads_gz
             N.check(L.fc2_caller_set_reads_gz(self.h, path.encode(), int(level), int(threads), int(piece)))
@@ -128,6 +131,12 @@ class NativeCaller:
         """Finish spliced_alignments.bam (EOF block); raises on a write error."""
         if self.bam_out:
             N.check(N.lib().fc2_ingest_close_bam_out(N.lib().fc2_caller_ingest(self.h)))
+
+    def inflate_counts(self):
+        """(BGZF blocks inflated on the GPU, on the CPU) since the GPU inflate was set (0, 0 without)."""
+        g, c = ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(N.lib().fc2_caller_inflate_counts(self.h, ctypes.byref(g), ctypes.byref(c)))
+        return int(g.value), int(c.value)
 
     def stats(self):
         nr, npairs = ctypes.c_uint64(), ctypes.c_uint64()

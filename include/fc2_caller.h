@@ -69,6 +69,9 @@ int  fc2_caller_open(const char *path, int is_bam, const fc2_caller_opts *opts, 
 int  fc2_caller_set_genome(fc2_caller *h, const int32_t *tid_to_chrom, int32_t n_tid, const fc2_fasta *fasta,
                            uint64_t *n_known_circ, uint64_t *n_known_lin);
 fc2_ingest *fc2_caller_ingest(fc2_caller *h);    /* reference names, header (NULL after the rows, below) */
+/* BGZF blocks the input's GPU inflate took and left to the CPU (fc2_ingest_inflate_counts; kept
+ * after the input is released). */
+int fc2_caller_inflate_counts(const fc2_caller *h, uint64_t *gpu_blocks, uint64_t *cpu_blocks);
 void fc2_caller_close(fc2_caller *h);
 
 /* Read on until `chunksize` fragments carry pairs (or the input ends); *b = the pairs

@@ -86,6 +86,21 @@ int fc2_ingest_close_bam_out(fc2_ingest *h);
  * sam_parse1 does (the -B encoder above), BGZF blocks (zlib level 1, as samtools view -1) + EOF block.  Used to make BAM inputs for
  * tests and the bench's stdin-BAM CLI run. */
 int fc2_sam_to_bam(const char *sam_path, const char *bam_path);
+/* The BAM input's BGZF blocks inflated on GPU `device` (fc2_inflate.hip) instead of the CPU from the
+ * next batch on; call before reading (the CLI's read loop does, on its first device).  Batches grow to
+ * 1024 blocks (FC2_BGZF_BATCH still sets them); the host still checks every block's CRC-32 and ISIZE
+ * and inflates on the CPU any block the GPU refused or got wrong, and every block from then on if the
+ * device fails.  device < 0, a non-BGZF input or FC2_GPU_INFLATE=0: the CPU inflates (the default). */
+int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device);
+/* Blocks inflated on the GPU and on the CPU since fc2_ingest_set_gpu_inflate (0, 0 without it). */
+int fc2_ingest_inflate_counts(const fc2_ingest *h, uint64_t *gpu_blocks, uint64_t *cpu_blocks);
+/* BGZF blocks inflated on the GPU (fc2_inflate.hip; the BAM input's inflate, which pysam/htslib does for
+ * the reference, find_circ.py:461-469): n blocks, block i = len[i] bytes of raw DEFLATE at src + off[i]
+ * (device memory, readable 8 bytes past every payload: a BGZF block's trailer) holding isize[i] <= 65536
+ * bytes, inflated into dst + i * 65536 and, when crc is not NULL, checked against crc[i] (the gzip
+ * CRC-32); status[i] = 0, or why the block was refused (the host then inflates it on the CPU). */
+int fc2_bgzf_inflate_launch(const uint8_t *src, const uint32_t *off, const uint32_t *len, const uint32_t *isize,
+                            const uint32_t *crc, uint8_t *dst, uint32_t *status, uint32_t n, void *stream);
 #ifdef __cplusplus
 }
 #endif

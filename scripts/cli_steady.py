@@ -19,7 +19,7 @@ With --check the largest size also runs through the Python read loop (--python-c
 search) and every output file must be byte-identical.  One JSON line on stdout; progress on stderr.
 
 usage: python scripts/cli_steady.py [--sizes 2000000,20000000] [--threads 4,8,16,32] [--reps 1]
-                                    [--check] [--out DIR] [--keep] [--sites K]
+                                    [--check] [--out DIR] [--keep] [--sites K] [--variants K=V,...]
 --sites K: the spliced reads cross K planted junctions (many reads per junction, as in a real
 library) instead of one junction each (the junction tables then stay small).
 Each run's record is printed as its own JSON line as soon as it is done; the summary comes last.
@@ -70,9 +70,10 @@ def quota():
         return None
 
 
-def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False, by_path=False):
+def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False, by_path=False, env_extra=None):
     """One CLI process on `bam` (piped on stdin; by_path: given as the input path) -> its record."""
     env = dict(os.environ)
+    env.update(env_extra or {})
     if timing:
         env["FC2_CALLER_TIMING"] = "1"
     if threads:
@@ -142,6 +143,10 @@ def run_cli(fa, bam, out, threads, extra=(), timeout=900, timing=False, by_path=
         "loop_spans_per_s_after_genome": round(spans / net, 1) if net and net > 0 else None,
         "wall_reads_per_s": round(reads / wall, 1), "wall_spans_per_s": round(spans / wall, 1) if spans else None,
         "stages_s": stages, "cpu_s_per_stage": cpu_s, "phases_s": phases, "n_chunks": len(subs) or None,
+        "gpu_inflate": (re.search(r"gpu inflate: (.*)", errt) or [None, None])[1],
+        "upstream_ms": [round(sum(float(m[k]) for m in re.findall(
+            r"upstream: inflate wait ([0-9.]+), splitter blocked ([0-9.]+), parsers idle ([0-9.]+)", errt)), 1)
+            for k in range(3)],                 # inflate wait, splitter blocked, parsers idle (summed)
         "submit_phase_ms": {k: round(v, 1) for k, v in sub_ms.items()} or None,
         "next_phase_ms": {k: round(v, 1) for k, v in nxt.items()} or None,
     }
@@ -202,6 +207,9 @@ def main():
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--out", default="")
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--variants", default="",
+                    help="comma-separated K=V environment settings, each run as well as the default "
+                         "(e.g. FC2_GPU_INFLATE=0)")
     ap.add_argument("--sites", type=int, default=0,
                     help="junction sites the spliced reads cross (scripts/gen_reads.c); 0: one per read")
     a = ap.parse_args()
@@ -219,19 +227,22 @@ def main():
         res.update(info)
         run_cli(fa, bams[min(sizes)], os.path.join(d, "warm"), 0)       # builds genome.fa.byo_index
         runs = []
+        variants = [""] + [v for v in a.variants.split(",") if v]
         for n in sorted(sizes):
-            for t in [0] + threads:
+            for t, var in [(t, v) for t in [0] + threads for v in variants]:
                 # the clean runs (what a user gets), then one with FC2_CALLER_TIMING's per-stage CPU
                 # accounting (it also closes the caller at exit to print the totals)
                 for r in list(range(a.reps)) + ["timing"]:
-                    out = os.path.join(d, "o_%d_%d_%s" % (n, t, r))
-                    x = run_cli(fa, bams[n], out, t, timing=(r == "timing"))
+                    out = os.path.join(d, "o_%d_%d_%s%s" % (n, t, r, "_" + var.replace("=", "") if var else ""))
+                    x = run_cli(fa, bams[n], out, t, timing=(r == "timing"),
+                                env_extra=dict([var.split("=", 1)]) if var else None)
                     x["size"] = n
                     x["rep"] = r
+                    x["variant"] = var or "default"
                     runs.append(x)
                     print(json.dumps(x), flush=True)
-                    log("size %d threads %s rep %s: loop %.3f s, %.3g spans/s loop, %.3g spans/s wall, cpu %s" % (
-                        n, t or "default", r, x["loop_s"], x["loop_spans_per_s"] or 0, x["wall_spans_per_s"] or 0,
+                    log("size %d threads %s %s rep %s: loop %.3f s, %.3g spans/s loop, %.3g spans/s wall, cpu %s" % (
+                        n, t or "default", var, r, x["loop_s"], x["loop_spans_per_s"] or 0, x["wall_spans_per_s"] or 0,
                         x["cpu_s_per_stage"]))
                     if not a.keep and not (a.check and n == max(sizes) and t == 0 and r == 0):
                         shutil.rmtree(out, ignore_errors=True)

@@ -18,7 +18,7 @@ case $KIND in
 esac
 cd $ROOT/find_circ2_amd/csrc
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O1 -g -std=c++17 -fPIC -Wall -Wno-unused-result -I../../include $SAN \
-    -shared -o ../libfc2_$KIND.so fc2_kernels.hip fc2_scan32.hip fc2_reorder.hip fc2_host.cpp fc2_ingest.cpp \
+    -shared -o ../libfc2_$KIND.so fc2_kernels.hip fc2_scan32.hip fc2_reorder.hip fc2_inflate.hip fc2_host.cpp fc2_ingest.cpp \
     fc2_caller.cpp fc2_bamout.cpp fc2_ctx.cpp -lpthread -lz -ldl
 cd $ROOT
 shift || true
