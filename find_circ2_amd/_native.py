@@ -295,7 +295,7 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_counter": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(ctypes.c_double)]),
         "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_bgzf_inflate_launch": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
-        "fc2_ingest_set_gpu_inflate": (ctypes.c_int, [vp, ctypes.c_int]),
+        "fc2_ingest_set_gpu_inflate": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
         "fc2_ingest_inflate_counts": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_caller_inflate_counts": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_ctx_create": (ctypes.c_int, [ctypes.c_int, P(vp)]),

@@ -278,7 +278,10 @@ def _devices(options):
 
 
 def _inflate_device(options):
-    """The GPU that inflates a BAM input's BGZF blocks: the first of the run's devices."""
+    """The GPU that inflates a BAM input's BGZF blocks when FC2_GPU_INFLATE is 1 or 2 (the first of the
+    run's devices), else None: the CPU inflates them (the default; DESIGN.md "GPU inflate")."""
+    if os.environ.get("FC2_GPU_INFLATE", "0") not in ("1", "2"):
+        return None
     from .ctxpipe import device_index
     return device_index(options.device)
 

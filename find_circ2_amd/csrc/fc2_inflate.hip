@@ -619,6 +619,10 @@ Gpu *gpu_open(int device, uint32_t max_blocks, size_t pool_cap, std::string &err
     if (pool_cap) {              // the batches the parse blocks and the read loop's chunks still hold, and one in flight
         pool_open(pool_cap, 16);
         g->pooled = true;
+        void *first[3];                        // the first few made now (pinning takes ~10 ms each)
+        for (void *&b : first) b = pinned_take(pool_cap);
+        for (void *b : first)
+            if (b) pinned_give(b);
     }
     return g;
 }

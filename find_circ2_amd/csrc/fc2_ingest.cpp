@@ -218,6 +218,7 @@ struct GpuInflate {
     int device = -1;
     uint32_t max_blocks = 0;
     fc2::inf::Gpu *g = nullptr;
+    std::future<std::pair<fc2::inf::Gpu *, std::string>> opening;   // gpu_open, started by the set call
     bool failed = false;                       // the device could not be had or failed: CPU from then on
     std::string err;
     std::atomic<uint64_t> gpu_blocks{0}, cpu_blocks{0};
@@ -231,6 +232,7 @@ struct GpuInflate {
                     "read %.3f submit %.3f wait %.3f cpu %.3f\n", batches, pinned, (unsigned long long)gpu_blocks.load(),
                     (unsigned long long)cpu_blocks.load(), (read_ns - add_ns) * 1e-9, add_ns * 1e-9, wait_ns * 1e-9,
                     cpu_ns * 1e-9);
+        if (opening.valid()) g = opening.get().first;
         fc2::inf::gpu_close(g);
     }
 };
@@ -250,11 +252,15 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
     // the GPU inflates the batch in chunks as they are read (fc2_inflate.h), into the batch buffer
     // itself -- a pinned one from the pool, made max_blocks * 64 KiB long up front
     bool gpu = gi && !gi->failed && max_blocks <= (int)gi->max_blocks;
-    if (gpu && !gi->g) {                       // the device's buffers and the pinned pool, on first use
-        fc2::cpu::Scope acct(fc2::cpu::INFLATE);
-        gi->g = fc2::inf::gpu_open(gi->device, gi->max_blocks, kHead + (size_t)gi->max_blocks * 65536, gi->err);
-        if (!gi->g) gi->failed = true, gpu = false;
+    // the device's buffers and the pinned pool, made meanwhile: until they are ready (pinning the
+    // buffers takes a few hundred ms) the batches are inflated on the CPU
+    if (gpu && !gi->g && gi->opening.valid() &&
+        gi->opening.wait_for(std::chrono::seconds(0)) == std::future_status::ready) {
+        auto r = gi->opening.get();
+        gi->g = r.first;
+        if (!gi->g) gi->failed = true, gi->err = r.second;
     }
+    gpu = gpu && gi->g;
     size_t submitted = 0;
     auto submit = [&](bool last) {             // blocks read so far, in chunks of kGpuChunk
         if (!gpu) return;
@@ -353,10 +359,10 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
     if (nt > 0) work();
     for (auto &t : pool) t.join();
     if (bad) B.err = "corrupt BGZF block";
-    if (gi) {
+    if (gpu) {                                 // (the batches the GPU took: its blocks, and those it refused)
         gi->gpu_blocks += nb - todo.size();
         gi->cpu_blocks += todo.size();
-        if (gpu) gi->cpu_ns += now_ns() - t2;
+        gi->cpu_ns += now_ns() - t2;
     }
     return B;
 }
@@ -1753,10 +1759,11 @@ extern "C" int fc2_ingest_format(const fc2_ingest *h, int *compression) {
     return h->bam ? FC2_INGEST_BAM : FC2_INGEST_SAM;
 }
 
-extern "C" int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device) {
+extern "C" int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device, int wait) {
     if (!h) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_gpu_inflate: null argument");
     if (h->n_records) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_gpu_inflate: call before reading");
     const char *e = getenv("FC2_GPU_INFLATE");
+    if (e && atoi(e) == 2) wait = 1;           // (2: the buffers made before the first read, as the tests want)
     if (device < 0 || !h->bgzf || (e && atoi(e) == 0)) {
         h->gpu_inflate.reset();
         return FC2_OK;
@@ -1767,6 +1774,20 @@ extern "C" int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device) {
     // still rules
     if (!getenv("FC2_BGZF_BATCH")) h->bgzf_blocks = 1024;
     gi->max_blocks = (uint32_t)h->bgzf_blocks;
+    // the device's buffers and the first pinned batch buffers: now, or made while the first batches
+    // are read and inflated on the CPU
+    const int dev = device;
+    const uint32_t mb = gi->max_blocks;
+    gi->opening = std::async(wait ? std::launch::deferred : std::launch::async, [dev, mb]() {
+        std::string err;
+        fc2::inf::Gpu *g = fc2::inf::gpu_open(dev, mb, kHead + (size_t)mb * 65536, err);
+        return std::make_pair(g, err);
+    });
+    if (wait) {
+        auto r = gi->opening.get();
+        gi->g = r.first;
+        if (!gi->g) gi->failed = true, gi->err = r.second;
+    }
     h->gpu_inflate = gi;
     return FC2_OK;
 }

@@ -53,9 +53,10 @@ class NativeIngest:
         """-B/--bam: anchor alignments to ``path`` (include/fc2_ingest.h)."""
         N.check(N.lib().fc2_ingest_set_bam_out(self.h, path.encode()))
 
-    def set_gpu_inflate(self, device: int):
-        """A BGZF input's blocks inflated on GPU ``device`` from the next batch on (include/fc2_ingest.h)."""
-        N.check(N.lib().fc2_ingest_set_gpu_inflate(self.h, int(device)))
+    def set_gpu_inflate(self, device: int, wait: bool = True):
+        """A BGZF input's blocks inflated on GPU ``device`` from the next batch on (include/fc2_ingest.h);
+        wait: the device's buffers made now (else meanwhile, the CPU inflating until they are)."""
+        N.check(N.lib().fc2_ingest_set_gpu_inflate(self.h, int(device), int(bool(wait))))
 
     def inflate_counts(self) -> Tuple[int, int]:
         """(blocks inflated on the GPU, on the CPU) since set_gpu_inflate."""

@@ -109,7 +109,7 @@ class NativeCaller:
         if self.bam_out:
             N.check(L.fc2_ingest_set_bam_out(ing, self.bam_out.encode()))
         if self.inflate_device is not None:
-            N.check(L.fc2_ingest_set_gpu_inflate(ing, int(self.inflate_device)))
+            N.check(L.fc2_ingest_set_gpu_inflate(ing, int(self.inflate_device), 0))   # (buffers made meanwhile)
         if self.reads_gz:
             path, level, threads, piece = self.reads_gz
             N.check(L.fc2_caller_set_reads_gz(self.h, path.encode(), int(level), int(threads), int(piece)))

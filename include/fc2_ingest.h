@@ -87,12 +87,14 @@ int fc2_ingest_close_bam_out(fc2_ingest *h);
  * tests and the bench's stdin-BAM CLI run. */
 int fc2_sam_to_bam(const char *sam_path, const char *bam_path);
 /* The BAM input's BGZF blocks inflated on GPU `device` (fc2_inflate.hip) instead of the CPU from the
- * next batch on; call before reading (the CLI's read loop does, on its first device).  Batches grow to
- * 1024 blocks (FC2_BGZF_BATCH still sets them); the host still checks every block's CRC-32 and ISIZE
- * and inflates on the CPU any block the GPU refused or got wrong, and every block from then on if the
- * device fails.  device < 0, a non-BGZF input or FC2_GPU_INFLATE=0: the CPU inflates (the default). */
-int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device);
-/* Blocks inflated on the GPU and on the CPU since fc2_ingest_set_gpu_inflate (0, 0 without it). */
+ * next batch on; call before reading (the CLI's read loop does, on its first device, with
+ * FC2_GPU_INFLATE=1 or 2).  The device's
+ * buffers are made now (wait != 0) or meanwhile, the batches inflated on the CPU until they are ready.
+ * Batches grow to 1024 blocks (FC2_BGZF_BATCH still sets them); every block's CRC-32 and ISIZE are
+ * checked (on the device), and the CPU inflates any block the GPU refused, and every block from then
+ * on if the device fails.  device < 0, a non-BGZF input or FC2_GPU_INFLATE=0: the CPU inflates. */
+int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device, int wait);
+/* Blocks of the batches the GPU inflated: those it took, and those it left to the CPU. */
 int fc2_ingest_inflate_counts(const fc2_ingest *h, uint64_t *gpu_blocks, uint64_t *cpu_blocks);
 /* BGZF blocks inflated on the GPU (fc2_inflate.hip; the BAM input's inflate, which pysam/htslib does for
  * the reference, find_circ.py:461-469): n blocks, block i = len[i] bytes of raw DEFLATE at src + off[i]

@@ -228,12 +228,14 @@ def test_ingest_gpu_inflate_corrupt_block_same_error(tmp_path, monkeypatch):
 
 def test_cli_bam_input_inflated_on_the_gpu(tmp_path, monkeypatch):
     """The CLI on a BAM reads it with the GPU inflate (run.log's process phases count the blocks) and
-    writes the same files as with FC2_GPU_INFLATE=0."""
+    writes the same files as with FC2_GPU_INFLATE=0; and with the buffers made in the background (the
+    default) the same files again."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from test_cli import run_cli
     from test_cli_gpu import _compare, _sim_reads
     monkeypatch.setenv("FC2_BGZF_BATCH", "1")
+    monkeypatch.setenv("FC2_GPU_INFLATE", "2")          # the device's buffers ready before the first read
     fa = os.path.join(GOLDEN, "CDR1as_locus.fa")
     rd = _sim_reads(fa, 3000, seed=5)
     rc1, o1 = run_cli(tmp_path, fa, rd, bam=True, evaluator=None, tag="gpu_inflate")
@@ -249,3 +251,7 @@ def test_cli_bam_input_inflated_on_the_gpu(tmp_path, monkeypatch):
     g1, c1 = blocks(o1)
     assert g1 >= 2 and c1 == 0
     assert blocks(o2) == (0.0, 0.0)
+    monkeypatch.setenv("FC2_GPU_INFLATE", "1")
+    rc3, o3 = run_cli(tmp_path, fa, rd, bam=True, evaluator=None, tag="gpu_inflate_background")
+    assert rc3 == 0
+    _compare(o1, o3)
