@@ -10,8 +10,10 @@
 // code's tables (a ballot ranks the symbols of each length; each lane fills its own codes' entries),
 // the bytes of a match (every source byte precedes the match -- p - dist + j mod dist -- so one
 // iteration moves 64 bytes even for overlapping copies), stored blocks, and the stores to HBM.
-// The output goes through a 32 KiB ring in LDS (DEFLATE's window) flushed to HBM 4 KiB at a time,
-// so a workgroup takes 40 KB of LDS and four run on a CU.  A table entry carries the symbol's
+// The output goes through a 16 KiB ring in LDS flushed to HBM 4 KiB at a time; a match reaching
+// farther back (DEFLATE's window is 32 KiB) reads the stored output.  Fast tables of 9 and 7 bits
+// (longer codes: the canonical test from there on) keep a workgroup at 20 KB of LDS: eight a CU,
+// two waves a SIMD, one decoding while the other waits.  A table entry carries the symbol's
 // meaning (literal / length or distance base and its extra-bit count / end of block), so a length
 // or a distance is one lookup and one shift.  Every access is bounds-checked: a malformed block sets
 // its status word, and the host, which checks each block's CRC-32 and ISIZE on the bytes it copies
@@ -33,11 +35,11 @@
 namespace {
 
 constexpr uint32_t kOutMax = 65536;            // BGZF ISIZE limit
-constexpr uint32_t kRing = 32768;              // DEFLATE's window
+constexpr uint32_t kRing = 16384;              // the LDS ring: half DEFLATE's window (farther: HBM)
 constexpr uint32_t kRingMask = kRing - 1;
 constexpr uint32_t kFlush = 4096;              // ring -> HBM granule
-constexpr int kLitBits = 10;                   // fast-table bits: literal/length code
-constexpr int kDistBits = 9;                   // distance code (the code-length code uses 7 of them)
+constexpr int kLitBits = 9;                    // fast-table bits: literal/length code
+constexpr int kDistBits = 7;                   // distance code, and the code-length code
 
 enum : uint32_t { INF_OK = 0, INF_BAD_TYPE = 1, INF_BAD_STORED = 2, INF_BAD_COUNTS = 3, INF_BAD_CODE = 4,
                   INF_BAD_DIST = 5, INF_OVERFLOW = 6, INF_OVERRUN = 7, INF_SHORT = 8, INF_TOO_BIG = 9,
@@ -52,11 +54,11 @@ __device__ __forceinline__ uint32_t entry(uint32_t len, uint32_t extra, uint32_t
     return len | (extra << 4) | (kind << 8) | (value << 16);
 }
 
-struct Lds {
+struct Lds {                                   // 19968 B: eight workgroups a CU, two waves a SIMD
     uint8_t ring[kRing];
     uint32_t lfast[1 << kLitBits];
     uint32_t dfast[1 << kDistBits];            // (also the code-length code's table)
-    uint32_t lcnt[16], dcnt[16];               // codes per length
+    uint32_t cnt[16];                          // codes per length, while a code is built
     uint16_t lsym[288], dsym[32];              // symbols in canonical order (codes past the fast tables)
     uint8_t lens[320];
 };
@@ -142,26 +144,31 @@ __device__ __forceinline__ uint32_t bits(Bits &b, int n) {  // n <= 16
     return v;
 }
 
+// a canonical code's per-length numbers, lane l holding those of length l: the count, the first
+// code (MSB-first) and the index in sym[] of the first symbol
+struct CodeV {
+    uint32_t cnt, first, index;
+};
+
 // the entry of the next symbol (0: no such code); consumes its codeword and extra bits and puts the
-// decoded value (base + extra bits, or the literal / code-length symbol) into `val`
+// decoded value (base + extra bits, or the literal / code-length symbol) into `val`.  A code longer
+// than the fast table is found by the canonical test from length F + 1 on (RFC 1951 3.2.2)
 template <int F>
-__device__ __forceinline__ uint32_t decode(Bits &b, const uint32_t *fast, uint32_t cnt_v, const uint16_t *sym, Table t,
+__device__ __forceinline__ uint32_t decode(Bits &b, const uint32_t *fast, const CodeV &cv, const uint16_t *sym, Table t,
                                            uint32_t &val) {
     const uint32_t v = peek(b);
     uint32_t e = uni(fast[v & ((1u << F) - 1u)]);
-    if (!(e & 15u)) {                          // longer than the fast table, or no code: canonical walk
-        int code = 0, first = 0, index = 0;
+    if (!(e & 15u)) {
         e = 0;
-        for (int l = 1; l <= 15; ++l) {
-            code |= (int)((v >> (l - 1)) & 1u);
-            const int n = __builtin_amdgcn_readlane((int)cnt_v, l);
-            if (code - n < first) {
-                e = meaning(t, uni(sym[index + (code - first)]), (uint32_t)l);
+        const uint32_t rv = __builtin_bitreverse32(v);
+        for (int l = F + 1; l <= 15; ++l) {
+            const uint32_t code = rv >> (32 - l);
+            const uint32_t f = (uint32_t)__builtin_amdgcn_readlane((int)cv.first, l);
+            if (code - f < (uint32_t)__builtin_amdgcn_readlane((int)cv.cnt, l)) {
+                const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)cv.index, l) + code - f;
+                e = meaning(t, uni(sym[k]), (uint32_t)l);
                 break;
             }
-            index += n;
-            first = (first + n) << 1;
-            code <<= 1;
         }
         if (!e) return 0;
     }
@@ -176,7 +183,7 @@ __device__ __forceinline__ uint32_t decode(Bits &b, const uint32_t *fast, uint32
 // count of length l), the symbols in canonical order (sym); false if over-subscribed
 template <int F>
 __device__ bool build(const uint8_t *lens, int n, uint32_t *fast, uint32_t *cnt, uint16_t *sym, Table t, int lane,
-                      uint32_t &cnt_v) {
+                      CodeV &cv) {
     if (lane < 16) cnt[lane] = 0;
     for (int i = lane; i < (1 << F); i += 64) fast[i] = 0;
     __syncthreads();
@@ -185,8 +192,9 @@ __device__ bool build(const uint8_t *lens, int n, uint32_t *fast, uint32_t *cnt,
         if (l) atomicAdd(&cnt[l], 1u);
     }
     __syncthreads();
-    cnt_v = lane < 16 ? cnt[lane] : 0u;
+    uint32_t cnt_v = lane < 16 ? cnt[lane] : 0u;
     cnt_v = lane == 0 ? 0u : cnt_v;
+    cv.cnt = cnt_v;
     uint32_t start[16], next[16];              // scalar: the next sym[] slot and the next code per length
     int left = 1;
     uint32_t idx = 0, code = 0;
@@ -198,6 +206,10 @@ __device__ bool build(const uint8_t *lens, int n, uint32_t *fast, uint32_t *cnt,
         code = (code + np) << 1;               // RFC 1951 3.2.2 step 2
         start[l] = idx;
         next[l] = code;
+        if (lane == l) {
+            cv.first = code;
+            cv.index = idx;
+        }
         idx += nl;
     }
     if (left < 0) {                            // over-subscribed (once negative, left only falls)
@@ -299,6 +311,7 @@ __device__ void flush(const Lds &L, uint8_t *dst, uint32_t &flushed, uint32_t up
         }
         flushed = upto;
     }
+    __threadfence_block();                     // the stored rows visible to the wave's far-match loads
 }
 
 // block i: payload src + off[i] (len[i] bytes of raw DEFLATE), output into dst + i * 64 KiB
@@ -326,7 +339,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
     seek(b, (o & 3u) * 8u);
     uint32_t p = 0, flushed = 0;                // output bytes so far; of them, stored to HBM
     uint32_t R = 0;                             // raw CRC of the stored bytes
-    uint32_t lcnt_v = 0, dcnt_v = 0;
+    CodeV lcv = {0, 0, 0}, dcv = {0, 0, 0};
     bool last = false;
     while (st == INF_OK && !last) {
         if (b.pos + 3 > b.end) { st = INF_OVERRUN; break; }
@@ -355,8 +368,8 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
             for (int s = lane; s < 288 + 30; s += 64)
                 L.lens[s] = (uint8_t)(s < 144 ? 8 : s < 256 ? 9 : s < 280 ? 7 : s < 288 ? 8 : 5);
             __syncthreads();
-            if (!build<kLitBits>(L.lens, 288, L.lfast, L.lcnt, L.lsym, T_LIT, lane, lcnt_v) ||
-                !build<kDistBits>(L.lens + 288, 30, L.dfast, L.dcnt, L.dsym, T_DIST, lane, dcnt_v)) {
+            if (!build<kLitBits>(L.lens, 288, L.lfast, L.cnt, L.lsym, T_LIT, lane, lcv) ||
+                !build<kDistBits>(L.lens + 288, 30, L.dfast, L.cnt, L.dsym, T_DIST, lane, dcv)) {
                 st = INF_BAD_LITCODE;
                 break;
             }
@@ -371,13 +384,13 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
                 if (lane == 0) L.lens[kClOrder[k]] = (uint8_t)v;
             }
             __syncthreads();
-            if (!build<7>(L.lens, 19, L.dfast, L.dcnt, L.dsym, T_CL, lane, dcnt_v)) { st = INF_BAD_CLCODE; break; }
+            if (!build<7>(L.lens, 19, L.dfast, L.cnt, L.dsym, T_CL, lane, dcv)) { st = INF_BAD_CLCODE; break; }
             const int total = nlen + ndist;
             int k = 0;
             while (k < total) {
                 if (b.pos > b.end) { st = INF_OVERRUN; break; }
                 uint32_t sym;
-                if (!decode<7>(b, L.dfast, dcnt_v, L.dsym, T_CL, sym)) { st = INF_BAD_CLSYM; break; }
+                if (!decode<7>(b, L.dfast, dcv, L.dsym, T_CL, sym)) { st = INF_BAD_CLSYM; break; }
                 if (sym < 16) {
                     if (lane == 0) L.lens[k] = (uint8_t)sym;
                     ++k;
@@ -403,11 +416,11 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
             if (b.pos > b.end) { st = INF_OVERRUN; break; }
             __syncthreads();
             if (uni(L.lens[256]) == 0) { st = INF_NO_EOB; break; }
-            if (!build<kLitBits>(L.lens, nlen, L.lfast, L.lcnt, L.lsym, T_LIT, lane, lcnt_v)) {
+            if (!build<kLitBits>(L.lens, nlen, L.lfast, L.cnt, L.lsym, T_LIT, lane, lcv)) {
                 st = INF_BAD_LITCODE;
                 break;
             }
-            if (!build<kDistBits>(L.lens + nlen, ndist, L.dfast, L.dcnt, L.dsym, T_DIST, lane, dcnt_v)) {
+            if (!build<kDistBits>(L.lens + nlen, ndist, L.dfast, L.cnt, L.dsym, T_DIST, lane, dcv)) {
                 st = INF_BAD_DISTCODE;
                 break;
             }
@@ -416,7 +429,7 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
         for (;;) {
             if (b.pos > b.end) { st = INF_OVERRUN; break; }
             uint32_t val;
-            const uint32_t e = decode<kLitBits>(b, L.lfast, lcnt_v, L.lsym, T_LIT, val);
+            const uint32_t e = decode<kLitBits>(b, L.lfast, lcv, L.lsym, T_LIT, val);
             const uint32_t kind = (e >> 8) & 0xFFu;
             if (!e || kind == K_BAD) { st = INF_BAD_CODE; break; }
             if (kind == K_LIT) {
@@ -428,12 +441,19 @@ __global__ __launch_bounds__(64) void inflate_kernel(const uint8_t *__restrict__
             } else {
                 const uint32_t mlen = val;
                 uint32_t dist;
-                const uint32_t de = decode<kDistBits>(b, L.dfast, dcnt_v, L.dsym, T_DIST, dist);
+                const uint32_t de = decode<kDistBits>(b, L.dfast, dcv, L.dsym, T_DIST, dist);
                 if (!de || ((de >> 8) & 0xFFu) == K_BAD || dist > p) { st = INF_BAD_DIST; break; }
                 if (p + mlen > want) { st = INF_OVERFLOW; break; }
-                // every source byte precedes p: one iteration moves 64 bytes, overlapping copies too
-                for (uint32_t j = (uint32_t)lane; j < mlen; j += 64)
-                    L.ring[(p + j) & kRingMask] = L.ring[(p - dist + (j < dist ? j : j % dist)) & kRingMask];
+                // every source byte precedes p: one iteration moves 64 bytes, overlapping copies too.
+                // A source the ring no longer holds (dist + mlen > 16 KiB: it is more than 16 KiB
+                // - 258 back, past the unflushed 4 KiB + 258) is read from the stored output
+                if (dist + mlen <= kRing) {
+                    for (uint32_t j = (uint32_t)lane; j < mlen; j += 64)
+                        L.ring[(p + j) & kRingMask] = L.ring[(p - dist + (j < dist ? j : j % dist)) & kRingMask];
+                } else {
+                    for (uint32_t j = (uint32_t)lane; j < mlen; j += 64)
+                        L.ring[(p + j) & kRingMask] = out[p - dist + (j < dist ? j : j % dist)];
+                }
                 p += mlen;
             }
             if (p - flushed >= kFlush) flush(L, out, flushed, p, false, lane, R);
@@ -566,9 +586,9 @@ bool pinned_give(void *b) {
     return true;
 }
 
-// chunks of a batch in flight at once: two chunks of 256 blocks hold half the GPU's 1024 wave slots
-// (two 40 KB workgroups a CU), so the breakpoint search's kernels, launched meanwhile, find room
-constexpr int kStreams = 2;
+// chunks of a batch in flight at once: four chunks of 256 blocks hold half the GPU's 2048 wave slots
+// for this kernel (eight 20 KB workgroups a CU), so the breakpoint search's kernels find room
+constexpr int kStreams = 4;
 
 struct Gpu {
     int device = 0;
