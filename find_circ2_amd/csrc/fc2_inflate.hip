@@ -515,11 +515,14 @@ namespace inf {
 // batch allocator asks for them), made on first use, kept while a Gpu is open
 namespace {
 struct Pool {
+    struct Buf {
+        void *p;
+        size_t size;
+    };
     std::mutex mu;
-    size_t cap = 0;                            // bytes per buffer
-    int users = 0, max_buffers = 0, made = 0;
-    std::vector<void *> idle;
-    std::vector<void *> all;
+    size_t cap = 0;                            // bytes of a new buffer: the largest asked of the pool
+    int users = 0, max_buffers = 0;
+    std::vector<Buf> idle, all;                // (a buffer keeps the size it was made with)
 };
 Pool &pool() {
     static Pool *p = new Pool();               // (never destroyed: outlives the static destructors)
@@ -530,21 +533,28 @@ std::atomic<bool> pool_on{false};
 void pool_open(size_t cap, int max_buffers) {
     Pool &P = pool();
     std::lock_guard<std::mutex> g(P.mu);
-    if (P.users++ == 0 || cap > P.cap) P.cap = std::max(P.cap, cap);
+    ++P.users;
+    P.cap = std::max(P.cap, cap);
     P.max_buffers = std::max(P.max_buffers, max_buffers);
     pool_on = true;
+}
+void pool_drop(Pool &P, void *b) {             // (P.mu held)
+    (void)hipHostFree(b);
+    for (size_t k = 0; k < P.all.size(); ++k)
+        if (P.all[k].p == b) {
+            P.all.erase(P.all.begin() + (ptrdiff_t)k);
+            break;
+        }
 }
 void pool_close() {
     Pool &P = pool();
     std::lock_guard<std::mutex> g(P.mu);
     if (--P.users > 0) return;
     pool_on = false;
-    for (void *b : P.idle) {
-        (void)hipHostFree(b);
-        P.all.erase(std::find(P.all.begin(), P.all.end(), b));
-    }
-    P.made -= (int)P.idle.size();
+    for (const Pool::Buf &b : P.idle) pool_drop(P, b.p);
     P.idle.clear();                            // (buffers still in use are freed when given back)
+    P.cap = 0;
+    P.max_buffers = 0;
 }
 }  // namespace
 
@@ -553,37 +563,37 @@ void *pinned_take(size_t n) {
     Pool &P = pool();
     std::lock_guard<std::mutex> g(P.mu);
     if (!P.users || n > P.cap) return nullptr;
-    if (!P.idle.empty()) {
-        void *b = P.idle.back();
-        P.idle.pop_back();
-        return b;
-    }
-    if (P.made >= P.max_buffers) return nullptr;
+    for (size_t k = 0; k < P.idle.size(); ++k)
+        if (P.idle[k].size >= n) {
+            void *b = P.idle[k].p;
+            P.idle.erase(P.idle.begin() + (ptrdiff_t)k);
+            return b;
+        }
+    if ((int)P.all.size() >= P.max_buffers) return nullptr;
     void *b = nullptr;
     if (hipHostMalloc(&b, P.cap, hipHostMallocDefault) != hipSuccess) return nullptr;
-    ++P.made;
-    P.all.push_back(b);
+    P.all.push_back({b, P.cap});
     return b;
 }
 
 bool pinned_owns(const void *b) {
     Pool &P = pool();
     std::lock_guard<std::mutex> g(P.mu);
-    return std::find(P.all.begin(), P.all.end(), b) != P.all.end();
+    for (const Pool::Buf &x : P.all)
+        if (x.p == b) return true;
+    return false;
 }
 
 bool pinned_give(void *b) {
     Pool &P = pool();
     std::lock_guard<std::mutex> g(P.mu);
-    if (std::find(P.all.begin(), P.all.end(), b) == P.all.end()) return false;
-    if (P.users) {
-        P.idle.push_back(b);
-    } else {
-        (void)hipHostFree(b);
-        P.all.erase(std::find(P.all.begin(), P.all.end(), b));
-        --P.made;
-    }
-    return true;
+    for (const Pool::Buf &x : P.all)
+        if (x.p == b) {
+            if (P.users) P.idle.push_back(x);
+            else pool_drop(P, b);
+            return true;
+        }
+    return false;
 }
 
 // chunks of a batch in flight at once: four chunks of 256 blocks hold half the GPU's 2048 wave slots

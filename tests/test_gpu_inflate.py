@@ -255,3 +255,35 @@ def test_cli_bam_input_inflated_on_the_gpu(tmp_path, monkeypatch):
     rc3, o3 = run_cli(tmp_path, fa, rd, bam=True, evaluator=None, tag="gpu_inflate_background")
     assert rc3 == 0
     _compare(o1, o3)
+
+
+def test_two_ingests_with_different_batches_share_the_pinned_pool(tmp_path, monkeypatch):
+    """Two GPU-inflating ingests open at once with different batch sizes (so the pinned pool holds
+    buffers of two sizes) read, interleaved, what each reads alone."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from find_circ2_amd.ingest import NativeIngest
+    _, small, tiny = _bams(tmp_path)
+    want = {}
+    for bam, batch in ((small, "3"), (tiny, "600")):
+        monkeypatch.setenv("FC2_BGZF_BATCH", batch)
+        want[bam] = _read_all(bam)[:2]
+    ings = []
+    for bam, batch in ((small, "3"), (tiny, "600")):
+        monkeypatch.setenv("FC2_BGZF_BATCH", batch)
+        ing = NativeIngest(bam, True)
+        ing.set_gpu_inflate(0)
+        ings.append((bam, ing, []))
+    try:
+        while any(not ing.eof for _, ing, _ in ings):
+            for _, ing, frags in ings:
+                if not ing.eof:
+                    frags += [[(r.qname, r.flag, r.tid, r.pos, r.mapq, str(r.cigar), r.seq, r.qual, str(r.tags))
+                               for r in f] for f in ing.next_chunk(13, False, False, 31)]
+        for bam, ing, frags in ings:
+            c = ing.counts
+            assert (frags, tuple(getattr(c, f) for f, _ in c._fields_)) == want[bam]
+            assert ing.inflate_counts()[0] > 0 and ing.inflate_counts()[1] == 0
+    finally:
+        for _, ing, _ in ings:
+            ing.close()
