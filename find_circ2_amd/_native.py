@@ -157,7 +157,7 @@ EXPORTED = [
     "fc2_ingest_set_gpu_inflate", "fc2_ingest_inflate_counts",
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_inflate_counts", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
-    "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_submit_long", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_counter", "fc2_caller_stats",
+    "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_submit_long", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_write_rows", "fc2_caller_counter", "fc2_caller_stats",
     "fc2_caller_set_reads_gz", "fc2_caller_close_reads",
     # include/fc2_ctx.h
     "fc2_ctx_create", "fc2_ctx_create_sibling", "fc2_ctx_destroy", "fc2_ctx_genome_load", "fc2_ctx_genome_view", "fc2_ctx_scan_async",
@@ -292,6 +292,7 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_set_reads_gz": (ctypes.c_int, [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, u64]),
         "fc2_caller_close_reads": (ctypes.c_int, [vp]),
         "fc2_caller_rows": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_void_p), P(u64)]),
+        "fc2_caller_write_rows": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int, P(u64)]),
         "fc2_caller_counter": (ctypes.c_int, [vp, ctypes.c_int, P(ctypes.c_char_p), P(ctypes.c_double)]),
         "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_bgzf_inflate_launch": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),

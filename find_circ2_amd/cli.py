@@ -219,16 +219,6 @@ def main(argv=None, evaluator_factory=None) -> int:
     return 0
 
 
-def _write_bytes(fh, data: bytes):
-    """Bytes to a latin-1 text file (or stdout) without decoding and encoding them again."""
-    buf = getattr(fh, "buffer", None)
-    if buf is None:
-        fh.write(data.decode("latin-1"))
-        return
-    fh.flush()
-    buf.write(data)
-
-
 def _open_failed(out) -> int:
     """The input could not be opened: the reference's pysam.Samfile raises at module level
     (find_circ.py:461-469), an uncaught exception -- traceback, exit status 1."""
@@ -348,7 +338,7 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
         t_rows = time.time()
         for kind, key in ((0, "circs"), (1, "lins")):
             out[key].write(BED_HEADER)
-            _write_bytes(out[key], nc.rows_bytes(kind))
+            nc.write_rows(kind, out[key])
         if startup is not None:
             # the process's phases: what runs before the first record and after the last
             # (device_genome_s overlaps the start of the read loop)

@@ -6,6 +6,8 @@
 #include <stdlib.h>
 #include <stdio.h>
 #include <string.h>
+#include <errno.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <chrono>
@@ -2766,6 +2768,76 @@ extern "C" int fc2_caller_rows(fc2_caller *h, int kind, const char **text, uint6
     }
     *text = h->rows_text.c_str();
     *len = h->rows_text.size();
+    return FC2_OK;
+}
+
+// fc2_caller_rows written straight to a file descriptor: the dict order cut into ranges the workers
+// format while a writer thread writes each finished range in order and frees it -- no joined copy of
+// the table (over 1 GB when every read has a junction of its own), no copy into Python
+extern "C" int fc2_caller_write_rows(fc2_caller *h, int kind, int fd, uint64_t *len) {
+    if (!h || kind < 0 || kind > 1 || fd < 0) return fc2::fail(FC2_E_PARAM, "fc2_caller_write_rows: bad arguments");
+    release_read_side(h);
+    const size_t nj = h->order[kind].size();
+    const size_t W = h->pool ? (size_t)h->pool->size() : 1;
+    const size_t R = std::max<size_t>(1, std::min<size_t>(4 * W, nj / 4096));
+    std::vector<std::string> parts(R);
+    std::vector<std::vector<std::pair<const char *, double>>> Ns(R);
+    std::vector<char> ready(R, 0);
+    std::mutex mu;
+    std::condition_variable cv;
+    bool abandon = false;
+    int werr = 0;
+    uint64_t written = 0;
+    auto writer = [&]() {
+        for (size_t r = 0; r < R; ++r) {
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return ready[r] || abandon; });
+                if (!ready[r]) return;
+            }
+            const char *p = parts[r].data();
+            size_t left = parts[r].size();
+            while (left && !werr) {
+                const ssize_t w = ::write(fd, p, left);
+                if (w < 0) {
+                    if (errno == EINTR) continue;
+                    werr = errno;
+                    break;
+                }
+                p += w, left -= (size_t)w, written += (uint64_t)w;
+            }
+            std::string().swap(parts[r]);
+        }
+    };
+    auto range = [&](int r) {
+        storage_rows(h, kind, nj * (size_t)r / R, nj * (size_t)(r + 1) / R, parts[(size_t)r], Ns[(size_t)r]);
+        std::lock_guard<std::mutex> g(mu);
+        ready[(size_t)r] = 1;
+        cv.notify_all();
+    };
+    std::thread wt;
+    try {
+        wt = std::thread(writer);
+    } catch (const std::system_error &) {          // no thread: format all, then write here
+    }
+    try {
+        if (R > 1 && h->pool) h->pool->run_checked((int)R, range);
+        else for (size_t r = 0; r < R; ++r) range((int)r);
+    } catch (const std::bad_alloc &) {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            abandon = true;
+            cv.notify_all();
+        }
+        if (wt.joinable()) wt.join();
+        return fc2::fail(FC2_E_PARAM, "fc2_caller_write_rows: out of memory");
+    }
+    if (wt.joinable()) wt.join();
+    else writer();
+    for (size_t r = 0; r < R; ++r)
+        for (const auto &kv : Ns[r]) incN(h, kv.first, kv.second);
+    if (len) *len = written;
+    if (werr) return fc2::fail(FC2_E_IO, std::string("IOError: [Errno ") + std::to_string(werr) + "] " + strerror(werr));
     return FC2_OK;
 }
 

@@ -442,6 +442,28 @@ class NativeCaller:
     def rows(self, kind: int) -> str:
         return self.rows_bytes(kind).decode("latin-1")
 
+    def write_rows(self, kind: int, fh) -> int:
+        """The BED rows written straight into the open file fh (flushed first; the rows go to its
+        descriptor from the native workers, never through Python).  Falls back to rows_bytes for an
+        object without a descriptor."""
+        try:
+            fd = fh.fileno()
+        except (AttributeError, OSError, ValueError):
+            fd = -1
+        if fd < 0:
+            data = self.rows_bytes(kind)
+            buf = getattr(fh, "buffer", None)
+            if buf is None:
+                fh.write(data.decode("latin-1"))
+            else:
+                fh.flush()
+                buf.write(data)
+            return len(data)
+        fh.flush()
+        n = ctypes.c_uint64()
+        N.check(N.lib().fc2_caller_write_rows(self.h, kind, fd, ctypes.byref(n)))
+        return n.value
+
     def rows_bytes(self, kind: int) -> bytes:
         """The BED rows as the bytes written (the input's bytes: latin-1 both ways)."""
         t, n = ctypes.c_void_p(), ctypes.c_uint64()

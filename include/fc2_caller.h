@@ -122,6 +122,11 @@ int fc2_caller_close_reads(fc2_caller *h);
  * before), its parse blocks, the chunk buffers -- on a thread of its own: fc2_caller_ingest returns
  * NULL from then on, fc2_caller_next reports the end, the counters keep their final values. */
 int fc2_caller_rows(fc2_caller *h, int kind, const char **text, uint64_t *len);
+/* The same rows written to the file descriptor fd at its current offset (the CLI's BED files; the
+ * ranges are formatted on the workers and written in order as each is done, never joined in memory);
+ * *len (may be NULL) = bytes written.  FC2_E_IO if a write failed.  Call once per kind, instead of
+ * fc2_caller_rows. */
+int fc2_caller_write_rows(fc2_caller *h, int kind, int fd, uint64_t *len);
 /* The reference's N[...] counters in sorted key order: i-th name and value;
  * FC2_E_RANGE past the end. */
 int fc2_caller_counter(fc2_caller *h, int i, const char **name, double *value);
