@@ -952,15 +952,20 @@ void hit_quals(Hit &t, const Span &s) {
 void CanonSet::insert(const std::string &read, Arena &a) {
     const size_t n = read.size();
     const unsigned char *in = (const unsigned char *)read.data();
-    static thread_local std::string rc;         // rc(read) in one branch-free pass, then one memcmp
-    rc.resize(n);
-    char *o = &rc[0];
-    for (size_t k = 0; k < n; ++k) o[k] = kComp.t[in[n - 1 - k]];
-    const int cmp = n ? memcmp(read.data(), rc.data(), n) : 0;   // bytewise, as std::string compares
+    // read against rc(read) byte by byte (unsigned, as std::string compares) up to the first
+    // difference, which nearly always comes at once: rc is built only when it is the smaller
+    size_t k = 0;
+    auto rc_at = [&](size_t j) { return (unsigned char)kComp.t[in[n - 1 - j]]; };
+    while (k < n && in[k] == rc_at(k)) ++k;
+    const int cmp = k == n ? 0 : (in[k] < rc_at(k) ? -1 : 1);
     if (cmp <= 0) {
         if (canon.insert(read, a) && cmp == 0) palindromes += 1;
         return;
     }
+    static thread_local std::string rc;
+    rc.resize(n);
+    char *o = &rc[0];
+    for (size_t j = 0; j < n; ++j) o[j] = kComp.t[in[n - 1 - j]];
     canon.insert(rc, a);
 }
 
