@@ -7,6 +7,7 @@
  * The reference's default options (find_circ.py:383-413); writes circ_splice_sites.bed,
  * lin_splice_sites.bed, multi_events.tsv and spliced_reads.fastq.gz as the Python CLI does with its
  * native loop (tests/test_ctx_c_host.py compares them).  Sequential: next -> scan -> submit. */
+#define _POSIX_C_SOURCE 200809L   /* fileno */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -112,11 +113,17 @@ int main(int argc, char **argv) {
     for (int kind = 0; kind < 2; ++kind) {
         const char *t;
         uint64_t len;
-        if (fc2_caller_rows(c, kind, &t, &len) != FC2_OK) return fail("fc2_caller_rows", fc2_last_error());
         FILE *f = out_file(outdir, files[kind]);
         if (!f) return fail("open", files[kind]);
         fputs(kBedHeader, f);
-        if (len) fwrite(t, 1, len, f);
+        if (kind == 0) {                       /* the rows as text ... */
+            if (fc2_caller_rows(c, kind, &t, &len) != FC2_OK) return fail("fc2_caller_rows", fc2_last_error());
+            if (len) fwrite(t, 1, len, f);
+        } else {                               /* ... or written to the file by the library (the CLI's way) */
+            fflush(f);
+            if (fc2_caller_write_rows(c, kind, fileno(f), &len) != FC2_OK)
+                return fail("fc2_caller_write_rows", fc2_last_error());
+        }
         fclose(f);
     }
     fc2_caller_close(c);
