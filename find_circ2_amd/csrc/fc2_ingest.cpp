@@ -197,13 +197,75 @@ using CharBuf = std::vector<char, NoInitAlloc<char>>;
 // record cut by the previous batch's end there instead of copying the batch (bgzf_split_loop)
 constexpr size_t kHead = size_t(1) << 16;
 
+constexpr uint64_t kNoExit = ~uint64_t(0);
+
+// The BAM records of one inflated batch as the inflating threads saw them (bgzf_split_loop jumps
+// through these instead of reading every record's block_size from cold memory on its one thread):
+// per BGZF block, the record starts a walk visits inside the block when it begins at the block's
+// first plausible record (batch offsets, ascending), and where that walk leaves the block (kNoExit:
+// it met a block_size below 32 or could not read one).  A start is only a guess until the split
+// loop's own chain of records -- the reference's order of block sizes -- reaches it.
+struct RecLists {
+    size_t n = 0;                               // the batch's inflated bytes
+    std::vector<size_t> ooff;                   // block k's bytes: [ooff[k], ooff[k + 1])
+    std::vector<std::vector<uint32_t>> starts;
+    std::vector<uint64_t> exit;
+};
+
 struct BgzfBatch {
     CharBuf out;                 // kHead bytes of headroom, then the inflated bytes
     size_t n = 0;                // inflated bytes
     bool eof = false;
     std::string err;
+    std::shared_ptr<RecLists> recs;             // null: none (a batch of 4 GiB or more)
     const char *data() const { return out.data() + kHead; }
 };
+
+// a plausible BAM record at p (`avail` bytes readable from p): the fixed fields and read name as the
+// SAM/BAM specification constrains them (a guess; see RecLists)
+bool bam_plausible(const uint8_t *p, size_t avail) {
+    if (avail < 36) return false;
+    int32_t bs, ref, pos, lseq, nref, npos;
+    uint16_t ncig;
+    memcpy(&bs, p, 4), memcpy(&ref, p + 4, 4), memcpy(&pos, p + 8, 4), memcpy(&ncig, p + 16, 2);
+    memcpy(&lseq, p + 20, 4), memcpy(&nref, p + 24, 4), memcpy(&npos, p + 28, 4);
+    const uint32_t lname = p[12];
+    if (bs < 32 || bs >= (1 << 28) || ref < -1 || pos < -1 || lname < 1 || lseq < 0 || nref < -1 || npos < -1)
+        return false;
+    if (32u + lname + 4ull * ncig + ((uint64_t)lseq + 1) / 2 + (uint64_t)lseq > (uint64_t)bs) return false;
+    if (36 + (size_t)lname > avail) return true;
+    if (p[36 + lname - 1] != 0) return false;
+    for (uint32_t k = 0; k + 1 < lname; ++k)
+        if (p[36 + k] < 0x21 || p[36 + k] > 0x7e) return false;
+    return true;
+}
+
+// RecLists for the block [b0, b1) of data, reading nothing outside it (its neighbours may still be
+// being inflated): the first offset where a plausible record is followed by another plausible one
+// (or by the block's end), then block_size to block_size
+void walk_block(const char *data, size_t b0, size_t b1, std::vector<uint32_t> &starts, uint64_t &exit) {
+    starts.clear();
+    exit = kNoExit;
+    const uint8_t *d = (const uint8_t *)data;
+    size_t o = b0;
+    for (; o + 36 <= b1; ++o) {
+        if (!bam_plausible(d + o, b1 - o)) continue;
+        int32_t bs;
+        memcpy(&bs, d + o, 4);
+        const size_t nx = o + 4 + (size_t)bs;
+        if (nx + 36 <= b1 && !bam_plausible(d + nx, b1 - nx)) continue;
+        break;
+    }
+    if (o + 36 > b1) return;                    // inside one record, or too short to tell
+    while (o + 4 <= b1) {
+        int32_t bs;
+        memcpy(&bs, d + o, 4);
+        if (bs < 32) return;
+        starts.push_back((uint32_t)o);
+        o += 4 + (size_t)bs;
+    }
+    exit = o;
+}
 
 int bgzf_threads() {
     const char *e = getenv("FC2_INGEST_THREADS");
@@ -332,36 +394,52 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
     B.n = ooff[nb];
     B.out.resize(kHead + B.n);
     // the blocks the CPU inflates: all of them, or those the GPU refused
-    std::vector<uint32_t> todo;
-    todo.reserve(on_gpu ? 16 : nb);
-    for (size_t i = 0; i < nb; ++i)
-        if (!on_gpu || fc2::inf::gpu_status(gi->g, i) != 0) todo.push_back((uint32_t)i);
+    std::vector<uint8_t> on_cpu(nb, on_gpu ? 0 : 1);
+    size_t n_cpu = on_gpu ? 0 : nb;
+    if (on_gpu)
+        for (size_t i = 0; i < nb; ++i)
+            if (fc2::inf::gpu_status(gi->g, i) != 0) on_cpu[i] = 1, ++n_cpu;
+    // every block's records listed by the thread that inflated it, while they are in its cache
+    RecLists *R = nullptr;
+    if (B.n < (uint64_t(1) << 32) && nb) {
+        B.recs = std::make_shared<RecLists>();
+        R = B.recs.get();
+        R->n = B.n;
+        R->ooff = ooff;
+        R->starts.resize(nb);
+        R->exit.assign(nb, kNoExit);
+    }
     std::atomic<size_t> next{0};
     std::atomic<bool> bad{false};
     auto work = [&]() {
         fc2::cpu::Scope acct(fc2::cpu::INFLATE);
         fc2::dfl::Inflater inf;                 // libdeflate (zlib without it): fc2_deflate.h
         if (!inf.ok()) { bad = true; return; }
-        for (size_t k; (k = next.fetch_add(1)) < todo.size() && !bad;) {
-            const size_t i = todo[k];
-            const uint8_t *blk = raw.data() + boff[i];
-            const size_t xl = blk[10] | (blk[11] << 8);
+        for (size_t i; (i = next.fetch_add(1)) < nb && !bad;) {
             char *dst = B.out.data() + kHead + ooff[i];
             const size_t n = ooff[i + 1] - ooff[i];
-            const uint8_t *t = blk + bsz[i] - 8;
-            const uint32_t crc = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
-            if (!inf.exact(blk + 12 + xl, bsz[i] - 12 - xl - 8, dst, n) || fc2::dfl::crc32(dst, n) != crc) bad = true;
+            if (on_cpu[i]) {
+                const uint8_t *blk = raw.data() + boff[i];
+                const size_t xl = blk[10] | (blk[11] << 8);
+                const uint8_t *t = blk + bsz[i] - 8;
+                const uint32_t crc = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
+                if (!inf.exact(blk + 12 + xl, bsz[i] - 12 - xl - 8, dst, n) || fc2::dfl::crc32(dst, n) != crc) {
+                    bad = true;
+                    break;
+                }
+            }
+            if (R) walk_block(B.out.data() + kHead, ooff[i], ooff[i + 1], R->starts[i], R->exit[i]);
         }
     };
-    const int nt = (int)std::min<size_t>((size_t)n_threads, todo.size());
+    const int nt = (int)std::min<size_t>((size_t)n_threads, R ? nb : n_cpu);
     std::vector<std::thread> pool;
     for (int t = 1; t < nt; ++t) pool.emplace_back(work);
     if (nt > 0) work();
     for (auto &t : pool) t.join();
     if (bad) B.err = "corrupt BGZF block";
     if (gpu) {                                 // (the batches the GPU took: its blocks, and those it refused)
-        gi->gpu_blocks += nb - todo.size();
-        gi->cpu_blocks += todo.size();
+        gi->gpu_blocks += nb - n_cpu;
+        gi->cpu_blocks += n_cpu;
         gi->cpu_ns += now_ns() - t2;
     }
     return B;
@@ -481,6 +559,7 @@ struct fc2_ingest::SamAhead {
     // FC2_CALLER_TIMING: the splitter blocked on the consumer (all blocks in flight), the parsers
     // idle (no block to parse), summed over parser threads
     std::atomic<int64_t> split_block_ns{0}, parse_idle_ns{0};
+    uint64_t split_steps = 0, split_jumps = 0;  // bgzf_split_loop: records read one at a time, list jumps
     std::unique_ptr<Batch> cur;                 // the consumer's batch
     size_t pos = 0;
     // grouping on the parse threads (pull only: the sink path); the consumer's place in a batch's
@@ -520,6 +599,9 @@ struct fc2_ingest::SamAhead {
         for (std::thread &t : parsers) t.join();
         for (int fd : wake)
             if (fd >= 0) close(fd);
+        if ((split_steps || split_jumps) && getenv("FC2_CALLER_TIMING"))   // (the splitter has joined)
+            fprintf(stderr, "bgzf split: %llu records read one at a time, %llu jumps through the record lists\n",
+                    (unsigned long long)split_steps, (unsigned long long)split_jumps);
     }
 };
 
@@ -1180,6 +1262,8 @@ void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
                                                              h->buf.begin() + (ptrdiff_t)h->end);   // inflated with the header
     size_t beg = 0, end = cur->size();
     h->beg = h->end;
+    std::shared_ptr<RecLists> lists;            // the current batch's record lists, its bytes from `base` on
+    size_t base = 0;
     // the next batch behind the bytes not yet cut; false at the end of the input or an input error
     auto more = [&]() -> bool {
         if (h->z_done) return false;
@@ -1204,6 +1288,8 @@ void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
             beg = 0;
         }
         end = beg + L + b.n;
+        lists = std::move(b.recs);
+        base = beg + L;
         cur = std::move(nb);
         return true;
     };
@@ -1235,14 +1321,41 @@ void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
             b->eof = true;
         };
         for (;;) {
-            // every whole record from beg on, up to a block's worth
-            const char *base = cur->data();
+            // every whole record from beg on, up to a block's worth: the first record end at or past
+            // beg + A.block, or the last whole one.  Where the chain of records from beg reaches a start
+            // the inflating threads listed, the rest of that BGZF block's records are the list's (the
+            // same block sizes, already read): the cut is found there, or the chain continues at the
+            // list's exit; elsewhere (no list, a start it missed, a record past the batch's end, a
+            // block_size below 32) one record at a time
+            const char *bp = cur->data();
             size_t q = beg;
-            while (q + 4 <= end) {
+            for (;;) {
+                if (lists && q >= base && q - base < lists->n) {
+                    const uint64_t bq = q - base;
+                    const size_t j = (size_t)(std::upper_bound(lists->ooff.begin(), lists->ooff.end(), (size_t)bq) -
+                                              lists->ooff.begin()) - 1;
+                    const std::vector<uint32_t> &S = lists->starts[j];
+                    const auto it = std::lower_bound(S.begin(), S.end(), (uint32_t)bq);
+                    if (it != S.end() && *it == bq) {
+                        const uint64_t tb = beg + A.block - base;   // > bq: q - beg < A.block here
+                        const auto c = std::lower_bound(it + 1, S.end(), (uint32_t)std::min<uint64_t>(tb, UINT32_MAX));
+                        if (c != S.end() && *c >= tb) { q = base + *c; ++A.split_jumps; break; }
+                        const uint64_t ex = lists->exit[j];
+                        if (ex != kNoExit && base + ex <= end) {
+                            q = base + ex;
+                            ++A.split_jumps;
+                            if (q - beg >= A.block) break;
+                            continue;
+                        }
+                        q = base + S.back();            // its last record on, one at a time
+                    }
+                }
+                if (q + 4 > end) break;
                 int32_t bs;
-                memcpy(&bs, base + q, 4);
+                memcpy(&bs, bp + q, 4);
                 if (bs < 32 || q + 4 + (size_t)bs > end) break;
                 q += 4 + (size_t)bs;
+                ++A.split_steps;
                 if (q - beg >= A.block) break;
             }
             if (q > beg) {
@@ -1260,7 +1373,7 @@ void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
                 break;
             }
             int32_t bs;                         // the record at beg is not whole yet
-            memcpy(&bs, base + beg, 4);
+            memcpy(&bs, bp + beg, 4);
             if (bs < 32 || !more()) { truncated(); break; }
         }
         const bool last = b->eof;
@@ -1817,6 +1930,7 @@ extern "C" int fc2_ingest_close_bam_out(fc2_ingest *h) {
 }
 
 fc2_ingest::~fc2_ingest() { ahead.reset(); }
+
 
 extern "C" void fc2_ingest_close(fc2_ingest *h) {
     if (!h) return;

@@ -217,13 +217,17 @@ def long_bam(tmp_path_factory):
     return d, fa, open(p, "rb").read()
 
 
-@pytest.mark.parametrize("bgzf_block,batch,parse_block", [(3000, 2, None), (9000, 5, "20000"), (65280, 1, None)])
+@pytest.mark.parametrize("bgzf_block,batch,parse_block", [(3000, 2, None), (9000, 5, "20000"), (65280, 1, None),
+                                                       (65280, 8, "100000"), (20000, 16, "7000")])
 def test_bgzf_inplace_splitter_equals_copying_and_sequential(long_bam, tmp_path, monkeypatch, bgzf_block, batch,
                                                              parse_block):
     """The BGZF splitter that cuts parse blocks in place in the inflated batches (bgzf_split_loop:
     a record cut by a batch's end moved into the next batch's headroom, or joined by copy when it
-    is longer than the headroom) against the sequential reader (-B): tiny BGZF blocks and batches of 1-5 blocks put batch boundaries inside
-    records of every size; the files are identical, on the whole input and on truncations."""
+    is longer than the headroom) against the sequential reader (-B): tiny BGZF blocks and batches of 1-16 blocks put batch boundaries inside
+    records of every size; parse blocks smaller and larger than a BGZF block put the cuts inside the
+    record lists the inflating threads made (RecLists: jumps to a list's cut or exit, a block inside an
+    80-kb record with no list, the lists' guessed starts inside such records); the files are identical,
+    on the whole input and on truncations."""
     import os
     d, fa, raw = long_bam
     monkeypatch.setenv("FC2_BGZF_BATCH", str(batch))
@@ -308,3 +312,49 @@ def test_libdeflate_and_zlib_give_the_same_run(long_bam, tmp_path):
         assert res[0] == res[1], (k, res[0][0], res[1][0])
         if k == 0:
             assert res[0][0] == 0 and res[0][1]["reads"].count("\n") > 100
+
+
+def test_bgzf_splitter_jumps_through_record_lists(tmp_path):
+    """A bwa-mem-shaped BAM of 60,000 reads in standard ~64-KiB BGZF blocks (scripts/gen_reads +
+    fc2_sam_to_bam): the splitter finds nearly every parse block's cut through the record lists the
+    inflating threads made (FC2_CALLER_TIMING's "bgzf split" line: jumps, and records read one at a
+    time only where a list does not reach -- the first batch, a block's first record, a batch's
+    end), with small parse blocks so the cuts land inside the lists too; the files equal the
+    sequential reader's (-B)."""
+    import os
+    import re
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    gen = os.path.join(root, "scripts", "gen_reads")
+    if not os.path.exists(gen):
+        subprocess.check_call(["gcc", "-O2", "-o", gen, gen + ".c"])
+    sq = tmp_path / "sq.tsv"
+    sq.write_text("chrA\t300000\nchrB\t450000\nchrC\t250000\n")
+    fa, sam, bam = str(tmp_path / "g.fa"), str(tmp_path / "r.sam"), str(tmp_path / "r.bam")
+    subprocess.check_call([gen, str(sq), "60000", "11", fa, sam])
+    from find_circ2_amd.ingest import sam_to_bam as native_sam_to_bam
+    native_sam_to_bam(sam, bam)
+    n_records = sum(1 for l in open(sam) if l[0] != "@")
+    script = _CLI_SCRIPT % os.path.dirname(os.path.abspath(__file__))
+    files = []
+    for tag, extra, env_extra in (("lists", [], {"FC2_CALLER_TIMING": "1", "FC2_PARSE_BLOCK": "200000",
+                                                 "FC2_BGZF_BATCH": "24"}),
+                                  ("seq", ["-B"], {})):
+        o = str(tmp_path / tag)
+        env = dict(os.environ, **env_extra)
+        r = subprocess.run([sys.executable, "-c", script, "-G", fa, "-o", o, "-q"] + extra + [bam], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        if tag == "lists":
+            m = re.search(r"bgzf split: (\d+) records read one at a time, (\d+) jumps", r.stderr)
+            assert m, r.stderr[-2000:]
+            steps, jumps = int(m.group(1)), int(m.group(2))
+            assert jumps > 100 and steps < n_records // 10, (steps, jumps, n_records)
+        got = {}
+        for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
+            got[f] = open(os.path.join(o, f)).read()
+        got["reads"] = gzip.open(os.path.join(o, "spliced_reads.fastq.gz"), "rt").read()
+        files.append(got)
+    assert files[0] == files[1]
+    assert files[0]["lin_splice_sites.bed"].count("\n") > 1000
