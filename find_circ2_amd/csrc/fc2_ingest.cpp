@@ -305,166 +305,6 @@ static int64_t now_ns() {
 
 constexpr size_t kGpuChunk = 256;              // blocks per GPU chunk (16 MiB inflated)
 
-// bgzf_batch on the CPU: the blocks are inflated (and their records listed) by the workers while
-// this thread reads the ones after them, so reading the input and inflating it overlap.  Every
-// buffer the workers read is sized for max_blocks up front (a BGZF block is at most 64 KiB either
-// way), so nothing a worker reads is moved while the reader appends; a block is handed over under
-// the mutex once it is read whole.  The same results and errors as the sequential form.
-BgzfBatch bgzf_batch_cpu(int fd, std::vector<uint8_t> raw, int max_blocks, int n_threads) {
-    BgzfBatch B;
-    const size_t mb = (size_t)std::max(max_blocks, 1);
-    std::vector<size_t> boff, bsz, ooff;
-    boff.reserve(mb), bsz.reserve(mb), ooff.reserve(mb + 1);
-    ooff.push_back(0);
-    raw.reserve(raw.size() + mb * 65536 + 65536);
-    const uint8_t *rawp = raw.data();           // stays: raw never grows past its reserve
-    B.out.resize(kHead + mb * 65536);
-    RecLists *R = nullptr;
-    if (mb * 65536 < (uint64_t(1) << 32)) {
-        B.recs = std::make_shared<RecLists>();
-        R = B.recs.get();
-        R->starts.resize(mb);
-        R->exit.assign(mb, kNoExit);
-    }
-    std::mutex mu;
-    std::condition_variable cv;
-    size_t avail = 0;                           // blocks read whole (under mu)
-    bool reading = true;
-    std::atomic<size_t> next{0};
-    std::atomic<bool> bad{false};
-    auto work = [&]() {
-        fc2::cpu::Scope acct(fc2::cpu::INFLATE);
-        fc2::dfl::Inflater inf;                 // libdeflate (zlib without it): fc2_deflate.h
-        if (!inf.ok()) { bad = true; return; }
-        for (;;) {
-            const size_t i = next.fetch_add(1);
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return i < avail || !reading; });
-                if (i >= avail) return;
-            }
-            if (bad) return;
-            const uint8_t *blk = rawp + boff[i];
-            const size_t xl = blk[10] | (blk[11] << 8);
-            char *dst = B.out.data() + kHead + ooff[i];
-            const size_t n = ooff[i + 1] - ooff[i];
-            const uint8_t *t = blk + bsz[i] - 8;
-            const uint32_t crc = t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24);
-            if (!inf.exact(blk + 12 + xl, bsz[i] - 12 - xl - 8, dst, n) || fc2::dfl::crc32(dst, n) != crc) {
-                bad = true;
-                return;
-            }
-            if (R) walk_block(B.out.data() + kHead, ooff[i], ooff[i + 1], R->starts[i], R->exit[i]);
-        }
-    };
-    const int nt = std::max(1, n_threads);
-    std::vector<std::thread> pool;
-    try {
-        for (int t = 0; t < nt; ++t) pool.emplace_back(work);
-    } catch (const std::system_error &) {       // fewer threads (none: this one inflates at the end)
-    }
-    // a block past what B.out was sized for (a gzip member inflating to more than 64 KiB, which htslib
-    // reads too): the workers finish what they have, and the rest of the batch is read first, then
-    // inflated, into a grown buffer
-    bool overlapped = true;
-    size_t first_late = 0;
-    auto stop_overlap = [&]() {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            reading = false;
-            first_late = avail;
-        }
-        cv.notify_all();
-        for (auto &t : pool) t.join();
-        pool.clear();
-        overlapped = false;
-    };
-    size_t pos = 0;
-    while (boff.size() < mb) {
-        size_t got;
-        if (raw.size() - pos < 18) {           // header
-            const size_t have = raw.size() - pos;
-            raw.resize(pos + 18);
-            if (!read_full(fd, raw.data() + pos + have, 18 - have, got)) { B.err = "read error"; break; }
-            if (have + got == 0) { raw.resize(pos); B.eof = true; break; }
-            if (have + got < 18) { B.err = "truncated BGZF block header"; break; }
-        }
-        const size_t xlen = raw[pos + 10] | (raw[pos + 11] << 8);
-        if (raw.size() - pos < 12 + xlen) {
-            const size_t have = raw.size() - pos;
-            raw.resize(pos + 12 + xlen);
-            if (!read_full(fd, raw.data() + pos + have, 12 + xlen - have, got) || got < 12 + xlen - have) {
-                B.err = "truncated BGZF block header";
-                break;
-            }
-        }
-        const size_t bs = bgzf_block_size(raw.data() + pos, raw.size() - pos);
-        if (bs < 12 + xlen + 8) { B.err = "not a BGZF block"; break; }
-        const size_t have = raw.size() - pos;
-        raw.resize(pos + bs);
-        if (!read_full(fd, raw.data() + pos + have, bs - have, got) || got < bs - have) {
-            B.err = "truncated BGZF block";
-            break;
-        }
-        const uint8_t *t = raw.data() + pos + bs - 4;
-        const size_t isize = (size_t)(t[0] | (t[1] << 8) | (t[2] << 16) | ((uint32_t)t[3] << 24));
-        if (overlapped && ooff.back() + isize > mb * 65536) stop_overlap();
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            boff.push_back(pos);
-            bsz.push_back(bs);
-            ooff.push_back(ooff.back() + isize);
-            if (overlapped) avail = boff.size();
-        }
-        if (overlapped) cv.notify_all();
-        pos += bs;
-    }
-    if (overlapped) {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            reading = false;
-        }
-        cv.notify_all();
-        if (pool.empty()) work();
-        for (auto &t : pool) t.join();
-    }
-    const size_t nb = boff.size();
-    if (!overlapped && B.err.empty() && !bad) {  // the late blocks: read; now inflated, as bgzf_batch does
-        if (ooff[nb] >= (uint64_t(1) << 32)) B.recs.reset(), R = nullptr;
-        B.out.resize(kHead + ooff[nb]);
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            avail = nb;
-            next = first_late;
-        }
-        const int lt = (int)std::min<size_t>((size_t)nt, nb - first_late);
-        for (int k = 1; k < lt; ++k) {
-            try {
-                pool.emplace_back(work);
-            } catch (const std::system_error &) {
-                break;
-            }
-        }
-        if (lt > 0) work();
-        for (auto &t : pool) t.join();
-    }
-    if (!B.err.empty()) { B.recs.reset(); return B; }
-    B.n = ooff[nb];
-    B.out.resize(kHead + B.n);
-    if (bad) { B.err = "corrupt BGZF block"; B.recs.reset(); return B; }
-    if (R) {
-        if (nb) {
-            R->n = B.n;
-            R->ooff = ooff;
-            R->starts.resize(nb);
-            R->exit.resize(nb);
-        } else {
-            B.recs.reset();
-        }
-    }
-    return B;
-}
-
 // reads up to `max_blocks` blocks (the first `pre` bytes of the first header are in `pre`)
 BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_threads, std::shared_ptr<GpuInflate> gi) {
     BgzfBatch B;
@@ -483,8 +323,6 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
         if (!gi->g) gi->failed = true, gi->err = r.second;
     }
     gpu = gpu && gi->g;
-    static const bool overlap = !(getenv("FC2_BGZF_OVERLAP") && getenv("FC2_BGZF_OVERLAP")[0] == '0');   // (A/B: 0 = read, then inflate)
-    if (!gpu && overlap) return bgzf_batch_cpu(fd, std::move(raw), max_blocks, n_threads);
     size_t submitted = 0;
     auto submit = [&](bool last) {             // blocks read so far, in chunks of kGpuChunk
         if (!gpu) return;

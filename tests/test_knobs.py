@@ -25,7 +25,6 @@ KNOBS = {
     "FC2_PIN_MAX": "1",
     "FC2_INGEST_THREADS": "1",
     "FC2_BGZF_BATCH": "1",
-    "FC2_BGZF_OVERLAP": "0",         # read a batch's blocks, then inflate them (read once per process)
     "FC2_GPU_INFLATE": "1",          # (the CLI's GPU runs only; a no-op for the oracle runs here)
     "FC2_NEXT_THREADS": "16",
     "FC2_CALLER_THREADS": "16",
