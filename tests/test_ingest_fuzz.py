@@ -358,3 +358,52 @@ def test_bgzf_splitter_jumps_through_record_lists(tmp_path):
         files.append(got)
     assert files[0] == files[1]
     assert files[0]["lin_splice_sites.bed"].count("\n") > 1000
+
+
+@pytest.mark.parametrize("batch", ["2", "3", "8"])
+def test_bgzf_oversized_members_through_the_splitter(long_bam, tmp_path, monkeypatch, batch):
+    """Gzip members that inflate to far more than BGZF's 64 KiB (htslib reads them) in batches of 2-8
+    blocks, through the in-place splitter and its record lists: the files equal the sequential
+    reader's (-B), on the whole input and on truncations."""
+    import os
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_input_format import _bgzf_blocks
+    d, fa, raw = long_bam
+    n = len(raw)
+    import zlib
+
+    def fits(a, b):                                  # a BGZF block holds at most 64 KiB compressed
+        co = zlib.compressobj(6, zlib.DEFLATED, -15)
+        return len(co.compress(raw[a:b]) + co.flush()) + 26 <= 65536
+
+    edges = [0, 1, 7, 7, 5000, 70000, 70000]
+    while edges[-1] < n:                             # then members of ~120-kB of input where they fit
+        a, b = edges[-1], min(n, edges[-1] + 120000)
+        while not fits(a, b):
+            b = a + (b - a) // 2
+        edges.append(b)
+    data = _bgzf_blocks(raw, edges[1:-1])
+    rng = random.Random(int(batch))
+    script = _CLI_SCRIPT % os.path.dirname(os.path.abspath(__file__))
+    for k, size in enumerate([len(data)] + [rng.randrange(len(data) // 3, len(data)) for _ in range(2)]):
+        p = str(tmp_path / ("in%d.bam" % k))
+        with open(p, "wb") as fh:
+            fh.write(data[:size])
+        res = []
+        for tag, extra, env_extra in (("inplace", [], {}), ("seq", ["-B"], {})):
+            o = str(tmp_path / ("o%d_%s" % (k, tag)))
+            env = dict(os.environ, FC2_BGZF_BATCH=batch, FC2_INGEST_THREADS="3", **env_extra)
+            r = subprocess.run([sys.executable, "-c", script, "-G", fa, "-o", o, "-q"] + extra + [p], env=env,
+                               capture_output=True, text=True, timeout=300)
+            files = {}
+            for f in ("circ_splice_sites.bed", "lin_splice_sites.bed", "multi_events.tsv"):
+                fp = os.path.join(o, f)
+                files[f] = open(fp).read() if os.path.exists(fp) else None
+            fq = os.path.join(o, "spliced_reads.fastq.gz")
+            files["reads"] = gzip.open(fq, "rt").read() if os.path.exists(fq) and r.returncode == 0 else None
+            res.append((r.returncode, files))
+        assert res[0] == res[1], (k, size, [x[0] for x in res])
+        if k == 0:
+            assert res[0][0] == 0 and res[0][1]["circ_splice_sites.bed"].count("\n") > 20
