@@ -154,7 +154,7 @@ EXPORTED = [
     "fc2_ingest_open", "fc2_ingest_close", "fc2_ingest_n_refs", "fc2_ingest_ref_name", "fc2_ingest_header",
     "fc2_ingest_next", "fc2_ingest_counts_get", "fc2_ingest_set_bam_out", "fc2_ingest_close_bam_out",
     "fc2_ingest_format", "fc2_sam_to_bam", "fc2_bgzf_inflate_launch",
-    "fc2_ingest_set_gpu_inflate", "fc2_ingest_inflate_counts",
+    "fc2_ingest_set_gpu_inflate", "fc2_ingest_set_gpu_inflate_from", "fc2_ingest_inflate_counts",
     # include/fc2_caller.h
     "fc2_caller_open", "fc2_caller_set_genome", "fc2_caller_inflate_counts", "fc2_caller_ingest", "fc2_caller_close", "fc2_caller_next",
     "fc2_caller_submit", "fc2_caller_submit_compact", "fc2_caller_submit_long", "fc2_caller_queued", "fc2_caller_take", "fc2_caller_rows", "fc2_caller_write_rows", "fc2_caller_counter", "fc2_caller_stats",
@@ -297,6 +297,7 @@ def lib() -> ctypes.CDLL:
         "fc2_caller_stats": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_bgzf_inflate_launch": (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, u32, vp]),
         "fc2_ingest_set_gpu_inflate": (ctypes.c_int, [vp, ctypes.c_int, ctypes.c_int]),
+        "fc2_ingest_set_gpu_inflate_from": (ctypes.c_int, [vp, ctypes.c_int, u64]),
         "fc2_ingest_inflate_counts": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_caller_inflate_counts": (ctypes.c_int, [vp, P(u64), P(u64)]),
         "fc2_ctx_create": (ctypes.c_int, [ctypes.c_int, P(vp)]),

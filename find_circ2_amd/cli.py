@@ -267,13 +267,20 @@ def _devices(options):
     return ["cuda:%d" % ((first + k) % ndev) for k in range(options.gpus)]
 
 
+# BAM input read before its BGZF blocks move to the GPU (DESIGN.md §5 "The BAM input inflated on the
+# GPU"): a smaller input never touches the device for it, where setting it up costs more than it saves
+GPU_INFLATE_AFTER = 256 << 20
+
+
 def _inflate_device(options):
-    """The GPU that inflates a BAM input's BGZF blocks when FC2_GPU_INFLATE is 1 or 2 (the first of the
-    run's devices), else None: the CPU inflates them (the default; DESIGN.md "GPU inflate")."""
-    if os.environ.get("FC2_GPU_INFLATE", "0") not in ("1", "2"):
-        return None
+    """The GPU that inflates a BAM input's BGZF blocks (the first of the run's devices) and after how
+    many bytes of input: by default once GPU_INFLATE_AFTER bytes were read, at once with FC2_GPU_INFLATE
+    1 or 2; FC2_GPU_INFLATE=0: (None, 0), the CPU inflates every block."""
+    env = os.environ.get("FC2_GPU_INFLATE")
+    if env == "0":
+        return None, 0
     from .ctxpipe import device_index
-    return device_index(options.device)
+    return device_index(options.device), (0 if env in ("1", "2") else GPU_INFLATE_AFTER)
 
 
 def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory, genome, bam_path="",
@@ -298,7 +305,8 @@ def _run_native_caller(options, path, is_bam, out, hp, logger, evaluator_factory
                       write_multi=out.get("multi") is not None, genome_dummy=dummy,
                       known_circ=options.known_circ, known_lin=options.known_lin, bam_out=bam_path,
                       reads_gz=reads_gz,
-                      inflate_device=_inflate_device(options) if genome_eval is not None else None)
+                      **(dict(zip(("inflate_device", "inflate_after"), _inflate_device(options)))
+                         if genome_eval is not None else {}))
     try:
         try:
             n_kc, n_kl = nc.open()

@@ -288,6 +288,24 @@ struct GpuInflate {
     // inflating refused blocks; batches whose buffer was pinned (downloaded into directly)
     int64_t read_ns = 0, add_ns = 0, wait_ns = 0, cpu_ns = 0;
     int batches = 0, pinned = 0;
+    // fc2_ingest_set_gpu_inflate_from: nothing is made on the device until start_after bytes of the
+    // input were read (inputs smaller than that never touch it); `blocks` is then the batch size the
+    // next batches take (0: the ingest's own).  launched / read_bytes: the batch reader's alone (one
+    // batch at a time)
+    uint64_t start_after = 0, read_bytes = 0;
+    bool launched = true;
+    std::atomic<int> blocks{0};
+    void launch(bool wait) {
+        const int dev = device;
+        const uint32_t mb = max_blocks;
+        opening = std::async(wait ? std::launch::deferred : std::launch::async, [dev, mb]() {
+            std::string e;
+            fc2::inf::Gpu *g = fc2::inf::gpu_open(dev, mb, kHead + (size_t)mb * 65536, e);
+            return std::make_pair(g, e);
+        });
+        launched = true;
+        blocks = (int)max_blocks;
+    }
     ~GpuInflate() {
         if (getenv("FC2_CALLER_TIMING") && batches)
             fprintf(stderr, "gpu inflate: %d batches (%d pinned), %llu blocks on the GPU, %llu on the CPU; reader s: "
@@ -311,6 +329,7 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
     std::vector<uint8_t> raw;
     std::vector<size_t> boff, bsz;
     raw.swap(pre);
+    if (gi && !gi->launched && gi->read_bytes >= gi->start_after) gi->launch(false);
     // the GPU inflates the batch in chunks as they are read (fc2_inflate.h), into the batch buffer
     // itself -- a pinned one from the pool, made max_blocks * 64 KiB long up front
     bool gpu = gi && !gi->failed && max_blocks <= (int)gi->max_blocks;
@@ -384,6 +403,7 @@ BgzfBatch bgzf_batch(int fd, std::vector<uint8_t> pre, int max_blocks, int n_thr
         t2 = now_ns();
         gi->wait_ns += t2 - t1;
     }
+    if (gi) gi->read_bytes += pos;
     if (!B.err.empty()) return B;
     const size_t nb = boff.size();
     std::vector<size_t> ooff(nb + 1, 0);
@@ -515,6 +535,13 @@ struct fc2_ingest {
     ~fc2_ingest();
 };
 
+// BGZF blocks the next batch takes: the GPU inflate's size once it started, else the ingest's
+int batch_blocks(const fc2_ingest *h) {
+    const GpuInflate *gi = h->gpu_inflate.get();
+    const int b = gi ? gi->blocks.load() : 0;
+    return b > 0 ? b : h->bgzf_blocks;
+}
+
 // The parse-ahead threads.  The splitter reads the input into blocks cut after the last newline
 // (4 MiB each, numbered), parser threads turn each block into a batch of records, and the consumer
 // (next_record) takes the batches in block order.  Records travel back with their buffers (the
@@ -643,7 +670,7 @@ bool ensure(fc2_ingest *h, size_t n) {
             h->inflate_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
             if (!b.err.empty()) { h->z_err = b.err; h->z_done = true; return false; }
             if (b.eof) h->z_done = true;
-            else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), h->bgzf_blocks,
+            else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), batch_blocks(h),
                                            h->bgzf_nt, h->gpu_inflate);
             if (h->buf.size() < h->end + b.n) h->buf.resize(h->end + b.n);
             if (b.n) memcpy(h->buf.data() + h->end, b.data(), b.n);
@@ -1272,7 +1299,7 @@ void bgzf_split_loop(fc2_ingest *h, fc2_ingest::SamAhead *ap) {
         h->inflate_wait_ns += std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - w0).count();
         if (!b.err.empty()) { h->z_err = b.err; h->z_done = true; return false; }
         if (b.eof) h->z_done = true;
-        else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), h->bgzf_blocks, h->bgzf_nt,
+        else h->bgzf_next = std::async(std::launch::async, bgzf_batch, h->fd, std::vector<uint8_t>(), batch_blocks(h), h->bgzf_nt,
                                        h->gpu_inflate);
         const size_t L = end - beg;
         std::shared_ptr<CharBuf> nb;
@@ -1872,35 +1899,55 @@ extern "C" int fc2_ingest_format(const fc2_ingest *h, int *compression) {
     return h->bam ? FC2_INGEST_BAM : FC2_INGEST_SAM;
 }
 
-extern "C" int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device, int wait) {
+extern "C" int fc2_ingest_set_gpu_inflate_from(fc2_ingest *h, int device, uint64_t after_bytes) {
     if (!h) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_gpu_inflate: null argument");
     if (h->n_records) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_gpu_inflate: call before reading");
     const char *e = getenv("FC2_GPU_INFLATE");
-    if (e && atoi(e) == 2) wait = 1;           // (2: the buffers made before the first read, as the tests want)
+    const bool wait = e && atoi(e) == 2;       // (2: the buffers made before the first read, as the tests want)
+    if (e && (atoi(e) == 1 || wait)) after_bytes = 0;
     if (device < 0 || !h->bgzf || (e && atoi(e) == 0)) {
         h->gpu_inflate.reset();
         return FC2_OK;
     }
     auto gi = std::make_shared<GpuInflate>();
     gi->device = device;
-    // batches of 1024 blocks (64 MiB inflated, four chunks of 256; fc2_inflate.hip); FC2_BGZF_BATCH
-    // still rules
-    if (!getenv("FC2_BGZF_BATCH")) h->bgzf_blocks = 1024;
-    gi->max_blocks = (uint32_t)h->bgzf_blocks;
-    // the device's buffers and the first pinned batch buffers: now, or made while the first batches
-    // are read and inflated on the CPU
-    const int dev = device;
-    const uint32_t mb = gi->max_blocks;
-    gi->opening = std::async(wait ? std::launch::deferred : std::launch::async, [dev, mb]() {
-        std::string err;
-        fc2::inf::Gpu *g = fc2::inf::gpu_open(dev, mb, kHead + (size_t)mb * 65536, err);
-        return std::make_pair(g, err);
-    });
-    if (wait) {
-        auto r = gi->opening.get();
-        gi->g = r.first;
-        if (!gi->g) gi->failed = true, gi->err = r.second;
+    // batches of 1024 blocks (64 MiB inflated, four chunks of 256; fc2_inflate.hip) once the GPU
+    // inflates; FC2_BGZF_BATCH still rules
+    gi->max_blocks = getenv("FC2_BGZF_BATCH") ? (uint32_t)h->bgzf_blocks : 1024u;
+    if (after_bytes == 0) {
+        // the device's buffers and the first pinned batch buffers: now, or made while the first
+        // batches are read and inflated on the CPU
+        gi->launch(wait);
+        if (wait) {
+            auto r = gi->opening.get();
+            gi->g = r.first;
+            if (!gi->g) gi->failed = true, gi->err = r.second;
+        }
+    } else {
+        gi->launched = false;
+        gi->start_after = after_bytes;
     }
+    h->gpu_inflate = gi;
+    return FC2_OK;
+}
+
+extern "C" int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device, int wait) {
+    if (!h) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_gpu_inflate: null argument");
+    if (!wait) return fc2_ingest_set_gpu_inflate_from(h, device, 0);
+    const char *e = getenv("FC2_GPU_INFLATE");
+    if (e && atoi(e) == 0) return fc2_ingest_set_gpu_inflate_from(h, -1, 0);
+    if (h->n_records) return fc2::fail(FC2_E_PARAM, "fc2_ingest_set_gpu_inflate: call before reading");
+    if (device < 0 || !h->bgzf) {
+        h->gpu_inflate.reset();
+        return FC2_OK;
+    }
+    auto gi = std::make_shared<GpuInflate>();
+    gi->device = device;
+    gi->max_blocks = getenv("FC2_BGZF_BATCH") ? (uint32_t)h->bgzf_blocks : 1024u;
+    gi->launch(true);
+    auto r = gi->opening.get();
+    gi->g = r.first;
+    if (!gi->g) gi->failed = true, gi->err = r.second;
     h->gpu_inflate = gi;
     return FC2_OK;
 }

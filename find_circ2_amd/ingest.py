@@ -58,6 +58,11 @@ class NativeIngest:
         wait: the device's buffers made now (else meanwhile, the CPU inflating until they are)."""
         N.check(N.lib().fc2_ingest_set_gpu_inflate(self.h, int(device), int(bool(wait))))
 
+    def set_gpu_inflate_from(self, device: int, after_bytes: int):
+        """As set_gpu_inflate, with nothing made on the device until ``after_bytes`` of the input were
+        read (fc2_ingest_set_gpu_inflate_from; the CLI's default)."""
+        N.check(N.lib().fc2_ingest_set_gpu_inflate_from(self.h, int(device), int(after_bytes)))
+
     def inflate_counts(self) -> Tuple[int, int]:
         """(blocks inflated on the GPU, on the CPU) since set_gpu_inflate."""
         g, c = ctypes.c_uint64(), ctypes.c_uint64()

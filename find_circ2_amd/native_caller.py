@@ -72,7 +72,7 @@ class NativeCaller:
 
     def __init__(self, path: str, is_bam: bool, copts, genome_names, fasta_handle=None, write_reads=True,
                  write_multi=True, genome_dummy=False, known_circ: str = "", known_lin: str = "",
-                 bam_out: str = "", reads_gz=None, inflate_device=None):
+                 bam_out: str = "", reads_gz=None, inflate_device=None, inflate_after: int = 0):
         o = copts
         # the strings must outlive the handle's open call (fc2_caller_open copies them)
         self._keep = [o.name.encode(), known_circ.encode() if known_circ else None,
@@ -92,6 +92,7 @@ class NativeCaller:
         self.bam_out = bam_out
         self.reads_gz = reads_gz     # (path, level, threads, piece): spliced_reads.fastq.gz written natively
         self.inflate_device = inflate_device   # a BGZF input's blocks inflated on this GPU (None: the CPU)
+        self.inflate_after = inflate_after     # ... once this many bytes of the input were read
         self.opened = False
         self.format = None           # "sam" | "bam", detected from the bytes (open)
         self.loop_profile = {}       # seconds per stage of the last run (two-thread loop)
@@ -109,7 +110,7 @@ class NativeCaller:
         if self.bam_out:
             N.check(L.fc2_ingest_set_bam_out(ing, self.bam_out.encode()))
         if self.inflate_device is not None:
-            N.check(L.fc2_ingest_set_gpu_inflate(ing, int(self.inflate_device), 0))   # (buffers made meanwhile)
+            N.check(L.fc2_ingest_set_gpu_inflate_from(ing, int(self.inflate_device), int(self.inflate_after)))
         if self.reads_gz:
             path, level, threads, piece = self.reads_gz
             N.check(L.fc2_caller_set_reads_gz(self.h, path.encode(), int(level), int(threads), int(piece)))

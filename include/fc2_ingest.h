@@ -87,13 +87,18 @@ int fc2_ingest_close_bam_out(fc2_ingest *h);
  * tests and the bench's stdin-BAM CLI run. */
 int fc2_sam_to_bam(const char *sam_path, const char *bam_path);
 /* The BAM input's BGZF blocks inflated on GPU `device` (fc2_inflate.hip) instead of the CPU from the
- * next batch on; call before reading (the CLI's read loop does, on its first device, with
- * FC2_GPU_INFLATE=1 or 2).  The device's
+ * next batch on; call before reading (FC2_GPU_INFLATE=1 or 2 makes the CLI's read loop call this, on
+ * its first device; by default it calls fc2_ingest_set_gpu_inflate_from below).  The device's
  * buffers are made now (wait != 0) or meanwhile, the batches inflated on the CPU until they are ready.
  * Batches grow to 1024 blocks (FC2_BGZF_BATCH still sets them); every block's CRC-32 and ISIZE are
  * checked (on the device), and the CPU inflates any block the GPU refused, and every block from then
  * on if the device fails.  device < 0, a non-BGZF input or FC2_GPU_INFLATE=0: the CPU inflates. */
 int fc2_ingest_set_gpu_inflate(fc2_ingest *h, int device, int wait);
+/* The same, with nothing made on the device until after_bytes of the input were read (0: as
+ * fc2_ingest_set_gpu_inflate(h, device, 0)): smaller inputs never touch the device, and their batches
+ * keep the ingest's size.  The CLI's default, with 256 MiB (DESIGN.md §5 "The BAM input inflated on the
+ * GPU").  FC2_GPU_INFLATE=0 turns it off, 1 or 2 start it at once. */
+int fc2_ingest_set_gpu_inflate_from(fc2_ingest *h, int device, uint64_t after_bytes);
 /* Blocks of the batches the GPU inflated: those it took, and those it left to the CPU. */
 int fc2_ingest_inflate_counts(const fc2_ingest *h, uint64_t *gpu_blocks, uint64_t *cpu_blocks);
 /* BGZF blocks inflated on the GPU (fc2_inflate.hip; the BAM input's inflate, which pysam/htslib does for

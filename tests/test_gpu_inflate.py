@@ -147,14 +147,17 @@ def test_inflate_damaged_payloads_end_in_a_status():
             assert len(g) == n
 
 
-def _read_all(path, device=None):
+def _read_all(path, device=None, after=None):
     """Every handed-back fragment and the counts of a BAM read by the native ingest (GPU inflate on
-    `device`, or the CPU), and the inflate counts; or the error raised."""
+    `device` -- from the start, or once `after` bytes were read -- or the CPU), and the inflate counts;
+    or the error raised."""
     from find_circ2_amd.ingest import NativeIngest
     ing = None
     try:
         ing = NativeIngest(path, True)
-        if device is not None:
+        if device is not None and after is not None:
+            ing.set_gpu_inflate_from(device, after)
+        elif device is not None:
             ing.set_gpu_inflate(device)
         frags = []
         while not ing.eof:
@@ -206,6 +209,28 @@ def test_ingest_gpu_inflate_equals_cpu(tmp_path, monkeypatch, batch):
         assert cpu[2] == (0, 0)
 
 
+def test_ingest_gpu_inflate_from_a_threshold(tmp_path, monkeypatch):
+    """fc2_ingest_set_gpu_inflate_from (the CLI's default, 256 MiB): an input smaller than the threshold
+    never touches the device (no block counted on it); one past it switches to the GPU mid-stream (the
+    device's buffers made in the background from there) -- the same fragments and counts as the CPU
+    inflate either way, at every batch size."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    monkeypatch.delenv("FC2_GPU_INFLATE", raising=False)
+    for batch in ("3", "64"):
+        monkeypatch.setenv("FC2_BGZF_BATCH", batch)
+        for bam in _bams(tmp_path):
+            cpu = _read_all(bam)
+            size = os.path.getsize(bam)
+            never = _read_all(bam, 0, after=10 * size)
+            assert never[:2] == cpu[:2] and never[2] == (0, 0), (bam, never[2])
+            for after in (1, size // 3):
+                mid = _read_all(bam, 0, after=after)
+                assert mid[:2] == cpu[:2], (bam, after)
+                n_blocks = len(_bgzf_blocks(open(bam, "rb").read()))
+                assert sum(mid[2]) <= n_blocks, (bam, after, mid[2])
+
+
 def test_ingest_gpu_inflate_corrupt_block_same_error(tmp_path, monkeypatch):
     """A damaged block: the same error with the GPU inflate as with the CPU's (the host's CRC check
     and CPU retry stand behind every GPU block)."""
@@ -255,6 +280,18 @@ def test_cli_bam_input_inflated_on_the_gpu(tmp_path, monkeypatch):
     rc3, o3 = run_cli(tmp_path, fa, rd, bam=True, evaluator=None, tag="gpu_inflate_background")
     assert rc3 == 0
     _compare(o1, o3)
+    # the default: the GPU takes over past cli.GPU_INFLATE_AFTER bytes of input -- never for this
+    # input; at a threshold of one byte, from the first batches whose device buffers are ready
+    monkeypatch.delenv("FC2_GPU_INFLATE")
+    rc4, o4 = run_cli(tmp_path, fa, rd, bam=True, evaluator=None, tag="gpu_inflate_default")
+    assert rc4 == 0
+    _compare(o1, o4)
+    assert blocks(o4) == (0.0, 0.0)
+    from find_circ2_amd import cli
+    monkeypatch.setattr(cli, "GPU_INFLATE_AFTER", 1)
+    rc5, o5 = run_cli(tmp_path, fa, rd, bam=True, evaluator=None, tag="gpu_inflate_default_low")
+    assert rc5 == 0
+    _compare(o1, o5)
 
 
 def test_two_ingests_with_different_batches_share_the_pinned_pool(tmp_path, monkeypatch):
